@@ -1,0 +1,155 @@
+/*
+ * pj.h — C-ABI of libpj, the MI355X-native shortest-path relaxation library.
+ *
+ * The reference (fagan2888/ParallelJohnson) exposes no library API: its only
+ * boundary is the process CLI `parallel_johnson webfile source_node sol_file`
+ * (README:9, ParallelJohnson.cpp:294-303) and the internal seam
+ * `int parallel_johnson(int argc, char* argv[])` (ParallelJohnson.cpp:286).
+ * Each entry point below names the reference code it replaces; the CLI in
+ * paralleljohnson_amd/csrc/cli.cpp is the drop-in for the process boundary and
+ * is a plain client of this header.
+ *
+ * Conventions
+ *  - Every function returns an int status (PJ_OK = 0, negative on error);
+ *    pj_last_error() returns a thread-local message for the last failure.
+ *  - Distances are int32; PJ_INT_INF (= the reference's INT_INF, :29) marks
+ *    "unreachable", and any hop/weight distance >= PJ_INT_INF is reported as
+ *    PJ_INT_INF (reference contract).
+ *  - Host buffers are caller-owned; device memory is owned by the handles.
+ *  - A pj_ctx is bound to one GPU and is not thread-safe (one thread per ctx).
+ *  - No C++ exception crosses this boundary.
+ */
+#ifndef PJ_H
+#define PJ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PJ_INT_INF 100000 /* ParallelJohnson.cpp:29 */
+
+enum pj_status {
+    PJ_OK = 0,
+    PJ_ERR_ARG = -1,      /* bad argument (null pointer, bad size) */
+    PJ_ERR_IO = -2,       /* file could not be written */
+    PJ_ERR_PARSE = -3,    /* edge-list line the reference reads as UB (see pj_load_snap) */
+    PJ_ERR_HIP = -4,      /* HIP runtime error */
+    PJ_ERR_OOM = -5,      /* device or host allocation failed */
+    PJ_ERR_RANGE = -6,    /* id / size outside the supported range */
+    PJ_ERR_NODEVICE = -7, /* no usable gfx950 device */
+    PJ_ERR_STATE = -8,    /* call out of order (e.g. stats before a solve) */
+    PJ_ERR_COMM = -9      /* RCCL / multi-GPU error */
+};
+
+typedef struct pj_ctx pj_ctx;
+typedef struct pj_graph pj_graph;
+
+/* Per-solve statistics of the last pj_sssp* call on a graph. */
+typedef struct pj_stats {
+    double kernel_ms;        /* device time, dist init -> distances final (HIP events on the ctx stream);
+                                the analogue of the reference's timed region :459-462 ... :597-605 */
+    double wall_ms;          /* host wall time of the call, incl. D2H of dist when requested */
+    int64_t levels;          /* BFS levels / delta-stepping buckets processed */
+    int64_t td_levels;       /* top-down (push) levels */
+    int64_t bu_levels;       /* bottom-up (pull) levels */
+    int64_t reached;         /* n_r: vertices with dist < PJ_INT_INF (filled by pj_reach_stats) */
+    int64_t reached_edges;   /* m_r: sum of out-degree over reached vertices (pj_reach_stats) */
+    int64_t relax_rounds;    /* weighted: light/heavy relaxation rounds */
+} pj_stats;
+
+/* ---- context ------------------------------------------------------------ */
+
+/* Bind to HIP device `device` (ordinal as HIP sees it). Replaces MPI_Init
+ * (:679) + the per-rank setup of parallel_johnson (:291-292). */
+int pj_create(int device, pj_ctx** out);
+int pj_destroy(pj_ctx* ctx);
+/* HIP stream (hipStream_t) all work of this ctx is launched on. */
+void* pj_stream(pj_ctx* ctx);
+const char* pj_last_error(void);
+const char* pj_version(void);
+
+/* ---- graph ingestion (replaces read_webgraph :66-105 + coord2csr :117-159) */
+
+/* Parse a SNAP edge-list text file on the GPU and build CSR by a stable radix
+ * sort + scan. Line grammar follows the reference exactly: a line is an edge
+ * iff its first byte is '0'..'9' (:73, :91); fields are read with
+ * `istringstream >> int >> int` semantics (:92-93) — a non-numeric second
+ * field reads as 0, extra columns are ignored. N = max id + 1 (:319).
+ * With weighted != 0 a third integer column is the edge weight.
+ * A missing input file parses as an empty graph (N = 0), as in the reference
+ * (no is_open check at :67). Lines the reference turns into undefined
+ * behaviour (missing second field, negative or > INT32_MAX-1 ids) fail with
+ * PJ_ERR_PARSE; pj_last_error() names the 1-based line number. */
+int pj_load_snap(pj_ctx* ctx, const char* path, int weighted, pj_graph** out);
+/* Same, from an in-memory text buffer. */
+int pj_load_snap_buffer(pj_ctx* ctx, const char* text, int64_t len, int weighted, pj_graph** out);
+
+/* Build a graph from host COO arrays (file order = CSR column order, as the
+ * stable counting sort of coord2csr :143-149). n_vertices < 0 means
+ * max id + 1. w may be NULL (unit weights, :147). Ids must be in [0, 2^32-2];
+ * edge counts may exceed 2^31 (64-bit offsets are used then). */
+int pj_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, const uint32_t* w,
+                int64_t nnz, int64_t n_vertices, pj_graph** out);
+
+/* Graph500-style Kronecker generator on the GPU (A,B,C = 0.57,0.19,0.19),
+ * 2^scale vertices, edgefactor << scale tuples, labels permuted, every tuple
+ * written in both directions (tuple i -> entries 2i, 2i+1). Deterministic in
+ * (scale, edgefactor, seed); weighted != 0 gives w = 1 + hash(seed, i) % 255
+ * (same for both directions). No reference counterpart (benchmark input). */
+int pj_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int weighted,
+                          pj_graph** out);
+
+int pj_graph_destroy(pj_graph* g);
+/* n = number of vertices, nnz = number of CSR entries, weighted = 0/1,
+ * symmetric = 1 when the graph is known to equal its transpose. */
+int pj_graph_info(const pj_graph* g, int64_t* n, int64_t* nnz, int* weighted, int* symmetric);
+/* D2H export of the CSR: row_ptr[n+1] (int64), col[nnz] (int32), w[nnz] or NULL. */
+int pj_graph_get_csr(const pj_graph* g, int64_t* row_ptr, int32_t* col, uint32_t* w);
+/* Out-degree of vertex v (row_ptr[v+1] - row_ptr[v]). */
+int pj_graph_out_degree(const pj_graph* g, int64_t v, int64_t* deg);
+/* Pick `n` distinct roots with out-degree >= 1, deterministic in seed
+ * (Graph500 root sampling). Returns the count found in *found. */
+int pj_sample_roots(const pj_graph* g, uint64_t seed, int n, int64_t* roots, int* found);
+
+/* ---- relaxation (replaces the heap + BSP round loop :466-594) ------------ */
+
+/* Single-source shortest paths from `source` (atoi semantics are the
+ * caller's: any int64 is accepted; a source outside [0,n) leaves every
+ * distance at PJ_INT_INF, as the reference does). Unit-weight graphs run the
+ * direction-optimizing level-synchronous frontier kernels, weighted graphs
+ * run delta-stepping. dist_out (host, n int32) may be NULL: the result then
+ * stays on the device (pj_copy_dist fetches it). */
+int pj_sssp(pj_graph* g, int64_t source, int32_t* dist_out);
+/* Copy the last result to the host. */
+int pj_copy_dist(pj_graph* g, int32_t* dist_out);
+/* Device pointer to the last result (int32[n]); valid until the next solve. */
+const int32_t* pj_dist_device(pj_graph* g);
+/* Batched multi-source (Johnson-style all-pairs rows): dist_out is n_src x n
+ * int32, row i = pj_sssp(g, sources[i]). */
+int pj_sssp_batch(pj_graph* g, const int64_t* sources, int n_src, int32_t* dist_out);
+/* Statistics of the last solve. pj_reach_stats additionally computes
+ * reached / reached_edges on the device (not part of kernel_ms). */
+int pj_last_stats(const pj_graph* g, pj_stats* out);
+int pj_reach_stats(pj_graph* g, pj_stats* out);
+/* Tuning knobs: alpha/beta of the direction switch (Beamer), delta for
+ * delta-stepping (0 = automatic). Returns PJ_ERR_ARG on bad values. */
+int pj_set_option(pj_graph* g, const char* key, double value);
+
+/* ---- output (replaces output_vector :32-46 + the write at :615-620) ------ */
+
+/* Write the sol_file: "the vector is:\n" then, for v = 0..n-1, the decimal
+ * distance or "inf" when it equals PJ_INT_INF, one per line. Like the
+ * reference (ofstream without a check, :617), an unopenable path is not an
+ * error unless strict != 0. */
+int pj_write_sol(const int32_t* dist, int64_t n, const char* path, int strict);
+/* Format into a caller buffer; *len_out receives the byte count. With
+ * buf == NULL only the length is computed. */
+int pj_format_sol(const int32_t* dist, int64_t n, char* buf, int64_t cap, int64_t* len_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PJ_H */

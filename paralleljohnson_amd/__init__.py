@@ -1,0 +1,265 @@
+"""paralleljohnson_amd — MI355X-native shortest-path relaxation.
+
+Python binding (ctypes) of libpj, the C-ABI in include/pj.h. The compute path
+is the HIP library paralleljohnson_amd/lib/libpj.so; this module only moves
+arguments across the ABI. There is no CPU fallback: importing fails loudly if
+the library is missing, and every call raises PJError when libpj reports an
+error (e.g. no gfx950 device).
+
+The reference's only interface is its CLI (`parallel_johnson webfile
+source_node sol_file`, ParallelJohnson.cpp:286-303); the same CLI is built as
+paralleljohnson_amd/bin/parallel_johnson (see cli_path()).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+INT_INF = 100000  # ParallelJohnson.cpp:29
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpj.so")
+CLI_PATH = os.path.join(_HERE, "bin", "parallel_johnson")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+        "(make -C paralleljohnson_amd/csrc)")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+PJ_OK = 0
+_STATUS = {
+    -1: "PJ_ERR_ARG", -2: "PJ_ERR_IO", -3: "PJ_ERR_PARSE", -4: "PJ_ERR_HIP", -5: "PJ_ERR_OOM",
+    -6: "PJ_ERR_RANGE", -7: "PJ_ERR_NODEVICE", -8: "PJ_ERR_STATE", -9: "PJ_ERR_COMM",
+}
+
+
+class PJError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_STATUS.get(code, code)}: {msg}")
+        self.code = code
+        self.name = _STATUS.get(code, str(code))
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double), ("levels", ctypes.c_int64),
+                ("td_levels", ctypes.c_int64), ("bu_levels", ctypes.c_int64), ("reached", ctypes.c_int64),
+                ("reached_edges", ctypes.c_int64), ("relax_rounds", ctypes.c_int64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_P = ctypes.c_void_p
+_PP = ctypes.POINTER(ctypes.c_void_p)
+_I64 = ctypes.c_int64
+_INT = ctypes.c_int
+
+_SIGS = {
+    "pj_create": ([_INT, _PP], _INT),
+    "pj_destroy": ([_P], _INT),
+    "pj_stream": ([_P], _P),
+    "pj_last_error": ([], ctypes.c_char_p),
+    "pj_version": ([], ctypes.c_char_p),
+    "pj_load_snap": ([_P, ctypes.c_char_p, _INT, _PP], _INT),
+    "pj_load_snap_buffer": ([_P, ctypes.c_char_p, _I64, _INT, _PP], _INT),
+    "pj_load_coo": ([_P, _P, _P, _P, _I64, _I64, _PP], _INT),
+    "pj_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _PP], _INT),
+    "pj_graph_destroy": ([_P], _INT),
+    "pj_graph_info": ([_P, _P, _P, _P, _P], _INT),
+    "pj_graph_get_csr": ([_P, _P, _P, _P], _INT),
+    "pj_graph_out_degree": ([_P, _I64, _P], _INT),
+    "pj_sample_roots": ([_P, ctypes.c_uint64, _INT, _P, _P], _INT),
+    "pj_sssp": ([_P, _I64, _P], _INT),
+    "pj_copy_dist": ([_P, _P], _INT),
+    "pj_dist_device": ([_P], _P),
+    "pj_sssp_batch": ([_P, _P, _INT, _P], _INT),
+    "pj_last_stats": ([_P, _P], _INT),
+    "pj_reach_stats": ([_P, _P], _INT),
+    "pj_set_option": ([_P, ctypes.c_char_p, ctypes.c_double], _INT),
+    "pj_write_sol": ([_P, _I64, ctypes.c_char_p, _INT], _INT),
+    "pj_format_sol": ([_P, _I64, _P, _I64, _P], _INT),
+}
+for _name, (_args, _res) in _SIGS.items():
+    _fn = getattr(_lib, _name)
+    _fn.argtypes = _args
+    _fn.restype = _res
+
+EXPORTS = tuple(_SIGS)
+
+
+def _check(rc: int):
+    if rc != PJ_OK:
+        raise PJError(rc, (_lib.pj_last_error() or b"").decode(errors="replace"))
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def version() -> str:
+    return _lib.pj_version().decode()
+
+
+def cli_path() -> str:
+    return CLI_PATH
+
+
+class Graph:
+    """A graph resident on one GPU (CSR, plus CSC for pull levels)."""
+
+    def __init__(self, ctx: "Context", handle: ctypes.c_void_p):
+        self._ctx = ctx
+        self._h = handle
+        n, m, w, s = _I64(), _I64(), _INT(), _INT()
+        _check(_lib.pj_graph_info(self._h, ctypes.byref(n), ctypes.byref(m), ctypes.byref(w), ctypes.byref(s)))
+        self.n, self.nnz, self.weighted, self.symmetric = n.value, m.value, bool(w.value), bool(s.value)
+
+    def close(self):
+        if self._h:
+            _check(_lib.pj_graph_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- relaxation ------------------------------------------------------
+    def sssp(self, source: int, copy: bool = True) -> Optional[np.ndarray]:
+        """Distances from `source` (int32, INT_INF = unreachable)."""
+        out = np.empty(max(self.n, 1), np.int32) if copy else None
+        _check(_lib.pj_sssp(self._h, int(source), _ptr(out)))
+        return out[: self.n] if copy else None
+
+    def copy_dist(self) -> np.ndarray:
+        out = np.empty(max(self.n, 1), np.int32)
+        _check(_lib.pj_copy_dist(self._h, _ptr(out)))
+        return out[: self.n]
+
+    def dist_device_ptr(self) -> int:
+        return _lib.pj_dist_device(self._h) or 0
+
+    def sssp_batch(self, sources: Sequence[int]) -> np.ndarray:
+        src = np.ascontiguousarray(np.asarray(sources, dtype=np.int64))
+        out = np.empty((len(src), max(self.n, 1)), np.int32)
+        _check(_lib.pj_sssp_batch(self._h, _ptr(src), len(src), _ptr(out)))
+        return out[:, : self.n]
+
+    def stats(self) -> dict:
+        st = Stats()
+        _check(_lib.pj_last_stats(self._h, ctypes.byref(st)))
+        return st.as_dict()
+
+    def reach_stats(self) -> dict:
+        st = Stats()
+        _check(_lib.pj_reach_stats(self._h, ctypes.byref(st)))
+        return st.as_dict()
+
+    def set_option(self, key: str, value: float):
+        _check(_lib.pj_set_option(self._h, key.encode(), float(value)))
+
+    # -- inspection --------------------------------------------------------
+    def get_csr(self):
+        row = np.empty(self.n + 1, np.int64)
+        col = np.empty(max(self.nnz, 1), np.int32)
+        w = np.empty(max(self.nnz, 1), np.uint32) if self.weighted else None
+        _check(_lib.pj_graph_get_csr(self._h, _ptr(row), _ptr(col), _ptr(w)))
+        return row, col[: self.nnz], (w[: self.nnz] if w is not None else None)
+
+    def out_degree(self, v: int) -> int:
+        d = _I64()
+        _check(_lib.pj_graph_out_degree(self._h, int(v), ctypes.byref(d)))
+        return d.value
+
+    def sample_roots(self, seed: int, n: int) -> np.ndarray:
+        out = np.empty(max(n, 1), np.int64)
+        found = _INT()
+        _check(_lib.pj_sample_roots(self._h, ctypes.c_uint64(seed), int(n), _ptr(out), ctypes.byref(found)))
+        return out[: found.value]
+
+
+class Context:
+    """One GPU (pj_ctx). Not thread-safe; one thread per context."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(_lib.pj_create(int(device), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if self._h:
+            _check(_lib.pj_destroy(self._h))
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def stream(self) -> int:
+        return _lib.pj_stream(self._h) or 0
+
+    def load_snap(self, path: str, weighted: bool = False) -> Graph:
+        g = ctypes.c_void_p()
+        _check(_lib.pj_load_snap(self._h, os.fsencode(path), int(weighted), ctypes.byref(g)))
+        return Graph(self, g)
+
+    def load_snap_buffer(self, text: bytes, weighted: bool = False) -> Graph:
+        g = ctypes.c_void_p()
+        _check(_lib.pj_load_snap_buffer(self._h, text, len(text), int(weighted), ctypes.byref(g)))
+        return Graph(self, g)
+
+    def load_coo(self, src, dst, w=None, n: int = -1) -> Graph:
+        s = np.ascontiguousarray(np.asarray(src, dtype=np.int64))
+        d = np.ascontiguousarray(np.asarray(dst, dtype=np.int64))
+        if len(s) != len(d):
+            raise ValueError("src and dst differ in length")
+        wa = None if w is None else np.ascontiguousarray(np.asarray(w, dtype=np.uint32))
+        g = ctypes.c_void_p()
+        _check(_lib.pj_load_coo(self._h, _ptr(s), _ptr(d), _ptr(wa), len(s), int(n), ctypes.byref(g)))
+        return Graph(self, g)
+
+    def generate_kronecker(self, scale: int, edgefactor: int = 16, seed: int = 1, weighted: bool = False) -> Graph:
+        g = ctypes.c_void_p()
+        _check(_lib.pj_generate_kronecker(self._h, int(scale), int(edgefactor), ctypes.c_uint64(seed),
+                                          int(weighted), ctypes.byref(g)))
+        return Graph(self, g)
+
+
+def format_sol(dist) -> bytes:
+    """output_vector (:32-46) as bytes."""
+    d = np.ascontiguousarray(np.asarray(dist, dtype=np.int32))
+    ln = _I64()
+    _check(_lib.pj_format_sol(_ptr(d), len(d), None, 0, ctypes.byref(ln)))
+    buf = np.empty(max(ln.value, 1), np.uint8)
+    _check(_lib.pj_format_sol(_ptr(d), len(d), _ptr(buf), ln.value, ctypes.byref(ln)))
+    return buf[: ln.value].tobytes()
+
+
+def write_sol(dist, path: str, strict: bool = False):
+    d = np.ascontiguousarray(np.asarray(dist, dtype=np.int32))
+    _check(_lib.pj_write_sol(_ptr(d), len(d), os.fsencode(path), int(strict)))
+
+
+def device_count() -> int:
+    """Number of HIP devices (no GPU initialisation side effects beyond HIP's)."""
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:
+        return 0

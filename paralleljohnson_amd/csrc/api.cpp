@@ -1,0 +1,459 @@
+// api.cpp — the C-ABI of libpj (include/pj.h). Host code only: argument
+// checks, ownership, error translation; all graph work happens in the HIP
+// kernels of parse.hip / graph.hip / sort.hip / bfs.hip / delta.hip.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <thread>
+
+#include <sys/stat.h>
+
+#include "internal.h"
+
+namespace pj {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string& msg) { g_err = msg; }
+
+}  // namespace pj
+
+struct pj_ctx {
+    pj::Ctx c;
+};
+struct pj_graph {
+    pj::Graph g;
+};
+
+using namespace pj;
+
+namespace {
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const pj::Error& e) {
+        set_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        set_error("host allocation failed");
+        return PJ_ERR_OOM;
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return PJ_ERR_HIP;
+    } catch (...) {
+        set_error("unknown error");
+        return PJ_ERR_HIP;
+    }
+}
+
+int arg_error(const char* msg) {
+    set_error(msg);
+    return PJ_ERR_ARG;
+}
+
+void bind(const Ctx& c) { PJ_HIP(hipSetDevice(c.device)); }
+
+uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+i64 out_degree(const Graph& g, i64 v) {
+    if (g.off64) {
+        u64 h[2];
+        PJ_HIP(hipMemcpy(h, g.row64.p + v, sizeof(h), hipMemcpyDeviceToHost));
+        return (i64)(h[1] - h[0]);
+    }
+    u32 h[2];
+    PJ_HIP(hipMemcpy(h, g.row32.p + v, sizeof(h), hipMemcpyDeviceToHost));
+    return (i64)(h[1] - h[0]);
+}
+
+int finish_graph(pj_ctx* ctx, std::unique_ptr<pj_graph>& pg, pj_graph** out) {
+    (void)ctx;
+    *out = pg.release();
+    return PJ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pj_last_error(void) { return g_err.c_str(); }
+
+const char* pj_version(void) { return "libpj 0.1 (gfx950)"; }
+
+int pj_create(int device, pj_ctx** out) {
+    if (!out) return arg_error("pj_create: out is NULL");
+    *out = nullptr;
+    return guarded([&] {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+            set_error("no HIP device visible");
+            return (int)PJ_ERR_NODEVICE;
+        }
+        if (device < 0 || device >= count) {
+            set_error("device ordinal out of range");
+            return (int)PJ_ERR_NODEVICE;
+        }
+        hipDeviceProp_t prop;
+        PJ_HIP(hipGetDeviceProperties(&prop, device));
+        if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+            set_error(std::string("libpj is built for gfx950 only; device is ") + prop.gcnArchName);
+            return (int)PJ_ERR_NODEVICE;
+        }
+        auto c = std::make_unique<pj_ctx>();
+        c->c.device = device;
+        c->c.cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+        PJ_HIP(hipSetDevice(device));
+        PJ_HIP(hipStreamCreateWithFlags(&c->c.stream, hipStreamNonBlocking));
+        *out = c.release();
+        return (int)PJ_OK;
+    });
+}
+
+int pj_destroy(pj_ctx* ctx) {
+    if (!ctx) return PJ_OK;
+    return guarded([&] {
+        bind(ctx->c);
+        if (ctx->c.stream) (void)hipStreamDestroy(ctx->c.stream);
+        delete ctx;
+        return (int)PJ_OK;
+    });
+}
+
+void* pj_stream(pj_ctx* ctx) { return ctx ? (void*)ctx->c.stream : nullptr; }
+
+int pj_load_snap_buffer(pj_ctx* ctx, const char* text, int64_t len, int weighted, pj_graph** out) {
+    if (!ctx || !out || (len > 0 && !text) || len < 0) return arg_error("pj_load_snap_buffer: bad argument");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        DevBuf<u32> src, dst, w;
+        ParseResult r = parse_snap_device(ctx->c, text, len, weighted != 0, src, dst, w);
+        if (r.bad_line) {
+            set_error("edge list line " + std::to_string(r.bad_line) +
+                      ": second field missing, negative id or id out of range "
+                      "(undefined behaviour in the reference's read_webgraph)");
+            return (int)PJ_ERR_PARSE;
+        }
+        auto pg = std::make_unique<pj_graph>();
+        pg->g.ctx = &ctx->c;
+        build_graph_from_coo(pg->g, src, dst, weighted ? &w : nullptr, r.nnz, r.max_id + 1, false);
+        return finish_graph(ctx, pg, out);
+    });
+}
+
+int pj_load_snap(pj_ctx* ctx, const char* path, int weighted, pj_graph** out) {
+    if (!ctx || !path || !out) return arg_error("pj_load_snap: bad argument");
+    return guarded([&] {
+        std::vector<char> buf;
+        struct stat sb;
+        // A missing or unreadable file (or a directory) reads as empty, like the
+        // reference's unchecked ifstream (:67): N = 0, header-only sol_file.
+        FILE* f = (stat(path, &sb) == 0 && S_ISREG(sb.st_mode)) ? std::fopen(path, "rb") : nullptr;
+        if (f) {
+            if (sb.st_size > 0) {
+                buf.resize((size_t)sb.st_size);
+                size_t got = std::fread(buf.data(), 1, (size_t)sb.st_size, f);
+                buf.resize(got);
+            }
+            std::fclose(f);
+        }
+        return pj_load_snap_buffer(ctx, buf.data(), (int64_t)buf.size(), weighted, out);
+    });
+}
+
+int pj_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, const uint32_t* w, int64_t nnz,
+                int64_t n_vertices, pj_graph** out) {
+    if (!ctx || !out || nnz < 0 || (nnz > 0 && (!src || !dst))) return arg_error("pj_load_coo: bad argument");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        std::vector<u32> hs((size_t)nnz), hd((size_t)nnz);
+        i64 mx = -1;
+        for (i64 i = 0; i < nnz; ++i) {
+            const i64 a = src[i], b = dst[i];
+            if (a < 0 || b < 0 || a > 0xFFFFFFFEll || b > 0xFFFFFFFEll) {
+                set_error("pj_load_coo: vertex id out of range at edge " + std::to_string(i));
+                return (int)PJ_ERR_RANGE;
+            }
+            hs[(size_t)i] = (u32)a;
+            hd[(size_t)i] = (u32)b;
+            mx = std::max(mx, std::max(a, b));
+        }
+        i64 n = n_vertices < 0 ? mx + 1 : n_vertices;
+        if (n <= mx || n > 0xFFFFFFFFll) {
+            set_error("pj_load_coo: n_vertices must exceed every id and fit 32 bits");
+            return (int)PJ_ERR_RANGE;
+        }
+        hipStream_t s = ctx->c.stream;
+        DevBuf<u32> ds((size_t)nnz), dd((size_t)nnz), dw;
+        if (nnz) {
+            PJ_HIP(hipMemcpyAsync(ds.p, hs.data(), 4 * (size_t)nnz, hipMemcpyHostToDevice, s));
+            PJ_HIP(hipMemcpyAsync(dd.p, hd.data(), 4 * (size_t)nnz, hipMemcpyHostToDevice, s));
+        }
+        if (w) {
+            dw.alloc((size_t)nnz);
+            if (nnz) PJ_HIP(hipMemcpyAsync(dw.p, w, 4 * (size_t)nnz, hipMemcpyHostToDevice, s));
+        }
+        PJ_HIP(hipStreamSynchronize(s));
+        auto pg = std::make_unique<pj_graph>();
+        pg->g.ctx = &ctx->c;
+        build_graph_from_coo(pg->g, ds, dd, w ? &dw : nullptr, nnz, n, false);
+        return finish_graph(ctx, pg, out);
+    });
+}
+
+int pj_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int weighted, pj_graph** out) {
+    if (!ctx || !out || scale < 0 || scale > 31 || edgefactor < 1 || edgefactor > 1024)
+        return arg_error("pj_generate_kronecker: scale must be in [0,31], edgefactor in [1,1024]");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        DevBuf<u32> src, dst, w;
+        generate_kronecker_device(ctx->c, scale, edgefactor, seed, weighted != 0, src, dst, weighted ? &w : nullptr);
+        const i64 nnz = 2 * ((i64)edgefactor << scale);
+        auto pg = std::make_unique<pj_graph>();
+        pg->g.ctx = &ctx->c;
+        build_graph_from_coo(pg->g, src, dst, weighted ? &w : nullptr, nnz, (i64)1 << scale, true);
+        return finish_graph(ctx, pg, out);
+    });
+}
+
+int pj_graph_destroy(pj_graph* g) {
+    if (!g) return PJ_OK;
+    return guarded([&] {
+        bind(*g->g.ctx);
+        delete g;
+        return (int)PJ_OK;
+    });
+}
+
+int pj_graph_info(const pj_graph* g, int64_t* n, int64_t* nnz, int* weighted, int* symmetric) {
+    if (!g) return arg_error("pj_graph_info: graph is NULL");
+    if (n) *n = g->g.n;
+    if (nnz) *nnz = g->g.nnz;
+    if (weighted) *weighted = g->g.weighted ? 1 : 0;
+    if (symmetric) *symmetric = g->g.symmetric ? 1 : 0;
+    return PJ_OK;
+}
+
+int pj_graph_get_csr(const pj_graph* pg, int64_t* row_ptr, int32_t* col, uint32_t* w) {
+    if (!pg) return arg_error("pj_graph_get_csr: graph is NULL");
+    return guarded([&] {
+        const Graph& g = pg->g;
+        bind(*g.ctx);
+        if (row_ptr) {
+            if (g.off64) {
+                PJ_HIP(hipMemcpy(row_ptr, g.row64.p, 8 * (size_t)(g.n + 1), hipMemcpyDeviceToHost));
+            } else {
+                std::vector<u32> tmp((size_t)g.n + 1);
+                PJ_HIP(hipMemcpy(tmp.data(), g.row32.p, 4 * (size_t)(g.n + 1), hipMemcpyDeviceToHost));
+                for (size_t i = 0; i < tmp.size(); ++i) row_ptr[i] = tmp[i];
+            }
+        }
+        if (col && g.nnz) PJ_HIP(hipMemcpy(col, g.col.p, 4 * (size_t)g.nnz, hipMemcpyDeviceToHost));
+        if (w && g.nnz) {
+            if (g.weighted) PJ_HIP(hipMemcpy(w, g.w.p, 4 * (size_t)g.nnz, hipMemcpyDeviceToHost));
+            else std::fill(w, w + g.nnz, 1u);
+        }
+        return (int)PJ_OK;
+    });
+}
+
+int pj_graph_out_degree(const pj_graph* g, int64_t v, int64_t* deg) {
+    if (!g || !deg) return arg_error("pj_graph_out_degree: bad argument");
+    if (v < 0 || v >= g->g.n) return arg_error("pj_graph_out_degree: vertex out of range");
+    return guarded([&] {
+        bind(*g->g.ctx);
+        *deg = out_degree(g->g, v);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_sample_roots(const pj_graph* g, uint64_t seed, int n, int64_t* roots, int* found) {
+    if (!g || !roots || !found || n < 0) return arg_error("pj_sample_roots: bad argument");
+    return guarded([&] {
+        bind(*g->g.ctx);
+        int k = 0;
+        const i64 N = g->g.n;
+        for (uint64_t c = 0; k < n && N > 0 && c < (uint64_t)n * 4096ull; ++c) {
+            const i64 v = (i64)(splitmix64(seed + c) % (uint64_t)N);
+            if (out_degree(g->g, v) < 1) continue;
+            if (std::find(roots, roots + k, v) != roots + k) continue;
+            roots[k++] = v;
+        }
+        *found = k;
+        return (int)PJ_OK;
+    });
+}
+
+int pj_sssp(pj_graph* pg, int64_t source, int32_t* dist_out) {
+    if (!pg) return arg_error("pj_sssp: graph is NULL");
+    return guarded([&] {
+        Graph& g = pg->g;
+        bind(*g.ctx);
+        auto t0 = std::chrono::steady_clock::now();
+        if (g.weighted) delta_solve(g, source);
+        else bfs_solve(g, source);
+        if (dist_out && g.n) PJ_HIP(hipMemcpy(dist_out, g.dist.p, 4 * (size_t)g.n, hipMemcpyDeviceToHost));
+        g.stats.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return (int)PJ_OK;
+    });
+}
+
+int pj_copy_dist(pj_graph* pg, int32_t* dist_out) {
+    if (!pg || !dist_out) return arg_error("pj_copy_dist: bad argument");
+    if (!pg->g.have_result) {
+        set_error("pj_copy_dist: no solve has run on this graph");
+        return PJ_ERR_STATE;
+    }
+    return guarded([&] {
+        bind(*pg->g.ctx);
+        if (pg->g.n) PJ_HIP(hipMemcpy(dist_out, pg->g.dist.p, 4 * (size_t)pg->g.n, hipMemcpyDeviceToHost));
+        return (int)PJ_OK;
+    });
+}
+
+const int32_t* pj_dist_device(pj_graph* pg) { return (pg && pg->g.have_result) ? pg->g.dist.p : nullptr; }
+
+int pj_sssp_batch(pj_graph* pg, const int64_t* sources, int n_src, int32_t* dist_out) {
+    if (!pg || (n_src > 0 && !sources) || n_src < 0) return arg_error("pj_sssp_batch: bad argument");
+    for (int i = 0; i < n_src; ++i) {
+        int rc = pj_sssp(pg, sources[i], dist_out ? dist_out + (size_t)i * (size_t)pg->g.n : nullptr);
+        if (rc != PJ_OK) return rc;
+    }
+    return PJ_OK;
+}
+
+int pj_last_stats(const pj_graph* pg, pj_stats* out) {
+    if (!pg || !out) return arg_error("pj_last_stats: bad argument");
+    if (!pg->g.have_result) {
+        set_error("pj_last_stats: no solve has run on this graph");
+        return PJ_ERR_STATE;
+    }
+    *out = pg->g.stats;
+    return PJ_OK;
+}
+
+int pj_reach_stats(pj_graph* pg, pj_stats* out) {
+    if (!pg) return arg_error("pj_reach_stats: graph is NULL");
+    if (!pg->g.have_result) {
+        set_error("pj_reach_stats: no solve has run on this graph");
+        return PJ_ERR_STATE;
+    }
+    return guarded([&] {
+        bind(*pg->g.ctx);
+        i64 nr = 0, mr = 0;
+        reach_stats(pg->g, &nr, &mr);
+        pg->g.stats.reached = nr;
+        pg->g.stats.reached_edges = mr;
+        if (out) *out = pg->g.stats;
+        return (int)PJ_OK;
+    });
+}
+
+int pj_set_option(pj_graph* pg, const char* key, double value) {
+    if (!pg || !key) return arg_error("pj_set_option: bad argument");
+    Graph& g = pg->g;
+    std::string k(key);
+    if (k == "alpha" && value > 0) g.alpha = value;
+    else if (k == "beta" && value > 0) g.beta = value;
+    else if (k == "delta" && value >= 0) g.delta = value;
+    else if (k == "direction" && (value == 0 || value == 1 || value == 2)) g.force_mode = (int)value;
+    else return arg_error("pj_set_option: unknown key or bad value");
+    return PJ_OK;
+}
+
+// ---------------------------------------------------------------- output --
+// output_vector (:32-46): header line, then one decimal or "inf" per vertex.
+// Formatting is split over host threads into per-chunk buffers and written
+// in order, so the bytes are identical to the sequential writer.
+
+static size_t format_range(const int32_t* d, int64_t a, int64_t b, char* o) {
+    size_t k = 0;
+    for (int64_t i = a; i < b; ++i) {
+        int32_t x = d[i];
+        if (x == PJ_INT_INF) {
+            o[k++] = 'i';
+            o[k++] = 'n';
+            o[k++] = 'f';
+        } else {
+            char rev[12];
+            int r = 0;
+            long long y = x;
+            const bool neg = y < 0;
+            if (neg) y = -y;
+            do {
+                rev[r++] = (char)('0' + y % 10);
+                y /= 10;
+            } while (y);
+            if (neg) o[k++] = '-';
+            while (r) o[k++] = rev[--r];
+        }
+        o[k++] = '\n';
+    }
+    return k;
+}
+
+static const char kHeader[] = "the vector is:\n";
+
+int pj_format_sol(const int32_t* dist, int64_t n, char* buf, int64_t cap, int64_t* len_out) {
+    if (n < 0 || (n > 0 && !dist) || !len_out) return arg_error("pj_format_sol: bad argument");
+    std::vector<char> tmp((size_t)n * 12 + 16);
+    size_t k = sizeof(kHeader) - 1;
+    std::memcpy(tmp.data(), kHeader, k);
+    k += format_range(dist, 0, n, tmp.data() + k);
+    *len_out = (int64_t)k;
+    if (buf) {
+        if (cap < (int64_t)k) return arg_error("pj_format_sol: buffer too small");
+        std::memcpy(buf, tmp.data(), k);
+    }
+    return PJ_OK;
+}
+
+int pj_write_sol(const int32_t* dist, int64_t n, const char* path, int strict) {
+    if (!path || n < 0 || (n > 0 && !dist)) return arg_error("pj_write_sol: bad argument");
+    return guarded([&] {
+        FILE* f = std::fopen(path, "wb");
+        if (!f) {
+            if (strict) {
+                set_error(std::string("cannot open ") + path);
+                return (int)PJ_ERR_IO;
+            }
+            return (int)PJ_OK;  // the reference's ofstream fails silently (:617)
+        }
+        std::fwrite(kHeader, 1, sizeof(kHeader) - 1, f);
+        unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        const int64_t chunk = 1 << 18;
+        const int64_t nchunks = (n + chunk - 1) / chunk;
+        std::vector<std::vector<char>> out((size_t)std::min<int64_t>(nchunks, nt * 2));
+        for (int64_t c0 = 0; c0 < nchunks; c0 += (int64_t)out.size()) {
+            const int64_t cn = std::min<int64_t>((int64_t)out.size(), nchunks - c0);
+            std::vector<size_t> lens((size_t)cn);
+            std::vector<std::thread> th;
+            for (int64_t c = 0; c < cn; ++c) {
+                th.emplace_back([&, c] {
+                    const int64_t a = (c0 + c) * chunk, b = std::min(n, a + chunk);
+                    out[(size_t)c].resize((size_t)(b - a) * 12);
+                    lens[(size_t)c] = format_range(dist, a, b, out[(size_t)c].data());
+                });
+            }
+            for (auto& t : th) t.join();
+            for (int64_t c = 0; c < cn; ++c) std::fwrite(out[(size_t)c].data(), 1, lens[(size_t)c], f);
+        }
+        const bool ok = std::fclose(f) == 0;
+        if (!ok && strict) {
+            set_error(std::string("write failed: ") + path);
+            return (int)PJ_ERR_IO;
+        }
+        return (int)PJ_OK;
+    });
+}
+
+}  // extern "C"

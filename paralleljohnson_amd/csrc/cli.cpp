@@ -1,0 +1,96 @@
+// cli.cpp — `parallel_johnson webfile source_node sol_file`, the drop-in for
+// the reference's process boundary (README:9; parallel_johnson() :286-676,
+// main :678-684). Same arguments, same stderr progress lines, same stdout
+// `Time:` line and the same sol_file bytes; the work runs on the GPU through
+// libpj (include/pj.h).
+//
+// Differences that are not parity targets: lines the
+// reference reads as undefined behaviour are rejected with a message and exit
+// status 255 (the reference's error status, :35/:82/:302).
+//
+// Environment: PJ_DEVICE (HIP ordinal, default 0 or LOCAL_RANK), PJ_WEIGHTED=1
+// (third column = weight, delta-stepping). Under an MPI-style launcher only
+// rank 0 works; the other ranks exit 0.
+#include <cstdlib>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "../../include/pj.h"
+
+namespace {
+
+int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::atoi(v) : dflt;
+}
+
+int launcher_rank() {
+    for (const char* k : {"OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK", "RANK"}) {
+        const char* v = std::getenv(k);
+        if (v && *v) return std::atoi(v);
+    }
+    return 0;
+}
+
+// print_msg :49-53
+void print_msg(const std::string& msg, int rank) {
+    if (rank == 0) std::cerr << msg << std::endl;
+}
+
+[[noreturn]] void fail(const char* what, int rc) {
+    std::cerr << what << " failed (" << rc << "): " << pj_last_error() << std::endl;
+    std::exit(-1);
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+    const int rank = launcher_rank();
+    if (argc != 4) {  // :294-303
+        if (rank == 0) {
+            std::cerr << "to run this program must supply the following command "
+                         "line arguments (in order)"
+                      << std::endl;
+            std::cerr << "argv[1]---web graph file." << std::endl;
+            std::cerr << "argv[2]---source node number." << std::endl;
+            std::cerr << "argv[3]---file to save the solution." << std::endl;
+        }
+        std::exit(-1);
+    }
+    if (rank != 0) return 0;
+
+    print_msg("process 0 reads in the web graph data......", rank);
+    pj_ctx* ctx = nullptr;
+    int rc = pj_create(env_int("PJ_DEVICE", env_int("LOCAL_RANK", 0)), &ctx);
+    if (rc != PJ_OK) fail("pj_create", rc);
+    pj_graph* g = nullptr;
+    rc = pj_load_snap(ctx, argv[1], env_int("PJ_WEIGHTED", 0), &g);
+    if (rc != PJ_OK) fail("pj_load_snap", rc);
+    int64_t n = 0;
+    pj_graph_info(g, &n, nullptr, nullptr, nullptr);
+    std::cerr << "N = " << n << std::endl;  // :320
+    print_msg("read in the webgraph is done.", rank);
+    print_msg("distribute sparse matrix is done.", rank);
+
+    const int source_node = std::atoi(argv[2]);  // :448
+    std::cerr << "compute shortest paths from source node: " << source_node << std::endl;
+    std::cerr << "parallel Johnson's algorithm starts......" << std::endl;
+
+    std::vector<int32_t> dist((size_t)n);
+    rc = pj_sssp(g, source_node, dist.data());
+    if (rc != PJ_OK) fail("pj_sssp", rc);
+    pj_stats st{};
+    pj_last_stats(g, &st);
+    const double t_elapsed = st.kernel_ms / 1000.0;  // device time of the solve (:597-605 analogue)
+    std::cerr << "parallel Johnson's algorithm completes." << std::endl;
+    std::cout << "Time: " << t_elapsed << " seconds when using " << 1 << " processes." << std::endl;
+
+    rc = pj_write_sol(dist.data(), n, argv[3], 0);  // :615-618
+    if (rc != PJ_OK) fail("pj_write_sol", rc);
+    std::cerr << "the shortest path distance vector has been saved in file " << argv[3] << std::endl;
+
+    pj_graph_destroy(g);
+    pj_destroy(ctx);
+    return 0;
+}

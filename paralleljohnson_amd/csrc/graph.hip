@@ -1,0 +1,198 @@
+// graph.hip — CSR/CSC construction from device COO and the Kronecker generator.
+//
+// CSR build = stable radix sort by src + lower-bound row offsets: the GPU form
+// of coord2csr (ParallelJohnson.cpp:117-159), keeping duplicate edges,
+// self-loops and file order inside each row. The CSC (in-edges, used only by
+// the pull/bottom-up BFS step) is a second sort of the CSR by column.
+#include "devutil.h"
+
+namespace pj {
+
+namespace {
+
+__global__ void pack_dst_w_k(const u32* __restrict__ dst, const u32* __restrict__ w, u64* __restrict__ out,
+                             i64 n) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
+        out[i] = (u64)dst[i] | ((u64)w[i] << 32);
+}
+
+__global__ void unpack_dst_w_k(const u64* __restrict__ in, u32* __restrict__ dst, u32* __restrict__ w,
+                               i64 n) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+        u64 x = in[i];
+        dst[i] = (u32)x;
+        w[i] = (u32)(x >> 32);
+    }
+}
+
+int key_bits(i64 n) {
+    int b = 0;
+    while (b < 32 && ((u64)1 << b) < (u64)n) ++b;
+    return b;
+}
+
+template <typename Off>
+void bounds_into(Graph& g, const u32* keys, bool csc) {
+    hipStream_t s = g.ctx->stream;
+    if (sizeof(Off) == 8) {
+        DevBuf<u64>& r = csc ? g.crow64 : g.row64;
+        r.alloc((size_t)g.n + 1);
+        csr_bounds<u64>(keys, g.nnz, g.n, r.p, s);
+    } else {
+        DevBuf<u32>& r = csc ? g.crow32 : g.row32;
+        r.alloc((size_t)g.n + 1);
+        csr_bounds<u32>(keys, g.nnz, g.n, r.p, s);
+    }
+}
+
+void bounds(Graph& g, const u32* keys, bool csc) {
+    if (g.off64) bounds_into<u64>(g, keys, csc);
+    else bounds_into<u32>(g, keys, csc);
+}
+
+}  // namespace
+
+Graph::~Graph() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+}
+
+void build_graph_from_coo(Graph& g, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>* w, i64 nnz, i64 n,
+                          bool symmetric) {
+    hipStream_t s = g.ctx->stream;
+    g.n = n;
+    g.nnz = nnz;
+    g.weighted = (w != nullptr);
+    g.symmetric = symmetric;
+    g.off64 = (u64)nnz > 0xFFFFFFFFull;
+    const int bits = key_bits(n);
+    SortWs ws;
+    if (!g.weighted) {
+        DevBuf<u32> kalt((size_t)nnz), valt((size_t)nnz);
+        u32 *kr, *vr;
+        radix_sort_pairs<u32>(src.p, kalt.p, dst.p, valt.p, nnz, bits, ws, s, &kr, &vr);
+        DevBuf<u32>& K = (kr == src.p) ? src : kalt;
+        DevBuf<u32>& Kspare = (kr == src.p) ? kalt : src;
+        DevBuf<u32>& Vb = (vr == dst.p) ? dst : valt;
+        DevBuf<u32>& Vspare = (vr == dst.p) ? valt : dst;
+        bounds(g, K.p, false);
+        g.col = std::move(Vb);
+        if (!symmetric) {
+            // CSC: sort the (col, src) pairs of the CSR by col.
+            DevBuf<u32> k2((size_t)nnz);
+            if (nnz) PJ_HIP(hipMemcpyAsync(k2.p, g.col.p, sizeof(u32) * (size_t)nnz, hipMemcpyDeviceToDevice, s));
+            u32 *kr2, *vr2;
+            radix_sort_pairs<u32>(k2.p, Kspare.p, K.p, Vspare.p, nnz, bits, ws, s, &kr2, &vr2);
+            bounds(g, kr2, true);
+            PJ_HIP(hipStreamSynchronize(s));  // k2 is freed at scope exit
+            if (vr2 == K.p) g.ccol = std::move(K);
+            else g.ccol = std::move(Vspare);
+        }
+        PJ_HIP(hipStreamSynchronize(s));
+    } else {
+        DevBuf<u64> v((size_t)nnz), valt((size_t)nnz);
+        DevBuf<u32> kalt((size_t)nnz);
+        if (nnz) {
+            pack_dst_w_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(dst.p, w->p, v.p, nnz);
+            PJ_LAUNCH_CHECK();
+        }
+        u32* kr;
+        u64* vr;
+        radix_sort_pairs<u64>(src.p, kalt.p, v.p, valt.p, nnz, bits, ws, s, &kr, &vr);
+        bounds(g, kr, false);
+        g.col.alloc((size_t)nnz);
+        g.w.alloc((size_t)nnz);
+        if (nnz) {
+            unpack_dst_w_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(vr, g.col.p, g.w.p, nnz);
+            PJ_LAUNCH_CHECK();
+        }
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+}
+
+// ------------------------------------------------------------------------
+// Kronecker generator (benchmark input; no reference counterpart). Spec in
+// DESIGN.md §Inputs; restated independently in oracle/pj_oracle.c for tests.
+// ------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ u64 splitmix64(u64 x) {
+    u64 z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+u64 splitmix64_h(u64 x) {
+    u64 z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct PermKeys {
+    u64 mask, k1, k2, c1;
+    int sh;
+};
+
+__device__ __forceinline__ u64 kperm(u64 x, const PermKeys& p) {
+    x = (x * p.k1 + p.c1) & p.mask;
+    x ^= x >> p.sh;
+    x = (x * p.k2) & p.mask;
+    x ^= x >> p.sh;
+    x = (x * p.k1 + (p.c1 >> 7)) & p.mask;
+    return x;
+}
+
+__global__ __launch_bounds__(256) void kronecker_k(int scale, u64 M, u64 seed, int weighted, PermKeys pk,
+                                                   u32* __restrict__ src, u32* __restrict__ dst,
+                                                   u32* __restrict__ w) {
+    const u32 TA = 2448131358u, TAB = 3264175144u, TABC = 4080218931u;  // 0.57, 0.76, 0.95 of 2^32
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (u64)gridDim.x * blockDim.x) {
+        u64 u = 0, v = 0;
+        for (int l = 0; l < scale; ++l) {
+            const u32 r = (u32)(splitmix64(seed ^ ((i << 6) | (u64)l)) >> 32);
+            const u64 bu = r >= TAB;
+            const u64 bv = (r >= TA && r < TAB) || r >= TABC;
+            u = (u << 1) | bu;
+            v = (v << 1) | bv;
+        }
+        u32 pu = 0, pv = 0;
+        if (scale > 0) {
+            pu = (u32)kperm(u, pk);
+            pv = (u32)kperm(v, pk);
+        }
+        src[2 * i] = pu;
+        dst[2 * i] = pv;
+        src[2 * i + 1] = pv;
+        dst[2 * i + 1] = pu;
+        if (w) {
+            const u32 wt = weighted ? 1u + (u32)(splitmix64(seed ^ 0x5851F42D4C957F2Dull ^ i) % 255ull) : 1u;
+            w[2 * i] = wt;
+            w[2 * i + 1] = wt;
+        }
+    }
+}
+
+}  // namespace
+
+void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t seed, bool weighted,
+                               DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>* w) {
+    const u64 M = (u64)edgefactor << scale;
+    src.alloc((size_t)(2 * M));
+    dst.alloc((size_t)(2 * M));
+    if (w) w->alloc((size_t)(2 * M));
+    PermKeys pk;
+    pk.mask = scale >= 64 ? ~0ull : ((1ull << scale) - 1);
+    pk.k1 = splitmix64_h(seed ^ 0x243F6A8885A308D3ull) | 1ull;
+    pk.k2 = splitmix64_h(seed ^ 0x13198A2E03707344ull) | 1ull;
+    pk.c1 = splitmix64_h(seed ^ 0xA4093822299F31D0ull);
+    pk.sh = (scale + 1) / 2;
+    if (M) {
+        kronecker_k<<<grid_for((i64)M, 256, 256u * 64u), 256, 0, ctx.stream>>>(
+            scale, M, seed, weighted ? 1 : 0, pk, src.p, dst.p, w ? w->p : nullptr);
+        PJ_LAUNCH_CHECK();
+    }
+}
+
+}  // namespace pj

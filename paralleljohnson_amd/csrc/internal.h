@@ -1,0 +1,188 @@
+// internal.h — shared declarations of libpj (host + device). Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/pj.h"
+
+namespace pj {
+
+using u32 = uint32_t;
+using u64 = unsigned long long;  // matches HIP's 64-bit atomic overloads
+using i64 = int64_t;
+
+constexpr int32_t INT_INF = PJ_INT_INF;
+
+// ---------------------------------------------------------------- errors --
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_error(const std::string& msg);
+
+#define PJ_HIP(expr)                                                                     \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            throw ::pj::Error(e_ == hipErrorOutOfMemory ? PJ_ERR_OOM : PJ_ERR_HIP,       \
+                              std::string(#expr) + ": " + hipGetErrorString(e_));        \
+    } while (0)
+
+#define PJ_LAUNCH_CHECK() PJ_HIP(hipGetLastError())
+
+// ------------------------------------------------------------ device memory --
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t count) { alloc(count); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    void alloc(size_t count) {
+        release();
+        n = count;
+        if (count) PJ_HIP(hipMalloc(&p, count * sizeof(T)));
+    }
+    void ensure(size_t count) { if (count > n) alloc(count); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    T* get() const { return p; }
+    size_t bytes() const { return n * sizeof(T); }
+};
+
+template <typename T>
+struct PinnedBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+    void alloc(size_t count) {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = count;
+        if (count) PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), count * sizeof(T), hipHostMallocDefault));
+    }
+};
+
+inline unsigned grid_for(i64 work, int per_block, unsigned cap = 256u * 16u) {
+    i64 g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > (i64)cap) g = cap;
+    return (unsigned)g;
+}
+
+// ---------------------------------------------------------------- scan ----
+// Exclusive scan of n u32 (or u64) values into out[0..n] (out[n] = total).
+// Scratch is managed internally per call-site via ScanWs.
+struct ScanWs {
+    DevBuf<u64> part;  // block partials of every recursion level
+    void ensure(i64 n);
+};
+void exclusive_scan_u32(const u32* in, u64* out, i64 n, ScanWs& ws, hipStream_t s);
+void exclusive_scan_u64(const u64* in, u64* out, i64 n, ScanWs& ws, hipStream_t s);
+
+// ---------------------------------------------------------------- sort ----
+// Stable LSD radix sort of (key, value) pairs by key; `bits` = key width to
+// sort. Returns through `*kout/*vout` which of the two buffers holds the result.
+struct SortWs {
+    DevBuf<u32> hist;
+    DevBuf<u64> offs;
+    ScanWs scan;
+};
+template <typename V>
+void radix_sort_pairs(u32* keys, u32* keys_alt, V* vals, V* vals_alt, i64 n, int bits, SortWs& ws,
+                      hipStream_t s, u32** kout, V** vout);
+
+// row_ptr[v] = lower_bound(sorted_keys, v) for v in [0, nv]
+template <typename Off>
+void csr_bounds(const u32* sorted_keys, i64 nnz, i64 nv, Off* row, hipStream_t s);
+
+// ---------------------------------------------------------------- graph ---
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int cu_count = 256;
+};
+
+struct Graph {
+    Ctx* ctx = nullptr;
+    i64 n = 0, nnz = 0;
+    bool weighted = false, symmetric = false;
+    bool off64 = false;  // 64-bit row offsets when nnz >= 2^32
+    // CSR (out-edges)
+    DevBuf<u32> row32, crow32;
+    DevBuf<u64> row64, crow64;
+    DevBuf<u32> col, ccol;  // ccol/crow*: CSC (in-edges) for pull steps; alias CSR when symmetric
+    DevBuf<u32> w;          // CSR-aligned weights (weighted graphs)
+
+    // per-solve workspace (lazily sized)
+    DevBuf<int32_t> dist;
+    DevBuf<u64> visited, fcur, fnext;
+    DevBuf<u32> qv[2], qdeg[2];
+    DevBuf<u64> qbeg[2];
+    DevBuf<u64> qoff;
+    DevBuf<u64> counters;  // device counters (BfsCounters / DeltaCounters)
+    PinnedBuf<u64> hcounters;
+    ScanWs scan;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+    // options
+    double alpha = 14.0, beta = 24.0, delta = 0.0;
+    int force_mode = 0;  // 0 auto, 1 top-down only, 2 bottom-up after level 0
+
+    bool have_result = false;
+    pj_stats stats{};
+
+    const void* row_ptr() const { return off64 ? (const void*)row64.p : (const void*)row32.p; }
+    const void* crow_ptr() const {
+        if (symmetric) return row_ptr();
+        return off64 ? (const void*)crow64.p : (const void*)crow32.p;
+    }
+    const u32* ccol_ptr() const { return symmetric ? col.p : ccol.p; }
+    ~Graph();
+};
+
+// Build CSR (+CSC unless symmetric) from device COO (consumed: buffers are
+// used as sort scratch). n must already be known.
+void build_graph_from_coo(Graph& g, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>* w, i64 nnz,
+                          i64 n, bool symmetric);
+
+// ingestion
+struct ParseResult {
+    i64 nnz = 0;
+    i64 max_id = -1;
+    i64 bad_line = 0;  // 1-based, 0 = none
+};
+// Parses `len` bytes of host text on the device; fills device COO.
+ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool weighted,
+                              DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w);
+
+void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t seed, bool weighted,
+                               DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>* w);
+
+// solvers
+void bfs_solve(Graph& g, i64 source);
+void delta_solve(Graph& g, i64 source);
+void reach_stats(Graph& g, i64* n_r, i64* m_r);
+
+}  // namespace pj

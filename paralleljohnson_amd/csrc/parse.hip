@@ -1,0 +1,178 @@
+// parse.hip — SNAP edge-list text -> COO on the GPU (read_webgraph,
+// ParallelJohnson.cpp:66-105).
+//
+// The text is split into 64-byte segments, one per lane (16 KiB per 256-thread
+// block). Pass 1 counts, per block, the line starts whose first byte is a
+// decimal digit (the reference's edge test :73/:91); an exclusive scan turns
+// the counts into edge indices, so edges keep file order. Pass 2 recomputes
+// the per-lane line-start bitmask and parses each of its lines with
+// `istringstream >> int >> int` semantics (:92-93): leading blanks skipped,
+// optional sign, digits; a non-numeric field reads as 0; extra columns are
+// ignored. Lines the reference turns into undefined behaviour (second field
+// missing, negative id, id overflow) are reported by byte offset.
+#include "devutil.h"
+
+namespace pj {
+
+namespace {
+
+constexpr int PB = 256;
+constexpr int PSEG = 64;
+constexpr i64 PCHUNK = (i64)PB * PSEG;
+constexpr i64 ID_LIMIT = 2147483646;  // N = max + 1 must fit the reference's int (:319)
+
+__device__ __forceinline__ bool is_digit(u32 c) { return (c - (u32)'0') < 10u; }
+__device__ __forceinline__ bool is_blank(u32 c) {
+    return c == ' ' || c == '\t' || c == '\v' || c == '\f' || c == '\r';
+}
+
+// Bitmask of positions p in [seg, seg+64) with text[p] a digit and
+// (p == 0 or text[p-1] == '\n'). The buffer is zero-padded to a multiple of
+// 64 bytes (+64), and '\0' is neither a digit nor a newline.
+__device__ __forceinline__ u64 line_start_mask(const uint8_t* __restrict__ text, i64 seg) {
+    const uint4* p4 = reinterpret_cast<const uint4*>(text + seg);
+    uint4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
+    u32 words[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                     a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+    u32 prev = seg == 0 ? (u32)'\n' : (u32)text[seg - 1];
+    u64 mask = 0;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        const u32 c = (words[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
+        if (prev == (u32)'\n' && is_digit(c)) mask |= 1ull << k;
+        prev = c;
+    }
+    return mask;
+}
+
+// One `>> int` extraction. 1 = read, 0 = failed on a non-blank (value 0),
+// -1 = nothing but blanks before end of line, -2 = overflow.
+__device__ __forceinline__ int extract(const uint8_t* __restrict__ t, i64 len, i64& p, i64& out) {
+    while (p < len && is_blank(t[p])) ++p;
+    if (p >= len || t[p] == '\n') return -1;
+    bool neg = false;
+    u32 c = t[p];
+    if (c == '+' || c == '-') {
+        neg = (c == '-');
+        ++p;
+    }
+    if (p >= len || !is_digit(t[p])) {
+        out = 0;
+        return 0;
+    }
+    i64 acc = 0;
+    bool ovf = false;
+    while (p < len && is_digit(t[p])) {
+        acc = acc * 10 + (t[p] - '0');
+        if (acc > 4294967295ll) {
+            ovf = true;
+            acc = 4294967295ll;
+        }
+        ++p;
+    }
+    if (ovf) return -2;
+    out = neg ? -acc : acc;
+    return 1;
+}
+
+__global__ __launch_bounds__(PB) void parse_count_k(const uint8_t* __restrict__ text, i64 len,
+                                                    u32* __restrict__ block_cnt) {
+    __shared__ u32 lds[PB / WAVE];
+    const i64 seg = (i64)blockIdx.x * PCHUNK + (i64)threadIdx.x * PSEG;
+    u32 c = 0;
+    if (seg < len) c = (u32)__popcll(line_start_mask(text, seg));
+    c = block_sum<PB / WAVE>(c, lds);
+    if (threadIdx.x == 0) block_cnt[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(PB) void parse_lines_k(const uint8_t* __restrict__ text, i64 len, int weighted,
+                                                    const u64* __restrict__ block_off, u32* __restrict__ src,
+                                                    u32* __restrict__ dst, u32* __restrict__ w,
+                                                    u64* __restrict__ maxid, u64* __restrict__ errpos) {
+    __shared__ u64 lds[PB / WAVE];
+    const i64 seg = (i64)blockIdx.x * PCHUNK + (i64)threadIdx.x * PSEG;
+    u64 mask = 0;
+    if (seg < len) mask = line_start_mask(text, seg);
+    u64 tot;
+    u64 idx = block_off[blockIdx.x] + block_excl_scan<PB / WAVE>((u64)__popcll(mask), lds, tot);
+    i64 mx = -1;
+    while (mask) {
+        const int b = __ffsll((long long)mask) - 1;
+        mask &= mask - 1;
+        const i64 start = seg + b;
+        i64 p = start, u = 0, v = 0, wt = 1;
+        int r = extract(text, len, p, u);
+        bool bad = (r != 1) || u > ID_LIMIT;
+        if (!bad) {
+            r = extract(text, len, p, v);
+            bad = r < 0 || v < 0 || v > ID_LIMIT;
+            if (!bad && weighted) {
+                if (r == 0) wt = 0;  // stream failed: the weight extraction stores nothing -> 0
+                else {
+                    int r3 = extract(text, len, p, wt);
+                    bad = r3 < 0 || wt < 0;
+                }
+            }
+        }
+        if (bad) {
+            atomicMin(errpos, (u64)start);
+            u = 0;
+            v = 0;
+        }
+        src[idx] = (u32)u;
+        dst[idx] = (u32)v;
+        if (w) w[idx] = (u32)wt;
+        ++idx;
+        mx = u > mx ? u : mx;
+        mx = v > mx ? v : mx;
+    }
+    mx = wave_max(mx);
+    if (lane_id() == 0 && mx >= 0) atomicMax(maxid, (u64)(mx + 1));
+}
+
+}  // namespace
+
+ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool weighted, DevBuf<u32>& src,
+                              DevBuf<u32>& dst, DevBuf<u32>& w) {
+    hipStream_t s = ctx.stream;
+    ParseResult r;
+    const i64 nblocks = (len + PCHUNK - 1) / PCHUNK;
+    const i64 padded = nblocks * PCHUNK + 64;
+    DevBuf<uint8_t> text((size_t)padded);
+    PJ_HIP(hipMemsetAsync(text.p, 0, (size_t)padded, s));
+    if (len) PJ_HIP(hipMemcpyAsync(text.p, host_text, (size_t)len, hipMemcpyHostToDevice, s));
+    DevBuf<u32> bcnt((size_t)(nblocks > 0 ? nblocks : 1));
+    DevBuf<u64> boff((size_t)nblocks + 1);
+    DevBuf<u64> scal(2);  // [0] = max id + 1, [1] = first bad byte offset
+    ScanWs ws;
+    if (nblocks) {
+        parse_count_k<<<(unsigned)nblocks, PB, 0, s>>>(text.p, len, bcnt.p);
+        PJ_LAUNCH_CHECK();
+    }
+    exclusive_scan_u32(bcnt.p, boff.p, nblocks, ws, s);
+    u64 h[2] = {0ull, ~0ull};
+    u64 total = 0;
+    PJ_HIP(hipMemcpyAsync(&total, boff.p + nblocks, sizeof(u64), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipMemcpyAsync(scal.p, h, sizeof(h), hipMemcpyHostToDevice, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    src.alloc((size_t)total);
+    dst.alloc((size_t)total);
+    if (weighted) w.alloc((size_t)total);
+    if (nblocks && total) {
+        parse_lines_k<<<(unsigned)nblocks, PB, 0, s>>>(text.p, len, weighted ? 1 : 0, boff.p, src.p, dst.p,
+                                                      weighted ? w.p : nullptr, scal.p, scal.p + 1);
+        PJ_LAUNCH_CHECK();
+    }
+    PJ_HIP(hipMemcpyAsync(h, scal.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    r.nnz = (i64)total;
+    r.max_id = (i64)h[0] - 1;
+    if (h[1] != ~0ull) {
+        i64 line = 1;
+        for (i64 i = 0; i < (i64)h[1]; ++i) line += host_text[i] == '\n';
+        r.bad_line = line;
+    }
+    return r;
+}
+
+}  // namespace pj

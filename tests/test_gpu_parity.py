@@ -1,0 +1,205 @@
+"""GPU parity tests: libpj (HIP, via the C-ABI) against the oracle.
+
+Bar: bit-exact distances (integer work). Small cases compare every vertex
+with the oracle; the full-size Kronecker s22 case is checked vertex by vertex
+against the oracle BFS too (the CPU BFS finishes in seconds).
+"""
+import hashlib
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import chain_text, random_graph, to_text
+
+pytestmark = pytest.mark.gpu
+INF = 100000
+
+
+def _oracle_csr(oracle, text, weighted=False):
+    s, d, w, n = oracle.parse_snap(text, weighted=weighted)
+    row, col, wc = oracle.coo2csr(s, d, n, w)
+    return row, col, wc
+
+
+def test_appendix_b_on_gpu(ctx, pj, appendix_b):
+    import ctypes
+    atoi = ctypes.CDLL(None).atoi
+    for case in appendix_b:
+        if case.get("generator"):
+            continue
+        text = case["text"].encode()
+        if case["expect"] == "parse_error":
+            with pytest.raises(pj.PJError) as e:
+                ctx.load_snap_buffer(text)
+            assert e.value.name == "PJ_ERR_PARSE" and "line 2" in str(e.value)
+            continue
+        g = ctx.load_snap_buffer(text)
+        d = g.sssp(atoi(case["source"].encode()))
+        assert d.tolist() == case["expect"], case["name"]
+        assert pj.format_sol(d).decode() == case["sol"], case["name"]
+        g.close()
+
+
+def test_chain_cap(ctx, pj, appendix_b):
+    case = next(c for c in appendix_b if c.get("generator") == "chain")
+    g = ctx.load_snap_buffer(chain_text(case["n"]))
+    d = g.sssp(0)
+    out = pj.format_sol(d)
+    assert hashlib.sha256(out).hexdigest() == case["sol_sha256"]
+    assert d[99999] == 99999 and d[100000] == INF
+    assert g.stats()["levels"] == 99999
+
+
+@pytest.mark.parametrize("style", [0, 1, 2])
+def test_parse_and_csr_bit_exact(ctx, oracle, style):
+    rng = np.random.default_rng(11 + style)
+    for kind in ("uniform", "hub", "chain"):
+        n = int(rng.integers(2, 30000))
+        src, dst = random_graph(rng, kind, n)
+        text = to_text(src, dst, style=style)
+        row, col, _ = _oracle_csr(oracle, text)
+        g = ctx.load_snap_buffer(text)
+        grow, gcol, _ = g.get_csr()
+        assert g.n == len(row) - 1
+        assert (grow == row).all()
+        assert (gcol.astype(np.uint32) == col).all()  # stable: file order inside rows
+
+
+def test_parse_weird_lines(ctx, oracle):
+    text = b"12abc 3\n7\t+5\n4 -0\n9 -\n0x1 8\n#x\n \t1 2\n1\x002\n3 4 5 6\r\n"
+    row, col, _ = _oracle_csr(oracle, text)
+    g = ctx.load_snap_buffer(text)
+    grow, gcol, _ = g.get_csr()
+    assert (grow == row).all() and (gcol.astype(np.uint32) == col).all()
+    for bad in (b"0 1\n5\n", b"0 1\n5 \n", b"0 1\n1 -3\n", b"0 1\n1 99999999999\n"):
+        with pytest.raises(Exception):
+            ctx.load_snap_buffer(bad)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "hub", "chain"])
+@pytest.mark.parametrize("direction", [0, 1, 2])
+def test_bfs_random_graphs(ctx, oracle, kind, direction):
+    rng = np.random.default_rng(100 + 7 * direction + len(kind))
+    for trial in range(4):
+        n = int(rng.integers(2, 60000))
+        src, dst = random_graph(rng, kind, n)
+        g = ctx.load_coo(src, dst, n=n)
+        g.set_option("direction", direction)
+        row, col, _ = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n)
+        roots = [int(src[0]) if len(src) else 0, int(rng.integers(0, n)), n, -5]
+        for r in roots:
+            d = g.sssp(r)
+            assert (d == oracle.bfs(row, col, r)).all(), (kind, direction, trial, r)
+        g.close()
+
+
+def test_kronecker_generator_matches_spec(ctx, oracle):
+    for scale, ef, seed in ((1, 1, 5), (8, 4, 9), (12, 16, 1)):
+        g = ctx.generate_kronecker(scale, ef, seed)
+        assert g.symmetric and g.n == 1 << scale and g.nnz == 2 * (ef << scale)
+        s, d, _ = oracle.kronecker(scale, ef, seed)
+        row, col, _ = oracle.coo2csr(s, d, 1 << scale)
+        grow, gcol, _ = g.get_csr()
+        assert (grow == row).all() and (gcol.astype(np.uint32) == col).all()
+
+
+@pytest.mark.parametrize("scale", [10, 14, 16])
+def test_bfs_kronecker(ctx, oracle, scale):
+    g = ctx.generate_kronecker(scale, 16, 2)
+    row, col, _ = g.get_csr()
+    col = col.astype(np.uint32)
+    for r in g.sample_roots(3, 4):
+        d = g.sssp(int(r))
+        exp = oracle.bfs(row, col, int(r))
+        assert (d == exp).all()
+        st = g.reach_stats()
+        reached = exp < INF
+        assert st["reached"] == reached.sum()
+        assert st["reached_edges"] == np.diff(row)[reached].sum()
+
+
+def test_bfs_kronecker_s22_full_size(ctx, oracle):
+    """BASELINE.json configs[1] at full size, every vertex against the oracle."""
+    g = ctx.generate_kronecker(22, 16, 1)
+    assert g.nnz == 134217728
+    row, col, _ = g.get_csr()
+    col = col.astype(np.uint32)
+    r = int(g.sample_roots(1, 1)[0])
+    d = g.sssp(r)
+    exp = oracle.bfs(row, col, r)
+    assert (d == exp).all()
+    st = g.stats()
+    assert st["bu_levels"] > 0 and st["td_levels"] > 0  # direction switching exercised
+    g.close()
+
+
+def test_weighted_delta_stepping(ctx, oracle):
+    rng = np.random.default_rng(21)
+    for trial in range(6):
+        n = int(rng.integers(2, 40000))
+        src, dst = random_graph(rng, ["uniform", "hub", "chain"][trial % 3], n)
+        w = rng.integers(0 if trial % 2 else 1, [3, 300, 5000][trial % 3], len(src)).astype(np.uint32)
+        g = ctx.load_coo(src, dst, w=w, n=n)
+        row, col, wc = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n, w)
+        for delta in (0, 1, 37):
+            g.set_option("delta", delta)
+            for r in (int(src[0]) if len(src) else 0, int(rng.integers(0, n))):
+                assert (g.sssp(r) == oracle.dijkstra(row, col, wc, r)).all(), (trial, delta, r)
+        g.close()
+
+
+def test_weighted_text_and_kronecker(ctx, oracle):
+    text = b"0 1 5\n0 2 1\n2 1 1\n1 3 99999\n3 4 1\n2 4 200000\n"
+    g = ctx.load_snap_buffer(text, weighted=True)
+    row, col, wc = _oracle_csr(oracle, text, weighted=True)
+    assert g.sssp(0).tolist() == oracle.dijkstra(row, col, wc, 0).tolist() == [0, 2, 1, INF, INF]
+    g = ctx.generate_kronecker(14, 16, 4, weighted=True)
+    row, col, wc = g.get_csr()
+    col = col.astype(np.uint32)
+    for r in g.sample_roots(8, 3):
+        assert (g.sssp(int(r)) == oracle.dijkstra(row, col, wc, int(r))).all()
+
+
+def test_batch_and_empty(ctx, oracle):
+    g = ctx.generate_kronecker(11, 8, 6)
+    row, col, _ = g.get_csr()
+    col = col.astype(np.uint32)
+    roots = list(g.sample_roots(1, 5)) + [-1, 1 << 11]
+    out = g.sssp_batch(roots)
+    for i, r in enumerate(roots):
+        assert (out[i] == oracle.bfs(row, col, int(r))).all()
+    e = ctx.load_snap_buffer(b"")
+    assert e.n == 0 and e.sssp(0).size == 0
+
+
+def test_cli_end_to_end(pj, oracle, tmp_path):
+    rng = np.random.default_rng(3)
+    src, dst = random_graph(rng, "hub", 5000)
+    text = to_text(src, dst, style=1)
+    f = tmp_path / "g.txt"
+    f.write_bytes(text)
+    out = tmp_path / "sol.txt"
+    r = subprocess.run([pj.cli_path(), str(f), "7", str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    row, col, _ = _oracle_csr(oracle, text)
+    assert out.read_bytes() == oracle.format_sol(oracle.bfs(row, col, 7))
+    lines = r.stderr.splitlines()
+    assert lines == [
+        "process 0 reads in the web graph data......",
+        f"N = {len(row) - 1}",
+        "read in the webgraph is done.",
+        "distribute sparse matrix is done.",
+        "compute shortest paths from source node: 7",
+        "parallel Johnson's algorithm starts......",
+        "parallel Johnson's algorithm completes.",
+        f"the shortest path distance vector has been saved in file {out}",
+    ]
+    assert r.stdout.startswith("Time: ") and r.stdout.endswith(" seconds when using 1 processes.\n")
+    # missing input file -> N = 0, header-only sol_file, rc 0 (Appendix B)
+    r = subprocess.run([pj.cli_path(), str(tmp_path / "missing.txt"), "0", str(out)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and out.read_bytes() == b"the vector is:\n" and "N = 0" in r.stderr
+    # atoi source semantics
+    r = subprocess.run([pj.cli_path(), str(f), "7abc", str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and out.read_bytes() == oracle.format_sol(oracle.bfs(row, col, 7))
