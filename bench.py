@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_s22.json"))
+    ap.add_argument("--opt", action="append", default=[], help="libpj graph option key=value (tuning)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -64,6 +65,9 @@ def main():
 
     ctx = pj.Context(local)
     g = ctx.generate_kronecker(args.scale, args.edgefactor, args.seed)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        g.set_option(k, float(v))
     n_roots = 64
     roots = g.sample_roots(args.seed + 1, n_roots)
     # weak scaling: rank r takes roots r, r+world, ... (distinct roots per rank)

@@ -366,6 +366,8 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "beta" && value > 0) g.beta = value;
     else if (k == "delta" && value >= 0) g.delta = value;
     else if (k == "direction" && (value == 0 || value == 1 || value == 2)) g.force_mode = (int)value;
+    else if (k == "level_batch" && value >= 0 && value <= 4096) g.level_batch = (int)value;
+    else if (k == "grid_per_cu" && value >= 0 && value <= 16) g.grid_per_cu = (int)value;
     else return arg_error("pj_set_option: unknown key or bad value");
     return PJ_OK;
 }

@@ -4,21 +4,35 @@
 // the BSP round loop :507-594). With w == 1 (:147) the reference computes hop
 // distances capped at INT_INF; the result does not depend on
 // pop order, so each BFS level settles exactly the vertices the heap would
-// settle at that distance.
+// settle at that distance, and no level assigns a distance >= INT_INF.
 //
 // Device state (HBM):
-//   dist[n]      int32, PJ_INT_INF = unreached            (the reference's sp[] :443)
-//   visited      1 bit / vertex (u64 words)               (replaces the in-heap marker sp==INT_INF)
-//   fcur/fnext   frontier bitmaps for pull levels
-//   queue        (v, out-degree, row begin) per frontier vertex with out-degree > 0,
-//                plus an exclusive scan of the degrees for edge-balanced push levels
-// Push (top-down) level: every frontier edge is one work item; a 1024-edge
-//   tile finds its frontier slots by binary search in LDS, so a 300K-edge hub
-//   is split over ~300 workgroups. Claims use atomicOr on the visited word.
-// Pull (bottom-up) level: one wave per 64-vertex visited word; lanes scan the
-//   in-edges (CSC) of unvisited vertices and stop at the first parent in fcur.
-//   The wave owns its visited/fnext words, so no atomics are needed.
-// Switching follows Beamer's heuristic (alpha, beta).
+//   dist[n]      int32, PJ_INT_INF = unreached              (the reference's sp[] :443)
+//   vis[2]       visited bitmaps, 1 bit / vertex, seeded with the isolated-vertex
+//                mask (such vertices are never reached and never act as parents)
+//   normal queue frontier vertices with 1 <= out-degree <= HUBT, vertex ids only,
+//                in NQS segments of capacity n, one append counter per segment
+//                (counters on separate 64-B lines: NQS x the single-word atomic rate)
+//   hub queue    (v, row begin, edge offset) of frontier vertices with out-degree >
+//                HUBT; slot and edge offset come from ONE packed 64-bit atomic, so
+//                the offsets are monotonic in the slot index without a scan
+//   C[3], S[2]   per-level counters and control state (ring buffers, see below)
+//
+// One kernel launch per level and no host round trip inside a batch of levels:
+//   * every block re-derives the direction decision (Beamer's alpha/beta rule) from
+//     the previous level's counters C[(L+2)%3] and state S[(L+1)%2]; block 0
+//     publishes S[L%2] and zeroes C[(L+1)%3]; the level accumulates into C[L%3].
+//   * push (top-down) levels: a block takes 256 normal entries, reads their rows and
+//     walks their edges in 256-edge steps (owner found by binary search in LDS);
+//     hub edges go in 1024-edge tiles (slot found by binary search in LDS), so a
+//     300K-edge hub is spread over ~300 workgroups. Claims: atomicOr on vis.
+//   * pull (bottom-up) levels: a wave takes WPI 64-vertex words; an unvisited vertex
+//     looks for any in-neighbour that is already visited (for an unvisited vertex
+//     that is exactly "in the frontier"). Lanes probe their first edges with
+//     independent loads, then the whole wave scans the rest of long rows. The wave
+//     owns its words and writes vis_next[w] = vis[w] | found without atomics.
+//   * new frontier entries are staged in LDS and published with one atomic per
+//     block step (per segment), not one per wave.
 #include <chrono>
 
 #include "lb.h"
@@ -27,177 +41,650 @@ namespace pj {
 
 namespace {
 
-struct BfsCnt {
-    u64 n_next;   // queue entries appended (new vertices with out-degree > 0)
-    u64 m_next;   // sum of their out-degrees (edges of the next push level)
-    u64 found;    // newly visited vertices
-    u64 in_next;  // sum of in-degrees of newly visited vertices (Beamer's m_u bookkeeping)
+constexpr int TB = 256;
+constexpr int NW = TB / WAVE;
+constexpr u32 HUBT = 256;     // out-degree above which a frontier vertex goes to the hub queue
+constexpr int HUB_TILE = 1024;
+constexpr int WPI = 4;        // pull levels: visited words per wave and iteration
+constexpr int QCAP = TB * WPI;  // staging: most normal entries one block step can produce
+constexpr int HCAP = 256;     // staging for hubs (overflow goes straight to global)
+constexpr int BU_SERIAL = 16; // edges a lane probes alone before the wave helps
+constexpr int PB1 = 2;        // pull probes, stage A (every candidate)
+constexpr int PB2 = 8;        // pull probes, stage B (candidates still open)
+constexpr int NSH = 16;       // shards of the summed counters
+constexpr int NQS = 8;        // normal-queue segments
+constexpr int SC = 16;        // pull levels: visited words a wave screens at once
+
+struct alignas(64) Line {
+    u64 v;
+    u64 pad[7];
 };
 
-constexpr int TB = 256;
-constexpr int TD_IPT = 4;
-constexpr int TD_TILE = TB * TD_IPT;
+struct LevelCnt {
+    Line n_norm[NQS];  // normal-queue entries appended, per segment
+    Line hub_packed;   // (hub count << eb) | hub edges
+    u64 m_next[NSH];   // out-degree sum of the new frontier (edges of the next push level)
+    u64 found[NSH];    // newly visited vertices
+    u64 in_next[NSH];  // in-degree sum of newly visited vertices
+    u64 fnz[NSH];      // newly visited vertices with out-degree > 0 (the next frontier)
+};
+
+struct LevelState {
+    int32_t mode;  // 0 push, 1 pull
+    int32_t done;
+    int32_t vsel;  // visited buffer holding "dist <= level" at the start of the next level
+    int32_t level; // last level computed
+    double m_u;    // Beamer: in-edges of unvisited vertices
+    u64 prev_found;
+    u64 pad[5];
+};
+
+struct BfsArgs {
+    i64 n, nwords;
+    int eb;  // edge bits of the packed hub counter
+    double alpha, beta;
+    int force;  // 0 auto, 1 push only, 2 pull whenever possible
+    int32_t* dist;
+    u64* vis[2];
+    u64* fnew;   // pull levels: bitmap of the vertices they found (next frontier)
+    u32* qv[2];  // [parity], NQS segments of n entries
+    u32* hv[2];
+    u64* hbeg[2];
+    u64* hoff[2];
+    LevelCnt* C;    // [3]
+    LevelState* S;  // [2]
+    u64* nmode;     // [2] push / pull levels run (device)
+    int64_t* host;  // mapped host words: [0] levels run (-1 while running), [1] push, [2] pull
+};
 
 template <typename Off>
-__global__ void bfs_source_k(i64 s, const Off* __restrict__ row, const Off* __restrict__ crow,
-                             int32_t* __restrict__ dist, u64* __restrict__ visited, u32* __restrict__ qv,
-                             u32* __restrict__ qdeg, u64* __restrict__ qbeg, BfsCnt* __restrict__ c) {
-    dist[s] = 0;
-    visited[s >> 6] |= 1ull << (s & 63);
-    const Off b = row[s], e = row[s + 1];
-    const u32 deg = (u32)(e - b);
-    if (deg) {
-        qv[0] = (u32)s;
-        qdeg[0] = deg;
-        qbeg[0] = (u64)b;
-        c->n_next = 1;
-        c->m_next = deg;
-    }
-    c->found = 1;
-    c->in_next = (u64)(crow[s + 1] - crow[s]);
-}
+struct Graph_d {
+    const Off* row;
+    const u32* col;
+    const Off* crow;
+    const u32* ccol;
+};
 
-template <typename T>
-__device__ __forceinline__ void block_add3(T a, T b, T c, T* lds, u64* da, u64* db, u64* dc) {
-    a = block_sum<TB / WAVE>(a, lds);
-    b = block_sum<TB / WAVE>(b, lds);
-    c = block_sum<TB / WAVE>(c, lds);
-    if (threadIdx.x == 0) {
-        if (a) atomicAdd(da, (u64)a);
-        if (b) atomicAdd(db, (u64)b);
-        if (c) atomicAdd(dc, (u64)c);
-    }
-}
+struct Decision {
+    int32_t mode, vsel, prev_mode;
+    double m_u;
+    u64 found;
+    u64 nseg[NQS];
+    u64 nh, he;
+};
 
-// Push level over `total` frontier edges.
-template <typename Off, bool SYM>
-__global__ __launch_bounds__(TB) void td_expand_k(const u64* __restrict__ qbeg, const u64* __restrict__ qoff,
-                                                  u64 nq, u64 total, const u32* __restrict__ col,
-                                                  const Off* __restrict__ row, const Off* __restrict__ crow,
-                                                  u64* __restrict__ visited, int32_t* __restrict__ dist,
-                                                  int32_t nl, u32* __restrict__ qv_n, u32* __restrict__ qdeg_n,
-                                                  u64* __restrict__ qbeg_n, BfsCnt* __restrict__ cnt) {
-    __shared__ LbShared<TD_TILE> sh;
-    __shared__ u64 red[TB / WAVE];
-    const int t = threadIdx.x;
-    const u64 ntiles = (total + TD_TILE - 1) / TD_TILE;
-    u64 my_m = 0, my_found = 0, my_in = 0;
-    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const u64 e0 = tile * TD_TILE;
-        const u64 e1 = min(e0 + (u64)TD_TILE, total);
-        u64 s0;
-        u32 ns;
-        lb_tile_load<TD_TILE>(qoff, nq, e0, sh, s0, ns);
+// Decision for level L, identical in every block: 2 = run, 1 = the BFS ends at
+// this level, 0 = it ended before.
+__device__ __forceinline__ int decide(const BfsArgs& a, int32_t L, Decision& d) {
+    const LevelState& ps = a.S[(L + 1) & 1];
+    const LevelCnt& pc = a.C[(L + 2) % 3];
+    d.mode = ps.mode;
+    d.prev_mode = ps.mode;
+    d.vsel = ps.vsel;
+    d.m_u = ps.m_u;
+    d.found = ps.prev_found;
+    if (ps.done) return 0;
+    u64 nn = 0;
 #pragma unroll
-        for (int k = 0; k < TD_IPT; ++k) {
-            const u64 e = e0 + (u64)k * TB + t;
-            const bool valid = e < e1;
-            u32 v = 0;
-            bool claim = false;
-            if (valid) {
-                const u32 j = lb_find<TD_TILE>(sh, ns, e);
-                v = col[qbeg[s0 + j] + (e - sh.off[j])];
-                u64* wp = visited + (v >> 6);
-                const u64 bit = 1ull << (v & 63);
-                if (!(*wp & bit)) claim = !(atomicOr(wp, bit) & bit);
-            }
-            u32 deg = 0;
-            u64 beg = 0;
-            if (claim) {
-                dist[v] = nl;
-                const Off b = row[v], en = row[v + 1];
-                deg = (u32)(en - b);
-                beg = (u64)b;
-                my_m += deg;
-                my_found += 1;
-                my_in += SYM ? (u64)deg : (u64)(crow[v + 1] - crow[v]);
-            }
-            const bool app = claim && deg > 0;
-            const u64 slot = wave_append(app, &cnt->n_next);
-            if (app) {
-                qv_n[slot] = v;
-                qdeg_n[slot] = deg;
-                qbeg_n[slot] = beg;
-            }
-        }
-        __syncthreads();
+    for (int k = 0; k < NQS; ++k) {
+        d.nseg[k] = pc.n_norm[k].v;
+        nn += d.nseg[k];
     }
-    block_add3<u64>(my_m, my_found, my_in, red, &cnt->m_next, &cnt->found, &cnt->in_next);
+    const u64 hp = pc.hub_packed.v;
+    d.nh = hp >> a.eb;
+    d.he = hp & ((1ull << a.eb) - 1ull);
+    u64 mq = 0, fd = 0, in = 0, fz = 0;
+#pragma unroll
+    for (int k = 0; k < NSH; ++k) {
+        mq += pc.m_next[k];
+        fd += pc.found[k];
+        in += pc.in_next[k];
+        fz += pc.fnz[k];
+    }
+    (void)nn;
+    d.found = fd;
+    d.m_u = ps.m_u - (double)in;
+    if (fz == 0 || L + 1 >= INT_INF) return 1;
+    if (a.force == 1) d.mode = 0;
+    else if (a.force == 2) d.mode = 1;
+    else if (d.mode == 0) {
+        if ((double)mq > d.m_u / a.alpha) d.mode = 1;
+    } else if ((double)fd < (double)a.n / a.beta && fd < ps.prev_found) {
+        d.mode = 0;
+    }
+    return 2;
 }
 
-// Pull level: one wave per 64-vertex word of the visited bitmap.
-template <typename Off>
-__global__ __launch_bounds__(TB) void bu_step_k(i64 n, i64 nwords, u64* __restrict__ visited,
-                                                const u64* __restrict__ fcur, u64* __restrict__ fnext,
-                                                const Off* __restrict__ crow, const u32* __restrict__ ccol,
-                                                const Off* __restrict__ row, int32_t* __restrict__ dist,
-                                                int32_t nl, u32* __restrict__ qv_n, u32* __restrict__ qdeg_n,
-                                                u64* __restrict__ qbeg_n, BfsCnt* __restrict__ cnt) {
-    __shared__ u64 red[TB / WAVE];
-    const int lane = lane_id();
-    const i64 gw0 = (i64)blockIdx.x * (TB / WAVE) + wave_id();
-    const i64 gstride = (i64)gridDim.x * (TB / WAVE);
-    u64 my_m = 0, my_found = 0, my_in = 0;
-    for (i64 wd = gw0; wd < nwords; wd += gstride) {
-        const u64 vis = visited[wd];
-        const u64 valid = (wd == nwords - 1 && (n & 63)) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
-        const u64 todo = ~vis & valid;
-        if (todo == 0) {
-            if (lane == 0) fnext[wd] = 0;
-            continue;
+struct BlockQ {
+    u32 n, nh;
+    u64 base, hbase;
+    u32 v[QCAP];
+    u32 hv[HCAP];
+    u32 hdeg[HCAP];
+    u64 hbeg[HCAP];
+    u64 scan[NW];
+};
+
+struct Acc {
+    u64 m = 0, f = 0, in = 0, fz = 0;
+};
+
+__device__ __forceinline__ void hub_direct(const BfsArgs& a, int32_t L, bool ish, u32 v, u32 deg, u64 beg) {
+    // staging full: publish this wave's hubs with one packed atomic
+    const u64 hm = __ballot(ish);
+    if (!hm) return;
+    const int np = (L + 1) & 1;
+    const u64 d = ish ? (u64)deg : 0ull;
+    const u64 incl = wave_incl_scan(d);
+    const u64 tot = __shfl(incl, 63, 64);
+    const int leader = __ffsll((long long)hm) - 1;
+    u64 old = 0;
+    if (lane_id() == leader) old = atomicAdd(&a.C[L % 3].hub_packed.v, ((u64)__popcll(hm) << a.eb) + tot);
+    old = __shfl(old, leader, 64);
+    if (ish) {
+        const u64 hs = (old >> a.eb) + (u64)__popcll(hm & lanemask_lt());
+        a.hv[np][hs] = v;
+        a.hbeg[np][hs] = beg;
+        a.hoff[np][hs] = (old & ((1ull << a.eb) - 1ull)) + incl - d;
+    }
+}
+
+// Stage one candidate per lane (whole wave calls). KNOWN: row bounds supplied.
+template <typename Off, bool SYM, bool KNOWN = false>
+__device__ __forceinline__ void stage(BlockQ& q, const BfsArgs& a, const Graph_d<Off>& g, int32_t L, bool pred,
+                                      u32 v, u64 in_deg, Acc& acc, Off kb = 0, Off ke = 0) {
+    u32 deg = 0;
+    u64 beg = 0;
+    if (pred) {
+        Off b = kb, e = ke;
+        if (!KNOWN) {
+            b = g.row[v];
+            e = g.row[v + 1];
         }
-        const i64 v = wd * 64 + lane;
-        bool found = false;
-        Off b = 0, e = 0;
-        if ((todo >> lane) & 1ull) {
-            b = crow[v];
-            e = crow[v + 1];
-            for (Off k = b; k < e; ++k) {
-                const u32 u = ccol[k];
-                if ((fcur[u >> 6] >> (u & 63)) & 1ull) {
-                    found = true;
-                    break;
+        deg = (u32)(e - b);
+        beg = (u64)b;
+        acc.m += deg;
+        acc.f += 1;
+        acc.fz += deg > 0;
+        acc.in += SYM ? (u64)deg : in_deg;
+    }
+    const bool isn = pred && deg > 0 && deg <= HUBT;
+    const u64 m = __ballot(isn);
+    if (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        u32 pos = 0;
+        if (lane_id() == leader) pos = atomicAdd(&q.n, (u32)__popcll(m));
+        pos = __shfl(pos, leader, 64) + (u32)__popcll(m & lanemask_lt());
+        if (isn) q.v[pos] = v;
+    }
+    const bool ish = pred && deg > HUBT;
+    const u64 hm = __ballot(ish);
+    if (hm) {
+        const int leader = __ffsll((long long)hm) - 1;
+        u32 pos = 0;
+        if (lane_id() == leader) pos = atomicAdd(&q.nh, (u32)__popcll(hm));
+        pos = __shfl(pos, leader, 64);
+        if (pos + (u32)__popcll(hm) <= (u32)HCAP) {
+            pos += (u32)__popcll(hm & lanemask_lt());
+            if (ish) {
+                q.hv[pos] = v;
+                q.hdeg[pos] = deg;
+                q.hbeg[pos] = beg;
+            }
+        } else {
+            if (lane_id() == leader) atomicSub(&q.nh, (u32)__popcll(hm));
+            hub_direct(a, L, ish, v, deg, beg);
+        }
+    }
+}
+
+// Block-uniform: publish everything staged (one atomic per queue).
+__device__ __forceinline__ void flush(BlockQ& q, const BfsArgs& a, int32_t L) {
+    __syncthreads();
+    const u32 n = q.n, nh = q.nh;
+    if (!(n | nh)) return;
+    const int np = (L + 1) & 1;
+    LevelCnt* c = a.C + (L % 3);
+    const u32 t = threadIdx.x;
+    const int seg = blockIdx.x % NQS;
+    // hub edge offsets: block scan of the staged hub degrees (one per thread, HCAP == TB)
+    const u64 hd = t < nh ? (u64)q.hdeg[t] : 0ull;
+    u64 tot;
+    const u64 ex = block_excl_scan<NW>(hd, q.scan, tot);
+    if (t == 0) {
+        if (n) q.base = atomicAdd(&c->n_norm[seg].v, (u64)n);
+        if (nh) q.hbase = atomicAdd(&c->hub_packed.v, ((u64)nh << a.eb) + tot);
+    }
+    __syncthreads();
+    u32* qout = a.qv[np] + (u64)seg * (u64)a.n + q.base;
+    for (u32 i = t; i < n; i += TB) qout[i] = q.v[i];
+    if (t < nh) {
+        const u64 hs = (q.hbase >> a.eb) + t;
+        a.hv[np][hs] = q.hv[t];
+        a.hbeg[np][hs] = q.hbeg[t];
+        a.hoff[np][hs] = (q.hbase & ((1ull << a.eb) - 1ull)) + ex;
+    }
+    __syncthreads();
+    if (t == 0) q.n = q.nh = 0;
+    __syncthreads();
+}
+
+__device__ __forceinline__ void flush_acc(const BfsArgs& a, int32_t L, const Acc& acc, u64* red) {
+    const u64 m = block_sum<NW>(acc.m, red);
+    const u64 f = block_sum<NW>(acc.f, red);
+    const u64 in = block_sum<NW>(acc.in, red);
+    const u64 fz = block_sum<NW>(acc.fz, red);
+    if (threadIdx.x == 0) {
+        LevelCnt* c = a.C + (L % 3);
+        const int sh = blockIdx.x % NSH;
+        if (m) atomicAdd(&c->m_next[sh], m);
+        if (f) atomicAdd(&c->found[sh], f);
+        if (in) atomicAdd(&c->in_next[sh], in);
+        if (fz) atomicAdd(&c->fnz[sh], fz);
+    }
+}
+
+// position of the r-th set bit (0-based) of w; r < popcount(w)
+__device__ __forceinline__ u32 select_bit(u64 w, u32 r) {
+    u32 base = 0;
+#pragma unroll
+    for (int half = 32; half >= 8; half >>= 1) {
+        const u64 lo = w & ((1ull << half) - 1ull);
+        const u32 c = (u32)__popcll(lo);
+        if (r >= c) {
+            r -= c;
+            w >>= half;
+            base += half;
+        } else {
+            w = lo;
+        }
+    }
+    for (u32 k = 0; k < 8; ++k) {
+        if ((w >> k) & 1ull) {
+            if (r == 0) return base + k;
+            --r;
+        }
+    }
+    return base;
+}
+
+// claim v for level L+1 through the visited bitmap (push levels)
+__device__ __forceinline__ bool claim(u64* vis, u32 v) {
+    u64* wp = vis + (v >> 6);
+    const u64 bit = 1ull << (v & 63);
+    if (*wp & bit) return false;
+    return !(atomicOr(wp, bit) & bit);
+}
+
+template <typename Off, bool SYM>
+__global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int32_t L) {
+    __shared__ LbShared<HUB_TILE> sh;
+    __shared__ BlockQ q;
+    __shared__ u32 s_excl[TB];
+    __shared__ u64 s_beg[TB];
+    __shared__ u32 s_wex[TB];
+    __shared__ u64 s_fw[TB];
+    __shared__ u64 red[NW];
+    Decision d;
+    const int dec = decide(a, L, d);
+    const bool go = dec == 2;
+    const u32 t = threadIdx.x;
+    if (blockIdx.x == 0) {
+        u64* zp = reinterpret_cast<u64*>(a.C + (L + 1) % 3);
+        for (u32 i = t; i < sizeof(LevelCnt) / 8; i += TB) zp[i] = 0;
+        if (t == 0) {
+            LevelState& s = a.S[L & 1];
+            s.mode = d.mode;
+            s.done = go ? 0 : 1;
+            s.vsel = (go && d.mode == 1) ? 1 - d.vsel : d.vsel;
+            s.level = L;
+            s.m_u = d.m_u;
+            s.prev_found = d.found;
+            if (go) a.nmode[d.mode] += 1;
+            if (dec == 1) {
+                a.host[1] = (int64_t)a.nmode[0];
+                a.host[2] = (int64_t)a.nmode[1];
+                __atomic_store_n(&a.host[0], (int64_t)L, __ATOMIC_RELEASE);
+            }
+        }
+    }
+    if (!go) return;
+    if (t == 0) q.n = q.nh = 0;
+    const int32_t nl = L + 1;
+    const int cp = L & 1;
+    Acc acc;
+    const int lane = lane_id();
+
+    if (d.mode == 0) {
+        u64* vis = a.vis[d.vsel];
+        // ---- hub queue: 1024-edge tiles over monotonic edge offsets
+        const u64 ntiles = (d.he + HUB_TILE - 1) / HUB_TILE;
+        for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+            const u64 e0 = tile * HUB_TILE;
+            const u64 e1 = min(e0 + (u64)HUB_TILE, d.he);
+            u64 s0;
+            u32 ns;
+            lb_tile_load<HUB_TILE>(a.hoff[cp], d.nh, e0, sh, s0, ns);
+            bool c[HUB_TILE / TB];
+            u32 vv[HUB_TILE / TB];
+#pragma unroll
+            for (int k = 0; k < HUB_TILE / TB; ++k) {
+                const u64 e = e0 + (u64)k * TB + t;
+                c[k] = false;
+                vv[k] = 0;
+                if (e < e1) {
+                    const u32 j = lb_find<HUB_TILE>(sh, ns, e);
+                    vv[k] = g.col[a.hbeg[cp][s0 + j] + (e - sh.off[j])];
                 }
             }
+#pragma unroll
+            for (int k = 0; k < HUB_TILE / TB; ++k) {
+                if (e0 + (u64)k * TB + t < e1) {
+                    c[k] = claim(vis, vv[k]);
+                    if (c[k]) a.dist[vv[k]] = nl;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < HUB_TILE / TB; ++k)
+                stage<Off, SYM>(q, a, g, L, c[k], vv[k],
+                                c[k] && !SYM ? (u64)(g.crow[vv[k] + 1] - g.crow[vv[k]]) : 0ull, acc);
+            flush(q, a, L);
         }
-        const u64 m = __ballot(found);
-        if (lane == 0) {
-            visited[wd] = vis | m;
-            fnext[wd] = m;
+        // Walk the edges of up to 256 frontier vertices (one per thread: deg, beg) in
+        // 256-edge steps; owner of an edge = binary search over the block's degree scan.
+        auto expand_group = [&](u32 deg, u64 beg) {
+            s_beg[t] = beg;
+            u32 tot;
+            s_excl[t] = block_excl_scan<NW>(deg, reinterpret_cast<u32*>(red), tot);
+            __syncthreads();
+            for (u32 base = 0; base < tot; base += TB) {
+                const u32 e = base + t;
+                bool c = false;
+                u32 v = 0;
+                if (e < tot) {
+                    u32 lo = 0;  // largest j with s_excl[j] <= e
+#pragma unroll
+                    for (u32 step = TB / 2; step > 0; step >>= 1)
+                        if (s_excl[lo + step] <= e) lo += step;
+                    v = g.col[s_beg[lo] + (e - s_excl[lo])];
+                    c = claim(vis, v);
+                    if (c) a.dist[v] = nl;
+                }
+                stage<Off, SYM>(q, a, g, L, c, v, c && !SYM ? (u64)(g.crow[v + 1] - g.crow[v]) : 0ull, acc);
+                __syncthreads();
+                // block-uniform: tot is uniform and q.n is read after the barrier
+                if (base + TB >= tot || q.n > (u32)(QCAP - TB)) flush(q, a, L);
+            }
+        };
+        if (d.prev_mode == 0) {
+            // ---- normal queue: a block takes 256 entries
+            u64 gcount = 0, gpre[NQS];
+#pragma unroll
+            for (int k = 0; k < NQS; ++k) {
+                gpre[k] = gcount;
+                gcount += (d.nseg[k] + TB - 1) / TB;
+            }
+            for (u64 grp = blockIdx.x; grp < gcount; grp += gridDim.x) {
+                int seg = 0;
+                u64 sbase = 0, scount = d.nseg[0];
+#pragma unroll
+                for (int k = 1; k < NQS; ++k)
+                    if (grp >= gpre[k]) {
+                        seg = k;
+                        sbase = gpre[k];
+                        scount = d.nseg[k];
+                    }
+                const u64 i = (grp - sbase) * TB + t;
+                u32 deg = 0;
+                u64 beg = 0;
+                if (i < scount) {
+                    const u32 u = a.qv[cp][(u64)seg * (u64)a.n + i];
+                    const Off b = g.row[u], e = g.row[u + 1];
+                    deg = (u32)(e - b);
+                    beg = (u64)b;
+                }
+                expand_group(deg, beg);
+            }
+        } else {
+            // ---- frontier found by the previous (pull) level, as a bitmap: a block takes
+            // 256 words, ranks their bits, and expands 256 frontier vertices at a time.
+            for (i64 wc = blockIdx.x; wc * TB < a.nwords; wc += gridDim.x) {
+                const i64 w = wc * TB + t;
+                const u64 fw = w < a.nwords ? a.fnew[w] : 0ull;
+                u32 F;
+                const u32 wex = block_excl_scan<NW>((u32)__popcll(fw), reinterpret_cast<u32*>(red), F);
+                s_wex[t] = wex;
+                s_fw[t] = fw;
+                __syncthreads();
+                for (u32 fb = 0; fb < F; fb += TB) {
+                    const u32 f = fb + t;
+                    u32 deg = 0;
+                    u64 beg = 0;
+                    if (f < F) {
+                        u32 lo = 0;  // word holding the f-th frontier vertex of this block
+#pragma unroll
+                        for (u32 step = TB / 2; step > 0; step >>= 1)
+                            if (s_wex[lo + step] <= f) lo += step;
+                        const u32 u = (u32)((wc * TB + lo) * 64 + select_bit(s_fw[lo], f - s_wex[lo]));
+                        const Off b = g.row[u], e = g.row[u + 1];
+                        deg = (u32)(e - b);
+                        beg = (u64)b;
+                    }
+                    expand_group(deg, beg);
+                }
+                __syncthreads();
+            }
         }
-        u32 deg = 0;
-        u64 beg = 0;
-        if (found) {
-            dist[v] = nl;
-            const Off rb = row[v], re = row[v + 1];
-            deg = (u32)(re - rb);
-            beg = (u64)rb;
-            my_m += deg;
-            my_found += 1;
-            my_in += (u64)(e - b);
-        }
-        const bool app = found && deg > 0;
-        const u64 slot = wave_append(app, &cnt->n_next);
-        if (app) {
-            qv_n[slot] = (u32)v;
-            qdeg_n[slot] = deg;
-            qbeg_n[slot] = beg;
+    } else {
+        // ---- pull level: waves screen SC visited words at once and work only on
+        // words with unvisited vertices, WPI of them at a time. Output is bitmaps
+        // only (vis_next, fnew); no queue, no block barrier in the loop.
+        const u64* vis = a.vis[d.vsel];
+        u64* vout = a.vis[1 - d.vsel];
+        const i64 nsc = (a.nwords + SC - 1) / SC;
+        for (i64 sc = (i64)blockIdx.x * NW + wave_id(); sc < nsc; sc += (i64)gridDim.x * NW) {
+            const i64 wbase = sc * SC;
+            const bool mine = lane < SC && wbase + lane < a.nwords;
+            u64 myvis = ~0ull, mytodo = 0;
+            if (mine) {
+                const i64 wd = wbase + lane;
+                myvis = vis[wd];
+                const u64 valid = (wd == a.nwords - 1 && (a.n & 63)) ? ((1ull << (a.n & 63)) - 1ull) : ~0ull;
+                mytodo = ~myvis & valid;
+            }
+            u64 tw = __ballot(mytodo != 0);
+            u64 mynew = 0;
+            while (tw) {
+                int jj[WPI];
+                u64 todo[WPI];
+                bool fnd[WPI];
+                Off b[WPI], e[WPI], k[WPI];
+                u32 v[WPI];
+#pragma unroll
+                for (int j = 0; j < WPI; ++j) {
+                    jj[j] = -1;
+                    todo[j] = 0;
+                    if (tw) {
+                        jj[j] = __ffsll((long long)tw) - 1;
+                        tw &= tw - 1;
+                        todo[j] = __shfl(mytodo, jj[j], 64);
+                    }
+                    v[j] = (u32)((wbase + (jj[j] < 0 ? 0 : jj[j])) * 64 + lane);
+                    fnd[j] = false;
+                    b[j] = e[j] = k[j] = 0;
+                }
+#pragma unroll
+                for (int j = 0; j < WPI; ++j)
+                    if ((todo[j] >> lane) & 1ull) {
+                        b[j] = g.crow[v[j]];
+                        e[j] = g.crow[v[j] + 1];
+                    }
+                // probes, stage A: the first 2 in-edges of every candidate (independent
+                // loads); most vertices of a dense pull level find a parent here
+                u32 u[WPI][PB1];
+#pragma unroll
+                for (int j = 0; j < WPI; ++j)
+#pragma unroll
+                    for (int p = 0; p < PB1; ++p) u[j][p] = (b[j] + p < e[j]) ? g.ccol[b[j] + p] : 0u;
+#pragma unroll
+                for (int j = 0; j < WPI; ++j) {
+#pragma unroll
+                    for (int p = 0; p < PB1; ++p)
+                        fnd[j] |= (b[j] + p < e[j]) && ((vis[u[j][p] >> 6] >> (u[j][p] & 63)) & 1ull);
+                    k[j] = b[j] + PB1;
+                }
+                // stage B: the next PB2 in-edges at once, only for lanes still open
+                if (__ballot(!fnd[0] && k[0] < e[0]) | __ballot(!fnd[1] && k[1] < e[1]) |
+                    __ballot(!fnd[2] && k[2] < e[2]) | __ballot(!fnd[3] && k[3] < e[3])) {
+                    u32 x[WPI][PB2];
+#pragma unroll
+                    for (int j = 0; j < WPI; ++j)
+#pragma unroll
+                        for (int p = 0; p < PB2; ++p)
+                            x[j][p] = (!fnd[j] && k[j] + p < e[j]) ? g.ccol[k[j] + p] : 0u;
+#pragma unroll
+                    for (int j = 0; j < WPI; ++j) {
+                        if (!fnd[j]) {
+#pragma unroll
+                            for (int p = 0; p < PB2; ++p)
+                                fnd[j] |= (k[j] + p < e[j]) && ((vis[x[j][p] >> 6] >> (x[j][p] & 63)) & 1ull);
+                            k[j] += PB2;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < WPI; ++j) {
+                    const Off lim = (e[j] - b[j] > (Off)BU_SERIAL) ? b[j] + (Off)BU_SERIAL : e[j];
+                    for (; k[j] < lim && !fnd[j]; ++k[j]) {
+                        const u32 y = g.ccol[k[j]];
+                        fnd[j] = (vis[y >> 6] >> (y & 63)) & 1ull;
+                    }
+                }
+                // wave-cooperative scan of the long rows that are still open
+#pragma unroll
+                for (int j = 0; j < WPI; ++j) {
+                    u64 open = __ballot(!fnd[j] && k[j] < e[j]);
+                    while (open) {
+                        const int l = __ffsll((long long)open) - 1;
+                        open &= open - 1;
+                        const Off kb = __shfl(k[j], l, 64), ke = __shfl(e[j], l, 64);
+                        bool hit = false;
+                        for (Off kk = kb; kk < ke; kk += 2 * WAVE) {
+                            const Off k0 = kk + lane, k1 = kk + WAVE + lane;
+                            const u32 u0 = k0 < ke ? g.ccol[k0] : 0u;
+                            const u32 u1 = k1 < ke ? g.ccol[k1] : 0u;
+                            const u64 x0 = vis[u0 >> 6], x1 = vis[u1 >> 6];
+                            const bool h = (k0 < ke && ((x0 >> (u0 & 63)) & 1ull)) ||
+                                           (k1 < ke && ((x1 >> (u1 & 63)) & 1ull));
+                            if (__ballot(h)) {
+                                hit = true;
+                                break;
+                            }
+                        }
+                        if (lane == l) fnd[j] = hit;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < WPI; ++j) {
+                    const u64 m = __ballot(fnd[j]);
+                    if (lane == jj[j]) mynew = m;
+                    if (fnd[j]) {
+                        a.dist[v[j]] = nl;
+                        Off rb = b[j], re = e[j];
+                        if (!SYM) {
+                            rb = g.row[v[j]];
+                            re = g.row[v[j] + 1];
+                        }
+                        const u32 deg = (u32)(re - rb);
+                        acc.m += deg;
+                        acc.f += 1;
+                        acc.fz += deg > 0;
+                        acc.in += (u64)(e[j] - b[j]);
+                    }
+                }
+            }
+            if (mine) {
+                vout[wbase + lane] = myvis | mynew;
+                a.fnew[wbase + lane] = mynew;
+            }
         }
     }
-    block_add3<u64>(my_m, my_found, my_in, red, &cnt->m_next, &cnt->found, &cnt->in_next);
+    flush(q, a, L);
+    flush_acc(a, L, acc, red);
 }
 
-__global__ void q_to_bits_k(const u32* __restrict__ qv, u64 nq, u64* __restrict__ bits) {
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += (u64)gridDim.x * blockDim.x) {
-        const u32 v = qv[i];
-        atomicOr(bits + (v >> 6), 1ull << (v & 63));
+// dist := INF, vis := isolated-vertex mask, then the source; level -1's counters
+// C[2] / state S[1] describe the one-vertex frontier.
+template <typename Off>
+__global__ __launch_bounds__(TB) void bfs_init_k(BfsArgs a, Graph_d<Off> g, const u64* __restrict__ zmask, i64 s,
+                                                 double nnz) {
+    const i64 n4 = a.n / 4;
+    const i64 tid = (i64)blockIdx.x * TB + threadIdx.x, nth = (i64)gridDim.x * TB;
+    int4* d4 = reinterpret_cast<int4*>(a.dist);
+    for (i64 i = tid; i < n4; i += nth) {
+        int4 x = make_int4(INT_INF, INT_INF, INT_INF, INT_INF);
+        if (i == (s >> 2)) {
+            const int r = (int)(s & 3);
+            if (r == 0) x.x = 0;
+            else if (r == 1) x.y = 0;
+            else if (r == 2) x.z = 0;
+            else x.w = 0;
+        }
+        d4[i] = x;
+    }
+    for (i64 i = n4 * 4 + tid; i < a.n; i += nth) a.dist[i] = (i == s) ? 0 : INT_INF;
+    for (i64 w = tid; w < a.nwords; w += nth) a.vis[0][w] = zmask[w] | (w == (s >> 6) ? 1ull << (s & 63) : 0ull);
+    if (blockIdx.x == 0) {
+        u64* z0 = reinterpret_cast<u64*>(a.C);
+        for (u32 i = threadIdx.x; i < 3 * sizeof(LevelCnt) / 8; i += TB) z0[i] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const Off b = g.row[s], e = g.row[s + 1];
+        const u32 deg = (u32)(e - b);
+        LevelCnt& c = a.C[2];
+        if (deg > 0 && deg <= HUBT) {
+            a.qv[0][0] = (u32)s;  // segment 0
+            c.n_norm[0].v = 1;
+        } else if (deg > HUBT) {
+            a.hv[0][0] = (u32)s;
+            a.hbeg[0][0] = (u64)b;
+            a.hoff[0][0] = 0;
+            c.hub_packed.v = (1ull << a.eb) | (u64)deg;
+        }
+        c.m_next[0] = deg;
+        c.found[0] = 1;
+        c.fnz[0] = deg > 0;
+        c.in_next[0] = (u64)(g.crow[s + 1] - g.crow[s]);
+        LevelState& st = a.S[1];
+        st = LevelState{};
+        st.m_u = nnz;
+        a.nmode[0] = a.nmode[1] = 0;
+        a.host[0] = -1;
+    }
+}
+
+// Isolated vertices (no in- and no out-edges). They can never be reached, and,
+// having no out-edges, never serve as the "visited in-neighbour" of a pull test,
+// so they may start out marked visited. (A vertex with in-degree 0 but
+// out-edges may not: it would pose as a parent without ever being reached.)
+template <typename Off>
+__global__ void zmask_k(const Off* __restrict__ row, const Off* __restrict__ crow, i64 n, i64 nwords,
+                        u64* __restrict__ z) {
+    for (i64 w = (i64)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (i64)gridDim.x * blockDim.x) {
+        u64 m = 0;
+        for (int j = 0; j < 64; ++j) {
+            const i64 v = w * 64 + j;
+            if (v < n && crow[v + 1] == crow[v] && row[v + 1] == row[v]) m |= 1ull << j;
+        }
+        z[w] = m;
     }
 }
 
 template <typename Off>
 __global__ void reach_k(const int32_t* __restrict__ dist, i64 n, const Off* __restrict__ row,
                         u64* __restrict__ out) {
-    __shared__ u64 red[TB / WAVE];
+    __shared__ u64 red[NW];
     u64 c = 0, m = 0;
     for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
         if (dist[i] < INT_INF) {
@@ -205,97 +692,99 @@ __global__ void reach_k(const int32_t* __restrict__ dist, i64 n, const Off* __re
             m += (u64)(row[i + 1] - row[i]);
         }
     }
-    c = block_sum<TB / WAVE>(c, red);
-    m = block_sum<TB / WAVE>(m, red);
+    c = block_sum<NW>(c, red);
+    m = block_sum<NW>(m, red);
     if (threadIdx.x == 0) {
         if (c) atomicAdd(out, c);
         if (m) atomicAdd(out + 1, m);
     }
 }
 
+int edge_bits(i64 nnz) {
+    int b = 1;
+    while (b < 63 && ((u64)1 << b) <= (u64)nnz) ++b;
+    return b;
+}
+
+}  // namespace
+
+struct BfsWorkHolder {
+    DevBuf<u32> qv[2];  // NQS segments of n entries
+    DevBuf<u32> hv[2];
+    DevBuf<u64> hbeg[2], hoff[2];
+    DevBuf<u64> vis2;   // second visited buffer
+    DevBuf<u64> zmask;  // isolated vertices
+    DevBuf<u64> fnew;   // frontier bitmap written by pull levels
+    DevBuf<uint8_t> ctl;  // C[3] + S[2] + nmode[2]
+    int64_t* host = nullptr;  // mapped pinned host words (see BfsArgs::host)
+    int32_t last_depth = 0;   // levels of the previous solve: sizes the first batch
+    ~BfsWorkHolder() {
+        if (host) (void)hipHostFree(host);
+    }
+};
+
+void delete_bfs_work(BfsWorkHolder* p) { delete p; }
+
+namespace {
+
 template <typename Off>
-void bfs_run(Graph& g, i64 source) {
+void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     Ctx& ctx = *g.ctx;
     hipStream_t s = ctx.stream;
     const i64 n = g.n;
     const i64 nwords = (n + 63) / 64;
-    const Off* row = static_cast<const Off*>(g.row_ptr());
-    const Off* crow = static_cast<const Off*>(g.crow_ptr());
-    const u32* ccol = g.ccol_ptr();
-    const bool sym = g.symmetric;
-    BfsCnt* dcnt = reinterpret_cast<BfsCnt*>(g.counters.p);
-    BfsCnt* hcnt = reinterpret_cast<BfsCnt*>(g.hcounters.p);
-    const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
 
+    BfsArgs a{};
+    a.n = n;
+    a.nwords = nwords;
+    a.eb = edge_bits(g.nnz);
+    a.alpha = g.alpha;
+    a.beta = g.beta;
+    a.force = g.force_mode;
+    a.dist = g.dist.p;
+    a.vis[0] = g.visited.p;
+    a.vis[1] = w.vis2.p;
+    a.fnew = w.fnew.p;
+    for (int i = 0; i < 2; ++i) {
+        a.qv[i] = w.qv[i].p;
+        a.hv[i] = w.hv[i].p;
+        a.hbeg[i] = w.hbeg[i].p;
+        a.hoff[i] = w.hoff[i].p;
+    }
+    a.C = reinterpret_cast<LevelCnt*>(w.ctl.p);
+    a.S = reinterpret_cast<LevelState*>(w.ctl.p + 3 * sizeof(LevelCnt));
+    a.nmode = reinterpret_cast<u64*>(w.ctl.p + 3 * sizeof(LevelCnt) + 2 * sizeof(LevelState));
+    PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.host), w.host, 0));
+    Graph_d<Off> gd{static_cast<const Off*>(g.row_ptr()), g.col.p, static_cast<const Off*>(g.crow_ptr()),
+                    g.ccol_ptr()};
+
+    const unsigned grid = (unsigned)ctx.cu_count * (unsigned)(g.grid_per_cu > 0 ? g.grid_per_cu : 4);
     auto t_host0 = std::chrono::steady_clock::now();
     PJ_HIP(hipEventRecord(g.ev0, s));
-    if (n > 0) {
-        PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.dist.p), INT_INF, (size_t)n, s));
-        PJ_HIP(hipMemsetAsync(g.visited.p, 0, sizeof(u64) * (size_t)nwords, s));
-    }
     pj_stats st{};
-    if (source >= 0 && source < n) {
-        PJ_HIP(hipMemsetAsync(dcnt, 0, sizeof(BfsCnt), s));
-        bfs_source_k<Off><<<1, 1, 0, s>>>(source, row, crow, g.dist.p, g.visited.p, g.qv[0].p, g.qdeg[0].p,
-                                          g.qbeg[0].p, dcnt);
+    const bool valid = source >= 0 && source < n;
+    if (!valid) {
+        if (n > 0) PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.dist.p), INT_INF, (size_t)n, s));
+    } else {
+        bfs_init_k<Off><<<grid_for(std::max(n / 4, nwords), TB, (unsigned)ctx.cu_count * 4u), TB, 0, s>>>(
+            a, gd, w.zmask.p, source, (double)g.nnz);
         PJ_LAUNCH_CHECK();
-        PJ_HIP(hipMemcpyAsync(hcnt, dcnt, sizeof(BfsCnt), hipMemcpyDeviceToHost, s));
-        PJ_HIP(hipStreamSynchronize(s));
-        u64 nq = hcnt->n_next, mq = hcnt->m_next, nfound = hcnt->found;
-        double m_u = (double)g.nnz - (double)hcnt->in_next;
-        int cur = 0;
-        bool bottom_up = false;
-        u64 prev_found = 0;
-        int32_t level = 0;
-        while (nq > 0 && level + 1 < INT_INF) {
-            const int32_t nl = level + 1;
-            const int nx = 1 - cur;
-            if (!bottom_up) {
-                const bool go = g.force_mode == 2 ? true
-                                : g.force_mode == 1 ? false
-                                                    : (double)mq > m_u / g.alpha;
-                if (go) {
-                    PJ_HIP(hipMemsetAsync(g.fcur.p, 0, sizeof(u64) * (size_t)nwords, s));
-                    q_to_bits_k<<<grid_for((i64)nq, 256, maxgrid), 256, 0, s>>>(g.qv[cur].p, nq, g.fcur.p);
-                    PJ_LAUNCH_CHECK();
-                    bottom_up = true;
-                }
-            } else if (g.force_mode != 2 && (double)nfound < (double)n / g.beta && nfound < prev_found) {
-                bottom_up = false;
-            }
-            PJ_HIP(hipMemsetAsync(dcnt, 0, sizeof(BfsCnt), s));
-            if (!bottom_up) {
-                exclusive_scan_u32(g.qdeg[cur].p, g.qoff.p, (i64)nq, g.scan, s);
-                const unsigned grid = grid_for((i64)((mq + TD_TILE - 1) / TD_TILE), 1, maxgrid);
-                if (sym)
-                    td_expand_k<Off, true><<<grid, TB, 0, s>>>(g.qbeg[cur].p, g.qoff.p, nq, mq, g.col.p, row, crow,
-                                                               g.visited.p, g.dist.p, nl, g.qv[nx].p,
-                                                               g.qdeg[nx].p, g.qbeg[nx].p, dcnt);
-                else
-                    td_expand_k<Off, false><<<grid, TB, 0, s>>>(g.qbeg[cur].p, g.qoff.p, nq, mq, g.col.p, row,
-                                                                crow, g.visited.p, g.dist.p, nl, g.qv[nx].p,
-                                                                g.qdeg[nx].p, g.qbeg[nx].p, dcnt);
+        int32_t L = 0;
+        // first batch: the previous solve's depth + 1 (+1 for the level that detects the
+        // end), so a repeated solve on the same graph usually needs one host check
+        int batch = g.level_batch > 0 ? g.level_batch : std::max(4, w.last_depth + 2);
+        for (;;) {
+            for (int i = 0; i < batch && L < INT_INF; ++i, ++L) {
+                if (g.symmetric) bfs_level_k<Off, true><<<grid, TB, 0, s>>>(a, gd, L);
+                else bfs_level_k<Off, false><<<grid, TB, 0, s>>>(a, gd, L);
                 PJ_LAUNCH_CHECK();
-                st.td_levels++;
-            } else {
-                const unsigned grid = grid_for((nwords + 3) / 4, 1, (unsigned)ctx.cu_count * 16u);
-                bu_step_k<Off><<<grid, TB, 0, s>>>(n, nwords, g.visited.p, g.fcur.p, g.fnext.p, crow, ccol, row,
-                                                   g.dist.p, nl, g.qv[nx].p, g.qdeg[nx].p, g.qbeg[nx].p, dcnt);
-                PJ_LAUNCH_CHECK();
-                std::swap(g.fcur, g.fnext);
-                st.bu_levels++;
             }
-            PJ_HIP(hipMemcpyAsync(hcnt, dcnt, sizeof(BfsCnt), hipMemcpyDeviceToHost, s));
             PJ_HIP(hipStreamSynchronize(s));
-            prev_found = nfound;
-            nq = hcnt->n_next;
-            mq = hcnt->m_next;
-            nfound = hcnt->found;
-            m_u -= (double)hcnt->in_next;
-            cur = nx;
-            level = nl;
+            if (*(volatile int64_t*)w.host >= 0 || L >= INT_INF) break;
+            batch = batch < 1024 ? batch * 2 : batch;
         }
-        st.levels = level;
+        st.levels = *(volatile int64_t*)w.host;
+        w.last_depth = (int32_t)st.levels;
     }
     PJ_HIP(hipEventRecord(g.ev1, s));
     PJ_HIP(hipEventSynchronize(g.ev1));
@@ -303,6 +792,10 @@ void bfs_run(Graph& g, i64 source) {
     PJ_HIP(hipEventElapsedTime(&ms, g.ev0, g.ev1));
     st.kernel_ms = ms;
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+    if (valid) {
+        st.td_levels = ((volatile int64_t*)w.host)[1];
+        st.bu_levels = ((volatile int64_t*)w.host)[2];
+    }
     g.stats = st;
     g.have_result = true;
 }
@@ -312,17 +805,33 @@ void bfs_workspace(Graph& g) {
     const size_t nwords = (n + 63) / 64;
     g.dist.ensure(n ? n : 1);
     g.visited.ensure(nwords ? nwords : 1);
-    g.fcur.ensure(nwords ? nwords : 1);
-    g.fnext.ensure(nwords ? nwords : 1);
+    if (g.bfs_work) return;
+    g.bfs_work.reset(new BfsWorkHolder());
+    BfsWorkHolder& w = *g.bfs_work;
     for (int i = 0; i < 2; ++i) {
-        g.qv[i].ensure(n ? n : 1);
-        g.qdeg[i].ensure(n ? n : 1);
-        g.qbeg[i].ensure(n ? n : 1);
+        w.qv[i].alloc(n ? (size_t)NQS * n : 1);
+        w.hv[i].alloc(n ? n : 1);
+        w.hbeg[i].alloc(n ? n : 1);
+        w.hoff[i].alloc(n ? n : 1);
     }
-    g.qoff.ensure(n + 1);
-    g.scan.ensure((i64)n);
-    g.counters.ensure(16);
-    if (!g.hcounters.p) g.hcounters.alloc(16);
+    w.vis2.alloc(nwords ? nwords : 1);
+    w.zmask.alloc(nwords ? nwords : 1);
+    w.fnew.alloc(nwords ? nwords : 1);
+    w.ctl.alloc(3 * sizeof(LevelCnt) + 2 * sizeof(LevelState) + 2 * sizeof(u64));
+    PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.host), 4 * sizeof(int64_t), hipHostMallocMapped));
+    if (nwords) {
+        hipStream_t s = g.ctx->stream;
+        if (g.off64)
+            zmask_k<u64><<<grid_for((i64)nwords, 256), 256, 0, s>>>(static_cast<const u64*>(g.row_ptr()),
+                                                                    static_cast<const u64*>(g.crow_ptr()), g.n,
+                                                                    (i64)nwords, w.zmask.p);
+        else
+            zmask_k<u32><<<grid_for((i64)nwords, 256), 256, 0, s>>>(static_cast<const u32*>(g.row_ptr()),
+                                                                    static_cast<const u32*>(g.crow_ptr()), g.n,
+                                                                    (i64)nwords, w.zmask.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipStreamSynchronize(s));
+    }
     if (!g.ev0) PJ_HIP(hipEventCreate(&g.ev0));
     if (!g.ev1) PJ_HIP(hipEventCreate(&g.ev1));
 }
@@ -331,8 +840,8 @@ void bfs_workspace(Graph& g) {
 
 void bfs_solve(Graph& g, i64 source) {
     bfs_workspace(g);
-    if (g.off64) bfs_run<u64>(g, source);
-    else bfs_run<u32>(g, source);
+    if (g.off64) bfs_run<u64>(g, *g.bfs_work, source);
+    else bfs_run<u32>(g, *g.bfs_work, source);
 }
 
 void reach_stats(Graph& g, i64* n_r, i64* m_r) {

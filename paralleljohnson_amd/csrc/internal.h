@@ -124,6 +124,12 @@ struct Ctx {
     int cu_count = 256;
 };
 
+struct BfsWorkHolder;
+void delete_bfs_work(BfsWorkHolder* p);
+struct BfsWorkDeleter {
+    void operator()(BfsWorkHolder* p) const { delete_bfs_work(p); }
+};
+
 struct Graph {
     Ctx* ctx = nullptr;
     i64 n = 0, nnz = 0;
@@ -137,7 +143,7 @@ struct Graph {
 
     // per-solve workspace (lazily sized)
     DevBuf<int32_t> dist;
-    DevBuf<u64> visited, fcur, fnext;
+    DevBuf<u64> visited;
     DevBuf<u32> qv[2], qdeg[2];
     DevBuf<u64> qbeg[2];
     DevBuf<u64> qoff;
@@ -145,10 +151,13 @@ struct Graph {
     PinnedBuf<u64> hcounters;
     ScanWs scan;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::unique_ptr<BfsWorkHolder, BfsWorkDeleter> bfs_work;
 
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;
-    int force_mode = 0;  // 0 auto, 1 top-down only, 2 bottom-up after level 0
+    int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
+    int level_batch = 0; // BFS levels enqueued per host check (0 = default 8, doubling)
+    int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = default 4)
 
     bool have_result = false;
     pj_stats stats{};

@@ -17,7 +17,7 @@ struct LbShared {
     u64 s0;
 };
 
-// Collective (whole block). After return: s_off[0..ns] = qoff[s0..s0+ns].
+// Collective (whole block). After return: sh.off[0..ns) = qoff[s0..s0+ns).
 template <int TILE>
 __device__ __forceinline__ void lb_tile_load(const u64* __restrict__ qoff, u64 nq, u64 e0, LbShared<TILE>& sh,
                                              u64& s0, u32& ns) {
@@ -33,7 +33,7 @@ __device__ __forceinline__ void lb_tile_load(const u64* __restrict__ qoff, u64 n
     __syncthreads();
     s0 = sh.s0;
     ns = (u32)min(nq - s0, (u64)TILE);  // every slot holds >= 1 edge
-    for (u32 i = threadIdx.x; i <= ns; i += blockDim.x) sh.off[i] = qoff[s0 + i];
+    for (u32 i = threadIdx.x; i < ns; i += blockDim.x) sh.off[i] = qoff[s0 + i];
     __syncthreads();
 }
 
