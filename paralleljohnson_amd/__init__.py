@@ -21,7 +21,7 @@ import numpy as np
 INT_INF = 100000  # ParallelJohnson.cpp:29
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libpj.so")
+LIB_PATH = os.environ.get("PJ_LIB_OVERRIDE") or os.path.join(_HERE, "lib", "libpj.so")
 CLI_PATH = os.path.join(_HERE, "bin", "parallel_johnson")
 
 if not os.path.exists(LIB_PATH):

@@ -368,6 +368,7 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "direction" && (value == 0 || value == 1 || value == 2)) g.force_mode = (int)value;
     else if (k == "level_batch" && value >= 0 && value <= 4096) g.level_batch = (int)value;
     else if (k == "grid_per_cu" && value >= 0 && value <= 16) g.grid_per_cu = (int)value;
+    else if (k == "max_levels" && value >= 0) g.max_levels = (int)value;
     else return arg_error("pj_set_option: unknown key or bad value");
     return PJ_OK;
 }
@@ -454,6 +455,16 @@ int pj_write_sol(const int32_t* dist, int64_t n, const char* path, int strict) {
             set_error(std::string("write failed: ") + path);
             return (int)PJ_ERR_IO;
         }
+        return (int)PJ_OK;
+    });
+}
+
+// debug only (not declared in include/pj.h)
+int pj_debug_bitmaps(pj_graph* pg, uint64_t* vis0, uint64_t* vis1, uint64_t* fnew) {
+    if (!pg) return arg_error("pj_debug_bitmaps: graph is NULL");
+    return guarded([&] {
+        bind(*pg->g.ctx);
+        debug_bitmaps(pg->g, (u64*)vis0, (u64*)vis1, (u64*)fnew);
         return (int)PJ_OK;
     });
 }

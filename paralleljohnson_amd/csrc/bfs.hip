@@ -41,6 +41,12 @@ namespace pj {
 
 namespace {
 
+#ifndef PJ_RPI
+#define PJ_RPI 4
+#endif
+#ifndef PJ_PB2
+#define PJ_PB2 8
+#endif
 constexpr int TB = 256;
 constexpr int NW = TB / WAVE;
 constexpr u32 HUBT = 256;     // out-degree above which a frontier vertex goes to the hub queue
@@ -50,10 +56,11 @@ constexpr int QCAP = TB * WPI;  // staging: most normal entries one block step c
 constexpr int HCAP = 256;     // staging for hubs (overflow goes straight to global)
 constexpr int BU_SERIAL = 16; // edges a lane probes alone before the wave helps
 constexpr int PB1 = 2;        // pull probes, stage A (every candidate)
-constexpr int PB2 = 8;        // pull probes, stage B (candidates still open)
+constexpr int PB2 = PJ_PB2;   // pull probes, stage B (candidates still open)
 constexpr int NSH = 16;       // shards of the summed counters
 constexpr int NQS = 8;        // normal-queue segments
 constexpr int SC = 16;        // pull levels: visited words a wave screens at once
+constexpr int RPI = PJ_RPI;   // pull levels: rounds of 64 candidates in flight per wave
 
 struct alignas(64) Line {
     u64 v;
@@ -84,6 +91,7 @@ struct BfsArgs {
     int eb;  // edge bits of the packed hub counter
     double alpha, beta;
     int force;  // 0 auto, 1 push only, 2 pull whenever possible
+    int32_t max_levels;  // debug: stop after this many levels
     int32_t* dist;
     u64* vis[2];
     u64* fnew;   // pull levels: bitmap of the vertices they found (next frontier)
@@ -144,7 +152,7 @@ __device__ __forceinline__ int decide(const BfsArgs& a, int32_t L, Decision& d) 
     (void)nn;
     d.found = fd;
     d.m_u = ps.m_u - (double)in;
-    if (fz == 0 || L + 1 >= INT_INF) return 1;
+    if (fz == 0 || L + 1 >= INT_INF || L >= a.max_levels) return 1;
     if (a.force == 1) d.mode = 0;
     else if (a.force == 2) d.mode = 1;
     else if (d.mode == 0) {
@@ -324,6 +332,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
     __shared__ u64 s_beg[TB];
     __shared__ u32 s_wex[TB];
     __shared__ u64 s_fw[TB];
+    __shared__ u32 s_new[NW][2 * SC];
     __shared__ u64 red[NW];
     Decision d;
     const int dec = decide(a, L, d);
@@ -476,11 +485,12 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
             }
         }
     } else {
-        // ---- pull level: waves screen SC visited words at once and work only on
-        // words with unvisited vertices, WPI of them at a time. Output is bitmaps
-        // only (vis_next, fnew); no queue, no block barrier in the loop.
+        // ---- pull level: a wave screens SC visited words, compacts their unvisited
+        // (non-isolated) vertices into lanes, and works through them RPI rounds of 64
+        // at a time. Output is bitmaps only (vis_next, fnew): no queue, no block barrier.
         const u64* vis = a.vis[d.vsel];
         u64* vout = a.vis[1 - d.vsel];
+        u32* newb = s_new[wave_id()];  // found bits of the SC words, as 32-bit halves
         const i64 nsc = (a.nwords + SC - 1) / SC;
         for (i64 sc = (i64)blockIdx.x * NW + wave_id(); sc < nsc; sc += (i64)gridDim.x * NW) {
             const i64 wbase = sc * SC;
@@ -492,58 +502,64 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                 const u64 valid = (wd == a.nwords - 1 && (a.n & 63)) ? ((1ull << (a.n & 63)) - 1ull) : ~0ull;
                 mytodo = ~myvis & valid;
             }
-            u64 tw = __ballot(mytodo != 0);
-            u64 mynew = 0;
-            while (tw) {
-                int jj[WPI];
-                u64 todo[WPI];
-                bool fnd[WPI];
-                Off b[WPI], e[WPI], k[WPI];
-                u32 v[WPI];
+            if (lane < 2 * SC) newb[lane] = 0;
+            const u32 cnt = (u32)__popcll(mytodo);
+            const u32 incl = wave_incl_scan(cnt);
+            const u32 myex = incl - cnt;
+            const u32 T = __shfl(incl, 63, 64);
+            for (u32 r0 = 0; r0 < T; r0 += RPI * WAVE) {
+                bool fnd[RPI], act[RPI];
+                Off b[RPI], e[RPI], k[RPI];
+                u32 v[RPI];
 #pragma unroll
-                for (int j = 0; j < WPI; ++j) {
-                    jj[j] = -1;
-                    todo[j] = 0;
-                    if (tw) {
-                        jj[j] = __ffsll((long long)tw) - 1;
-                        tw &= tw - 1;
-                        todo[j] = __shfl(mytodo, jj[j], 64);
+                for (int j = 0; j < RPI; ++j) {
+                    const u32 c = r0 + (u32)j * WAVE + lane;
+                    act[j] = c < T;
+                    // word of candidate c: largest lane jw < SC with ex[jw] <= c
+                    u32 jw = 0;
+#pragma unroll
+                    for (u32 step = SC / 2; step > 0; step >>= 1) {
+                        const u32 x = __shfl(myex, jw + step, 64);
+                        if (x <= c) jw += step;
                     }
-                    v[j] = (u32)((wbase + (jj[j] < 0 ? 0 : jj[j])) * 64 + lane);
+                    const u32 ex = __shfl(myex, jw, 64);
+                    const u64 tw = __shfl(mytodo, jw, 64);
+                    v[j] = act[j] ? (u32)((wbase + jw) * 64 + select_bit(tw, c - ex)) : 0u;
                     fnd[j] = false;
                     b[j] = e[j] = k[j] = 0;
                 }
 #pragma unroll
-                for (int j = 0; j < WPI; ++j)
-                    if ((todo[j] >> lane) & 1ull) {
+                for (int j = 0; j < RPI; ++j)
+                    if (act[j]) {
                         b[j] = g.crow[v[j]];
                         e[j] = g.crow[v[j] + 1];
                     }
-                // probes, stage A: the first 2 in-edges of every candidate (independent
+                // probes, stage A: the first PB1 in-edges of every candidate (independent
                 // loads); most vertices of a dense pull level find a parent here
-                u32 u[WPI][PB1];
+                u32 u[RPI][PB1];
 #pragma unroll
-                for (int j = 0; j < WPI; ++j)
+                for (int j = 0; j < RPI; ++j)
 #pragma unroll
                     for (int p = 0; p < PB1; ++p) u[j][p] = (b[j] + p < e[j]) ? g.ccol[b[j] + p] : 0u;
+                bool open_any = false;
 #pragma unroll
-                for (int j = 0; j < WPI; ++j) {
+                for (int j = 0; j < RPI; ++j) {
 #pragma unroll
                     for (int p = 0; p < PB1; ++p)
                         fnd[j] |= (b[j] + p < e[j]) && ((vis[u[j][p] >> 6] >> (u[j][p] & 63)) & 1ull);
                     k[j] = b[j] + PB1;
+                    open_any |= !fnd[j] && k[j] < e[j];
                 }
-                // stage B: the next PB2 in-edges at once, only for lanes still open
-                if (__ballot(!fnd[0] && k[0] < e[0]) | __ballot(!fnd[1] && k[1] < e[1]) |
-                    __ballot(!fnd[2] && k[2] < e[2]) | __ballot(!fnd[3] && k[3] < e[3])) {
-                    u32 x[WPI][PB2];
+                // stage B: the next PB2 in-edges at once, only for candidates still open
+                if (PB2 > 0 && __ballot(open_any)) {
+                    u32 x[RPI][PB2 > 0 ? PB2 : 1];
 #pragma unroll
-                    for (int j = 0; j < WPI; ++j)
+                    for (int j = 0; j < RPI; ++j)
 #pragma unroll
                         for (int p = 0; p < PB2; ++p)
                             x[j][p] = (!fnd[j] && k[j] + p < e[j]) ? g.ccol[k[j] + p] : 0u;
 #pragma unroll
-                    for (int j = 0; j < WPI; ++j) {
+                    for (int j = 0; j < RPI; ++j) {
                         if (!fnd[j]) {
 #pragma unroll
                             for (int p = 0; p < PB2; ++p)
@@ -552,17 +568,35 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                         }
                     }
                 }
+                // serial probes up to BU_SERIAL edges: a wave-uniform loop with predicated
+                // bodies (all RPI rounds advance together; no divergent loop exits)
+                Off lim[RPI];
+                bool go[RPI];
 #pragma unroll
-                for (int j = 0; j < WPI; ++j) {
-                    const Off lim = (e[j] - b[j] > (Off)BU_SERIAL) ? b[j] + (Off)BU_SERIAL : e[j];
-                    for (; k[j] < lim && !fnd[j]; ++k[j]) {
-                        const u32 y = g.ccol[k[j]];
-                        fnd[j] = (vis[y >> 6] >> (y & 63)) & 1ull;
+                for (int j = 0; j < RPI; ++j) {
+                    lim[j] = (e[j] - b[j] > (Off)BU_SERIAL) ? b[j] + (Off)BU_SERIAL : e[j];
+                    go[j] = !fnd[j] && k[j] < lim[j];
+                }
+                for (;;) {
+                    bool any = false;
+#pragma unroll
+                    for (int j = 0; j < RPI; ++j) any |= go[j];
+                    if (!__ballot(any)) break;
+                    u32 y[RPI];
+#pragma unroll
+                    for (int j = 0; j < RPI; ++j) y[j] = go[j] ? g.ccol[k[j]] : 0u;
+#pragma unroll
+                    for (int j = 0; j < RPI; ++j) {
+                        if (go[j]) {
+                            fnd[j] = (vis[y[j] >> 6] >> (y[j] & 63)) & 1ull;
+                            ++k[j];
+                            go[j] = !fnd[j] && k[j] < lim[j];
+                        }
                     }
                 }
                 // wave-cooperative scan of the long rows that are still open
 #pragma unroll
-                for (int j = 0; j < WPI; ++j) {
+                for (int j = 0; j < RPI; ++j) {
                     u64 open = __ballot(!fnd[j] && k[j] < e[j]);
                     while (open) {
                         const int l = __ffsll((long long)open) - 1;
@@ -585,11 +619,10 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < WPI; ++j) {
-                    const u64 m = __ballot(fnd[j]);
-                    if (lane == jj[j]) mynew = m;
+                for (int j = 0; j < RPI; ++j) {
                     if (fnd[j]) {
                         a.dist[v[j]] = nl;
+                        atomicOr(&newb[2 * ((v[j] >> 6) - wbase) + ((v[j] >> 5) & 1)], 1u << (v[j] & 31));
                         Off rb = b[j], re = e[j];
                         if (!SYM) {
                             rb = g.row[v[j]];
@@ -604,6 +637,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                 }
             }
             if (mine) {
+                const u64 mynew = (u64)newb[2 * lane] | ((u64)newb[2 * lane + 1] << 32);
                 vout[wbase + lane] = myvis | mynew;
                 a.fnew[wbase + lane] = mynew;
             }
@@ -741,6 +775,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     a.alpha = g.alpha;
     a.beta = g.beta;
     a.force = g.force_mode;
+    a.max_levels = g.max_levels > 0 ? g.max_levels : INT_INF;
     a.dist = g.dist.p;
     a.vis[0] = g.visited.p;
     a.vis[1] = w.vis2.p;
@@ -861,4 +896,15 @@ void reach_stats(Graph& g, i64* n_r, i64* m_r) {
     *m_r = (i64)h[1];
 }
 
+}  // namespace pj
+
+namespace pj {
+// debug: copy both visited buffers and fnew to the host
+void debug_bitmaps(Graph& g, u64* vis0, u64* vis1, u64* fnew) {
+    const size_t nw = (size_t)((g.n + 63) / 64);
+    if (!g.bfs_work || !nw) return;
+    PJ_HIP(hipMemcpy(vis0, g.visited.p, 8 * nw, hipMemcpyDeviceToHost));
+    PJ_HIP(hipMemcpy(vis1, g.bfs_work->vis2.p, 8 * nw, hipMemcpyDeviceToHost));
+    PJ_HIP(hipMemcpy(fnew, g.bfs_work->fnew.p, 8 * nw, hipMemcpyDeviceToHost));
+}
 }  // namespace pj

@@ -158,6 +158,7 @@ struct Graph {
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
     int level_batch = 0; // BFS levels enqueued per host check (0 = default 8, doubling)
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = default 4)
+    int max_levels = 0;  // debug: truncate the BFS after this many levels (0 = off)
 
     bool have_result = false;
     pj_stats stats{};
@@ -193,5 +194,6 @@ void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t see
 void bfs_solve(Graph& g, i64 source);
 void delta_solve(Graph& g, i64 source);
 void reach_stats(Graph& g, i64* n_r, i64* m_r);
+void debug_bitmaps(Graph& g, u64* vis0, u64* vis1, u64* fnew);
 
 }  // namespace pj
