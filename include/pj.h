@@ -101,6 +101,13 @@ int pj_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, const uint3
 int pj_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int weighted,
                           pj_graph** out);
 
+/* web-Google-shaped synthetic graph (the SNAP file is not
+ * available): n_ids ids (about 95.6% used, the largest always used, so
+ * N = n_ids), n_edges directed edges with power-law out- and in-degrees and
+ * 30% "same-site" links. Deterministic in (n_ids, n_edges, seed). Benchmark
+ * input, no reference counterpart. */
+int pj_generate_webgraph(pj_ctx* ctx, int64_t n_ids, int64_t n_edges, uint64_t seed, pj_graph** out);
+
 int pj_graph_destroy(pj_graph* g);
 /* n = number of vertices, nnz = number of CSR entries, weighted = 0/1,
  * symmetric = 1 when the graph is known to equal its transpose. */
@@ -127,7 +134,9 @@ int pj_copy_dist(pj_graph* g, int32_t* dist_out);
 /* Device pointer to the last result (int32[n]); valid until the next solve. */
 const int32_t* pj_dist_device(pj_graph* g);
 /* Batched multi-source (Johnson-style all-pairs rows): dist_out is n_src x n
- * int32, row i = pj_sssp(g, sources[i]). */
+ * int32, row i = pj_sssp(g, sources[i]); NULL discards the rows (timing).
+ * Unit-weight graphs run 64 sources per pass with one bit per source
+ * (msbfs.hip); pj_last_stats then describes the whole batch. */
 int pj_sssp_batch(pj_graph* g, const int64_t* sources, int n_src, int32_t* dist_out);
 /* Statistics of the last solve. pj_reach_stats additionally computes
  * reached / reached_edges on the device (not part of kernel_ms). */

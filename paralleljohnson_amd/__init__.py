@@ -69,6 +69,7 @@ _SIGS = {
     "pj_load_snap_buffer": ([_P, ctypes.c_char_p, _I64, _INT, _PP], _INT),
     "pj_load_coo": ([_P, _P, _P, _P, _I64, _I64, _PP], _INT),
     "pj_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _PP], _INT),
+    "pj_generate_webgraph": ([_P, _I64, _I64, ctypes.c_uint64, _PP], _INT),
     "pj_graph_destroy": ([_P], _INT),
     "pj_graph_info": ([_P, _P, _P, _P, _P], _INT),
     "pj_graph_get_csr": ([_P, _P, _P, _P], _INT),
@@ -151,11 +152,12 @@ class Graph:
     def dist_device_ptr(self) -> int:
         return _lib.pj_dist_device(self._h) or 0
 
-    def sssp_batch(self, sources: Sequence[int]) -> np.ndarray:
+    def sssp_batch(self, sources: Sequence[int], copy: bool = True) -> Optional[np.ndarray]:
+        """Rows of the all-pairs distance matrix for `sources` (n_src x n int32)."""
         src = np.ascontiguousarray(np.asarray(sources, dtype=np.int64))
-        out = np.empty((len(src), max(self.n, 1)), np.int32)
+        out = np.empty((len(src), max(self.n, 1)), np.int32) if copy else None
         _check(_lib.pj_sssp_batch(self._h, _ptr(src), len(src), _ptr(out)))
-        return out[:, : self.n]
+        return out[:, : self.n] if copy else None
 
     def stats(self) -> dict:
         st = Stats()
@@ -232,6 +234,12 @@ class Context:
         wa = None if w is None else np.ascontiguousarray(np.asarray(w, dtype=np.uint32))
         g = ctypes.c_void_p()
         _check(_lib.pj_load_coo(self._h, _ptr(s), _ptr(d), _ptr(wa), len(s), int(n), ctypes.byref(g)))
+        return Graph(self, g)
+
+    def generate_webgraph(self, n_ids: int = 916428, n_edges: int = 5105039, seed: int = 1) -> Graph:
+        """web-Google-shaped synthetic graph."""
+        g = ctypes.c_void_p()
+        _check(_lib.pj_generate_webgraph(self._h, int(n_ids), int(n_edges), ctypes.c_uint64(seed), ctypes.byref(g)))
         return Graph(self, g)
 
     def generate_kronecker(self, scale: int, edgefactor: int = 16, seed: int = 1, weighted: bool = False) -> Graph:

@@ -225,6 +225,21 @@ int pj_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed,
     });
 }
 
+int pj_generate_webgraph(pj_ctx* ctx, int64_t n_ids, int64_t n_edges, uint64_t seed, pj_graph** out) {
+    if (!ctx || !out || n_ids < 2 || n_ids > 0xFFFFFFFEll || n_edges < 1)
+        return arg_error("pj_generate_webgraph: n_ids must be in [2, 2^32-2], n_edges >= 1");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        DevBuf<u32> src, dst;
+        generate_webgraph_device(ctx->c, n_ids, n_edges, seed, src, dst);
+        auto pg = std::make_unique<pj_graph>();
+        pg->g.ctx = &ctx->c;
+        build_graph_from_coo(pg->g, src, dst, nullptr, n_edges, n_ids, false);
+        return finish_graph(ctx, pg, out);
+    });
+}
+
 int pj_graph_destroy(pj_graph* g) {
     if (!g) return PJ_OK;
     return guarded([&] {
@@ -299,6 +314,7 @@ int pj_sssp(pj_graph* pg, int64_t source, int32_t* dist_out) {
         Graph& g = pg->g;
         bind(*g.ctx);
         auto t0 = std::chrono::steady_clock::now();
+        g.batch_stats = false;
         if (g.weighted) delta_solve(g, source);
         else bfs_solve(g, source);
         if (dist_out && g.n) PJ_HIP(hipMemcpy(dist_out, g.dist.p, 4 * (size_t)g.n, hipMemcpyDeviceToHost));
@@ -324,16 +340,25 @@ const int32_t* pj_dist_device(pj_graph* pg) { return (pg && pg->g.have_result) ?
 
 int pj_sssp_batch(pj_graph* pg, const int64_t* sources, int n_src, int32_t* dist_out) {
     if (!pg || (n_src > 0 && !sources) || n_src < 0) return arg_error("pj_sssp_batch: bad argument");
-    for (int i = 0; i < n_src; ++i) {
-        int rc = pj_sssp(pg, sources[i], dist_out ? dist_out + (size_t)i * (size_t)pg->g.n : nullptr);
-        if (rc != PJ_OK) return rc;
+    if (pg->g.weighted) {
+        for (int i = 0; i < n_src; ++i) {
+            int rc = pj_sssp(pg, sources[i], dist_out ? dist_out + (size_t)i * (size_t)pg->g.n : nullptr);
+            if (rc != PJ_OK) return rc;
+        }
+        return PJ_OK;
     }
-    return PJ_OK;
+    return guarded([&] {
+        bind(*pg->g.ctx);
+        msbfs_solve(pg->g, sources, n_src, dist_out);
+        pg->g.have_result = false;  // g.dist does not hold a batch row
+        pg->g.batch_stats = true;
+        return (int)PJ_OK;
+    });
 }
 
 int pj_last_stats(const pj_graph* pg, pj_stats* out) {
     if (!pg || !out) return arg_error("pj_last_stats: bad argument");
-    if (!pg->g.have_result) {
+    if (!pg->g.have_result && !pg->g.batch_stats) {
         set_error("pj_last_stats: no solve has run on this graph");
         return PJ_ERR_STATE;
     }

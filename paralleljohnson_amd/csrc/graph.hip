@@ -195,4 +195,66 @@ void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t see
     }
 }
 
+// ------------------------------------------------------------------------
+// web-Google-shaped generator (the SNAP file is not in the
+// image; configs[0] runs on a seeded synthetic of the same shape). Edge i:
+//   source rank  = floor(np * u1^g_out)            power-law out-degree
+//   target rank  = floor(np * u2^g_in)             power-law in-degree, or with
+//                  probability 3/10 a "same-site" link: source rank + 1..64
+// ranks are mapped to ids by an affine bijection mod n_ids over the first np
+// ranks (np ~ 95.6% of the id range, as in web-Google), and edge 0 is pinned
+// to the largest id so that N = max id + 1 = n_ids.
+// ------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ double u01(u64 h) { return (double)(h >> 11) * (1.0 / 9007199254740992.0); }
+
+__global__ __launch_bounds__(256) void webgraph_k(u64 n_ids, u64 np, u64 m, u64 seed, u64 mul, u64 add, double g_out,
+                                                  double g_in, u32* __restrict__ src, u32* __restrict__ dst) {
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (u64)gridDim.x * blockDim.x) {
+        const u64 h1 = splitmix64(seed ^ (i * 4 + 0));
+        const u64 h2 = splitmix64(seed ^ (i * 4 + 1));
+        const u64 h3 = splitmix64(seed ^ (i * 4 + 2));
+        u64 rs = (u64)((double)np * pow(u01(h1), g_out));
+        if (rs >= np) rs = np - 1;
+        u64 rd;
+        if ((h3 % 10) < 3) {
+            rd = (rs + 1 + (h3 >> 8) % 64) % np;
+        } else {
+            rd = (u64)((double)np * pow(u01(h2), g_in));
+            if (rd >= np) rd = np - 1;
+        }
+        u64 a = (rs * mul + add) % n_ids, b = (rd * mul + add) % n_ids;
+        if (i == 0) b = n_ids - 1;
+        src[i] = (u32)a;
+        dst[i] = (u32)b;
+    }
+}
+
+u64 gcd_u64(u64 a, u64 b) {
+    while (b) {
+        u64 t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+}  // namespace
+
+void generate_webgraph_device(Ctx& ctx, i64 n_ids, i64 n_edges, uint64_t seed, DevBuf<u32>& src,
+                              DevBuf<u32>& dst) {
+    src.alloc((size_t)n_edges);
+    dst.alloc((size_t)n_edges);
+    const u64 np = (u64)((double)n_ids * 0.9556);
+    u64 mul = (splitmix64_h(seed ^ 0x6A09E667F3BCC908ull) % (u64)n_ids) | 1ull;
+    while (gcd_u64(mul, (u64)n_ids) != 1) mul += 2;
+    const u64 add = splitmix64_h(seed ^ 0xBB67AE8584CAA73Bull) % (u64)n_ids;
+    if (n_edges) {
+        webgraph_k<<<grid_for(n_edges, 256, 256u * 64u), 256, 0, ctx.stream>>>(
+            (u64)n_ids, np ? np : 1, (u64)n_edges, seed, mul, add, 1.47, 2.0, src.p, dst.p);
+        PJ_LAUNCH_CHECK();
+    }
+}
+
 }  // namespace pj

@@ -129,6 +129,11 @@ void delete_bfs_work(BfsWorkHolder* p);
 struct BfsWorkDeleter {
     void operator()(BfsWorkHolder* p) const { delete_bfs_work(p); }
 };
+struct MsWork;
+void delete_ms_work(MsWork* p);
+struct MsWorkDeleter {
+    void operator()(MsWork* p) const { delete_ms_work(p); }
+};
 
 struct Graph {
     Ctx* ctx = nullptr;
@@ -152,6 +157,7 @@ struct Graph {
     ScanWs scan;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::unique_ptr<BfsWorkHolder, BfsWorkDeleter> bfs_work;
+    std::unique_ptr<MsWork, MsWorkDeleter> ms_work;
 
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;
@@ -161,6 +167,7 @@ struct Graph {
     int max_levels = 0;  // debug: truncate the BFS after this many levels (0 = off)
 
     bool have_result = false;
+    bool batch_stats = false;  // stats describe the last pj_sssp_batch
     pj_stats stats{};
 
     const void* row_ptr() const { return off64 ? (const void*)row64.p : (const void*)row32.p; }
@@ -187,12 +194,15 @@ struct ParseResult {
 ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool weighted,
                               DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w);
 
+void generate_webgraph_device(Ctx& ctx, i64 n_ids, i64 n_edges, uint64_t seed, DevBuf<u32>& src,
+                              DevBuf<u32>& dst);
 void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t seed, bool weighted,
                                DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>* w);
 
 // solvers
 void bfs_solve(Graph& g, i64 source);
 void delta_solve(Graph& g, i64 source);
+void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out);
 void reach_stats(Graph& g, i64* n_r, i64* m_r);
 void debug_bitmaps(Graph& g, u64* vis0, u64* vis1, u64* fnew);
 

@@ -37,3 +37,12 @@ def to_text(src, dst, w=None, style=0):
         if style and i % 97 == 0:
             lines.append("\n# comment line\n")
     return "".join(lines).encode()
+
+
+def csr_to_text(row, col):
+    """SNAP-style edge list (tab-separated, '#' header) of a CSR, rows in order."""
+    import numpy as np
+    src = np.repeat(np.arange(len(row) - 1, dtype=np.int64), np.diff(row))
+    body = np.char.add(np.char.add(src.astype(str), "\t"), np.asarray(col, dtype=np.int64).astype(str))
+    return ("# Directed graph (synthetic, web-Google-shaped)\n# FromNodeId\tToNodeId\n" +
+            "\n".join(body.tolist()) + "\n").encode()

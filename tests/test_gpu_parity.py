@@ -10,7 +10,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from helpers import chain_text, random_graph, to_text
+from helpers import chain_text, csr_to_text, random_graph, to_text
 
 pytestmark = pytest.mark.gpu
 INF = 100000
@@ -203,3 +203,52 @@ def test_cli_end_to_end(pj, oracle, tmp_path):
     # atoi source semantics
     r = subprocess.run([pj.cli_path(), str(f), "7abc", str(out)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and out.read_bytes() == oracle.format_sol(oracle.bfs(row, col, 7))
+
+
+@pytest.mark.parametrize("kind", ["uniform", "hub", "chain"])
+def test_msbfs_batch_rows(ctx, oracle, kind):
+    """pj_sssp_batch (64 sources per pass, msbfs.hip): every row equals a single-source run."""
+    rng = np.random.default_rng(77 + len(kind))
+    n = 20000
+    src, dst = random_graph(rng, kind, n)
+    g = ctx.load_coo(src, dst, n=n)
+    row, col, _ = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n)
+    sources = [int(x) for x in rng.integers(0, n, 70)] + [-1, n, int(src[0]), int(src[0])]
+    out = g.sssp_batch(sources)
+    assert out.shape == (len(sources), n)
+    for i, r in enumerate(sources):
+        assert (out[i] == oracle.bfs(row, col, r)).all(), (kind, i, r)
+
+
+def test_msbfs_kronecker_and_chain_cap(ctx, oracle, pj):
+    g = ctx.generate_kronecker(14, 16, 3)
+    row, col, _ = g.get_csr()
+    col = col.astype(np.uint32)
+    roots = list(g.sample_roots(5, 64))
+    out = g.sssp_batch(roots)
+    for i, r in enumerate(roots):
+        assert (out[i] == oracle.bfs(row, col, int(r))).all()
+    # R9 cap applies per source in batch mode too
+    c = ctx.load_snap_buffer(chain_text(100010))
+    out = c.sssp_batch([0, 5])
+    assert out[0][99999] == 99999 and out[0][100000] == INF and out[1][100004] == 99999 and out[1][100005] == INF
+
+
+def test_webgraph_cli_config0(ctx, pj, oracle, tmp_path):
+    """BASELINE configs[0] on the web-Google-shaped synthetic (the SNAP file is not
+    available): sol_file bytes equal the oracle BFS and the reference's BSP algorithm
+    at np=4 (the mpirun -np 4 analogue)."""
+    g = ctx.generate_webgraph(916428, 5105039, 1)
+    assert g.n == 916428 and g.nnz == 5105039
+    row, col, _ = g.get_csr()
+    col = col.astype(np.uint32)
+    f = tmp_path / "web-Google-synthetic.txt"
+    f.write_bytes(csr_to_text(row, col))
+    out = tmp_path / "sol.txt"
+    r = subprocess.run([pj.cli_path(), str(f), "0", str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    exp = oracle.bfs(row, col, 0)
+    ref4, st = oracle.reference_sssp(row, col, 0, 4)
+    assert (ref4 == exp).all()
+    assert out.read_bytes() == oracle.format_sol(exp)
+    assert (exp < INF).sum() > 100000  # source 0 reaches a large part of the graph
