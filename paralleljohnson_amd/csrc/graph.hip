@@ -1,28 +1,45 @@
-// graph.hip — CSR/CSC construction from device COO and the Kronecker generator.
+// graph.hip — CSR/CSC construction from device COO, and the benchmark generators.
 //
 // CSR build = stable radix sort by src + lower-bound row offsets: the GPU form
 // of coord2csr (ParallelJohnson.cpp:117-159), keeping duplicate edges,
 // self-loops and file order inside each row. The CSC (in-edges, used only by
 // the pull/bottom-up BFS step) is a second sort of the CSR by column.
+// Weighted graphs (no reference counterpart: the reference hard-codes w = 1,
+// :147) keep each row sorted by weight instead, for delta-stepping.
 #include "devutil.h"
 
 namespace pj {
 
 namespace {
 
-__global__ void pack_dst_w_k(const u32* __restrict__ dst, const u32* __restrict__ w, u64* __restrict__ out,
-                             i64 n) {
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
-        out[i] = (u64)dst[i] | ((u64)w[i] << 32);
+__global__ void iota_k(u32* __restrict__ p, i64 n) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) p[i] = (u32)i;
 }
 
-__global__ void unpack_dst_w_k(const u64* __restrict__ in, u32* __restrict__ dst, u32* __restrict__ w,
-                               i64 n) {
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
-        u64 x = in[i];
-        dst[i] = (u32)x;
-        w[i] = (u32)(x >> 32);
-    }
+__global__ void gather_k(const u32* __restrict__ in, const u32* __restrict__ idx, u32* __restrict__ out, i64 n) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) out[i] = in[idx[i]];
+}
+
+__global__ void max_k(const u32* __restrict__ in, i64 n, u32* __restrict__ out) {
+    u32 m = 0;
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) m = max(m, in[i]);
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+}
+
+// number of significant bits of max(w[0..n))
+int max_bits_device(const u32* w, i64 n, hipStream_t s) {
+    if (n == 0) return 0;
+    DevBuf<u32> m(1);
+    PJ_HIP(hipMemsetAsync(m.p, 0, sizeof(u32), s));
+    max_k<<<grid_for(n, 256, 4096), 256, 0, s>>>(w, n, m.p);
+    PJ_LAUNCH_CHECK();
+    u32 h = 0;
+    PJ_HIP(hipMemcpyAsync(&h, m.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    int b = 0;
+    while (b < 32 && (h >> b)) ++b;
+    return b;
 }
 
 int key_bits(i64 n) {
@@ -90,20 +107,35 @@ void build_graph_from_coo(Graph& g, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u
         }
         PJ_HIP(hipStreamSynchronize(s));
     } else {
-        DevBuf<u64> v((size_t)nnz), valt((size_t)nnz);
-        DevBuf<u32> kalt((size_t)nnz);
+        // Weighted: rows sorted by weight (ties in file order), so that for any
+        // delta the light edges of a vertex are a prefix of its row. Two stable
+        // LSD sorts of a permutation: by weight, then by source.
+        DevBuf<u32> perm((size_t)nnz), palt((size_t)nnz), k2((size_t)nnz), kalt((size_t)nnz);
         if (nnz) {
-            pack_dst_w_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(dst.p, w->p, v.p, nnz);
+            iota_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(perm.p, nnz);
+            PJ_LAUNCH_CHECK();
+            PJ_HIP(hipMemcpyAsync(k2.p, w->p, sizeof(u32) * (size_t)nnz, hipMemcpyDeviceToDevice, s));
+        }
+        const int wbits = max_bits_device(w->p, nnz, s);
+        u32 *kr, *pr;
+        radix_sort_pairs<u32>(k2.p, kalt.p, perm.p, palt.p, nnz, wbits, ws, s, &kr, &pr);
+        // keys := src[perm]
+        u32* keys = (kr == k2.p) ? kalt.p : k2.p;  // the free key buffer
+        u32* pfree = (pr == perm.p) ? palt.p : perm.p;
+        if (nnz) {
+            gather_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(src.p, pr, keys, nnz);
             PJ_LAUNCH_CHECK();
         }
-        u32* kr;
-        u64* vr;
-        radix_sort_pairs<u64>(src.p, kalt.p, v.p, valt.p, nnz, bits, ws, s, &kr, &vr);
-        bounds(g, kr, false);
+        u32* kfree = (keys == k2.p) ? kalt.p : k2.p;
+        u32 *kr2, *pr2;
+        radix_sort_pairs<u32>(keys, kfree, pr, pfree, nnz, bits, ws, s, &kr2, &pr2);
+        bounds(g, kr2, false);
         g.col.alloc((size_t)nnz);
         g.w.alloc((size_t)nnz);
         if (nnz) {
-            unpack_dst_w_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(vr, g.col.p, g.w.p, nnz);
+            gather_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(dst.p, pr2, g.col.p, nnz);
+            PJ_LAUNCH_CHECK();
+            gather_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(w->p, pr2, g.w.p, nnz);
             PJ_LAUNCH_CHECK();
         }
         PJ_HIP(hipStreamSynchronize(s));

@@ -134,6 +134,11 @@ void delete_ms_work(MsWork* p);
 struct MsWorkDeleter {
     void operator()(MsWork* p) const { delete_ms_work(p); }
 };
+struct DeltaWork;
+void delete_delta_work(DeltaWork* p);
+struct DeltaWorkDeleter {
+    void operator()(DeltaWork* p) const { delete_delta_work(p); }
+};
 
 struct Graph {
     Ctx* ctx = nullptr;
@@ -158,6 +163,8 @@ struct Graph {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::unique_ptr<BfsWorkHolder, BfsWorkDeleter> bfs_work;
     std::unique_ptr<MsWork, MsWorkDeleter> ms_work;
+    std::unique_ptr<DeltaWork, DeltaWorkDeleter> delta_work;
+    double mean_weight = -1.0;  // weighted: computed on first delta solve
 
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;

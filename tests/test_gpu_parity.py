@@ -142,6 +142,12 @@ def test_weighted_delta_stepping(ctx, oracle):
         w = rng.integers(0 if trial % 2 else 1, [3, 300, 5000][trial % 3], len(src)).astype(np.uint32)
         g = ctx.load_coo(src, dst, w=w, n=n)
         row, col, wc = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n, w)
+        # weighted rows are stored weight-sorted, ties in file order (graph.hip)
+        grow, gcol, gw = g.get_csr()
+        rid = np.repeat(np.arange(n), np.diff(row))
+        perm = np.lexsort((wc, rid))
+        assert (grow == row).all()
+        assert (gcol.astype(np.uint32) == col[perm]).all() and (gw == wc[perm]).all()
         for delta in (0, 1, 37):
             g.set_option("delta", delta)
             for r in (int(src[0]) if len(src) else 0, int(rng.integers(0, n))):
