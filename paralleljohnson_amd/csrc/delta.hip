@@ -1,23 +1,36 @@
-// delta.hip — weighted SSSP: delta-stepping with light/heavy edges.
+// delta.hip — weighted SSSP: delta-stepping with light/heavy edges and
+// in-workgroup recursion for the near phase.
 //
 // Generalises the reference's label-correcting relaxation (extract_local_pq
 // :226-278, apply loop :557-573) to integer weights >= 0, keeping its output
 // contract: candidates >= INT_INF are discarded and the
 // result is the true distance when it is < INT_INF. The reference settles one
-// vertex per heap pop; here a whole distance band [thr - delta, thr) is
-// settled at once (Meyer & Sanders' delta-stepping):
-//   rows are sorted by weight (graph.hip), so the light edges (w < delta) of v
-//   are the prefix row[v] .. row[v] + lsplit[v];
-//   near rounds : the vertices improved below thr relax their LIGHT edges,
-//                 edge-balanced (lb.h tiles), dist lowered with atomicMin;
-//                 improvements below thr re-enter the near queue, the rest go
-//                 to the far pile (per-epoch stamp: each vertex at most once)
-//   heavy pass  : when the band is stable, every vertex settled in it relaxes
-//                 its HEAVY edges once (their targets land at >= thr)
-//   split       : thr jumps to the first band holding a far vertex; far entries
-//                 below the new thr become the near queue
-// Each round / pass is one kernel; the host reads a few counters between them
-// (the analogue of the reference's termination allreduce :579-593).
+// vertex per heap pop; here a whole distance band [lo, hi = lo + delta) is
+// settled at once (Meyer & Sanders' delta-stepping). Rows are sorted by weight
+// (graph.hip), so the light edges (w < delta) of v are the prefix
+// row[v] .. row[v] + lsplit[v] and the heavy ones the rest of the row.
+//
+// Per band:
+//   select(DIST) : one streaming pass over dist lists the band's members
+//                  (lo <= dist < hi) with their light and heavy edge ranges and
+//                  yields min{dist >= lo}, so an empty band jumps straight to the
+//                  next occupied one. No far pile is kept: far vertices are simply
+//                  those with dist >= hi.
+//   light pass   : edge-balanced (lb.h) over the members' light edges, atomicMin
+//                  on dist. A vertex lowered below hi joins the band: the
+//                  workgroup that lowered it pushes it on an LDS worklist and
+//                  relaxes its whole row itself, recursively, before it exits, so
+//                  the band's near phase is ONE launch instead of one launch per
+//                  Bellman-Ford round. Worklist overflow and rows longer than
+//                  LOCAL_MAX go to the `chg` bitmap instead, and select(BITS)
+//                  turns that into a follow-up round (rare).
+//   heavy pass   : edge-balanced over the members' heavy edges; their targets
+//                  land at >= hi, so nothing joins the band.
+// Frontier lists are built without atomics: pass 1 counts per wave (64 bitmap
+// words each), a one-block scan turns the counts into offsets, pass 2 writes the
+// entries in vertex order. The host reads the band totals from mapped memory
+// once per band (the analogue of the reference's termination allreduce,
+// :579-593).
 #include <chrono>
 #include <cmath>
 
@@ -27,86 +40,377 @@ namespace pj {
 
 namespace {
 
-struct DCnt {
-    u64 n_near;   // near-queue entries appended
-    u64 m_near;   // their light-edge sum
-    u64 n_far;    // far-pile entries appended
-    u64 min_far;  // smallest distance in the far pile (split pre-pass)
-    u64 n_r;      // settled-in-band entries with heavy edges appended
-    u64 m_r;      // their heavy-edge sum
-    u64 pad[2];
-};
-
-constexpr int DB = 256;
+constexpr int DB = 256;             // relax workgroup
 constexpr int D_IPT = 4;
-constexpr int D_TILE = DB * D_IPT;
+constexpr int D_TILE = DB * D_IPT;  // edges per relax tile
+constexpr int WL_CAP = 2048;        // LDS worklist of a relax workgroup
+constexpr u32 LOCAL_BUDGET = 512;   // worklist vertices a workgroup relaxes itself
+constexpr int WL_BATCH = DB;        // worklist entries expanded per step
+constexpr u64 LOCAL_MAX = 4096;     // longest row a workgroup relaxes alone
+constexpr int SB = 256;             // select workgroup
+constexpr int SNW = SB / WAVE;
+constexpr int WPW = 64;             // bitmap words per select wave (one per lane in pass 2)
+constexpr int SU = 8;               // words whose loads a select wave issues together
+constexpr int SCAN_T = 1024;        // threads of the one-block scan
 
-struct DQueues {
-    // near queue (next), band list, far pile (current epoch)
-    u32 *qv, *qdeg;
-    u64* qbeg;
-    u32 *rv, *rdeg;
-    u64* rbeg;
-    u32* far;
-    int32_t *st_near, *st_band, *st_far;
-    int32_t round, band, epoch;
+// DIST_L / DIST_H: band members (lo <= dist < hi) with their light / heavy edges;
+// BITS: the deferred vertices of `chg` with their light edges.
+enum SelMode : int { SEL_DIST_L = 0, SEL_BITS = 1, SEL_DIST_H = 2 };
+
+// Totals of one selection, written by sel_scan_k (device + mapped host copy).
+struct DTot {
+    u64 nl, ml;    // light list: entries with light edges, their light edges (BITS: whole rows)
+    u64 nh, mh;    // heavy list: entries with heavy edges, their heavy edges (BITS: none)
+    u64 members;   // DIST: vertices with lo <= dist < hi
+    u64 minv;      // DIST: min{dist : lo <= dist < INT_INF} (INT_INF if none)
+    u64 overflow;  // a relax since the previous selection deferred vertices to `chg`
 };
 
-// v's distance just dropped below thr (or v came out of the far pile): queue its
-// light edges for the next near round and, once per band, its heavy edges.
-template <typename Off>
-__device__ __forceinline__ void near_append(u32 v, const Off* __restrict__ row, const u32* __restrict__ lsplit,
-                                            bool pred, const DQueues& q, DCnt* c, u64& m_acc, u64& h_acc) {
-    u32 lc = 0, hc = 0;
-    u64 beg = 0;
-    bool first_in_band = false;
-    if (pred) {
-        const Off b = row[v], e = row[v + 1];
-        lc = lsplit[v];
-        hc = (u32)(e - b) - lc;
-        beg = (u64)b;
-        first_in_band = atomicExch(q.st_band + v, q.band) != q.band;
-    }
-    const bool app = pred && lc > 0;
-    const u64 slot = wave_append(app, &c->n_near);
-    if (app) {
-        q.qv[slot] = v;
-        q.qdeg[slot] = lc;
-        q.qbeg[slot] = beg;
-        m_acc += lc;
-    }
-    const bool rap = first_in_band && hc > 0;
-    const u64 rslot = wave_append(rap, &c->n_r);
-    if (rap) {
-        q.rv[rslot] = v;
-        q.rdeg[rslot] = hc;
-        q.rbeg[rslot] = beg + lc;
-        h_acc += hc;
+struct SelArgs {
+    i64 n, nwords;
+    i64 nwaves;  // select waves (WPW words each)
+    int32_t lo, hi;
+    const int32_t* dist;
+    const u32* lsplit;
+    u64* chg;   // vertices deferred by a relax workgroup (worklist overflow / long rows)
+    u64* sel;   // the frontier being built
+    u64* part;  // [6][nwaves]: light count/edges, heavy count/edges, members, min per wave
+    u64* boff;  // [4][nwaves]: exclusive light count/edges, heavy count/edges per wave
+    // two frontier lists (every entry has >= 1 edge in its range, as lb.h requires)
+    u32 *qvl, *qvh;
+    u64 *qbl, *qbh;  // range begin: row[v] / row[v] + lsplit[v]
+    u64 *qol, *qoh;  // [n + 1] exclusive edge offsets
+    u32* flag;  // set by relax workgroups that wrote `chg`
+    DTot* tot;
+    DTot* host;  // mapped pinned copy of *tot
+};
+
+// Light / heavy edge counts of v for the list MODE builds.
+template <typename Off, int MODE>
+__device__ __forceinline__ void edge_split(const SelArgs& a, const Off* __restrict__ row, i64 v, u64& lc,
+                                           u64& hc, u64& hskip) {
+    if (MODE == SEL_DIST_H) {
+        hskip = a.lsplit[v];  // the heavy range starts after the light prefix
+        lc = 0;
+        hc = (u64)(row[v + 1] - row[v]) - hskip;
+    } else {
+        lc = a.lsplit[v];
+        hc = 0;
+        hskip = 0;
     }
 }
 
-template <typename Off>
-__global__ void d_source_k(i64 s, const Off* __restrict__ row, const u32* __restrict__ lsplit,
-                           int32_t* __restrict__ dist, DQueues q, DCnt* __restrict__ c) {
-    dist[s] = 0;
-    const Off b = row[s], e = row[s + 1];
-    const u32 lc = lsplit[s], hc = (u32)(e - b) - lc;
-    q.st_band[s] = q.band;
-    if (lc) {
-        q.qv[0] = (u32)s;
-        q.qdeg[0] = lc;
-        q.qbeg[0] = (u64)b;
-        c->n_near = 1;
-        c->m_near = lc;
+// Pass 1: each wave classifies its WPW bitmap words (lane = vertex of a word,
+// SU words' loads in flight at once), writes the `sel` words and publishes
+// (count, light edges, heavy edges, members, min) for the wave.
+template <typename Off, int MODE>
+__global__ __launch_bounds__(SB) void sel_count_k(SelArgs a, const Off* __restrict__ row) {
+    const int lane = lane_id();
+    const i64 wave = (i64)blockIdx.x * SNW + wave_id();
+    if (wave >= a.nwaves) return;
+    const i64 wb = wave * WPW;
+    u64 cl = 0, chh = 0, el = 0, eh = 0, members = 0;
+    long long mn = INT_INF;
+    for (int k0 = 0; k0 < WPW; k0 += SU) {
+        bool s[SU];
+        if (MODE != SEL_BITS) {
+            int32_t d[SU];
+#pragma unroll
+            for (int k = 0; k < SU; ++k) {
+                const i64 v = ((wb + k0 + k) << 6) + lane;
+                d[k] = v < a.n ? a.dist[v] : INT_INF;
+            }
+#pragma unroll
+            for (int k = 0; k < SU; ++k) {
+                s[k] = d[k] >= a.lo && d[k] < a.hi;
+                if (d[k] >= a.lo && d[k] < mn) mn = d[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < SU; ++k) {
+                const i64 wi = wb + k0 + k;
+                const u64 word = wi < a.nwords ? a.chg[wi] : 0ull;  // wave-uniform
+                s[k] = (word >> lane) & 1ull;
+                if (word && lane == 0) a.chg[wi] = 0;
+            }
+        }
+        u64 lc[SU], hc[SU];
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            u64 skip = 0;
+            lc[k] = hc[k] = 0;
+            if (s[k]) edge_split<Off, MODE>(a, row, ((wb + k0 + k) << 6) + lane, lc[k], hc[k], skip);
+        }
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const i64 wi = wb + k0 + k;
+            if (MODE != SEL_BITS) members += __popcll(__ballot(s[k]));
+            const u64 sb = __ballot(lc[k] + hc[k] > 0);
+            cl += __popcll(__ballot(lc[k] > 0));
+            chh += __popcll(__ballot(hc[k] > 0));
+            el += lc[k];
+            eh += hc[k];
+            if (lane == 0 && wi < a.nwords) a.sel[wi] = sb;
+        }
     }
-    if (hc) {
-        q.rv[0] = (u32)s;
-        q.rdeg[0] = hc;
-        q.rbeg[0] = (u64)b + lc;
-        c->n_r = 1;
-        c->m_r = hc;
+    el = wave_sum(el);
+    eh = wave_sum(eh);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const long long y = __shfl_xor(mn, off, 64);
+        mn = y < mn ? y : mn;
+    }
+    if (lane == 0) {
+        const i64 nw = a.nwaves;
+        a.part[wave] = cl;
+        a.part[nw + wave] = el;
+        a.part[2 * nw + wave] = chh;
+        a.part[3 * nw + wave] = eh;
+        a.part[4 * nw + wave] = members;
+        a.part[5 * nw + wave] = (u64)mn;
     }
 }
+
+// One block: exclusive scans of the per-wave partials, the totals, and the
+// relax overflow flag. Thread t owns the consecutive partials [t*per, (t+1)*per).
+__global__ __launch_bounds__(SCAN_T) void sel_scan_k(SelArgs a) {
+    __shared__ u64 lds[SCAN_T / WAVE];
+    const i64 nw = a.nwaves;
+    const i64 per = (nw + SCAN_T - 1) / SCAN_T;
+    const i64 i0 = (i64)threadIdx.x * per, i1 = min(i0 + per, nw);
+    u64 x[4] = {0, 0, 0, 0}, m = 0, mi = INT_INF;
+    for (i64 i = i0; i < i1; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] += a.part[j * nw + i];
+        m += a.part[4 * nw + i];
+        mi = min(mi, a.part[5 * nw + i]);
+    }
+    u64 ex[4], tt[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ex[j] = block_excl_scan<SCAN_T / WAVE>(x[j], lds, tt[j]);
+    for (i64 i = i0; i < i1; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            a.boff[j * nw + i] = ex[j];
+            ex[j] += a.part[j * nw + i];
+        }
+    }
+    m = block_sum<SCAN_T / WAVE>(m, lds);
+    mi = ~wave_max(~mi);  // wave min via max of complements
+    if (lane_id() == 0) lds[wave_id()] = mi;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 y = INT_INF;
+        for (int w = 0; w < SCAN_T / WAVE; ++w) y = lds[w] < y ? lds[w] : y;
+        const u64 ov = *a.flag;
+        *a.flag = 0;
+        DTot t{tt[0], tt[1], tt[2], tt[3], m, y, ov};
+        *a.tot = t;
+        a.host->nl = t.nl;
+        a.host->ml = t.ml;
+        a.host->nh = t.nh;
+        a.host->mh = t.mh;
+        a.host->members = t.members;
+        a.host->minv = t.minv;
+        a.host->overflow = t.overflow;
+        a.qol[t.nl] = t.ml;
+        a.qoh[t.nh] = t.mh;
+    }
+}
+
+// Pass 2: each wave writes the entries of its WPW `sel` words in vertex order at
+// its offsets (lane = word to find the non-empty words, then lane = vertex),
+// and clears the words.
+template <typename Off, int MODE>
+__global__ __launch_bounds__(SB) void sel_write_k(SelArgs a, const Off* __restrict__ row) {
+    const int lane = lane_id();
+    const i64 wave = (i64)blockIdx.x * SNW + wave_id();
+    if (wave >= a.nwaves) return;
+    const i64 nw = a.nwaves;
+    const i64 wb = wave * WPW;
+    const i64 my = wb + lane;
+    const u64 myword = my < a.nwords ? a.sel[my] : 0ull;
+    if (myword) a.sel[my] = 0;
+    u64 nz = __ballot(myword != 0);
+    u64 pl = a.boff[wave], el = a.boff[nw + wave], ph = a.boff[2 * nw + wave], eh = a.boff[3 * nw + wave];
+    while (nz) {
+        int kw[SU];
+        u64 word[SU];
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            kw[k] = nz ? __ffsll((long long)nz) - 1 : -1;
+            if (nz) nz &= nz - 1;
+            word[k] = kw[k] >= 0 ? __shfl(myword, kw[k], 64) : 0ull;
+        }
+        u64 lc[SU], hc[SU], b[SU], hb[SU];
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            lc[k] = hc[k] = b[k] = hb[k] = 0;
+            if ((word[k] >> lane) & 1ull) {
+                const i64 v = ((wb + kw[k]) << 6) + lane;
+                u64 skip = 0;
+                b[k] = (u64)row[v];
+                edge_split<Off, MODE>(a, row, v, lc[k], hc[k], skip);
+                hb[k] = b[k] + skip;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            if (!word[k]) continue;  // wave-uniform
+            const u32 v = (u32)(((wb + kw[k]) << 6) + lane);
+            const u64 ml = __ballot(lc[k] > 0), mh = __ballot(hc[k] > 0);
+            const u64 il = wave_incl_scan(lc[k]);
+            const u64 ih = wave_incl_scan(hc[k]);
+            if (lc[k] > 0) {
+                const u64 slot = pl + (u64)__popcll(ml & lanemask_lt());
+                a.qvl[slot] = v;
+                a.qbl[slot] = b[k];
+                a.qol[slot] = el + il - lc[k];
+            }
+            if (hc[k] > 0) {
+                const u64 slot = ph + (u64)__popcll(mh & lanemask_lt());
+                a.qvh[slot] = v;
+                a.qbh[slot] = hb[k];
+                a.qoh[slot] = eh + ih - hc[k];
+            }
+            pl += __popcll(ml);
+            ph += __popcll(mh);
+            el += __shfl(il, 63, 64);
+            eh += __shfl(ih, 63, 64);
+        }
+    }
+}
+
+struct Wl {
+    u32 n;  // entries pushed (may exceed WL_CAP: the excess went to chg)
+    u32 v[WL_CAP];
+    int32_t bdu[WL_BATCH];
+    u64 bbeg[WL_BATCH];
+    u64 boff[WL_BATCH + 1];
+    u64 scan[DB / WAVE];
+};
+
+__device__ __forceinline__ void defer_vertex(u32 v, u64* __restrict__ chg, u32* __restrict__ flag) {
+    atomicOr(chg + (v >> 6), 1ull << (v & 63));
+    *flag = 1u;
+}
+
+// Push the lanes' newly in-band vertices on the workgroup's worklist.
+__device__ __forceinline__ void wl_push(bool p, u32 v, Wl& wl, u64* __restrict__ chg, u32* __restrict__ flag) {
+    const u64 m = __ballot(p);
+    if (!m) return;
+    const int leader = __ffsll((long long)m) - 1;
+    u32 base = 0;
+    if (lane_id() == leader) base = atomicAdd(&wl.n, (u32)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (p) {
+        const u32 slot = base + (u32)__popcll(m & lanemask_lt());
+        if (slot < WL_CAP) wl.v[slot] = v;
+        else defer_vertex(v, chg, flag);
+    }
+}
+
+// One edge: relax u -> col[idx]; true if the target was lowered into the band.
+__device__ __forceinline__ bool relax_edge(u64 idx, int32_t du, const u32* __restrict__ col,
+                                           const u32* __restrict__ wt, int32_t* __restrict__ dist, int32_t hi,
+                                           u32& v) {
+    v = col[idx];
+    const long long nd = (long long)du + (long long)wt[idx];
+    if (nd < INT_INF && (int32_t)nd < dist[v]) {
+        const int32_t old = atomicMin(dist + v, (int32_t)nd);
+        return (int32_t)nd < old && (int32_t)nd < hi;
+    }
+    return false;
+}
+
+// Relax the edges [ib[i], ib[i] + deg_i) of the frontier, edge-balanced.
+// LIGHT: targets lowered below hi are relaxed (whole rows) by this workgroup
+// before it exits; HEAVY targets cannot land below hi.
+template <typename Off, bool LIGHT>
+__global__ __launch_bounds__(DB) void d_relax_k(const u32* __restrict__ iv, const u64* __restrict__ ib,
+                                                const u64* __restrict__ io, const DTot* __restrict__ tot,
+                                                const Off* __restrict__ row, const u32* __restrict__ lsplit,
+                                                const u32* __restrict__ col, const u32* __restrict__ wt,
+                                                int32_t* __restrict__ dist, int32_t hi, u64* __restrict__ chg,
+                                                u32* __restrict__ flag) {
+    __shared__ LbShared<D_TILE> sh;
+    __shared__ int32_t s_du[D_TILE];
+    __shared__ Wl wl;
+    if (LIGHT && threadIdx.x == 0) wl.n = 0;
+    const u64 nq = LIGHT ? tot->nl : tot->nh, total = LIGHT ? tot->ml : tot->mh;
+    const u64 ntiles = (total + D_TILE - 1) / D_TILE;
+    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const u64 e0 = tile * D_TILE;
+        const u64 e1 = min(e0 + (u64)D_TILE, total);
+        u64 s0;
+        u32 ns;
+        lb_tile_load<D_TILE>(io, nq, e0, sh, s0, ns);
+        for (u32 i = threadIdx.x; i < ns; i += DB) s_du[i] = dist[iv[s0 + i]];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < D_IPT; ++k) {
+            const u64 e = e0 + (u64)k * DB + threadIdx.x;
+            bool p = false;
+            u32 v = 0;
+            if (e < e1) {
+                const u32 j = lb_find<D_TILE>(sh, ns, e);
+                p = relax_edge(ib[s0 + j] + (e - sh.off[j]), s_du[j], col, wt, dist, hi, v);
+            }
+            if (LIGHT) wl_push(p, v, wl, chg, flag);
+        }
+        __syncthreads();
+    }
+    if (!LIGHT) return;
+    // ---- drain the worklist FIFO: relax the light edges of the vertices this
+    // workgroup lowered into the band (their heavy edges wait for the heavy pass), WL_BATCH per step, at most LOCAL_BUDGET in
+    // all (a cascade larger than that is spread over the grid by a BITS round)
+    u32 head = 0;
+    for (;;) {
+        __syncthreads();
+        const u32 n = min(wl.n, (u32)WL_CAP);
+        if (head >= n) break;
+        const u32 t = threadIdx.x;
+        if (head >= LOCAL_BUDGET) {
+            for (u32 i = head + t; i < n; i += DB) defer_vertex(wl.v[i], chg, flag);
+            break;
+        }
+        const u32 take = min(n - head, (u32)WL_BATCH);
+        u64 deg = 0;
+        if (t < take) {
+            const u32 v = wl.v[head + t];
+            const Off b = row[v];
+            deg = lsplit[v];
+            if (deg > LOCAL_MAX) {
+                defer_vertex(v, chg, flag);
+                deg = 0;
+            }
+            wl.bdu[t] = dist[v];
+            wl.bbeg[t] = (u64)b;
+        }
+        u64 total_e;
+        const u64 ex = block_excl_scan<DB / WAVE>(deg, wl.scan, total_e);
+        if (t < take) wl.boff[t] = ex;
+        head += take;
+        __syncthreads();
+        for (u64 f0 = 0; f0 < total_e; f0 += DB) {
+            const u64 f = f0 + t;
+            bool p = false;
+            u32 v = 0;
+            if (f < total_e) {
+                u32 lo = 0, hi2 = take - 1;  // last entry with boff <= f
+                while (lo < hi2) {
+                    const u32 mid = (lo + hi2 + 1) >> 1;
+                    if (wl.boff[mid] <= f) lo = mid;
+                    else hi2 = mid - 1;
+                }
+                p = relax_edge(wl.bbeg[lo] + (f - wl.boff[lo]), wl.bdu[lo], col, wt, dist, hi, v);
+            }
+            wl_push(p, v, wl, chg, flag);
+        }
+    }
+}
+
+__global__ void d_source_k(i64 s, int32_t* __restrict__ dist) { dist[s] = 0; }
 
 // lsplit[v] = number of edges of v with weight < delta (rows are weight-sorted)
 template <typename Off>
@@ -124,108 +428,6 @@ __global__ void light_split_k(const Off* __restrict__ row, const u32* __restrict
     }
 }
 
-// Relax the edges [qbeg[i], qbeg[i] + qdeg[i]) of queue entries (light edges in
-// near rounds, heavy edges in the band's heavy pass), edge-balanced.
-template <typename Off>
-__global__ __launch_bounds__(DB) void d_relax_k(const u32* __restrict__ iv, const u64* __restrict__ ibeg,
-                                                const u64* __restrict__ ioff, u64 nq, u64 total,
-                                                const u32* __restrict__ col, const u32* __restrict__ wt,
-                                                const Off* __restrict__ row, const u32* __restrict__ lsplit,
-                                                int32_t* __restrict__ dist, int32_t thr, DQueues q,
-                                                DCnt* __restrict__ cnt) {
-    __shared__ LbShared<D_TILE> sh;
-    __shared__ int32_t s_du[D_TILE];
-    __shared__ u64 red[DB / WAVE];
-    const u64 ntiles = (total + D_TILE - 1) / D_TILE;
-    u64 m_acc = 0, h_acc = 0;
-    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const u64 e0 = tile * D_TILE;
-        const u64 e1 = min(e0 + (u64)D_TILE, total);
-        u64 s0;
-        u32 ns;
-        lb_tile_load<D_TILE>(ioff, nq, e0, sh, s0, ns);
-        for (u32 i = threadIdx.x; i < ns; i += DB) s_du[i] = dist[iv[s0 + i]];
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < D_IPT; ++k) {
-            const u64 e = e0 + (u64)k * DB + threadIdx.x;
-            bool to_near = false, to_far = false;
-            u32 v = 0;
-            if (e < e1) {
-                const u32 j = lb_find<D_TILE>(sh, ns, e);
-                const u64 idx = ibeg[s0 + j] + (e - sh.off[j]);
-                v = col[idx];
-                const long long nd = (long long)s_du[j] + (long long)wt[idx];
-                if (nd < INT_INF && (int32_t)nd < dist[v]) {
-                    const int32_t old = atomicMin(dist + v, (int32_t)nd);
-                    if ((int32_t)nd < old) {
-                        if ((int32_t)nd < thr) to_near = atomicExch(q.st_near + v, q.round) != q.round;
-                        else to_far = atomicExch(q.st_far + v, q.epoch) != q.epoch;
-                    }
-                }
-            }
-            near_append<Off>(v, row, lsplit, to_near, q, cnt, m_acc, h_acc);
-            const u64 fslot = wave_append(to_far, &cnt->n_far);
-            if (to_far) q.far[fslot] = v;
-        }
-        __syncthreads();
-    }
-    m_acc = block_sum<DB / WAVE>(m_acc, red);
-    h_acc = block_sum<DB / WAVE>(h_acc, red);
-    if (threadIdx.x == 0) {
-        if (m_acc) atomicAdd(&cnt->m_near, m_acc);
-        if (h_acc) atomicAdd(&cnt->m_r, h_acc);
-    }
-}
-
-__global__ __launch_bounds__(DB) void d_far_min_k(const u32* __restrict__ far, u64 nf,
-                                                  const int32_t* __restrict__ dist, int32_t thr,
-                                                  DCnt* __restrict__ cnt) {
-    long long mn = INT_INF;
-    for (u64 i = (u64)blockIdx.x * DB + threadIdx.x; i < nf; i += (u64)gridDim.x * DB) {
-        const int32_t d = dist[far[i]];
-        if (d >= thr && d < mn) mn = d;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        long long y = __shfl_xor(mn, off, 64);
-        mn = y < mn ? y : mn;
-    }
-    if (lane_id() == 0 && mn < INT_INF) atomicMin(&cnt->min_far, (u64)mn);
-}
-
-template <typename Off>
-__global__ __launch_bounds__(DB) void d_split_k(const u32* __restrict__ far, u64 nf, const Off* __restrict__ row,
-                                                const u32* __restrict__ lsplit, const int32_t* __restrict__ dist,
-                                                int32_t old_thr, int32_t thr, DQueues q,
-                                                DCnt* __restrict__ cnt) {
-    __shared__ u64 red[DB / WAVE];
-    u64 m_acc = 0, h_acc = 0;
-    const u64 nloop = (nf + DB - 1) / DB;
-    for (u64 it = blockIdx.x; it < nloop; it += gridDim.x) {
-        const u64 i = it * DB + threadIdx.x;
-        bool to_near = false, to_far = false;
-        u32 v = 0;
-        if (i < nf) {
-            v = far[i];
-            const int32_t d = dist[v];
-            if (d >= old_thr) {  // entries below old_thr were settled in an earlier band
-                if (d < thr) to_near = atomicExch(q.st_near + v, q.round) != q.round;
-                else to_far = atomicExch(q.st_far + v, q.epoch) != q.epoch;
-            }
-        }
-        near_append<Off>(v, row, lsplit, to_near, q, cnt, m_acc, h_acc);
-        const u64 fslot = wave_append(to_far, &cnt->n_far);
-        if (to_far) q.far[fslot] = v;
-    }
-    m_acc = block_sum<DB / WAVE>(m_acc, red);
-    h_acc = block_sum<DB / WAVE>(h_acc, red);
-    if (threadIdx.x == 0) {
-        if (m_acc) atomicAdd(&cnt->m_near, m_acc);
-        if (h_acc) atomicAdd(&cnt->m_r, h_acc);
-    }
-}
-
 __global__ __launch_bounds__(DB) void wsum_k(const u32* __restrict__ w, i64 n, u64* __restrict__ out) {
     u64 acc = 0;
     for (i64 i = (i64)blockIdx.x * DB + threadIdx.x; i < n; i += (i64)gridDim.x * DB) acc += w[i];
@@ -236,12 +438,18 @@ __global__ __launch_bounds__(DB) void wsum_k(const u32* __restrict__ w, i64 n, u
 }  // namespace
 
 struct DeltaWork {
-    DevBuf<int32_t> st_near, st_band, st_far;
-    DevBuf<u32> far[2];
-    DevBuf<u32> rv, rdeg;
-    DevBuf<u64> rbeg;
+    DevBuf<u64> chg, sel;  // 1 bit per vertex
+    DevBuf<u32> qvl, qvh;
+    DevBuf<u64> qbl, qbh, qol, qoh;
+    DevBuf<u64> part, boff;
+    DevBuf<DTot> tot;
+    DevBuf<u32> flag;
     DevBuf<u32> lsplit;
+    DTot* host = nullptr;  // mapped pinned
     u32 lsplit_delta = 0;  // delta lsplit was computed for (0 = none)
+    ~DeltaWork() {
+        if (host) (void)hipHostFree(host);
+    }
 };
 
 void delete_delta_work(DeltaWork* p) { delete p; }
@@ -253,9 +461,8 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
     Ctx& ctx = *g.ctx;
     hipStream_t s = ctx.stream;
     const i64 n = g.n;
+    const i64 nwords = (n + 63) / 64;
     const Off* row = static_cast<const Off*>(g.row_ptr());
-    DCnt* dcnt = reinterpret_cast<DCnt*>(g.counters.p);
-    DCnt* hcnt = reinterpret_cast<DCnt*>(g.hcounters.p);
     const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
 
     // delta: explicit option, else (mean weight / mean out-degree) * 4 — light
@@ -272,136 +479,106 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
         w.lsplit_delta = (u32)delta;
     }
 
-    DQueues q{};
-    q.st_near = w.st_near.p;
-    q.st_band = w.st_band.p;
-    q.st_far = w.st_far.p;
-    q.rv = w.rv.p;
-    q.rdeg = w.rdeg.p;
-    q.rbeg = w.rbeg.p;
+    SelArgs a{};
+    a.n = n;
+    a.nwords = nwords;
+    a.nwaves = (nwords + WPW - 1) / WPW;
+    a.dist = g.dist.p;
+    a.lsplit = w.lsplit.p;
+    a.chg = w.chg.p;
+    a.sel = w.sel.p;
+    a.part = w.part.p;
+    a.boff = w.boff.p;
+    a.qvl = w.qvl.p;
+    a.qvh = w.qvh.p;
+    a.qbl = w.qbl.p;
+    a.qbh = w.qbh.p;
+    a.qol = w.qol.p;
+    a.qoh = w.qoh.p;
+    a.flag = w.flag.p;
+    a.tot = w.tot.p;
+    PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.host), w.host, 0));
+    const unsigned sgrid = (unsigned)((a.nwaves + SNW - 1) / SNW);
+
+    auto select = [&](int mode, int32_t lo, int32_t hi) -> DTot {
+        a.lo = lo;
+        a.hi = hi;
+        if (mode == SEL_DIST_L) sel_count_k<Off, SEL_DIST_L><<<sgrid, SB, 0, s>>>(a, row);
+        else if (mode == SEL_DIST_H) sel_count_k<Off, SEL_DIST_H><<<sgrid, SB, 0, s>>>(a, row);
+        else sel_count_k<Off, SEL_BITS><<<sgrid, SB, 0, s>>>(a, row);
+        PJ_LAUNCH_CHECK();
+        sel_scan_k<<<1, SCAN_T, 0, s>>>(a);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipStreamSynchronize(s));
+        const volatile DTot* h = w.host;
+        DTot t;
+        t.nl = h->nl;
+        t.ml = h->ml;
+        t.nh = h->nh;
+        t.mh = h->mh;
+        t.members = h->members;
+        t.minv = h->minv;
+        t.overflow = h->overflow;
+        return t;
+    };
+    pj_stats st{};
+    // write the selected list, then relax it (light: with recursion; heavy: plain)
+    auto relax = [&](int mode, const DTot& t, int32_t hi) {
+        if (mode == SEL_DIST_L) sel_write_k<Off, SEL_DIST_L><<<sgrid, SB, 0, s>>>(a, row);
+        else if (mode == SEL_DIST_H) sel_write_k<Off, SEL_DIST_H><<<sgrid, SB, 0, s>>>(a, row);
+        else sel_write_k<Off, SEL_BITS><<<sgrid, SB, 0, s>>>(a, row);
+        PJ_LAUNCH_CHECK();
+        if (t.ml > 0) {
+            const unsigned grid = grid_for((i64)((t.ml + D_TILE - 1) / D_TILE), 1, maxgrid);
+            d_relax_k<Off, true><<<grid, DB, 0, s>>>(w.qvl.p, w.qbl.p, w.qol.p, w.tot.p, row, w.lsplit.p, g.col.p,
+                                                     g.w.p, g.dist.p, hi, w.chg.p, w.flag.p);
+            PJ_LAUNCH_CHECK();
+            st.relax_rounds++;
+        }
+        if (t.mh > 0) {
+            const unsigned grid = grid_for((i64)((t.mh + D_TILE - 1) / D_TILE), 1, maxgrid);
+            d_relax_k<Off, false><<<grid, DB, 0, s>>>(w.qvh.p, w.qbh.p, w.qoh.p, w.tot.p, row, w.lsplit.p,
+                                                      g.col.p, g.w.p, g.dist.p, hi, w.chg.p, w.flag.p);
+            PJ_LAUNCH_CHECK();
+            st.relax_rounds++;
+        }
+    };
 
     auto t_host0 = std::chrono::steady_clock::now();
     PJ_HIP(hipEventRecord(g.ev0, s));
-    pj_stats st{};
     if (n > 0) {
         PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.dist.p), INT_INF, (size_t)n, s));
-        PJ_HIP(hipMemsetAsync(w.st_near.p, 0xFF, sizeof(int32_t) * (size_t)n, s));
-        PJ_HIP(hipMemsetAsync(w.st_band.p, 0xFF, sizeof(int32_t) * (size_t)n, s));
-        PJ_HIP(hipMemsetAsync(w.st_far.p, 0xFF, sizeof(int32_t) * (size_t)n, s));
+        PJ_HIP(hipMemsetAsync(w.chg.p, 0, sizeof(u64) * (size_t)nwords, s));
+        PJ_HIP(hipMemsetAsync(w.flag.p, 0, sizeof(u32), s));
     }
     if (source >= 0 && source < n) {
-        int cur = 0, fcur = 0;
-        q.round = 0;
-        q.band = 0;
-        q.epoch = 0;
-        q.qv = g.qv[0].p;
-        q.qdeg = g.qdeg[0].p;
-        q.qbeg = g.qbeg[0].p;
-        PJ_HIP(hipMemsetAsync(dcnt, 0, sizeof(DCnt), s));
-        d_source_k<Off><<<1, 1, 0, s>>>(source, row, w.lsplit.p, g.dist.p, q, dcnt);
+        d_source_k<<<1, 1, 0, s>>>(source, g.dist.p);
         PJ_LAUNCH_CHECK();
-        PJ_HIP(hipMemcpyAsync(hcnt, dcnt, sizeof(DCnt), hipMemcpyDeviceToHost, s));
-        PJ_HIP(hipStreamSynchronize(s));
-        u64 nq = hcnt->n_near, mq = hcnt->m_near, nf = 0, nr = hcnt->n_r, mr = hcnt->m_r;
-        int32_t round = 0, epoch = 0, band = 0;
-        int32_t thr = delta;
-        for (;;) {
-            // ---- near rounds: light edges of the vertices improved below thr
-            while (nq > 0) {
-                ++round;
-                const int nx = 1 - cur;
-                PJ_HIP(hipMemsetAsync(dcnt, 0, sizeof(DCnt), s));
-                exclusive_scan_u32(g.qdeg[cur].p, g.qoff.p, (i64)nq, g.scan, s);
-                q.round = round;
-                q.band = band;
-                q.epoch = epoch;
-                q.qv = g.qv[nx].p;
-                q.qdeg = g.qdeg[nx].p;
-                q.qbeg = g.qbeg[nx].p;
-                q.rv = w.rv.p + nr;
-                q.rdeg = w.rdeg.p + nr;
-                q.rbeg = w.rbeg.p + nr;
-                q.far = w.far[fcur].p + nf;
-                const unsigned grid = grid_for((i64)((mq + D_TILE - 1) / D_TILE), 1, maxgrid);
-                d_relax_k<Off><<<grid, DB, 0, s>>>(g.qv[cur].p, g.qbeg[cur].p, g.qoff.p, nq, mq, g.col.p, g.w.p,
-                                                   row, w.lsplit.p, g.dist.p, thr, q, dcnt);
-                PJ_LAUNCH_CHECK();
-                PJ_HIP(hipMemcpyAsync(hcnt, dcnt, sizeof(DCnt), hipMemcpyDeviceToHost, s));
-                PJ_HIP(hipStreamSynchronize(s));
-                nq = hcnt->n_near;
-                mq = hcnt->m_near;
-                nf += hcnt->n_far;
-                nr += hcnt->n_r;
-                mr += hcnt->m_r;
-                cur = nx;
-                st.relax_rounds++;
-            }
-            // ---- heavy pass: the band's settled vertices relax their heavy edges once
-            if (nr > 0) {
-                ++round;
-                PJ_HIP(hipMemsetAsync(dcnt, 0, sizeof(DCnt), s));
-                exclusive_scan_u32(w.rdeg.p, g.qoff.p, (i64)nr, g.scan, s);
-                q.round = round;
-                q.band = band;
-                q.epoch = epoch;
-                q.qv = g.qv[1 - cur].p;  // unused: heavy targets land at >= thr
-                q.qdeg = g.qdeg[1 - cur].p;
-                q.qbeg = g.qbeg[1 - cur].p;
-                q.rv = w.rv.p;  // unused for the same reason
-                q.rdeg = w.rdeg.p;
-                q.rbeg = w.rbeg.p;
-                q.far = w.far[fcur].p + nf;
-                const unsigned grid = grid_for((i64)((mr + D_TILE - 1) / D_TILE), 1, maxgrid);
-                d_relax_k<Off><<<grid, DB, 0, s>>>(w.rv.p, w.rbeg.p, g.qoff.p, nr, mr, g.col.p, g.w.p, row,
-                                                   w.lsplit.p, g.dist.p, thr, q, dcnt);
-                PJ_LAUNCH_CHECK();
-                PJ_HIP(hipMemcpyAsync(hcnt, dcnt, sizeof(DCnt), hipMemcpyDeviceToHost, s));
-                PJ_HIP(hipStreamSynchronize(s));
-                nf += hcnt->n_far;
-                nr = 0;
-                mr = 0;
-                st.relax_rounds++;
+        long long lo = 0;
+        while (lo < INT_INF) {
+            const int32_t hi = (int32_t)std::min<long long>(lo + delta, INT_INF);
+            DTot t = select(SEL_DIST_L, (int32_t)lo, hi);
+            if (t.members == 0) {
+                if (t.minv >= (u64)INT_INF) break;  // nothing reached beyond the settled bands
+                lo = (long long)t.minv / delta * delta;  // jump to the next occupied band
+                continue;
             }
             st.levels++;
-            if (nf == 0) break;
-            // ---- next non-empty band
-            DCnt init{};
-            init.min_far = (u64)INT_INF;
-            PJ_HIP(hipMemcpyAsync(dcnt, &init, sizeof(DCnt), hipMemcpyHostToDevice, s));
-            d_far_min_k<<<grid_for((i64)nf, DB, maxgrid), DB, 0, s>>>(w.far[fcur].p, nf, g.dist.p, thr, dcnt);
-            PJ_LAUNCH_CHECK();
-            PJ_HIP(hipMemcpyAsync(hcnt, dcnt, sizeof(DCnt), hipMemcpyDeviceToHost, s));
-            PJ_HIP(hipStreamSynchronize(s));
-            const u64 mn = hcnt->min_far;
-            if (mn >= (u64)INT_INF) break;  // every far entry was settled below thr
-            const int32_t old_thr = thr;
-            const long long nthr = ((long long)mn / delta + 1) * (long long)delta;
-            thr = (int32_t)std::min<long long>(nthr, INT_INF);
-            ++round;
-            ++epoch;
-            ++band;
-            q.round = round;
-            q.band = band;
-            q.epoch = epoch;
-            q.qv = g.qv[cur].p;
-            q.qdeg = g.qdeg[cur].p;
-            q.qbeg = g.qbeg[cur].p;
-            q.rv = w.rv.p;
-            q.rdeg = w.rdeg.p;
-            q.rbeg = w.rbeg.p;
-            q.far = w.far[1 - fcur].p;
-            PJ_HIP(hipMemsetAsync(dcnt, 0, sizeof(DCnt), s));
-            d_split_k<Off><<<grid_for((i64)nf, DB, maxgrid), DB, 0, s>>>(w.far[fcur].p, nf, row, w.lsplit.p, g.dist.p,
-                                                                         old_thr, thr, q, dcnt);
-            PJ_LAUNCH_CHECK();
-            PJ_HIP(hipMemcpyAsync(hcnt, dcnt, sizeof(DCnt), hipMemcpyDeviceToHost, s));
-            PJ_HIP(hipStreamSynchronize(s));
-            nq = hcnt->n_near;
-            mq = hcnt->m_near;
-            nf = hcnt->n_far;
-            nr = hcnt->n_r;
-            mr = hcnt->m_r;
-            fcur = 1 - fcur;
+            // near phase: the members' light edges, cascades relaxed in-workgroup
+            if (t.nl > 0) relax(SEL_DIST_L, t, hi);
+            // heavy pass over the final members; deferred vertices (worklist
+            // overflow, long light rows) first get BITS rounds of their own
+            for (;;) {
+                t = select(SEL_DIST_H, (int32_t)lo, hi);
+                if (!t.overflow) break;
+                DTot b = select(SEL_BITS, (int32_t)lo, hi);
+                while (b.nl > 0) {
+                    relax(SEL_BITS, b, hi);
+                    b = select(SEL_BITS, (int32_t)lo, hi);
+                }
+            }
+            if (t.nh > 0) relax(SEL_DIST_H, t, hi);
+            lo = hi;
         }
     }
     PJ_HIP(hipEventRecord(g.ev1, s));
@@ -418,31 +595,29 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
 
 void delta_solve(Graph& g, i64 source) {
     const size_t n = (size_t)g.n;
+    const size_t nwords = (n + 63) / 64;
     g.dist.ensure(n ? n : 1);
-    for (int i = 0; i < 2; ++i) {
-        g.qv[i].ensure(n ? n : 1);
-        g.qdeg[i].ensure(n ? n : 1);
-        g.qbeg[i].ensure(n ? n : 1);
-    }
-    g.qoff.ensure(n + 1);
-    g.scan.ensure((i64)n);
-    g.counters.ensure(16);
-    if (!g.hcounters.p) g.hcounters.alloc(16);
     if (!g.ev0) PJ_HIP(hipEventCreate(&g.ev0));
     if (!g.ev1) PJ_HIP(hipEventCreate(&g.ev1));
     if (!g.delta_work) {
         g.delta_work.reset(new DeltaWork());
         DeltaWork& w = *g.delta_work;
         const size_t m = n ? n : 1;
-        w.st_near.alloc(m);
-        w.st_band.alloc(m);
-        w.st_far.alloc(m);
-        w.far[0].alloc(m);  // each epoch appends every vertex at most once
-        w.far[1].alloc(m);
-        w.rv.alloc(m);  // each band appends every vertex at most once
-        w.rdeg.alloc(m);
-        w.rbeg.alloc(m);
+        const size_t nwaves = (nwords + WPW - 1) / WPW + 1;
+        w.chg.alloc(nwords ? nwords : 1);
+        w.sel.alloc(nwords ? nwords : 1);
+        w.qvl.alloc(m);
+        w.qvh.alloc(m);
+        w.qbl.alloc(m);
+        w.qbh.alloc(m);
+        w.qol.alloc(m + 1);
+        w.qoh.alloc(m + 1);
+        w.part.alloc(6 * nwaves);
+        w.boff.alloc(4 * nwaves);
+        w.tot.alloc(1);
+        w.flag.alloc(1);
         w.lsplit.alloc(m);
+        PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.host), sizeof(DTot), hipHostMallocMapped));
     }
     if (g.mean_weight < 0.0) {
         u64 sum = 0;

@@ -155,6 +155,28 @@ def test_weighted_delta_stepping(ctx, oracle):
         g.close()
 
 
+def test_weighted_deferral_paths(ctx, oracle):
+    """In-band vertices that a relax workgroup cannot finish itself: a row longer
+    than LOCAL_MAX (4096) reached by a light edge, and more in-band improvements
+    than the LDS worklist holds (2048). Both go through the `chg` bitmap and the
+    follow-up rounds of delta.hip."""
+    rng = np.random.default_rng(5)
+    fan = 9000
+    leaves = np.arange(2, 2 + fan)
+    nxt = 2 + fan + rng.integers(0, 3000, fan)
+    src = np.concatenate([[0], np.ones(fan, np.int64), leaves, nxt[:500]])
+    dst = np.concatenate([[1], leaves, nxt, rng.integers(0, 2 + fan + 3000, 500)])
+    n = 2 + fan + 3000
+    for wmax in (1, 4):
+        w = rng.integers(0, wmax, len(src)).astype(np.uint32)
+        g = ctx.load_coo(src, dst, w=w, n=n)
+        row, col, wc = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n, w)
+        for delta in (0, 8, 1000):
+            g.set_option("delta", delta)
+            assert (g.sssp(0) == oracle.dijkstra(row, col, wc, 0)).all(), (wmax, delta)
+        g.close()
+
+
 def test_weighted_text_and_kronecker(ctx, oracle):
     text = b"0 1 5\n0 2 1\n2 1 1\n1 3 99999\n3 4 1\n2 4 200000\n"
     g = ctx.load_snap_buffer(text, weighted=True)

@@ -1,0 +1,16 @@
+"""Fixed SSSP workload for rocprofv3 --pmc passes (HBM traffic per solve).
+Runs SOLVES unit-weight solves on Kronecker s{scale}; every bfs_* dispatch belongs to a solve.
+Usage: python tools/traffic_probe.py [scale] [solves]"""
+import os, sys
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, R)
+import paralleljohnson_amd as pj
+
+scale = int(sys.argv[1]) if len(sys.argv) > 1 else 22
+solves = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+ctx = pj.Context(0)
+g = ctx.generate_kronecker(scale, 16, 1)
+roots = g.sample_roots(2, solves)
+for r in roots:
+    g.sssp(int(r), copy=False)
+print(f"traffic_probe scale {scale} solves {len(roots)} roots {list(map(int, roots))}", flush=True)
