@@ -412,6 +412,15 @@ __global__ __launch_bounds__(DB) void d_relax_k(const u32* __restrict__ iv, cons
 
 __global__ void d_source_k(i64 s, int32_t* __restrict__ dist) { dist[s] = 0; }
 
+// distances back to input ids: out[v] = dist'[inv[v]] (INT_INF past n_scan)
+__global__ void unlabel_k(const u32* __restrict__ inv, const int32_t* __restrict__ dl, i64 n, i64 n_scan,
+                          int32_t* __restrict__ out) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
+        const u32 x = inv[v];
+        out[v] = (i64)x < n_scan ? dl[x] : INT_INF;
+    }
+}
+
 // lsplit[v] = number of edges of v with weight < delta (rows are weight-sorted)
 template <typename Off>
 __global__ void light_split_k(const Off* __restrict__ row, const u32* __restrict__ w, i64 n, u32 delta,
@@ -460,21 +469,23 @@ template <typename Off>
 void delta_run(Graph& g, DeltaWork& w, i64 source) {
     Ctx& ctx = *g.ctx;
     hipStream_t s = ctx.stream;
-    const i64 n = g.n;
+    Relabeled& R = *g.rl;
+    const i64 n = R.n_scan;  // the solver works on the relabeled vertices with edges
     const i64 nwords = (n + 63) / 64;
-    const Off* row = static_cast<const Off*>(g.row_ptr());
+    const Off* row = static_cast<const Off*>(R.row_ptr(g.off64));
     const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
 
-    // delta: explicit option, else (mean weight / mean out-degree) * 4 — light
-    // edges are then a small fraction of each row (tuned on Kronecker)
+    // delta: explicit option, else 6 * mean weight / mean out-degree (over all
+    // input ids) — light edges are then ~10% of a row. Swept on Kronecker s22 and
+    // s26 with weights 1..255 (profiles/r01/delta_sweep.txt): flat from 24 to 48.
     int32_t delta = (int32_t)g.delta;
     if (delta <= 0) {
-        const double mean_deg = n ? (double)g.nnz / (double)n : 1.0;
-        const double d = 4.0 * g.mean_weight / std::max(1.0, mean_deg);
+        const double mean_deg = g.n ? (double)g.nnz / (double)g.n : 1.0;
+        const double d = 6.0 * g.mean_weight / std::max(1.0, mean_deg);
         delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(d)));
     }
     if (w.lsplit_delta != (u32)delta && n > 0) {
-        light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, g.w.p, n, (u32)delta, w.lsplit.p);
+        light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)delta, w.lsplit.p);
         PJ_LAUNCH_CHECK();
         w.lsplit_delta = (u32)delta;
     }
@@ -483,7 +494,7 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
     a.n = n;
     a.nwords = nwords;
     a.nwaves = (nwords + WPW - 1) / WPW;
-    a.dist = g.dist.p;
+    a.dist = R.dist.p;
     a.lsplit = w.lsplit.p;
     a.chg = w.chg.p;
     a.sel = w.sel.p;
@@ -530,15 +541,15 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
         PJ_LAUNCH_CHECK();
         if (t.ml > 0) {
             const unsigned grid = grid_for((i64)((t.ml + D_TILE - 1) / D_TILE), 1, maxgrid);
-            d_relax_k<Off, true><<<grid, DB, 0, s>>>(w.qvl.p, w.qbl.p, w.qol.p, w.tot.p, row, w.lsplit.p, g.col.p,
-                                                     g.w.p, g.dist.p, hi, w.chg.p, w.flag.p);
+            d_relax_k<Off, true><<<grid, DB, 0, s>>>(w.qvl.p, w.qbl.p, w.qol.p, w.tot.p, row, w.lsplit.p, R.col.p,
+                                                     R.w.p, R.dist.p, hi, w.chg.p, w.flag.p);
             PJ_LAUNCH_CHECK();
             st.relax_rounds++;
         }
         if (t.mh > 0) {
             const unsigned grid = grid_for((i64)((t.mh + D_TILE - 1) / D_TILE), 1, maxgrid);
             d_relax_k<Off, false><<<grid, DB, 0, s>>>(w.qvh.p, w.qbh.p, w.qoh.p, w.tot.p, row, w.lsplit.p,
-                                                      g.col.p, g.w.p, g.dist.p, hi, w.chg.p, w.flag.p);
+                                                      R.col.p, R.w.p, R.dist.p, hi, w.chg.p, w.flag.p);
             PJ_LAUNCH_CHECK();
             st.relax_rounds++;
         }
@@ -546,13 +557,15 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
 
     auto t_host0 = std::chrono::steady_clock::now();
     PJ_HIP(hipEventRecord(g.ev0, s));
+    const bool valid = source >= 0 && source < g.n;
+    const i64 ls = valid ? (i64)R.inv_h[(size_t)source] : -1;  // the source's new id
     if (n > 0) {
-        PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.dist.p), INT_INF, (size_t)n, s));
+        PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(R.dist.p), INT_INF, (size_t)n, s));
         PJ_HIP(hipMemsetAsync(w.chg.p, 0, sizeof(u64) * (size_t)nwords, s));
         PJ_HIP(hipMemsetAsync(w.flag.p, 0, sizeof(u32), s));
     }
-    if (source >= 0 && source < n) {
-        d_source_k<<<1, 1, 0, s>>>(source, g.dist.p);
+    if (valid && ls < n) {
+        d_source_k<<<1, 1, 0, s>>>(ls, R.dist.p);
         PJ_LAUNCH_CHECK();
         long long lo = 0;
         while (lo < INT_INF) {
@@ -581,6 +594,11 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
             lo = hi;
         }
     }
+    if (g.n > 0) {
+        unlabel_k<<<grid_for(g.n, 256, maxgrid), 256, 0, s>>>(R.inv.p, R.dist.p, g.n, n, g.dist.p);
+        PJ_LAUNCH_CHECK();
+        if (valid && ls >= n) d_source_k<<<1, 1, 0, s>>>(source, g.dist.p);  // a source without edges
+    }
     PJ_HIP(hipEventRecord(g.ev1, s));
     PJ_HIP(hipEventSynchronize(g.ev1));
     float ms = 0.f;
@@ -599,6 +617,10 @@ void delta_solve(Graph& g, i64 source) {
     g.dist.ensure(n ? n : 1);
     if (!g.ev0) PJ_HIP(hipEventCreate(&g.ev0));
     if (!g.ev1) PJ_HIP(hipEventCreate(&g.ev1));
+    if (!g.rl) {
+        build_relabeled(g);
+        g.delta_work.reset();
+    }
     if (!g.delta_work) {
         g.delta_work.reset(new DeltaWork());
         DeltaWork& w = *g.delta_work;

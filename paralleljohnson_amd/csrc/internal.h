@@ -140,6 +140,21 @@ struct DeltaWorkDeleter {
     void operator()(DeltaWork* p) const { delete_delta_work(p); }
 };
 
+// Degree-ordered copy of a graph for the weighted solver (relabel.hip): new
+// ids put vertices with in- or out-edges first, by out-degree descending, so
+// the distance entries the relaxations hit are dense and the hot ones share
+// cache lines. Rows keep their edge order (weight-sorted).
+struct Relabeled {
+    i64 n_scan = 0;           // vertices with any edge: new ids [0, n_scan)
+    DevBuf<u32> perm, inv;    // new -> old, old -> new
+    std::vector<u32> inv_h;   // host copy of inv (source lookup)
+    DevBuf<u32> row32;
+    DevBuf<u64> row64;
+    DevBuf<u32> col, w;
+    DevBuf<int32_t> dist;     // solver distances in new ids
+    const void* row_ptr(bool off64) const { return off64 ? (const void*)row64.p : (const void*)row32.p; }
+};
+
 struct Graph {
     Ctx* ctx = nullptr;
     i64 n = 0, nnz = 0;
@@ -165,6 +180,7 @@ struct Graph {
     std::unique_ptr<MsWork, MsWorkDeleter> ms_work;
     std::unique_ptr<DeltaWork, DeltaWorkDeleter> delta_work;
     double mean_weight = -1.0;  // weighted: computed on first delta solve
+    std::unique_ptr<Relabeled> rl;  // weighted: built on the first delta solve
 
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;
@@ -188,6 +204,9 @@ struct Graph {
 
 // Build CSR (+CSC unless symmetric) from device COO (consumed: buffers are
 // used as sort scratch). n must already be known.
+// Builds g.rl from g's CSR (weighted graphs).
+void build_relabeled(Graph& g);
+
 void build_graph_from_coo(Graph& g, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>* w, i64 nnz,
                           i64 n, bool symmetric);
 
