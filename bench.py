@@ -1,19 +1,28 @@
 #!/usr/bin/env python3
-"""Benchmark: unit-weight SSSP on Graph500 Kronecker s22/ef16 (BASELINE.json configs[1]).
+"""Benchmark of the relaxation hot path (BASELINE.json metric: "GTEPS + time-to-solution,
+SSSP web-Google & Graph500 s26, 1/2/4/8 GPUs").
 
-One step = one SSSP (dist init -> distances final on the device) from one root
-over the HBM-resident graph. Multi-GPU (torchrun, one process per GPU): the
-graph is replicated and the roots are sharded across ranks (Graph500-style
-source sharding, no data-path collective) -> weak scaling.
+Main workload (the `value` of the JSON line): BASELINE.json configs[2], Graph500
+Kronecker scale 26, edgefactor 16 (2^31 directed CSR entries, both directions),
+integer weights 1..255, SSSP by delta-stepping, single GPU resident. One step =
+one SSSP (dist init -> distances final in input ids on the device) from one root.
+Multi-GPU (torchrun, one process per GPU): the graph is replicated and the roots
+are sharded across ranks (Graph500-style source sharding, no data-path
+collective) -> weak scaling.
 
-Prints ONE JSON line (rank 0):
-  value    = GTEPS = sum over ranks of m_r (edges of the reached component,
-             Graph500 TEPS convention over directed CSR entries) / max-over-ranks time
-  roofline = algorithmic bytes per SSSP (SURVEY.md §8d:
-             B = 4N + n_r(12 + 2*O) + m_r(8 + 4*weighted)) / the solve's device
-             time measured with HIP events on libpj's stream
-  cpu_baseline = the reference's BSP heap algorithm (oracle port, host threads)
-             on a bounded sample of the same roots, rank 0 at N=1 only
+At N=1 the same line also carries `secondary` results: configs[1] (Kronecker s22
+unit weights, direction-optimizing BFS) and configs[0] (web-Google-shaped
+synthetic, source 0). Inputs are generated on the device (no dataset access).
+
+  value        = GTEPS = sum over ranks of m_r / max-over-ranks wall time of the
+                 timed steps; m_r = CSR entries of the reached vertices
+                 (Graph500 TEPS over directed entries; gteps_graph500 = value / 2)
+  roofline     = SURVEY.md §8d algorithmic bytes per SSSP
+                 B = 4N + n_r(12 + 2*O) + m_r(8 + 4*weighted) divided by the
+                 solve's device time (HIP events on libpj's stream)
+  cpu_baseline = the reference's BSP heap algorithm (oracle port of :466-594,
+                 weights honoured) on host threads, rank 0 at N=1 only, on a
+                 bounded sample of one solve of the same graph
 """
 import argparse
 import json
@@ -29,24 +38,78 @@ sys.path.insert(0, ROOT)
 METRIC = "GTEPS + time-to-solution, SSSP web-Google & Graph500 s26, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
+WORKLOADS = {
+    "k26w": dict(kind="kronecker", scale=26, weighted=True,
+                 name="graph500-kronecker-s26-ef16-w1..255-delta-stepping-sssp"),
+    "k22": dict(kind="kronecker", scale=22, weighted=False, name="graph500-kronecker-s22-ef16-unit-sssp"),
+    "wg": dict(kind="webgraph", weighted=False, name="web-google-shaped-synthetic-unit-sssp-source0"),
+}
+
 
 def algorithmic_bytes(n, n_r, m_r, nnz, weighted=False):
     o = 4 if nnz < 2**31 else 8
     return 4 * n + n_r * (12 + 2 * o) + m_r * (8 + 4 * int(weighted))
 
 
+def make_graph(ctx, wl, args):
+    if wl["kind"] == "webgraph":
+        return ctx.generate_webgraph(seed=args.seed)
+    scale = args.scale if args.scale else wl["scale"]
+    return ctx.generate_kronecker(scale, args.edgefactor, args.seed, weighted=wl["weighted"])
+
+
+def run_workload(ctx, key, args, rank, world, barrier, steps, warmup):
+    """Timed SSSPs of one workload on this rank; returns per-rank sums."""
+    import paralleljohnson_amd as pj  # noqa: F401
+    wl = WORKLOADS[key]
+    t_gen = time.perf_counter()
+    g = make_graph(ctx, wl, args)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        g.set_option(k, float(v))
+    if wl["kind"] == "webgraph":
+        roots = [0]  # configs[0]: source 0
+    else:
+        roots = [int(r) for r in g.sample_roots(args.seed + 1, 64)]
+    my_roots = [roots[(rank + world * k) % len(roots)] for k in range(max(steps, 1))]
+    g.sssp(my_roots[0], copy=False)  # first solve builds the solver workspace (untimed)
+    gen_s = time.perf_counter() - t_gen
+    for k in range(warmup):
+        g.sssp(my_roots[k % len(my_roots)], copy=False)
+    kernel_ms = []
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        g.sssp(my_roots[k], copy=False)
+        kernel_ms.append(g.stats()["kernel_ms"])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    reach, levels = {}, {}
+    for r in set(my_roots):  # untimed: reached-component statistics per root
+        g.sssp(r, copy=False)
+        st = g.reach_stats()
+        reach[r] = (st["reached"], st["reached_edges"])
+        levels[r] = (st["levels"], st["td_levels"], st["bu_levels"], st["relax_rounds"])
+    m_sum = float(sum(reach[r][1] for r in my_roots[:steps]))
+    b_sum = float(sum(algorithmic_bytes(g.n, reach[r][0], reach[r][1], g.nnz, wl["weighted"])
+                      for r in my_roots[:steps]))
+    return dict(g=g, wl=wl, elapsed=elapsed, m_sum=m_sum, b_sum=b_sum, t_kernel=sum(kernel_ms) / 1000.0,
+                roots=my_roots[:steps], reach=reach, levels=levels, gen_s=gen_s)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
-    ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--scale", type=int, default=22)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="k26w", choices=sorted(WORKLOADS))
+    ap.add_argument("--scale", type=int, default=0, help="override the Kronecker scale (testing only)")
     ap.add_argument("--edgefactor", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_s22.json"))
+    ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--opt", action="append", default=[], help="libpj graph option key=value (tuning)")
     args = ap.parse_args()
 
@@ -63,70 +126,61 @@ def main():
 
     import paralleljohnson_amd as pj
 
-    ctx = pj.Context(local)
-    g = ctx.generate_kronecker(args.scale, args.edgefactor, args.seed)
-    for kv in args.opt:
-        k, v = kv.split("=")
-        g.set_option(k, float(v))
-    n_roots = 64
-    roots = g.sample_roots(args.seed + 1, n_roots)
-    # weak scaling: rank r takes roots r, r+world, ... (distinct roots per rank)
-    my_roots = [int(roots[(rank + world * k) % len(roots)]) for k in range(args.steps)]
-
-    for k in range(args.warmup):
-        g.sssp(my_roots[k % len(my_roots)], copy=False)
-
     def barrier():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
-    kernel_ms = []
-    barrier()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        g.sssp(my_roots[k], copy=False)
-        kernel_ms.append(g.stats()["kernel_ms"])
-    barrier()
-    elapsed = time.perf_counter() - t0
-
-    # untimed: reached-component statistics per root (m_r, n_r)
-    reach = {}
-    levels = {}
-    for r in set(my_roots):
-        g.sssp(r, copy=False)
-        st = g.reach_stats()
-        reach[r] = (st["reached"], st["reached_edges"])
-        levels[r] = (st["td_levels"], st["bu_levels"])
-    m_sum = float(sum(reach[r][1] for r in my_roots))
-    b_sum = float(sum(algorithmic_bytes(g.n, reach[r][0], reach[r][1], g.nnz) for r in my_roots))
-    t_kernel_sum = sum(kernel_ms) / 1000.0
-
+    ctx = pj.Context(local)
+    main_res = run_workload(ctx, args.workload, args, rank, world, barrier, args.steps, args.warmup)
+    elapsed, m_sum, b_sum, t_kernel = main_res["elapsed"], main_res["m_sum"], main_res["b_sum"], main_res["t_kernel"]
     if dist is not None:
-        t = torch.tensor([elapsed, m_sum, b_sum, t_kernel_sum], dtype=torch.float64, device="cuda")
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        t = torch.tensor([elapsed, m_sum, b_sum, t_kernel], dtype=torch.float64, device="cuda")
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
-        m_sum, b_sum, t_kernel_sum = float(t[1]), float(t[2]), float(t[3])
-
+        m_sum, b_sum, t_kernel = float(t[1]), float(t[2]), float(t[3])
+    wl = main_res["wl"]
+    g = main_res["g"]
     value = m_sum / elapsed / 1e9
-    achieved = b_sum / t_kernel_sum / 1e9  # GB/s, per-solve algorithmic bytes / device time
+    achieved = b_sum / t_kernel / 1e9  # GB/s: algorithmic bytes per solve / device time per solve
 
     traffic = None
-    if os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        if tj.get("scale") == args.scale and tj.get("edgefactor") == args.edgefactor:
-            traffic = tj.get("hbm_bytes_per_sssp")
+    tj_path = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
+    if os.path.exists(tj_path) and not args.scale:
+        with open(tj_path) as f:
+            traffic = json.load(f).get("hbm_bytes_per_sssp")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(g, my_roots, reach, args)
+        cpu = cpu_baseline(g, main_res, args)
+    n_vertices, nnz = g.n, g.nnz
+    r0 = main_res["roots"][0]
+    g.close()
+
+    secondary = {}
+    if world == 1 and not args.no_secondary and not args.scale:
+        for key in ("k22", "wg"):
+            if key == args.workload:
+                continue
+            res = run_workload(ctx, key, args, 0, 1, barrier, 8, 2)
+            gg, rr = res["g"], res["roots"][0]
+            secondary[key] = {
+                "workload": res["wl"]["name"], "n_vertices": gg.n, "nnz": gg.nnz,
+                "gteps": round(res["m_sum"] / res["elapsed"] / 1e9, 3),
+                "ms_per_sssp": round(1000.0 * res["elapsed"] / 8, 4),
+                "kernel_ms_mean": round(1000.0 * res["t_kernel"] / 8, 4),
+                "hbm_frac_algorithmic": round(res["b_sum"] / res["t_kernel"] / 1e9 / HBM_PEAK_GBS, 4),
+                "reached": res["reach"][rr][0], "m_r": res["reach"][rr][1],
+                "levels_td_bu": list(res["levels"][rr][1:3]),
+            }
+            gg.close()
 
     if rank == 0:
         mean_ms = 1000.0 * elapsed / args.steps
+        lv = main_res["levels"][r0]
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -139,17 +193,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": f"synthetic: Graph500 Kronecker (A,B,C=0.57,0.19,0.19) scale {args.scale} edgefactor "
-                    f"{args.edgefactor}, both directions, on-GPU generator seed {args.seed}",
+            "data": (f"synthetic: Graph500 Kronecker (A,B,C=0.57,0.19,0.19) generated on the device, seed "
+                     f"{args.seed}, both directions" + (", weights 1 + hash mod 255" if wl["weighted"] else "")
+                     if wl["kind"] == "kronecker" else "synthetic web-Google-shaped graph (SNAP file absent)"),
             "config": {
-                "workload": f"graph500-kronecker-s{args.scale}-ef{args.edgefactor}-unit-sssp",
-                "n_vertices": g.n, "nnz": g.nnz, "roots_per_rank": args.steps,
+                "workload": wl["name"] if not args.scale else f"{wl['name']} (scale override {args.scale})",
+                "n_vertices": n_vertices, "nnz": nnz, "roots_per_rank": args.steps,
                 "parallelism": f"source-sharded x{world} (graph replicated, no data-path collective)",
             },
             "gteps_graph500": round(value / 2, 3),
             "time_to_solution_ms": round(mean_ms, 4),
-            "kernel_ms_mean": round(1000.0 * t_kernel_sum / (args.steps * world), 4),
-            "levels_td_bu": levels[my_roots[0]],
+            "kernel_ms_mean": round(1000.0 * t_kernel / (args.steps * world), 4),
+            "bands_or_levels": lv[0], "relax_launches": lv[3],
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -157,43 +212,45 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "scope": "whole SSSP solve (all frontier kernels of one root); "
-                         "bytes = SURVEY.md §8d algorithmic bytes",
+                "scope": "one launch = one SSSP solve (every kernel of the solve); bytes = SURVEY.md §8d "
+                         "algorithmic bytes; time = HIP events on libpj's stream; traffic = PMC "
+                         "2*FETCH_SIZE + WRITE_SIZE per solve (profiles/)",
             },
             "cpu_baseline": cpu,
+            "secondary": secondary or None,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
-def cpu_baseline(g, my_roots, reach, args):
-    """The reference algorithm (oracle port of :466-594) on host threads, bounded sample."""
+def cpu_baseline(g, res, args):
+    """The reference algorithm (oracle port of :466-594) on host threads, bounded sample of one solve."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # cpu_baseline leg only
 
     O.build()
-    row, col, _ = g.get_csr()
+    row, col, w = g.get_csr()
     col = col.view(np.uint32)
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    t_sum, m_sum, done = 0.0, 0, []
-    t_start = time.perf_counter()
-    for r in dict.fromkeys(my_roots):
-        dist, st = O.reference_sssp(row, col, r, threads)
-        t_sum += st.solve_s
-        m_sum += reach[r][1]
-        done.append(r)
-        if time.perf_counter() - t_start > args.cpu_seconds:
-            break
+    r = res["roots"][0]
+    _, st = O.reference_sssp(row, col, r, threads, w=w, budget_s=args.cpu_seconds)
+    m_r = res["reach"][r][1]
+    if st.truncated:
+        rate = st.scans / st.solve_s
+        sample = (f"first {st.solve_s:.1f} s of one solve (root {r}) of the same graph, truncated at a round "
+                  f"boundary: {st.scans} CSR entries scanned in {st.rounds} BSP rounds; value = scans/s")
+    else:
+        rate = m_r / st.solve_s
+        sample = f"one full solve (root {r}) of the same graph in {st.solve_s:.2f} s; value = m_r/s"
+    del row, col, w
     return {
-        "value": round(m_sum / t_sum / 1e9, 4),
+        "value": round(rate / 1e9, 5),
         "unit": "GTEPS",
         "cores": threads,
         "kind": "port",
-        "sample": f"{len(done)} root(s) of the same s{args.scale} graph, reference BSP heap algorithm "
-                  f"(30 pops/round, {threads} partitions on {threads} host threads), solve time only "
-                  f"({t_sum:.2f} s)",
-        "ms_per_sssp": round(1000.0 * t_sum / len(done), 2),
+        "sample": sample + f"; reference BSP heap algorithm, 30 pops/round, {threads} partitions on "
+                           f"{threads} host threads",
     }
 
 

@@ -44,6 +44,8 @@ def lib():
         L.pjo_dijkstra.restype = None
         L.pjo_reference_sssp.argtypes = [P, P, P, i64, i64, ctypes.c_int, P, P]
         L.pjo_reference_sssp.restype = ctypes.c_int
+        L.pjo_reference_sssp_budget.argtypes = [P, P, P, i64, i64, ctypes.c_int, ctypes.c_double, P, P]
+        L.pjo_reference_sssp_budget.restype = ctypes.c_int
         L.pjo_format_sol.argtypes = [P, i64, P]
         L.pjo_format_sol.restype = i64
         L.pjo_kronecker.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, P, P, P]
@@ -117,17 +119,20 @@ def dijkstra(row, col, w, source):
 class RefStats(ctypes.Structure):
     _fields_ = [("solve_s", ctypes.c_double), ("rounds", ctypes.c_int64), ("pops", ctypes.c_int64),
                 ("scans", ctypes.c_int64), ("decreases", ctypes.c_int64),
-                ("reinserts", ctypes.c_int64), ("messages", ctypes.c_int64)]
+                ("reinserts", ctypes.c_int64), ("messages", ctypes.c_int64), ("truncated", ctypes.c_int64)]
 
 
-def reference_sssp(row, col, source, nproc=1, w=None):
-    """The reference's BSP heap algorithm (:466-594) on nproc host threads."""
+def reference_sssp(row, col, source, nproc=1, w=None, budget_s=0.0):
+    """The reference's BSP heap algorithm (:466-594) on nproc host threads.
+    budget_s > 0 stops it at the first round boundary after that much solve time
+    (st.truncated = 1, dist incomplete): the bounded CPU-baseline sample."""
     n = len(row) - 1
     dist = np.zeros(max(n, 1), np.int32)
     st = RefStats()
     wa = None if w is None else np.ascontiguousarray(w, np.uint32)
-    rc = lib().pjo_reference_sssp(_p(row), _p(np.ascontiguousarray(col, np.uint32)), _p(wa), n,
-                                  int(source), int(nproc), _p(dist), ctypes.byref(st))
+    rc = lib().pjo_reference_sssp_budget(_p(row), _p(np.ascontiguousarray(col, np.uint32)), _p(wa), n,
+                                         int(source), int(nproc), ctypes.c_double(budget_s), _p(dist),
+                                         ctypes.byref(st))
     if rc != 0:
         raise ValueError("nproc out of range")
     return dist[:n], st

@@ -274,6 +274,8 @@ typedef struct {
     pthread_barrier_t bar;
     pjo_ref_stats st[64];
     double t0, t1;
+    double budget_s;        /* > 0: stop after this much solve time (bounded CPU-baseline sample) */
+    int stop;
 } ref_shared;
 
 typedef struct { ref_shared* sh; int rank; } ref_arg;
@@ -345,10 +347,11 @@ static void* ref_rank(void* p) {
             for (int64_t j = 0; j < b->n; j++) relax_local(&h, S->sp, start, b->m[j].v, b->m[j].d, st);
         }
         S->flags[rank] = (h.n > 0 && h.key[0] != PJO_INT_INF) ? 1 : 0; /* :579-588 */
+        if (rank == 0 && S->budget_s > 0 && now_s() - S->t0 > S->budget_s) S->stop = 1;
         pthread_barrier_wait(&S->bar); /* MPI_Allreduce :589-590 */
         int total = 0;
         for (int r = 0; r < P; r++) total += S->flags[r];
-        if (total == 0) break;
+        if (total == 0 || S->stop) break;
         pthread_barrier_wait(&S->bar); /* keep flags stable until every rank has summed */
     }
     pthread_barrier_wait(&S->bar); /* :597 */
@@ -359,8 +362,15 @@ static void* ref_rank(void* p) {
 
 int pjo_reference_sssp(const int64_t* row_ptr, const uint32_t* col, const uint32_t* w, int64_t n,
                        int64_t source, int nproc, int32_t* dist, pjo_ref_stats* stats) {
+    return pjo_reference_sssp_budget(row_ptr, col, w, n, source, nproc, 0.0, dist, stats);
+}
+
+int pjo_reference_sssp_budget(const int64_t* row_ptr, const uint32_t* col, const uint32_t* w, int64_t n,
+                              int64_t source, int nproc, double budget_s, int32_t* dist,
+                              pjo_ref_stats* stats) {
     if (nproc < 1 || nproc > 64) return -1;
     ref_shared* S = (ref_shared*)calloc(1, sizeof(ref_shared));
+    S->budget_s = budget_s;
     S->row_ptr = row_ptr; S->col = col; S->w = w; S->n = n; S->source = source; S->nproc = nproc;
     S->sp = dist; /* MPI_Gatherv :612 is implicit: the slices are written in place */
     S->out = (mbuf*)calloc((size_t)nproc * nproc, sizeof(mbuf));
@@ -376,6 +386,7 @@ int pjo_reference_sssp(const int64_t* row_ptr, const uint32_t* col, const uint32
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->solve_s = S->t1 - S->t0;
+        stats->truncated = S->stop;
         for (int r = 0; r < nproc; r++) {
             if (S->st[r].rounds > stats->rounds) stats->rounds = S->st[r].rounds;
             stats->pops += S->st[r].pops; stats->scans += S->st[r].scans;

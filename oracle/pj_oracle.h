@@ -53,6 +53,7 @@ typedef struct pjo_ref_stats {
     int64_t decreases;   /* decrease-key calls (:254, :564) */
     int64_t reinserts;   /* label-correcting re-pushes (:261, :570) */
     int64_t messages;    /* (v, d) pairs exchanged (:553) */
+    int64_t truncated;   /* 1 if the budget stopped the solve early (dist incomplete) */
 } pjo_ref_stats;
 
 /* The reference algorithm itself (:466-594): 1D contiguous vertex blocks
@@ -63,6 +64,12 @@ typedef struct pjo_ref_stats {
  * reference's unit weight (:147). */
 int pjo_reference_sssp(const int64_t* row_ptr, const uint32_t* col, const uint32_t* w, int64_t n,
                        int64_t source, int nproc, int32_t* dist, pjo_ref_stats* stats);
+/* Same, stopped at the first round boundary after budget_s seconds of solve
+ * time (budget_s <= 0: no limit). Used only for the bounded CPU-baseline
+ * sample of bench.py: the scan rate of the truncated run is what is reported. */
+int pjo_reference_sssp_budget(const int64_t* row_ptr, const uint32_t* col, const uint32_t* w, int64_t n,
+                              int64_t source, int nproc, double budget_s, int32_t* dist,
+                              pjo_ref_stats* stats);
 
 /* output_vector :32-46. Returns the byte length; buf == NULL only measures. */
 int64_t pjo_format_sol(const int32_t* dist, int64_t n, char* buf);

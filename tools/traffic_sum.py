@@ -1,21 +1,23 @@
-"""Sum rocprofv3 --pmc counters over the dispatches of kernels matching PATTERN, per solve.
-Usage: python tools/traffic_sum.py OUTDIR PATTERN SOLVES > json
+"""Sum rocprofv3 --pmc counters over the dispatches of kernels matching any PATTERN, per solve.
+Usage: python tools/traffic_sum.py OUTDIR SOLVES PATTERN [PATTERN...] > json
 OUTDIR holds one sub-directory per pass (each with *counter_collection.csv)."""
 import csv, glob, json, os, sys
 from collections import defaultdict
-root, pat, solves = sys.argv[1], sys.argv[2], int(sys.argv[3])
+root, solves, pats = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
 tot = defaultdict(float)
 disp = defaultdict(set)
 for p in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(p)):
-        if pat not in r["Kernel_Name"]:
+        if not any(pt in r["Kernel_Name"] for pt in pats):
             continue
         tot[r["Counter_Name"]] += float(r["Counter_Value"])
         disp[r["Counter_Name"]].add(r["Dispatch_Id"])
 res = {k: v / solves for k, v in tot.items()}
-res["dispatches"] = {k: len(v) for k, v in disp.items()}
+res["dispatches_per_solve"] = {k: len(v) / solves for k, v in disp.items()}
+res["patterns"] = pats
 # MI355X_MICROARCH.md §HBM: FETCH_SIZE (kB) reports 1/2 of wide streaming reads on gfx950 -> x2;
-# WRITE_SIZE (kB) is exact for streaming stores.
+# WRITE_SIZE (kB) is exact for streaming stores. Random 4-byte gathers are uncalibrated: the
+# uncorrected sum is kept beside the corrected one.
 if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
     res["hbm_bytes_per_sssp"] = 1024.0 * (2.0 * res["FETCH_SIZE"] + res["WRITE_SIZE"])
     res["hbm_bytes_per_sssp_uncorrected"] = 1024.0 * (res["FETCH_SIZE"] + res["WRITE_SIZE"])
