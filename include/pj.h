@@ -146,6 +146,84 @@ int pj_reach_stats(pj_graph* g, pj_stats* out);
  * delta-stepping (0 = automatic). Returns PJ_ERR_ARG on bad values. */
 int pj_set_option(pj_graph* g, const char* key, double value);
 
+/* ---- stream ---------------------------------------------------------------- */
+
+/* Launch all later work of ctx on `stream` (a hipStream_t of the same device,
+ * e.g. torch's current stream, so that libpj kernels and RCCL collectives are
+ * ordered without host synchronisation). NULL restores the ctx's own stream.
+ * The caller keeps ownership of an external stream. */
+int pj_set_stream(pj_ctx* ctx, void* stream);
+
+/* ---- 1D vertex partition: one process per GPU -------------
+ *
+ * Replaces the reference's block distribution nn2rank / get_start_nn
+ * (ParallelJohnson.cpp:169-200) and the row scatter :344-410: rank r of world
+ * keeps the out-rows (and, for non-symmetric graphs, the in-rows) of the
+ * vertex block [lo, hi), lo = r * block, block = ceil(N / world) rounded up
+ * to a multiple of 64 (so ranks never share a 64-bit visited word). Column
+ * ids stay global. The level loop and the exchange are driven by the caller
+ * (paralleljohnson_amd/partition.py, torch.distributed over RCCL), which
+ * replaces the reference's per-round MPI_Alltoall(v) and MPI_Allreduce
+ * (:522-554, :589-590):
+ *
+ *   stats = pj_part_begin(source)                     (level 0 = {source})
+ *   while sum_ranks(stats.n_f) > 0:
+ *     push level:  pj_part_push -> counts[world]; all_to_all_single(ids);
+ *                  pj_part_apply(received ids)
+ *     pull level:  pj_part_pull (reads the exact global vis snapshot)
+ *     stats = pj_part_end_level; all_reduce(stats); all-gather vis slices
+ *                  before a pull level (and after one)
+ *
+ * `vis` (device, world * words_per_rank u64) is the caller-owned replicated
+ * visited bitmap of all vertices; slice r (words [r*wpr, (r+1)*wpr)) belongs
+ * to rank r. Distances are BFS hops (unit weights, the reference's w = 1,
+ * :147); no level assigns a distance >= PJ_INT_INF (the caller stops there). */
+typedef struct pj_part pj_part;
+
+typedef struct pj_part_info {
+    int64_t n;              /* vertices of the whole graph */
+    int64_t lo, hi;         /* owned block [lo, hi) */
+    int64_t block;          /* vertices per rank (multiple of 64) */
+    int64_t words_per_rank; /* block / 64: u64 words of one vis slice */
+    int64_t nnz_local;      /* out-edges of the owned block */
+    int64_t nnz_in_local;   /* in-edges of the owned block (== nnz_local if symmetric) */
+    int32_t rank, world, symmetric, off64;
+} pj_part_info;
+
+/* The rank's share of pj_generate_kronecker(scale, edgefactor, seed, unit
+ * weights): every rank enumerates the same tuples and keeps its rows. */
+int pj_part_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int rank, int world,
+                               pj_part** out);
+/* The rank's share of a host COO graph (file order kept inside rows, as
+ * coord2csr :143-149). n_vertices < 0 means max id + 1. symmetric != 0 promises
+ * the edge list equals its transpose (no in-rows are built). */
+int pj_part_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, int64_t nnz, int64_t n_vertices,
+                     int symmetric, int rank, int world, pj_part** out);
+int pj_part_destroy(pj_part* p);
+int pj_part_info_get(const pj_part* p, pj_part_info* out);
+/* Copy the rank's isolated-vertex mask (words_per_rank u64, device) to
+ * own_words; all-gathered once, it is the `iso` argument of pj_part_begin. */
+int pj_part_zmask(pj_part* p, uint64_t* own_words);
+/* Start a solve: dist := INF, vis := iso, then the source. stats[3] =
+ * (n_f, m_f, frontier vertices with out-edges) of level 0, this rank's share. */
+int pj_part_begin(pj_part* p, int64_t source, const uint64_t* iso, uint64_t* vis, int64_t* stats);
+/* Top-down expansion of level `level` (this rank's frontier). Owned targets are
+ * settled at distance level+1; the others are written to send (device,
+ * capacity world * block u32) owner-major, counts[world] (host) per owner. */
+int pj_part_push(pj_part* p, int level, uint64_t* vis, uint32_t* send, int64_t* counts);
+/* Settle the ids received for this rank after the exchange of a push level. */
+int pj_part_apply(pj_part* p, int level, uint64_t* vis, const uint32_t* recv, int64_t n_recv);
+/* Bottom-up step of level `level` over the owned block (vis = exact snapshot). */
+int pj_part_pull(pj_part* p, int level, uint64_t* vis);
+/* Close a level: the new frontier becomes current, the own vis slice is
+ * updated; stats[3] as in pj_part_begin. */
+int pj_part_end_level(pj_part* p, uint64_t* vis, int64_t* stats);
+/* out[2] = (reached vertices, their out-edge sum) of the owned block. */
+int pj_part_reach(pj_part* p, int64_t* out);
+/* The owned block's distances (hi - lo int32): to the host, or in place. */
+int pj_part_copy_dist(pj_part* p, int32_t* dist_out);
+const int32_t* pj_part_dist_device(pj_part* p);
+
 /* ---- output (replaces output_vector :32-46 + the write at :615-620) ------ */
 
 /* Write the sol_file: "the vector is:\n" then, for v = 0..n-1, the decimal

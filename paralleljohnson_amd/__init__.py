@@ -29,6 +29,15 @@ if not os.path.exists(LIB_PATH):
         f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
         "(make -C paralleljohnson_amd/csrc)")
 
+# PyTorch-ROCm bundles its own libamdhip64 (same SONAME as /opt/rocm's). Load it
+# first when it is installed, so that libpj binds to the same HIP runtime and
+# torch streams / RCCL collectives and libpj kernels share one device context
+# (two runtimes in one process make the second one report "no GPUs").
+try:
+    import torch  # noqa: F401
+except ImportError:  # the C-ABI path does not need torch
+    pass
+
 _lib = ctypes.CDLL(LIB_PATH)
 
 PJ_OK = 0
@@ -84,6 +93,20 @@ _SIGS = {
     "pj_set_option": ([_P, ctypes.c_char_p, ctypes.c_double], _INT),
     "pj_write_sol": ([_P, _I64, ctypes.c_char_p, _INT], _INT),
     "pj_format_sol": ([_P, _I64, _P, _I64, _P], _INT),
+    "pj_set_stream": ([_P, _P], _INT),
+    "pj_part_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _INT, _PP], _INT),
+    "pj_part_load_coo": ([_P, _P, _P, _I64, _I64, _INT, _INT, _INT, _PP], _INT),
+    "pj_part_destroy": ([_P], _INT),
+    "pj_part_info_get": ([_P, _P], _INT),
+    "pj_part_zmask": ([_P, _P], _INT),
+    "pj_part_begin": ([_P, _I64, _P, _P, _P], _INT),
+    "pj_part_push": ([_P, _INT, _P, _P, _P], _INT),
+    "pj_part_apply": ([_P, _INT, _P, _P, _I64], _INT),
+    "pj_part_pull": ([_P, _INT, _P], _INT),
+    "pj_part_end_level": ([_P, _P, _P], _INT),
+    "pj_part_reach": ([_P, _P], _INT),
+    "pj_part_copy_dist": ([_P, _P], _INT),
+    "pj_part_dist_device": ([_P], _P),
 }
 for _name, (_args, _res) in _SIGS.items():
     _fn = getattr(_lib, _name)
@@ -215,6 +238,10 @@ class Context:
     @property
     def stream(self) -> int:
         return _lib.pj_stream(self._h) or 0
+
+    def set_stream(self, stream: Optional[int]):
+        """Launch later work on an external hipStream_t (e.g. torch's current stream); None = own."""
+        _check(_lib.pj_set_stream(self._h, ctypes.c_void_p(stream) if stream else None))
 
     def load_snap(self, path: str, weighted: bool = False) -> Graph:
         g = ctypes.c_void_p()

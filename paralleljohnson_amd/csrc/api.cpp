@@ -110,7 +110,8 @@ int pj_create(int device, pj_ctx** out) {
         c->c.device = device;
         c->c.cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
         PJ_HIP(hipSetDevice(device));
-        PJ_HIP(hipStreamCreateWithFlags(&c->c.stream, hipStreamNonBlocking));
+        PJ_HIP(hipStreamCreateWithFlags(&c->c.own_stream, hipStreamNonBlocking));
+        c->c.stream = c->c.own_stream;
         *out = c.release();
         return (int)PJ_OK;
     });
@@ -120,13 +121,23 @@ int pj_destroy(pj_ctx* ctx) {
     if (!ctx) return PJ_OK;
     return guarded([&] {
         bind(ctx->c);
-        if (ctx->c.stream) (void)hipStreamDestroy(ctx->c.stream);
+        if (ctx->c.own_stream) (void)hipStreamDestroy(ctx->c.own_stream);
         delete ctx;
         return (int)PJ_OK;
     });
 }
 
 void* pj_stream(pj_ctx* ctx) { return ctx ? (void*)ctx->c.stream : nullptr; }
+
+int pj_set_stream(pj_ctx* ctx, void* stream) {
+    if (!ctx) return arg_error("pj_set_stream: ctx is NULL");
+    return guarded([&] {
+        bind(ctx->c);
+        PJ_HIP(hipStreamSynchronize(ctx->c.stream));  // finish work queued on the previous stream
+        ctx->c.stream = stream ? (hipStream_t)stream : ctx->c.own_stream;
+        return (int)PJ_OK;
+    });
+}
 
 int pj_load_snap_buffer(pj_ctx* ctx, const char* text, int64_t len, int weighted, pj_graph** out) {
     if (!ctx || !out || (len > 0 && !text) || len < 0) return arg_error("pj_load_snap_buffer: bad argument");
@@ -493,5 +504,150 @@ int pj_debug_bitmaps(pj_graph* pg, uint64_t* vis0, uint64_t* vis1, uint64_t* fne
         return (int)PJ_OK;
     });
 }
+
+// ---- 1D vertex partition (part.hip) ---------------------------------------
+
+int pj_part_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int rank, int world,
+                               pj_part** out) {
+    if (!ctx || !out || scale < 0 || scale > 31 || edgefactor < 1 || edgefactor > 1024)
+        return arg_error("pj_part_generate_kronecker: scale must be in [0,31], edgefactor in [1,1024]");
+    if (world < 1 || world > 64 || rank < 0 || rank >= world)
+        return arg_error("pj_part_generate_kronecker: need 0 <= rank < world <= 64");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        *out = reinterpret_cast<pj_part*>(part_from_kronecker(ctx->c, scale, edgefactor, seed, rank, world));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, int64_t nnz, int64_t n_vertices,
+                     int symmetric, int rank, int world, pj_part** out) {
+    if (!ctx || !out || nnz < 0 || (nnz > 0 && (!src || !dst)))
+        return arg_error("pj_part_load_coo: bad argument");
+    if (world < 1 || world > 64 || rank < 0 || rank >= world)
+        return arg_error("pj_part_load_coo: need 0 <= rank < world <= 64");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        i64 n = n_vertices;
+        std::vector<u32> hs((size_t)nnz), hd((size_t)nnz);
+        i64 mx = -1;
+        for (i64 i = 0; i < nnz; ++i) {
+            if (src[i] < 0 || dst[i] < 0 || src[i] > 0xFFFFFFFEll || dst[i] > 0xFFFFFFFEll)
+                throw Error(PJ_ERR_RANGE, "pj_part_load_coo: id outside [0, 2^32-2]");
+            mx = std::max(mx, std::max(src[i], dst[i]));
+            hs[(size_t)i] = (u32)src[i];
+            hd[(size_t)i] = (u32)dst[i];
+        }
+        if (n < 0) n = mx + 1;
+        if (mx >= n) throw Error(PJ_ERR_RANGE, "pj_part_load_coo: id >= n_vertices");
+        DevBuf<u32> s((size_t)nnz), d((size_t)nnz);
+        if (nnz) {
+            PJ_HIP(hipMemcpyAsync(s.p, hs.data(), sizeof(u32) * (size_t)nnz, hipMemcpyHostToDevice, ctx->c.stream));
+            PJ_HIP(hipMemcpyAsync(d.p, hd.data(), sizeof(u32) * (size_t)nnz, hipMemcpyHostToDevice, ctx->c.stream));
+            PJ_HIP(hipStreamSynchronize(ctx->c.stream));
+        }
+        *out = reinterpret_cast<pj_part*>(part_from_coo(ctx->c, s, d, nnz, n, rank, world, symmetric != 0));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_destroy(pj_part* p) {
+    if (!p) return PJ_OK;
+    return guarded([&] {
+        delete_part(reinterpret_cast<Part*>(p));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_info_get(const pj_part* p, pj_part_info* out) {
+    if (!p || !out) return arg_error("pj_part_info_get: bad argument");
+    i64 v[11];
+    part_info(*reinterpret_cast<const Part*>(p), v);
+    out->n = v[0];
+    out->lo = v[1];
+    out->hi = v[2];
+    out->block = v[3];
+    out->words_per_rank = v[4];
+    out->nnz_local = v[5];
+    out->symmetric = (int32_t)v[6];
+    out->off64 = (int32_t)v[7];
+    out->rank = (int32_t)v[8];
+    out->world = (int32_t)v[9];
+    out->nnz_in_local = v[10];
+    return PJ_OK;
+}
+
+int pj_part_zmask(pj_part* p, uint64_t* own_words) {
+    if (!p || !own_words) return arg_error("pj_part_zmask: bad argument");
+    return guarded([&] {
+        part_zmask(*reinterpret_cast<Part*>(p), reinterpret_cast<u64*>(own_words));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_begin(pj_part* p, int64_t source, const uint64_t* iso, uint64_t* vis, int64_t* stats) {
+    if (!p || !iso || !vis || !stats) return arg_error("pj_part_begin: bad argument");
+    return guarded([&] {
+        part_begin(*reinterpret_cast<Part*>(p), source, reinterpret_cast<const u64*>(iso), reinterpret_cast<u64*>(vis),
+                   stats);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_push(pj_part* p, int level, uint64_t* vis, uint32_t* send, int64_t* counts) {
+    if (!p || !vis || !counts || level < 0) return arg_error("pj_part_push: bad argument");
+    return guarded([&] {
+        Part& P = *reinterpret_cast<Part*>(p);
+        i64 info[11];
+        part_info(P, info);
+        if (info[9] > 1 && !send) throw Error(PJ_ERR_ARG, "pj_part_push: send is NULL");
+        part_push(P, level, reinterpret_cast<u64*>(vis), send, counts);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_apply(pj_part* p, int level, uint64_t* vis, const uint32_t* recv, int64_t n_recv) {
+    if (!p || !vis || n_recv < 0 || (n_recv > 0 && !recv) || level < 0) return arg_error("pj_part_apply: bad argument");
+    return guarded([&] {
+        part_apply(*reinterpret_cast<Part*>(p), level, reinterpret_cast<u64*>(vis), recv, n_recv);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_pull(pj_part* p, int level, uint64_t* vis) {
+    if (!p || !vis || level < 0) return arg_error("pj_part_pull: bad argument");
+    return guarded([&] {
+        part_pull(*reinterpret_cast<Part*>(p), level, reinterpret_cast<u64*>(vis));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_end_level(pj_part* p, uint64_t* vis, int64_t* stats) {
+    if (!p || !vis || !stats) return arg_error("pj_part_end_level: bad argument");
+    return guarded([&] {
+        part_end_level(*reinterpret_cast<Part*>(p), reinterpret_cast<u64*>(vis), stats);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_reach(pj_part* p, int64_t* out) {
+    if (!p || !out) return arg_error("pj_part_reach: bad argument");
+    return guarded([&] {
+        part_reach(*reinterpret_cast<Part*>(p), out);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_copy_dist(pj_part* p, int32_t* dist_out) {
+    if (!p || !dist_out) return arg_error("pj_part_copy_dist: bad argument");
+    return guarded([&] {
+        part_copy_dist(*reinterpret_cast<Part*>(p), dist_out);
+        return (int)PJ_OK;
+    });
+}
+
+const int32_t* pj_part_dist_device(pj_part* p) { return p ? part_dist_device(*reinterpret_cast<Part*>(p)) : nullptr; }
 
 }  // extern "C"

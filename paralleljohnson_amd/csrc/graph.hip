@@ -7,6 +7,7 @@
 // Weighted graphs (no reference counterpart: the reference hard-codes w = 1,
 // :147) keep each row sorted by weight instead, for delta-stepping.
 #include "devutil.h"
+#include "kron.h"
 
 namespace pj {
 
@@ -148,58 +149,18 @@ void build_graph_from_coo(Graph& g, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u
 // ------------------------------------------------------------------------
 namespace {
 
-__device__ __forceinline__ u64 splitmix64(u64 x) {
-    u64 z = x + 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-u64 splitmix64_h(u64 x) {
-    u64 z = x + 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-struct PermKeys {
-    u64 mask, k1, k2, c1;
-    int sh;
-};
-
-__device__ __forceinline__ u64 kperm(u64 x, const PermKeys& p) {
-    x = (x * p.k1 + p.c1) & p.mask;
-    x ^= x >> p.sh;
-    x = (x * p.k2) & p.mask;
-    x ^= x >> p.sh;
-    x = (x * p.k1 + (p.c1 >> 7)) & p.mask;
-    return x;
-}
-
 __global__ __launch_bounds__(256) void kronecker_k(int scale, u64 M, u64 seed, int weighted, PermKeys pk,
                                                    u32* __restrict__ src, u32* __restrict__ dst,
                                                    u32* __restrict__ w) {
-    const u32 TA = 2448131358u, TAB = 3264175144u, TABC = 4080218931u;  // 0.57, 0.76, 0.95 of 2^32
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (u64)gridDim.x * blockDim.x) {
-        u64 u = 0, v = 0;
-        for (int l = 0; l < scale; ++l) {
-            const u32 r = (u32)(splitmix64(seed ^ ((i << 6) | (u64)l)) >> 32);
-            const u64 bu = r >= TAB;
-            const u64 bv = (r >= TA && r < TAB) || r >= TABC;
-            u = (u << 1) | bu;
-            v = (v << 1) | bv;
-        }
-        u32 pu = 0, pv = 0;
-        if (scale > 0) {
-            pu = (u32)kperm(u, pk);
-            pv = (u32)kperm(v, pk);
-        }
+        u32 pu, pv;
+        kron_tuple(scale, seed, pk, i, pu, pv);
         src[2 * i] = pu;
         dst[2 * i] = pv;
         src[2 * i + 1] = pv;
         dst[2 * i + 1] = pu;
         if (w) {
-            const u32 wt = weighted ? 1u + (u32)(splitmix64(seed ^ 0x5851F42D4C957F2Dull ^ i) % 255ull) : 1u;
+            const u32 wt = kron_weight(seed, i, weighted != 0);
             w[2 * i] = wt;
             w[2 * i + 1] = wt;
         }
@@ -214,12 +175,7 @@ void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t see
     src.alloc((size_t)(2 * M));
     dst.alloc((size_t)(2 * M));
     if (w) w->alloc((size_t)(2 * M));
-    PermKeys pk;
-    pk.mask = scale >= 64 ? ~0ull : ((1ull << scale) - 1);
-    pk.k1 = splitmix64_h(seed ^ 0x243F6A8885A308D3ull) | 1ull;
-    pk.k2 = splitmix64_h(seed ^ 0x13198A2E03707344ull) | 1ull;
-    pk.c1 = splitmix64_h(seed ^ 0xA4093822299F31D0ull);
-    pk.sh = (scale + 1) / 2;
+    const PermKeys pk = make_perm_keys(scale, seed);
     if (M) {
         kronecker_k<<<grid_for((i64)M, 256, 256u * 64u), 256, 0, ctx.stream>>>(
             scale, M, seed, weighted ? 1 : 0, pk, src.p, dst.p, w ? w->p : nullptr);

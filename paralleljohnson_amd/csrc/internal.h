@@ -120,7 +120,8 @@ void csr_bounds(const u32* sorted_keys, i64 nnz, i64 nv, Off* row, hipStream_t s
 // ---------------------------------------------------------------- graph ---
 struct Ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // where work is launched (own or external)
+    hipStream_t own_stream = nullptr;  // created by pj_create, destroyed by pj_destroy
     int cu_count = 256;
 };
 
@@ -231,5 +232,22 @@ void delta_solve(Graph& g, i64 source);
 void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out);
 void reach_stats(Graph& g, i64* n_r, i64* m_r);
 void debug_bitmaps(Graph& g, u64* vis0, u64* vis1, u64* fnew);
+
+// 1D vertex partition (part.hip)
+struct Part;
+void delete_part(Part* p);
+Part* part_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, int rank, int world);
+Part* part_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, i64 nnz, i64 n, int rank, int world,
+                    bool symmetric);
+void part_info(const Part& p, i64* out);  // n lo hi block bw nnz_local sym off64 rank world nnz_in_local
+void part_zmask(Part& p, u64* out_dev);
+void part_begin(Part& p, i64 source, const u64* iso, u64* vis, i64* out3);
+void part_push(Part& p, int level, u64* vis, u32* packed, i64* counts);
+void part_apply(Part& p, int level, u64* vis, const u32* recv, i64 nr);
+void part_pull(Part& p, int level, u64* vis);
+void part_end_level(Part& p, u64* vis, i64* out3);
+void part_reach(Part& p, i64* out2);
+void part_copy_dist(Part& p, int32_t* host);
+const int32_t* part_dist_device(const Part& p);
 
 }  // namespace pj

@@ -1,0 +1,821 @@
+// part.hip — 1D vertex-partitioned BFS, one process per GPU (SURVEY.md §8e.2,
+// BASELINE.json configs[3]: Kronecker s28 across 2/4/8 MI355X).
+//
+// This is the GPU form of the reference's distributed layout: nn2rank /
+// get_start_nn (ParallelJohnson.cpp:169-200) give each rank a contiguous
+// vertex block and the scatter at :344-410 hands it the out-rows of that
+// block. Here blocks are multiples of 64 vertices (owner(v) = v / block) so
+// that no 64-bit visited word is shared by two ranks; partitioning is
+// result-neutral.
+//
+// Per rank (HBM):
+//   row/col     out-rows of the owned block, global column ids (u32), offsets
+//               u32 or u64 (nnz_local >= 2^32)
+//   crow/ccol   in-rows of the owned block (pull levels); alias row/col when the
+//               graph is symmetric (Kronecker, both directions written)
+//   dist[nl]    int32, PJ_INT_INF = unreached
+//   vis         caller-owned (torch) replicated visited bitmap of ALL vertices,
+//               world slices of bw = block/64 words; exact for the owned slice,
+//               exact everywhere after the per-level all-gather of slices
+//   fr / frn    own-slice bitmaps: current and next frontier
+//   send        world x SH regions of `block` ids (targets for owner o, shard s);
+//               one rank claims a target at most once, so a region cannot overflow
+//
+// A level (driven by paralleljohnson_amd/partition.py):
+//   push : queue := fr (vertices with out-degree >= 1), edge-balanced expansion;
+//          a target is claimed with atomicOr on vis; owned targets are settled
+//          at once, others are appended to the owner's send region, then packed
+//          owner-major for all_to_all_single; pj_part_apply settles the received
+//          ids (claim on the owner's exact slice). This is the analogue of the
+//          reference's per-owner send buffers and MPI_Alltoall(v) at :522-554.
+//   pull : every unvisited owned vertex probes its in-neighbours in the exact
+//          global vis snapshot (for an unvisited vertex "an in-neighbour is
+//          visited" is exactly "an in-neighbour is in the frontier").
+//   end  : fr := frn, own vis slice |= fr, counts (n_f, frontier with edges,
+//          m_f); the driver sums them over ranks (the analogue of the
+//          MPI_Allreduce termination test at :589-590) and all-gathers the vis
+//          slices before pull levels.
+#include "kron.h"
+#include "lb.h"
+
+namespace pj {
+
+namespace {
+
+constexpr int TB = 256;
+constexpr int NW = TB / WAVE;
+constexpr int EPT = 4;              // push: edges per lane per tile
+constexpr int PTILE = TB * EPT;     // push: edges per tile
+constexpr int SH = 8;               // send-counter shards per owner (own 64-B lines)
+constexpr int MAXW = 64;            // largest world size
+constexpr int SC = 16;              // pull: visited words a wave screens at once
+constexpr int PB1 = 4;              // pull: independent first probes per candidate
+constexpr int BU_SERIAL = 32;       // pull: edges a lane probes alone before the wave helps
+constexpr int IPT = 8;              // filter: items per thread per block
+
+template <typename Off>
+struct PartD {
+    const Off* row;
+    const u32* col;
+    const Off* crow;
+    const u32* ccol;
+};
+
+__device__ __forceinline__ bool claim(u64* vis, u32 v) {
+    u64* wp = vis + (v >> 6);
+    const u64 bit = 1ull << (v & 63);
+    if (*wp & bit) return false;
+    return !(atomicOr(wp, bit) & bit);
+}
+
+// ---------------------------------------------------------------- build ----
+// Stable filter of an edge source into the local COO of one rank: entries whose
+// key (src for out-rows, dst for in-rows) lies in [lo, hi) are written as
+// (key - lo, other) in source order. Two passes over the same enumeration: a
+// per-block count, an exclusive scan, and the write.
+struct CooSrc {
+    const u32* src;
+    const u32* dst;
+    i64 n;
+    static constexpr int K = 1;
+    __device__ __forceinline__ i64 items() const { return n; }
+    __device__ __forceinline__ void get(u64 i, u32* s, u32* d) const {
+        s[0] = src[i];
+        d[0] = dst[i];
+    }
+};
+
+struct KronSrc {
+    int scale;
+    u64 seed;
+    u64 M;  // tuples
+    PermKeys pk;
+    static constexpr int K = 2;
+    __device__ __forceinline__ i64 items() const { return (i64)M; }
+    __device__ __forceinline__ void get(u64 i, u32* s, u32* d) const {
+        u32 pu, pv;
+        kron_tuple(scale, seed, pk, i, pu, pv);
+        s[0] = pu;
+        d[0] = pv;
+        s[1] = pv;
+        d[1] = pu;
+    }
+};
+
+template <class S>
+__global__ __launch_bounds__(TB) void filter_count_k(S src, bool by_dst, u64 lo, u64 hi, u32* __restrict__ bcnt) {
+    __shared__ u32 red[NW];
+    const i64 base = (i64)blockIdx.x * TB * IPT;
+    const i64 ni = src.items();
+    u32 c = 0;
+    for (int k = 0; k < IPT; ++k) {
+        const i64 i = base + (i64)k * TB + threadIdx.x;
+        if (i < ni) {
+            u32 s[S::K], d[S::K];
+            src.get((u64)i, s, d);
+#pragma unroll
+            for (int j = 0; j < S::K; ++j) {
+                const u64 key = by_dst ? d[j] : s[j];
+                c += (key >= lo && key < hi);
+            }
+        }
+    }
+    const u32 tot = block_sum<NW>(c, red);
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
+}
+
+template <class S>
+__global__ __launch_bounds__(TB) void filter_write_k(S src, bool by_dst, u64 lo, u64 hi, const u64* __restrict__ boff,
+                                                     u32* __restrict__ okey, u32* __restrict__ oval) {
+    __shared__ u32 red[NW];
+    const i64 base = (i64)blockIdx.x * TB * IPT;
+    const i64 ni = src.items();
+    u64 pos = boff[blockIdx.x];
+    for (int k = 0; k < IPT; ++k) {
+        const i64 i = base + (i64)k * TB + threadIdx.x;
+        u32 s[S::K], d[S::K];
+        u32 c = 0;
+        bool keep[S::K];
+#pragma unroll
+        for (int j = 0; j < S::K; ++j) keep[j] = false;
+        if (i < ni) {
+            src.get((u64)i, s, d);
+#pragma unroll
+            for (int j = 0; j < S::K; ++j) {
+                const u64 key = by_dst ? d[j] : s[j];
+                keep[j] = key >= lo && key < hi;
+                c += keep[j];
+            }
+        }
+        u32 tot;
+        u64 p = pos + block_excl_scan<NW>(c, red, tot);
+#pragma unroll
+        for (int j = 0; j < S::K; ++j)
+            if (keep[j]) {
+                okey[p] = (by_dst ? d[j] : s[j]) - (u32)lo;
+                oval[p] = by_dst ? s[j] : d[j];
+                ++p;
+            }
+        pos += tot;
+    }
+}
+
+// Own-slice isolated mask: no in- and no out-edges (never reached, never a
+// parent), plus the padding bits past the last owned vertex. Such bits start
+// out visited so that pull levels never test them.
+template <typename Off>
+__global__ void part_zmask_k(PartD<Off> g, i64 nl, i64 bw, u64* __restrict__ z) {
+    for (i64 w = (i64)blockIdx.x * blockDim.x + threadIdx.x; w < bw; w += (i64)gridDim.x * blockDim.x) {
+        u64 m = 0;
+        for (int b = 0; b < 64; ++b) {
+            const i64 v = w * 64 + b;
+            bool iso = true;
+            if (v < nl) iso = g.row[v] == g.row[v + 1] && g.crow[v] == g.crow[v + 1];
+            m |= (u64)iso << b;
+        }
+        z[w] = m;
+    }
+}
+
+// --------------------------------------------------------------- solve ----
+struct PartArgs {
+    i64 n, lo, nl, block, bw;
+    int rank, world;
+    int32_t* dist;
+    u64* vis;   // world * bw words (global)
+    u64* fr;    // bw
+    u64* frn;   // bw
+    u32* q;     // frontier queue (local ids)
+    u32* qdeg;
+    u64* qoff;
+    u32* send;  // world * SH * block
+    u64* ctr;   // world * SH counters, 8 words apart
+    u64* stat;  // [0] n_f, [1] m_f, [2] frontier with out-edges, [3] queue fill, [4] bad ids, [8..8+world) packed counts
+};
+
+// dist := INF, vis := iso (global), fr = frn = 0; then the source: its vis bit
+// on every rank, and on its owner dist 0 and the frn bit (end_level makes it
+// the frontier of level 0).
+__global__ void part_begin_k(PartArgs a, const u64* __restrict__ iso, i64 s) {
+    const i64 gs = (i64)gridDim.x * blockDim.x;
+    const i64 t0 = (i64)blockIdx.x * blockDim.x + threadIdx.x;
+    for (i64 i = t0; i < a.nl; i += gs) a.dist[i] = INT_INF;
+    for (i64 i = t0; i < (i64)a.world * a.bw; i += gs) a.vis[i] = iso[i];
+    for (i64 i = t0; i < a.bw; i += gs) {
+        a.fr[i] = 0;
+        a.frn[i] = 0;
+    }
+    if (t0 < 16) a.stat[t0] = 0;
+}
+
+__global__ void part_source_k(PartArgs a, i64 s) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && s >= 0 && s < a.n) {
+        a.vis[s >> 6] |= 1ull << (s & 63);
+        const i64 l = s - a.lo;
+        if (l >= 0 && l < a.nl) {
+            a.dist[l] = 0;
+            a.frn[l >> 6] |= 1ull << (l & 63);
+        }
+    }
+}
+
+// fr := frn, frn := 0, own vis |= fr; stat[0..2] += (n_f, m_f, frontier vertices with out-edges)
+template <typename Off>
+__global__ __launch_bounds__(TB) void part_end_k(PartArgs a, PartD<Off> g) {
+    __shared__ u64 red[NW];
+    u64 nf = 0, mf = 0, nz = 0;
+    for (i64 w = (i64)blockIdx.x * TB + threadIdx.x; w < a.bw; w += (i64)gridDim.x * TB) {
+        const u64 f = a.frn[w];
+        a.frn[w] = 0;
+        a.fr[w] = f;
+        if (f) {
+            a.vis[(i64)a.rank * a.bw + w] |= f;
+            nf += (u64)__popcll(f);
+            u64 m = f;
+            while (m) {
+                const int b = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const i64 v = w * 64 + b;
+                const u64 d = (u64)(g.row[v + 1] - g.row[v]);
+                mf += d;
+                nz += d > 0;
+            }
+        }
+    }
+    nf = block_sum<NW>(nf, red);
+    mf = block_sum<NW>(mf, red);
+    nz = block_sum<NW>(nz, red);
+    if (threadIdx.x == 0) {
+        if (nf) atomicAdd(&a.stat[0], nf);
+        if (mf) atomicAdd(&a.stat[1], mf);
+        if (nz) atomicAdd(&a.stat[2], nz);
+    }
+}
+
+// Push queue: frontier vertices with out-degree >= 1 (local ids) and their degrees.
+template <typename Off>
+__global__ __launch_bounds__(TB) void part_queue_k(PartArgs a, PartD<Off> g) {
+    __shared__ u32 red[NW];
+    __shared__ u64 base_s;
+    for (i64 w0 = (i64)blockIdx.x * TB; w0 < a.bw; w0 += (i64)gridDim.x * TB) {
+        const i64 w = w0 + threadIdx.x;
+        u64 f = w < a.bw ? a.fr[w] : 0;
+        // drop vertices without out-edges (the edge-balanced mapping needs >= 1 edge per slot)
+        u64 keep = 0;
+        for (u64 m = f; m;) {
+            const int b = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const i64 v = w * 64 + b;
+            if (g.row[v + 1] != g.row[v]) keep |= 1ull << b;
+        }
+        u32 tot;
+        const u32 ex = block_excl_scan<NW>((u32)__popcll(keep), red, tot);
+        if (threadIdx.x == 0) base_s = tot ? atomicAdd(&a.stat[3], (u64)tot) : 0;
+        __syncthreads();
+        u64 p = base_s + ex;
+        while (keep) {
+            const int b = __ffsll((long long)keep) - 1;
+            keep &= keep - 1;
+            const i64 v = w * 64 + b;
+            a.q[p] = (u32)v;
+            a.qdeg[p] = (u32)(g.row[v + 1] - g.row[v]);
+            ++p;
+        }
+        __syncthreads();
+    }
+}
+
+template <typename Off>
+__global__ __launch_bounds__(TB) void part_push_k(PartArgs a, PartD<Off> g, u64 nq, u64 mq, int32_t nlev) {
+    __shared__ LbShared<PTILE> sh;
+    __shared__ u32 lcnt[MAXW];
+    __shared__ u64 lbase[MAXW];
+    const int shard = blockIdx.x % SH;
+    const u32 blk = (u32)a.block;
+    for (u64 e0 = (u64)blockIdx.x * PTILE; e0 < mq; e0 += (u64)gridDim.x * PTILE) {
+        u64 s0;
+        u32 ns;
+        lb_tile_load<PTILE>(a.qoff, nq, e0, sh, s0, ns);
+        if (threadIdx.x < (u32)a.world) lcnt[threadIdx.x] = 0;
+        __syncthreads();
+        u32 tgt[EPT], own[EPT], rk[EPT];
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            own[j] = 0xFFFFFFFFu;
+            const u64 e = e0 + (u64)j * TB + threadIdx.x;
+            if (e < mq) {
+                const u32 slot = lb_find<PTILE>(sh, ns, e);
+                const u32 u = a.q[s0 + slot];
+                const u32 t = g.col[(u64)g.row[u] + (e - sh.off[slot])];
+                tgt[j] = t;
+                if (claim(a.vis, t)) {
+                    const u32 o = t / blk;
+                    if ((int)o == a.rank) {
+                        const u32 l = t - (u32)a.lo;
+                        a.dist[l] = nlev;
+                        atomicOr(&a.frn[l >> 6], 1ull << (l & 63));
+                    } else {
+                        own[j] = o;
+                        rk[j] = atomicAdd(&lcnt[o], 1u);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < (u32)a.world) {
+            const u32 c = lcnt[threadIdx.x];
+            lbase[threadIdx.x] = c ? atomicAdd(&a.ctr[((u64)threadIdx.x * SH + shard) * 8], (u64)c) : 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < EPT; ++j)
+            if (own[j] != 0xFFFFFFFFu)
+                a.send[((u64)own[j] * SH + shard) * a.block + lbase[own[j]] + rk[j]] = tgt[j];
+        __syncthreads();
+    }
+}
+
+// Pack the send regions owner-major: packed = [owner 0 | owner 1 | ...], shards
+// in order inside an owner; stat[8 + o] = ids for owner o.
+__global__ __launch_bounds__(TB) void part_pack_k(PartArgs a, u32* __restrict__ packed) {
+    __shared__ u64 pre[MAXW * SH + 1];
+    const int ns = a.world * SH;
+    if (threadIdx.x == 0) {
+        u64 s = 0;
+        for (int i = 0; i < ns; ++i) {
+            pre[i] = s;
+            s += a.ctr[(u64)i * 8];
+        }
+        pre[ns] = s;
+        if (blockIdx.x == 0)
+            for (int o = 0; o < a.world; ++o) a.stat[8 + o] = pre[(o + 1) * SH] - pre[o * SH];
+    }
+    __syncthreads();
+    const u64 T = pre[ns];
+    for (u64 i = (u64)blockIdx.x * TB + threadIdx.x; i < T; i += (u64)gridDim.x * TB) {
+        int lo = 0, hi = ns - 1;  // last segment with pre[seg] <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pre[mid] <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        packed[i] = a.send[(u64)lo * a.block + (i - pre[lo])];
+    }
+}
+
+// Settle received ids (all owned by this rank).
+__global__ void part_apply_k(PartArgs a, const u32* __restrict__ recv, i64 nr, int32_t nlev) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += (i64)gridDim.x * blockDim.x) {
+        const u32 t = recv[i];
+        const i64 l = (i64)t - a.lo;
+        if (l < 0 || l >= a.nl) {
+            atomicAdd(&a.stat[4], 1ull);  // not ours: exchange corrupted (reported as PJ_ERR_COMM)
+            continue;
+        }
+        if (claim(a.vis, t)) {
+            a.dist[l] = nlev;
+            atomicOr(&a.frn[l >> 6], 1ull << (l & 63));
+        }
+    }
+}
+
+// position of the r-th set bit (0-based) of w; r < popcount(w)
+__device__ __forceinline__ u32 select_bit(u64 w, u32 r) {
+    u32 base = 0;
+#pragma unroll
+    for (int half = 32; half >= 8; half >>= 1) {
+        const u64 lo = w & ((1ull << half) - 1ull);
+        const u32 c = (u32)__popcll(lo);
+        if (r >= c) {
+            r -= c;
+            w >>= half;
+            base += half;
+        } else {
+            w = lo;
+        }
+    }
+    for (u32 k = 0; k < 8; ++k) {
+        if ((w >> k) & 1ull) {
+            if (r == 0) return base + k;
+            --r;
+        }
+    }
+    return base;
+}
+
+__device__ __forceinline__ bool vbit(const u64* vis, u32 u) { return (vis[u >> 6] >> (u & 63)) & 1ull; }
+
+// Pull level over the owned slice. A wave screens SC own words, compacts their
+// unvisited vertices into lanes, probes PB1 in-edges per candidate with
+// independent loads, then probes serially (wave-uniform loop, predicated
+// bodies) up to BU_SERIAL edges, then scans the remaining long rows with the
+// whole wave. The wave owns its words: frn is written without atomics.
+template <typename Off>
+__global__ __launch_bounds__(TB) void part_pull_k(PartArgs a, PartD<Off> g, int32_t nlev) {
+    __shared__ u32 s_new[NW][2 * SC];
+    const int lane = lane_id();
+    const u64* vis = a.vis;
+    const i64 obase = (i64)a.rank * a.bw;
+    u32* newb = s_new[wave_id()];
+    const i64 nsc = (a.bw + SC - 1) / SC;
+    for (i64 sc = (i64)blockIdx.x * NW + wave_id(); sc < nsc; sc += (i64)gridDim.x * NW) {
+        const i64 wbase = sc * SC;
+        const bool mine = lane < SC && wbase + lane < a.bw;
+        u64 mytodo = 0;
+        if (mine) mytodo = ~vis[obase + wbase + lane];
+        if (lane < 2 * SC) newb[lane] = 0;
+        const u32 cnt = (u32)__popcll(mytodo);
+        const u32 incl = wave_incl_scan(cnt);
+        const u32 myex = incl - cnt;
+        const u32 T = __shfl(incl, 63, 64);
+        for (u32 r0 = 0; r0 < T; r0 += WAVE) {
+            const u32 c = r0 + lane;
+            const bool act = c < T;
+            u32 jw = 0;  // word of candidate c: largest lane jw < SC with ex[jw] <= c
+#pragma unroll
+            for (u32 step = SC / 2; step > 0; step >>= 1) {
+                const u32 x = __shfl(myex, jw + step, 64);
+                if (x <= c) jw += step;
+            }
+            const u32 ex = __shfl(myex, jw, 64);
+            const u64 tw = __shfl(mytodo, jw, 64);
+            const u32 v = act ? (u32)((wbase + jw) * 64 + select_bit(tw, c - ex)) : 0u;  // local id
+            Off b = 0, e = 0;
+            if (act) {
+                b = g.crow[v];
+                e = g.crow[v + 1];
+            }
+            bool fnd = false;
+            u32 u[PB1];
+#pragma unroll
+            for (int p = 0; p < PB1; ++p) u[p] = (b + p < e) ? g.ccol[b + p] : 0u;
+#pragma unroll
+            for (int p = 0; p < PB1; ++p) fnd |= (b + p < e) && vbit(vis, u[p]);
+            Off k = b + PB1;
+            const Off lim = (e - b > (Off)BU_SERIAL) ? b + (Off)BU_SERIAL : e;
+            bool go = !fnd && k < lim;
+            while (__ballot(go)) {
+                const u32 y = go ? g.ccol[k] : 0u;
+                if (go) {
+                    fnd = vbit(vis, y);
+                    ++k;
+                    go = !fnd && k < lim;
+                }
+            }
+            u64 open = __ballot(!fnd && k < e);
+            while (open) {
+                const int l = __ffsll((long long)open) - 1;
+                open &= open - 1;
+                const Off kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
+                bool hit = false;
+                for (Off kk = kb; kk < ke; kk += WAVE) {
+                    const Off k0 = kk + lane;
+                    const u32 u0 = k0 < ke ? g.ccol[k0] : 0u;
+                    const bool h = k0 < ke && vbit(vis, u0);
+                    if (__ballot(h)) {
+                        hit = true;
+                        break;
+                    }
+                }
+                if (lane == l) fnd = hit;
+            }
+            if (fnd) {
+                a.dist[v] = nlev;
+                atomicOr(&newb[2 * ((v >> 6) - wbase) + ((v >> 5) & 1)], 1u << (v & 31));
+            }
+        }
+        if (mine) a.frn[wbase + lane] = (u64)newb[2 * lane] | ((u64)newb[2 * lane + 1] << 32);
+    }
+}
+
+template <typename Off>
+__global__ __launch_bounds__(TB) void part_reach_k(PartArgs a, PartD<Off> g) {
+    __shared__ u64 red[NW];
+    u64 nr = 0, mr = 0;
+    for (i64 v = (i64)blockIdx.x * TB + threadIdx.x; v < a.nl; v += (i64)gridDim.x * TB)
+        if (a.dist[v] < INT_INF) {
+            ++nr;
+            mr += (u64)(g.row[v + 1] - g.row[v]);
+        }
+    nr = block_sum<NW>(nr, red);
+    mr = block_sum<NW>(mr, red);
+    if (threadIdx.x == 0) {
+        if (nr) atomicAdd(&a.stat[5], nr);
+        if (mr) atomicAdd(&a.stat[6], mr);
+    }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host ---
+struct Part {
+    Ctx* ctx = nullptr;
+    int rank = 0, world = 1;
+    i64 n = 0, block = 64, lo = 0, hi = 0, nl = 0, bw = 1;
+    i64 nnz_local = 0, nnz_in_local = 0;
+    bool symmetric = false, off64 = false;
+    DevBuf<u32> row32, crow32, col, ccol;
+    DevBuf<u64> row64, crow64;
+    DevBuf<int32_t> dist;
+    DevBuf<u64> zmask, fr, frn, qoff, ctr, stat;
+    DevBuf<u32> q, qdeg, send;
+    PinnedBuf<u64> hstat;
+    ScanWs scan;
+    u64 nq = 0, mq = 0;  // push queue of the current frontier (host copy from end_level)
+    int32_t level = 0;
+};
+
+void delete_part(Part* p) { delete p; }
+
+namespace {
+
+template <typename Off>
+PartD<Off> part_d(const Part& p) {
+    PartD<Off> d;
+    if (sizeof(Off) == 8) {
+        d.row = (const Off*)p.row64.p;
+        d.crow = (const Off*)(p.symmetric ? p.row64.p : p.crow64.p);
+    } else {
+        d.row = (const Off*)p.row32.p;
+        d.crow = (const Off*)(p.symmetric ? p.row32.p : p.crow32.p);
+    }
+    d.col = p.col.p;
+    d.ccol = p.symmetric ? p.col.p : p.ccol.p;
+    return d;
+}
+
+PartArgs part_args(Part& p, u64* vis) {
+    PartArgs a;
+    a.n = p.n;
+    a.lo = p.lo;
+    a.nl = p.nl;
+    a.block = p.block;
+    a.bw = p.bw;
+    a.rank = p.rank;
+    a.world = p.world;
+    a.dist = p.dist.p;
+    a.vis = vis;
+    a.fr = p.fr.p;
+    a.frn = p.frn.p;
+    a.q = p.q.p;
+    a.qdeg = p.qdeg.p;
+    a.qoff = p.qoff.p;
+    a.send = p.send.p;
+    a.ctr = p.ctr.p;
+    a.stat = p.stat.p;
+    return a;
+}
+
+template <class S>
+i64 filter_into(Ctx& ctx, const S& src, i64 items, bool by_dst, i64 lo, i64 hi, DevBuf<u32>& key,
+                DevBuf<u32>& val) {
+    hipStream_t s = ctx.stream;
+    const i64 per = (i64)TB * IPT;
+    const i64 nb = (items + per - 1) / per;
+    if (nb == 0) {
+        key.alloc(0);
+        val.alloc(0);
+        return 0;
+    }
+    DevBuf<u32> bcnt((size_t)nb);
+    DevBuf<u64> boff((size_t)nb + 1);
+    ScanWs ws;
+    filter_count_k<S><<<(unsigned)nb, TB, 0, s>>>(src, by_dst, (u64)lo, (u64)hi, bcnt.p);
+    PJ_LAUNCH_CHECK();
+    exclusive_scan_u32(bcnt.p, boff.p, nb, ws, s);
+    u64 total = 0;
+    PJ_HIP(hipMemcpyAsync(&total, boff.p + nb, sizeof(u64), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    key.alloc((size_t)total);
+    val.alloc((size_t)total);
+    if (total) {
+        filter_write_k<S><<<(unsigned)nb, TB, 0, s>>>(src, by_dst, (u64)lo, (u64)hi, boff.p, key.p, val.p);
+        PJ_LAUNCH_CHECK();
+    }
+    PJ_HIP(hipStreamSynchronize(s));
+    return (i64)total;
+}
+
+// sort the local COO by key and turn it into rows [nl+1] (Off) + vals
+void rows_from_local(Part& p, DevBuf<u32>& key, DevBuf<u32>& val, i64 m, DevBuf<u32>& r32, DevBuf<u64>& r64,
+                     DevBuf<u32>& out) {
+    hipStream_t s = p.ctx->stream;
+    int bits = 0;
+    while (bits < 32 && ((u64)1 << bits) < (u64)p.nl) ++bits;
+    SortWs ws;
+    DevBuf<u32> kalt((size_t)m), valt((size_t)m);
+    u32 *kr, *vr;
+    radix_sort_pairs<u32>(key.p, kalt.p, val.p, valt.p, m, bits, ws, s, &kr, &vr);
+    if (p.off64) {
+        r64.alloc((size_t)p.nl + 1);
+        csr_bounds<u64>(kr, m, p.nl, r64.p, s);
+    } else {
+        r32.alloc((size_t)p.nl + 1);
+        csr_bounds<u32>(kr, m, p.nl, r32.p, s);
+    }
+    PJ_HIP(hipStreamSynchronize(s));
+    out = std::move(vr == val.p ? val : valt);
+}
+
+template <class S>
+void build_part(Part& p, const S& src, i64 items, bool symmetric) {
+    hipStream_t s = p.ctx->stream;
+    p.symmetric = symmetric;
+    DevBuf<u32> key, val;
+    const i64 m = filter_into(*p.ctx, src, items, false, p.lo, p.hi, key, val);
+    p.nnz_local = m;
+    i64 mi = m;
+    DevBuf<u32> ikey, ival;
+    if (!symmetric) mi = filter_into(*p.ctx, src, items, true, p.lo, p.hi, ikey, ival);
+    p.nnz_in_local = mi;
+    p.off64 = (u64)std::max(m, mi) > 0xFFFFFFFFull;
+    rows_from_local(p, key, val, m, p.row32, p.row64, p.col);
+    key.release();
+    if (!symmetric) rows_from_local(p, ikey, ival, mi, p.crow32, p.crow64, p.ccol);
+    // per-solve state
+    p.dist.alloc((size_t)std::max<i64>(p.nl, 1));
+    p.zmask.alloc((size_t)p.bw);
+    p.fr.alloc((size_t)p.bw);
+    p.frn.alloc((size_t)p.bw);
+    p.q.alloc((size_t)std::max<i64>(p.nl, 1));
+    p.qdeg.alloc((size_t)std::max<i64>(p.nl, 1));
+    p.qoff.alloc((size_t)std::max<i64>(p.nl, 1) + 1);
+    if (p.world > 1) p.send.alloc((size_t)p.world * SH * (size_t)p.block);
+    p.ctr.alloc((size_t)p.world * SH * 8);
+    p.stat.alloc(64);
+    p.hstat.alloc(64);
+    p.scan.ensure(std::max<i64>(p.nl, 1));
+    PJ_HIP(hipMemsetAsync(p.ctr.p, 0, p.ctr.bytes(), s));
+    if (p.off64) part_zmask_k<u64><<<grid_for(p.bw, 256, 4096), 256, 0, s>>>(part_d<u64>(p), p.nl, p.bw, p.zmask.p);
+    else part_zmask_k<u32><<<grid_for(p.bw, 256, 4096), 256, 0, s>>>(part_d<u32>(p), p.nl, p.bw, p.zmask.p);
+    PJ_LAUNCH_CHECK();
+    PJ_HIP(hipStreamSynchronize(s));
+}
+
+void part_geometry(Part& p, i64 n, int rank, int world) {
+    if (world < 1 || world > MAXW || rank < 0 || rank >= world) throw Error(PJ_ERR_ARG, "rank/world out of range");
+    p.n = n;
+    p.rank = rank;
+    p.world = world;
+    const i64 per = (n + world - 1) / world;
+    p.block = std::max<i64>(64, (per + 63) / 64 * 64);
+    if ((u64)p.block * (u64)world > 0xFFFFFFFFull + 1ull) throw Error(PJ_ERR_RANGE, "too many vertices for u32 ids");
+    p.bw = p.block / 64;
+    p.lo = std::min<i64>((i64)rank * p.block, n);
+    p.hi = std::min<i64>(p.lo + p.block, n);
+    p.nl = p.hi - p.lo;
+}
+
+template <typename Off>
+void end_level_impl(Part& p, u64* vis) {
+    hipStream_t s = p.ctx->stream;
+    PartArgs a = part_args(p, vis);
+    part_end_k<Off><<<grid_for(p.bw, TB, 2048), TB, 0, s>>>(a, part_d<Off>(p));
+    PJ_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+Part* part_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, int rank, int world) {
+    auto p = std::make_unique<Part>();
+    p->ctx = &ctx;
+    part_geometry(*p, (i64)1 << scale, rank, world);
+    KronSrc ks;
+    ks.scale = scale;
+    ks.seed = seed;
+    ks.M = (u64)edgefactor << scale;
+    ks.pk = make_perm_keys(scale, seed);
+    build_part(*p, ks, (i64)ks.M, true);
+    return p.release();
+}
+
+Part* part_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, i64 nnz, i64 n, int rank, int world,
+                    bool symmetric) {
+    auto p = std::make_unique<Part>();
+    p->ctx = &ctx;
+    part_geometry(*p, n, rank, world);
+    CooSrc cs;
+    cs.src = src.p;
+    cs.dst = dst.p;
+    cs.n = nnz;
+    build_part(*p, cs, nnz, symmetric);
+    return p.release();
+}
+
+void part_info(const Part& p, i64* out) {
+    out[0] = p.n;
+    out[1] = p.lo;
+    out[2] = p.hi;
+    out[3] = p.block;
+    out[4] = p.bw;
+    out[5] = p.nnz_local;
+    out[6] = p.symmetric;
+    out[7] = p.off64;
+    out[8] = p.rank;
+    out[9] = p.world;
+    out[10] = p.nnz_in_local;
+}
+
+void part_zmask(Part& p, u64* out_dev) {
+    PJ_HIP(hipMemcpyAsync(out_dev, p.zmask.p, sizeof(u64) * (size_t)p.bw, hipMemcpyDeviceToDevice, p.ctx->stream));
+}
+
+static void read_stats(Part& p, i64* out3) {
+    hipStream_t s = p.ctx->stream;
+    PJ_HIP(hipMemcpyAsync(p.hstat.p, p.stat.p, sizeof(u64) * 8, hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    if (p.hstat.p[4]) throw Error(PJ_ERR_COMM, "received ids owned by another rank (corrupted exchange)");
+    p.nq = p.hstat.p[2];
+    p.mq = p.hstat.p[1];
+    out3[0] = (i64)p.hstat.p[0];
+    out3[1] = (i64)p.hstat.p[1];
+    out3[2] = (i64)p.hstat.p[2];
+    PJ_HIP(hipMemsetAsync(p.stat.p, 0, sizeof(u64) * 8, s));
+}
+
+void part_end_level(Part& p, u64* vis, i64* out3) {
+    if (p.off64) end_level_impl<u64>(p, vis);
+    else end_level_impl<u32>(p, vis);
+    read_stats(p, out3);
+}
+
+void part_begin(Part& p, i64 source, const u64* iso, u64* vis, i64* out3) {
+    hipStream_t s = p.ctx->stream;
+    PartArgs a = part_args(p, vis);
+    const i64 work = std::max<i64>(p.nl, (i64)p.world * p.bw);
+    part_begin_k<<<grid_for(work, 256, 8192), 256, 0, s>>>(a, iso, source);
+    PJ_LAUNCH_CHECK();
+    part_source_k<<<1, 64, 0, s>>>(a, source);
+    PJ_LAUNCH_CHECK();
+    p.level = 0;
+    part_end_level(p, vis, out3);
+}
+
+namespace {
+template <typename Off>
+void push_impl(Part& p, int level, u64* vis, u32* packed, i64* counts) {
+    hipStream_t s = p.ctx->stream;
+    PartArgs a = part_args(p, vis);
+    if (p.nq) {
+        PJ_HIP(hipMemsetAsync(p.stat.p + 3, 0, sizeof(u64), s));
+        part_queue_k<Off><<<grid_for(p.bw, TB, 2048), TB, 0, s>>>(a, part_d<Off>(p));
+        PJ_LAUNCH_CHECK();
+        exclusive_scan_u32(p.qdeg.p, p.qoff.p, (i64)p.nq, p.scan, s);
+        const u64 tiles = (p.mq + PTILE - 1) / PTILE;
+        const unsigned grid = (unsigned)std::min<u64>(tiles, (u64)p.ctx->cu_count * 8);
+        part_push_k<Off><<<grid, TB, 0, s>>>(a, part_d<Off>(p), p.nq, p.mq, level + 1);
+        PJ_LAUNCH_CHECK();
+    }
+    part_pack_k<<<(unsigned)p.ctx->cu_count * 4, TB, 0, s>>>(a, packed);
+    PJ_LAUNCH_CHECK();
+    PJ_HIP(hipMemcpyAsync(p.hstat.p + 8, p.stat.p + 8, sizeof(u64) * (size_t)p.world, hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipMemsetAsync(p.ctr.p, 0, p.ctr.bytes(), s));
+    PJ_HIP(hipStreamSynchronize(s));
+    for (int o = 0; o < p.world; ++o) counts[o] = (i64)p.hstat.p[8 + o];
+}
+}  // namespace
+
+void part_push(Part& p, int level, u64* vis, u32* packed, i64* counts) {
+    if (p.off64) push_impl<u64>(p, level, vis, packed, counts);
+    else push_impl<u32>(p, level, vis, packed, counts);
+}
+
+void part_apply(Part& p, int level, u64* vis, const u32* recv, i64 nr) {
+    if (nr <= 0) return;
+    PartArgs a = part_args(p, vis);
+    part_apply_k<<<grid_for(nr, 256, 8192), 256, 0, p.ctx->stream>>>(a, recv, nr, level + 1);
+    PJ_LAUNCH_CHECK();
+}
+
+void part_pull(Part& p, int level, u64* vis) {
+    hipStream_t s = p.ctx->stream;
+    PartArgs a = part_args(p, vis);
+    const i64 nsc = (p.bw + SC - 1) / SC;
+    const unsigned grid = grid_for(nsc, NW, (unsigned)p.ctx->cu_count * 8);
+    if (p.off64) part_pull_k<u64><<<grid, TB, 0, s>>>(a, part_d<u64>(p), level + 1);
+    else part_pull_k<u32><<<grid, TB, 0, s>>>(a, part_d<u32>(p), level + 1);
+    PJ_LAUNCH_CHECK();
+}
+
+void part_reach(Part& p, i64* out2) {
+    hipStream_t s = p.ctx->stream;
+    PartArgs a = part_args(p, nullptr);
+    PJ_HIP(hipMemsetAsync(p.stat.p + 5, 0, 2 * sizeof(u64), s));
+    if (p.off64) part_reach_k<u64><<<grid_for(p.nl, TB, 4096), TB, 0, s>>>(a, part_d<u64>(p));
+    else part_reach_k<u32><<<grid_for(p.nl, TB, 4096), TB, 0, s>>>(a, part_d<u32>(p));
+    PJ_LAUNCH_CHECK();
+    PJ_HIP(hipMemcpyAsync(p.hstat.p + 5, p.stat.p + 5, 2 * sizeof(u64), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    out2[0] = (i64)p.hstat.p[5];
+    out2[1] = (i64)p.hstat.p[6];
+}
+
+void part_copy_dist(Part& p, int32_t* host) {
+    hipStream_t s = p.ctx->stream;
+    if (p.nl) PJ_HIP(hipMemcpyAsync(host, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+}
+
+const int32_t* part_dist_device(const Part& p) { return p.dist.p; }
+
+}  // namespace pj

@@ -1,0 +1,144 @@
+"""Numpy restatement of the pj_part_* device steps (part.hip), for the CPU tests
+of the partitioned protocol (paralleljohnson_amd/partition.py) under gloo.
+
+Test infrastructure only: it lets the world_size > 1 exchange, termination and
+direction logic run without a GPU. The product path is DevicePart (libpj).
+Semantics per step are those documented in include/pj.h (pj_part_*)."""
+import numpy as np
+import torch
+
+from paralleljohnson_amd.partition import block_geometry
+
+INF = 100000
+
+
+class NumpyPart:
+    def __init__(self, src, dst, n, rank, world, symmetric=False):
+        src = np.asarray(src, np.int64)
+        dst = np.asarray(dst, np.int64)
+        self.n, self.rank, self.world = n, rank, world
+        self.block, ranges = block_geometry(n, world)
+        self.bw = self.block // 64
+        self.lo, self.hi = ranges[rank]
+        self.nl = self.hi - self.lo
+        self.symmetric = symmetric
+
+        def rows(key, val):
+            m = (key >= self.lo) & (key < self.hi)
+            k, v = key[m] - self.lo, val[m]
+            order = np.argsort(k, kind="stable")
+            row = np.zeros(self.nl + 1, np.int64)
+            np.add.at(row, k + 1, 1)
+            return np.cumsum(row), v[order]
+
+        self.row, self.col = rows(src, dst)
+        self.crow, self.ccol = (self.row, self.col) if symmetric else rows(dst, src)
+        self.nnz_local = len(self.col)
+        self.vis = torch.zeros(world * self.bw, dtype=torch.int64)
+        self.iso = torch.zeros_like(self.vis)
+        cap = world * self.block if world > 1 else 1
+        self.send = torch.zeros(cap, dtype=torch.int32)
+        self.recv = torch.zeros(cap, dtype=torch.int32)
+        self.dist = np.full(max(self.nl, 1), INF, np.int32)[: self.nl]
+        self.fr = np.zeros(self.bw, np.uint64)
+        self.frn = np.zeros(self.bw, np.uint64)
+
+    # bit helpers over the torch-owned visited words
+    def _v(self):
+        return self.vis.numpy().view(np.uint64)
+
+    @staticmethod
+    def _get(words, ids):
+        ids = np.asarray(ids, np.int64)
+        return (words[ids >> 6] >> (ids & 63).astype(np.uint64)) & np.uint64(1)
+
+    @staticmethod
+    def _set(words, ids):
+        ids = np.asarray(ids, np.int64)
+        np.bitwise_or.at(words, ids >> 6, np.uint64(1) << (ids & 63).astype(np.uint64))
+
+    def own_slice(self):
+        return self.vis[self.rank * self.bw:(self.rank + 1) * self.bw]
+
+    def zmask(self):
+        z = np.zeros(self.bw, np.uint64)
+        v = np.arange(self.block)
+        iso = np.ones(self.block, bool)  # padding past the last owned vertex counts as isolated
+        iso[: self.nl] = (np.diff(self.row) == 0) & (np.diff(self.crow) == 0)
+        self._set(z, v[iso])
+        return torch.from_numpy(z.view(np.int64).copy())
+
+    def _settle(self, ids, level):
+        """ids: global ids owned by this rank, newly claimed."""
+        loc = np.asarray(ids, np.int64) - self.lo
+        self.dist[loc] = level + 1
+        self._set(self.frn, loc)
+
+    def begin(self, s):
+        self._v()[:] = self.iso.numpy().view(np.uint64)
+        self.dist[:] = INF
+        self.fr[:] = 0
+        self.frn[:] = 0
+        if 0 <= s < self.n:
+            self._set(self._v(), [s])
+            if self.lo <= s < self.hi:
+                self.dist[s - self.lo] = 0
+                self._set(self.frn, [s - self.lo])
+        return self.end_level()
+
+    def _frontier(self, words):
+        ids = np.nonzero(np.unpackbits(words.view(np.uint8), bitorder="little"))[0]
+        return ids[ids < self.nl]
+
+    def push(self, level):
+        vis = self._v()
+        f = self._frontier(self.fr)
+        if len(f):
+            tg = np.concatenate([self.col[self.row[u]:self.row[u + 1]] for u in f])
+        else:
+            tg = np.zeros(0, np.int64)
+        tg = tg[self._get(vis, tg) == 0]
+        tg = np.unique(tg)
+        self._set(vis, tg)
+        owner = tg // self.block
+        mine = owner == self.rank
+        self._settle(tg[mine], level)
+        out = tg[~mine]
+        counts = [int(np.sum(owner[~mine] == o)) for o in range(self.world)]
+        packed = np.concatenate([out[owner[~mine] == o] for o in range(self.world)]) if len(out) else out
+        if len(packed):
+            self.send[: len(packed)] = torch.from_numpy(packed.astype(np.int32))
+        return counts
+
+    def apply(self, level, nr):
+        vis = self._v()
+        ids = self.recv[:nr].numpy().astype(np.int64)
+        assert np.all((ids >= self.lo) & (ids < self.hi)), "received ids owned by another rank"
+        ids = np.unique(ids[self._get(vis, ids) == 0])
+        self._set(vis, ids)
+        self._settle(ids, level)
+
+    def pull(self, level):
+        vis = self._v().copy()  # snapshot: pull writes only frn
+        own = vis[self.rank * self.bw:(self.rank + 1) * self.bw]
+        cand = np.nonzero(np.unpackbits(own.view(np.uint8), bitorder="little") == 0)[0]
+        found = [v for v in cand
+                 if v < self.nl and np.any(self._get(vis, self.ccol[self.crow[v]:self.crow[v + 1]]))]
+        if found:
+            self._settle(np.asarray(found, np.int64) + self.lo, level)
+
+    def end_level(self):
+        self.fr[:] = self.frn
+        self.frn[:] = 0
+        own = self._v()[self.rank * self.bw:(self.rank + 1) * self.bw]
+        own |= self.fr
+        f = self._frontier(self.fr)
+        deg = np.diff(self.row)[f] if len(f) else np.zeros(0, np.int64)
+        return [int(len(f)), int(deg.sum()), int(np.sum(deg > 0))]
+
+    def reach(self):
+        r = self.dist < INF
+        return int(r.sum()), int(np.diff(self.row)[r].sum())
+
+    def dist_local(self):
+        return self.dist.copy()

@@ -1,0 +1,200 @@
+"""1D vertex-partitioned BFS: protocol tests on CPU (gloo,
+world_size 1-3, numpy restatement of the device steps) and parity of the HIP
+kernels (libpj pj_part_*) against the oracle on the GPU, at world_size 1 and
+at world_size 2 with both ranks sharing the one GPU (gloo, host-staged).
+
+Bar: bit-exact distances against the oracle BFS (the reference's R9 contract);
+partitioning is result-neutral."""
+import os
+import socket
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from helpers import random_graph
+
+INF = 100000
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_dist(oracle, src, dst, n, source):
+    row, col, _ = oracle.coo2csr(np.asarray(src, np.int64), np.asarray(dst, np.int64), n)
+    return oracle.bfs(row, col, source)
+
+
+def _cases():
+    rng = np.random.default_rng(2024)
+    out = []
+    for kind, n in (("uniform", 300), ("hub", 700), ("chain", 257), ("uniform", 64), ("hub", 1500)):
+        s, d = random_graph(rng, kind, n)
+        out.append((kind, n, s.astype(np.int64), d.astype(np.int64)))
+    # symmetric (both directions written, like the Kronecker inputs)
+    s, d = random_graph(rng, "hub", 900)
+    out.append(("sym", 900, np.concatenate([s, d]).astype(np.int64), np.concatenate([d, s]).astype(np.int64)))
+    return out
+
+
+# ----------------------------------------------------------------- CPU ----
+
+def test_block_geometry():
+    from paralleljohnson_amd.partition import block_geometry
+    for n in (0, 1, 63, 64, 65, 1000, 4096, 100003):
+        for world in (1, 2, 3, 8):
+            block, ranges = block_geometry(n, world)
+            assert block % 64 == 0 and block >= 64
+            assert ranges[0][0] == 0 and ranges[-1][1] == n
+            for r in range(world - 1):
+                assert ranges[r][1] == ranges[r + 1][0]
+            for v in range(0, n, max(1, n // 97)):
+                r = v // block
+                assert ranges[r][0] <= v < ranges[r][1]
+
+
+@pytest.mark.parametrize("force", [0, 1, 2])
+def test_protocol_world1_numpy(oracle, force):
+    from part_numpy import NumpyPart
+    from paralleljohnson_amd.partition import PartitionedBFS, gather_dist
+    for kind, n, s, d in _cases():
+        sym = kind == "sym"
+        ops = NumpyPart(s, d, n, 0, 1, symmetric=sym)
+        bfs = PartitionedBFS(ops, None, force=force)
+        for source in (0, n // 3, n - 1, n + 5, -1):
+            bfs.solve(source)
+            got = gather_dist(ops, None)
+            exp = _oracle_dist(oracle, s, d, n, source) if 0 <= source < n else np.full(n, INF, np.int32)
+            assert np.array_equal(got, exp), (kind, source, force)
+
+
+def _rank_main(rank, world, port, path, force, device):
+    """One rank of a gloo job: every case, every source; rank 0 saves the results."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    from paralleljohnson_amd.partition import Exchange, PartitionedBFS, gather_dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ex = Exchange()
+    res = {}
+    if device:
+        import paralleljohnson_amd as pj
+        from paralleljohnson_amd.partition import load_coo, load_kronecker
+        ctx = pj.Context(0)
+        cases = [(k, n, s, d) for k, n, s, d in _cases()]
+        for ci, (kind, n, s, d) in enumerate(cases):
+            ops = load_coo(ctx, s, d, n, rank, world, symmetric=(kind == "sym"))
+            bfs = PartitionedBFS(ops, ex, force=force)
+            for source in (0, n // 3, n - 1):
+                st = bfs.solve(source)
+                res[f"{ci}_{source}"] = gather_dist(ops, ex)
+                res[f"{ci}_{source}_reached"] = np.array([st["reached"], st["reached_edges"]])
+            ops.close()
+        ops = load_kronecker(ctx, 14, 16, 7, rank, world)
+        bfs = PartitionedBFS(ops, ex, force=force)
+        for source in (1, 777, 12345):
+            bfs.solve(source)
+            res[f"k14_{source}"] = gather_dist(ops, ex)
+        ops.close()
+    else:
+        from part_numpy import NumpyPart
+        for ci, (kind, n, s, d) in enumerate(_cases()):
+            ops = NumpyPart(s, d, n, rank, world, symmetric=(kind == "sym"))
+            bfs = PartitionedBFS(ops, ex, force=force)
+            for source in (0, n // 3, n - 1, n + 5):
+                bfs.solve(source)
+                res[f"{ci}_{source}"] = gather_dist(ops, ex)
+    if rank == 0:
+        np.savez(path, **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_world(world, force, device=False):
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "res.npz")
+        mp.spawn(_rank_main, args=(world, _free_port(), path, force, device), nprocs=world, join=True)
+        with np.load(path) as z:
+            return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("world,force", [(2, 0), (2, 1), (2, 2), (3, 0)])
+def test_protocol_gloo_numpy(oracle, world, force):
+    res = _run_world(world, force)
+    for ci, (kind, n, s, d) in enumerate(_cases()):
+        for source in (0, n // 3, n - 1, n + 5):
+            exp = _oracle_dist(oracle, s, d, n, source) if source < n else np.full(n, INF, np.int32)
+            assert np.array_equal(res[f"{ci}_{source}"], exp), (world, force, kind, source)
+
+
+# ----------------------------------------------------------------- GPU ----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("force", [0, 1, 2])
+def test_part_world1_gpu(ctx, oracle, force):
+    from paralleljohnson_amd.partition import PartitionedBFS, gather_dist, load_coo
+    for kind, n, s, d in _cases():
+        ops = load_coo(ctx, s, d, n, 0, 1, symmetric=(kind == "sym"))
+        bfs = PartitionedBFS(ops, None, force=force)
+        for source in (0, n // 3, n - 1, n + 5, -1):
+            st = bfs.solve(source)
+            got = gather_dist(ops, None)
+            exp = _oracle_dist(oracle, s, d, n, source) if 0 <= source < n else np.full(n, INF, np.int32)
+            assert np.array_equal(got, exp), (kind, source, force)
+            assert st["reached"] == int(np.sum(exp < INF))
+            assert ops.reach()[0] == st["reached"]
+        ops.close()
+
+
+@pytest.mark.gpu
+def test_part_kronecker_matches_single_gpu(ctx, pj, oracle):
+    """The partitioned generator yields the same graph: s16, world 1, vs pj.Graph and the oracle."""
+    from paralleljohnson_amd.partition import PartitionedBFS, gather_dist, load_kronecker
+    g = ctx.generate_kronecker(16, 16, 3)
+    row, col, _ = g.get_csr()
+    ops = load_kronecker(ctx, 16, 16, 3, 0, 1)
+    assert ops.nnz_local == g.nnz
+    bfs = PartitionedBFS(ops, None)
+    for r in g.sample_roots(5, 4):
+        st = bfs.solve(int(r))
+        got = gather_dist(ops, None)
+        assert np.array_equal(got, g.sssp(int(r))), r
+        assert np.array_equal(got, oracle.bfs(row, col.view(np.uint32), int(r))), r
+        rs = g.reach_stats()
+        assert (st["reached"], st["reached_edges"]) == (rs["reached"], rs["reached_edges"])
+        assert st["td_levels"] >= 1 and st["bu_levels"] >= 1  # both directions exercised
+    ops.close()
+    g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("force", [0, 2])
+def test_part_world2_one_gpu(oracle, force):
+    """Two ranks on the one GPU, gloo with host staging: kernels + exchange end to end."""
+    res = _run_world(2, force, device=True)
+    for ci, (kind, n, s, d) in enumerate(_cases()):
+        for source in (0, n // 3, n - 1):
+            exp = _oracle_dist(oracle, s, d, n, source)
+            assert np.array_equal(res[f"{ci}_{source}"], exp), (kind, source)
+            row, col, _ = _csr(oracle, s, d, n)
+            reached = exp < INF
+            assert res[f"{ci}_{source}_reached"].tolist() == [int(reached.sum()),
+                                                             int(np.diff(row)[reached].sum())]
+    k = oracle.kronecker(14, 16, 7)
+    row, col, _ = oracle.coo2csr(k[0], k[1], 1 << 14)
+    for source in (1, 777, 12345):
+        assert np.array_equal(res[f"k14_{source}"], oracle.bfs(row, col, source)), source
+
+
+def _csr(oracle, s, d, n):
+    return oracle.coo2csr(np.asarray(s, np.int64), np.asarray(d, np.int64), n)
