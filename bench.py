@@ -97,6 +97,61 @@ def run_workload(ctx, key, args, rank, world, barrier, steps, warmup):
                 roots=my_roots[:steps], reach=reach, levels=levels, gen_s=gen_s)
 
 
+def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
+    """configs[3]: Kronecker s{part_scale} unit-weight BFS, 1D vertex partition over the
+    `world` ranks (RCCL exchange, paralleljohnson_amd/partition.py); strong scaling."""
+    from paralleljohnson_amd.partition import Exchange, PartitionedBFS, load_kronecker
+    t0 = time.perf_counter()
+    ops = load_kronecker(ctx, args.part_scale, args.edgefactor, args.seed, rank, world)
+    bfs = PartitionedBFS(ops, Exchange() if world > 1 else None)
+    build_s = time.perf_counter() - t0
+    rng = np.random.default_rng(args.seed + 7)
+    roots = []
+    for c in rng.integers(0, 1 << args.part_scale, 64):  # same candidates on every rank
+        st = bfs.solve(int(c))  # untimed: keep roots in the giant component (degree >= 1)
+        if st["reached"] > 1:
+            roots.append((int(c), dict(st)))
+        if len(roots) == nroots:
+            break
+    barrier()
+    t = time.perf_counter()
+    for r, _ in roots:
+        bfs.solve(r)
+    barrier()
+    elapsed = time.perf_counter() - t
+    m = float(sum(st["reached_edges"] for _, st in roots))
+    b = float(sum(algorithmic_bytes(ops.n, st["reached"], st["reached_edges"], 2 * (args.edgefactor << args.part_scale))
+                  for _, st in roots))
+    st0 = roots[0][1]
+    res = dict(elapsed=elapsed, m=m, b=b, n=ops.n, nnz_local=ops.nnz_local, build_s=build_s, roots=len(roots),
+               st0=st0)
+    ops.close()
+    return res
+
+
+def run_multisource(ctx, args, rank, world, barrier, n_src=1024):
+    """configs[4]: 1024 sources on the web-Google-shaped graph, batched (64 per pass),
+    source batches sharded over the ranks (no data-path collective)."""
+    g = ctx.generate_webgraph(seed=args.seed)
+    row, _, _ = g.get_csr()
+    deg = np.diff(row)
+    sources = np.nonzero(deg >= 1)[0][:n_src]  # SURVEY.md §8d: the smallest ids with out-degree >= 1
+    mine = sources[rank::world]
+    g.sssp_batch(mine[:64], copy=False)  # untimed warmup (workspace)
+    barrier()
+    t = time.perf_counter()
+    g.sssp_batch(mine, copy=False)
+    barrier()
+    elapsed = time.perf_counter() - t
+    # m_r per source (untimed): every source's reached out-edge sum
+    m = 0.0
+    for s0 in range(0, len(mine), 64):
+        d = g.sssp_batch(mine[s0:s0 + 64])
+        m += float(((d < 100000) * deg[None, :]).sum())
+    g.close()
+    return dict(elapsed=elapsed, m=m, n_src=len(mine))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,6 +165,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--part-scale", type=int, default=28, help="Kronecker scale of the partitioned run (configs[3])")
+    ap.add_argument("--no-partitioned", action="store_true")
     ap.add_argument("--opt", action="append", default=[], help="libpj graph option key=value (tuning)")
     args = ap.parse_args()
 
@@ -177,6 +234,41 @@ def main():
                 "levels_td_bu": list(res["levels"][rr][1:3]),
             }
             gg.close()
+
+    def max_sum(el, m):
+        if dist is None:
+            return el, m
+        t = torch.tensor([el, m], dtype=torch.float64, device="cuda")
+        tm = t[:1].clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(tm[0]), float(t[1])
+
+    if not args.no_secondary and not args.scale:
+        ms = run_multisource(ctx, args, rank, world, barrier)
+        el, m = max_sum(ms["elapsed"], ms["m"])
+        secondary["ms1024"] = {
+            "workload": "web-google-shaped-synthetic, 1024 sources (smallest ids with out-degree >= 1), "
+                        "64 per batched pass, source-sharded over the ranks",
+            "sources_per_rank": ms["n_src"], "time_to_solution_ms": round(1000.0 * el, 3),
+            "gteps": round(m / el / 1e9, 3), "scaling": "strong (1024 sources in total)",
+        }
+    if not args.no_partitioned and not args.scale:
+        pr = run_partitioned(ctx, args, rank, world, barrier)
+        el, _ = max_sum(pr["elapsed"], 0.0)
+        per = el / pr["roots"]
+        secondary["k28_partitioned"] = {
+            "workload": f"graph500-kronecker-s{args.part_scale}-ef{args.edgefactor}-unit-bfs, 1D vertex "
+                        f"partition over {world} GPU(s)" + (" (RCCL all_to_all / all_gather / all_reduce)"
+                                                           if world > 1 else ""),
+            "n_vertices": pr["n"], "nnz": 2 * (args.edgefactor << args.part_scale),
+            "nnz_local_rank0": pr["nnz_local"], "roots": pr["roots"],
+            "time_to_solution_ms": round(1000.0 * per, 3),
+            "gteps": round(pr["m"] / el / 1e9, 3), "gteps_graph500": round(pr["m"] / el / 2e9, 3),
+            "hbm_frac_algorithmic": round(pr["b"] / el / 1e9 / (HBM_PEAK_GBS * world), 4),
+            "levels_td_bu": [pr["st0"]["td_levels"], pr["st0"]["bu_levels"]],
+            "build_s": round(pr["build_s"], 2), "scaling": "strong (one graph, all ranks)",
+        }
 
     if rank == 0:
         mean_ms = 1000.0 * elapsed / args.steps

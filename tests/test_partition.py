@@ -75,15 +75,20 @@ def test_protocol_world1_numpy(oracle, force):
             assert np.array_equal(got, exp), (kind, source, force)
 
 
-def _rank_main(rank, world, port, path, force, device):
-    """One rank of a gloo job: every case, every source; rank 0 saves the results."""
+def _rank_main(rank, world, port, path, force, device, backend="gloo"):
+    """One rank of a gloo (or nccl) job: every case, every source; rank 0 saves the results."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
     import torch.distributed as dist
     from paralleljohnson_amd.partition import Exchange, PartitionedBFS, gather_dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     ex = Exchange()
     res = {}
     if device:
@@ -119,11 +124,11 @@ def _rank_main(rank, world, port, path, force, device):
     dist.destroy_process_group()
 
 
-def _run_world(world, force, device=False):
+def _run_world(world, force, device=False, backend="gloo"):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "res.npz")
-        mp.spawn(_rank_main, args=(world, _free_port(), path, force, device), nprocs=world, join=True)
+        mp.spawn(_rank_main, args=(world, _free_port(), path, force, device, backend), nprocs=world, join=True)
         with np.load(path) as z:
             return {k: z[k] for k in z.files}
 
@@ -178,10 +183,11 @@ def test_part_kronecker_matches_single_gpu(ctx, pj, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("force", [0, 2])
-def test_part_world2_one_gpu(oracle, force):
-    """Two ranks on the one GPU, gloo with host staging: kernels + exchange end to end."""
-    res = _run_world(2, force, device=True)
+@pytest.mark.parametrize("world,force,backend", [(2, 0, "gloo"), (2, 2, "gloo"), (1, 0, "nccl")])
+def test_part_world2_one_gpu(oracle, world, force, backend):
+    """Two ranks on the one GPU (gloo, host-staged): kernels + exchange end to end; and the
+    RCCL (nccl backend) code path of the exchange at world 1, device tensors, no staging."""
+    res = _run_world(world, force, device=True, backend=backend)
     for ci, (kind, n, s, d) in enumerate(_cases()):
         for source in (0, n // 3, n - 1):
             exp = _oracle_dist(oracle, s, d, n, source)
