@@ -40,11 +40,26 @@ namespace pj {
 
 namespace {
 
+#ifndef PJ_D_IPT
+#define PJ_D_IPT 4
+#endif
+#ifndef PJ_D_SETTLED
+#define PJ_D_SETTLED 0
+#endif
+#ifndef PJ_D_STAGE_IB
+#define PJ_D_STAGE_IB 0
+#endif
 constexpr int DB = 256;             // relax workgroup
-constexpr int D_IPT = 4;
+constexpr int D_IPT = PJ_D_IPT;
 constexpr int D_TILE = DB * D_IPT;  // edges per relax tile
-constexpr int WL_CAP = 2048;        // LDS worklist of a relax workgroup
-constexpr u32 LOCAL_BUDGET = 512;   // worklist vertices a workgroup relaxes itself
+#ifndef PJ_WL_CAP
+#define PJ_WL_CAP 2048
+#endif
+#ifndef PJ_LOCAL_BUDGET
+#define PJ_LOCAL_BUDGET 512
+#endif
+constexpr int WL_CAP = PJ_WL_CAP;   // LDS worklist of a relax workgroup
+constexpr u32 LOCAL_BUDGET = PJ_LOCAL_BUDGET;  // worklist vertices a workgroup relaxes itself
 constexpr int WL_BATCH = DB;        // worklist entries expanded per step
 constexpr u64 LOCAL_MAX = 4096;     // longest row a workgroup relaxes alone
 constexpr int SB = 256;             // select workgroup
@@ -73,6 +88,7 @@ struct SelArgs {
     const int32_t* dist;
     const u32* lsplit;
     u64* chg;   // vertices deferred by a relax workgroup (worklist overflow / long rows)
+    u64* settled;  // DIST_L selections write it: bit v = dist[v] < lo (final, never improved again)
     u64* sel;   // the frontier being built
     u64* part;  // [6][nwaves]: light count/edges, heavy count/edges, members, min per wave
     u64* boff;  // [4][nwaves]: exclusive light count/edges, heavy count/edges per wave
@@ -125,6 +141,14 @@ __global__ __launch_bounds__(SB) void sel_count_k(SelArgs a, const Off* __restri
                 s[k] = d[k] >= a.lo && d[k] < a.hi;
                 if (d[k] >= a.lo && d[k] < mn) mn = d[k];
             }
+            if (MODE == SEL_DIST_L) {
+#pragma unroll
+                for (int k = 0; k < SU; ++k) {
+                    const u64 fin = __ballot(d[k] < a.lo);
+                    const i64 wi = wb + k0 + k;
+                    if (lane == 0 && wi < a.nwords) a.settled[wi] = fin;
+                }
+            }
         } else {
 #pragma unroll
             for (int k = 0; k < SU; ++k) {
@@ -172,39 +196,57 @@ __global__ __launch_bounds__(SB) void sel_count_k(SelArgs a, const Off* __restri
 }
 
 // One block: exclusive scans of the per-wave partials, the totals, and the
-// relax overflow flag. Thread t owns the consecutive partials [t*per, (t+1)*per).
+// relax overflow flag. The partials are walked in chunks of SCAN_T consecutive
+// entries (coalesced loads; the four scans of a chunk share two barriers).
 __global__ __launch_bounds__(SCAN_T) void sel_scan_k(SelArgs a) {
-    __shared__ u64 lds[SCAN_T / WAVE];
+    __shared__ u64 lds[4][SCAN_T / WAVE];
     const i64 nw = a.nwaves;
-    const i64 per = (nw + SCAN_T - 1) / SCAN_T;
-    const i64 i0 = (i64)threadIdx.x * per, i1 = min(i0 + per, nw);
-    u64 x[4] = {0, 0, 0, 0}, m = 0, mi = INT_INF;
-    for (i64 i = i0; i < i1; ++i) {
+    const int lane = lane_id(), wid = wave_id();
+    u64 run[4] = {0, 0, 0, 0}, m = 0, mi = INT_INF;
+    for (i64 c0 = 0; c0 < nw; c0 += SCAN_T) {
+        const i64 i = c0 + threadIdx.x;
+        const bool ok = i < nw;
+        u64 x[4], inc[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[j] += a.part[j * nw + i];
-        m += a.part[4 * nw + i];
-        mi = min(mi, a.part[5 * nw + i]);
-    }
-    u64 ex[4], tt[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) ex[j] = block_excl_scan<SCAN_T / WAVE>(x[j], lds, tt[j]);
-    for (i64 i = i0; i < i1; ++i) {
+        for (int j = 0; j < 4; ++j) x[j] = ok ? a.part[j * nw + i] : 0;
+        if (ok) {
+            m += a.part[4 * nw + i];
+            const u64 y = a.part[5 * nw + i];
+            mi = y < mi ? y : mi;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            a.boff[j * nw + i] = ex[j];
-            ex[j] += a.part[j * nw + i];
+            inc[j] = wave_incl_scan(x[j]);
+            if (lane == 63) lds[j][wid] = inc[j];
         }
+        __syncthreads();
+        u64 wp[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
+#pragma unroll 2
+        for (int w = 0; w < SCAN_T / WAVE; ++w) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u64 v = lds[j][w];
+                wp[j] += w < wid ? v : 0;
+                tot[j] += v;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (ok) a.boff[j * nw + i] = run[j] + wp[j] + inc[j] - x[j];
+            run[j] += tot[j];
+        }
+        __syncthreads();
     }
-    m = block_sum<SCAN_T / WAVE>(m, lds);
+    m = block_sum<SCAN_T / WAVE>(m, lds[0]);
     mi = ~wave_max(~mi);  // wave min via max of complements
-    if (lane_id() == 0) lds[wave_id()] = mi;
+    if (lane_id() == 0) lds[1][wave_id()] = mi;
     __syncthreads();
     if (threadIdx.x == 0) {
         u64 y = INT_INF;
-        for (int w = 0; w < SCAN_T / WAVE; ++w) y = lds[w] < y ? lds[w] : y;
+        for (int w = 0; w < SCAN_T / WAVE; ++w) y = lds[1][w] < y ? lds[1][w] : y;
         const u64 ov = *a.flag;
         *a.flag = 0;
-        DTot t{tt[0], tt[1], tt[2], tt[3], m, y, ov};
+        DTot t{run[0], run[1], run[2], run[3], m, y, ov};
         *a.tot = t;
         a.host->nl = t.nl;
         a.host->ml = t.ml;
@@ -313,9 +355,12 @@ __device__ __forceinline__ void wl_push(bool p, u32 v, Wl& wl, u64* __restrict__
 // One edge: relax u -> col[idx]; true if the target was lowered into the band.
 __device__ __forceinline__ bool relax_edge(u64 idx, int32_t du, const u32* __restrict__ col,
                                            const u32* __restrict__ wt, int32_t* __restrict__ dist, int32_t hi,
-                                           u32& v) {
+                                           const u64* __restrict__ settled, u32& v) {
     v = col[idx];
     const long long nd = (long long)du + (long long)wt[idx];
+    // a target settled in an earlier band cannot improve: skip its dist probe (the
+    // settled bitmap is 1/32 of dist and mostly L2-resident; dist lines are not)
+    if (PJ_D_SETTLED && ((settled[v >> 6] >> (v & 63)) & 1ull)) return false;
     if (nd < INT_INF && (int32_t)nd < dist[v]) {
         const int32_t old = atomicMin(dist + v, (int32_t)nd);
         return (int32_t)nd < old && (int32_t)nd < hi;
@@ -332,9 +377,10 @@ __global__ __launch_bounds__(DB) void d_relax_k(const u32* __restrict__ iv, cons
                                                 const Off* __restrict__ row, const u32* __restrict__ lsplit,
                                                 const u32* __restrict__ col, const u32* __restrict__ wt,
                                                 int32_t* __restrict__ dist, int32_t hi, u64* __restrict__ chg,
-                                                u32* __restrict__ flag) {
+                                                u32* __restrict__ flag, const u64* __restrict__ settled) {
     __shared__ LbShared<D_TILE> sh;
     __shared__ int32_t s_du[D_TILE];
+    __shared__ u64 s_ib[PJ_D_STAGE_IB ? D_TILE : 1];
     __shared__ Wl wl;
     if (LIGHT && threadIdx.x == 0) wl.n = 0;
     const u64 nq = LIGHT ? tot->nl : tot->nh, total = LIGHT ? tot->ml : tot->mh;
@@ -345,7 +391,10 @@ __global__ __launch_bounds__(DB) void d_relax_k(const u32* __restrict__ iv, cons
         u64 s0;
         u32 ns;
         lb_tile_load<D_TILE>(io, nq, e0, sh, s0, ns);
-        for (u32 i = threadIdx.x; i < ns; i += DB) s_du[i] = dist[iv[s0 + i]];
+        for (u32 i = threadIdx.x; i < ns; i += DB) {
+            s_du[i] = dist[iv[s0 + i]];
+            if (PJ_D_STAGE_IB) s_ib[i] = ib[s0 + i];
+        }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < D_IPT; ++k) {
@@ -354,7 +403,8 @@ __global__ __launch_bounds__(DB) void d_relax_k(const u32* __restrict__ iv, cons
             u32 v = 0;
             if (e < e1) {
                 const u32 j = lb_find<D_TILE>(sh, ns, e);
-                p = relax_edge(ib[s0 + j] + (e - sh.off[j]), s_du[j], col, wt, dist, hi, v);
+                const u64 rb = PJ_D_STAGE_IB ? s_ib[j] : ib[s0 + j];
+                p = relax_edge(rb + (e - sh.off[j]), s_du[j], col, wt, dist, hi, settled, v);
             }
             if (LIGHT) wl_push(p, v, wl, chg, flag);
         }
@@ -403,7 +453,7 @@ __global__ __launch_bounds__(DB) void d_relax_k(const u32* __restrict__ iv, cons
                     if (wl.boff[mid] <= f) lo = mid;
                     else hi2 = mid - 1;
                 }
-                p = relax_edge(wl.bbeg[lo] + (f - wl.boff[lo]), wl.bdu[lo], col, wt, dist, hi, v);
+                p = relax_edge(wl.bbeg[lo] + (f - wl.boff[lo]), wl.bdu[lo], col, wt, dist, hi, settled, v);
             }
             wl_push(p, v, wl, chg, flag);
         }
@@ -447,7 +497,7 @@ __global__ __launch_bounds__(DB) void wsum_k(const u32* __restrict__ w, i64 n, u
 }  // namespace
 
 struct DeltaWork {
-    DevBuf<u64> chg, sel;  // 1 bit per vertex
+    DevBuf<u64> chg, sel, settled;  // 1 bit per vertex
     DevBuf<u32> qvl, qvh;
     DevBuf<u64> qbl, qbh, qol, qoh;
     DevBuf<u64> part, boff;
@@ -497,6 +547,7 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
     a.dist = R.dist.p;
     a.lsplit = w.lsplit.p;
     a.chg = w.chg.p;
+    a.settled = w.settled.p;
     a.sel = w.sel.p;
     a.part = w.part.p;
     a.boff = w.boff.p;
@@ -542,14 +593,15 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
         if (t.ml > 0) {
             const unsigned grid = grid_for((i64)((t.ml + D_TILE - 1) / D_TILE), 1, maxgrid);
             d_relax_k<Off, true><<<grid, DB, 0, s>>>(w.qvl.p, w.qbl.p, w.qol.p, w.tot.p, row, w.lsplit.p, R.col.p,
-                                                     R.w.p, R.dist.p, hi, w.chg.p, w.flag.p);
+                                                     R.w.p, R.dist.p, hi, w.chg.p, w.flag.p, w.settled.p);
             PJ_LAUNCH_CHECK();
             st.relax_rounds++;
         }
         if (t.mh > 0) {
             const unsigned grid = grid_for((i64)((t.mh + D_TILE - 1) / D_TILE), 1, maxgrid);
             d_relax_k<Off, false><<<grid, DB, 0, s>>>(w.qvh.p, w.qbh.p, w.qoh.p, w.tot.p, row, w.lsplit.p,
-                                                      R.col.p, R.w.p, R.dist.p, hi, w.chg.p, w.flag.p);
+                                                      R.col.p, R.w.p, R.dist.p, hi, w.chg.p, w.flag.p,
+                                                      w.settled.p);
             PJ_LAUNCH_CHECK();
             st.relax_rounds++;
         }
@@ -562,6 +614,7 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
     if (n > 0) {
         PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(R.dist.p), INT_INF, (size_t)n, s));
         PJ_HIP(hipMemsetAsync(w.chg.p, 0, sizeof(u64) * (size_t)nwords, s));
+        PJ_HIP(hipMemsetAsync(w.settled.p, 0, sizeof(u64) * (size_t)nwords, s));
         PJ_HIP(hipMemsetAsync(w.flag.p, 0, sizeof(u32), s));
     }
     if (valid && ls < n) {
@@ -627,6 +680,7 @@ void delta_solve(Graph& g, i64 source) {
         const size_t m = n ? n : 1;
         const size_t nwaves = (nwords + WPW - 1) / WPW + 1;
         w.chg.alloc(nwords ? nwords : 1);
+        w.settled.alloc(nwords ? nwords : 1);
         w.sel.alloc(nwords ? nwords : 1);
         w.qvl.alloc(m);
         w.qvh.alloc(m);
