@@ -33,6 +33,7 @@
 // :579-593).
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 
 #include "lb.h"
 
@@ -66,7 +67,13 @@ constexpr int SB = 256;             // select workgroup
 constexpr int SNW = SB / WAVE;
 constexpr int WPW = 64;             // bitmap words per select wave (one per lane in pass 2)
 constexpr int SU = 8;               // words whose loads a select wave issues together
-constexpr int SCAN_T = 1024;        // threads of the one-block scan
+#ifndef PJ_SCAN_T
+#define PJ_SCAN_T 1024
+#endif
+#ifndef PJ_SCAN_HOSTCOPY
+#define PJ_SCAN_HOSTCOPY 0
+#endif
+constexpr int SCAN_T = PJ_SCAN_T;   // threads of the one-block scan
 
 // DIST_L / DIST_H: band members (lo <= dist < hi) with their light / heavy edges;
 // BITS: the deferred vertices of `chg` with their light edges.
@@ -196,27 +203,36 @@ __global__ __launch_bounds__(SB) void sel_count_k(SelArgs a, const Off* __restri
 }
 
 // One block: exclusive scans of the per-wave partials, the totals, and the
-// relax overflow flag. The partials are walked in chunks of SCAN_T consecutive
-// entries (coalesced loads; the four scans of a chunk share two barriers).
+// relax overflow flag. Thread t owns SPT consecutive partials of each pass, so
+// all of its loads are issued before the block scan (one barrier pair per pass).
+constexpr int SPT = 8;
 __global__ __launch_bounds__(SCAN_T) void sel_scan_k(SelArgs a) {
     __shared__ u64 lds[4][SCAN_T / WAVE];
     const i64 nw = a.nwaves;
     const int lane = lane_id(), wid = wave_id();
     u64 run[4] = {0, 0, 0, 0}, m = 0, mi = INT_INF;
-    for (i64 c0 = 0; c0 < nw; c0 += SCAN_T) {
-        const i64 i = c0 + threadIdx.x;
-        const bool ok = i < nw;
-        u64 x[4], inc[4];
+    for (i64 base = 0; base < nw; base += (i64)SCAN_T * SPT) {
+        const i64 i0 = base + (i64)threadIdx.x * SPT;
+        u64 x[4][SPT], sum[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[j] = ok ? a.part[j * nw + i] : 0;
-        if (ok) {
-            m += a.part[4 * nw + i];
-            const u64 y = a.part[5 * nw + i];
-            mi = y < mi ? y : mi;
+        for (int k = 0; k < SPT; ++k) {
+            const i64 i = i0 + k;
+            const bool ok = i < nw;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                x[j][k] = ok ? a.part[j * nw + i] : 0;
+                sum[j] += x[j][k];
+            }
+            if (ok) {
+                m += a.part[4 * nw + i];
+                const u64 y = a.part[5 * nw + i];
+                mi = y < mi ? y : mi;
+            }
         }
+        u64 inc[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            inc[j] = wave_incl_scan(x[j]);
+            inc[j] = wave_incl_scan(sum[j]);
             if (lane == 63) lds[j][wid] = inc[j];
         }
         __syncthreads();
@@ -232,7 +248,12 @@ __global__ __launch_bounds__(SCAN_T) void sel_scan_k(SelArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (ok) a.boff[j * nw + i] = run[j] + wp[j] + inc[j] - x[j];
+            u64 o = run[j] + wp[j] + inc[j] - sum[j];
+#pragma unroll
+            for (int k = 0; k < SPT; ++k) {
+                if (i0 + k < nw) a.boff[j * nw + i0 + k] = o;
+                o += x[j][k];
+            }
             run[j] += tot[j];
         }
         __syncthreads();
@@ -248,13 +269,15 @@ __global__ __launch_bounds__(SCAN_T) void sel_scan_k(SelArgs a) {
         *a.flag = 0;
         DTot t{run[0], run[1], run[2], run[3], m, y, ov};
         *a.tot = t;
-        a.host->nl = t.nl;
-        a.host->ml = t.ml;
-        a.host->nh = t.nh;
-        a.host->mh = t.mh;
-        a.host->members = t.members;
-        a.host->minv = t.minv;
-        a.host->overflow = t.overflow;
+        if (!PJ_SCAN_HOSTCOPY) {
+            a.host->nl = t.nl;
+            a.host->ml = t.ml;
+            a.host->nh = t.nh;
+            a.host->mh = t.mh;
+            a.host->members = t.members;
+            a.host->minv = t.minv;
+            a.host->overflow = t.overflow;
+        }
         a.qol[t.nl] = t.ml;
         a.qoh[t.nh] = t.mh;
     }
@@ -352,6 +375,19 @@ __device__ __forceinline__ void wl_push(bool p, u32 v, Wl& wl, u64* __restrict__
     }
 }
 
+#ifndef PJ_COHERENT_CHECK
+#define PJ_COHERENT_CHECK 1
+#endif
+// The pre-check of dist[t] before the atomicMin: per-XCD L2s are not coherent
+// with each other, so a plain load can return a stale (higher) value for a hot
+// target and let every relaxation into it through to the atomic, which then
+// serialises at ~88 per us per address. An agent-scope load (sc1) sees the
+// value the atomics left.
+__device__ __forceinline__ int32_t dist_now(const int32_t* p) {
+    if (PJ_COHERENT_CHECK) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return *p;
+}
+
 // One edge: relax u -> col[idx]; true if the target was lowered into the band.
 __device__ __forceinline__ bool relax_edge(u64 idx, int32_t du, const u32* __restrict__ col,
                                            const u32* __restrict__ wt, int32_t* __restrict__ dist, int32_t hi,
@@ -361,7 +397,7 @@ __device__ __forceinline__ bool relax_edge(u64 idx, int32_t du, const u32* __res
     // a target settled in an earlier band cannot improve: skip its dist probe (the
     // settled bitmap is 1/32 of dist and mostly L2-resident; dist lines are not)
     if (PJ_D_SETTLED && ((settled[v >> 6] >> (v & 63)) & 1ull)) return false;
-    if (nd < INT_INF && (int32_t)nd < dist[v]) {
+    if (nd < INT_INF && (int32_t)nd < dist_now(dist + v)) {
         const int32_t old = atomicMin(dist + v, (int32_t)nd);
         return (int32_t)nd < old && (int32_t)nd < hi;
     }
@@ -472,6 +508,117 @@ __global__ void unlabel_k(const u32* __restrict__ inv, const int32_t* __restrict
 }
 
 // lsplit[v] = number of edges of v with weight < delta (rows are weight-sorted)
+// Pull step for the heavy edges of band [lo, hi) — symmetric graphs only, where
+// a row is also the vertex's in-edges with the same weights. Every vertex with
+// dist >= hi looks through the heavy part of its own row (weights ascending)
+// for in-neighbours in the band and stops as soon as lo + w >= the best value
+// it has, since no band member can then offer less. This replaces pushing the
+// members' heavy edges when few edges remain unsettled: most of a late band's
+// heavy pushes hit vertices that are already settled (measured on Kronecker
+// s20: 94% of all heavy relaxations), while the unsettled rows are short and
+// cut early. A lane writes only its own vertex's dist, with a plain store; the
+// old and new values are both >= hi, so the band tests of other lanes do not
+// change. Screening as in the BFS pull: a wave reads the dists of PSC groups of
+// 64 vertices, compacts the candidates into lanes, probes PSERIAL edges per lane
+// (wave-uniform loop), then scans the long rows with the whole wave.
+constexpr int PSC = 16;
+constexpr int PSERIAL = 32;
+template <typename Off>
+__global__ __launch_bounds__(DB) void d_pull_heavy_k(const Off* __restrict__ row, const u32* __restrict__ lsplit,
+                                                     const u32* __restrict__ col, const u32* __restrict__ wt,
+                                                     int32_t* __restrict__ dist, i64 n, int32_t lo, int32_t hi) {
+    constexpr int NWV = DB / WAVE;
+    const int lane = lane_id();
+    const i64 ngroups = (n + 63) / 64;
+    const i64 nsc = (ngroups + PSC - 1) / PSC;
+    for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
+        const i64 gbase = sc * PSC;
+        u64 mytodo = 0;
+#pragma unroll
+        for (int k = 0; k < PSC; ++k) {
+            const i64 v = (gbase + k) * 64 + lane;
+            const int32_t d = v < n ? dist[v] : 0;
+            const u64 m = __ballot(v < n && d >= hi);
+            if (lane == k) mytodo = m;
+        }
+        const u32 cnt = (u32)__popcll(mytodo);
+        const u32 incl = wave_incl_scan(cnt);
+        const u32 myex = incl - cnt;
+        const u32 T = __shfl(incl, 63, 64);
+        for (u32 r0 = 0; r0 < T; r0 += WAVE) {
+            const u32 c = r0 + lane;
+            const bool act = c < T;
+            u32 jw = 0;  // group of candidate c: largest lane jw < PSC with ex[jw] <= c
+#pragma unroll
+            for (u32 step = PSC / 2; step > 0; step >>= 1) {
+                const u32 x = __shfl(myex, jw + step, 64);
+                if (x <= c) jw += step;
+            }
+            const u32 ex = __shfl(myex, jw, 64);
+            const u64 tw = __shfl(mytodo, jw, 64);
+            const i64 v = act ? (gbase + jw) * 64 + select_bit(tw, c - ex) : 0;
+            int32_t d0 = INT_INF, cur = INT_INF;
+            Off k = 0, e = 0;
+            if (act) {
+                d0 = dist[v];
+                cur = d0;
+                k = row[v] + (Off)lsplit[v];
+                e = row[v + 1];
+            }
+            const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
+            bool go = act && k < lim, done = !act || k >= e;
+            while (__ballot(go)) {
+                if (go) {
+                    const u32 w = wt[k];
+                    if ((long long)lo + w >= (long long)cur) {
+                        done = true;
+                        go = false;
+                    } else {
+                        const int32_t du = dist[col[k]];
+                        if (du >= lo && du < hi) {
+                            const long long nd = (long long)du + w;
+                            if (nd < cur) cur = (int32_t)nd;
+                        }
+                        ++k;
+                        go = k < lim;
+                        done = k >= e;
+                    }
+                }
+            }
+            u64 open = __ballot(!done);
+            while (open) {
+                const int l = __ffsll((long long)open) - 1;
+                open &= open - 1;
+                const Off kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
+                int32_t cl = __shfl(cur, l, 64);
+                for (Off kk = kb; kk < ke; kk += WAVE) {
+                    const Off k0 = kk + lane;
+                    const bool valid = k0 < ke;
+                    const u32 w = valid ? wt[k0] : 0u;
+                    const bool stop = !valid || (long long)lo + w >= (long long)cl;
+                    int32_t cand = INT_INF;
+                    if (!stop) {
+                        const int32_t du = dist[col[k0]];
+                        if (du >= lo && du < hi) {
+                            const long long nd = (long long)du + w;
+                            cand = nd < INT_INF ? (int32_t)nd : INT_INF;
+                        }
+                    }
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) {
+                        const int32_t y = __shfl_xor(cand, off, 64);
+                        cand = y < cand ? y : cand;
+                    }
+                    cl = cand < cl ? cand : cl;
+                    if (__ballot(stop)) break;  // weights ascend: every later edge stops too
+                }
+                if (lane == l) cur = cl;
+            }
+            if (act && cur < d0) dist[v] = cur;
+        }
+    }
+}
+
 template <typename Off>
 __global__ void light_split_k(const Off* __restrict__ row, const u32* __restrict__ w, i64 n, u32 delta,
                               u32* __restrict__ lsplit) {
@@ -494,6 +641,670 @@ __global__ __launch_bounds__(DB) void wsum_k(const u32* __restrict__ w, i64 n, u
     if (lane_id() == 0 && acc) atomicAdd(out, acc);
 }
 
+
+// ---------------------------------------------------------------------------
+// v2 band loop: bitmap frontiers, no per-band list building.
+//
+//   light round : the band's frontier bitmap F_in (members whose light edges are
+//                 not relaxed yet) is screened wave by wave; a lane relaxes the
+//                 light prefix of its vertex's row (<= V2_LS edges alone, then the
+//                 whole wave for segments <= V2_HT, longer segments go to a hub
+//                 queue relaxed edge-balanced by v2_hub_k). A target lowered below
+//                 hi is marked in F_out: the next round's frontier. Every frontier
+//                 vertex joins the band's member bitmap mb; new members add their
+//                 heavy-edge count to ctl.mh (the push cost of the heavy step).
+//   heavy step  : pull (d_pull-style, fused with the next band's selection) when
+//                 the heavy edges left on unsettled vertices are few, else a push
+//                 over mb's heavy segments (same kernel, heavy mode) and a select.
+//   counts      : frontier sizes live in a ring of 4 slots (a light round reads
+//                 slot c, adds to c+1, zeroes c+2), each slot sharded over 8
+//                 64-B lines; hub queues in a ring of 3. The host reads the ring
+//                 once per batch of light rounds and once per band.
+// ---------------------------------------------------------------------------
+constexpr int V2_SC = 16;     // frontier words a wave screens at once
+constexpr int V2_LS = 8;      // segment edges a lane relaxes alone
+#ifndef PJ_V2_HT
+#define PJ_V2_HT 64
+#endif
+constexpr u64 V2_HT = PJ_V2_HT;  // longer segments: hub queue (edge-balanced). The low ids hold the
+                                 // high-degree vertices, so a wave that relaxed mid-size rows itself
+                                 // would carry a whole dense chunk of them alone (load imbalance).
+constexpr int V2_EB = 40;     // hub counter: (slots << V2_EB) | edges
+constexpr int V2_NSH = 8;     // shards of a count slot
+constexpr int V2_HTILE = DB * 4;
+#ifndef PJ_V2_PLMAX
+#define PJ_V2_PLMAX 32
+#endif
+#ifndef PJ_V2_PCH
+#define PJ_V2_PCH 256
+#endif
+constexpr u32 V2_PLMAX = PJ_V2_PLMAX;  // pull rounds: longer light rows go to v2_pull_long_k
+constexpr u32 V2_PCH = PJ_V2_PCH;      // light edges per v2_pull_long_k work item
+
+struct alignas(64) V2Line {
+    u64 v;
+    u64 pad[7];
+};
+struct V2Ctl {
+    V2Line cnt[4][V2_NSH];  // frontier vertices marked per light round (ring)
+    V2Line hub[3];          // hub queue packed counters (ring)
+    V2Line mh[V2_NSH];      // heavy edges of this band's members
+    V2Line minv;            // min dist >= lo of the last select / pull (next band search)
+    V2Line dbg[8];          // PJ_V2_STATS builds: vertices, edges, atomics, marks, hub edges
+};
+#ifndef PJ_V2_STATS
+#define PJ_V2_STATS 0
+#endif
+
+struct V2Args {
+    i64 n, nwords;
+    int32_t lo, hi;
+    int32_t* dist;
+    const u32* lsplit;
+    const u32* col;
+    const u32* wt;
+    u64* mb;
+    V2Ctl* ctl;
+    u32* hv;     // [3][hcap]
+    u64* hbeg;   // [3][hcap]
+    u64* hoff;   // [3][hcap]
+    u64 hcap;
+};
+
+__device__ __forceinline__ u64 v2_slot_sum(const V2Line* sl) {
+    u64 t = 0;
+#pragma unroll
+    for (int i = 0; i < V2_NSH; ++i) t += sl[i].v;
+    return t;
+}
+
+// one relaxation; LIGHT: a target lowered below hi is marked in fout (returns 1 if newly marked)
+template <bool LIGHT>
+__device__ __forceinline__ u32 v2_relax(const V2Args& a, u64 k, int32_t du, u64* __restrict__ fout, u64& fe) {
+    const u32 t = a.col[k];
+    const long long nd = (long long)du + (long long)a.wt[k];
+    if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[1].v, 1ull);
+    if (nd < INT_INF && (int32_t)nd < dist_now(a.dist + t)) {
+        if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
+        const int32_t old = atomicMin(a.dist + t, (int32_t)nd);
+        if (LIGHT && (int32_t)nd < old && (int32_t)nd < a.hi) {
+            const u64 bit = 1ull << (t & 63);
+            const u32 nw = (atomicOr(fout + (t >> 6), bit) & bit) ? 0u : 1u;
+            if (PJ_V2_STATS && nw) atomicAdd(&a.ctl->dbg[3].v, 1ull);
+            if (nw) fe += a.lsplit[t];  // the next round's push cost
+            return nw;
+        }
+    }
+    return 0u;
+}
+
+// (vertices, their light edges) into a count slot: .v and .pad[0]
+__device__ __forceinline__ void v2_flush2(u64 x, u64 e, V2Line* sl, u64* red) {
+    x = block_sum<DB / WAVE>(x, red);
+    e = block_sum<DB / WAVE>(e, red);
+    if (threadIdx.x == 0) {
+        if (x) atomicAdd(&sl[blockIdx.x % V2_NSH].v, x);
+        if (e) atomicAdd(&sl[blockIdx.x % V2_NSH].pad[0], e);
+    }
+}
+__device__ __forceinline__ u64 v2_slot_edges(const V2Line* sl) {
+    u64 t = 0;
+#pragma unroll
+    for (int i = 0; i < V2_NSH; ++i) t += sl[i].pad[0];
+    return t;
+}
+
+// LIGHT: relax the light prefixes of fin's vertices (a band round); HEAVY: the
+// heavy segments of fin = mb (push heavy step). fin words are cleared as read.
+template <typename Off, bool LIGHT>
+__global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
+                                                  u64* __restrict__ fout, int cin, int hs, u64 pull_thresh) {
+    constexpr int NWV = DB / WAVE;
+    __shared__ u64 red[NWV];
+    if (LIGHT) {
+        if (blockIdx.x == 0 && threadIdx.x < V2_NSH) {
+            a.ctl->cnt[(cin + 2) & 3][threadIdx.x].v = 0;
+            a.ctl->cnt[(cin + 2) & 3][threadIdx.x].pad[0] = 0;
+        }
+        if (v2_slot_sum(a.ctl->cnt[cin]) == 0) return;  // empty frontier (block-uniform)
+        if (v2_slot_edges(a.ctl->cnt[cin]) > pull_thresh) {
+            // v2_pull_light_k relaxed this round; it could not clear fin (other waves
+            // were reading it), so clear it here
+            for (i64 wi = (i64)blockIdx.x * DB + threadIdx.x; wi < a.nwords; wi += (i64)gridDim.x * DB) fin[wi] = 0;
+            return;
+        }
+    }
+    const int lane = lane_id();
+    const u64 mask = (1ull << V2_EB) - 1ull;
+    u32 newc = 0;
+    u64 mh = 0, ml = 0, fe = 0;
+    const i64 nsc = (a.nwords + V2_SC - 1) / V2_SC;
+    for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
+        const i64 wbase = sc * V2_SC;
+        u64 mytodo = 0, mynew = 0;
+        if (lane < V2_SC && wbase + lane < a.nwords) {
+            mytodo = fin[wbase + lane];
+            if (mytodo) {
+                fin[wbase + lane] = 0;
+                if (LIGHT) {  // the wave owns these words of mb: plain read-modify-write
+                    const u64 old = a.mb[wbase + lane];
+                    mynew = mytodo & ~old;
+                    if (mynew) a.mb[wbase + lane] = old | mytodo;
+                }
+            }
+        }
+        if (!__ballot(mytodo != 0)) continue;
+        const u32 cnt = (u32)__popcll(mytodo);
+        const u32 incl = wave_incl_scan(cnt);
+        const u32 myex = incl - cnt;
+        const u32 T = __shfl(incl, 63, 64);
+        for (u32 r0 = 0; r0 < T; r0 += WAVE) {
+            const u32 c = r0 + lane;
+            const bool act = c < T;
+            u32 jw = 0;
+#pragma unroll
+            for (u32 step = V2_SC / 2; step > 0; step >>= 1) {
+                const u32 x = __shfl(myex, jw + step, 64);
+                if (x <= c) jw += step;
+            }
+            const u32 ex = __shfl(myex, jw, 64);
+            const u64 tw = __shfl(mytodo, jw, 64);
+            const u64 tn = __shfl(mynew, jw, 64);
+            int32_t du = 0;
+            u64 b = 0, e = 0;
+            u32 v = 0;
+            if (act) {
+                const u32 bit = select_bit(tw, c - ex);
+                v = (u32)((wbase + jw) * 64 + bit);
+                du = a.dist[v];
+                const u64 rb = (u64)row[v];
+                const u64 ls = a.lsplit[v];
+                if (PJ_V2_STATS && LIGHT) atomicAdd(&a.ctl->dbg[0].v, 1ull);
+                if (LIGHT) {
+                    b = rb;
+                    e = rb + ls;
+                    if ((tn >> bit) & 1ull) {
+                        mh += (u64)row[v + 1] - rb - ls;
+                        ml += ls;
+                    }
+                } else {
+                    b = rb + ls;
+                    e = (u64)row[v + 1];
+                }
+            }
+            // long segment -> hub queue (wave-aggregated packed append; all lanes here)
+            const bool hub = e - b > V2_HT;
+            const u64 hm = __ballot(hub);
+            if (hm) {
+                const u64 seg = hub ? e - b : 0;
+                const u64 ie = wave_incl_scan(seg);
+                const u64 tot = __shfl(ie, 63, 64);
+                const int leader = __ffsll((long long)hm) - 1;
+                u64 base = 0;
+                if (lane == leader) base = atomicAdd(&a.ctl->hub[hs].v, ((u64)__popcll(hm) << V2_EB) | tot);
+                base = __shfl(base, leader, 64);
+                if (hub) {
+                    const u64 slot = (base >> V2_EB) + (u64)__popcll(hm & lanemask_lt());
+                    const u64 q = (u64)hs * a.hcap + slot;
+                    a.hv[q] = v;
+                    a.hbeg[q] = b;
+                    a.hoff[q] = (base & mask) + ie - seg;
+                    e = b;  // the hub kernel relaxes this segment
+                }
+            }
+            // lane-serial part
+            u64 k = b;
+            const u64 lim = (e - b > (u64)V2_LS) ? b + V2_LS : e;
+            bool go = k < lim;
+            while (__ballot(go)) {
+                if (go) {
+                    newc += v2_relax<LIGHT>(a, k, du, fout, fe);
+                    ++k;
+                    go = k < lim;
+                }
+            }
+            // wave-cooperative part (segments <= V2_HT)
+            u64 open = __ballot(k < e);
+            while (open) {
+                const int l = __ffsll((long long)open) - 1;
+                open &= open - 1;
+                const u64 kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
+                const int32_t dl = __shfl(du, l, 64);
+                for (u64 kk = kb; kk < ke; kk += WAVE) {
+                    const u64 k0 = kk + lane;
+                    if (k0 < ke) newc += v2_relax<LIGHT>(a, k0, dl, fout, fe);
+                }
+            }
+        }
+    }
+    if (LIGHT) {
+        v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+        v2_flush2(mh, ml, a.ctl->mh, red);
+    }
+}
+
+// Edge-balanced relaxation of hub queue hs (slots' edge offsets are monotonic:
+// one packed atomic gave both). Zeroes the next ring slot hz for later appends.
+template <bool LIGHT>
+__global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout, int cin, int hs, int hz) {
+    __shared__ LbShared<V2_HTILE> sh;
+    __shared__ int32_t s_du[V2_HTILE];
+    __shared__ u64 s_b[V2_HTILE];
+    __shared__ u64 red[DB / WAVE];
+    const u64 packed = a.ctl->hub[hs].v;
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->hub[hz].v = 0;
+    const u64 nq = packed >> V2_EB, total = packed & ((1ull << V2_EB) - 1ull);
+    if (nq == 0) return;
+    const u32* hv = a.hv + (u64)hs * a.hcap;
+    const u64* hb = a.hbeg + (u64)hs * a.hcap;
+    const u64* ho = a.hoff + (u64)hs * a.hcap;
+    u32 newc = 0;
+    u64 fe = 0;
+    for (u64 e0 = (u64)blockIdx.x * V2_HTILE; e0 < total; e0 += (u64)gridDim.x * V2_HTILE) {
+        u64 s0;
+        u32 ns;
+        lb_tile_load<V2_HTILE>(ho, nq, e0, sh, s0, ns);
+        for (u32 i = threadIdx.x; i < ns; i += DB) {
+            s_du[i] = a.dist[hv[s0 + i]];
+            s_b[i] = hb[s0 + i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < V2_HTILE / DB; ++j) {
+            const u64 e = e0 + (u64)j * DB + threadIdx.x;
+            if (e < total) {
+                const u32 sl = lb_find<V2_HTILE>(sh, ns, e);
+                newc += v2_relax<LIGHT>(a, s_b[sl] + (e - sh.off[sl]), s_du[sl], fout, fe);
+            }
+        }
+        __syncthreads();
+    }
+    if (LIGHT) v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+}
+
+// Next band [lo, hi): fout words = members, count into slot cout, min dist >= lo.
+__global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fout, int cout) {
+    __shared__ u64 red[DB / WAVE];
+    const int lane = lane_id();
+    u32 c = 0;
+    u64 fe = 0;
+    int32_t mn = INT_INF;
+    for (i64 wi = (i64)blockIdx.x * (DB / WAVE) + wave_id(); wi < a.nwords; wi += (i64)gridDim.x * (DB / WAVE)) {
+        const i64 v = wi * 64 + lane;
+        const int32_t d = v < a.n ? a.dist[v] : INT_INF;
+        const bool mem = d >= a.lo && d < a.hi;
+        const u64 m = __ballot(mem);
+        if (d >= a.lo && d < mn) mn = d;
+        if (mem) fe += a.lsplit[v];
+        if (lane == 0) fout[wi] = m;
+        c += lane == 0 ? (u32)__popcll(m) : 0u;
+    }
+    v2_flush2(c, fe, a.ctl->cnt[cout], red);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int32_t y = __shfl_xor(mn, off, 64);
+        mn = y < mn ? y : mn;
+    }
+    if (lane == 0 && mn < INT_INF) atomicMin(&a.ctl->minv.v, (u64)mn);
+}
+
+// Pull step of the heavy edges of band [lo, hi) fused with the selection of the
+// next band [hi, nhi): see d_pull_heavy_k for the pull rule. The wave owns its
+// PSC words: it writes the next band's member words of fout whole (and so clears
+// them), counts them into slot cout and folds min{new dist >= hi} into minv.
+template <typename Off>
+__global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fout,
+                                                int32_t nhi, int cout) {
+    constexpr int NWV = DB / WAVE;
+    __shared__ u32 s_new[NWV][2 * PSC];
+    __shared__ u64 red[NWV];
+    const int lane = lane_id();
+    const int32_t lo = a.lo, hi = a.hi;
+    u32* newb = s_new[wave_id()];
+    u32 ccount = 0;
+    u64 fe = 0;
+    int32_t mn = INT_INF;
+    const i64 ngroups = a.nwords;
+    const i64 nsc = (ngroups + PSC - 1) / PSC;
+    for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
+        const i64 gbase = sc * PSC;
+        u64 mytodo = 0;
+#pragma unroll
+        for (int k = 0; k < PSC; ++k) {
+            const i64 v = (gbase + k) * 64 + lane;
+            const int32_t d = v < a.n ? a.dist[v] : 0;
+            const u64 m = __ballot(v < a.n && d >= hi);
+            if (lane == k) mytodo = m;
+        }
+        if (lane < 2 * PSC) newb[lane] = 0;
+        const u32 cnt = (u32)__popcll(mytodo);
+        const u32 incl = wave_incl_scan(cnt);
+        const u32 myex = incl - cnt;
+        const u32 T = __shfl(incl, 63, 64);
+        for (u32 r0 = 0; r0 < T; r0 += WAVE) {
+            const u32 c = r0 + lane;
+            const bool act = c < T;
+            u32 jw = 0;
+#pragma unroll
+            for (u32 step = PSC / 2; step > 0; step >>= 1) {
+                const u32 x = __shfl(myex, jw + step, 64);
+                if (x <= c) jw += step;
+            }
+            const u32 ex = __shfl(myex, jw, 64);
+            const u64 tw = __shfl(mytodo, jw, 64);
+            const i64 v = act ? (gbase + jw) * 64 + select_bit(tw, c - ex) : 0;
+            int32_t d0 = INT_INF, cur = INT_INF;
+            Off k = 0, e = 0;
+            if (act) {
+                d0 = a.dist[v];
+                cur = d0;
+                k = row[v] + (Off)a.lsplit[v];
+                e = row[v + 1];
+            }
+            const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
+            bool go = act && k < lim, done = !act || k >= e;
+            while (__ballot(go)) {
+                if (go) {
+                    const u32 w = a.wt[k];
+                    if ((long long)lo + w >= (long long)cur) {
+                        done = true;
+                        go = false;
+                    } else {
+                        const int32_t du = a.dist[a.col[k]];
+                        if (du >= lo && du < hi) {
+                            const long long nd = (long long)du + w;
+                            if (nd < cur) cur = (int32_t)nd;
+                        }
+                        ++k;
+                        go = k < lim;
+                        done = k >= e;
+                    }
+                }
+            }
+            u64 open = __ballot(!done);
+            while (open) {
+                const int l = __ffsll((long long)open) - 1;
+                open &= open - 1;
+                const Off kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
+                int32_t cl = __shfl(cur, l, 64);
+                for (Off kk = kb; kk < ke; kk += WAVE) {
+                    const Off k0 = kk + lane;
+                    const bool valid = k0 < ke;
+                    const u32 w = valid ? a.wt[k0] : 0u;
+                    const bool stop = !valid || (long long)lo + w >= (long long)cl;
+                    int32_t cand = INT_INF;
+                    if (!stop) {
+                        const int32_t du = a.dist[a.col[k0]];
+                        if (du >= lo && du < hi) {
+                            const long long nd = (long long)du + w;
+                            cand = nd < INT_INF ? (int32_t)nd : INT_INF;
+                        }
+                    }
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) {
+                        const int32_t y = __shfl_xor(cand, off, 64);
+                        cand = y < cand ? y : cand;
+                    }
+                    cl = cand < cl ? cand : cl;
+                    if (__ballot(stop)) break;
+                }
+                if (lane == l) cur = cl;
+            }
+            if (act) {
+                if (cur < d0) a.dist[v] = cur;
+                if (cur < mn) mn = cur;
+                if (cur < nhi) {  // cur >= hi always here
+                    const i64 wl = (v >> 6) - gbase;
+                    atomicOr(&newb[2 * wl + ((v >> 5) & 1)], 1u << (v & 31));
+                    fe += a.lsplit[v];
+                }
+            }
+        }
+        if (lane < PSC && gbase + lane < a.nwords) {
+            const u64 word = (u64)newb[2 * lane] | ((u64)newb[2 * lane + 1] << 32);
+            fout[gbase + lane] = word;
+            ccount += (u32)__popcll(word);
+        }
+    }
+    v2_flush2(ccount, fe, a.ctl->cnt[cout], red);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int32_t y = __shfl_xor(mn, off, 64);
+        mn = y < mn ? y : mn;
+    }
+    if (lane == 0 && mn < INT_INF) atomicMin(&a.ctl->minv.v, (u64)mn);
+}
+
+// Pull form of a light round (symmetric graphs): every vertex that can still
+// improve (dist > lo) scans the light prefix of its own row (= its light
+// in-edges) for in-neighbours in the round's frontier fin — a bitmap probe, fin
+// being 1/32 of dist and mostly L2-resident — and stops once lo + w >= its best
+// value. Run instead of the push when the frontier's light edges exceed
+// pull_thresh (the big rounds of the first bands). No atomics: a lane writes only
+// its own vertex. The wave owns its PSC words of fout (written whole) and of mb
+// (new members add their heavy / light degrees to ctl.mh).
+template <typename Off>
+__global__ __launch_bounds__(DB) void v2_pull_light_k(V2Args a, const Off* __restrict__ row,
+                                                      const u64* __restrict__ fin, u64* __restrict__ fout, int cin,
+                                                      u64 pull_thresh) {
+    constexpr int NWV = DB / WAVE;
+    __shared__ u32 s_new[NWV][2 * PSC];
+    __shared__ u64 red[NWV];
+    if (v2_slot_sum(a.ctl->cnt[cin]) == 0 || v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) return;
+    const int lane = lane_id();
+    const int32_t lo = a.lo, hi = a.hi;
+    u32* newb = s_new[wave_id()];
+    u32 newc = 0;
+    u64 fe = 0, mh = 0, ml = 0;
+    const i64 nsc = (a.nwords + PSC - 1) / PSC;
+    for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
+        const i64 gbase = sc * PSC;
+        if (lane < PSC && gbase + lane < a.nwords) {
+            const u64 f = fin[gbase + lane];
+            if (f) {
+                const u64 old = a.mb[gbase + lane];
+                u64 nm = f & ~old;
+                if (nm) a.mb[gbase + lane] = old | f;
+                while (nm) {
+                    const int b = __ffsll((long long)nm) - 1;
+                    nm &= nm - 1;
+                    const i64 v = (gbase + lane) * 64 + b;
+                    const u64 rb = (u64)row[v], ls = a.lsplit[v];
+                    mh += (u64)row[v + 1] - rb - ls;
+                    ml += ls;
+                }
+            }
+        }
+        u64 mytodo = 0;
+#pragma unroll
+        for (int k = 0; k < PSC; ++k) {
+            const i64 v = (gbase + k) * 64 + lane;
+            const int32_t d = v < a.n ? a.dist[v] : 0;
+            const u64 m = __ballot(v < a.n && d > lo);
+            if (lane == k) mytodo = m;
+        }
+        if (lane < 2 * PSC) newb[lane] = 0;
+        const u32 cnt = (u32)__popcll(mytodo);
+        const u32 incl = wave_incl_scan(cnt);
+        const u32 myex = incl - cnt;
+        const u32 T = __shfl(incl, 63, 64);
+        for (u32 r0 = 0; r0 < T; r0 += WAVE) {
+            const u32 c = r0 + lane;
+            const bool act = c < T;
+            u32 jw = 0;
+#pragma unroll
+            for (u32 step = PSC / 2; step > 0; step >>= 1) {
+                const u32 x = __shfl(myex, jw + step, 64);
+                if (x <= c) jw += step;
+            }
+            const u32 ex = __shfl(myex, jw, 64);
+            const u64 tw = __shfl(mytodo, jw, 64);
+            const i64 v = act ? (gbase + jw) * 64 + select_bit(tw, c - ex) : 0;
+            int32_t d0 = INT_INF, cur = INT_INF;
+            Off k = 0, e = 0;
+            u32 ls = 0;
+            if (act) {
+                d0 = a.dist[v];
+                cur = d0;
+                k = row[v];
+                ls = a.lsplit[v];
+                e = ls > V2_PLMAX ? k : k + (Off)ls;  // long rows: v2_pull_long_k
+            }
+            const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
+            bool go = act && k < lim, done = !act || k >= e;
+            while (__ballot(go)) {
+                if (go) {
+                    const u32 w = a.wt[k];
+                    if ((long long)lo + w >= (long long)cur) {
+                        done = true;
+                        go = false;
+                    } else {
+                        const u32 u = a.col[k];
+                        if ((fin[u >> 6] >> (u & 63)) & 1ull) {
+                            const long long nd = (long long)a.dist[u] + w;
+                            if (nd < cur) cur = (int32_t)nd;
+                        }
+                        ++k;
+                        go = k < lim;
+                        done = k >= e;
+                    }
+                }
+            }
+            u64 open = __ballot(!done);
+            while (open) {
+                const int l = __ffsll((long long)open) - 1;
+                open &= open - 1;
+                const Off kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
+                int32_t cl = __shfl(cur, l, 64);
+                for (Off kk = kb; kk < ke; kk += WAVE) {
+                    const Off k0 = kk + lane;
+                    const bool valid = k0 < ke;
+                    const u32 w = valid ? a.wt[k0] : 0u;
+                    const bool stop = !valid || (long long)lo + w >= (long long)cl;
+                    int32_t cand = INT_INF;
+                    if (!stop) {
+                        const u32 u = a.col[k0];
+                        if ((fin[u >> 6] >> (u & 63)) & 1ull) {
+                            const long long nd = (long long)a.dist[u] + w;
+                            cand = nd < INT_INF ? (int32_t)nd : INT_INF;
+                        }
+                    }
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) {
+                        const int32_t y = __shfl_xor(cand, off, 64);
+                        cand = y < cand ? y : cand;
+                    }
+                    cl = cand < cl ? cand : cl;
+                    if (__ballot(stop)) break;
+                }
+                if (lane == l) cur = cl;
+            }
+            if (act && cur < d0) {
+                a.dist[v] = cur;
+                if (cur < hi) {
+                    const i64 wl = (v >> 6) - gbase;
+                    atomicOr(&newb[2 * wl + ((v >> 5) & 1)], 1u << (v & 31));
+                    ++newc;
+                    fe += ls;
+                }
+            }
+        }
+        if (lane < PSC && gbase + lane < a.nwords)
+            fout[gbase + lane] = (u64)newb[2 * lane] | ((u64)newb[2 * lane + 1] << 32);
+    }
+    v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+    v2_flush2(mh, ml, a.ctl->mh, red);
+}
+
+// Long light rows (lsplit > V2_PLMAX, the high-degree vertices) are left out of
+// v2_pull_light_k: one lane scanning tens of thousands of edges would hold up
+// its wave. Their pull runs here instead, over a static list of (vertex, chunk
+// of V2_PCH light edges) built once per delta; a wave takes a chunk, skips it
+// when even its lightest edge cannot help, and folds the result in with
+// atomicMin (the vertex's chunks run in different waves).
+template <typename Off>
+__global__ __launch_bounds__(DB) void v2_pull_long_k(V2Args a, const Off* __restrict__ row,
+                                                     const u64* __restrict__ fin, u64* __restrict__ fout, int cin,
+                                                     u64 pull_thresh, const u32* __restrict__ lcv,
+                                                     const u32* __restrict__ lcc, u64 nlc) {
+    __shared__ u64 red[DB / WAVE];
+    if (v2_slot_sum(a.ctl->cnt[cin]) == 0 || v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) return;
+    const int lane = lane_id();
+    const int32_t lo = a.lo, hi = a.hi;
+    u32 newc = 0;
+    u64 fe = 0;
+    for (u64 it = (u64)blockIdx.x * (DB / WAVE) + wave_id(); it < nlc; it += (u64)gridDim.x * (DB / WAVE)) {
+        const u32 v = lcv[it];
+        const int32_t d0 = dist_now(a.dist + v);
+        if (d0 <= lo) continue;
+        const u64 rb = (u64)row[v];
+        const u32 ls = a.lsplit[v];
+        const u64 kb = rb + (u64)lcc[it] * V2_PCH;
+        const u64 ke = min(rb + ls, kb + V2_PCH);
+        if ((long long)lo + a.wt[kb] >= (long long)d0) continue;
+        int32_t cur = d0;
+        for (u64 kk = kb; kk < ke; kk += WAVE) {
+            const u64 k0 = kk + lane;
+            const bool valid = k0 < ke;
+            const u32 w = valid ? a.wt[k0] : 0u;
+            const bool stop = !valid || (long long)lo + w >= (long long)cur;
+            int32_t cand = INT_INF;
+            if (!stop) {
+                const u32 u = a.col[k0];
+                if ((fin[u >> 6] >> (u & 63)) & 1ull) {
+                    const long long nd = (long long)a.dist[u] + w;
+                    cand = nd < INT_INF ? (int32_t)nd : INT_INF;
+                }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const int32_t y = __shfl_xor(cand, off, 64);
+                cand = y < cand ? y : cand;
+            }
+            cur = cand < cur ? cand : cur;
+            if (__ballot(stop)) break;
+        }
+        if (lane == 0 && cur < d0) {
+            const int32_t old = atomicMin(a.dist + v, cur);
+            if (cur < old && cur < hi) {
+                const u64 bit = 1ull << (v & 63);
+                if (!(atomicOr(fout + (v >> 6), bit) & bit)) {
+                    ++newc;
+                    fe += ls;
+                }
+            }
+        }
+    }
+    v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+}
+
+// static chunk list of the long light rows: count, then append (order is irrelevant)
+__global__ void v2_long_count_k(const u32* __restrict__ lsplit, i64 n, u64* __restrict__ cnt) {
+    u64 c = 0;
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x)
+        if (lsplit[v] > V2_PLMAX) c += (lsplit[v] + V2_PCH - 1) / V2_PCH;
+    c = wave_sum(c);
+    if (lane_id() == 0 && c) atomicAdd(cnt, c);
+}
+__global__ void v2_long_fill_k(const u32* __restrict__ lsplit, i64 n, u64* __restrict__ cnt, u32* __restrict__ lcv,
+                               u32* __restrict__ lcc) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x)
+        if (lsplit[v] > V2_PLMAX) {
+            const u32 nc = (lsplit[v] + V2_PCH - 1) / V2_PCH;
+            const u64 b = atomicAdd(cnt, (u64)nc);
+            for (u32 c = 0; c < nc; ++c) {
+                lcv[b + c] = (u32)v;
+                lcc[b + c] = c;
+            }
+        }
+}
+
+__global__ void v2_source_k(V2Args a, i64 s, u64* __restrict__ f, int cin) {
+    a.dist[s] = 0;
+    f[s >> 6] = 1ull << (s & 63);
+    a.ctl->cnt[cin][0].v = 1;
+}
+
 }  // namespace
 
 struct DeltaWork {
@@ -506,14 +1317,74 @@ struct DeltaWork {
     DevBuf<u32> lsplit;
     DTot* host = nullptr;  // mapped pinned
     u32 lsplit_delta = 0;  // delta lsplit was computed for (0 = none)
+    u64 heavy_total = 0;   // edges with w >= delta (for the pull decision)
+    u64 light_total = 0;   // edges with w < delta
+    // v2 band loop
+    DevBuf<u64> f[2], mb;
+    DevBuf<V2Ctl> ctl;
+    V2Ctl* hctl = nullptr;  // pinned host copy
+    DevBuf<u32> hv;
+    DevBuf<u64> hbeg, hoff;
+    u64 hcap = 0;
+    DevBuf<u32> lcv, lcc;  // long light rows: (vertex, chunk) work items
+    u64 nlc = 0;
     ~DeltaWork() {
         if (host) (void)hipHostFree(host);
+        if (hctl) (void)hipHostFree(hctl);
     }
 };
 
 void delete_delta_work(DeltaWork* p) { delete p; }
 
 namespace {
+
+// delta (explicit option, else 6 * mean weight / mean out-degree over all input
+// ids: light edges are then ~10% of a row; swept on Kronecker s22 / s26 with
+// weights 1..255, profiles/r01/delta_sweep.txt) and, once per delta, the light
+// prefix length of every row and the number of heavy edges.
+template <typename Off>
+int32_t prepare_delta(Graph& g, DeltaWork& w) {
+    Ctx& ctx = *g.ctx;
+    hipStream_t s = ctx.stream;
+    Relabeled& R = *g.rl;
+    const i64 n = R.n_scan;
+    const Off* row = static_cast<const Off*>(R.row_ptr(g.off64));
+    const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
+    int32_t delta = (int32_t)g.delta;
+    if (delta <= 0) {
+        const double mean_deg = g.n ? (double)g.nnz / (double)g.n : 1.0;
+        const double d = 6.0 * g.mean_weight / std::max(1.0, mean_deg);
+        delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(d)));
+    }
+    if (w.lsplit_delta != (u32)delta && n > 0) {
+        light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)delta, w.lsplit.p);
+        PJ_LAUNCH_CHECK();
+        w.lsplit_delta = (u32)delta;
+        DevBuf<u64> acc(1);
+        PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
+        wsum_k<<<grid_for(n, DB, maxgrid), DB, 0, s>>>(w.lsplit.p, n, acc.p);
+        PJ_LAUNCH_CHECK();
+        u64 light = 0;
+        PJ_HIP(hipMemcpyAsync(&light, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+        w.heavy_total = (u64)g.nnz - light;
+        w.light_total = light;
+        PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
+        v2_long_count_k<<<grid_for(n, 256, maxgrid), 256, 0, s>>>(w.lsplit.p, n, acc.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipMemcpyAsync(&w.nlc, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+        w.lcv.alloc(std::max<u64>(w.nlc, 1));
+        w.lcc.alloc(std::max<u64>(w.nlc, 1));
+        PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
+        if (w.nlc) {
+            v2_long_fill_k<<<grid_for(n, 256, maxgrid), 256, 0, s>>>(w.lsplit.p, n, acc.p, w.lcv.p, w.lcc.p);
+            PJ_LAUNCH_CHECK();
+        }
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+    return delta;
+}
 
 template <typename Off>
 void delta_run(Graph& g, DeltaWork& w, i64 source) {
@@ -525,20 +1396,7 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
     const Off* row = static_cast<const Off*>(R.row_ptr(g.off64));
     const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
 
-    // delta: explicit option, else 6 * mean weight / mean out-degree (over all
-    // input ids) — light edges are then ~10% of a row. Swept on Kronecker s22 and
-    // s26 with weights 1..255 (profiles/r01/delta_sweep.txt): flat from 24 to 48.
-    int32_t delta = (int32_t)g.delta;
-    if (delta <= 0) {
-        const double mean_deg = g.n ? (double)g.nnz / (double)g.n : 1.0;
-        const double d = 6.0 * g.mean_weight / std::max(1.0, mean_deg);
-        delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(d)));
-    }
-    if (w.lsplit_delta != (u32)delta && n > 0) {
-        light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)delta, w.lsplit.p);
-        PJ_LAUNCH_CHECK();
-        w.lsplit_delta = (u32)delta;
-    }
+    const int32_t delta = prepare_delta<Off>(g, w);
 
     SelArgs a{};
     a.n = n;
@@ -571,6 +1429,7 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
         PJ_LAUNCH_CHECK();
         sel_scan_k<<<1, SCAN_T, 0, s>>>(a);
         PJ_LAUNCH_CHECK();
+        if (PJ_SCAN_HOSTCOPY) PJ_HIP(hipMemcpyAsync(w.host, w.tot.p, sizeof(DTot), hipMemcpyDeviceToHost, s));
         PJ_HIP(hipStreamSynchronize(s));
         const volatile DTot* h = w.host;
         DTot t;
@@ -621,6 +1480,8 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
         d_source_k<<<1, 1, 0, s>>>(ls, R.dist.p);
         PJ_LAUNCH_CHECK();
         long long lo = 0;
+        u64 heavy_left = w.heavy_total;  // heavy edges of vertices not settled yet
+        const bool can_pull = g.symmetric && g.pull_factor > 0.0;
         while (lo < INT_INF) {
             const int32_t hi = (int32_t)std::min<long long>(lo + delta, INT_INF);
             DTot t = select(SEL_DIST_L, (int32_t)lo, hi);
@@ -643,7 +1504,195 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
                     b = select(SEL_BITS, (int32_t)lo, hi);
                 }
             }
-            if (t.nh > 0) relax(SEL_DIST_H, t, hi);
+            // heavy edges: push the members' (t.mh) or let the unsettled vertices
+            // pull (at most heavy_left edges, cut early by the weight order)
+            heavy_left = heavy_left > t.mh ? heavy_left - t.mh : 0;
+            if (t.nh > 0) {
+                if (can_pull && (double)heavy_left < g.pull_factor * (double)t.mh) {
+                    d_pull_heavy_k<Off><<<maxgrid, DB, 0, s>>>(row, w.lsplit.p, R.col.p, R.w.p, R.dist.p, n,
+                                                               (int32_t)lo, hi);
+                    PJ_LAUNCH_CHECK();
+                    st.bu_levels++;
+                } else {
+                    relax(SEL_DIST_H, t, hi);
+                    st.td_levels++;
+                }
+            }
+            lo = hi;
+        }
+    }
+    if (g.n > 0) {
+        unlabel_k<<<grid_for(g.n, 256, maxgrid), 256, 0, s>>>(R.inv.p, R.dist.p, g.n, n, g.dist.p);
+        PJ_LAUNCH_CHECK();
+        if (valid && ls >= n) d_source_k<<<1, 1, 0, s>>>(source, g.dist.p);  // a source without edges
+    }
+    PJ_HIP(hipEventRecord(g.ev1, s));
+    PJ_HIP(hipEventSynchronize(g.ev1));
+    float ms = 0.f;
+    PJ_HIP(hipEventElapsedTime(&ms, g.ev0, g.ev1));
+    st.kernel_ms = ms;
+    st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+    g.stats = st;
+    g.have_result = true;
+}
+
+template <typename Off>
+void delta2_run(Graph& g, DeltaWork& w, i64 source) {
+    Ctx& ctx = *g.ctx;
+    hipStream_t s = ctx.stream;
+    Relabeled& R = *g.rl;
+    const i64 n = R.n_scan;
+    const i64 nwords = (n + 63) / 64;
+    const Off* row = static_cast<const Off*>(R.row_ptr(g.off64));
+    const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
+    const int32_t delta = prepare_delta<Off>(g, w);
+    if (!w.hctl) {
+        const size_t nw = nwords ? (size_t)nwords : 1;
+        w.f[0].alloc(nw);
+        w.f[1].alloc(nw);
+        w.mb.alloc(nw);
+        w.ctl.alloc(1);
+        w.hcap = (u64)std::max<i64>(1, std::min<i64>(n, g.nnz / (i64)V2_HT + 1));
+        w.hv.alloc(3 * w.hcap);
+        w.hbeg.alloc(3 * w.hcap);
+        w.hoff.alloc(3 * w.hcap);
+        PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.hctl), sizeof(V2Ctl), hipHostMallocDefault));
+    }
+    V2Args a{};
+    a.n = n;
+    a.nwords = nwords;
+    a.dist = R.dist.p;
+    a.lsplit = w.lsplit.p;
+    a.col = R.col.p;
+    a.wt = R.w.p;
+    a.mb = w.mb.p;
+    a.ctl = w.ctl.p;
+    a.hv = w.hv.p;
+    a.hbeg = w.hbeg.p;
+    a.hoff = w.hoff.p;
+    a.hcap = w.hcap;
+    auto sync_ctl = [&]() {
+        PJ_HIP(hipMemcpyAsync(w.hctl, w.ctl.p, sizeof(V2Ctl), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+    };
+    auto slot = [&](int c) {
+        u64 t = 0;
+        for (int i = 0; i < V2_NSH; ++i) t += w.hctl->cnt[c][i].v;
+        return t;
+    };
+    auto reset_minv = [&]() { PJ_HIP(hipMemsetAsync(&w.ctl.p->minv, 0xFF, sizeof(V2Line), s)); };
+
+    pj_stats st{};
+    auto t_host0 = std::chrono::steady_clock::now();
+    PJ_HIP(hipEventRecord(g.ev0, s));
+    const bool valid = source >= 0 && source < g.n;
+    const i64 ls = valid ? (i64)R.inv_h[(size_t)source] : -1;
+    if (n > 0) {
+        PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(R.dist.p), INT_INF, (size_t)n, s));
+        PJ_HIP(hipMemsetAsync(w.f[0].p, 0, sizeof(u64) * (size_t)nwords, s));
+        PJ_HIP(hipMemsetAsync(w.f[1].p, 0, sizeof(u64) * (size_t)nwords, s));
+        PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
+        PJ_HIP(hipMemsetAsync(w.ctl.p, 0, sizeof(V2Ctl), s));
+    }
+    if (valid && ls < n) {
+        int cs = 0, hr = 0, fi = 0;
+        v2_source_k<<<1, 1, 0, s>>>(a, ls, w.f[fi].p, cs);
+        PJ_LAUNCH_CHECK();
+        long long lo = 0;
+        u64 heavy_left = w.heavy_total, light_left = w.light_total;
+        const bool can_pull = g.symmetric && g.pull_factor > 0.0;
+        const bool can_pull_light = g.symmetric && g.light_pull > 0.0;
+        u64 last_fe = 1;  // light edges of the frontier at the last host sync (round 0: unknown)
+        while (lo < INT_INF) {
+            const int32_t hi = (int32_t)std::min<long long>(lo + delta, INT_INF);
+            const int32_t nhi = (int32_t)std::min<long long>((long long)hi + delta, INT_INF);
+            a.lo = (int32_t)lo;
+            a.hi = hi;
+            st.levels++;
+            PJ_HIP(hipMemsetAsync(w.ctl.p->mh, 0, sizeof(w.ctl.p->mh), s));
+            // light rounds until the band's frontier is empty
+            int K = PJ_V2_STATS ? 1 : 2;
+            for (;;) {
+                const u64 pull_thresh = can_pull_light ? (u64)((double)light_left / g.light_pull) : ~0ull;
+                // launch the pull kernels (which decide on the device, per round) only
+                // when the last frontier seen could grow past the threshold in this batch
+                const bool try_pull = can_pull_light && last_fe * 64 > pull_thresh;
+                for (int q = 0; q < K; ++q) {
+                    if (try_pull) {
+                        v2_pull_light_k<Off><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh);
+                        PJ_LAUNCH_CHECK();
+                        if (w.nlc) {
+                            v2_pull_long_k<Off><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh,
+                                                                       w.lcv.p, w.lcc.p, w.nlc);
+                            PJ_LAUNCH_CHECK();
+                        }
+                    }
+                    // (without the pull kernels the expand must push every round)
+                    v2_expand_k<Off, true><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, hr,
+                                                                  try_pull ? pull_thresh : ~0ull);
+                    PJ_LAUNCH_CHECK();
+                    v2_hub_k<true><<<maxgrid, DB, 0, s>>>(a, w.f[1 - fi].p, cs, hr, (hr + 1) % 3);
+                    PJ_LAUNCH_CHECK();
+                    fi ^= 1;
+                    cs = (cs + 1) & 3;
+                    hr = (hr + 1) % 3;
+                    st.relax_rounds++;
+                }
+                sync_ctl();
+                last_fe = 0;
+                for (int i = 0; i < V2_NSH; ++i) last_fe += w.hctl->cnt[cs][i].pad[0];
+                if (PJ_V2_STATS) {
+                    fprintf(stderr, "band %d lo %lld rounds %d: frontier %llu edges %llu atomics %llu marks %llu next %llu\n",
+                            (int)st.levels, lo, K, w.hctl->dbg[0].v, w.hctl->dbg[1].v, w.hctl->dbg[2].v,
+                            w.hctl->dbg[3].v, slot(cs));
+                    PJ_HIP(hipMemsetAsync(w.ctl.p->dbg, 0, sizeof(w.ctl.p->dbg), s));
+                }
+                if (slot(cs) == 0) break;
+                K = PJ_V2_STATS ? 1 : std::min(2 * K, 16);
+            }
+            u64 mh = 0, ml = 0;
+            for (int i = 0; i < V2_NSH; ++i) {
+                mh += w.hctl->mh[i].v;
+                ml += w.hctl->mh[i].pad[0];
+            }
+            heavy_left = heavy_left > mh ? heavy_left - mh : 0;
+            light_left = light_left > ml ? light_left - ml : 0;
+            reset_minv();
+            if (can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh) {
+                v2_pull_k<Off><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi, cs);
+                PJ_LAUNCH_CHECK();
+                PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
+                st.bu_levels++;
+            } else {
+                if (mh > 0) {
+                    v2_expand_k<Off, false><<<maxgrid, DB, 0, s>>>(a, row, w.mb.p, nullptr, cs, hr, ~0ull);
+                    PJ_LAUNCH_CHECK();
+                    v2_hub_k<false><<<maxgrid, DB, 0, s>>>(a, nullptr, cs, hr, (hr + 1) % 3);
+                    PJ_LAUNCH_CHECK();
+                    hr = (hr + 1) % 3;
+                    st.td_levels++;
+                } else {
+                    PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
+                }
+                a.lo = hi;
+                a.hi = nhi;
+                v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
+                PJ_LAUNCH_CHECK();
+            }
+            sync_ctl();
+            last_fe = 0;
+            for (int i = 0; i < V2_NSH; ++i) last_fe += w.hctl->cnt[cs][i].pad[0];
+            if (slot(cs) == 0) {
+                const u64 mv = w.hctl->minv.v;
+                if (mv >= (u64)INT_INF) break;  // nothing reached beyond the settled bands
+                lo = (long long)mv / delta * delta;  // jump to the next occupied band
+                a.lo = (int32_t)lo;
+                a.hi = (int32_t)std::min<long long>(lo + delta, INT_INF);
+                reset_minv();
+                v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
+                PJ_LAUNCH_CHECK();
+                continue;
+            }
             lo = hi;
         }
     }
@@ -708,8 +1757,13 @@ void delta_solve(Graph& g, i64 source) {
         }
         g.mean_weight = g.nnz > 0 ? (double)sum / (double)g.nnz : 1.0;
     }
-    if (g.off64) delta_run<u64>(g, *g.delta_work, source);
-    else delta_run<u32>(g, *g.delta_work, source);
+    if (g.delta_impl == 1) {
+        if (g.off64) delta_run<u64>(g, *g.delta_work, source);
+        else delta_run<u32>(g, *g.delta_work, source);
+    } else {
+        if (g.off64) delta2_run<u64>(g, *g.delta_work, source);
+        else delta2_run<u32>(g, *g.delta_work, source);
+    }
 }
 
 }  // namespace pj

@@ -72,6 +72,30 @@ __device__ __forceinline__ T block_sum(T x, T* lds) {
     return tot;
 }
 
+// position of the r-th set bit (0-based) of w; r < popcount(w)
+__device__ __forceinline__ u32 select_bit(u64 w, u32 r) {
+    u32 base = 0;
+#pragma unroll
+    for (int half = 32; half >= 8; half >>= 1) {
+        const u64 lo = w & ((1ull << half) - 1ull);
+        const u32 c = (u32)__popcll(lo);
+        if (r >= c) {
+            r -= c;
+            w >>= half;
+            base += half;
+        } else {
+            w = lo;
+        }
+    }
+    for (u32 k = 0; k < 8; ++k) {
+        if ((w >> k) & 1ull) {
+            if (r == 0) return base + k;
+            --r;
+        }
+    }
+    return base;
+}
+
 // Wave-aggregated append: one atomic per wave for all lanes with pred set.
 // Returns this lane's slot (valid only when pred).
 __device__ __forceinline__ u64 wave_append(bool pred, u64* counter) {

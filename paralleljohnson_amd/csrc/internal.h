@@ -185,6 +185,11 @@ struct Graph {
 
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;
+    double pull_factor = 4.0;
+    double light_pull = 2.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
+                               // the light edges of unsettled vertices / light_pull (0 = never)
+    int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based  // weighted, symmetric: pull a band's heavy edges when the heavy edges
+                               // of unsettled vertices < pull_factor x the members' heavy edges (0 = never)
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
     int level_batch = 0; // BFS levels enqueued per host check (0 = default 8, doubling)
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = default 4)

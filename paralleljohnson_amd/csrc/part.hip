@@ -379,30 +379,6 @@ __global__ void part_apply_k(PartArgs a, const u32* __restrict__ recv, i64 nr, i
     }
 }
 
-// position of the r-th set bit (0-based) of w; r < popcount(w)
-__device__ __forceinline__ u32 select_bit(u64 w, u32 r) {
-    u32 base = 0;
-#pragma unroll
-    for (int half = 32; half >= 8; half >>= 1) {
-        const u64 lo = w & ((1ull << half) - 1ull);
-        const u32 c = (u32)__popcll(lo);
-        if (r >= c) {
-            r -= c;
-            w >>= half;
-            base += half;
-        } else {
-            w = lo;
-        }
-    }
-    for (u32 k = 0; k < 8; ++k) {
-        if ((w >> k) & 1ull) {
-            if (r == 0) return base + k;
-            --r;
-        }
-    }
-    return base;
-}
-
 __device__ __forceinline__ bool vbit(const u64* vis, u32 u) { return (vis[u >> 6] >> (u & 63)) & 1ull; }
 
 // Pull level over the owned slice. A wave screens SC own words, compacts their

@@ -148,10 +148,12 @@ def test_weighted_delta_stepping(ctx, oracle):
         perm = np.lexsort((wc, rid))
         assert (grow == row).all()
         assert (gcol.astype(np.uint32) == col[perm]).all() and (gw == wc[perm]).all()
-        for delta in (0, 1, 37):
-            g.set_option("delta", delta)
-            for r in (int(src[0]) if len(src) else 0, int(rng.integers(0, n))):
-                assert (g.sssp(r) == oracle.dijkstra(row, col, wc, r)).all(), (trial, delta, r)
+        for impl in (1, 2):  # list-based and bitmap-frontier band loops (delta.hip)
+            g.set_option("delta_impl", impl)
+            for delta in (0, 1, 37):
+                g.set_option("delta", delta)
+                for r in (int(src[0]) if len(src) else 0, int(rng.integers(0, n))):
+                    assert (g.sssp(r) == oracle.dijkstra(row, col, wc, r)).all(), (trial, impl, delta, r)
         g.close()
 
 
@@ -171,9 +173,11 @@ def test_weighted_deferral_paths(ctx, oracle):
         w = rng.integers(0, wmax, len(src)).astype(np.uint32)
         g = ctx.load_coo(src, dst, w=w, n=n)
         row, col, wc = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n, w)
-        for delta in (0, 8, 1000):
-            g.set_option("delta", delta)
-            assert (g.sssp(0) == oracle.dijkstra(row, col, wc, 0)).all(), (wmax, delta)
+        for impl in (1, 2):
+            g.set_option("delta_impl", impl)
+            for delta in (0, 8, 1000):
+                g.set_option("delta", delta)
+                assert (g.sssp(0) == oracle.dijkstra(row, col, wc, 0)).all(), (wmax, impl, delta)
         g.close()
 
 
@@ -187,6 +191,33 @@ def test_weighted_text_and_kronecker(ctx, oracle):
     col = col.astype(np.uint32)
     for r in g.sample_roots(8, 3):
         assert (g.sssp(int(r)) == oracle.dijkstra(row, col, wc, int(r))).all()
+
+
+@pytest.mark.parametrize("scale,ef", [(12, 16), (14, 4), (16, 1), (15, 16)])
+def test_weighted_pull_heavy(ctx, oracle, scale, ef):
+    """Heavy edges by pull (symmetric graphs): never (push only), by the default
+    rule, and in every band; several deltas. Bit-exact against the oracle Dijkstra."""
+    g = ctx.generate_kronecker(scale, ef, 9 + scale, weighted=True)
+    row, col, wc = g.get_csr()
+    col = col.astype(np.uint32)
+    roots = [int(r) for r in g.sample_roots(3 + ef, 3)]
+    exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
+    # (band loop, heavy pull factor, light pull factor): list-based; bitmap with
+    # push only, default rules, pull whenever possible
+    for impl, pf, lp in ((1, 1.0, 0.0), (2, 0.0, 0.0), (2, 4.0, 2.0), (2, 1e15, 1e15)):
+        g.set_option("delta_impl", impl)
+        g.set_option("pull_factor", pf)
+        g.set_option("light_pull", lp)
+        for delta in (0, 7, 60):
+            g.set_option("delta", delta)
+            for r in roots:
+                assert (g.sssp(r) == exp[r]).all(), (impl, pf, lp, delta, r)
+                st = g.stats()
+                if pf == 0.0:
+                    assert st["bu_levels"] == 0
+                if pf == 1e15:
+                    assert st["td_levels"] == 0
+    g.close()
 
 
 def test_batch_and_empty(ctx, oracle):

@@ -6,4 +6,5 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method threa
 timeout -k 10 200 python -u tools/probe_weighted_scales.py 26 > $OUT/wscales.log 2>&1 || { echo probe failed; tail -20 $OUT/wscales.log; exit 1; }
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py --no-cpu-baseline --no-secondary --no-partitioned --steps 8 --warmup 1 > $OUT/kt.log 2>&1 || { echo kt failed; tail -20 $OUT/kt.log; exit 1; }
+timeout -k 10 200 python -u tools/probe_weighted.py 26 8 12 16 32 > $OUT/dsweep.log 2>&1 || { echo dsweep failed; exit 1; }
 echo quick ok
