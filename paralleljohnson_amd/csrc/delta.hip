@@ -508,6 +508,151 @@ __global__ void unlabel_k(const u32* __restrict__ inv, const int32_t* __restrict
 }
 
 // lsplit[v] = number of edges of v with weight < delta (rows are weight-sorted)
+// Serial probes of a weight-sorted row, PU edges per step with independent
+// loads (the probes are latency-bound; one edge per step leaves the memory
+// system idle). Weights ascend along the row, so once lo + w >= cur for an
+// edge, that edge and every later one are useless: the step returns true.
+constexpr int PU = 4;
+// pull from band members [lo, hi)
+template <typename Off>
+__device__ __forceinline__ bool pull_step_band(const u32* __restrict__ wt, const u32* __restrict__ col,
+                                               const int32_t* __restrict__ dist, Off& k, Off lim, int32_t lo,
+                                               int32_t hi, int32_t& cur) {
+    u32 w[PU], u[PU];
+    bool ok[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        ok[j] = k + (Off)j < lim;
+        w[j] = ok[j] ? wt[k + j] : 0u;
+        u[j] = ok[j] ? col[k + j] : 0u;
+    }
+    bool stop = false;
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        if (ok[j] && (long long)lo + w[j] >= (long long)cur) stop = true;
+        ok[j] = ok[j] && !stop;
+        nv += ok[j];
+    }
+    int32_t du[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) du[j] = ok[j] ? dist[u[j]] : INT_INF;
+#pragma unroll
+    for (int j = 0; j < PU; ++j)
+        if (ok[j] && du[j] >= lo && du[j] < hi) {
+            const long long nd = (long long)du[j] + w[j];
+            if (nd < cur) cur = (int32_t)nd;
+        }
+    k += (Off)nv;
+    return stop;
+}
+// pull from the frontier bitmap fin (members of the band's last round)
+template <typename Off>
+__device__ __forceinline__ bool pull_step_fin(const u32* __restrict__ wt, const u32* __restrict__ col,
+                                              const int32_t* __restrict__ dist, const u64* __restrict__ fin, Off& k,
+                                              Off lim, int32_t lo, int32_t& cur) {
+    u32 w[PU], u[PU];
+    bool ok[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        ok[j] = k + (Off)j < lim;
+        w[j] = ok[j] ? wt[k + j] : 0u;
+        u[j] = ok[j] ? col[k + j] : 0u;
+    }
+    bool stop = false;
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        if (ok[j] && (long long)lo + w[j] >= (long long)cur) stop = true;
+        ok[j] = ok[j] && !stop;
+        nv += ok[j];
+    }
+    u64 fw[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) fw[j] = ok[j] ? fin[u[j] >> 6] : 0ull;
+    int32_t du[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) du[j] = (ok[j] && ((fw[j] >> (u[j] & 63)) & 1ull)) ? dist[u[j]] : INT_INF;
+#pragma unroll
+    for (int j = 0; j < PU; ++j)
+        if (du[j] < INT_INF) {
+            const long long nd = (long long)du[j] + w[j];
+            if (nd < cur) cur = (int32_t)nd;
+        }
+    k += (Off)nv;
+    return stop;
+}
+
+// the same over interleaved edges (col | w << 32)
+template <typename Off>
+__device__ __forceinline__ bool pull_step_band_cw(const u64* __restrict__ ed, const int32_t* __restrict__ dist, Off& k,
+                                                  Off lim, int32_t lo, int32_t hi, int32_t& cur) {
+    u32 w[PU], u[PU];
+    bool ok[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        ok[j] = k + (Off)j < lim;
+        const u64 x = ok[j] ? ed[k + j] : 0ull;
+        w[j] = (u32)(x >> 32);
+        u[j] = (u32)x;
+    }
+    bool stop = false;
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        if (ok[j] && (long long)lo + w[j] >= (long long)cur) stop = true;
+        ok[j] = ok[j] && !stop;
+        nv += ok[j];
+    }
+    int32_t du[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) du[j] = ok[j] ? dist[u[j]] : INT_INF;
+#pragma unroll
+    for (int j = 0; j < PU; ++j)
+        if (ok[j] && du[j] >= lo && du[j] < hi) {
+            const long long nd = (long long)du[j] + w[j];
+            if (nd < cur) cur = (int32_t)nd;
+        }
+    k += (Off)nv;
+    return stop;
+}
+template <typename Off>
+__device__ __forceinline__ bool pull_step_fin_cw(const u64* __restrict__ ed, const int32_t* __restrict__ dist,
+                                                 const u64* __restrict__ fin, Off& k, Off lim, int32_t lo,
+                                                 int32_t& cur) {
+    u32 w[PU], u[PU];
+    bool ok[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        ok[j] = k + (Off)j < lim;
+        const u64 x = ok[j] ? ed[k + j] : 0ull;
+        w[j] = (u32)(x >> 32);
+        u[j] = (u32)x;
+    }
+    bool stop = false;
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        if (ok[j] && (long long)lo + w[j] >= (long long)cur) stop = true;
+        ok[j] = ok[j] && !stop;
+        nv += ok[j];
+    }
+    u64 fw[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) fw[j] = ok[j] ? fin[u[j] >> 6] : 0ull;
+    int32_t du[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) du[j] = (ok[j] && ((fw[j] >> (u[j] & 63)) & 1ull)) ? dist[u[j]] : INT_INF;
+#pragma unroll
+    for (int j = 0; j < PU; ++j)
+        if (du[j] < INT_INF) {
+            const long long nd = (long long)du[j] + w[j];
+            if (nd < cur) cur = (int32_t)nd;
+        }
+    k += (Off)nv;
+    return stop;
+}
+
 // Pull step for the heavy edges of band [lo, hi) — symmetric graphs only, where
 // a row is also the vertex's in-edges with the same weights. Every vertex with
 // dist >= hi looks through the heavy part of its own row (weights ascending)
@@ -569,17 +714,10 @@ __global__ __launch_bounds__(DB) void d_pull_heavy_k(const Off* __restrict__ row
             bool go = act && k < lim, done = !act || k >= e;
             while (__ballot(go)) {
                 if (go) {
-                    const u32 w = wt[k];
-                    if ((long long)lo + w >= (long long)cur) {
+                    if (pull_step_band<Off>(wt, col, dist, k, lim, lo, hi, cur)) {
                         done = true;
                         go = false;
                     } else {
-                        const int32_t du = dist[col[k]];
-                        if (du >= lo && du < hi) {
-                            const long long nd = (long long)du + w;
-                            if (nd < cur) cur = (int32_t)nd;
-                        }
-                        ++k;
                         go = k < lim;
                         done = k >= e;
                     }
@@ -701,8 +839,9 @@ struct V2Args {
     int32_t lo, hi;
     int32_t* dist;
     const u32* lsplit;
-    const u32* col;
-    const u32* wt;
+    const u64* cw;    // edges interleaved: col | w << 32 (the relabeled CSR)
+    const u64* lrow;  // light CSR: the light prefixes of the rows, packed
+    const u64* lcw;
     u64* mb;
     V2Ctl* ctl;
     u32* hv;     // [3][hcap]
@@ -720,9 +859,11 @@ __device__ __forceinline__ u64 v2_slot_sum(const V2Line* sl) {
 
 // one relaxation; LIGHT: a target lowered below hi is marked in fout (returns 1 if newly marked)
 template <bool LIGHT>
-__device__ __forceinline__ u32 v2_relax(const V2Args& a, u64 k, int32_t du, u64* __restrict__ fout, u64& fe) {
-    const u32 t = a.col[k];
-    const long long nd = (long long)du + (long long)a.wt[k];
+__device__ __forceinline__ u32 v2_relax(const V2Args& a, const u64* __restrict__ ed, u64 k, int32_t du,
+                                        u64* __restrict__ fout, u64& fe) {
+    const u64 x = ed[k];
+    const u32 t = (u32)x;
+    const long long nd = (long long)du + (long long)(x >> 32);
     if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[1].v, 1ull);
     if (nd < INT_INF && (int32_t)nd < dist_now(a.dist + t)) {
         if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
@@ -752,6 +893,41 @@ __device__ __forceinline__ u64 v2_slot_edges(const V2Line* sl) {
 #pragma unroll
     for (int i = 0; i < V2_NSH; ++i) t += sl[i].pad[0];
     return t;
+}
+
+// PU consecutive edges [k, min(k + PU, lim)) of one source in one step (independent loads).
+template <bool LIGHT>
+__device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const u64* __restrict__ ed, u64 k, u64 lim, int32_t du,
+                                          u64* __restrict__ fout, u64& fe) {
+    u32 t[PU];
+    long long nd[PU];
+    bool ok[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        ok[j] = k + j < lim;
+        const u64 x = ok[j] ? ed[k + j] : 0ull;
+        t[j] = (u32)x;
+        nd[j] = (long long)du + (long long)(x >> 32);
+        ok[j] = ok[j] && nd[j] < INT_INF;
+    }
+    int32_t cd[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) cd[j] = ok[j] ? dist_now(a.dist + t[j]) : 0;
+    u32 newc = 0;
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        if (ok[j] && (int32_t)nd[j] < cd[j]) {
+            const int32_t old = atomicMin(a.dist + t[j], (int32_t)nd[j]);
+            if (LIGHT && (int32_t)nd[j] < old && (int32_t)nd[j] < a.hi) {
+                const u64 bit = 1ull << (t[j] & 63);
+                if (!(atomicOr(fout + (t[j] >> 6), bit) & bit)) {
+                    ++newc;
+                    fe += a.lsplit[t[j]];
+                }
+            }
+        }
+    }
+    return newc;
 }
 
 // LIGHT: relax the light prefixes of fin's vertices (a band round); HEAVY: the
@@ -817,18 +993,16 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
                 const u32 bit = select_bit(tw, c - ex);
                 v = (u32)((wbase + jw) * 64 + bit);
                 du = a.dist[v];
-                const u64 rb = (u64)row[v];
-                const u64 ls = a.lsplit[v];
                 if (PJ_V2_STATS && LIGHT) atomicAdd(&a.ctl->dbg[0].v, 1ull);
-                if (LIGHT) {
-                    b = rb;
-                    e = rb + ls;
+                if (LIGHT) {  // light CSR
+                    b = a.lrow[v];
+                    e = a.lrow[v + 1];
                     if ((tn >> bit) & 1ull) {
-                        mh += (u64)row[v + 1] - rb - ls;
-                        ml += ls;
+                        mh += (u64)row[v + 1] - (u64)row[v] - (e - b);
+                        ml += e - b;
                     }
-                } else {
-                    b = rb + ls;
+                } else {      // heavy suffix of the row
+                    b = (u64)row[v] + a.lsplit[v];
                     e = (u64)row[v + 1];
                 }
             }
@@ -858,8 +1032,8 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
             bool go = k < lim;
             while (__ballot(go)) {
                 if (go) {
-                    newc += v2_relax<LIGHT>(a, k, du, fout, fe);
-                    ++k;
+                    newc += v2_relax_n<LIGHT>(a, LIGHT ? a.lcw : a.cw, k, lim, du, fout, fe);
+                    k = k + PU < lim ? k + PU : lim;
                     go = k < lim;
                 }
             }
@@ -872,7 +1046,7 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
                 const int32_t dl = __shfl(du, l, 64);
                 for (u64 kk = kb; kk < ke; kk += WAVE) {
                     const u64 k0 = kk + lane;
-                    if (k0 < ke) newc += v2_relax<LIGHT>(a, k0, dl, fout, fe);
+                    if (k0 < ke) newc += v2_relax<LIGHT>(a, LIGHT ? a.lcw : a.cw, k0, dl, fout, fe);
                 }
             }
         }
@@ -914,7 +1088,7 @@ __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout,
             const u64 e = e0 + (u64)j * DB + threadIdx.x;
             if (e < total) {
                 const u32 sl = lb_find<V2_HTILE>(sh, ns, e);
-                newc += v2_relax<LIGHT>(a, s_b[sl] + (e - sh.off[sl]), s_du[sl], fout, fe);
+                newc += v2_relax<LIGHT>(a, LIGHT ? a.lcw : a.cw, s_b[sl] + (e - sh.off[sl]), s_du[sl], fout, fe);
             }
         }
         __syncthreads();
@@ -1000,22 +1174,15 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                 cur = d0;
                 k = row[v] + (Off)a.lsplit[v];
                 e = row[v + 1];
-            }
+            }  // (edges in a.cw)
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
             bool go = act && k < lim, done = !act || k >= e;
             while (__ballot(go)) {
                 if (go) {
-                    const u32 w = a.wt[k];
-                    if ((long long)lo + w >= (long long)cur) {
+                    if (pull_step_band_cw<Off>(a.cw, a.dist, k, lim, lo, hi, cur)) {
                         done = true;
                         go = false;
                     } else {
-                        const int32_t du = a.dist[a.col[k]];
-                        if (du >= lo && du < hi) {
-                            const long long nd = (long long)du + w;
-                            if (nd < cur) cur = (int32_t)nd;
-                        }
-                        ++k;
                         go = k < lim;
                         done = k >= e;
                     }
@@ -1030,11 +1197,12 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                 for (Off kk = kb; kk < ke; kk += WAVE) {
                     const Off k0 = kk + lane;
                     const bool valid = k0 < ke;
-                    const u32 w = valid ? a.wt[k0] : 0u;
+                    const u64 x = valid ? a.cw[k0] : 0ull;
+                    const u32 w = (u32)(x >> 32);
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
                     int32_t cand = INT_INF;
                     if (!stop) {
-                        const int32_t du = a.dist[a.col[k0]];
+                        const int32_t du = a.dist[(u32)x];
                         if (du >= lo && du < hi) {
                             const long long nd = (long long)du + w;
                             cand = nd < INT_INF ? (int32_t)nd : INT_INF;
@@ -1146,25 +1314,18 @@ __global__ __launch_bounds__(DB) void v2_pull_light_k(V2Args a, const Off* __res
             if (act) {
                 d0 = a.dist[v];
                 cur = d0;
-                k = row[v];
-                ls = a.lsplit[v];
+                k = (Off)a.lrow[v];
+                ls = (u32)(a.lrow[v + 1] - a.lrow[v]);
                 e = ls > V2_PLMAX ? k : k + (Off)ls;  // long rows: v2_pull_long_k
             }
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
             bool go = act && k < lim, done = !act || k >= e;
             while (__ballot(go)) {
                 if (go) {
-                    const u32 w = a.wt[k];
-                    if ((long long)lo + w >= (long long)cur) {
+                    if (pull_step_fin_cw<Off>(a.lcw, a.dist, fin, k, lim, lo, cur)) {
                         done = true;
                         go = false;
                     } else {
-                        const u32 u = a.col[k];
-                        if ((fin[u >> 6] >> (u & 63)) & 1ull) {
-                            const long long nd = (long long)a.dist[u] + w;
-                            if (nd < cur) cur = (int32_t)nd;
-                        }
-                        ++k;
                         go = k < lim;
                         done = k >= e;
                     }
@@ -1179,11 +1340,12 @@ __global__ __launch_bounds__(DB) void v2_pull_light_k(V2Args a, const Off* __res
                 for (Off kk = kb; kk < ke; kk += WAVE) {
                     const Off k0 = kk + lane;
                     const bool valid = k0 < ke;
-                    const u32 w = valid ? a.wt[k0] : 0u;
+                    const u64 x = valid ? a.lcw[k0] : 0ull;
+                    const u32 w = (u32)(x >> 32);
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
                     int32_t cand = INT_INF;
                     if (!stop) {
-                        const u32 u = a.col[k0];
+                        const u32 u = (u32)x;
                         if ((fin[u >> 6] >> (u & 63)) & 1ull) {
                             const long long nd = (long long)a.dist[u] + w;
                             cand = nd < INT_INF ? (int32_t)nd : INT_INF;
@@ -1237,20 +1399,21 @@ __global__ __launch_bounds__(DB) void v2_pull_long_k(V2Args a, const Off* __rest
         const u32 v = lcv[it];
         const int32_t d0 = dist_now(a.dist + v);
         if (d0 <= lo) continue;
-        const u64 rb = (u64)row[v];
-        const u32 ls = a.lsplit[v];
+        const u64 rb = a.lrow[v];
+        const u32 ls = (u32)(a.lrow[v + 1] - rb);
         const u64 kb = rb + (u64)lcc[it] * V2_PCH;
         const u64 ke = min(rb + ls, kb + V2_PCH);
-        if ((long long)lo + a.wt[kb] >= (long long)d0) continue;
+        if ((long long)lo + (a.lcw[kb] >> 32) >= (long long)d0) continue;
         int32_t cur = d0;
         for (u64 kk = kb; kk < ke; kk += WAVE) {
             const u64 k0 = kk + lane;
             const bool valid = k0 < ke;
-            const u32 w = valid ? a.wt[k0] : 0u;
+            const u64 x = valid ? a.lcw[k0] : 0ull;
+            const u32 w = (u32)(x >> 32);
             const bool stop = !valid || (long long)lo + w >= (long long)cur;
             int32_t cand = INT_INF;
             if (!stop) {
-                const u32 u = a.col[k0];
+                const u32 u = (u32)x;
                 if ((fin[u >> 6] >> (u & 63)) & 1ull) {
                     const long long nd = (long long)a.dist[u] + w;
                     cand = nd < INT_INF ? (int32_t)nd : INT_INF;
@@ -1299,6 +1462,35 @@ __global__ void v2_long_fill_k(const u32* __restrict__ lsplit, i64 n, u64* __res
         }
 }
 
+// Interleaved copy of the relabeled CSR edges: cw[k] = col[k] | w[k] << 32.
+__global__ void v2_interleave_k(const u32* __restrict__ col, const u32* __restrict__ w, i64 m, u64* __restrict__ cw) {
+    for (i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (i64)gridDim.x * blockDim.x)
+        cw[k] = (u64)col[k] | ((u64)w[k] << 32);
+}
+// Light CSR: lcw[lrow[v] + j] = cw[row[v] + j] for j < lsplit[v] (a wave per vertex
+// for long prefixes, a lane per vertex otherwise).
+template <typename Off>
+__global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restrict__ lsplit, const u64* __restrict__ lrow,
+                               const u64* __restrict__ cw, i64 n, u64* __restrict__ lcw) {
+    const int lane = lane_id();
+    for (i64 v0 = ((i64)blockIdx.x * blockDim.x + threadIdx.x) & ~63ll; v0 < n; v0 += (i64)gridDim.x * blockDim.x) {
+        const i64 v = v0 + lane;
+        const u32 ls = v < n ? lsplit[v] : 0u;
+        const bool longp = ls > 64;
+        if (v < n && !longp)
+            for (u32 j = 0; j < ls; ++j) lcw[lrow[v] + j] = cw[(u64)row[v] + j];
+        u64 lm = __ballot(longp);
+        while (lm) {
+            const int l = __ffsll((long long)lm) - 1;
+            lm &= lm - 1;
+            const i64 vl = v0 + l;
+            const u64 src = (u64)row[vl], dst = lrow[vl];
+            const u32 cnt = lsplit[vl];
+            for (u32 j = lane; j < cnt; j += WAVE) lcw[dst + j] = cw[src + j];
+        }
+    }
+}
+
 __global__ void v2_source_k(V2Args a, i64 s, u64* __restrict__ f, int cin) {
     a.dist[s] = 0;
     f[s >> 6] = 1ull << (s & 63);
@@ -1328,6 +1520,9 @@ struct DeltaWork {
     u64 hcap = 0;
     DevBuf<u32> lcv, lcc;  // long light rows: (vertex, chunk) work items
     u64 nlc = 0;
+    DevBuf<u64> cw;        // interleaved relabeled edges
+    ScanWs lscan;
+    DevBuf<u64> lrow, lcw; // light CSR (per delta)
     ~DeltaWork() {
         if (host) (void)hipHostFree(host);
         if (hctl) (void)hipHostFree(hctl);
@@ -1374,6 +1569,18 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         PJ_LAUNCH_CHECK();
         PJ_HIP(hipMemcpyAsync(&w.nlc, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
         PJ_HIP(hipStreamSynchronize(s));
+        // interleaved edges (once) and the light CSR of this delta
+        if (!w.cw.p && g.nnz > 0) {
+            w.cw.alloc((size_t)g.nnz);
+            v2_interleave_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.col.p, R.w.p, g.nnz, w.cw.p);
+            PJ_LAUNCH_CHECK();
+        }
+        w.lrow.alloc((size_t)n + 1);
+        exclusive_scan_u32(w.lsplit.p, w.lrow.p, n, w.lscan, s);
+        w.lcw.alloc(std::max<u64>(light, 1));
+        if (light)
+            v2_light_csr_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, n, w.lcw.p);
+        PJ_LAUNCH_CHECK();
         w.lcv.alloc(std::max<u64>(w.nlc, 1));
         w.lcc.alloc(std::max<u64>(w.nlc, 1));
         PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
@@ -1563,8 +1770,9 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     a.nwords = nwords;
     a.dist = R.dist.p;
     a.lsplit = w.lsplit.p;
-    a.col = R.col.p;
-    a.wt = R.w.p;
+    a.cw = w.cw.p;
+    a.lrow = w.lrow.p;
+    a.lcw = w.lcw.p;
     a.mb = w.mb.p;
     a.ctl = w.ctl.p;
     a.hv = w.hv.p;
