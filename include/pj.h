@@ -199,6 +199,10 @@ int pj_part_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t 
  * the edge list equals its transpose (no in-rows are built). */
 int pj_part_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, int64_t nnz, int64_t n_vertices,
                      int symmetric, int rank, int world, pj_part** out);
+/* The rank's share of a SNAP edge-list file (the pj_load_snap grammar, unit
+ * weights; N = max id + 1 as :319). Every rank parses the file on its GPU and
+ * keeps its rows, so no rank has to scatter (the reference's :344-410). */
+int pj_part_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_part** out);
 int pj_part_destroy(pj_part* p);
 int pj_part_info_get(const pj_part* p, pj_part_info* out);
 /* Copy the rank's isolated-vertex mask (words_per_rank u64, device) to

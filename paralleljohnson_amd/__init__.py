@@ -96,6 +96,7 @@ _SIGS = {
     "pj_set_stream": ([_P, _P], _INT),
     "pj_part_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _INT, _PP], _INT),
     "pj_part_load_coo": ([_P, _P, _P, _I64, _I64, _INT, _INT, _INT, _PP], _INT),
+    "pj_part_load_snap": ([_P, ctypes.c_char_p, _INT, _INT, _PP], _INT),
     "pj_part_destroy": ([_P], _INT),
     "pj_part_info_get": ([_P, _P], _INT),
     "pj_part_zmask": ([_P, _P], _INT),

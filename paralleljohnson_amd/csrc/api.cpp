@@ -556,6 +556,37 @@ int pj_part_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, int64_
     });
 }
 
+int pj_part_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_part** out) {
+    if (!ctx || !path || !out) return arg_error("pj_part_load_snap: bad argument");
+    if (world < 1 || world > 64 || rank < 0 || rank >= world)
+        return arg_error("pj_part_load_snap: need 0 <= rank < world <= 64");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        std::vector<char> buf;
+        struct stat sb;
+        // missing / unreadable file: empty graph, as pj_load_snap (reference :67)
+        FILE* f = (stat(path, &sb) == 0 && S_ISREG(sb.st_mode)) ? std::fopen(path, "rb") : nullptr;
+        if (f) {
+            if (sb.st_size > 0) {
+                buf.resize((size_t)sb.st_size);
+                buf.resize(std::fread(buf.data(), 1, (size_t)sb.st_size, f));
+            }
+            std::fclose(f);
+        }
+        DevBuf<u32> src, dst, w;
+        ParseResult r = parse_snap_device(ctx->c, buf.data(), (i64)buf.size(), false, src, dst, w);
+        if (r.bad_line) {
+            set_error("edge list line " + std::to_string(r.bad_line) +
+                      ": second field missing, negative id or id out of range "
+                      "(undefined behaviour in the reference's read_webgraph)");
+            return (int)PJ_ERR_PARSE;
+        }
+        *out = reinterpret_cast<pj_part*>(part_from_coo(ctx->c, src, dst, r.nnz, r.max_id + 1, rank, world, false));
+        return (int)PJ_OK;
+    });
+}
+
 int pj_part_destroy(pj_part* p) {
     if (!p) return PJ_OK;
     return guarded([&] {

@@ -25,6 +25,7 @@ restatement of the same steps to exercise the protocol on CPU.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -186,6 +187,13 @@ def load_kronecker(ctx, scale: int, edgefactor: int, seed: int, rank: int, world
     h = ctypes.c_void_p()
     _check(_lib.pj_part_generate_kronecker(ctx._h, int(scale), int(edgefactor), ctypes.c_uint64(seed),
                                            int(rank), int(world), ctypes.byref(h)))
+    return DevicePart(ctx, h)
+
+
+def load_snap(ctx, path: str, rank: int, world: int) -> DevicePart:
+    """The rank's share of a SNAP edge list (pj_part_load_snap)."""
+    h = ctypes.c_void_p()
+    _check(_lib.pj_part_load_snap(ctx._h, os.fsencode(path), int(rank), int(world), ctypes.byref(h)))
     return DevicePart(ctx, h)
 
 

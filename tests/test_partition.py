@@ -204,3 +204,35 @@ def test_part_world2_one_gpu(oracle, world, force, backend):
 
 def _csr(oracle, s, d, n):
     return oracle.coo2csr(np.asarray(s, np.int64), np.asarray(d, np.int64), n)
+
+
+@pytest.mark.gpu
+def test_run_module_matches_cli(pj, oracle, tmp_path):
+    """`python -m paralleljohnson_amd.run` (1 process, and 2 ranks on the one GPU under
+    torchrun with gloo) writes the same sol_file bytes as the single-GPU CLI and the oracle."""
+    import subprocess
+    from helpers import to_text
+    rng = np.random.default_rng(77)
+    s, d = random_graph(rng, "hub", 3000)
+    path = tmp_path / "g.txt"
+    path.write_bytes(to_text(s, d, style=1))
+    src = int(s[0])
+    env = dict(os.environ, PJ_DEVICE="0")
+    ref = tmp_path / "cli.sol"
+    subprocess.run([pj.cli_path(), str(path), str(src), str(ref)], check=True, capture_output=True, env=env)
+    row, col, _ = oracle.coo2csr(np.asarray(s, np.int64), np.asarray(d, np.int64), int(max(s.max(), d.max())) + 1)
+    assert ref.read_bytes() == oracle.format_sol(oracle.bfs(row, col, src))
+    one = tmp_path / "one.sol"
+    r = subprocess.run([sys.executable, "-m", "paralleljohnson_amd.run", str(path), str(src), str(one)],
+                       check=True, capture_output=True, text=True, env=env, cwd=ROOT)
+    assert one.read_bytes() == ref.read_bytes()
+    assert r.stdout.startswith("Time: ") and r.stdout.rstrip().endswith("seconds when using 1 processes.")
+    assert "parallel Johnson's algorithm completes." in r.stderr
+    two = tmp_path / "two.sol"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        "-m", "paralleljohnson_amd.run", str(path), str(src), str(two)],
+                       capture_output=True, text=True, env=dict(env, PJ_BACKEND="gloo"), cwd=ROOT, timeout=200)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert two.read_bytes() == ref.read_bytes()
+    assert "when using 2 processes." in r.stdout
