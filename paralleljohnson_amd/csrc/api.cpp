@@ -404,6 +404,11 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "pull_factor" && value >= 0) g.pull_factor = value;
     else if (k == "delta_impl" && (value == 1 || value == 2)) g.delta_impl = (int)value;
     else if (k == "light_pull" && value >= 0) g.light_pull = value;
+    else if (k == "pull_grow" && value >= 0) g.pull_grow = value;
+    else if (k == "band_width" && value >= 0) g.band_width = value;
+    else if (k == "tail_delta") g.tail_delta = value;
+    else if (k == "tail_after" && value >= 0 && value < 1e6) g.tail_after = (int)value;
+    else if (k == "tail_frac" && value >= 0) g.tail_frac = value;
     else if (k == "direction" && (value == 0 || value == 1 || value == 2)) g.force_mode = (int)value;
     else if (k == "level_batch" && value >= 0 && value <= 4096) g.level_batch = (int)value;
     else if (k == "grid_per_cu" && value >= 0 && value <= 16) g.grid_per_cu = (int)value;

@@ -842,6 +842,7 @@ struct V2Args {
     const u64* cw;    // edges interleaved: col | w << 32 (the relabeled CSR)
     const u64* lrow;  // light CSR: the light prefixes of the rows, packed
     const u64* lcw;
+    int ltail;        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
     u64* mb;
     V2Ctl* ctl;
     u32* hv;     // [3][hcap]
@@ -994,9 +995,9 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
                 v = (u32)((wbase + jw) * 64 + bit);
                 du = a.dist[v];
                 if (PJ_V2_STATS && LIGHT) atomicAdd(&a.ctl->dbg[0].v, 1ull);
-                if (LIGHT) {  // light CSR
-                    b = a.lrow[v];
-                    e = a.lrow[v + 1];
+                if (LIGHT) {  // light CSR (tail mode: the light prefix in cw)
+                    b = a.ltail ? (u64)row[v] : a.lrow[v];
+                    e = a.ltail ? b + a.lsplit[v] : a.lrow[v + 1];
                     if ((tn >> bit) & 1ull) {
                         mh += (u64)row[v + 1] - (u64)row[v] - (e - b);
                         ml += e - b;
@@ -1032,7 +1033,7 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
             bool go = k < lim;
             while (__ballot(go)) {
                 if (go) {
-                    newc += v2_relax_n<LIGHT>(a, LIGHT ? a.lcw : a.cw, k, lim, du, fout, fe);
+                    newc += v2_relax_n<LIGHT>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, k, lim, du, fout, fe);
                     k = k + PU < lim ? k + PU : lim;
                     go = k < lim;
                 }
@@ -1046,7 +1047,7 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
                 const int32_t dl = __shfl(du, l, 64);
                 for (u64 kk = kb; kk < ke; kk += WAVE) {
                     const u64 k0 = kk + lane;
-                    if (k0 < ke) newc += v2_relax<LIGHT>(a, LIGHT ? a.lcw : a.cw, k0, dl, fout, fe);
+                    if (k0 < ke) newc += v2_relax<LIGHT>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, k0, dl, fout, fe);
                 }
             }
         }
@@ -1088,7 +1089,7 @@ __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout,
             const u64 e = e0 + (u64)j * DB + threadIdx.x;
             if (e < total) {
                 const u32 sl = lb_find<V2_HTILE>(sh, ns, e);
-                newc += v2_relax<LIGHT>(a, LIGHT ? a.lcw : a.cw, s_b[sl] + (e - sh.off[sl]), s_du[sl], fout, fe);
+                newc += v2_relax<LIGHT>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, s_b[sl] + (e - sh.off[sl]), s_du[sl], fout, fe);
             }
         }
         __syncthreads();
@@ -1179,7 +1180,9 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
             bool go = act && k < lim, done = !act || k >= e;
             while (__ballot(go)) {
                 if (go) {
-                    if (pull_step_band_cw<Off>(a.cw, a.dist, k, lim, lo, hi, cur)) {
+                    // band members are exactly mb's bits: probe the (cache-resident)
+                    // bitmap first, read dist only for members
+                    if (pull_step_fin_cw<Off>(a.cw, a.dist, a.mb, k, lim, lo, cur)) {
                         done = true;
                         go = false;
                     } else {
@@ -1202,9 +1205,9 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
                     int32_t cand = INT_INF;
                     if (!stop) {
-                        const int32_t du = a.dist[(u32)x];
-                        if (du >= lo && du < hi) {
-                            const long long nd = (long long)du + w;
+                        const u32 u = (u32)x;
+                        if ((a.mb[u >> 6] >> (u & 63)) & 1ull) {
+                            const long long nd = (long long)a.dist[u] + w;
                             cand = nd < INT_INF ? (int32_t)nd : INT_INF;
                         }
                     }
@@ -1491,6 +1494,19 @@ __global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restric
     }
 }
 
+// heavy edges (w >= the current light threshold) of the vertices not settled
+// below lo: the pull decision's heavy_left after a switch of the threshold
+template <typename Off>
+__global__ __launch_bounds__(DB) void v2_heavy_left_k(const Off* __restrict__ row, const u32* __restrict__ lsplit,
+                                                      const int32_t* __restrict__ dist, i64 n, int32_t lo,
+                                                      u64* __restrict__ out) {
+    u64 acc = 0;
+    for (i64 v = (i64)blockIdx.x * DB + threadIdx.x; v < n; v += (i64)gridDim.x * DB)
+        if (dist[v] >= lo) acc += (u64)(row[v + 1] - row[v]) - lsplit[v];
+    acc = wave_sum(acc);
+    if (lane_id() == 0 && acc) atomicAdd(out, acc);
+}
+
 __global__ void v2_source_k(V2Args a, i64 s, u64* __restrict__ f, int cin) {
     a.dist[s] = 0;
     f[s >> 6] = 1ull << (s & 63);
@@ -1507,6 +1523,8 @@ struct DeltaWork {
     DevBuf<DTot> tot;
     DevBuf<u32> flag;
     DevBuf<u32> lsplit;
+    DevBuf<u32> lsplit2;   // light prefixes for the tail threshold (g.tail_delta)
+    u32 lsplit2_delta = 0;
     DTot* host = nullptr;  // mapped pinned
     u32 lsplit_delta = 0;  // delta lsplit was computed for (0 = none)
     u64 heavy_total = 0;   // edges with w >= delta (for the pull decision)
@@ -1533,7 +1551,7 @@ void delete_delta_work(DeltaWork* p) { delete p; }
 
 namespace {
 
-// delta (explicit option, else 6 * mean weight / mean out-degree over all input
+// delta (explicit option, else 3.5 * mean weight / mean out-degree over all input
 // ids: light edges are then ~10% of a row; swept on Kronecker s22 / s26 with
 // weights 1..255, profiles/r01/delta_sweep.txt) and, once per delta, the light
 // prefix length of every row and the number of heavy edges.
@@ -1548,7 +1566,7 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
     int32_t delta = (int32_t)g.delta;
     if (delta <= 0) {
         const double mean_deg = g.n ? (double)g.nnz / (double)g.n : 1.0;
-        const double d = 6.0 * g.mean_weight / std::max(1.0, mean_deg);
+        const double d = 3.5 * g.mean_weight / std::max(1.0, mean_deg);
         delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(d)));
     }
     if (w.lsplit_delta != (u32)delta && n > 0) {
@@ -1753,6 +1771,9 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     const Off* row = static_cast<const Off*>(R.row_ptr(g.off64));
     const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
     const int32_t delta = prepare_delta<Off>(g, w);
+    // band width: at most the light threshold (an edge that can stay inside its
+    // band must be light, so the band's light rounds see it)
+    int32_t bw = g.band_width > 0 ? std::min<int32_t>(delta, (int32_t)g.band_width) : delta;
     if (!w.hctl) {
         const size_t nw = nwords ? (size_t)nwords : 1;
         w.f[0].alloc(nw);
@@ -1809,11 +1830,56 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         long long lo = 0;
         u64 heavy_left = w.heavy_total, light_left = w.light_total;
         const bool can_pull = g.symmetric && g.pull_factor > 0.0;
-        const bool can_pull_light = g.symmetric && g.light_pull > 0.0;
+        bool can_pull_light = g.symmetric && g.light_pull > 0.0;
+        bool tail = false;
+        const int32_t tdelta = (int32_t)std::min(65536.0, g.tail_delta < 0 ? 64.0 * delta : g.tail_delta);
         u64 last_fe = 1;  // light edges of the frontier at the last host sync (round 0: unknown)
         while (lo < INT_INF) {
-            const int32_t hi = (int32_t)std::min<long long>(lo + delta, INT_INF);
-            const int32_t nhi = (int32_t)std::min<long long>((long long)hi + delta, INT_INF);
+            if (!tail && tdelta > delta && (int)st.levels >= g.tail_after &&
+                (double)(heavy_left + light_left) < g.tail_frac * (double)g.nnz) {
+                // Tail: past the dense first bands the remaining rows are short and
+                // the bands sparse, so wider bands (fewer band steps) pay off. Switch
+                // to the light threshold tdelta: light rows from lsplit2 (push only;
+                // the packed light CSR belongs to delta), band width tdelta, the
+                // heavy edges left recounted, and the current band reselected.
+                tail = true;
+                if (w.lsplit2_delta != (u32)tdelta) {
+                    w.lsplit2.ensure((size_t)n);
+                    light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)tdelta,
+                                                                                 w.lsplit2.p);
+                    PJ_LAUNCH_CHECK();
+                    w.lsplit2_delta = (u32)tdelta;
+                }
+                a.lsplit = w.lsplit2.p;
+                a.ltail = 1;
+                bw = tdelta;
+                can_pull_light = false;
+                PJ_HIP(hipMemsetAsync(&w.ctl.p->minv, 0, sizeof(V2Line) * 2, s));  // (minv, dbg[0]: scratch)
+                v2_heavy_left_k<Off><<<maxgrid, DB, 0, s>>>(row, a.lsplit, R.dist.p, n, (int32_t)lo,
+                                                            &w.ctl.p->dbg[0].v);
+                PJ_LAUNCH_CHECK();
+                reset_minv();
+                PJ_HIP(hipMemsetAsync(w.ctl.p->cnt[cs], 0, sizeof(V2Line) * V2_NSH, s));
+                a.lo = (int32_t)lo;
+                a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
+                v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
+                PJ_LAUNCH_CHECK();
+                sync_ctl();
+                heavy_left = w.hctl->dbg[0].v;
+                PJ_HIP(hipMemsetAsync(&w.ctl.p->dbg[0], 0, sizeof(V2Line), s));
+                if (slot(cs) == 0) {
+                    const u64 mv = w.hctl->minv.v;
+                    if (mv >= (u64)INT_INF) break;
+                    lo = (long long)mv / bw * bw;
+                    a.lo = (int32_t)lo;
+                    a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
+                    reset_minv();
+                    v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
+                    PJ_LAUNCH_CHECK();
+                }
+            }
+            const int32_t hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
+            const int32_t nhi = (int32_t)std::min<long long>((long long)hi + bw, INT_INF);
             a.lo = (int32_t)lo;
             a.hi = hi;
             st.levels++;
@@ -1824,7 +1890,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 const u64 pull_thresh = can_pull_light ? (u64)((double)light_left / g.light_pull) : ~0ull;
                 // launch the pull kernels (which decide on the device, per round) only
                 // when the last frontier seen could grow past the threshold in this batch
-                const bool try_pull = can_pull_light && last_fe * 64 > pull_thresh;
+                const bool try_pull = can_pull_light && (double)last_fe * g.pull_grow > (double)pull_thresh;
                 for (int q = 0; q < K; ++q) {
                     if (try_pull) {
                         v2_pull_light_k<Off><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh);
@@ -1893,9 +1959,9 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             if (slot(cs) == 0) {
                 const u64 mv = w.hctl->minv.v;
                 if (mv >= (u64)INT_INF) break;  // nothing reached beyond the settled bands
-                lo = (long long)mv / delta * delta;  // jump to the next occupied band
+                lo = (long long)mv / bw * bw;  // jump to the next occupied band
                 a.lo = (int32_t)lo;
-                a.hi = (int32_t)std::min<long long>(lo + delta, INT_INF);
+                a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
                 reset_minv();
                 v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
                 PJ_LAUNCH_CHECK();

@@ -186,6 +186,12 @@ struct Graph {
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;
     double pull_factor = 4.0;
+    double band_width = 0.0;   // v2: width of a band [lo, lo + band_width) (0 = delta, at most delta)
+    double tail_delta = -1.0;  // v2: light threshold and band width of the tail (0 = off, < 0 = 64 x delta):
+    int tail_after = 1;        // from the first band >= tail_after at which the edges of unsettled
+    double tail_frac = 0.1;    // vertices are < tail_frac x nnz (profiles/r01/tail_sweep.txt)
+    double pull_grow = 1e9;   // v2: launch the light-pull kernels in a batch of rounds when the last seen
+                               // frontier's light edges x pull_grow exceed the pull threshold
     double light_pull = 2.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
                                // the light edges of unsettled vertices / light_pull (0 = never)
     int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based  // weighted, symmetric: pull a band's heavy edges when the heavy edges

@@ -193,6 +193,31 @@ def test_weighted_text_and_kronecker(ctx, oracle):
         assert (g.sssp(int(r)) == oracle.dijkstra(row, col, wc, int(r))).all()
 
 
+@pytest.mark.parametrize("scale,ef", [(13, 16), (15, 4)])
+def test_weighted_band_width(ctx, oracle, scale, ef):
+    """Bands narrower than the light threshold (delta.hip band_width): light edges
+    may then leave the band; the band's rounds must still settle it exactly. And
+    the switch to a wider tail threshold/band after tail_after bands."""
+    g = ctx.generate_kronecker(scale, ef, 3 + scale, weighted=True)
+    row, col, wc = g.get_csr()
+    col = col.astype(np.uint32)
+    roots = [int(r) for r in g.sample_roots(5 + ef, 3)]
+    exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
+    for pf, lp in ((0.0, 0.0), (4.0, 2.0), (1e15, 1e15)):
+        g.set_option("pull_factor", pf)
+        g.set_option("light_pull", lp)
+        for delta, bw, td, ta in ((24, 1, 0, 0), (24, 5, 0, 0), (24, 12, 0, 0), (60, 7, 0, 0), (7, 100, 0, 0),
+                                  (24, 0, 96, 0), (24, 0, 96, 1), (24, 0, 96, 3), (7, 3, 50, 2), (24, 0, 10, 2)):
+            g.set_option("delta", delta)
+            g.set_option("band_width", bw)
+            g.set_option("tail_delta", td)
+            g.set_option("tail_after", ta)
+            g.set_option("tail_frac", 2.0 if td else 0.0)  # (switch as soon as tail_after allows)
+            for r in roots:
+                assert (g.sssp(r) == exp[r]).all(), (pf, lp, delta, bw, td, ta, r)
+    g.close()
+
+
 @pytest.mark.parametrize("scale,ef", [(12, 16), (14, 4), (16, 1), (15, 16)])
 def test_weighted_pull_heavy(ctx, oracle, scale, ef):
     """Heavy edges by pull (symmetric graphs): never (push only), by the default
