@@ -1038,16 +1038,24 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
                     go = k < lim;
                 }
             }
-            // wave-cooperative part (segments <= V2_HT)
-            u64 open = __ballot(k < e);
-            while (open) {
-                const int l = __ffsll((long long)open) - 1;
-                open &= open - 1;
-                const u64 kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
-                const int32_t dl = __shfl(du, l, 64);
-                for (u64 kk = kb; kk < ke; kk += WAVE) {
-                    const u64 k0 = kk + lane;
-                    if (k0 < ke) newc += v2_relax<LIGHT>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, k0, dl, fout, fe);
+            // the rest of the segments (<= V2_HT): edge-balanced over the wave, 64
+            // edges per step (a lane finds its segment by binary search over the
+            // lanes' inclusive edge counts)
+            if (__ballot(k < e)) {
+                const u64 rem = k < e ? e - k : 0;
+                const u64 inc = wave_incl_scan(rem);
+                const u64 exc = inc - rem;
+                const u64 tot = __shfl(inc, 63, 64);
+                for (u64 r0 = 0; r0 < tot; r0 += WAVE) {
+                    const u64 gi = r0 + lane;
+                    int l = 0;
+#pragma unroll
+                    for (int step = 32; step > 0; step >>= 1)
+                        if (__shfl(inc, l + step - 1, 64) <= gi) l += step;
+                    const u64 kl = __shfl(k, l, 64), xl = __shfl(exc, l, 64);
+                    const int32_t dl = __shfl(du, l, 64);
+                    if (gi < tot)
+                        newc += v2_relax<LIGHT>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, kl + (gi - xl), dl, fout, fe);
                 }
             }
         }
@@ -1552,8 +1560,9 @@ void delete_delta_work(DeltaWork* p) { delete p; }
 namespace {
 
 // delta (explicit option, else 3.5 * mean weight / mean out-degree over all input
-// ids: light edges are then ~10% of a row; swept on Kronecker s22 / s26 with
-// weights 1..255, profiles/r01/delta_sweep.txt) and, once per delta, the light
+// ids: light edges are then ~5% of a row; swept on Kronecker s26 with weights
+// 1..255 together with the tail switch, profiles/r01/tail_sweep.txt) and, once
+// per delta, the light
 // prefix length of every row and the number of heavy edges.
 template <typename Off>
 int32_t prepare_delta(Graph& g, DeltaWork& w) {
