@@ -931,6 +931,42 @@ __device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const u64* __restrict
     return newc;
 }
 
+// N independent edges (any positions, own source distances) with the loads
+// issued together: edge words, then target distances, then the atomics.
+template <bool LIGHT, int N>
+__device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const u64* __restrict__ ed, const u64 (&idx)[N],
+                                          const int32_t (&du)[N], const bool (&val)[N], u64* __restrict__ fout,
+                                          u64& fe) {
+    u32 t[N];
+    long long nd[N];
+    bool ok[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const u64 x = val[j] ? ed[idx[j]] : 0ull;
+        t[j] = (u32)x;
+        nd[j] = (long long)du[j] + (long long)(x >> 32);
+        ok[j] = val[j] && nd[j] < INT_INF;
+    }
+    int32_t cd[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) cd[j] = ok[j] ? dist_now(a.dist + t[j]) : 0;
+    u32 newc = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        if (ok[j] && (int32_t)nd[j] < cd[j]) {
+            const int32_t old = atomicMin(a.dist + t[j], (int32_t)nd[j]);
+            if (LIGHT && (int32_t)nd[j] < old && (int32_t)nd[j] < a.hi) {
+                const u64 bit = 1ull << (t[j] & 63);
+                if (!(atomicOr(fout + (t[j] >> 6), bit) & bit)) {
+                    ++newc;
+                    fe += a.lsplit[t[j]];
+                }
+            }
+        }
+    }
+    return newc;
+}
+
 // LIGHT: relax the light prefixes of fin's vertices (a band round); HEAVY: the
 // heavy segments of fin = mb (push heavy step). fin words are cleared as read.
 template <typename Off, bool LIGHT>
@@ -1092,14 +1128,19 @@ __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout,
             s_b[i] = hb[s0 + i];
         }
         __syncthreads();
+        constexpr int NJ = V2_HTILE / DB;
+        u64 idx[NJ];
+        int32_t du[NJ];
+        bool val[NJ];
 #pragma unroll
-        for (int j = 0; j < V2_HTILE / DB; ++j) {
+        for (int j = 0; j < NJ; ++j) {
             const u64 e = e0 + (u64)j * DB + threadIdx.x;
-            if (e < total) {
-                const u32 sl = lb_find<V2_HTILE>(sh, ns, e);
-                newc += v2_relax<LIGHT>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, s_b[sl] + (e - sh.off[sl]), s_du[sl], fout, fe);
-            }
+            val[j] = e < total;
+            const u32 sl = val[j] ? lb_find<V2_HTILE>(sh, ns, e) : 0u;
+            idx[j] = val[j] ? s_b[sl] + (e - sh.off[sl]) : 0ull;
+            du[j] = val[j] ? s_du[sl] : 0;
         }
+        newc += v2_relax_g<LIGHT, NJ>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, idx, du, val, fout, fe);
         __syncthreads();
     }
     if (LIGHT) v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);

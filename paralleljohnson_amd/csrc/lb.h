@@ -21,14 +21,23 @@ struct LbShared {
 template <int TILE>
 __device__ __forceinline__ void lb_tile_load(const u64* __restrict__ qoff, u64 nq, u64 e0, LbShared<TILE>& sh,
                                              u64& s0, u32& ns) {
-    if (threadIdx.x == 0) {
-        u64 lo = 0, hi = nq - 1;  // last slot with qoff[slot] <= e0
-        while (lo < hi) {
-            const u64 mid = (lo + hi + 1) >> 1;
-            if (qoff[mid] <= e0) lo = mid;
-            else hi = mid - 1;
+    if (threadIdx.x < WAVE) {
+        // last slot with qoff[slot] <= e0, by a 64-ary search of wave 0: each step
+        // probes 64 evenly spaced slots at once (one load latency per 64x
+        // narrowing instead of one per halving; qoff[0] = 0 <= e0)
+        const int lane = threadIdx.x;
+        u64 lo = 0, hi = nq;  // answer in [lo, hi)
+        while (hi - lo > 1) {
+            const u64 step = (hi - lo + WAVE - 1) / WAVE;
+            const u64 p = lo + (u64)lane * step;
+            const bool ok = p < hi && qoff[p] <= e0;
+            const u64 m = __ballot(ok);  // a prefix of the lanes (qoff ascends); lane 0 is set
+            const u64 j = (u64)(63 - __clzll((long long)m));
+            const u64 nlo = lo + j * step;
+            hi = min(hi, nlo + step);
+            lo = nlo;
         }
-        sh.s0 = lo;
+        if (lane == 0) sh.s0 = lo;
     }
     __syncthreads();
     s0 = sh.s0;
