@@ -868,8 +868,8 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const u64* __restrict__
     if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[1].v, 1ull);
     if (nd < INT_INF && (int32_t)nd < dist_now(a.dist + t)) {
         if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
-        const int32_t old = atomicMin(a.dist + t, (int32_t)nd);
-        if (LIGHT && (int32_t)nd < old && (int32_t)nd < a.hi) {
+        atomicMin(a.dist + t, (int32_t)nd);  // no return: see v2_relax_g
+        if (LIGHT && (int32_t)nd < a.hi) {
             const u64 bit = 1ull << (t & 63);
             const u32 nw = (atomicOr(fout + (t >> 6), bit) & bit) ? 0u : 1u;
             if (PJ_V2_STATS && nw) atomicAdd(&a.ctl->dbg[3].v, 1ull);
@@ -918,8 +918,8 @@ __device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const u64* __restrict
 #pragma unroll
     for (int j = 0; j < PU; ++j) {
         if (ok[j] && (int32_t)nd[j] < cd[j]) {
-            const int32_t old = atomicMin(a.dist + t[j], (int32_t)nd[j]);
-            if (LIGHT && (int32_t)nd[j] < old && (int32_t)nd[j] < a.hi) {
+            atomicMin(a.dist + t[j], (int32_t)nd[j]);
+            if (LIGHT && (int32_t)nd[j] < a.hi) {
                 const u64 bit = 1ull << (t[j] & 63);
                 if (!(atomicOr(fout + (t[j] >> 6), bit) & bit)) {
                     ++newc;
@@ -932,7 +932,11 @@ __device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const u64* __restrict
 }
 
 // N independent edges (any positions, own source distances) with the loads
-// issued together: edge words, then target distances, then the atomics.
+// issued together: edge words, then target distances, then the atomics. The
+// atomicMin is issued without a return value (nothing waits for it): a target
+// whose read distance was above nd has been lowered to <= nd this round, by
+// this lane or another, so it belongs in the next frontier either way; the
+// atomicOr's old bit keeps the count of new frontier vertices exact.
 template <bool LIGHT, int N>
 __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const u64* __restrict__ ed, const u64 (&idx)[N],
                                           const int32_t (&du)[N], const bool (&val)[N], u64* __restrict__ fout,
@@ -954,8 +958,8 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const u64* __restrict
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         if (ok[j] && (int32_t)nd[j] < cd[j]) {
-            const int32_t old = atomicMin(a.dist + t[j], (int32_t)nd[j]);
-            if (LIGHT && (int32_t)nd[j] < old && (int32_t)nd[j] < a.hi) {
+            atomicMin(a.dist + t[j], (int32_t)nd[j]);
+            if (LIGHT && (int32_t)nd[j] < a.hi) {
                 const u64 bit = 1ull << (t[j] & 63);
                 if (!(atomicOr(fout + (t[j] >> 6), bit) & bit)) {
                     ++newc;
