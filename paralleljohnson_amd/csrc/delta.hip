@@ -843,6 +843,8 @@ struct V2Args {
     const u64* lrow;  // light CSR: the light prefixes of the rows, packed
     const u64* lcw;
     int ltail;        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
+    const u64* sbits; // tail mode: settled-before-the-tail bitmap; relaxations skip its targets
+    u64* swrite;      // the heavy step entering the tail writes that bitmap (pull / select)
     u64* mb;
     V2Ctl* ctl;
     u32* hv;     // [3][hcap]
@@ -866,6 +868,7 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const u64* __restrict__
     const u32 t = (u32)x;
     const long long nd = (long long)du + (long long)(x >> 32);
     if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[1].v, 1ull);
+    if (a.sbits && ((a.sbits[t >> 6] >> (t & 63)) & 1ull)) return 0u;
     if (nd < INT_INF && (int32_t)nd < dist_now(a.dist + t)) {
         if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
         atomicMin(a.dist + t, (int32_t)nd);  // no return: see v2_relax_g
@@ -911,6 +914,13 @@ __device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const u64* __restrict
         nd[j] = (long long)du + (long long)(x >> 32);
         ok[j] = ok[j] && nd[j] < INT_INF;
     }
+    if (a.sbits) {  // tail: skip targets settled before the tail (a cache-resident bit, not dist)
+        u64 sw[PU];
+#pragma unroll
+        for (int j = 0; j < PU; ++j) sw[j] = ok[j] ? a.sbits[t[j] >> 6] : 0ull;
+#pragma unroll
+        for (int j = 0; j < PU; ++j) ok[j] = ok[j] && !((sw[j] >> (t[j] & 63)) & 1ull);
+    }
     int32_t cd[PU];
 #pragma unroll
     for (int j = 0; j < PU; ++j) cd[j] = ok[j] ? dist_now(a.dist + t[j]) : 0;
@@ -950,6 +960,13 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const u64* __restrict
         t[j] = (u32)x;
         nd[j] = (long long)du[j] + (long long)(x >> 32);
         ok[j] = val[j] && nd[j] < INT_INF;
+    }
+    if (a.sbits) {
+        u64 sw[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) sw[j] = ok[j] ? a.sbits[t[j] >> 6] : 0ull;
+#pragma unroll
+        for (int j = 0; j < N; ++j) ok[j] = ok[j] && !((sw[j] >> (t[j] & 63)) & 1ull);
     }
     int32_t cd[N];
 #pragma unroll
@@ -1162,6 +1179,10 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fo
         const int32_t d = v < a.n ? a.dist[v] : INT_INF;
         const bool mem = d >= a.lo && d < a.hi;
         const u64 m = __ballot(mem);
+        if (a.swrite) {
+            const u64 sm = __ballot(v < a.n && d < a.lo);
+            if (lane == 0) a.swrite[wi] = sm;
+        }
         if (d >= a.lo && d < mn) mn = d;
         if (mem) fe += a.lsplit[v];
         if (lane == 0) fout[wi] = m;
@@ -1203,6 +1224,10 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
             const int32_t d = v < a.n ? a.dist[v] : 0;
             const u64 m = __ballot(v < a.n && d >= hi);
             if (lane == k) mytodo = m;
+            if (a.swrite) {
+                const u64 sm = __ballot(v < a.n && d < hi);
+                if (lane == k && gbase + k < a.nwords) a.swrite[gbase + k] = sm;
+            }
         }
         if (lane < 2 * PSC) newb[lane] = 0;
         const u32 cnt = (u32)__popcll(mytodo);
@@ -1560,6 +1585,13 @@ __global__ __launch_bounds__(DB) void v2_heavy_left_k(const Off* __restrict__ ro
     if (lane_id() == 0 && acc) atomicAdd(out, acc);
 }
 
+__global__ void v2_wmax_k(const u32* __restrict__ w, i64 m, u32* __restrict__ out) {
+    u32 x = 0;
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x) x = max(x, w[i]);
+    x = wave_max(x);
+    if (lane_id() == 0 && x) atomicMax(out, x);
+}
+
 __global__ void v2_source_k(V2Args a, i64 s, u64* __restrict__ f, int cin) {
     a.dist[s] = 0;
     f[s >> 6] = 1ull << (s & 63);
@@ -1578,6 +1610,8 @@ struct DeltaWork {
     DevBuf<u32> lsplit;
     DevBuf<u32> lsplit2;   // light prefixes for the tail threshold (g.tail_delta)
     u32 lsplit2_delta = 0;
+    DevBuf<u64> sb;        // settled-before-the-tail bitmap
+    long long maxw = -1;   // largest edge weight (-1: not computed)
     DTot* host = nullptr;  // mapped pinned
     u32 lsplit_delta = 0;  // delta lsplit was computed for (0 = none)
     u64 heavy_total = 0;   // edges with w >= delta (for the pull decision)
@@ -1661,6 +1695,18 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
             PJ_LAUNCH_CHECK();
         }
         PJ_HIP(hipStreamSynchronize(s));
+    }
+    if (w.maxw < 0) {  // largest weight: decides whether the tail has heavy edges at all
+        u32 h = 0;
+        if (g.nnz > 0) {
+            DevBuf<u32> m(1);
+            PJ_HIP(hipMemsetAsync(m.p, 0, sizeof(u32), s));
+            v2_wmax_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.w.p, g.nnz, m.p);
+            PJ_LAUNCH_CHECK();
+            PJ_HIP(hipMemcpyAsync(&h, m.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipStreamSynchronize(s));
+        }
+        w.maxw = (long long)h;
     }
     return delta;
 }
@@ -1889,51 +1935,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         const int32_t tdelta = (int32_t)std::min(65536.0, g.tail_delta < 0 ? 64.0 * delta : g.tail_delta);
         u64 last_fe = 1;  // light edges of the frontier at the last host sync (round 0: unknown)
         while (lo < INT_INF) {
-            if (!tail && tdelta > delta && (int)st.levels >= g.tail_after &&
-                (double)(heavy_left + light_left) < g.tail_frac * (double)g.nnz) {
-                // Tail: past the dense first bands the remaining rows are short and
-                // the bands sparse, so wider bands (fewer band steps) pay off. Switch
-                // to the light threshold tdelta: light rows from lsplit2 (push only;
-                // the packed light CSR belongs to delta), band width tdelta, the
-                // heavy edges left recounted, and the current band reselected.
-                tail = true;
-                if (w.lsplit2_delta != (u32)tdelta) {
-                    w.lsplit2.ensure((size_t)n);
-                    light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)tdelta,
-                                                                                 w.lsplit2.p);
-                    PJ_LAUNCH_CHECK();
-                    w.lsplit2_delta = (u32)tdelta;
-                }
-                a.lsplit = w.lsplit2.p;
-                a.ltail = 1;
-                bw = tdelta;
-                can_pull_light = false;
-                PJ_HIP(hipMemsetAsync(&w.ctl.p->minv, 0, sizeof(V2Line) * 2, s));  // (minv, dbg[0]: scratch)
-                v2_heavy_left_k<Off><<<maxgrid, DB, 0, s>>>(row, a.lsplit, R.dist.p, n, (int32_t)lo,
-                                                            &w.ctl.p->dbg[0].v);
-                PJ_LAUNCH_CHECK();
-                reset_minv();
-                PJ_HIP(hipMemsetAsync(w.ctl.p->cnt[cs], 0, sizeof(V2Line) * V2_NSH, s));
-                a.lo = (int32_t)lo;
-                a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
-                v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
-                PJ_LAUNCH_CHECK();
-                sync_ctl();
-                heavy_left = w.hctl->dbg[0].v;
-                PJ_HIP(hipMemsetAsync(&w.ctl.p->dbg[0], 0, sizeof(V2Line), s));
-                if (slot(cs) == 0) {
-                    const u64 mv = w.hctl->minv.v;
-                    if (mv >= (u64)INT_INF) break;
-                    lo = (long long)mv / bw * bw;
-                    a.lo = (int32_t)lo;
-                    a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
-                    reset_minv();
-                    v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
-                    PJ_LAUNCH_CHECK();
-                }
-            }
             const int32_t hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
-            const int32_t nhi = (int32_t)std::min<long long>((long long)hi + bw, INT_INF);
             a.lo = (int32_t)lo;
             a.hi = hi;
             st.levels++;
@@ -1986,8 +1988,32 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             heavy_left = heavy_left > mh ? heavy_left - mh : 0;
             light_left = light_left > ml ? light_left - ml : 0;
             reset_minv();
+            // Tail: past the dense first bands the remaining rows are short and the
+            // bands sparse, so wide bands (few band steps) pay off. Once the edges of
+            // the unsettled vertices drop below tail_frac x nnz, the bands after this
+            // one use the light threshold tdelta (light prefixes from lsplit2, push
+            // only: the packed light CSR belongs to delta) and width tdelta. Decided
+            // here, before the heavy step, so that its fused selection already picks
+            // the first tail band and writes the settled bitmap the tail's
+            // relaxations filter their targets with. Exact at any band boundary:
+            // everything below hi is settled and relaxed after this heavy step.
+            const bool enter_tail = !tail && tdelta > delta && (int)st.levels >= g.tail_after &&
+                                    (double)(heavy_left + light_left) < g.tail_frac * (double)g.nnz;
+            const int32_t nbw = enter_tail ? tdelta : bw;
+            const int32_t nhi_t = (int32_t)std::min<long long>((long long)hi + nbw, INT_INF);
+            if (enter_tail) {
+                if (w.lsplit2_delta != (u32)tdelta) {
+                    w.lsplit2.ensure((size_t)n);
+                    light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)tdelta,
+                                                                                 w.lsplit2.p);
+                    PJ_LAUNCH_CHECK();
+                    w.lsplit2_delta = (u32)tdelta;
+                }
+                w.sb.ensure((size_t)nwords);
+                a.swrite = w.sb.p;
+            }
             if (can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh) {
-                v2_pull_k<Off><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi, cs);
+                v2_pull_k<Off><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi_t, cs);
                 PJ_LAUNCH_CHECK();
                 PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 st.bu_levels++;
@@ -2003,11 +2029,28 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                     PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 }
                 a.lo = hi;
-                a.hi = nhi;
+                a.hi = nhi_t;
                 v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
                 PJ_LAUNCH_CHECK();
             }
+            if (enter_tail) {
+                tail = true;
+                a.swrite = nullptr;
+                a.sbits = w.sb.p;
+                a.lsplit = w.lsplit2.p;
+                a.ltail = 1;
+                bw = tdelta;
+                can_pull_light = false;
+                if ((long long)tdelta > w.maxw) {
+                    heavy_left = 0;  // every edge is light in the tail
+                } else {
+                    PJ_HIP(hipMemsetAsync(&w.ctl.p->dbg[0], 0, sizeof(V2Line), s));
+                    v2_heavy_left_k<Off><<<maxgrid, DB, 0, s>>>(row, a.lsplit, R.dist.p, n, hi, &w.ctl.p->dbg[0].v);
+                    PJ_LAUNCH_CHECK();
+                }
+            }
             sync_ctl();
+            if (enter_tail && (long long)tdelta <= w.maxw) heavy_left = w.hctl->dbg[0].v;
             last_fe = 0;
             for (int i = 0; i < V2_NSH; ++i) last_fe += w.hctl->cnt[cs][i].pad[0];
             if (slot(cs) == 0) {
