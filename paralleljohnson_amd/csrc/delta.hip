@@ -512,7 +512,10 @@ __global__ void unlabel_k(const u32* __restrict__ inv, const int32_t* __restrict
 // loads (the probes are latency-bound; one edge per step leaves the memory
 // system idle). Weights ascend along the row, so once lo + w >= cur for an
 // edge, that edge and every later one are useless: the step returns true.
-constexpr int PU = 4;
+#ifndef PJ_PU
+#define PJ_PU 4
+#endif
+constexpr int PU = PJ_PU;
 // pull from band members [lo, hi)
 template <typename Off>
 __device__ __forceinline__ bool pull_step_band(const u32* __restrict__ wt, const u32* __restrict__ col,
@@ -800,7 +803,10 @@ __global__ __launch_bounds__(DB) void wsum_k(const u32* __restrict__ w, i64 n, u
 //                 once per batch of light rounds and once per band.
 // ---------------------------------------------------------------------------
 constexpr int V2_SC = 16;     // frontier words a wave screens at once
-constexpr int V2_LS = 8;      // segment edges a lane relaxes alone
+#ifndef PJ_V2_LS
+#define PJ_V2_LS 8
+#endif
+constexpr int V2_LS = PJ_V2_LS;  // segment edges a lane relaxes alone
 #ifndef PJ_V2_HT
 #define PJ_V2_HT 64
 #endif
