@@ -1,10 +1,10 @@
 // msbfs.hip — batched multi-source unit-weight SSSP (Johnson-style rows of
-// the all-pairs matrix), 64 sources per pass.
+// the all-pairs matrix), up to 64 x W sources per pass (W = 1, 2 or 4 words).
 //
 // The reference answers one source per run (`atoi(argv[2])`, :448); a batch of
-// 64 runs shares every CSR read here. Per vertex v the pass keeps three 64-bit
-// words, one bit per source of the batch:
-//   V[v]  sources that have reached v          (the 64 reference sp[] arrays, as bits)
+// 64 W runs shares every CSR read here. Per vertex v the pass keeps three masks
+// of W 64-bit words, one bit per source of the batch:
+//   V[v]  sources that have reached v          (the reference's sp[] arrays, as bits)
 //   F[v]  sources that reached v at the last level (their frontier)
 //   Fn[v] the same for the level being computed
 // A level is a pull over in-edges: Fn[v] = (OR over in-neighbours u of F[u]) & ~V[v],
@@ -13,7 +13,10 @@
 //
 // Work mapping: one wave per 64 consecutive vertices; each lane walks its first
 // MS_SERIAL in-edges in a wave-uniform loop (predicated body), then the whole wave
-// scans the rest of long rows (web-graph in-hubs) 64 edges at a time.
+// scans the rest of long rows (web-graph in-hubs) 64 edges at a time. The masks
+// are stored vertex-major (W words contiguous), so a probe of F[u] is one 8W-byte
+// access: wider passes do the same number of random probes for 4x the sources
+// (the levels are probe-latency-bound, profiles/r01).
 #include <chrono>
 
 #include "devutil.h"
@@ -24,11 +27,63 @@ namespace {
 
 constexpr int MB = 256;
 constexpr int MS_SERIAL = 16;
+constexpr int MS_WMAX = 4;  // widest pass: 256 sources
 
 struct MsCtl {
     u64 active[3];  // ring: level L reads [(L+2)%3] (level L-1), writes [L%3], block 0 zeroes [(L+1)%3]
+    u64 fedges[3];  // same ring: out-edges of the vertices newly reached by a level (its frontier's push cost)
     u64 done;       // set once by block 0 of the first level that finds nothing to do
 };
+
+// Direction of level L, identical in every kernel of the level: push (top-down,
+// atomicOr of the frontier masks into the targets' next masks) while the last
+// frontier's out-edges are few, else pull over in-edges.
+__device__ __forceinline__ bool ms_is_push(const MsCtl* c, int32_t L, u64 push_max) {
+    return c->fedges[(L + 2) % 3] < push_max;
+}
+__device__ __forceinline__ bool ms_live(const MsCtl* c, int32_t L) {
+    return c->active[(L + 2) % 3] != 0 && L + 1 < INT_INF;
+}
+
+template <int W>
+struct Mask {
+    u64 w[W];
+};
+
+template <int W>
+__device__ __forceinline__ Mask<W> mload(const u64* __restrict__ p, i64 v) {
+    Mask<W> m;
+    if constexpr (W == 4) {
+        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p + v * 4);
+        const ulonglong2 x = q[0], y = q[1];
+        m.w[0] = x.x; m.w[1] = x.y; m.w[2] = y.x; m.w[3] = y.y;
+    } else if constexpr (W == 2) {
+        const ulonglong2 x = reinterpret_cast<const ulonglong2*>(p)[v];
+        m.w[0] = x.x; m.w[1] = x.y;
+    } else {
+        m.w[0] = p[v];
+    }
+    return m;
+}
+template <int W>
+__device__ __forceinline__ void mstore(u64* __restrict__ p, i64 v, const Mask<W>& m) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) p[v * W + j] = m.w[j];
+}
+template <int W>
+__device__ __forceinline__ bool many(const Mask<W>& m) {
+    u64 x = 0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) x |= m.w[j];
+    return x != 0;
+}
+template <int W>
+__device__ __forceinline__ bool mopen(const Mask<W>& need, const Mask<W>& acc) {  // need & ~acc != 0
+    u64 x = 0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) x |= need.w[j] & ~acc.w[j];
+    return x != 0;
+}
 
 __device__ __forceinline__ u64 wave_or(u64 x) {
 #pragma unroll
@@ -36,10 +91,19 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
     return x;
 }
 
-__global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __restrict__ F, i64 n,
-                                                int32_t* __restrict__ dist, i64 nb_dist) {
+__global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __restrict__ F, i64 nw,
+                                                int32_t* __restrict__ dist, i64 nb_dist, MsCtl* ctl,
+                                                int64_t* host_done) {
     const i64 tid = (i64)blockIdx.x * MB + threadIdx.x, nth = (i64)gridDim.x * MB;
-    for (i64 i = tid; i < n; i += nth) {
+    if (tid == 0) {
+        for (int i = 0; i < 3; ++i) {
+            ctl->active[i] = 0;
+            ctl->fedges[i] = 0;
+        }
+        ctl->done = 0;
+        *host_done = -1;
+    }
+    for (i64 i = tid; i < nw; i += nth) {
         V[i] = 0;
         F[i] = 0;
     }
@@ -49,103 +113,243 @@ __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __rest
     for (i64 i = n4 * 4 + tid; i < nb_dist; i += nth) dist[i] = INT_INF;
 }
 
-__global__ void ms_sources_k(const int64_t* __restrict__ src, int ns, i64 n, u64* __restrict__ V, u64* __restrict__ F,
-                             int32_t* __restrict__ dist, MsCtl* ctl, int64_t* host_done) {
-    // one thread: sources may repeat
-    u64 any = 0;
-    for (int i = 0; i < ns; ++i) {
-        const int64_t s = src[i];
-        if (s < 0 || s >= n) continue;
-        V[s] |= 1ull << i;
-        F[s] |= 1ull << i;
-        dist[(i64)i * n + s] = 0;
-        any = 1;
-    }
-    ctl->active[2] = any;  // "level -1" found the sources
-    ctl->active[0] = 0;
-    ctl->active[1] = 0;
-    ctl->done = 0;
-    *host_done = -1;
+// one thread per source (sources may repeat: atomics on the masks)
+template <typename Off>
+__global__ void ms_sources_k(const int64_t* __restrict__ src, int ns, int W, i64 n, const Off* __restrict__ row,
+                             u64* __restrict__ V, u64* __restrict__ F, int32_t* __restrict__ dist, MsCtl* ctl) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ns) return;
+    const int64_t s = src[i];
+    if (s < 0 || s >= n) return;
+    atomicOr(&V[s * W + (i >> 6)], 1ull << (i & 63));
+    atomicOr(&F[s * W + (i >> 6)], 1ull << (i & 63));
+    dist[(i64)i * n + s] = 0;
+    ctl->active[2] = 1;  // "level -1" found the sources
+    atomicAdd(&ctl->fedges[2], (u64)(row[s + 1] - row[s]));
 }
 
-template <typename Off>
-__global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ crow, const u32* __restrict__ ccol,
-                                                 u64* __restrict__ V, const u64* __restrict__ F,
-                                                 u64* __restrict__ Fn, int32_t* __restrict__ dist, int32_t L,
-                                                 u64 smask, MsCtl* ctl, int64_t* host_done) {
-    // level L computes distance L+1 from the frontier of level L-1
-    if (ctl->active[(L + 2) % 3] == 0 || L + 1 >= INT_INF) {
+// First kernel of level L: ends the pass when level L-1 found nothing, zeroes
+// the ring slots level L+1 writes, and (push levels) clears the output masks.
+template <int W>
+__global__ __launch_bounds__(MB) void ms_prep_k(i64 n, u64* __restrict__ Fn, int32_t L, u64 push_max, MsCtl* ctl,
+                                                int64_t* host_done) {
+    if (!ms_live(ctl, L)) {
         if (blockIdx.x == 0 && threadIdx.x == 0 && !ctl->done) {
             ctl->done = 1;
             *host_done = L;
         }
         return;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctl->active[(L + 1) % 3] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl->active[(L + 1) % 3] = 0;
+        ctl->fedges[(L + 1) % 3] = 0;
+    }
+    if (!ms_is_push(ctl, L, push_max)) return;
+    ulonglong2* p = reinterpret_cast<ulonglong2*>(Fn);
+    const i64 n2 = n * W / 2;
+    for (i64 i = (i64)blockIdx.x * MB + threadIdx.x; i < n2; i += (i64)gridDim.x * MB) p[i] = make_ulonglong2(0, 0);
+    if ((n * W) & 1) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) Fn[n * W - 1] = 0;
+    }
+}
+
+// distances of newly reached (source, v) pairs: loop over the sources any lane
+// reached (wave-uniform), so each store is one coalesced run of the wave's 64
+// consecutive vertices in that source's row
+template <int W>
+__device__ __forceinline__ void ms_write_dist(const Mask<W>& newb, int32_t* __restrict__ dist, i64 n, i64 v,
+                                              int32_t val) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        u64 un = wave_or(newb.w[j]);
+        while (un) {
+            const int sbit = __ffsll((long long)un) - 1;
+            un &= un - 1;
+            if ((newb.w[j] >> sbit) & 1ull) dist[(i64)(sbit + 64 * j) * n + v] = val;
+        }
+    }
+}
+
+// Push level: every vertex u with a nonzero frontier mask ORs it into the next
+// mask of each out-neighbour (no-return atomics); ms_fin_k then keeps the bits
+// not yet in V.
+template <typename Off, int W>
+__global__ __launch_bounds__(MB) void ms_push_k(i64 n, const Off* __restrict__ row, const u32* __restrict__ col,
+                                                const u64* __restrict__ F, u64* __restrict__ Fn, int32_t L,
+                                                u64 push_max, const MsCtl* ctl) {
+    if (!ms_live(ctl, L) || !ms_is_push(ctl, L, push_max)) return;
     const int lane = lane_id();
-    u64 found_any = 0;
+    const i64 nwaves = (i64)gridDim.x * (MB / WAVE);
+    for (i64 base = ((i64)blockIdx.x * (MB / WAVE) + wave_id()) * 64; base < n; base += nwaves * 64) {
+        const i64 u = base + lane;
+        Mask<W> f{};
+        if (u < n) f = mload<W>(F, u);
+        const bool act = many<W>(f);
+        if (!__ballot(act)) continue;
+        Off b = 0, e = 0;
+        if (act) {
+            b = row[u];
+            e = row[u + 1];
+        }
+        const Off lim = (e - b > (Off)MS_SERIAL) ? b + (Off)MS_SERIAL : e;
+        for (Off k = b; k < lim; ++k) {
+            const u32 v = col[k];
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+                if (f.w[j]) atomicOr(&Fn[(i64)v * W + j], f.w[j]);
+        }
+        u64 open = __ballot(lim < e);
+        while (open) {
+            const int l = __ffsll((long long)open) - 1;
+            open &= open - 1;
+            const Off kb = __shfl(lim, l, 64), ke = __shfl(e, l, 64);
+            Mask<W> fl;
+#pragma unroll
+            for (int j = 0; j < W; ++j) fl.w[j] = __shfl(f.w[j], l, 64);
+            for (Off kk = kb + lane; kk < ke; kk += WAVE) {
+                const u32 v = col[kk];
+#pragma unroll
+                for (int j = 0; j < W; ++j)
+                    if (fl.w[j]) atomicOr(&Fn[(i64)v * W + j], fl.w[j]);
+            }
+        }
+    }
+}
+
+template <typename Off, int W>
+__global__ __launch_bounds__(MB) void ms_fin_k(i64 n, const Off* __restrict__ row, u64* __restrict__ V,
+                                               u64* __restrict__ Fn, int32_t* __restrict__ dist, int32_t L,
+                                               Mask<W> smask, u64 push_max, MsCtl* ctl) {
+    if (!ms_live(ctl, L) || !ms_is_push(ctl, L, push_max)) return;
+    __shared__ u64 red[MB / WAVE];
+    const int lane = lane_id();
+    u64 found_any = 0, fe = 0;
+    const i64 nwaves = (i64)gridDim.x * (MB / WAVE);
+    for (i64 base = ((i64)blockIdx.x * (MB / WAVE) + wave_id()) * 64; base < n; base += nwaves * 64) {
+        const i64 v = base + lane;
+        Mask<W> fn{};
+        if (v < n) fn = mload<W>(Fn, v);
+        const bool act = many<W>(fn);
+        if (!__ballot(act)) continue;
+        Mask<W> newb{};
+        bool anynew = false;
+        if (act) {
+            const Mask<W> vv = mload<W>(V, v);
+            Mask<W> nv;
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                newb.w[j] = fn.w[j] & ~vv.w[j] & smask.w[j];
+                nv.w[j] = vv.w[j] | newb.w[j];
+                anynew |= newb.w[j] != 0;
+            }
+            mstore<W>(Fn, v, newb);
+            if (anynew) {
+                mstore<W>(V, v, nv);
+                fe += (u64)(row[v + 1] - row[v]);
+            }
+        }
+        found_any |= anynew ? 1ull : 0ull;
+        ms_write_dist<W>(newb, dist, n, v, L + 1);
+    }
+    fe = block_sum<MB / WAVE>(fe, red);
+    if (threadIdx.x == 0 && fe) atomicAdd(&ctl->fedges[L % 3], fe);
+    if (__ballot(found_any != 0) && lane == 0) ctl->active[L % 3] = 1;
+}
+
+template <typename Off, int W>
+__global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ crow, const u32* __restrict__ ccol,
+                                                 const Off* __restrict__ row, u64* __restrict__ V,
+                                                 const u64* __restrict__ F, u64* __restrict__ Fn,
+                                                 int32_t* __restrict__ dist, int32_t L, Mask<W> smask,
+                                                 u64 push_max, MsCtl* ctl) {
+    // level L computes distance L+1 from the frontier of level L-1 (pull form)
+    if (!ms_live(ctl, L) || ms_is_push(ctl, L, push_max)) return;
+    __shared__ u64 red[MB / WAVE];
+    const int lane = lane_id();
+    u64 found_any = 0, fe = 0;
     const i64 nwaves = (i64)gridDim.x * (MB / WAVE);
     for (i64 base = ((i64)blockIdx.x * (MB / WAVE) + wave_id()) * 64; base < n; base += nwaves * 64) {
         const i64 v = base + lane;
         const bool inr = v < n;
-        const u64 vv = inr ? V[v] : ~0ull;
-        const u64 need = ~vv & smask;  // sources of this batch that have not reached v
-        if (__ballot(need != 0) == 0) {
-            if (inr) Fn[v] = 0;
+        Mask<W> vv, need;
+        if (inr) vv = mload<W>(V, v);
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            if (!inr) vv.w[j] = ~0ull;
+            need.w[j] = ~vv.w[j] & smask.w[j];  // sources of this batch that have not reached v
+        }
+        const bool hasneed = many<W>(need);
+        if (__ballot(hasneed) == 0) {
+            if (inr) mstore<W>(Fn, v, Mask<W>{});
             continue;
         }
         Off b = 0, e = 0;
-        if (need) {
+        if (hasneed) {
             b = crow[v];
             e = crow[v + 1];
         }
-        u64 acc = 0;
+        Mask<W> acc{};
         Off k = b;
         const Off lim = (e - b > (Off)MS_SERIAL) ? b + (Off)MS_SERIAL : e;
-        bool go = need && k < lim;
+        bool go = hasneed && k < lim;
         while (__ballot(go)) {
             if (go) {
-                acc |= F[ccol[k]];
+                const Mask<W> f = mload<W>(F, ccol[k]);
+#pragma unroll
+                for (int j = 0; j < W; ++j) acc.w[j] |= f.w[j];
                 ++k;
-                go = (need & ~acc) && k < lim;
+                go = mopen<W>(need, acc) && k < lim;
             }
         }
-        u64 open = __ballot((need & ~acc) != 0 && k < e);
+        u64 open = __ballot(mopen<W>(need, acc) && k < e);
         while (open) {
             const int l = __ffsll((long long)open) - 1;
             open &= open - 1;
             const Off kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
-            const u64 want = __shfl(need, l, 64);
-            u64 got = __shfl(acc, l, 64);
-            for (Off kk = kb; kk < ke && (want & ~got); kk += WAVE) {
+            Mask<W> want, got;
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                want.w[j] = __shfl(need.w[j], l, 64);
+                got.w[j] = __shfl(acc.w[j], l, 64);
+            }
+            for (Off kk = kb; kk < ke && mopen<W>(want, got); kk += WAVE) {
                 const Off kx = kk + lane;
-                const u64 x = kx < ke ? F[ccol[kx]] : 0ull;
-                got |= wave_or(x);
+                Mask<W> x{};
+                if (kx < ke) x = mload<W>(F, ccol[kx]);
+#pragma unroll
+                for (int j = 0; j < W; ++j) got.w[j] |= wave_or(x.w[j]);
             }
             if (lane == l) acc = got;
         }
-        const u64 newb = acc & need;
-        if (inr) {
-            Fn[v] = newb;
-            if (newb) V[v] = vv | newb;
+        Mask<W> newb;
+        bool anynew = false;
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            newb.w[j] = acc.w[j] & need.w[j];
+            anynew |= newb.w[j] != 0;
         }
-        found_any |= newb;
-        // distances of the newly reached (source, v) pairs: a wave-uniform loop
-        u64 rest = newb;
-        while (__ballot(rest != 0)) {
-            if (rest) {
-                const int sbit = __ffsll((long long)rest) - 1;
-                rest &= rest - 1;
-                dist[(i64)sbit * n + v] = L + 1;
+        if (inr) {
+            mstore<W>(Fn, v, newb);
+            if (anynew) {
+                Mask<W> nv;
+#pragma unroll
+                for (int j = 0; j < W; ++j) nv.w[j] = vv.w[j] | newb.w[j];
+                mstore<W>(V, v, nv);
             }
         }
+        found_any |= anynew ? 1ull : 0ull;
+        if (anynew) fe += (u64)(row[v + 1] - row[v]);
+        ms_write_dist<W>(newb, dist, n, v, L + 1);
     }
+    fe = block_sum<MB / WAVE>(fe, red);
+    if (threadIdx.x == 0 && fe) atomicAdd(&ctl->fedges[L % 3], fe);
     if (__ballot(found_any != 0) && lane == 0) ctl->active[L % 3] = 1;
 }
 
 }  // namespace
 
 struct MsWork {
+    int W = 0;  // words per vertex mask of the allocation
     DevBuf<u64> V, F, Fn;
     DevBuf<int32_t> dist;
     DevBuf<int64_t> src;
@@ -158,7 +362,7 @@ struct MsWork {
 
 void delete_ms_work(MsWork* p) { delete p; }
 
-template <typename Off>
+template <typename Off, int W>
 static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, int32_t* dist_out, double* kernel_ms,
                     i64* levels) {
     hipStream_t s = g.ctx->stream;
@@ -168,15 +372,23 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, int32_t
     PJ_HIP(hipMemcpyAsync(w.src.p, sources, sizeof(int64_t) * (size_t)ns, hipMemcpyHostToDevice, s));
     int64_t* host_dev = nullptr;
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&host_dev), w.host, 0));
-    u64 smask = 0;  // bits of the valid sources of this batch
+    Mask<W> smask{};  // bits of the valid sources of this batch
+    bool any = false;
     for (int i = 0; i < ns; ++i)
-        if (sources[i] >= 0 && sources[i] < n) smask |= 1ull << i;
+        if (sources[i] >= 0 && sources[i] < n) {
+            smask.w[i >> 6] |= 1ull << (i & 63);
+            any = true;
+        }
     const unsigned grid = (unsigned)g.ctx->cu_count * 4u;
+    const Off* row = static_cast<const Off*>(g.row_ptr());
+    const u32* col = g.col.p;
+    // push while the frontier's out-edges are below nnz / ms_alpha (0: never)
+    const u64 push_max = g.ms_alpha > 0 ? (u64)((double)g.nnz / g.ms_alpha) : 0ull;
     PJ_HIP(hipEventRecord(g.ev0, s));
-    ms_init_k<<<grid_for(std::max<i64>(n, (i64)ns * n / 4), MB, (unsigned)g.ctx->cu_count * 8u), MB, 0, s>>>(
-        w.V.p, w.F.p, n, w.dist.p, (i64)ns * n);
+    ms_init_k<<<grid_for(std::max<i64>(n * W, (i64)ns * n / 4), MB, (unsigned)g.ctx->cu_count * 8u), MB, 0, s>>>(
+        w.V.p, w.F.p, n * W, w.dist.p, (i64)ns * n, w.ctl.p, host_dev);
     PJ_LAUNCH_CHECK();
-    ms_sources_k<<<1, 1, 0, s>>>(w.src.p, ns, n, w.V.p, w.F.p, w.dist.p, w.ctl.p, host_dev);
+    ms_sources_k<Off><<<(ns + 255) / 256, 256, 0, s>>>(w.src.p, ns, W, n, row, w.V.p, w.F.p, w.dist.p, w.ctl.p);
     PJ_LAUNCH_CHECK();
     int32_t L = 0;
     int batch = 16;
@@ -184,12 +396,21 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, int32_t
     u64* Fn = w.Fn.p;
     for (;;) {
         for (int i = 0; i < batch && L < INT_INF; ++i, ++L) {
-            ms_level_k<Off><<<grid, MB, 0, s>>>(n, crow, ccol, w.V.p, F, Fn, w.dist.p, L, smask, w.ctl.p, host_dev);
+            ms_prep_k<W><<<grid, MB, 0, s>>>(n, Fn, L, push_max, w.ctl.p, host_dev);
             PJ_LAUNCH_CHECK();
+            ms_level_k<Off, W><<<grid, MB, 0, s>>>(n, crow, ccol, row, w.V.p, F, Fn, w.dist.p, L, smask, push_max,
+                                                   w.ctl.p);
+            PJ_LAUNCH_CHECK();
+            if (push_max) {
+                ms_push_k<Off, W><<<grid, MB, 0, s>>>(n, row, col, F, Fn, L, push_max, w.ctl.p);
+                PJ_LAUNCH_CHECK();
+                ms_fin_k<Off, W><<<grid, MB, 0, s>>>(n, row, w.V.p, Fn, w.dist.p, L, smask, push_max, w.ctl.p);
+                PJ_LAUNCH_CHECK();
+            }
             std::swap(F, Fn);
         }
         PJ_HIP(hipStreamSynchronize(s));
-        if (*(volatile int64_t*)w.host >= 0 || L >= INT_INF || smask == 0) break;
+        if (*(volatile int64_t*)w.host >= 0 || L >= INT_INF || !any) break;
         batch = batch < 1024 ? batch * 2 : batch;
     }
     PJ_HIP(hipEventRecord(g.ev1, s));
@@ -202,16 +423,35 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, int32_t
     if (dist_out && n) PJ_HIP(hipMemcpy(dist_out, w.dist.p, sizeof(int32_t) * (size_t)ns * (size_t)n, hipMemcpyDeviceToHost));
 }
 
+template <typename Off>
+static void ms_pass_w(int W, Graph& g, MsWork& w, const int64_t* sources, int ns, int32_t* dist_out,
+                      double* kernel_ms, i64* levels) {
+    if (W == 4) ms_pass<Off, 4>(g, w, sources, ns, dist_out, kernel_ms, levels);
+    else if (W == 2) ms_pass<Off, 2>(g, w, sources, ns, dist_out, kernel_ms, levels);
+    else ms_pass<Off, 1>(g, w, sources, ns, dist_out, kernel_ms, levels);
+}
+
+// Pass width: the fewest words that hold the batch, at most MS_WMAX (g.ms_width
+// caps it), and the pass's distance block (64 W x n int32) kept under 16 GB.
+static int ms_words(const Graph& g, int n_src) {
+    int W = 1;
+    const int cap = g.ms_width > 0 ? std::min(g.ms_width, MS_WMAX) : MS_WMAX;
+    while (W < cap && 64 * W < n_src && (double)(128 * W) * 4.0 * (double)g.n <= 16e9) W *= 2;
+    return W;
+}
+
 void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out) {
     const size_t n = (size_t)g.n;
-    if (!g.ms_work) {
+    const int W = ms_words(g, n_src);
+    if (!g.ms_work || g.ms_work->W < W) {
         g.ms_work.reset(new MsWork());
         MsWork& w = *g.ms_work;
-        w.V.alloc(n ? n : 1);
-        w.F.alloc(n ? n : 1);
-        w.Fn.alloc(n ? n : 1);
-        w.dist.alloc(n ? 64 * n : 1);
-        w.src.alloc(64);
+        w.W = W;
+        w.V.alloc(n ? n * W : 1);
+        w.F.alloc(n ? n * W : 1);
+        w.Fn.alloc(n ? n * W : 1);
+        w.dist.alloc(n ? 64 * W * n : 1);
+        w.src.alloc(64 * W);
         w.ctl.alloc(1);
         PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.host), sizeof(int64_t), hipHostMallocMapped));
     }
@@ -221,11 +461,12 @@ void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out)
     pj_stats st{};
     double kms = 0;
     i64 levels = 0;
-    for (int off = 0; off < n_src; off += 64) {
-        const int ns = std::min(64, n_src - off);
+    const int per = 64 * W;
+    for (int off = 0; off < n_src; off += per) {
+        const int ns = std::min(per, n_src - off);
         int32_t* out = dist_out ? dist_out + (size_t)off * n : nullptr;
-        if (g.off64) ms_pass<u64>(g, *g.ms_work, sources + off, ns, out, &kms, &levels);
-        else ms_pass<u32>(g, *g.ms_work, sources + off, ns, out, &kms, &levels);
+        if (g.off64) ms_pass_w<u64>(W, g, *g.ms_work, sources + off, ns, out, &kms, &levels);
+        else ms_pass_w<u32>(W, g, *g.ms_work, sources + off, ns, out, &kms, &levels);
     }
     st.kernel_ms = kms;
     st.levels = levels;

@@ -291,7 +291,7 @@ def test_cli_end_to_end(pj, oracle, tmp_path):
 
 @pytest.mark.parametrize("kind", ["uniform", "hub", "chain"])
 def test_msbfs_batch_rows(ctx, oracle, kind):
-    """pj_sssp_batch (64 sources per pass, msbfs.hip): every row equals a single-source run."""
+    """pj_sssp_batch (64 x W sources per pass, msbfs.hip): every row equals a single-source run."""
     rng = np.random.default_rng(77 + len(kind))
     n = 20000
     src, dst = random_graph(rng, kind, n)
@@ -302,6 +302,25 @@ def test_msbfs_batch_rows(ctx, oracle, kind):
     assert out.shape == (len(sources), n)
     for i, r in enumerate(sources):
         assert (out[i] == oracle.bfs(row, col, r)).all(), (kind, i, r)
+
+
+@pytest.mark.parametrize("width,alpha", [(1, 16), (2, 0), (4, 16), (4, 1e9)])
+def test_msbfs_pass_widths(ctx, oracle, width, alpha):
+    """Passes of 64 x W sources (W words per vertex mask): 300 sources cross several
+    passes and a partial last word; push and pull levels; rows equal single-source runs."""
+    rng = np.random.default_rng(5 + width)
+    n = 12000
+    src, dst = random_graph(rng, "hub", n)
+    g = ctx.load_coo(src, dst, n=n)
+    g.set_option("ms_width", width)
+    g.set_option("ms_alpha", alpha)  # push levels: default rule, never, always
+    row, col, _ = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n)
+    sources = [int(x) for x in rng.integers(-2, n + 2, 300)]
+    out = g.sssp_batch(sources)
+    exp = {r: oracle.bfs(row, col, r) for r in set(sources)}
+    for i, r in enumerate(sources):
+        assert (out[i] == exp[r]).all(), (width, i, r)
+    g.close()
 
 
 def test_msbfs_kronecker_and_chain_cap(ctx, oracle, pj):
