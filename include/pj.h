@@ -228,6 +228,57 @@ int pj_part_reach(pj_part* p, int64_t* out);
 int pj_part_copy_dist(pj_part* p, int32_t* dist_out);
 const int32_t* pj_part_dist_device(pj_part* p);
 
+/* ---- weighted SSSP over a 1D vertex partition (the
+ * delta-stepping variant) ---------------------------------------------------
+ *
+ * Same block geometry as pj_part_*. Rank r keeps the weighted out-rows of its
+ * block, cut from a weighted graph loaded on its GPU (the reference's rank 0
+ * builds the whole CSR and scatters row blocks, :344-410; here every rank cuts
+ * its own block, nothing is scattered). The band loop runs in the caller
+ * (paralleljohnson_amd/partition.py PartitionedDelta), the analogue of the
+ * reference's round loop :488-594 with bands of width delta:
+ *
+ *   delta = pj_wpart_begin(source, delta or 0 for the default)
+ *   lo = 0
+ *   loop: pj_wpart_select(lo, lo + delta) -> (count, min dist >= lo)
+ *         all_reduce sum(count), min(min): count 0 -> jump lo to the band of
+ *         min, or stop when min = INF (the termination test :579-593)
+ *         light rounds until all_reduce sum(new frontier) = 0:
+ *           pj_wpart_relax(light = 1) -> send (u64 id | cand << 32, owner-major),
+ *           counts[world]; all_to_all_single; pj_wpart_apply(received);
+ *           pj_wpart_end_round -> new frontier size on this rank
+ *         heavy step: pj_wpart_relax(light = 0); exchange; pj_wpart_apply
+ *         lo += delta
+ *
+ * send and recv are device buffers of capacity world * block u64. Distances
+ * follow the R9 contract with the graph's integer weights. */
+typedef struct pj_wpart pj_wpart;
+/* The rank's block of a weighted graph (pj_load_coo / pj_load_snap(weighted) /
+ * pj_generate_kronecker(weighted)); the graph may be destroyed afterwards. */
+int pj_wpart_from_graph(pj_graph* g, int rank, int world, pj_wpart** out);
+int pj_wpart_destroy(pj_wpart* p);
+/* out[8] = (n, lo, hi, block, nnz_local, world, rank, nnz of the whole graph) */
+int pj_wpart_info(const pj_wpart* p, int64_t* out);
+/* Start a solve from `source` (dist := INF, then the source); delta <= 0 picks
+ * the single-GPU default (3.5 x mean weight / mean degree). *delta_out = delta. */
+int pj_wpart_begin(pj_wpart* p, int64_t source, int32_t delta, int32_t* delta_out);
+/* Band [lo, hi): frontier := owned vertices with dist in [lo, hi). out[2] =
+ * (its size, min owned dist >= lo or PJ_INT_INF). */
+int pj_wpart_select(pj_wpart* p, int32_t lo, int32_t hi, int64_t* out);
+/* light != 0: the frontier relaxes its light edges (w < delta) and joins the
+ * band's members; light == 0: the members relax their heavy edges. Remote
+ * candidates are written to send owner-major, counts[world] per owner. */
+int pj_wpart_relax(pj_wpart* p, int light, int32_t lo, int32_t hi, uint64_t* send, int64_t* counts);
+/* Fold the received candidates into the owned distances (light: those below hi
+ * join the next frontier). */
+int pj_wpart_apply(pj_wpart* p, const uint64_t* recv, int64_t n_recv, int light, int32_t lo, int32_t hi);
+/* The round's new frontier becomes current; *n_f = its size on this rank. */
+int pj_wpart_end_round(pj_wpart* p, int64_t* n_f);
+/* out[2] = (reached owned vertices, their out-edge sum) */
+int pj_wpart_reach(pj_wpart* p, int64_t* out);
+/* The owned block's distances (hi - lo int32) to the host. */
+int pj_wpart_copy_dist(pj_wpart* p, int32_t* dist_out);
+
 /* ---- output (replaces output_vector :32-46 + the write at :615-620) ------ */
 
 /* Write the sol_file: "the vector is:\n" then, for v = 0..n-1, the decimal

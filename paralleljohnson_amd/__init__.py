@@ -108,6 +108,16 @@ _SIGS = {
     "pj_part_reach": ([_P, _P], _INT),
     "pj_part_copy_dist": ([_P, _P], _INT),
     "pj_part_dist_device": ([_P], _P),
+    "pj_wpart_from_graph": ([_P, _INT, _INT, _PP], _INT),
+    "pj_wpart_destroy": ([_P], _INT),
+    "pj_wpart_info": ([_P, _P], _INT),
+    "pj_wpart_begin": ([_P, _I64, ctypes.c_int32, _P], _INT),
+    "pj_wpart_select": ([_P, ctypes.c_int32, ctypes.c_int32, _P], _INT),
+    "pj_wpart_relax": ([_P, _INT, ctypes.c_int32, ctypes.c_int32, _P, _P], _INT),
+    "pj_wpart_apply": ([_P, _P, _I64, _INT, ctypes.c_int32, ctypes.c_int32], _INT),
+    "pj_wpart_end_round": ([_P, _P], _INT),
+    "pj_wpart_reach": ([_P, _P], _INT),
+    "pj_wpart_copy_dist": ([_P, _P], _INT),
 }
 for _name, (_args, _res) in _SIGS.items():
     _fn = getattr(_lib, _name)

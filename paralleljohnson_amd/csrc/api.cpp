@@ -505,6 +505,91 @@ int pj_write_sol(const int32_t* dist, int64_t n, const char* path, int strict) {
     });
 }
 
+// ---- weighted SSSP over a 1D vertex partition (wpart.hip) -----------------
+
+int pj_wpart_from_graph(pj_graph* g, int rank, int world, pj_wpart** out) {
+    if (!g || !out) return arg_error("pj_wpart_from_graph: bad argument");
+    if (world < 1 || world > 64 || rank < 0 || rank >= world)
+        return arg_error("pj_wpart_from_graph: need 0 <= rank < world <= 64");
+    *out = nullptr;
+    return guarded([&] {
+        bind(*g->g.ctx);
+        *out = reinterpret_cast<pj_wpart*>(wpart_from_graph(g->g, rank, world));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_destroy(pj_wpart* p) {
+    if (!p) return PJ_OK;
+    return guarded([&] {
+        delete_wpart(reinterpret_cast<WPart*>(p));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_info(const pj_wpart* p, int64_t* out) {
+    if (!p || !out) return arg_error("pj_wpart_info: bad argument");
+    wpart_info(*reinterpret_cast<const WPart*>(p), out);
+    return PJ_OK;
+}
+
+int pj_wpart_begin(pj_wpart* p, int64_t source, int32_t delta, int32_t* delta_out) {
+    if (!p) return arg_error("pj_wpart_begin: bad argument");
+    return guarded([&] {
+        const int32_t d = wpart_begin(*reinterpret_cast<WPart*>(p), source, delta);
+        if (delta_out) *delta_out = d;
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_select(pj_wpart* p, int32_t lo, int32_t hi, int64_t* out) {
+    if (!p || !out || lo < 0 || hi < lo) return arg_error("pj_wpart_select: bad argument");
+    return guarded([&] {
+        wpart_select(*reinterpret_cast<WPart*>(p), lo, hi, out);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_relax(pj_wpart* p, int light, int32_t lo, int32_t hi, uint64_t* send, int64_t* counts) {
+    if (!p || !counts || lo < 0 || hi < lo) return arg_error("pj_wpart_relax: bad argument");
+    return guarded([&] {
+        wpart_relax(*reinterpret_cast<WPart*>(p), light, lo, hi, (u64*)send, counts);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_apply(pj_wpart* p, const uint64_t* recv, int64_t n_recv, int light, int32_t lo, int32_t hi) {
+    if (!p || n_recv < 0 || (n_recv > 0 && !recv)) return arg_error("pj_wpart_apply: bad argument");
+    return guarded([&] {
+        wpart_apply(*reinterpret_cast<WPart*>(p), (const u64*)recv, n_recv, light, lo, hi);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_end_round(pj_wpart* p, int64_t* n_f) {
+    if (!p || !n_f) return arg_error("pj_wpart_end_round: bad argument");
+    return guarded([&] {
+        *n_f = wpart_end_round(*reinterpret_cast<WPart*>(p));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_reach(pj_wpart* p, int64_t* out) {
+    if (!p || !out) return arg_error("pj_wpart_reach: bad argument");
+    return guarded([&] {
+        wpart_reach(*reinterpret_cast<WPart*>(p), out);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_copy_dist(pj_wpart* p, int32_t* dist_out) {
+    if (!p || !dist_out) return arg_error("pj_wpart_copy_dist: bad argument");
+    return guarded([&] {
+        wpart_copy_dist(*reinterpret_cast<WPart*>(p), dist_out);
+        return (int)PJ_OK;
+    });
+}
+
 // debug only (not declared in include/pj.h)
 int pj_debug_bitmaps(pj_graph* pg, uint64_t* vis0, uint64_t* vis1, uint64_t* fnew) {
     if (!pg) return arg_error("pj_debug_bitmaps: graph is NULL");

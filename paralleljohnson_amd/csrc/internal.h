@@ -247,6 +247,18 @@ void reach_stats(Graph& g, i64* n_r, i64* m_r);
 void debug_bitmaps(Graph& g, u64* vis0, u64* vis1, u64* fnew);
 
 // 1D vertex partition (part.hip)
+struct WPart;
+void delete_wpart(WPart* p);
+WPart* wpart_from_graph(Graph& g, int rank, int world);
+void wpart_info(const WPart& p, i64* out8);
+int32_t wpart_begin(WPart& p, i64 source, int32_t delta);
+void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2);
+void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts);
+void wpart_apply(WPart& p, const u64* recv, i64 nr, int light, int32_t lo, int32_t hi);
+i64 wpart_end_round(WPart& p);
+void wpart_reach(WPart& p, i64* out2);
+void wpart_copy_dist(WPart& p, int32_t* host);
+
 struct Part;
 void delete_part(Part* p);
 Part* part_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, int rank, int world);

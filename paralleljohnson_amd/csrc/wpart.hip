@@ -1,0 +1,559 @@
+// wpart.hip — weighted SSSP (delta-stepping) over a 1D vertex partition, one
+// process per GPU ("Δ-stepping variant").
+//
+// Same block geometry as part.hip (the reference's nn2rank / get_start_nn,
+// ParallelJohnson.cpp:169-200, with 64-aligned blocks): rank r owns vertices
+// [lo, hi) and their out-rows (weights kept, rows weight-sorted as graph.hip
+// stores them). The band loop runs in the caller (paralleljohnson_amd/
+// partition.py, torch.distributed over RCCL), the analogue of the reference's
+// round loop :488-594:
+//
+//   select(lo, hi)     : frontier := owned vertices with dist in [lo, hi);
+//                        all_reduce(sum) of its size, all_reduce(min) of the
+//                        smallest owned dist >= lo (the next occupied band when
+//                        this one is empty; INF everywhere = the end, cf. :579-593)
+//   light rounds       : relax the frontier's light edges (w < delta). An owned
+//                        target is lowered with atomicMin and joins the next
+//                        frontier when it lands below hi; a remote target's
+//                        candidate is folded into a full-size `cand` array
+//                        (atomicMin) and its `touched` bit set. pack: every
+//                        touched remote target once, as (id, cand) owner-major —
+//                        the per-owner send buffers of :537-542 — exchanged with
+//                        all_to_all_single (:522-554); apply: the owner folds the
+//                        received candidates in the same way. A round ends with
+//                        all_reduce(sum) of the new frontier sizes.
+//   heavy step         : the band's members relax their heavy edges once (same
+//                        relax / pack / exchange / apply).
+//
+// `cand` keeps the best value sent for each remote id during a solve, so a
+// target is re-sent only when this rank improves on it: the send volume of a
+// round is bounded by the distinct remote targets improved (<= block per
+// owner), unlike the reference's unbounded buffers.
+// Rows longer than WP_LONG edges go to a queue relaxed by the whole grid.
+#include <algorithm>
+#include <cmath>
+
+#include "devutil.h"
+
+namespace pj {
+
+namespace {
+
+// current value of a distance that atomics may have lowered (agent-scope load:
+// the L2 of this XCD may hold a stale line; see delta.hip dist_now)
+__device__ __forceinline__ int32_t wp_now(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int WB = 256;
+constexpr int WSC = 16;        // frontier words a wave screens at once
+constexpr int WP_SERIAL = 8;   // edges a lane relaxes alone
+constexpr u64 WP_LONG = 1024;  // longer row segments: the grid-wide queue
+constexpr int WP_MAXW = 64;    // largest world size
+
+// stat slots (u64): [0, 64) per-owner region counts, then:
+constexpr int ST_LONGQ = 64;   // long-row queue length
+constexpr int ST_NF = 65;      // vertices marked in the next frontier
+constexpr int ST_MIN = 66;     // min owned dist >= lo (select)
+constexpr int ST_CNT = 67;     // selected frontier size
+constexpr int ST_REACH = 68;   // reached vertices, [69] their out-edges
+constexpr int ST_N = 72;
+
+struct WArgs {
+    i64 n, lo, nl, block, bw;
+    int rank;
+    int32_t dlo, dhi;  // band [dlo, dhi)
+    const u64* row;    // nl + 1
+    const u32* col;
+    const u32* w;
+    const u32* lsplit;
+    int32_t* dist;     // nl
+    int32_t* cand;     // n (world > 1)
+    u64* touched;      // n / 64 words (world > 1)
+    u64* fr;           // bw
+    u64* frn;          // bw
+    u64* mb;           // bw
+    u32* lq_v;         // long-row queue: local vertex, begin, end
+    u64* lq_b;
+    u64* lq_e;
+    u64* stat;
+};
+
+__device__ __forceinline__ void wp_edge(const WArgs& a, bool light, u32 t, long long nd) {
+    if (nd >= INT_INF) return;
+    const i64 tl = (i64)t - a.lo;
+    if (tl >= 0 && tl < a.nl) {
+        if ((int32_t)nd < wp_now(a.dist + tl)) {
+            atomicMin(a.dist + tl, (int32_t)nd);
+            if (light && (int32_t)nd < a.dhi) {
+                const u64 bit = 1ull << (tl & 63);
+                if (!(atomicOr(a.frn + (tl >> 6), bit) & bit)) atomicAdd(&a.stat[ST_NF], 1ull);
+            }
+        }
+    } else if ((int32_t)nd < wp_now(a.cand + t)) {
+        atomicMin(a.cand + t, (int32_t)nd);
+        atomicOr(a.touched + (t >> 6), 1ull << (t & 63));
+    }
+}
+
+__global__ void wp_seed_k(WArgs a, i64 s) {
+    const i64 sl = s - a.lo;
+    if (sl >= 0 && sl < a.nl) a.dist[sl] = 0;
+}
+
+// frontier := owned vertices with dist in [dlo, dhi); frn := 0; mb := 0 (new band)
+__global__ __launch_bounds__(WB) void wp_select_k(WArgs a) {
+    __shared__ u64 red[WB / WAVE];
+    const int lane = lane_id();
+    u64 c = 0;
+    int32_t mn = INT_INF;
+    for (i64 wi = (i64)blockIdx.x * (WB / WAVE) + wave_id(); wi < a.bw; wi += (i64)gridDim.x * (WB / WAVE)) {
+        const i64 v = wi * 64 + lane;
+        const int32_t d = v < a.nl ? a.dist[v] : INT_INF;
+        const u64 m = __ballot(d >= a.dlo && d < a.dhi);
+        if (d >= a.dlo && d < mn) mn = d;
+        if (lane == 0) {
+            a.fr[wi] = m;
+            a.frn[wi] = 0;
+            a.mb[wi] = 0;
+            c += (u64)__popcll(m);
+        }
+    }
+    c = block_sum<WB / WAVE>(c, red);
+    if (threadIdx.x == 0 && c) atomicAdd(&a.stat[ST_CNT], c);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int32_t y = __shfl_xor(mn, off, 64);
+        mn = y < mn ? y : mn;
+    }
+    if (lane == 0 && mn < INT_INF) atomicMin(&a.stat[ST_MIN], (u64)mn);
+}
+
+// LIGHT: the frontier fr relaxes its light prefixes (fr words are cleared as
+// read, members join mb); HEAVY: mb relaxes its heavy suffixes.
+template <bool LIGHT>
+__global__ __launch_bounds__(WB) void wp_relax_k(WArgs a) {
+    const int lane = lane_id();
+    const i64 nsc = (a.bw + WSC - 1) / WSC;
+    for (i64 sc = (i64)blockIdx.x * (WB / WAVE) + wave_id(); sc < nsc; sc += (i64)gridDim.x * (WB / WAVE)) {
+        const i64 wbase = sc * WSC;
+        u64 mytodo = 0;
+        if (lane < WSC && wbase + lane < a.bw) {
+            if (LIGHT) {
+                mytodo = a.fr[wbase + lane];
+                if (mytodo) {
+                    a.fr[wbase + lane] = 0;
+                    a.mb[wbase + lane] |= mytodo;  // the wave owns these words
+                }
+            } else {
+                mytodo = a.mb[wbase + lane];
+            }
+        }
+        if (!__ballot(mytodo != 0)) continue;
+        const u32 cnt = (u32)__popcll(mytodo);
+        const u32 incl = wave_incl_scan(cnt);
+        const u32 myex = incl - cnt;
+        const u32 T = __shfl(incl, 63, 64);
+        for (u32 r0 = 0; r0 < T; r0 += WAVE) {
+            const u32 c = r0 + lane;
+            const bool act = c < T;
+            u32 jw = 0;
+#pragma unroll
+            for (u32 step = WSC / 2; step > 0; step >>= 1) {
+                const u32 x = __shfl(myex, jw + step, 64);
+                if (x <= c) jw += step;
+            }
+            const u32 ex = __shfl(myex, jw, 64);
+            const u64 tw = __shfl(mytodo, jw, 64);
+            u64 b = 0, e = 0;
+            int32_t du = 0;
+            u32 v = 0;
+            if (act) {
+                v = (u32)((wbase + jw) * 64 + select_bit(tw, c - ex));
+                du = a.dist[v];
+                const u64 r0v = a.row[v], sp = r0v + a.lsplit[v];
+                b = LIGHT ? r0v : sp;
+                e = LIGHT ? sp : a.row[v + 1];
+                if (e - b > WP_LONG) {  // long segment: the grid-wide queue
+                    const u64 q = atomicAdd(&a.stat[ST_LONGQ], 1ull);
+                    a.lq_v[q] = v;
+                    a.lq_b[q] = b;
+                    a.lq_e[q] = e;
+                    e = b;
+                }
+            }
+            u64 k = b;
+            const u64 lim = (e - b > (u64)WP_SERIAL) ? b + WP_SERIAL : e;
+            for (; k < lim; ++k) wp_edge(a, LIGHT, a.col[k], (long long)du + a.w[k]);
+            // the rest, edge-balanced over the wave
+            if (__ballot(k < e)) {
+                const u64 rem = k < e ? e - k : 0;
+                const u64 inc = wave_incl_scan(rem);
+                const u64 exc = inc - rem;
+                const u64 tot = __shfl(inc, 63, 64);
+                for (u64 g0 = 0; g0 < tot; g0 += WAVE) {
+                    const u64 gi = g0 + lane;
+                    int l = 0;
+#pragma unroll
+                    for (int step = 32; step > 0; step >>= 1)
+                        if (__shfl(inc, l + step - 1, 64) <= gi) l += step;
+                    const u64 kl = __shfl(k, l, 64), xl = __shfl(exc, l, 64);
+                    const int32_t dl = __shfl(du, l, 64);
+                    if (gi < tot) {
+                        const u64 kk = kl + (gi - xl);
+                        wp_edge(a, LIGHT, a.col[kk], (long long)dl + a.w[kk]);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// the long segments queued by wp_relax_k, each spread over the whole grid
+template <bool LIGHT>
+__global__ __launch_bounds__(WB) void wp_long_k(WArgs a) {
+    const u64 nq = a.stat[ST_LONGQ];
+    const u64 tid = (u64)blockIdx.x * WB + threadIdx.x, nth = (u64)gridDim.x * WB;
+    for (u64 q = 0; q < nq; ++q) {
+        const u64 b = a.lq_b[q], e = a.lq_e[q];
+        const int32_t du = a.dist[a.lq_v[q]];
+        for (u64 k = b + tid; k < e; k += nth) wp_edge(a, LIGHT, a.col[k], (long long)du + a.w[k]);
+    }
+}
+
+// Touched remote targets -> (id | cand << 32) in the owner's region of `reg`
+// (region o at o * block; one entry per distinct target, so no region
+// overflows). Bits are cleared as read. A lane owns one touched word (64 ids
+// of one owner); per-owner counts are wave-aggregated.
+__global__ __launch_bounds__(WB) void wp_pack_k(WArgs a, i64 nwords, u64* __restrict__ reg) {
+    const int lane = lane_id();
+    const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
+    for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; w0 < nwords; w0 += nwaves * 64) {
+        const i64 wi = w0 + lane;
+        u64 bits = 0;
+        if (wi < nwords) {
+            bits = a.touched[wi];
+            if (bits) a.touched[wi] = 0;
+        }
+        const u32 cnt = (u32)__popcll(bits);
+        const int owner = wi < nwords ? (int)((wi * 64) / a.block) : -1;
+        u64 pending = __ballot(cnt != 0);
+        u64 base = 0;
+        while (pending) {  // one atomic per (wave, owner)
+            const int l = __ffsll((long long)pending) - 1;
+            const int o = __shfl(owner, l, 64);
+            const bool mine = cnt != 0 && owner == o;
+            const u64 grp = __ballot(mine);
+            pending &= ~grp;
+            const u32 x = mine ? cnt : 0u;
+            const u32 inc = wave_incl_scan(x);
+            const u32 tot = __shfl(inc, 63, 64);
+            u64 ob = 0;
+            if (lane == l) ob = atomicAdd(&a.stat[o], (u64)tot);
+            ob = __shfl(ob, l, 64);
+            if (mine) base = ob + (inc - x);
+        }
+        u64* out = cnt ? reg + (i64)owner * a.block + base : nullptr;
+        while (bits) {
+            const int bb = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            const u32 t = (u32)(wi * 64 + bb);
+            *out++ = (u64)t | ((u64)(u32)a.cand[t] << 32);
+        }
+    }
+}
+
+// received (id | cand << 32) for this rank
+__global__ __launch_bounds__(WB) void wp_apply_k(WArgs a, const u64* __restrict__ recv, i64 nr, int light) {
+    for (i64 i = (i64)blockIdx.x * WB + threadIdx.x; i < nr; i += (i64)gridDim.x * WB) {
+        const u64 x = recv[i];
+        wp_edge(a, light != 0, (u32)x, (long long)(int32_t)(u32)(x >> 32));
+    }
+}
+
+// fr := frn, frn := 0 (the round's new frontier becomes current)
+__global__ void wp_swap_k(WArgs a) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < a.bw; i += (i64)gridDim.x * blockDim.x) {
+        a.fr[i] = a.frn[i];
+        a.frn[i] = 0;
+    }
+}
+
+__global__ void wp_rebase_k(const void* row, bool off64, i64 lo, i64 nl, u64* __restrict__ out) {
+    const u64 base = off64 ? ((const u64*)row)[lo] : (u64)((const u32*)row)[lo];
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i <= nl; i += (i64)gridDim.x * blockDim.x)
+        out[i] = (off64 ? ((const u64*)row)[lo + i] : (u64)((const u32*)row)[lo + i]) - base;
+}
+
+__global__ void wp_lsplit_k(const u64* __restrict__ row, const u32* __restrict__ w, i64 nl, u32 delta,
+                            u32* __restrict__ out) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < nl; v += (i64)gridDim.x * blockDim.x) {
+        u64 lo = row[v], hi = row[v + 1];
+        const u64 b = lo;
+        while (lo < hi) {  // rows are weight-sorted
+            const u64 mid = lo + (hi - lo) / 2;
+            if (w[mid] < delta) lo = mid + 1;
+            else hi = mid;
+        }
+        out[v] = (u32)(lo - b);
+    }
+}
+
+__global__ __launch_bounds__(WB) void wp_reach_k(WArgs a) {
+    __shared__ u64 red[WB / WAVE];
+    u64 c = 0, m = 0;
+    for (i64 v = (i64)blockIdx.x * WB + threadIdx.x; v < a.nl; v += (i64)gridDim.x * WB)
+        if (a.dist[v] < INT_INF) {
+            ++c;
+            m += a.row[v + 1] - a.row[v];
+        }
+    c = block_sum<WB / WAVE>(c, red);
+    m = block_sum<WB / WAVE>(m, red);
+    if (threadIdx.x == 0) {
+        if (c) atomicAdd(&a.stat[ST_REACH], c);
+        if (m) atomicAdd(&a.stat[ST_REACH + 1], m);
+    }
+}
+
+__global__ void wsum_all_k(const u32* __restrict__ w, i64 m, u64* __restrict__ out) {
+    u64 s = 0;
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x) s += w[i];
+    s = wave_sum(s);
+    if (lane_id() == 0 && s) atomicAdd(out, s);
+}
+
+}  // namespace
+
+struct WPart {
+    Ctx* ctx = nullptr;
+    i64 n = 0, lo = 0, hi = 0, nl = 0, block = 64, bw = 1, nnz_local = 0, nnz = 0;
+    int rank = 0, world = 1;
+    double mean_w = 1.0;
+    int32_t delta = 0;
+    DevBuf<u64> row;
+    DevBuf<u32> col, w, lsplit;
+    DevBuf<int32_t> dist, cand;
+    DevBuf<u64> touched, fr, frn, mb, reg, stat;
+    DevBuf<u32> lq_v;
+    DevBuf<u64> lq_b, lq_e;
+    std::vector<u64> hstat;
+    unsigned grid() const { return (unsigned)ctx->cu_count * 8u; }
+    WArgs args(int32_t dlo = 0, int32_t dhi = 0) {
+        WArgs a{};
+        a.n = n;
+        a.lo = lo;
+        a.nl = nl;
+        a.block = block;
+        a.bw = bw;
+        a.rank = rank;
+        a.dlo = dlo;
+        a.dhi = dhi;
+        a.row = row.p;
+        a.col = col.p;
+        a.w = w.p;
+        a.lsplit = lsplit.p;
+        a.dist = dist.p;
+        a.cand = cand.p;
+        a.touched = touched.p;
+        a.fr = fr.p;
+        a.frn = frn.p;
+        a.mb = mb.p;
+        a.lq_v = lq_v.p;
+        a.lq_b = lq_b.p;
+        a.lq_e = lq_e.p;
+        a.stat = stat.p;
+        return a;
+    }
+    void read_stat() {
+        PJ_HIP(hipMemcpyAsync(hstat.data(), stat.p, sizeof(u64) * ST_N, hipMemcpyDeviceToHost, ctx->stream));
+        PJ_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    void clear_stat() { PJ_HIP(hipMemsetAsync(stat.p, 0, sizeof(u64) * ST_N, ctx->stream)); }
+};
+
+void delete_wpart(WPart* p) { delete p; }
+
+WPart* wpart_from_graph(Graph& g, int rank, int world) {
+    if (!g.weighted) throw Error(PJ_ERR_ARG, "pj_wpart_from_graph: the graph has no weights");
+    if (world < 1 || world > WP_MAXW || rank < 0 || rank >= world) throw Error(PJ_ERR_ARG, "rank/world out of range");
+    hipStream_t s = g.ctx->stream;
+    std::unique_ptr<WPart> p(new WPart());
+    p->ctx = g.ctx;
+    p->n = g.n;
+    p->nnz = g.nnz;
+    p->rank = rank;
+    p->world = world;
+    const i64 per = (g.n + world - 1) / world;
+    p->block = std::max<i64>(64, (per + 63) / 64 * 64);
+    p->bw = p->block / 64;
+    p->lo = std::min<i64>((i64)rank * p->block, g.n);
+    p->hi = std::min<i64>(p->lo + p->block, g.n);
+    p->nl = p->hi - p->lo;
+    // rows [lo, hi) of the CSR: offsets rebased, edges and weights copied
+    u64 eb = 0, ee = 0;
+    if (g.n > 0) {
+        if (g.off64) {
+            PJ_HIP(hipMemcpyAsync(&eb, g.row64.p + p->lo, sizeof(u64), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipMemcpyAsync(&ee, g.row64.p + p->hi, sizeof(u64), hipMemcpyDeviceToHost, s));
+        } else {
+            u32 b32 = 0, e32 = 0;
+            PJ_HIP(hipMemcpyAsync(&b32, g.row32.p + p->lo, sizeof(u32), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipMemcpyAsync(&e32, g.row32.p + p->hi, sizeof(u32), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipStreamSynchronize(s));
+            eb = b32;
+            ee = e32;
+        }
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+    p->nnz_local = (i64)(ee - eb);
+    p->row.alloc((size_t)p->nl + 1);
+    if (g.n > 0) {
+        wp_rebase_k<<<grid_for(p->nl + 1, 256, p->grid()), 256, 0, s>>>(g.row_ptr(), g.off64, p->lo, p->nl, p->row.p);
+        PJ_LAUNCH_CHECK();
+    } else {
+        PJ_HIP(hipMemsetAsync(p->row.p, 0, sizeof(u64), s));
+    }
+    p->col.alloc((size_t)std::max<i64>(p->nnz_local, 1));
+    p->w.alloc((size_t)std::max<i64>(p->nnz_local, 1));
+    if (p->nnz_local) {
+        PJ_HIP(hipMemcpyAsync(p->col.p, g.col.p + eb, sizeof(u32) * (size_t)p->nnz_local, hipMemcpyDeviceToDevice, s));
+        PJ_HIP(hipMemcpyAsync(p->w.p, g.w.p + eb, sizeof(u32) * (size_t)p->nnz_local, hipMemcpyDeviceToDevice, s));
+    }
+    // mean weight over the whole graph (the default delta, as delta.hip)
+    u64 wsum = 0;
+    if (g.nnz > 0) {
+        DevBuf<u64> acc(1);
+        PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
+        wsum_all_k<<<grid_for(g.nnz, 256, p->grid()), 256, 0, s>>>(g.w.p, g.nnz, acc.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipMemcpyAsync(&wsum, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
+    }
+    PJ_HIP(hipStreamSynchronize(s));
+    p->mean_w = g.nnz > 0 ? (double)wsum / (double)g.nnz : 1.0;
+    const size_t nl1 = (size_t)std::max<i64>(p->nl, 1);
+    p->lsplit.alloc(nl1);
+    p->dist.alloc(nl1);
+    p->fr.alloc((size_t)p->bw);
+    p->frn.alloc((size_t)p->bw);
+    p->mb.alloc((size_t)p->bw);
+    p->lq_v.alloc(nl1);
+    p->lq_b.alloc(nl1);
+    p->lq_e.alloc(nl1);
+    p->stat.alloc(ST_N);
+    p->hstat.assign(ST_N, 0);
+    if (world > 1) {
+        p->cand.alloc((size_t)std::max<i64>(g.n, 1));
+        p->touched.alloc((size_t)std::max<i64>((g.n + 63) / 64, 1));
+        p->reg.alloc((size_t)world * (size_t)p->block);
+        PJ_HIP(hipMemsetAsync(p->touched.p, 0, p->touched.bytes(), s));
+    }
+    PJ_HIP(hipStreamSynchronize(s));
+    return p.release();
+}
+
+void wpart_info(const WPart& p, i64* out) {
+    out[0] = p.n;
+    out[1] = p.lo;
+    out[2] = p.hi;
+    out[3] = p.block;
+    out[4] = p.nnz_local;
+    out[5] = p.world;
+    out[6] = p.rank;
+    out[7] = p.nnz;
+}
+
+int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
+    hipStream_t s = p.ctx->stream;
+    if (delta <= 0) {
+        const double mean_deg = p.n ? (double)p.nnz / (double)p.n : 1.0;
+        delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(3.5 * p.mean_w / std::max(1.0, mean_deg))));
+    }
+    if (delta != p.delta && p.nl > 0) {
+        wp_lsplit_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, s>>>(p.row.p, p.w.p, p.nl, (u32)delta, p.lsplit.p);
+        PJ_LAUNCH_CHECK();
+    }
+    p.delta = delta;
+    if (p.nl > 0) PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.dist.p), INT_INF, (size_t)p.nl, s));
+    if (p.world > 1 && p.n > 0)
+        PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.cand.p), INT_INF, (size_t)p.n, s));
+    if (source >= 0 && source < p.n) {
+        wp_seed_k<<<1, 1, 0, s>>>(p.args(), source);
+        PJ_LAUNCH_CHECK();
+    }
+    PJ_HIP(hipStreamSynchronize(s));
+    return delta;
+}
+
+void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2) {
+    hipStream_t s = p.ctx->stream;
+    p.clear_stat();
+    PJ_HIP(hipMemsetAsync(p.stat.p + ST_MIN, 0xFF, sizeof(u64), s));
+    wp_select_k<<<grid_for(p.bw * 64, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi));
+    PJ_LAUNCH_CHECK();
+    p.read_stat();
+    out2[0] = (i64)p.hstat[ST_CNT];
+    out2[1] = p.hstat[ST_MIN] >= (u64)INT_INF ? (i64)INT_INF : (i64)p.hstat[ST_MIN];
+}
+
+void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts) {
+    hipStream_t s = p.ctx->stream;
+    p.clear_stat();
+    const WArgs a = p.args(lo, hi);
+    if (light) wp_relax_k<true><<<p.grid(), WB, 0, s>>>(a);
+    else wp_relax_k<false><<<p.grid(), WB, 0, s>>>(a);
+    PJ_LAUNCH_CHECK();
+    if (light) wp_long_k<true><<<p.grid(), WB, 0, s>>>(a);
+    else wp_long_k<false><<<p.grid(), WB, 0, s>>>(a);
+    PJ_LAUNCH_CHECK();
+    if (p.world > 1) {
+        const i64 nwords = (p.n + 63) / 64;
+        wp_pack_k<<<p.grid(), WB, 0, s>>>(a, nwords, p.reg.p);
+        PJ_LAUNCH_CHECK();
+    }
+    p.read_stat();
+    u64 off = 0;
+    for (int o = 0; o < p.world; ++o) {
+        const u64 c = p.world > 1 ? p.hstat[o] : 0;
+        counts[o] = (i64)c;
+        if (c) {
+            PJ_HIP(hipMemcpyAsync(send + off, p.reg.p + (size_t)o * (size_t)p.block, sizeof(u64) * c,
+                                  hipMemcpyDeviceToDevice, s));
+            off += c;
+        }
+    }
+    PJ_HIP(hipStreamSynchronize(s));
+}
+
+void wpart_apply(WPart& p, const u64* recv, i64 nr, int light, int32_t lo, int32_t hi) {
+    hipStream_t s = p.ctx->stream;
+    if (nr > 0) {
+        wp_apply_k<<<grid_for(nr, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), recv, nr, light);
+        PJ_LAUNCH_CHECK();
+    }
+    PJ_HIP(hipStreamSynchronize(s));
+}
+
+// The round's new frontier becomes current; returns its size on this rank (the
+// marks counted by the round's relax and apply: each vertex once, by the
+// atomicOr's old bit).
+i64 wpart_end_round(WPart& p) {
+    wp_swap_k<<<grid_for(p.bw, 256, p.grid()), 256, 0, p.ctx->stream>>>(p.args());
+    PJ_LAUNCH_CHECK();
+    p.read_stat();
+    return (i64)p.hstat[ST_NF];
+}
+
+void wpart_reach(WPart& p, i64* out2) {
+    p.clear_stat();
+    wp_reach_k<<<grid_for(std::max<i64>(p.nl, 1), WB, p.grid()), WB, 0, p.ctx->stream>>>(p.args());
+    PJ_LAUNCH_CHECK();
+    p.read_stat();
+    out2[0] = (i64)p.hstat[ST_REACH];
+    out2[1] = (i64)p.hstat[ST_REACH + 1];
+}
+
+void wpart_copy_dist(WPart& p, int32_t* host) {
+    if (p.nl > 0) PJ_HIP(hipMemcpy(host, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToHost));
+}
+
+}  // namespace pj

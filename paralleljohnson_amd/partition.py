@@ -69,6 +69,12 @@ class Exchange:
         self.dist.all_reduce(t, group=self.group)
         return t.tolist()
 
+    def allreduce_min(self, vals: List[int], like) -> List[int]:
+        import torch
+        t = torch.tensor(vals, dtype=torch.int64, device=self._dev(like))
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+        return t.tolist()
+
     def alltoall_counts(self, counts: List[int], like) -> List[int]:
         import torch
         s = torch.tensor(counts, dtype=torch.int64, device=self._dev(like))
@@ -299,8 +305,143 @@ def gather_dist(ops, exchange: Optional[Exchange]) -> np.ndarray:
     if exchange.stage:
         exchange.dist.all_gather_into_tensor(out, buf, group=exchange.group)
     else:
-        dev = ops.vis.device
+        dev = (ops.vis if hasattr(ops, "vis") else ops.send).device
         o = out.to(dev)
         exchange.dist.all_gather_into_tensor(o, buf.to(dev), group=exchange.group)
         out = o.cpu()
     return out.numpy()[: ops.n]
+
+
+# ---- weighted SSSP over the 1D partition (delta-stepping; wpart.hip) --------
+
+class DeviceWPart:
+    """This rank's block of a weighted graph on its GPU (libpj pj_wpart_*)."""
+
+    def __init__(self, ctx, graph, rank: int, world: int):
+        import torch
+        h = ctypes.c_void_p()
+        _check(_lib.pj_wpart_from_graph(graph._h, int(rank), int(world), ctypes.byref(h)))
+        self._ctx = ctx
+        self._h = h
+        info = (_I64 * 8)()
+        _check(_lib.pj_wpart_info(self._h, info))
+        self.n, self.lo, self.hi, self.block, self.nnz_local, self.world, self.rank, self.nnz = list(info)
+        self.nl = self.hi - self.lo
+        dev = torch.device("cuda", ctx.device)
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        cap = self.world * self.block if self.world > 1 else 1
+        self.send = torch.empty(cap, dtype=torch.int64, device=dev)
+        self.recv = torch.empty(cap, dtype=torch.int64, device=dev)
+        self._counts = (_I64 * max(self.world, 1))()
+        self._o2 = (_I64 * 2)()
+
+    @staticmethod
+    def _p(t):
+        return ctypes.c_void_p(t.data_ptr())
+
+    def begin(self, source: int, delta: int = 0) -> int:
+        d = ctypes.c_int32()
+        _check(_lib.pj_wpart_begin(self._h, int(source), int(delta), ctypes.byref(d)))
+        return d.value
+
+    def select(self, lo: int, hi: int):
+        _check(_lib.pj_wpart_select(self._h, int(lo), int(hi), self._o2))
+        return int(self._o2[0]), int(self._o2[1])
+
+    def relax(self, light: bool, lo: int, hi: int) -> List[int]:
+        _check(_lib.pj_wpart_relax(self._h, int(light), int(lo), int(hi), self._p(self.send), self._counts))
+        return list(self._counts)[: self.world]
+
+    def apply(self, n_recv: int, light: bool, lo: int, hi: int):
+        _check(_lib.pj_wpart_apply(self._h, self._p(self.recv), int(n_recv), int(light), int(lo), int(hi)))
+
+    def end_round(self) -> int:
+        nf = _I64()
+        _check(_lib.pj_wpart_end_round(self._h, ctypes.byref(nf)))
+        return nf.value
+
+    def reach(self):
+        _check(_lib.pj_wpart_reach(self._h, self._o2))
+        return int(self._o2[0]), int(self._o2[1])
+
+    def dist_local(self) -> np.ndarray:
+        out = np.empty(max(self.nl, 1), np.int32)
+        _check(_lib.pj_wpart_copy_dist(self._h, _ptr(out)))
+        return out[: self.nl]
+
+    def close(self):
+        if self._h:
+            _check(_lib.pj_wpart_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PartitionedDelta:
+    """The band loop of one rank (delta-stepping, Meyer & Sanders) over a 1D
+    vertex partition; every rank calls solve() with the same source. The
+    reference's round loop (:488-594) with its exchange (:522-554) and its
+    termination all-reduce (:579-593); R9 makes the result independent of the
+    partition and of the band structure."""
+
+    def __init__(self, ops, exchange: Optional[Exchange] = None, delta: int = 0):
+        self.ops = ops
+        self.ex = exchange
+        self.delta = delta
+        self.world = 1 if exchange is None else exchange.world
+        if self.world != ops.world:
+            raise PJError(-9, f"exchange has {self.world} ranks, the partition {ops.world}")
+        self.stats = {}
+
+    def _sum(self, vals):
+        return vals if self.ex is None else self.ex.allreduce_sum(vals, self.ops.send)
+
+    def _min(self, vals):
+        return vals if self.ex is None else self.ex.allreduce_min(vals, self.ops.send)
+
+    def _exchange_apply(self, light, lo, hi):
+        ops = self.ops
+        counts = ops.relax(light, lo, hi)
+        nr = 0
+        if self.ex is not None:
+            rc = self.ex.alltoall_counts(counts, ops.send)
+            self.ex.alltoall_ids(ops.send, counts, ops.recv, rc)
+            nr = sum(rc)
+            self.sent += sum(counts)
+        ops.apply(nr, light, lo, hi)
+
+    def solve(self, source: int) -> dict:
+        ops = self.ops
+        delta = ops.begin(source, self.delta)
+        lo, bands, rounds = 0, 0, 0
+        self.sent = 0
+        while lo < INT_INF:
+            hi = min(lo + delta, INT_INF)
+            cnt, mn = ops.select(lo, hi)
+            cnt = self._sum([cnt])[0]
+            if cnt == 0:
+                mn = self._min([mn])[0]
+                if mn >= INT_INF:
+                    break
+                lo = max(mn // delta * delta, hi)  # jump to the next occupied band
+                continue
+            bands += 1
+            while True:  # light rounds until no rank has a frontier
+                self._exchange_apply(True, lo, hi)
+                rounds += 1
+                if self._sum([ops.end_round()])[0] == 0:
+                    break
+            self._exchange_apply(False, lo, hi)  # heavy edges of the band's members
+            lo = hi
+        r, m = self._sum(list(ops.reach()))
+        self.stats = dict(delta=delta, bands=bands, rounds=rounds, reached=r, reached_edges=m, sent=self.sent)
+        return self.stats
+
+
+def load_weighted(ctx, graph, rank: int, world: int) -> DeviceWPart:
+    """The rank's block of a weighted pj Graph (the graph may be closed afterwards)."""
+    return DeviceWPart(ctx, graph, rank, world)

@@ -236,3 +236,84 @@ def test_run_module_matches_cli(pj, oracle, tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert two.read_bytes() == ref.read_bytes()
     assert "when using 2 processes." in r.stdout
+
+
+# ------------------------------------------- weighted (delta-stepping) ----
+
+def _wcases():
+    rng = np.random.default_rng(99)
+    out = []
+    for kind, n, wmax in (("uniform", 500, 300), ("hub", 900, 40), ("chain", 300, 5), ("uniform", 64, 2)):
+        s, d = random_graph(rng, kind, n)
+        w = rng.integers(0 if kind == "uniform" else 1, wmax, len(s)).astype(np.uint32)
+        out.append((kind, n, s.astype(np.int64), d.astype(np.int64), w))
+    return out
+
+
+def _wrank_main(rank, world, port, path, backend):
+    """One rank: weighted delta-stepping over the partition for every case; rank 0 saves."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    import paralleljohnson_amd as pj
+    from paralleljohnson_amd.partition import Exchange, PartitionedDelta, gather_dist, load_weighted
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    ex = Exchange()
+    ctx = pj.Context(0)
+    res = {}
+    graphs = [(f"c{i}", ctx.load_coo(s, d, w=w, n=n)) for i, (_, n, s, d, w) in enumerate(_wcases())]
+    graphs.append(("k12", ctx.generate_kronecker(12, 16, 3, weighted=True)))
+    for name, g in graphs:
+        ops = load_weighted(ctx, g, rank, world)
+        n = g.n
+        g.close()
+        for delta in (0, 7, 60):
+            sp = PartitionedDelta(ops, ex, delta=delta)
+            for source in (0, n // 3, n - 1, n + 2):
+                st = sp.solve(source)
+                res[f"{name}_{delta}_{source}"] = gather_dist(ops, ex)
+                res[f"{name}_{delta}_{source}_reached"] = np.array([st["reached"], st["reached_edges"]])
+        ops.close()
+    if rank == 0:
+        np.savez(path, **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,backend", [(1, "nccl"), (2, "gloo"), (3, "gloo")])
+def test_wpart_delta_stepping(pj, oracle, world, backend):
+    """Weighted SSSP over the 1D partition (wpart.hip + PartitionedDelta): every
+    rank on the one GPU; distances bit-exact against the oracle Dijkstra, for
+    several band widths and sources (including one outside [0, n))."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "res.npz")
+        mp.spawn(_wrank_main, args=(world, _free_port(), path, backend), nprocs=world, join=True)
+        with np.load(path) as z:
+            res = {k: z[k] for k in z.files}
+    exp_graphs = []
+    for i, (_, n, s, d, w) in enumerate(_wcases()):
+        row, col, wc = oracle.coo2csr(s.astype(np.uint32), d.astype(np.uint32), n, w)
+        exp_graphs.append((f"c{i}", n, row, col, wc))
+    ctx = pj.Context(0)
+    g = ctx.generate_kronecker(12, 16, 3, weighted=True)
+    row, col, wc = g.get_csr()
+    exp_graphs.append(("k12", g.n, row, col.astype(np.uint32), wc))
+    g.close()
+    ctx.close()
+    for name, n, row, col, wc in exp_graphs:
+        for source in (0, n // 3, n - 1, n + 2):
+            exp = oracle.dijkstra(row, col, wc, source) if source < n else np.full(n, INF, np.int32)
+            reached = exp < INF
+            for delta in (0, 7, 60):
+                got = res[f"{name}_{delta}_{source}"]
+                assert np.array_equal(got, exp), (name, delta, source, world)
+                assert res[f"{name}_{delta}_{source}_reached"].tolist() == [
+                    int(reached.sum()), int(np.diff(row)[reached].sum())], (name, delta, source)
