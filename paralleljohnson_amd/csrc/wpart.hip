@@ -29,11 +29,12 @@
 // target is re-sent only when this rank improves on it: the send volume of a
 // round is bounded by the distinct remote targets improved (<= block per
 // owner), unlike the reference's unbounded buffers.
-// Rows longer than WP_LONG edges go to a queue relaxed by the whole grid.
+// Row segments longer than WP_LONG edges go to a queue relaxed edge-balanced
+// over the whole grid (1024-edge tiles, lb.h).
 #include <algorithm>
 #include <cmath>
 
-#include "devutil.h"
+#include "lb.h"
 
 namespace pj {
 
@@ -50,6 +51,8 @@ constexpr int WSC = 16;        // frontier words a wave screens at once
 constexpr int WP_SERIAL = 8;   // edges a lane relaxes alone
 constexpr u64 WP_LONG = 1024;  // longer row segments: the grid-wide queue
 constexpr int WP_MAXW = 64;    // largest world size
+constexpr int WP_EB = 40;      // long queue counter: (slots << WP_EB) | edges
+constexpr int WP_TILE = WB * 4;
 
 // stat slots (u64): [0, 64) per-owner region counts, then:
 constexpr int ST_LONGQ = 64;   // long-row queue length
@@ -73,7 +76,7 @@ struct WArgs {
     u64* fr;           // bw
     u64* frn;          // bw
     u64* mb;           // bw
-    u32* lq_v;         // long-row queue: local vertex, begin, end
+    u32* lq_v;         // long-row queue: local vertex, row position, edge offset of the slot
     u64* lq_b;
     u64* lq_e;
     u64* stat;
@@ -174,11 +177,24 @@ __global__ __launch_bounds__(WB) void wp_relax_k(WArgs a) {
                 const u64 r0v = a.row[v], sp = r0v + a.lsplit[v];
                 b = LIGHT ? r0v : sp;
                 e = LIGHT ? sp : a.row[v + 1];
-                if (e - b > WP_LONG) {  // long segment: the grid-wide queue
-                    const u64 q = atomicAdd(&a.stat[ST_LONGQ], 1ull);
+            }
+            // long segments: the edge-balanced queue (one packed atomic per wave
+            // gives slots and edge offsets, monotonic in the slot)
+            const bool lng = act && e - b > WP_LONG;
+            const u64 hm = __ballot(lng);
+            if (hm) {
+                const u64 seg = lng ? e - b : 0;
+                const u64 ie = wave_incl_scan(seg);
+                const u64 tot = __shfl(ie, 63, 64);
+                const int leader = __ffsll((long long)hm) - 1;
+                u64 base = 0;
+                if (lane == leader) base = atomicAdd(&a.stat[ST_LONGQ], ((u64)__popcll(hm) << WP_EB) | tot);
+                base = __shfl(base, leader, 64);
+                if (lng) {
+                    const u64 q = (base >> WP_EB) + (u64)__popcll(hm & lanemask_lt());
                     a.lq_v[q] = v;
                     a.lq_b[q] = b;
-                    a.lq_e[q] = e;
+                    a.lq_e[q] = (base & ((1ull << WP_EB) - 1ull)) + ie - seg;  // edge offset of the slot
                     e = b;
                 }
             }
@@ -209,15 +225,35 @@ __global__ __launch_bounds__(WB) void wp_relax_k(WArgs a) {
     }
 }
 
-// the long segments queued by wp_relax_k, each spread over the whole grid
+// the long segments queued by wp_relax_k, edge-balanced: 1024-edge tiles over
+// the slots' monotonic edge offsets (lb.h), the source distances staged in LDS
 template <bool LIGHT>
 __global__ __launch_bounds__(WB) void wp_long_k(WArgs a) {
-    const u64 nq = a.stat[ST_LONGQ];
-    const u64 tid = (u64)blockIdx.x * WB + threadIdx.x, nth = (u64)gridDim.x * WB;
-    for (u64 q = 0; q < nq; ++q) {
-        const u64 b = a.lq_b[q], e = a.lq_e[q];
-        const int32_t du = a.dist[a.lq_v[q]];
-        for (u64 k = b + tid; k < e; k += nth) wp_edge(a, LIGHT, a.col[k], (long long)du + a.w[k]);
+    __shared__ LbShared<WP_TILE> sh;
+    __shared__ int32_t s_du[WP_TILE];
+    __shared__ u64 s_b[WP_TILE];
+    const u64 packed = a.stat[ST_LONGQ];
+    const u64 nq = packed >> WP_EB, total = packed & ((1ull << WP_EB) - 1ull);
+    if (nq == 0) return;
+    for (u64 e0 = (u64)blockIdx.x * WP_TILE; e0 < total; e0 += (u64)gridDim.x * WP_TILE) {
+        u64 s0;
+        u32 ns;
+        lb_tile_load<WP_TILE>(a.lq_e, nq, e0, sh, s0, ns);
+        for (u32 i = threadIdx.x; i < ns; i += WB) {
+            s_du[i] = a.dist[a.lq_v[s0 + i]];
+            s_b[i] = a.lq_b[s0 + i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < WP_TILE / WB; ++j) {
+            const u64 e = e0 + (u64)j * WB + threadIdx.x;
+            if (e < total) {
+                const u32 sl = lb_find<WP_TILE>(sh, ns, e);
+                const u64 k = s_b[sl] + (e - sh.off[sl]);
+                wp_edge(a, LIGHT, a.col[k], (long long)s_du[sl] + a.w[k]);
+            }
+        }
+        __syncthreads();
     }
 }
 
