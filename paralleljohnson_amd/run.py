@@ -10,7 +10,9 @@ split in contiguous blocks (nn2rank :169-200), the exchange over RCCL
 stdout `Time:` line and the sol_file bytes follow the reference (see the
 single-GPU CLI, paralleljohnson_amd/csrc/cli.cpp); with one process and no
 launcher it runs alone on one GPU. Unit weights only (the reference's w = 1,
-:147). Environment: PJ_DEVICE overrides the GPU ordinal (default LOCAL_RANK),
+:147) unless PJ_WEIGHTED=1: then the third column is an integer weight (as in
+the single-GPU CLI) and the solve is delta-stepping over the partition
+(PartitionedDelta, wpart.hip). Environment: PJ_DEVICE overrides the GPU ordinal (default LOCAL_RANK),
 PJ_BACKEND overrides the torch.distributed backend (default nccl = RCCL; gloo
 stages the exchange through host memory, for rehearsals with several ranks
 on one GPU).
@@ -40,7 +42,8 @@ def main(argv=None) -> int:
         return 255
     import torch
     import paralleljohnson_amd as pj
-    from paralleljohnson_amd.partition import Exchange, PartitionedBFS, gather_dist, load_snap
+    from paralleljohnson_amd.partition import (Exchange, PartitionedBFS, PartitionedDelta, gather_dist,
+                                               load_snap, load_weighted)
 
     local = int(os.environ.get("PJ_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(local)
@@ -60,14 +63,20 @@ def main(argv=None) -> int:
 
     msg("process 0 reads in the web graph data......")
     ctx = pj.Context(local)
-    ops = load_snap(ctx, argv[1], rank, world)
+    weighted = os.environ.get("PJ_WEIGHTED", "0") not in ("", "0")
+    if weighted:  # every rank parses the file on its GPU and cuts its weighted block
+        g = ctx.load_snap(argv[1], weighted=True)
+        ops = load_weighted(ctx, g, rank, world)
+        g.close()
+    else:
+        ops = load_snap(ctx, argv[1], rank, world)
     msg(f"N = {ops.n}")  # :320
     msg("read in the webgraph is done.")
     msg("distribute sparse matrix is done.")
     source = _atoi(argv[2])
     msg(f"compute shortest paths from source node: {source}")
     msg("parallel Johnson's algorithm starts......")
-    bfs = PartitionedBFS(ops, ex)
+    bfs = PartitionedDelta(ops, ex) if weighted else PartitionedBFS(ops, ex)
     torch.cuda.synchronize()
     if ex is not None:
         ex.dist.barrier()

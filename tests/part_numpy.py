@@ -142,3 +142,112 @@ class NumpyPart:
 
     def dist_local(self):
         return self.dist.copy()
+
+
+class NumpyWPart:
+    """Numpy restatement of the pj_wpart_* steps (wpart.hip; semantics as in
+    include/pj.h), driven by partition.PartitionedDelta under gloo on CPU.
+    Same block geometry; send/recv are int64 (id | cand << 32), owner-major."""
+
+    def __init__(self, src, dst, w, n, rank, world):
+        src = np.asarray(src, np.int64)
+        dst = np.asarray(dst, np.int64)
+        w = np.asarray(w, np.int64)
+        self.n, self.rank, self.world = n, rank, world
+        self.block, ranges = block_geometry(n, world)
+        self.lo, self.hi = ranges[rank]
+        self.nl = self.hi - self.lo
+        self.nnz = len(src)
+        self.mean_w = float(w.sum()) / len(w) if len(w) else 1.0
+        m = (src >= self.lo) & (src < self.hi)
+        k = src[m] - self.lo
+        order = np.argsort(k, kind="stable")
+        row = np.zeros(self.nl + 1, np.int64)
+        np.add.at(row, k + 1, 1)
+        self.row, self.col, self.w = np.cumsum(row), dst[m][order], w[m][order]
+        self.nnz_local = len(self.col)
+        cap = world * self.block if world > 1 else 1
+        self.send = torch.zeros(cap, dtype=torch.int64)
+        self.recv = torch.zeros(cap, dtype=torch.int64)
+        self.dist = np.full(self.nl, INF, np.int64)
+        self.cand = np.full(n, INF, np.int64)
+        self.fr = np.zeros(self.nl, bool)
+        self.frn = np.zeros(self.nl, bool)
+        self.mb = np.zeros(self.nl, bool)
+        self.delta = 1
+
+    def begin(self, source, delta=0):
+        if delta <= 0:
+            mean_deg = self.nnz / self.n if self.n else 1.0
+            delta = int(max(1.0, min(65536.0, np.floor(3.5 * self.mean_w / max(1.0, mean_deg) + 0.5))))
+        self.delta = delta
+        self.dist[:] = INF
+        self.cand[:] = INF
+        if 0 <= source < self.n and self.lo <= source < self.hi:
+            self.dist[source - self.lo] = 0
+        return delta
+
+    def select(self, lo, hi):
+        self.fr = (self.dist >= lo) & (self.dist < hi)
+        self.frn[:] = False
+        self.mb[:] = False
+        above = self.dist[self.dist >= lo]
+        return int(self.fr.sum()), int(above.min()) if len(above) else INF
+
+    def _lower(self, v, c, hi, light):
+        """Owned target v (global) gets candidate c (atomicMin; light: joins frn below hi)."""
+        i = v - self.lo
+        if c < self.dist[i]:
+            self.dist[i] = c
+            if light and c < hi:
+                self.frn[i] = True
+
+    def relax(self, light, lo, hi):
+        if light:
+            self.mb |= self.fr
+            us = np.nonzero(self.fr)[0]
+        else:
+            us = np.nonzero(self.mb)[0]
+        touched = {}
+        for u in us:
+            a, b = self.row[u], self.row[u + 1]
+            for v, wt in zip(self.col[a:b], self.w[a:b]):
+                if (wt < self.delta) != bool(light):
+                    continue
+                c = self.dist[u] + wt
+                if c >= INF:
+                    continue
+                if self.lo <= v < self.hi:
+                    self._lower(v, c, hi, light)
+                elif c < self.cand[v]:  # re-sent only when this rank improves on it
+                    self.cand[v] = c
+                    touched[int(v)] = True
+        ids = np.array(sorted(touched), np.int64)
+        owner = ids // self.block
+        counts = [int(np.sum(owner == o)) for o in range(self.world)]
+        if len(ids):
+            packed = ids | (self.cand[ids] << 32)  # ids are sorted, hence owner-major
+            self.send[: len(ids)] = torch.from_numpy(packed)
+        return counts
+
+    def apply(self, nr, light, lo, hi):
+        rec = self.recv[:nr].numpy()
+        ids, cs = rec & 0xFFFFFFFF, rec >> 32
+        assert np.all((ids >= self.lo) & (ids < self.hi)), "received ids owned by another rank"
+        for v, c in zip(ids, cs):
+            self._lower(int(v), int(c), hi, light)
+
+    def end_round(self):
+        self.fr = self.frn.copy()
+        self.frn[:] = False
+        return int(self.fr.sum())
+
+    def reach(self):
+        r = self.dist < INF
+        return int(r.sum()), int(np.diff(self.row)[r].sum())
+
+    def dist_local(self):
+        return self.dist.astype(np.int32)
+
+    def close(self):
+        pass

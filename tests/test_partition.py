@@ -238,6 +238,41 @@ def test_run_module_matches_cli(pj, oracle, tmp_path):
     assert "when using 2 processes." in r.stdout
 
 
+@pytest.mark.gpu
+def test_run_module_weighted(pj, oracle, tmp_path):
+    """PJ_WEIGHTED=1: the single-GPU CLI (delta-stepping) and `python -m
+    paralleljohnson_amd.run` at 1 and 2 ranks (PartitionedDelta, gloo) write the
+    oracle Dijkstra's sol_file bytes."""
+    import subprocess
+    from helpers import to_text
+    rng = np.random.default_rng(78)
+    s, d = random_graph(rng, "hub", 2500)
+    w = rng.integers(1, 200, len(s)).astype(np.uint32)
+    text = to_text(s, d, w=w, style=1)
+    path = tmp_path / "gw.txt"
+    path.write_bytes(text)
+    src = int(s[0])
+    ps, pd, pw, n = oracle.parse_snap(text, weighted=True)
+    row, col, wc = oracle.coo2csr(ps, pd, n, pw)
+    exp = oracle.format_sol(oracle.dijkstra(row, col, wc, src))
+    env = dict(os.environ, PJ_DEVICE="0", PJ_WEIGHTED="1")
+    ref = tmp_path / "cli.sol"
+    subprocess.run([pj.cli_path(), str(path), str(src), str(ref)], check=True, capture_output=True, env=env)
+    assert ref.read_bytes() == exp
+    one = tmp_path / "one.sol"
+    subprocess.run([sys.executable, "-m", "paralleljohnson_amd.run", str(path), str(src), str(one)],
+                   check=True, capture_output=True, text=True, env=env, cwd=ROOT)
+    assert one.read_bytes() == exp
+    two = tmp_path / "two.sol"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        "-m", "paralleljohnson_amd.run", str(path), str(src), str(two)],
+                       capture_output=True, text=True, env=dict(env, PJ_BACKEND="gloo"), cwd=ROOT, timeout=200)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert two.read_bytes() == exp
+    assert "when using 2 processes." in r.stdout
+
+
 # ------------------------------------------- weighted (delta-stepping) ----
 
 def _wcases():
@@ -284,6 +319,81 @@ def _wrank_main(rank, world, port, path, backend):
         np.savez(path, **res)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _wexpected(oracle):
+    out = []
+    for i, (_, n, s, d, w) in enumerate(_wcases()):
+        row, col, wc = oracle.coo2csr(s.astype(np.uint32), d.astype(np.uint32), n, w)
+        out.append((f"c{i}", n, row, col, wc))
+    return out
+
+
+def _wcheck(res, exp_graphs, oracle, deltas, world):
+    for name, n, row, col, wc in exp_graphs:
+        for source in (0, n // 3, n - 1, n + 2):
+            exp = oracle.dijkstra(row, col, wc, source) if source < n else np.full(n, INF, np.int32)
+            reached = exp < INF
+            for delta in deltas:
+                got = res[f"{name}_{delta}_{source}"]
+                assert np.array_equal(got, exp), (name, delta, source, world)
+                assert res[f"{name}_{delta}_{source}_reached"].tolist() == [
+                    int(reached.sum()), int(np.diff(row)[reached].sum())], (name, delta, source)
+
+
+def _wrank_numpy(rank, world, port, path):
+    """One rank of the weighted protocol on CPU (gloo), device steps restated in numpy."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    from part_numpy import NumpyWPart
+    from paralleljohnson_amd.partition import Exchange, PartitionedDelta, gather_dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ex = Exchange()
+    res = {}
+    for i, (_, n, s, d, w) in enumerate(_wcases()):
+        ops = NumpyWPart(s, d, w, n, rank, world)
+        for delta in (0, 7, 60):
+            sp = PartitionedDelta(ops, ex, delta=delta)
+            for source in (0, n // 3, n - 1, n + 2):
+                st = sp.solve(source)
+                res[f"c{i}_{delta}_{source}"] = gather_dist(ops, ex)
+                res[f"c{i}_{delta}_{source}_reached"] = np.array([st["reached"], st["reached_edges"]])
+    if rank == 0:
+        np.savez(path, **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_wprotocol_world1_numpy(oracle):
+    """The band loop (PartitionedDelta) without an exchange, numpy device steps."""
+    from part_numpy import NumpyWPart
+    from paralleljohnson_amd.partition import PartitionedDelta, gather_dist
+    res = {}
+    for i, (_, n, s, d, w) in enumerate(_wcases()):
+        ops = NumpyWPart(s, d, w, n, 0, 1)
+        for delta in (0, 1, 7, 60):
+            sp = PartitionedDelta(ops, None, delta=delta)
+            for source in (0, n // 3, n - 1, n + 2):
+                st = sp.solve(source)
+                res[f"c{i}_{delta}_{source}"] = gather_dist(ops, None)
+                res[f"c{i}_{delta}_{source}_reached"] = np.array([st["reached"], st["reached_edges"]])
+    _wcheck(res, _wexpected(oracle), oracle, (0, 1, 7, 60), 1)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_wprotocol_gloo_numpy(oracle, world):
+    """Weighted band loop at world 2-3 over gloo: all_to_all of packed (id, cand)
+    pairs, all_reduce sum/min termination; bit-exact vs the oracle Dijkstra."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "res.npz")
+        mp.spawn(_wrank_numpy, args=(world, _free_port(), path), nprocs=world, join=True)
+        with np.load(path) as z:
+            res = {k: z[k] for k in z.files}
+    _wcheck(res, _wexpected(oracle), oracle, (0, 7, 60), world)
 
 
 @pytest.mark.gpu
