@@ -402,12 +402,19 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
             }
         };
         if (d.prev_mode == 0) {
-            // ---- normal queue: a block takes 256 entries
+            // ---- normal queue: a block takes G entries. A block walks its group's edges
+            // in dependent 256-edge steps, so a small frontier in 256-entry groups would run
+            // on a handful of blocks; G shrinks while the groups still fit in one pass of the grid.
+            u64 nn = 0;
+#pragma unroll
+            for (int k = 0; k < NQS; ++k) nn += d.nseg[k];
+            u32 G = TB;
+            while (G > 1 && (nn + G / 2 - 1) / (G / 2) <= (u64)gridDim.x) G >>= 1;
             u64 gcount = 0, gpre[NQS];
 #pragma unroll
             for (int k = 0; k < NQS; ++k) {
                 gpre[k] = gcount;
-                gcount += (d.nseg[k] + TB - 1) / TB;
+                gcount += (d.nseg[k] + G - 1) / G;
             }
             for (u64 grp = blockIdx.x; grp < gcount; grp += gridDim.x) {
                 int seg = 0;
@@ -419,10 +426,10 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                         sbase = gpre[k];
                         scount = d.nseg[k];
                     }
-                const u64 i = (grp - sbase) * TB + t;
+                const u64 i = (grp - sbase) * G + t;
                 u32 deg = 0;
                 u64 beg = 0;
-                if (i < scount) {
+                if (t < G && i < scount) {
                     const u32 u = a.qv[cp][(u64)seg * (u64)a.n + i];
                     const Off b = g.row[u], e = g.row[u + 1];
                     deg = (u32)(e - b);
@@ -433,9 +440,11 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
         } else {
             // ---- frontier found by the previous (pull) level, as a bitmap: a block takes
             // 256 words, ranks their bits, and expands 256 frontier vertices at a time.
-            for (i64 wc = blockIdx.x; wc * TB < a.nwords; wc += gridDim.x) {
-                const i64 w = wc * TB + t;
-                const u64 fw = w < a.nwords ? a.fnew[w] : 0ull;
+            u32 WB = TB;  // words per block step, halved while the steps do not cover the grid
+            while (WB > 16 && (a.nwords + WB - 1) / WB < (i64)gridDim.x) WB >>= 1;
+            for (i64 wc = blockIdx.x; wc * WB < a.nwords; wc += gridDim.x) {
+                const i64 w = wc * WB + t;
+                const u64 fw = (t < WB && w < a.nwords) ? a.fnew[w] : 0ull;
                 u32 F;
                 const u32 wex = block_excl_scan<NW>((u32)__popcll(fw), reinterpret_cast<u32*>(red), F);
                 s_wex[t] = wex;
@@ -450,7 +459,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
 #pragma unroll
                         for (u32 step = TB / 2; step > 0; step >>= 1)
                             if (s_wex[lo + step] <= f) lo += step;
-                        const u32 u = (u32)((wc * TB + lo) * 64 + select_bit(s_fw[lo], f - s_wex[lo]));
+                        const u32 u = (u32)((wc * WB + lo) * 64 + select_bit(s_fw[lo], f - s_wex[lo]));
                         const Off b = g.row[u], e = g.row[u + 1];
                         deg = (u32)(e - b);
                         beg = (u64)b;
@@ -466,11 +475,15 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
         // at a time. Output is bitmaps only (vis_next, fnew): no queue, no block barrier.
         const u64* vis = a.vis[d.vsel];
         u64* vout = a.vis[1 - d.vsel];
-        u32* newb = s_new[wave_id()];  // found bits of the SC words, as 32-bit halves
-        const i64 nsc = (a.nwords + SC - 1) / SC;
+        u32* newb = s_new[wave_id()];  // found bits of the scw words, as 32-bit halves
+        // words per wave task: SC, halved while the tasks do not cover the grid's waves
+        // (a small graph would otherwise leave most of the chip idle)
+        u32 scw = SC;
+        while (scw > 1 && (a.nwords + scw - 1) / scw < (i64)gridDim.x * NW) scw >>= 1;
+        const i64 nsc = (a.nwords + scw - 1) / scw;
         for (i64 sc = (i64)blockIdx.x * NW + wave_id(); sc < nsc; sc += (i64)gridDim.x * NW) {
-            const i64 wbase = sc * SC;
-            const bool mine = lane < SC && wbase + lane < a.nwords;
+            const i64 wbase = sc * scw;
+            const bool mine = lane < (int)scw && wbase + lane < a.nwords;
             u64 myvis = ~0ull, mytodo = 0;
             if (mine) {
                 const i64 wd = wbase + lane;
@@ -493,8 +506,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                     act[j] = c < T;
                     // word of candidate c: largest lane jw < SC with ex[jw] <= c
                     u32 jw = 0;
-#pragma unroll
-                    for (u32 step = SC / 2; step > 0; step >>= 1) {
+                    for (u32 step = scw / 2; step > 0; step >>= 1) {
                         const u32 x = __shfl(myex, jw + step, 64);
                         if (x <= c) jw += step;
                     }
