@@ -235,6 +235,9 @@ def main():
             }
             gg.close()
 
+    if world == 1 and not args.no_secondary and not args.scale and not args.no_cpu_baseline:
+        secondary["wg_cli"] = run_wg_cli(ctx, args)
+
     def max_sum(el, m):
         if dist is None:
             return el, m
@@ -314,6 +317,60 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def run_wg_cli(ctx, args):
+    """configs[0] end to end: the web-Google-shaped synthetic written as a SNAP text file, the
+    parallel_johnson CLI timed from process start to sol_file closed (time-to-solution: HIP
+    init, GPU parse + CSR, solve, output), next to the reference's BSP algorithm at np = 4
+    (oracle port of :466-594, the `mpirun -np 4` analogue) on the same graph, sol_file bytes
+    compared."""
+    import hashlib
+    import subprocess
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # cpu_baseline leg only (reference timing and the byte comparison)
+    import paralleljohnson_amd as pj
+
+    O.build()
+    g = ctx.generate_webgraph(seed=args.seed)
+    row, col, _ = g.get_csr()
+    g.close()
+    col = col.view(np.uint32)
+    src = np.repeat(np.arange(len(row) - 1, dtype=np.int64), np.diff(row))
+    with tempfile.TemporaryDirectory() as td:
+        path, out = os.path.join(td, "web-Google-synthetic.txt"), os.path.join(td, "sol.txt")
+        body = np.char.add(np.char.add(src.astype(str), "\t"), col.astype(np.int64).astype(str))
+        with open(path, "wb") as f:
+            f.write(("# Directed graph (synthetic, web-Google-shaped)\n# FromNodeId\tToNodeId\n" +
+                     "\n".join(body.tolist()) + "\n").encode())
+        del body, src
+        walls = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = subprocess.run([pj.cli_path(), path, "0", out], capture_output=True, text=True, timeout=300)
+            walls.append(time.perf_counter() - t0)
+            if r.returncode != 0:
+                raise RuntimeError(f"parallel_johnson failed: {r.stderr[-500:]}")
+        t_line = r.stdout.strip()
+        got = open(out, "rb").read()
+        text_mb = os.path.getsize(path) / 1e6
+    t0 = time.perf_counter()
+    ref, st = O.reference_sssp(row, col, 0, 4)
+    ref_s = time.perf_counter() - t0
+    exp = O.format_sol(ref)
+    m_r = int(np.diff(row)[ref < 100000].sum())
+    return {
+        "workload": "web-google-shaped-synthetic, SNAP text file, source 0, parallel_johnson CLI end to end",
+        "text_mb": round(text_mb, 1), "n_vertices": len(row) - 1, "nnz": int(len(col)),
+        "time_to_solution_s": round(min(walls), 3), "time_line": t_line,
+        "sol_bytes_identical_to_reference_np4": got == exp,
+        "sol_sha256": hashlib.sha256(got).hexdigest()[:16],
+        "reference_np4_solve_s": round(st.solve_s, 3), "reference_np4_wall_s": round(ref_s, 3),
+        "reference_np4_gteps": round(m_r / st.solve_s / 1e9, 5), "reference_cores": 4,
+        "reference_kind": "port (oracle restatement of the reference's BSP heap algorithm, 4 host threads)",
+    }
 
 
 def cpu_baseline(g, res, args):
