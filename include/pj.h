@@ -93,6 +93,20 @@ int pj_load_snap_buffer(pj_ctx* ctx, const char* text, int64_t len, int weighted
 int pj_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, const uint32_t* w,
                 int64_t nnz, int64_t n_vertices, pj_graph** out);
 
+/* Binary CSR cache (no reference counterpart: the
+ * reference re-parses the text on every run, read_webgraph :66-105 +
+ * coord2csr :117-159). The file holds the graph's device arrays as they sit in
+ * HBM -- a 64-byte header, row offsets (4 or 8 bytes), col, weights when
+ * weighted, and the in-edge CSC when the graph is not symmetric -- so loading
+ * it is file -> pinned staging -> HBM with no sort. src_size / src_mtime_ns
+ * stamp the text the graph came from (-1: none); pj_load_csr_file with an
+ * expected stamp other than -1 fails with PJ_ERR_STATE when the file's stamp
+ * differs (a stale cache). A missing or unreadable file is PJ_ERR_IO; a bad
+ * magic, version or size is PJ_ERR_PARSE. */
+int pj_graph_save(const pj_graph* g, const char* path, int64_t src_size, int64_t src_mtime_ns);
+int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int64_t expect_src_mtime_ns,
+                     pj_graph** out);
+
 /* Graph500-style Kronecker generator on the GPU (A,B,C = 0.57,0.19,0.19),
  * 2^scale vertices, edgefactor << scale tuples, labels permuted, every tuple
  * written in both directions (tuple i -> entries 2i, 2i+1). Deterministic in

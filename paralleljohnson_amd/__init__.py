@@ -79,6 +79,8 @@ _SIGS = {
     "pj_load_coo": ([_P, _P, _P, _P, _I64, _I64, _PP], _INT),
     "pj_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _PP], _INT),
     "pj_generate_webgraph": ([_P, _I64, _I64, ctypes.c_uint64, _PP], _INT),
+    "pj_graph_save": ([_P, ctypes.c_char_p, _I64, _I64], _INT),
+    "pj_load_csr_file": ([_P, ctypes.c_char_p, _I64, _I64, _PP], _INT),
     "pj_graph_destroy": ([_P], _INT),
     "pj_graph_info": ([_P, _P, _P, _P, _P], _INT),
     "pj_graph_get_csr": ([_P, _P, _P, _P], _INT),
@@ -207,6 +209,10 @@ class Graph:
         _check(_lib.pj_set_option(self._h, key.encode(), float(value)))
 
     # -- inspection --------------------------------------------------------
+    def save(self, path: str, src_size: int = -1, src_mtime_ns: int = -1):
+        """Binary CSR cache of this graph (pj_graph_save)."""
+        _check(_lib.pj_graph_save(self._h, os.fsencode(path), int(src_size), int(src_mtime_ns)))
+
     def get_csr(self):
         row = np.empty(self.n + 1, np.int64)
         col = np.empty(max(self.nnz, 1), np.int32)
@@ -272,6 +278,13 @@ class Context:
         wa = None if w is None else np.ascontiguousarray(np.asarray(w, dtype=np.uint32))
         g = ctypes.c_void_p()
         _check(_lib.pj_load_coo(self._h, _ptr(s), _ptr(d), _ptr(wa), len(s), int(n), ctypes.byref(g)))
+        return Graph(self, g)
+
+    def load_csr_file(self, path: str, expect_src_size: int = -1, expect_src_mtime_ns: int = -1) -> "Graph":
+        """A graph saved by Graph.save (pj_load_csr_file): no parse, no sort."""
+        g = ctypes.c_void_p()
+        _check(_lib.pj_load_csr_file(self._h, os.fsencode(path), int(expect_src_size), int(expect_src_mtime_ns),
+                                     ctypes.byref(g)))
         return Graph(self, g)
 
     def generate_webgraph(self, n_ids: int = 916428, n_edges: int = 5105039, seed: int = 1) -> Graph:

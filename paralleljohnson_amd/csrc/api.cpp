@@ -419,6 +419,165 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     return PJ_OK;
 }
 
+// ------------------------------------------------------- binary CSR cache --
+// Header + the device arrays in HBM order (pj.h). Streamed through one pinned
+// staging buffer in 64 MiB pieces.
+
+namespace {
+
+struct CsrFileHeader {
+    char magic[8];  // "PJCSR\0\0\1"
+    uint32_t version;
+    uint32_t flags;  // 1 weighted, 2 symmetric, 4 64-bit row offsets
+    int64_t n, nnz;
+    int64_t src_size, src_mtime_ns;
+    uint64_t payload;  // bytes after the header
+    uint64_t reserved;
+};
+static_assert(sizeof(CsrFileHeader) == 64, "header is 64 bytes");
+constexpr char kCsrMagic[8] = {'P', 'J', 'C', 'S', 'R', 0, 0, 1};
+constexpr size_t kStage = (size_t)64 << 20;
+
+struct FileCloser {
+    void operator()(FILE* f) const { if (f) std::fclose(f); }
+};
+
+void put_dev(FILE* f, const void* d, size_t bytes, PinnedBuf<char>& st, hipStream_t s) {
+    for (size_t off = 0; off < bytes; off += kStage) {
+        const size_t k = std::min(kStage, bytes - off);
+        PJ_HIP(hipMemcpyAsync(st.p, static_cast<const char*>(d) + off, k, hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+        if (std::fwrite(st.p, 1, k, f) != k) throw Error(PJ_ERR_IO, "pj_graph_save: write failed");
+    }
+}
+
+void get_dev(FILE* f, void* d, size_t bytes, PinnedBuf<char>& st, hipStream_t s) {
+    for (size_t off = 0; off < bytes; off += kStage) {
+        const size_t k = std::min(kStage, bytes - off);
+        if (std::fread(st.p, 1, k, f) != k) throw Error(PJ_ERR_PARSE, "pj_load_csr_file: file is truncated");
+        PJ_HIP(hipMemcpyAsync(static_cast<char*>(d) + off, st.p, k, hipMemcpyHostToDevice, s));
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+}
+
+uint64_t csr_payload(int64_t n, int64_t nnz, uint32_t flags) {
+    const uint64_t ob = (flags & 4) ? 8 : 4;
+    uint64_t b = ob * (uint64_t)(n + 1) + 4ull * (uint64_t)nnz;
+    if (flags & 1) b += 4ull * (uint64_t)nnz;
+    if (!(flags & 2)) b += ob * (uint64_t)(n + 1) + 4ull * (uint64_t)nnz;
+    return b;
+}
+
+}  // namespace
+
+int pj_graph_save(const pj_graph* pg, const char* path, int64_t src_size, int64_t src_mtime_ns) {
+    if (!pg || !path) return arg_error("pj_graph_save: bad argument");
+    return guarded([&] {
+        const Graph& g = pg->g;
+        bind(*g.ctx);
+        hipStream_t s = g.ctx->stream;
+        CsrFileHeader h{};
+        std::memcpy(h.magic, kCsrMagic, 8);
+        h.version = 1;
+        h.flags = (g.weighted ? 1u : 0u) | (g.symmetric ? 2u : 0u) | (g.off64 ? 4u : 0u);
+        h.n = g.n;
+        h.nnz = g.nnz;
+        h.src_size = src_size;
+        h.src_mtime_ns = src_mtime_ns;
+        h.payload = csr_payload(g.n, g.nnz, h.flags);
+        // write to a temporary name and rename, so a reader never sees a partial cache
+        const std::string tmp = std::string(path) + ".tmp";
+        std::unique_ptr<FILE, FileCloser> f(std::fopen(tmp.c_str(), "wb"));
+        if (!f) {
+            set_error(std::string("pj_graph_save: cannot open ") + tmp);
+            return (int)PJ_ERR_IO;
+        }
+        if (std::fwrite(&h, sizeof h, 1, f.get()) != 1) throw Error(PJ_ERR_IO, "pj_graph_save: write failed");
+        PinnedBuf<char> st;
+        st.alloc(kStage);
+        const size_t ob = g.off64 ? 8 : 4;
+        put_dev(f.get(), g.row_ptr(), ob * (size_t)(g.n + 1), st, s);
+        put_dev(f.get(), g.col.p, 4 * (size_t)g.nnz, st, s);
+        if (g.weighted) put_dev(f.get(), g.w.p, 4 * (size_t)g.nnz, st, s);
+        if (!g.symmetric) {
+            put_dev(f.get(), g.crow_ptr(), ob * (size_t)(g.n + 1), st, s);
+            put_dev(f.get(), g.ccol.p, 4 * (size_t)g.nnz, st, s);
+        }
+        if (std::fclose(f.release()) != 0 || std::rename(tmp.c_str(), path) != 0) {
+            std::remove(tmp.c_str());
+            set_error(std::string("pj_graph_save: cannot write ") + path);
+            return (int)PJ_ERR_IO;
+        }
+        return (int)PJ_OK;
+    });
+}
+
+int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int64_t expect_src_mtime_ns,
+                     pj_graph** out) {
+    if (!ctx || !path || !out) return arg_error("pj_load_csr_file: bad argument");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        std::unique_ptr<FILE, FileCloser> f(std::fopen(path, "rb"));
+        if (!f) {
+            set_error(std::string("pj_load_csr_file: cannot open ") + path);
+            return (int)PJ_ERR_IO;
+        }
+        CsrFileHeader h{};
+        struct stat sb {};
+        if (std::fread(&h, sizeof h, 1, f.get()) != 1 || std::memcmp(h.magic, kCsrMagic, 8) != 0 ||
+            h.version != 1 || (h.flags & ~7u) != 0 || h.n < 0 || h.n > 0xFFFFFFFFll || h.nnz < 0 ||
+            ((h.flags & 4) == 0 && (uint64_t)h.nnz > 0xFFFFFFFFull) ||
+            h.payload != csr_payload(h.n, h.nnz, h.flags) || fstat(fileno(f.get()), &sb) != 0 ||
+            (uint64_t)sb.st_size != sizeof h + h.payload) {
+            set_error(std::string("pj_load_csr_file: not a libpj CSR file (or truncated): ") + path);
+            return (int)PJ_ERR_PARSE;
+        }
+        if ((expect_src_size != -1 && expect_src_size != h.src_size) ||
+            (expect_src_mtime_ns != -1 && expect_src_mtime_ns != h.src_mtime_ns)) {
+            set_error(std::string("pj_load_csr_file: stale cache (source stamp differs): ") + path);
+            return (int)PJ_ERR_STATE;
+        }
+        hipStream_t s = ctx->c.stream;
+        auto pg = std::make_unique<pj_graph>();
+        Graph& g = pg->g;
+        g.ctx = &ctx->c;
+        g.n = h.n;
+        g.nnz = h.nnz;
+        g.weighted = (h.flags & 1) != 0;
+        g.symmetric = (h.flags & 2) != 0;
+        g.off64 = (h.flags & 4) != 0;
+        PinnedBuf<char> st;
+        st.alloc(kStage);
+        const size_t nr = (size_t)g.n + 1;
+        if (g.off64) {
+            g.row64.alloc(nr);
+            get_dev(f.get(), g.row64.p, 8 * nr, st, s);
+        } else {
+            g.row32.alloc(nr);
+            get_dev(f.get(), g.row32.p, 4 * nr, st, s);
+        }
+        g.col.alloc((size_t)g.nnz);
+        get_dev(f.get(), g.col.p, 4 * (size_t)g.nnz, st, s);
+        if (g.weighted) {
+            g.w.alloc((size_t)g.nnz);
+            get_dev(f.get(), g.w.p, 4 * (size_t)g.nnz, st, s);
+        }
+        if (!g.symmetric) {
+            if (g.off64) {
+                g.crow64.alloc(nr);
+                get_dev(f.get(), g.crow64.p, 8 * nr, st, s);
+            } else {
+                g.crow32.alloc(nr);
+                get_dev(f.get(), g.crow32.p, 4 * nr, st, s);
+            }
+            g.ccol.alloc((size_t)g.nnz);
+            get_dev(f.get(), g.ccol.p, 4 * (size_t)g.nnz, st, s);
+        }
+        return finish_graph(ctx, pg, out);
+    });
+}
+
 // ---------------------------------------------------------------- output --
 // output_vector (:32-46): header line, then one decimal or "inf" per vertex.
 // Formatting is split over host threads into per-chunk buffers and written

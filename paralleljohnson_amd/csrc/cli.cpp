@@ -9,8 +9,12 @@
 // status 255 (the reference's error status, :35/:82/:302).
 //
 // Environment: PJ_DEVICE (HIP ordinal, default 0 or LOCAL_RANK), PJ_WEIGHTED=1
-// (third column = weight, delta-stepping). Under an MPI-style launcher only
-// rank 0 works; the other ranks exit 0.
+// (third column = weight, delta-stepping), PJ_CSR_CACHE (binary CSR cache: "1"
+// for <webfile>.pjcsr, or a path; loaded instead of parsing when its stamp --
+// the text's size and mtime -- and weight mode match, else written after the
+// parse). Under an MPI-style launcher only rank 0 works; the other ranks exit 0.
+#include <sys/stat.h>
+
 #include <cstdlib>
 #include <iostream>
 #include <string>
@@ -31,6 +35,28 @@ int launcher_rank() {
         if (v && *v) return std::atoi(v);
     }
     return 0;
+}
+
+// The graph of `path`: from the binary CSR cache when PJ_CSR_CACHE names a fresh one,
+// else parsed (pj_load_snap) and, with PJ_CSR_CACHE set, cached for the next run.
+int load_graph(pj_ctx* ctx, const char* path, int weighted, pj_graph** g) {
+    const char* cache = std::getenv("PJ_CSR_CACHE");
+    struct stat sb {};
+    if (!cache || !*cache || stat(path, &sb) != 0) return pj_load_snap(ctx, path, weighted, g);
+    const std::string cpath = std::string(cache) == "1" ? std::string(path) + ".pjcsr" : std::string(cache);
+    const int64_t size = (int64_t)sb.st_size;
+    const int64_t mtime = (int64_t)sb.st_mtim.tv_sec * 1000000000ll + (int64_t)sb.st_mtim.tv_nsec;
+    if (pj_load_csr_file(ctx, cpath.c_str(), size, mtime, g) == PJ_OK) {
+        int w = 0;
+        pj_graph_info(*g, nullptr, nullptr, &w, nullptr);
+        if (w == (weighted != 0)) return PJ_OK;
+        pj_graph_destroy(*g);
+        *g = nullptr;
+    }
+    const int rc = pj_load_snap(ctx, path, weighted, g);
+    if (rc == PJ_OK && pj_graph_save(*g, cpath.c_str(), size, mtime) != PJ_OK)
+        std::cerr << "warning: could not write the CSR cache " << cpath << ": " << pj_last_error() << std::endl;
+    return rc;
 }
 
 // print_msg :49-53
@@ -65,7 +91,7 @@ int main(int argc, char* argv[]) {
     int rc = pj_create(env_int("PJ_DEVICE", env_int("LOCAL_RANK", 0)), &ctx);
     if (rc != PJ_OK) fail("pj_create", rc);
     pj_graph* g = nullptr;
-    rc = pj_load_snap(ctx, argv[1], env_int("PJ_WEIGHTED", 0), &g);
+    rc = load_graph(ctx, argv[1], env_int("PJ_WEIGHTED", 0), &g);
     if (rc != PJ_OK) fail("pj_load_snap", rc);
     int64_t n = 0;
     pj_graph_info(g, &n, nullptr, nullptr, nullptr);
