@@ -12,13 +12,6 @@ constexpr int WAVE = 64;
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 __device__ __forceinline__ u64 lanemask_lt() { return (1ull << lane_id()) - 1ull; }
-// LDS written by some lanes of a wave and read by others: order the accesses (compiler
-// and lgkm counter) without a block barrier
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T x) {

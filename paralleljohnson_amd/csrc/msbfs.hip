@@ -26,7 +26,14 @@ namespace pj {
 namespace {
 
 constexpr int MB = 256;
-constexpr int MS_SERIAL = 16;
+#ifndef PJ_MS_SERIAL
+#define PJ_MS_SERIAL 16
+#endif
+constexpr int MS_SERIAL = PJ_MS_SERIAL;  // in-edges a lane scans alone before the wave helps
+#ifndef PJ_MS_U
+#define PJ_MS_U 8
+#endif
+constexpr int MS_U = PJ_MS_U;  // pull: in-edges a lane loads per serial step
 constexpr int MS_WMAX = 4;  // widest pass: 256 sources
 
 struct MsCtl {
@@ -294,10 +301,21 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
         bool go = hasneed && k < lim;
         while (__ballot(go)) {
             if (go) {
-                const Mask<W> f = mload<W>(F, ccol[k]);
+                // MS_U in-edges per step: their ids, then their masks, as independent loads
+                u32 u[MS_U];
 #pragma unroll
-                for (int j = 0; j < W; ++j) acc.w[j] |= f.w[j];
-                ++k;
+                for (int q = 0; q < MS_U; ++q) u[q] = (k + (Off)q < lim) ? ccol[k + q] : 0u;
+                Mask<W> f[MS_U];
+#pragma unroll
+                for (int q = 0; q < MS_U; ++q) {
+                    if (k + (Off)q < lim) f[q] = mload<W>(F, u[q]);
+                    else f[q] = Mask<W>{};
+                }
+#pragma unroll
+                for (int q = 0; q < MS_U; ++q)
+#pragma unroll
+                    for (int j = 0; j < W; ++j) acc.w[j] |= f[q].w[j];
+                k = (lim - k > (Off)MS_U) ? k + (Off)MS_U : lim;
                 go = mopen<W>(need, acc) && k < lim;
             }
         }
@@ -312,12 +330,15 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
                 want.w[j] = __shfl(need.w[j], l, 64);
                 got.w[j] = __shfl(acc.w[j], l, 64);
             }
-            for (Off kk = kb; kk < ke && mopen<W>(want, got); kk += WAVE) {
-                const Off kx = kk + lane;
-                Mask<W> x{};
-                if (kx < ke) x = mload<W>(F, ccol[kx]);
+            // two 64-edge chunks per step (independent loads), one wave reduction
+            for (Off kk = kb; kk < ke && mopen<W>(want, got); kk += 2 * WAVE) {
+                const Off k0 = kk + lane, k1 = kk + WAVE + lane;
+                const u32 u0 = k0 < ke ? ccol[k0] : 0u, u1 = k1 < ke ? ccol[k1] : 0u;
+                Mask<W> x{}, y{};
+                if (k0 < ke) x = mload<W>(F, u0);
+                if (k1 < ke) y = mload<W>(F, u1);
 #pragma unroll
-                for (int j = 0; j < W; ++j) got.w[j] |= wave_or(x.w[j]);
+                for (int j = 0; j < W; ++j) got.w[j] |= wave_or(x.w[j] | y.w[j]);
             }
             if (lane == l) acc = got;
         }
