@@ -39,6 +39,55 @@ def to_text(src, dst, w=None, style=0):
     return "".join(lines).encode()
 
 
+def sssp_certificate(row, col, w, dist, root, inf=100000, device="cpu", chunk=1 << 27):
+    """Size-independent proof that `dist` is the capped shortest-path vector of the CSR
+    graph from `root` (the R9 contract): returns a list of violations
+    (empty = exact).
+
+    With weights >= 1 (w is None = unit), `dist` is exact iff
+      (1) dist[root] == 0 when 0 <= root < n, every entry in [0, inf];
+      (2) no edge u->v with dist[u] + w < inf has dist[v] > dist[u] + w;
+      (3) every v != root with dist[v] < inf has a tight in-edge u->v,
+          dist[u] + w == dist[v] (so dist[v] is the length of a real path).
+    (2) bounds dist from above by induction along shortest paths; (3) gives a
+    strictly decreasing predecessor chain that ends at the root, so dist is a path
+    length; a true distance >= inf therefore forces dist = inf. Edges are streamed
+    in row chunks of about `chunk` entries, on `device` (torch)."""
+    import torch
+    n = len(row) - 1
+    d = torch.as_tensor(np.asarray(dist, dtype=np.int64)).to(device)
+    bad = []
+    if n == 0:
+        return bad
+    if int(d.min()) < 0 or int(d.max()) > inf:
+        bad.append("entry outside [0, inf]")
+    if 0 <= root < n and int(d[root]) != 0:
+        bad.append(f"dist[root] = {int(d[root])}")
+    best = torch.full((n,), inf, dtype=torch.int64, device=device)  # min over in-edges of dist[u] + w
+    row = np.asarray(row, dtype=np.int64)
+    r0 = 0
+    while r0 < n:
+        r1 = int(np.searchsorted(row, row[r0] + chunk, side="right")) - 1
+        r1 = min(max(r1, r0 + 1), n)
+        e0, e1 = int(row[r0]), int(row[r1])
+        if e1 > e0:
+            deg = torch.as_tensor(np.diff(row[r0:r1 + 1])).to(device)
+            u = torch.repeat_interleave(torch.arange(r0, r1, device=device), deg)
+            v = torch.as_tensor(np.asarray(col[e0:e1]).view(np.uint32).astype(np.int64)).to(device)
+            cand = d[u] + (1 if w is None else torch.as_tensor(np.asarray(w[e0:e1], dtype=np.int64)).to(device))
+            cand = torch.where(d[u] < inf, cand, torch.full_like(cand, inf)).clamp_(max=inf)
+            if bool((d[v] > cand).any()):
+                bad.append(f"edge rows [{r0}, {r1}): an edge relaxes further (condition 2)")
+            best.scatter_reduce_(0, v, cand, reduce="amin")
+        r0 = r1
+    reached = d < inf
+    if 0 <= root < n:
+        reached[root] = False
+    if bool((best[reached] != d[reached]).any()):
+        bad.append("a reached vertex has no tight in-edge (condition 3)")
+    return bad
+
+
 def csr_to_text(row, col):
     """SNAP-style edge list (tab-separated, '#' header) of a CSR, rows in order."""
     import numpy as np

@@ -355,3 +355,56 @@ def test_webgraph_cli_config0(ctx, pj, oracle, tmp_path):
     assert (ref4 == exp).all()
     assert out.read_bytes() == oracle.format_sol(exp)
     assert (exp < INF).sum() > 100000  # source 0 reaches a large part of the graph
+
+
+def test_weighted_kronecker_s26_full_size(ctx):
+    """BASELINE.json configs[2] at full size (2^31 entries, weights 1..255), the bench's
+    first roots: every distance proven exact by the shortest-path certificate
+    (helpers.sssp_certificate: no edge relaxes further, every reached vertex has a
+    tight in-edge), which needs no CPU solve. Also checks reach_stats against dist."""
+    import torch
+    from helpers import sssp_certificate
+    g = ctx.generate_kronecker(26, 16, 1, weighted=True)
+    assert g.nnz == 1 << 31 and g.weighted
+    roots = [int(r) for r in g.sample_roots(2, 2)]  # bench.py: sample_roots(seed + 1, 64)
+    dists = {r: g.sssp(r) for r in roots}
+    row, col, w = g.get_csr()
+    g.close()
+    assert int(w.min()) >= 1 and int(w.max()) <= 255
+    deg = np.diff(row)
+    for r, d in dists.items():
+        assert sssp_certificate(row, col, w, d, r, device="cuda", chunk=1 << 28) == [], r
+        reached = d < INF
+        assert reached.sum() > (1 << 24)  # the giant component (~49% of the ids at s26)
+        assert d[reached].max() > 255  # multi-hop weighted paths, several bands
+    torch.cuda.empty_cache()
+
+
+def test_partitioned_bfs_s28_full_size(ctx):
+    """BASELINE.json configs[3]'s solver (part.hip + partition.py, 1D vertex partition)
+    at world 1 on the full Kronecker s28 (2^33 entries, 64-bit row offsets): gathered
+    distances proven exact by the certificate against the CSR of the same graph built
+    by the single-GPU loader (a different code path: kronecker -> radix sort -> CSR)."""
+    import torch
+    from helpers import sssp_certificate
+    from paralleljohnson_amd.partition import PartitionedBFS, gather_dist, load_kronecker
+    ops = load_kronecker(ctx, 28, 16, 1, 0, 1)
+    bfs = PartitionedBFS(ops, None)
+    dists = {}
+    for c in np.random.default_rng(8).integers(0, 1 << 28, 64):  # bench.py's root rule: reached > 1
+        st = bfs.solve(int(c))
+        if st["reached"] > 1:
+            dists[int(c)] = gather_dist(ops, None)
+            assert st["reached"] == int((dists[int(c)] < INF).sum())
+        if len(dists) == 2:
+            break
+    ops.close()
+    torch.cuda.empty_cache()
+    g = ctx.generate_kronecker(28, 16, 1)
+    assert g.nnz == 1 << 33
+    row, col, _ = g.get_csr()
+    g.close()
+    for r, d in dists.items():
+        assert sssp_certificate(row, col, None, d, r, device="cuda", chunk=1 << 28) == [], r
+        assert (d < INF).sum() > (1 << 26)
+    torch.cuda.empty_cache()

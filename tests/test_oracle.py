@@ -127,3 +127,37 @@ def test_kronecker_spec(oracle):
     assert (s2 == s).all()
     deg = np.bincount(s, minlength=1024)
     assert deg.max() > 20 * deg.mean()  # skewed (Kronecker), not uniform
+
+
+def test_sssp_certificate_checker(oracle):
+    """The full-size GPU tests prove exactness with helpers.sssp_certificate (no CPU
+    solve at 2^31 entries); here the checker itself is pinned: it accepts the oracle's
+    distances and rejects single-entry corruptions, unit and weighted, capped."""
+    from helpers import sssp_certificate
+    rng = np.random.default_rng(77)
+    for trial in range(6):
+        n = int(rng.integers(2, 3000))
+        src, dst = random_graph(rng, ["uniform", "hub", "chain"][trial % 3], n)
+        w = None if trial % 2 else rng.integers(1, [3, 40000, 60000][trial % 3], len(src)).astype(np.uint32)
+        row, col, wc = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n, w)
+        r = int(src[0]) if len(src) else 0
+        d = oracle.bfs(row, col, r) if w is None else oracle.dijkstra(row, col, wc, r)
+        assert sssp_certificate(row, col, wc, d, r, chunk=997) == [], trial
+        reached = np.nonzero((d < INF) & (np.arange(n) != r))[0]
+        if len(reached):
+            v = int(reached[len(reached) // 2])
+            for delta in (-1, 1):
+                bad = d.copy()
+                bad[v] += delta
+                assert sssp_certificate(row, col, wc, bad, r, chunk=997), (trial, v, delta)
+        unreached = np.nonzero(d == INF)[0]
+        if len(unreached):
+            bad = d.copy()
+            bad[unreached[0]] = INF - 1
+            assert sssp_certificate(row, col, wc, bad, r), trial
+    # chain longer than the cap: the R9 cut at 100000 is exact, not a violation
+    n = 100010
+    row = np.arange(n + 1, dtype=np.int64).clip(max=n - 1)
+    col = np.arange(1, n, dtype=np.int32)
+    d = np.minimum(np.arange(n), INF).astype(np.int32)
+    assert sssp_certificate(row, col, None, d, 0) == []
