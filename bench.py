@@ -175,11 +175,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
+    # one rank per GPU; PJ_BENCH_BACKEND=gloo rehearses the N>1 bookkeeping with several
+    # ranks sharing fewer GPUs (the driver's runs use RCCL, one GPU per rank)
+    backend = os.environ.get("PJ_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
 
     import paralleljohnson_amd as pj
 
@@ -262,8 +269,8 @@ def main():
         per = el / pr["roots"]
         secondary["k28_partitioned"] = {
             "workload": f"graph500-kronecker-s{args.part_scale}-ef{args.edgefactor}-unit-bfs, 1D vertex "
-                        f"partition over {world} GPU(s)" + (" (RCCL all_to_all / all_gather / all_reduce)"
-                                                           if world > 1 else ""),
+                        f"partition over {world} GPU(s)" + ((" (RCCL all_to_all / all_gather / all_reduce)" if backend == "nccl" else
+                                                            f" ({backend}, rehearsal)") if world > 1 else ""),
             "n_vertices": pr["n"], "nnz": 2 * (args.edgefactor << args.part_scale),
             "nnz_local_rank0": pr["nnz_local"], "roots": pr["roots"],
             "time_to_solution_ms": round(1000.0 * per, 3),
