@@ -46,6 +46,20 @@ WORKLOADS = {
 }
 
 
+def host_cpu():
+    """Host CPU model and logical core count (report nproc and the CPU model)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "host_nproc": os.cpu_count()}
+
+
 def algorithmic_bytes(n, n_r, m_r, nnz, weighted=False):
     o = 4 if nnz < 2**31 else 8
     return 4 * n + n_r * (12 + 2 * o) + m_r * (8 + 4 * int(weighted))
@@ -148,8 +162,24 @@ def run_multisource(ctx, args, rank, world, barrier, n_src=1024):
     for s0 in range(0, len(mine), 64):
         d = g.sssp_batch(mine[s0:s0 + 64])
         m += float(((d < 100000) * deg[None, :]).sum())
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the reference takes one source per run, so 1024 single-source runs;
+        # time the first 16 sources and scale to 1024 (labelled extrapolated)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # cpu_baseline leg only
+        O.build()
+        col = g.get_csr()[1].view(np.uint32)
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        k, solve_s = 16, 0.0
+        for s in sources[:k]:
+            _, st = O.reference_sssp(row, col, int(s), threads)
+            solve_s += st.solve_s
+        cpu = {"value_s_extrapolated": round(solve_s * len(sources) / k, 3), "sample": f"{k} of {len(sources)} "
+               f"single-source solves timed ({solve_s:.3f} s), scaled to {len(sources)}", "cores": threads,
+               "kind": "port"}
     g.close()
-    return dict(elapsed=elapsed, m=m, n_src=len(mine))
+    return dict(elapsed=elapsed, m=m, n_src=len(mine), cpu=cpu)
 
 
 def main():
@@ -263,6 +293,8 @@ def main():
             "sources_per_rank": ms["n_src"], "time_to_solution_ms": round(1000.0 * el, 3),
             "gteps": round(m / el / 1e9, 3), "scaling": "strong (1024 sources in total)",
         }
+        if ms["cpu"]:
+            secondary["ms1024"]["cpu_baseline"] = ms["cpu"]
     if not args.no_partitioned and not args.scale:
         pr = run_partitioned(ctx, args, rank, world, barrier)
         el, _ = max_sum(pr["elapsed"], 0.0)
@@ -368,6 +400,15 @@ def run_wg_cli(ctx, args):
     ref_s = time.perf_counter() - t0
     exp = O.format_sol(ref)
     m_r = int(np.diff(row)[ref < 100000].sum())
+    np_scan = {}  # np = 1, 4 and the host threads bench.py uses
+    for p in sorted({1, 4, max(1, min(args.cpu_threads, os.cpu_count() or 1))}):
+        if p == 4:
+            np_scan[p] = round(st.solve_s, 4)
+            continue
+        d_p, st_p = O.reference_sssp(row, col, 0, p)
+        if not (d_p == ref).all():
+            raise RuntimeError(f"reference algorithm at np={p} disagrees with np=4")
+        np_scan[p] = round(st_p.solve_s, 4)
     return {
         "workload": "web-google-shaped-synthetic, SNAP text file, source 0, parallel_johnson CLI end to end",
         "text_mb": round(text_mb, 1), "n_vertices": len(row) - 1, "nnz": int(len(col)),
@@ -377,6 +418,8 @@ def run_wg_cli(ctx, args):
         "reference_np4_solve_s": round(st.solve_s, 3), "reference_np4_wall_s": round(ref_s, 3),
         "reference_np4_gteps": round(m_r / st.solve_s / 1e9, 5), "reference_cores": 4,
         "reference_kind": "port (oracle restatement of the reference's BSP heap algorithm, 4 host threads)",
+        "reference_solve_s_by_np": np_scan,
+        **host_cpu(),
     }
 
 
@@ -407,6 +450,7 @@ def cpu_baseline(g, res, args):
         "kind": "port",
         "sample": sample + f"; reference BSP heap algorithm, 30 pops/round, {threads} partitions on "
                            f"{threads} host threads",
+        **host_cpu(),
     }
 
 
