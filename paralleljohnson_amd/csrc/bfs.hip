@@ -802,6 +802,9 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
                 else bfs_level_k<Off, false><<<grid, TB, 0, s>>>(a, gd, L);
                 PJ_LAUNCH_CHECK();
             }
+            // end event right behind this batch's last level (re-recorded per batch), so the
+            // device time does not include the host's done-word round trip
+            PJ_HIP(hipEventRecord(g.ev1, s));
             PJ_HIP(hipStreamSynchronize(s));
             if (*(volatile int64_t*)w.host >= 0 || L >= INT_INF) break;
             batch = batch < 1024 ? batch * 2 : batch;
@@ -809,7 +812,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
         st.levels = *(volatile int64_t*)w.host;
         w.last_depth = (int32_t)st.levels;
     }
-    PJ_HIP(hipEventRecord(g.ev1, s));
+    if (!valid) PJ_HIP(hipEventRecord(g.ev1, s));
     PJ_HIP(hipEventSynchronize(g.ev1));
     float ms = 0.f;
     PJ_HIP(hipEventElapsedTime(&ms, g.ev0, g.ev1));
