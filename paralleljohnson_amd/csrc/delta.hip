@@ -498,6 +498,12 @@ __global__ __launch_bounds__(DB) void d_relax_k(const u32* __restrict__ iv, cons
 
 __global__ void d_source_k(i64 s, int32_t* __restrict__ dist) { dist[s] = 0; }
 
+#ifndef PJ_V2_GPC
+#define PJ_V2_GPC 24  // swept 4..48 on s26w: 8 -> 24 is ~+4% (profiles/r01/v2_grid_sweep.txt)
+#endif
+#ifndef PJ_V2_GPC_PULL
+#define PJ_V2_GPC_PULL PJ_V2_GPC
+#endif
 // distances back to input ids: out[v] = dist'[inv[v]] (INT_INF past n_scan)
 __global__ void unlabel_k(const u32* __restrict__ inv, const int32_t* __restrict__ dl, i64 n, i64 n_scan,
                           int32_t* __restrict__ out) {
@@ -1875,7 +1881,8 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     const i64 n = R.n_scan;
     const i64 nwords = (n + 63) / 64;
     const Off* row = static_cast<const Off*>(R.row_ptr(g.off64));
-    const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
+    const unsigned maxgrid = (unsigned)ctx.cu_count * (unsigned)PJ_V2_GPC;  // workgroups per CU of the v2 kernels (grid-stride)
+    const unsigned pullgrid = (unsigned)ctx.cu_count * (unsigned)PJ_V2_GPC_PULL;
     const int32_t delta = prepare_delta<Off>(g, w);
     // band width: at most the light threshold (an edge that can stay inside its
     // band must be light, so the band's light rounds see it)
@@ -1955,10 +1962,10 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 const bool try_pull = can_pull_light && (double)last_fe * g.pull_grow > (double)pull_thresh;
                 for (int q = 0; q < K; ++q) {
                     if (try_pull) {
-                        v2_pull_light_k<Off><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh);
+                        v2_pull_light_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh);
                         PJ_LAUNCH_CHECK();
                         if (w.nlc) {
-                            v2_pull_long_k<Off><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh,
+                            v2_pull_long_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh,
                                                                        w.lcv.p, w.lcc.p, w.nlc);
                             PJ_LAUNCH_CHECK();
                         }
@@ -2019,7 +2026,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 a.swrite = w.sb.p;
             }
             if (can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh) {
-                v2_pull_k<Off><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi_t, cs);
+                v2_pull_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi_t, cs);
                 PJ_LAUNCH_CHECK();
                 PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 st.bu_levels++;
