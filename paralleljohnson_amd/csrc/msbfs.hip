@@ -98,6 +98,9 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
     return x;
 }
 
+#ifndef PJ_MS_GPC
+#define PJ_MS_GPC 4  // level-kernel workgroups per CU
+#endif
 __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __restrict__ F, i64 nw,
                                                 int32_t* __restrict__ dist, i64 nb_dist, MsCtl* ctl,
                                                 int64_t* host_done) {
@@ -400,7 +403,7 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, int32_t
             smask.w[i >> 6] |= 1ull << (i & 63);
             any = true;
         }
-    const unsigned grid = (unsigned)g.ctx->cu_count * 4u;
+    const unsigned grid = (unsigned)g.ctx->cu_count * (unsigned)PJ_MS_GPC;
     const Off* row = static_cast<const Off*>(g.row_ptr());
     const u32* col = g.col.p;
     // push while the frontier's out-edges are below nnz / ms_alpha (0: never)

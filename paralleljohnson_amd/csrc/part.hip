@@ -103,6 +103,9 @@ struct KronSrc {
 };
 
 template <class S>
+#ifndef PJ_PART_GPC
+#define PJ_PART_GPC 32  // push/pull workgroups per CU (swept 4..48 on s28 at world 1: 8 -> 32 is 14.66 -> 13.80 ms, profiles/r01/part_grid_sweep.txt)
+#endif
 __global__ __launch_bounds__(TB) void filter_count_k(S src, bool by_dst, u64 lo, u64 hi, u32* __restrict__ bcnt) {
     __shared__ u32 red[NW];
     const i64 base = (i64)blockIdx.x * TB * IPT;
@@ -738,7 +741,7 @@ void push_impl(Part& p, int level, u64* vis, u32* packed, i64* counts) {
         PJ_LAUNCH_CHECK();
         exclusive_scan_u32(p.qdeg.p, p.qoff.p, (i64)p.nq, p.scan, s);
         const u64 tiles = (p.mq + PTILE - 1) / PTILE;
-        const unsigned grid = (unsigned)std::min<u64>(tiles, (u64)p.ctx->cu_count * 8);
+        const unsigned grid = (unsigned)std::min<u64>(tiles, (u64)p.ctx->cu_count * PJ_PART_GPC);
         part_push_k<Off><<<grid, TB, 0, s>>>(a, part_d<Off>(p), p.nq, p.mq, level + 1);
         PJ_LAUNCH_CHECK();
     }
@@ -767,7 +770,7 @@ void part_pull(Part& p, int level, u64* vis) {
     hipStream_t s = p.ctx->stream;
     PartArgs a = part_args(p, vis);
     const i64 nsc = (p.bw + SC - 1) / SC;
-    const unsigned grid = grid_for(nsc, NW, (unsigned)p.ctx->cu_count * 8);
+    const unsigned grid = grid_for(nsc, NW, (unsigned)p.ctx->cu_count * PJ_PART_GPC);
     if (p.off64) part_pull_k<u64><<<grid, TB, 0, s>>>(a, part_d<u64>(p), level + 1);
     else part_pull_k<u32><<<grid, TB, 0, s>>>(a, part_d<u32>(p), level + 1);
     PJ_LAUNCH_CHECK();
