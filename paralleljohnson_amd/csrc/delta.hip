@@ -519,7 +519,7 @@ __global__ void unlabel_k(const u32* __restrict__ inv, const int32_t* __restrict
 // system idle). Weights ascend along the row, so once lo + w >= cur for an
 // edge, that edge and every later one are useless: the step returns true.
 #ifndef PJ_PU
-#define PJ_PU 4
+#define PJ_PU 2  // swept 1..8 with the 24-per-CU grid: 2 is ~+3% over 4 (profiles/r01/v2_unroll_sweep.txt)
 #endif
 constexpr int PU = PJ_PU;
 // pull from band members [lo, hi)
@@ -823,7 +823,7 @@ constexpr int V2_EB = 40;     // hub counter: (slots << V2_EB) | edges
 constexpr int V2_NSH = 8;     // shards of a count slot
 constexpr int V2_HTILE = DB * 4;
 #ifndef PJ_V2_PLMAX
-#define PJ_V2_PLMAX 32
+#define PJ_V2_PLMAX 64
 #endif
 #ifndef PJ_V2_PCH
 #define PJ_V2_PCH 256
