@@ -676,7 +676,10 @@ __device__ __forceinline__ bool pull_step_fin_cw(const u64* __restrict__ ed, con
 // 64 vertices, compacts the candidates into lanes, probes PSERIAL edges per lane
 // (wave-uniform loop), then scans the long rows with the whole wave.
 constexpr int PSC = 16;
-constexpr int PSERIAL = 32;
+#ifndef PJ_PSERIAL
+#define PJ_PSERIAL 32
+#endif
+constexpr int PSERIAL = PJ_PSERIAL;
 template <typename Off>
 __global__ __launch_bounds__(DB) void d_pull_heavy_k(const Off* __restrict__ row, const u32* __restrict__ lsplit,
                                                      const u32* __restrict__ col, const u32* __restrict__ wt,
@@ -810,7 +813,7 @@ __global__ __launch_bounds__(DB) void wsum_k(const u32* __restrict__ w, i64 n, u
 // ---------------------------------------------------------------------------
 constexpr int V2_SC = 16;     // frontier words a wave screens at once
 #ifndef PJ_V2_LS
-#define PJ_V2_LS 8
+#define PJ_V2_LS 2
 #endif
 constexpr int V2_LS = PJ_V2_LS;  // segment edges a lane relaxes alone
 #ifndef PJ_V2_HT
