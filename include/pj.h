@@ -64,6 +64,8 @@ typedef struct pj_stats {
 /* Bind to HIP device `device` (ordinal as HIP sees it). Replaces MPI_Init
  * (:679) + the per-rank setup of parallel_johnson (:291-292). */
 int pj_create(int device, pj_ctx** out);
+/* Number of visible HIP devices (0 when none). */
+int pj_device_count(int* out);
 int pj_destroy(pj_ctx* ctx);
 /* HIP stream (hipStream_t) all work of this ctx is launched on. */
 void* pj_stream(pj_ctx* ctx);
@@ -149,9 +151,19 @@ int pj_copy_dist(pj_graph* g, int32_t* dist_out);
 const int32_t* pj_dist_device(pj_graph* g);
 /* Batched multi-source (Johnson-style all-pairs rows): dist_out is n_src x n
  * int32, row i = pj_sssp(g, sources[i]); NULL discards the rows (timing).
- * Unit-weight graphs run 64 sources per pass with one bit per source
- * (msbfs.hip); pj_last_stats then describes the whole batch. */
+ * Unit-weight graphs run up to 256 sources per pass, one bit per source
+ * (msbfs.hip; the option ms_width caps the pass at 64 x ms_width); weighted
+ * graphs run one delta-stepping solve per source. Either way pj_last_stats
+ * then describes the whole batch (kernel_ms and levels summed over passes or
+ * solves) and pj_copy_dist / pj_reach_stats fail with PJ_ERR_STATE until the
+ * next pj_sssp. No reference counterpart: the reference answers one source
+ * per run (atoi(argv[2]), :448). */
 int pj_sssp_batch(pj_graph* g, const int64_t* sources, int n_src, int32_t* dist_out);
+/* The multi-source drop-in: the same batch, with row i written as a sol_file
+ * to paths[i] (the bytes of pj_write_sol, i.e. of a single-source run
+ * :615-620). Rows are copied to the host in groups and written by a pool of
+ * host threads while the GPU computes the next pass. strict as pj_write_sol. */
+int pj_sssp_batch_write(pj_graph* g, const int64_t* sources, int n_src, const char* const* paths, int strict);
 /* Statistics of the last solve. pj_reach_stats additionally computes
  * reached / reached_edges on the device (not part of kernel_ms). */
 int pj_last_stats(const pj_graph* g, pj_stats* out);

@@ -40,6 +40,8 @@ def lib():
         L.pjo_coo2csr.restype = None
         L.pjo_bfs.argtypes = [P, P, i64, i64, P]
         L.pjo_bfs.restype = None
+        L.pjo_bfs_batch.argtypes = [P, P, i64, P, i64, ctypes.c_int, P]
+        L.pjo_bfs_batch.restype = None
         L.pjo_dijkstra.argtypes = [P, P, P, i64, i64, P]
         L.pjo_dijkstra.restype = None
         L.pjo_reference_sssp.argtypes = [P, P, P, i64, i64, ctypes.c_int, P, P]
@@ -106,6 +108,16 @@ def bfs(row, col, source):
     dist = np.zeros(max(n, 1), np.int32)
     lib().pjo_bfs(_p(row), _p(np.ascontiguousarray(col, np.uint32)), n, int(source), _p(dist))
     return dist[:n]
+
+
+def bfs_batch(row, col, sources, threads=8):
+    """pjo_bfs for every source (rows of a k x n int32 matrix), on host threads."""
+    n = len(row) - 1
+    src = np.ascontiguousarray(np.asarray(sources, dtype=np.int64))
+    out = np.zeros((max(len(src), 1), max(n, 1)), np.int32)
+    lib().pjo_bfs_batch(_p(row), _p(np.ascontiguousarray(col, np.uint32)), n, _p(src), len(src), int(threads),
+                        _p(out))
+    return out[: len(src), :n]
 
 
 def dijkstra(row, col, w, source):

@@ -141,6 +141,32 @@ void pjo_bfs(const int64_t* row_ptr, const uint32_t* col, int64_t n, int64_t sou
     free(q);
 }
 
+/* pjo_bfs for k sources on `threads` host threads (test helper for the
+ * batched multi-source rows; each row is exactly pjo_bfs). */
+typedef struct {
+    const int64_t* row; const uint32_t* col; int64_t n;
+    const int64_t* src; int64_t k; int32_t* out; int t, nt;
+} bfs_job;
+static void* bfs_batch_worker(void* p) {
+    bfs_job* j = (bfs_job*)p;
+    for (int64_t i = j->t; i < j->k; i += j->nt)
+        pjo_bfs(j->row, j->col, j->n, j->src[i], j->out + (size_t)i * (size_t)j->n);
+    return NULL;
+}
+void pjo_bfs_batch(const int64_t* row_ptr, const uint32_t* col, int64_t n, const int64_t* sources,
+                   int64_t k, int threads, int32_t* dist) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    bfs_job jobs[256];
+    for (int t = 0; t < threads; t++) {
+        bfs_job j = {row_ptr, col, n, sources, k, dist, t, threads};
+        jobs[t] = j;
+        pthread_create(&th[t], NULL, bfs_batch_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}
+
 /* binary heap keyed by int64 distance, lazy deletion */
 typedef struct { int64_t d; uint32_t v; } hent;
 static void hpush(hent** h, int64_t* n, int64_t* cap, int64_t d, uint32_t v) {

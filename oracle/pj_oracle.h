@@ -41,6 +41,9 @@ void pjo_coo2csr(const uint32_t* src, const uint32_t* dst, const uint32_t* w, in
 /* R9 contract: hop distances from `source` with the INT_INF cap. */
 void pjo_bfs(const int64_t* row_ptr, const uint32_t* col, int64_t n, int64_t source,
              int32_t* dist);
+/* pjo_bfs for sources[0..k) on `threads` host threads; dist is k x n (test helper). */
+void pjo_bfs_batch(const int64_t* row_ptr, const uint32_t* col, int64_t n, const int64_t* sources,
+                   int64_t k, int threads, int32_t* dist);
 /* R9 generalised to integer weights >= 0 (no reference counterpart). */
 void pjo_dijkstra(const int64_t* row_ptr, const uint32_t* col, const uint32_t* w, int64_t n,
                   int64_t source, int32_t* dist);

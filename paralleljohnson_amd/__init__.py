@@ -90,6 +90,8 @@ _SIGS = {
     "pj_copy_dist": ([_P, _P], _INT),
     "pj_dist_device": ([_P], _P),
     "pj_sssp_batch": ([_P, _P, _INT, _P], _INT),
+    "pj_sssp_batch_write": ([_P, _P, _INT, _P, _INT], _INT),
+    "pj_device_count": ([_P], _INT),
     "pj_last_stats": ([_P, _P], _INT),
     "pj_reach_stats": ([_P, _P], _INT),
     "pj_set_option": ([_P, ctypes.c_char_p, ctypes.c_double], _INT),
@@ -194,6 +196,15 @@ class Graph:
         out = np.empty((len(src), max(self.n, 1)), np.int32) if copy else None
         _check(_lib.pj_sssp_batch(self._h, _ptr(src), len(src), _ptr(out)))
         return out[:, : self.n] if copy else None
+
+    def sssp_batch_write(self, sources: Sequence[int], paths: Sequence[str], strict: bool = True):
+        """Row i of the batch written as the sol_file paths[i] (pj_sssp_batch_write)."""
+        src = np.ascontiguousarray(np.asarray(sources, dtype=np.int64))
+        if len(paths) != len(src):
+            raise ValueError("one path per source")
+        arr = (ctypes.c_char_p * max(len(paths), 1))(*[os.fsencode(p) for p in paths])
+        _check(_lib.pj_sssp_batch_write(self._h, _ptr(src), len(src), ctypes.cast(arr, ctypes.c_void_p),
+                                        int(strict)))
 
     def stats(self) -> dict:
         st = Stats()
@@ -316,9 +327,7 @@ def write_sol(dist, path: str, strict: bool = False):
 
 
 def device_count() -> int:
-    """Number of HIP devices (no GPU initialisation side effects beyond HIP's)."""
-    try:
-        import torch
-        return torch.cuda.device_count()
-    except Exception:
-        return 0
+    """Number of visible HIP devices (pj_device_count)."""
+    n = _INT()
+    _check(_lib.pj_device_count(ctypes.byref(n)))
+    return n.value

@@ -2,6 +2,8 @@
 // checks, ownership, error translation; all graph work happens in the HIP
 // kernels of parse.hip / graph.hip / sort.hip / bfs.hip / delta.hip.
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <chrono>
 #include <cstdio>
 #include <thread>
@@ -79,6 +81,130 @@ int finish_graph(pj_ctx* ctx, std::unique_ptr<pj_graph>& pg, pj_graph** out) {
     return PJ_OK;
 }
 
+// Weighted batch: one delta-stepping solve per source (no shared passes);
+// stats are summed over the batch like the unit-weight msbfs path.
+template <typename F>
+void weighted_batch(Graph& g, const int64_t* sources, int n_src, F&& on_row) {
+    auto t0 = std::chrono::steady_clock::now();
+    pj_stats sum{};
+    for (int i = 0; i < n_src; ++i) {
+        delta_solve(g, sources[i]);
+        sum.kernel_ms += g.stats.kernel_ms;
+        sum.levels += g.stats.levels;
+        sum.relax_rounds += g.stats.relax_rounds;
+        on_row(i, g.dist.p);
+    }
+    sum.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    g.stats = sum;
+}
+
+size_t format_rows(const int32_t* d, int64_t a, int64_t b, char* o) {
+    size_t k = 0;
+    for (int64_t i = a; i < b; ++i) {
+        int32_t x = d[i];
+        if (x == PJ_INT_INF) {
+            o[k++] = 'i';
+            o[k++] = 'n';
+            o[k++] = 'f';
+        } else {
+            char rev[12];
+            int r = 0;
+            long long y = x;
+            const bool neg = y < 0;
+            if (neg) y = -y;
+            do {
+                rev[r++] = (char)('0' + y % 10);
+                y /= 10;
+            } while (y);
+            if (neg) o[k++] = '-';
+            while (r) o[k++] = rev[--r];
+        }
+        o[k++] = '\n';
+    }
+    return k;
+}
+
+
+// D2H of batch rows into pinned groups (double-buffered) and a pool of host
+// threads that format and write one sol_file per row (output_vector :32-46,
+// the bytes of pj_write_sol), overlapped with the next rows' GPU work.
+class BatchWriter {
+  public:
+    BatchWriter(size_t n, const char* const* paths, bool strict, std::atomic<int>* err)
+        : n_(n), paths_in_(paths), strict_(strict), err_(err) {
+        const size_t row_bytes = std::max<size_t>(4 * n, 4);
+        group_ = (int)std::max<size_t>(1, std::min<size_t>(256, ((size_t)256 << 20) / row_bytes));
+        for (auto& b : buf_) b.alloc(row_bytes / 4 * (size_t)group_);
+        nthreads_ = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    }
+    ~BatchWriter() { join(); }
+    void add_row(int idx, const int32_t* dev_row) {
+        if (fill_ == 0) join_slot(cur_);
+        if (n_) PJ_HIP(hipMemcpy(buf_[cur_].p + (size_t)fill_ * n_, dev_row, 4 * n_, hipMemcpyDeviceToHost));
+        paths_[cur_].push_back(paths_in_[idx]);
+        if (++fill_ == group_) flush();
+    }
+    void finish() {
+        if (fill_) flush();
+        join();
+    }
+    std::string error() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return msg_;
+    }
+
+  private:
+    void flush() {
+        const int slot = cur_, k = fill_;
+        for (int t = 0; t < nthreads_ && t < k; ++t)
+            th_[slot].emplace_back([this, slot, k, t] {
+                std::vector<char> out(n_ * 12 + 16);
+                for (int r = t; r < k; r += nthreads_) write_one(buf_[slot].p + (size_t)r * n_, paths_[slot][r], out);
+            });
+        cur_ ^= 1;
+        fill_ = 0;
+    }
+    void write_one(const int32_t* d, const std::string& path, std::vector<char>& out) {
+        FILE* f = std::fopen(path.c_str(), "wb");
+        if (!f) {
+            if (strict_) fail(PJ_ERR_IO, "cannot open " + path);
+            return;
+        }
+        static const char hdr[] = "the vector is:\n";
+        size_t k = sizeof(hdr) - 1;
+        std::memcpy(out.data(), hdr, k);
+        k += format_rows(d, 0, (int64_t)n_, out.data() + k);
+        const bool ok = std::fwrite(out.data(), 1, k, f) == k;
+        if ((std::fclose(f) != 0 || !ok) && strict_) fail(PJ_ERR_IO, "write failed: " + path);
+    }
+    void fail(int code, const std::string& m) {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (err_->load() == PJ_OK) {
+            err_->store(code);
+            msg_ = m;
+        }
+    }
+    void join_slot(int slot) {
+        for (auto& t : th_[slot]) t.join();
+        th_[slot].clear();
+        paths_[slot].clear();
+    }
+    void join() {
+        join_slot(0);
+        join_slot(1);
+    }
+    size_t n_;
+    const char* const* paths_in_;
+    bool strict_;
+    std::atomic<int>* err_;
+    int group_ = 1, nthreads_ = 1, cur_ = 0, fill_ = 0;
+    PinnedBuf<int32_t> buf_[2];
+    std::vector<std::string> paths_[2];
+    std::vector<std::thread> th_[2];
+    std::mutex mu_;
+    std::string msg_;
+};
+
 }  // namespace
 
 extern "C" {
@@ -86,6 +212,14 @@ extern "C" {
 const char* pj_last_error(void) { return g_err.c_str(); }
 
 const char* pj_version(void) { return "libpj 0.1 (gfx950)"; }
+
+int pj_device_count(int* out) {
+    if (!out) return arg_error("pj_device_count: out is NULL");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+    *out = count;
+    return PJ_OK;
+}
 
 int pj_create(int device, pj_ctx** out) {
     if (!out) return arg_error("pj_create: out is NULL");
@@ -351,18 +485,48 @@ const int32_t* pj_dist_device(pj_graph* pg) { return (pg && pg->g.have_result) ?
 
 int pj_sssp_batch(pj_graph* pg, const int64_t* sources, int n_src, int32_t* dist_out) {
     if (!pg || (n_src > 0 && !sources) || n_src < 0) return arg_error("pj_sssp_batch: bad argument");
-    if (pg->g.weighted) {
-        for (int i = 0; i < n_src; ++i) {
-            int rc = pj_sssp(pg, sources[i], dist_out ? dist_out + (size_t)i * (size_t)pg->g.n : nullptr);
-            if (rc != PJ_OK) return rc;
-        }
-        return PJ_OK;
-    }
     return guarded([&] {
-        bind(*pg->g.ctx);
-        msbfs_solve(pg->g, sources, n_src, dist_out);
-        pg->g.have_result = false;  // g.dist does not hold a batch row
-        pg->g.batch_stats = true;
+        Graph& g = pg->g;
+        bind(*g.ctx);
+        if (g.weighted) {
+            weighted_batch(g, sources, n_src, [&](int i, const int32_t* dev) {
+                if (dist_out && g.n)
+                    PJ_HIP(hipMemcpy(dist_out + (size_t)i * (size_t)g.n, dev, 4 * (size_t)g.n, hipMemcpyDeviceToHost));
+            });
+        } else {
+            msbfs_solve(g, sources, n_src, dist_out);
+        }
+        g.have_result = false;  // g.dist does not hold a batch row
+        g.batch_stats = true;
+        return (int)PJ_OK;
+    });
+}
+
+int pj_sssp_batch_write(pj_graph* pg, const int64_t* sources, int n_src, const char* const* paths, int strict) {
+    if (!pg || (n_src > 0 && (!sources || !paths)) || n_src < 0) return arg_error("pj_sssp_batch_write: bad argument");
+    for (int i = 0; i < n_src; ++i)
+        if (!paths[i]) return arg_error("pj_sssp_batch_write: a path is NULL");
+    return guarded([&] {
+        Graph& g = pg->g;
+        bind(*g.ctx);
+        const size_t n = (size_t)g.n;
+        std::atomic<int> err{PJ_OK};
+        BatchWriter wr(n, paths, strict != 0, &err);
+        if (g.weighted) {
+            // one solve per source; rows are gathered into host groups and written by the pool
+            weighted_batch(g, sources, n_src, [&](int i, const int32_t* dev) { wr.add_row(i, dev); });
+        } else {
+            msbfs_each(g, sources, n_src, [&](int off, int ns, const int32_t* rows) {
+                for (int k = 0; k < ns; ++k) wr.add_row(off + k, rows + (size_t)k * n);
+            });
+        }
+        wr.finish();
+        g.have_result = false;
+        g.batch_stats = true;
+        if (err.load() != PJ_OK) {
+            set_error(wr.error());
+            return err.load();
+        }
         return (int)PJ_OK;
     });
 }
@@ -583,32 +747,6 @@ int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int
 // Formatting is split over host threads into per-chunk buffers and written
 // in order, so the bytes are identical to the sequential writer.
 
-static size_t format_range(const int32_t* d, int64_t a, int64_t b, char* o) {
-    size_t k = 0;
-    for (int64_t i = a; i < b; ++i) {
-        int32_t x = d[i];
-        if (x == PJ_INT_INF) {
-            o[k++] = 'i';
-            o[k++] = 'n';
-            o[k++] = 'f';
-        } else {
-            char rev[12];
-            int r = 0;
-            long long y = x;
-            const bool neg = y < 0;
-            if (neg) y = -y;
-            do {
-                rev[r++] = (char)('0' + y % 10);
-                y /= 10;
-            } while (y);
-            if (neg) o[k++] = '-';
-            while (r) o[k++] = rev[--r];
-        }
-        o[k++] = '\n';
-    }
-    return k;
-}
-
 static const char kHeader[] = "the vector is:\n";
 
 int pj_format_sol(const int32_t* dist, int64_t n, char* buf, int64_t cap, int64_t* len_out) {
@@ -616,7 +754,7 @@ int pj_format_sol(const int32_t* dist, int64_t n, char* buf, int64_t cap, int64_
     std::vector<char> tmp((size_t)n * 12 + 16);
     size_t k = sizeof(kHeader) - 1;
     std::memcpy(tmp.data(), kHeader, k);
-    k += format_range(dist, 0, n, tmp.data() + k);
+    k += format_rows(dist, 0, n, tmp.data() + k);
     *len_out = (int64_t)k;
     if (buf) {
         if (cap < (int64_t)k) return arg_error("pj_format_sol: buffer too small");
@@ -649,7 +787,7 @@ int pj_write_sol(const int32_t* dist, int64_t n, const char* path, int strict) {
                 th.emplace_back([&, c] {
                     const int64_t a = (c0 + c) * chunk, b = std::min(n, a + chunk);
                     out[(size_t)c].resize((size_t)(b - a) * 12);
-                    lens[(size_t)c] = format_range(dist, a, b, out[(size_t)c].data());
+                    lens[(size_t)c] = format_rows(dist, a, b, out[(size_t)c].data());
                 });
             }
             for (auto& t : th) t.join();

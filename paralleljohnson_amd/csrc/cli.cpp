@@ -13,11 +13,25 @@
 // for <webfile>.pjcsr, or a path; loaded instead of parsing when its stamp --
 // the text's size and mtime -- and weight mode match, else written after the
 // parse). Under an MPI-style launcher only rank 0 works; the other ranks exit 0.
+//
+// Multi-source (Johnson-style rows; no reference counterpart, the reference
+// takes one source per run, :448): PJ_SOURCES = a list of sources separated by
+// commas or blanks, or "@file" with one source per line (each read with atoi,
+// like argv[2]). argv[2] is then ignored and argv[3] is a pattern: "{s}" is
+// replaced by the source, "{i}" by its index (no token: argv[3].<source>). Each
+// file is byte-identical to a single-source run. With PJ_GPUS = P > 1 the
+// sources are sharded over P GPUs (source r, r+P, ... on GPU r), each holding a
+// copy of the graph.
 #include <sys/stat.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstdlib>
+#include <fstream>
 #include <iostream>
+#include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pj.h"
@@ -69,6 +83,112 @@ void print_msg(const std::string& msg, int rank) {
     std::exit(-1);
 }
 
+int device_count() {
+    static int n = -1;
+    if (n < 0) {
+        n = 0;
+        pj_device_count(&n);
+    }
+    return n;
+}
+
+// PJ_SOURCES: "a,b c" or "@file" (one per line); every token read with atoi (:448)
+std::vector<int64_t> parse_sources(const char* spec) {
+    std::string text;
+    if (spec[0] == '@') {
+        std::ifstream f(spec + 1);
+        if (!f) {
+            std::cerr << "cannot read the source list " << (spec + 1) << std::endl;
+            std::exit(-1);
+        }
+        std::stringstream ss;
+        ss << f.rdbuf();
+        text = ss.str();
+    } else {
+        text = spec;
+    }
+    std::vector<int64_t> out;
+    std::string tok;
+    auto flush = [&] {
+        if (!tok.empty()) out.push_back(std::atoi(tok.c_str()));
+        tok.clear();
+    };
+    for (char c : text) {
+        if (c == ',' || c == '\n' || c == '\r' || c == ' ' || c == '\t') flush();
+        else tok += c;
+    }
+    flush();
+    return out;
+}
+
+// Per-source sol_file path: every "{s}" in the pattern becomes the source (decimal,
+// as atoi read it), every "{i}" its index in the list; no token: pattern + "." + source.
+std::string sol_path(const std::string& pat, int64_t src, size_t idx) {
+    std::string out;
+    bool tok = false;
+    for (size_t i = 0; i < pat.size(); ++i) {
+        if (pat.compare(i, 3, "{s}") == 0 || pat.compare(i, 3, "{i}") == 0) {
+            out += std::to_string(pat[i + 1] == 's' ? src : (int64_t)idx);
+            i += 2;
+            tok = true;
+        } else {
+            out += pat[i];
+        }
+    }
+    if (!tok) out += "." + std::to_string(src);
+    return out;
+}
+
+// Source-sharded multi-source run: GPU r solves sources r, r+P, ... and writes their files.
+int run_multi_source(const char* webfile, const std::vector<int64_t>& sources, const char* pattern, int gpus,
+                     int weighted) {
+    std::cerr << "compute shortest paths from " << sources.size() << " source nodes on " << gpus << " GPU(s)"
+              << std::endl;
+    std::cerr << "parallel Johnson's algorithm starts......" << std::endl;
+    std::vector<double> kms((size_t)gpus, 0.0);
+    std::vector<int> rcs((size_t)gpus, PJ_OK);
+    std::vector<std::string> errs((size_t)gpus);
+    std::vector<std::thread> th;
+    int64_t n_all = 0;
+    for (int r = 0; r < gpus; ++r)
+        th.emplace_back([&, r] {
+            pj_ctx* ctx = nullptr;
+            pj_graph* g = nullptr;
+            int rc = pj_create(r % std::max(1, device_count()), &ctx);
+            if (rc == PJ_OK) rc = load_graph(ctx, webfile, weighted, &g);
+            std::vector<int64_t> mine;
+            std::vector<std::string> paths;
+            for (size_t i = (size_t)r; i < sources.size(); i += (size_t)gpus) {
+                mine.push_back(sources[i]);
+                paths.push_back(sol_path(pattern, sources[i], i));
+            }
+            std::vector<const char*> pp;
+            for (auto& q : paths) pp.push_back(q.c_str());
+            if (rc == PJ_OK && r == 0) pj_graph_info(g, &n_all, nullptr, nullptr, nullptr);
+            if (rc == PJ_OK && !mine.empty()) {
+                rc = pj_sssp_batch_write(g, mine.data(), (int)mine.size(), pp.data(), 0);
+                pj_stats st{};
+                if (rc == PJ_OK && pj_last_stats(g, &st) == PJ_OK) kms[(size_t)r] = st.kernel_ms;
+            }
+            if (rc != PJ_OK) errs[(size_t)r] = pj_last_error();
+            rcs[(size_t)r] = rc;
+            pj_graph_destroy(g);
+            pj_destroy(ctx);
+        });
+    for (auto& t : th) t.join();
+    for (int r = 0; r < gpus; ++r)
+        if (rcs[(size_t)r] != PJ_OK) {
+            std::cerr << "GPU " << r << " failed (" << rcs[(size_t)r] << "): " << errs[(size_t)r] << std::endl;
+            std::exit(-1);
+        }
+    std::cerr << "N = " << n_all << std::endl;
+    std::cerr << "parallel Johnson's algorithm completes." << std::endl;
+    const double t = *std::max_element(kms.begin(), kms.end()) / 1000.0;
+    std::cout << "Time: " << t << " seconds when using " << gpus << " processes." << std::endl;
+    std::cerr << "the shortest path distance vectors have been saved in files " << pattern << std::endl;
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char* argv[]) {
@@ -85,6 +205,13 @@ int main(int argc, char* argv[]) {
         std::exit(-1);
     }
     if (rank != 0) return 0;
+
+    const char* srcs = std::getenv("PJ_SOURCES");
+    if (srcs && *srcs) {
+        print_msg("process 0 reads in the web graph data......", rank);
+        const int gpus = std::max(1, env_int("PJ_GPUS", 1));
+        return run_multi_source(argv[1], parse_sources(srcs), argv[3], gpus, env_int("PJ_WEIGHTED", 0));
+    }
 
     print_msg("process 0 reads in the web graph data......", rank);
     pj_ctx* ctx = nullptr;

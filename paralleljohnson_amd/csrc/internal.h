@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -243,6 +244,10 @@ void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t see
 void bfs_solve(Graph& g, i64 source);
 void delta_solve(Graph& g, i64 source);
 void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out);
+// Batched passes of up to 256 sources; after each pass on_pass(first source
+// index, sources in the pass, device rows [ns][n]) runs with the device idle.
+using MsPassFn = std::function<void(int, int, const int32_t*)>;
+void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_pass);
 void reach_stats(Graph& g, i64* n_r, i64* m_r);
 void debug_bitmaps(Graph& g, u64* vis0, u64* vis1, u64* fnew);
 

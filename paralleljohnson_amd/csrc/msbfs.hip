@@ -387,8 +387,7 @@ struct MsWork {
 void delete_ms_work(MsWork* p) { delete p; }
 
 template <typename Off, int W>
-static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, int32_t* dist_out, double* kernel_ms,
-                    i64* levels) {
+static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double* kernel_ms, i64* levels) {
     hipStream_t s = g.ctx->stream;
     const i64 n = g.n;
     const Off* crow = static_cast<const Off*>(g.crow_ptr());
@@ -444,15 +443,13 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, int32_t
     *kernel_ms += ms;
     const i64 lv = (i64)*(volatile int64_t*)w.host;
     *levels = std::max<i64>(*levels, lv);
-    if (dist_out && n) PJ_HIP(hipMemcpy(dist_out, w.dist.p, sizeof(int32_t) * (size_t)ns * (size_t)n, hipMemcpyDeviceToHost));
 }
 
 template <typename Off>
-static void ms_pass_w(int W, Graph& g, MsWork& w, const int64_t* sources, int ns, int32_t* dist_out,
-                      double* kernel_ms, i64* levels) {
-    if (W == 4) ms_pass<Off, 4>(g, w, sources, ns, dist_out, kernel_ms, levels);
-    else if (W == 2) ms_pass<Off, 2>(g, w, sources, ns, dist_out, kernel_ms, levels);
-    else ms_pass<Off, 1>(g, w, sources, ns, dist_out, kernel_ms, levels);
+static void ms_pass_w(int W, Graph& g, MsWork& w, const int64_t* sources, int ns, double* kernel_ms, i64* levels) {
+    if (W == 4) ms_pass<Off, 4>(g, w, sources, ns, kernel_ms, levels);
+    else if (W == 2) ms_pass<Off, 2>(g, w, sources, ns, kernel_ms, levels);
+    else ms_pass<Off, 1>(g, w, sources, ns, kernel_ms, levels);
 }
 
 // Pass width: the fewest words that hold the batch, at most MS_WMAX (g.ms_width
@@ -464,7 +461,7 @@ static int ms_words(const Graph& g, int n_src) {
     return W;
 }
 
-void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out) {
+void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_pass) {
     const size_t n = (size_t)g.n;
     const int W = ms_words(g, n_src);
     if (!g.ms_work || g.ms_work->W < W) {
@@ -488,15 +485,25 @@ void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out)
     const int per = 64 * W;
     for (int off = 0; off < n_src; off += per) {
         const int ns = std::min(per, n_src - off);
-        int32_t* out = dist_out ? dist_out + (size_t)off * n : nullptr;
-        if (g.off64) ms_pass_w<u64>(W, g, *g.ms_work, sources + off, ns, out, &kms, &levels);
-        else ms_pass_w<u32>(W, g, *g.ms_work, sources + off, ns, out, &kms, &levels);
+        if (g.off64) ms_pass_w<u64>(W, g, *g.ms_work, sources + off, ns, &kms, &levels);
+        else ms_pass_w<u32>(W, g, *g.ms_work, sources + off, ns, &kms, &levels);
+        if (on_pass) on_pass(off, ns, g.ms_work->dist.p);
     }
     st.kernel_ms = kms;
     st.levels = levels;
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     g.stats = st;
     // the per-source result of the last pass's final source is not kept in g.dist
+}
+
+void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out) {
+    const size_t n = (size_t)g.n;
+    MsPassFn copy;
+    if (dist_out && n)
+        copy = [&](int off, int ns, const int32_t* rows) {
+            PJ_HIP(hipMemcpy(dist_out + (size_t)off * n, rows, sizeof(int32_t) * (size_t)ns * n, hipMemcpyDeviceToHost));
+        };
+    msbfs_each(g, sources, n_src, copy);
 }
 
 }  // namespace pj
