@@ -498,3 +498,7 @@ def cpu_baseline(g, res, args):
         "cpu_share": share,
         **host_cpu(),
     }
+
+
+if __name__ == "__main__":
+    main()
