@@ -146,16 +146,23 @@ def time_to_solution(ctx_s, res):
 
 def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
     """configs[3]: Kronecker s{part_scale} unit-weight BFS, 1D vertex partition over the
-    `world` ranks (RCCL exchange, paralleljohnson_amd/partition.py); strong scaling."""
-    from paralleljohnson_amd.partition import Exchange, PartitionedBFS, load_kronecker
+    `world` ranks (libpj's level loop, pj_part_bfs, over RCCL: one process per GPU, the
+    group id handed out by rank 0 over torch.distributed); strong scaling."""
+    from paralleljohnson_amd.partition import Comm, load_kronecker
     t0 = time.perf_counter()
     ops = load_kronecker(ctx, args.part_scale, args.edgefactor, args.seed, rank, world)
-    bfs = PartitionedBFS(ops, Exchange() if world > 1 else None)
+    if world > 1:
+        import torch.distributed as dist
+        box = [Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)  # bootstrap only: the solve's collectives are libpj's RCCL calls
+        comm = Comm.for_rank(ctx, world, rank, box[0])
+    else:
+        comm = Comm.for_rank(ctx, 1, 0)
     build_s = time.perf_counter() - t0
     rng = np.random.default_rng(args.seed + 7)
     roots = []
     for c in rng.integers(0, 1 << args.part_scale, 64):  # same candidates on every rank
-        st = bfs.solve(int(c))  # untimed: keep roots in the giant component (degree >= 1)
+        st = ops.bfs(comm, int(c))  # untimed: keep roots in the giant component (degree >= 1)
         if st["reached"] > 1:
             roots.append((int(c), dict(st)))
         if len(roots) == nroots:
@@ -163,7 +170,7 @@ def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
     barrier()
     t = time.perf_counter()
     for r, _ in roots:
-        bfs.solve(r)
+        ops.bfs(comm, r)
     barrier()
     elapsed = time.perf_counter() - t
     m = float(sum(st["reached_edges"] for _, st in roots))
@@ -171,8 +178,9 @@ def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
                   for _, st in roots))
     st0 = roots[0][1]
     res = dict(elapsed=elapsed, m=m, b=b, n=ops.n, nnz_local=ops.nnz_local, build_s=build_s, roots=len(roots),
-               st0=st0)
+               st0=st0, transport=comm.kind)
     ops.close()
+    comm.close()
     return res
 
 
@@ -331,14 +339,14 @@ def main():
         }
         if ms["cpu"]:
             secondary["ms1024"]["cpu_baseline"] = ms["cpu"]
-    if not args.no_partitioned and not args.scale:
+    if not args.no_partitioned and not args.scale and (world == 1 or backend == "nccl"):
+        # (a gloo rehearsal shares one GPU between ranks; RCCL needs a GPU per rank)
         pr = run_partitioned(ctx, args, rank, world, barrier)
         el, _ = max_sum(pr["elapsed"], 0.0)
         per = el / pr["roots"]
         secondary["k28_partitioned"] = {
             "workload": f"graph500-kronecker-s{args.part_scale}-ef{args.edgefactor}-unit-bfs, 1D vertex "
-                        f"partition over {world} GPU(s)" + ((" (RCCL all_to_all / all_gather / all_reduce)" if backend == "nccl" else
-                                                            f" ({backend}, rehearsal)") if world > 1 else ""),
+                        f"partition over {world} GPU(s), libpj level loop, transport {pr['transport']}",
             "n_vertices": pr["n"], "nnz": 2 * (args.edgefactor << args.part_scale),
             "nnz_local_rank0": pr["nnz_local"], "roots": pr["roots"],
             "time_to_solution_ms": round(1000.0 * per, 3),

@@ -187,10 +187,10 @@ int pj_set_stream(pj_ctx* ctx, void* stream);
  * keeps the out-rows (and, for non-symmetric graphs, the in-rows) of the
  * vertex block [lo, hi), lo = r * block, block = ceil(N / world) rounded up
  * to a multiple of 64 (so ranks never share a 64-bit visited word). Column
- * ids stay global. The level loop and the exchange are driven by the caller
- * (paralleljohnson_amd/partition.py, torch.distributed over RCCL), which
- * replaces the reference's per-round MPI_Alltoall(v) and MPI_Allreduce
- * (:522-554, :589-590):
+ * ids stay global. The level loop and the exchange run inside libpj
+ * (pj_part_bfs over a pj_comm, below), replacing the reference's per-round
+ * MPI_Alltoall(v) and MPI_Allreduce (:522-554, :589-590); the steps are also
+ * exported one by one, and pj_part_bfs runs exactly this sequence:
  *
  *   stats = pj_part_begin(source)                     (level 0 = {source})
  *   while sum_ranks(stats.n_f) > 0:
@@ -260,9 +260,9 @@ const int32_t* pj_part_dist_device(pj_part* p);
  * Same block geometry as pj_part_*. Rank r keeps the weighted out-rows of its
  * block, cut from a weighted graph loaded on its GPU (the reference's rank 0
  * builds the whole CSR and scatters row blocks, :344-410; here every rank cuts
- * its own block, nothing is scattered). The band loop runs in the caller
- * (paralleljohnson_amd/partition.py PartitionedDelta), the analogue of the
- * reference's round loop :488-594 with bands of width delta:
+ * its own block, nothing is scattered). The band loop runs in libpj
+ * (pj_wpart_delta, below), the analogue of the reference's round loop
+ * :488-594 with bands of width delta; the steps it runs:
  *
  *   delta = pj_wpart_begin(source, delta or 0 for the default)
  *   lo = 0
@@ -280,7 +280,9 @@ const int32_t* pj_part_dist_device(pj_part* p);
  * follow the R9 contract with the graph's integer weights. */
 typedef struct pj_wpart pj_wpart;
 /* The rank's block of a weighted graph (pj_load_coo / pj_load_snap(weighted) /
- * pj_generate_kronecker(weighted)); the graph may be destroyed afterwards. */
+ * pj_generate_kronecker(weighted)); the graph may be destroyed afterwards.
+ * Memory: the whole graph is resident on the rank's GPU while the block is cut
+ * (the unit-weight pj_part_load_* keep only the rank's rows while building). */
 int pj_wpart_from_graph(pj_graph* g, int rank, int world, pj_wpart** out);
 int pj_wpart_destroy(pj_wpart* p);
 /* out[8] = (n, lo, hi, block, nnz_local, world, rank, nnz of the whole graph) */
@@ -304,6 +306,114 @@ int pj_wpart_end_round(pj_wpart* p, int64_t* n_f);
 int pj_wpart_reach(pj_wpart* p, int64_t* out);
 /* The owned block's distances (hi - lo int32) to the host. */
 int pj_wpart_copy_dist(pj_wpart* p, int32_t* dist_out);
+
+/* ---- multi-GPU transport and partitioned solves ------------
+ *
+ * A pj_comm is one rank's endpoint of a group: the replacement for the
+ * reference's MPI_COMM_WORLD (MPI_Init :679, MPI_Comm_size/rank :291-292) and
+ * its collectives. Kinds:
+ *  - RCCL, one process per GPU: rank 0 makes an id with pj_comm_unique_id and
+ *    the launcher hands it to every rank (pj_comm_create_rank);
+ *  - a group in one process, one pj_ctx (and one host thread) per rank
+ *    (pj_comm_create_group): PJ_TRANSPORT_RCCL (ncclCommInitAll, one GPU per
+ *    rank) or PJ_TRANSPORT_HOST (device copies between the ranks' buffers; ranks
+ *    may share a GPU -- the "fake cluster" of SURVEY.md §4.3);
+ *  - caller callbacks (pj_comm_create_callbacks), e.g. an MPI program's own
+ *    MPI_Allreduce / MPI_Alltoall(v) / MPI_Allgather.
+ * Every rank of a group must make the same pj_* calls in the same order. */
+typedef struct pj_comm pj_comm;
+
+enum pj_transport { PJ_TRANSPORT_AUTO = 0, PJ_TRANSPORT_RCCL = 1, PJ_TRANSPORT_HOST = 2 };
+
+int pj_comm_unique_id(uint8_t id[128]);
+/* id may be NULL only for world == 1 (a one-rank transport without RCCL). */
+int pj_comm_create_rank(pj_ctx* ctx, int world, int rank, const uint8_t id[128], pj_comm** out);
+/* out[r] is rank r's endpoint, bound to ctxs[r]; AUTO = RCCL when world > 1 and
+ * every ctx has its own GPU, else HOST (a single rank: no transport at all). */
+int pj_comm_create_group(pj_ctx* const* ctxs, int world, int transport, pj_comm** out);
+
+typedef struct pj_comm_callbacks {
+    void* user;
+    int rank, world;
+    /* each returns 0 on success; vals / counts are host arrays, the buffers are
+     * whatever the steps expose (device memory for libpj's own partitions) */
+    int (*allreduce)(void* user, int64_t* vals, int k, int is_min);      /* in place, sum or min */
+    int (*alltoall_counts)(void* user, const int64_t* send, int64_t* recv); /* world counts each */
+    int (*alltoallv)(void* user, const void* send, const int64_t* scounts, void* recv, const int64_t* rcounts,
+                     int64_t elem_bytes); /* owner-major segments */
+    int (*allgather)(void* user, const void* own, void* all, int64_t bytes); /* all[r*bytes] = rank r's own */
+} pj_comm_callbacks;
+int pj_comm_create_callbacks(const pj_comm_callbacks* cb, pj_comm** out);
+/* kind: "self", "rccl", "host" or "callbacks" */
+int pj_comm_info(const pj_comm* c, int* rank, int* world, const char** kind);
+int pj_comm_destroy(pj_comm* c);
+
+/* Statistics of one rank's partitioned solve. reached / reached_edges are for
+ * the whole graph (summed over the ranks). */
+typedef struct pj_part_stats {
+    double solve_ms;      /* host wall time of the solve on this rank, device work included
+                             (the reference's timed region :459-462 ... :597-605) */
+    int64_t levels;       /* BFS levels, or delta-stepping bands */
+    int64_t td_levels, bu_levels;
+    int64_t bands, rounds; /* delta-stepping: non-empty bands, light rounds */
+    int64_t reached, reached_edges;
+    int64_t sent;         /* ids (BFS) or (id, dist) pairs (delta) this rank sent */
+    int32_t delta, reserved;
+} pj_part_stats;
+
+/* The partitioned BFS of this rank (part.hip + the level loop of engine.cpp,
+ * the analogue of :488-594): every rank of comm calls it with the same source.
+ * pj_part_set_option keys: "alpha", "beta" (Beamer), "direction" (0 auto,
+ * 1 push, 2 pull). */
+int pj_part_bfs(pj_part* p, pj_comm* comm, int64_t source, pj_part_stats* st);
+int pj_part_set_option(pj_part* p, const char* key, double value);
+/* All ranks of a one-process group at once (one host thread per rank);
+ * st[world] may be NULL. */
+int pj_part_bfs_group(int world, pj_part* const* parts, pj_comm* const* comms, int64_t source, pj_part_stats* st);
+/* The whole distance vector (n int32) on this rank (dist_out may be NULL on
+ * ranks that do not need it; every rank must call): the MPI_Gatherv of :612-614. */
+int pj_part_gather_dist(pj_part* p, pj_comm* comm, int32_t* dist_out);
+
+/* Weighted partitioned solve (delta-stepping, wpart.hip + engine.cpp);
+ * delta <= 0 picks the single-GPU default. */
+int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st);
+int pj_wpart_delta_group(int world, pj_wpart* const* parts, pj_comm* const* comms, int64_t source, int32_t delta,
+                         pj_part_stats* st);
+int pj_wpart_gather_dist(pj_wpart* p, pj_comm* comm, int32_t* dist_out);
+
+/* The same loops over caller-supplied steps (tests, other backends): the
+ * callbacks have the semantics of pj_part_* / pj_wpart_* above, and the
+ * buffers (replicated vis / iso: world * words_per_rank u64; zown:
+ * words_per_rank u64; send / recv: world * block u32, or u64 for delta) are
+ * handed to the transport as they are. */
+typedef struct pj_bfs_steps {
+    void* user;
+    int64_t n, nnz_local, words_per_rank, block;
+    int32_t rank, world;
+    void *vis, *iso, *zown, *send, *recv;
+    int (*zmask)(void* user);                                   /* own isolated words -> zown */
+    int (*begin)(void* user, int64_t source, int64_t* st3);
+    int (*push)(void* user, int level, int64_t* counts);        /* fills send, counts[world] */
+    int (*apply)(void* user, int level, int64_t n_recv);        /* reads recv */
+    int (*pull)(void* user, int level);
+    int (*end_level)(void* user, int64_t* st3);
+} pj_bfs_steps;
+int pj_engine_bfs(const pj_bfs_steps* steps, pj_comm* comm, int64_t source, double alpha, double beta, int force,
+                  pj_part_stats* st);
+
+typedef struct pj_delta_steps {
+    void* user;
+    int64_t n;
+    int32_t rank, world;
+    void *send, *recv;
+    int (*begin)(void* user, int64_t source, int32_t delta, int32_t* delta_out);
+    int (*select)(void* user, int32_t lo, int32_t hi, int64_t* out2);
+    int (*relax)(void* user, int light, int32_t lo, int32_t hi, int64_t* counts);
+    int (*apply)(void* user, int64_t n_recv, int light, int32_t lo, int32_t hi);
+    int (*end_round)(void* user, int64_t* n_f);
+    int (*reach)(void* user, int64_t* out2);
+} pj_delta_steps;
+int pj_engine_delta(const pj_delta_steps* steps, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st);
 
 /* ---- output (replaces output_vector :32-46 + the write at :615-620) ------ */
 

@@ -122,6 +122,22 @@ _SIGS = {
     "pj_wpart_end_round": ([_P, _P], _INT),
     "pj_wpart_reach": ([_P, _P], _INT),
     "pj_wpart_copy_dist": ([_P, _P], _INT),
+    # transport and partitioned solves (partition.py wraps them)
+    "pj_comm_unique_id": ([_P], _INT),
+    "pj_comm_create_rank": ([_P, _INT, _INT, _P, _PP], _INT),
+    "pj_comm_create_group": ([_P, _INT, _INT, _P], _INT),
+    "pj_comm_create_callbacks": ([_P, _PP], _INT),
+    "pj_comm_info": ([_P, _P, _P, _P], _INT),
+    "pj_comm_destroy": ([_P], _INT),
+    "pj_part_bfs": ([_P, _P, _I64, _P], _INT),
+    "pj_part_set_option": ([_P, ctypes.c_char_p, ctypes.c_double], _INT),
+    "pj_part_bfs_group": ([_INT, _P, _P, _I64, _P], _INT),
+    "pj_part_gather_dist": ([_P, _P, _P], _INT),
+    "pj_wpart_delta": ([_P, _P, _I64, ctypes.c_int32, _P], _INT),
+    "pj_wpart_delta_group": ([_INT, _P, _P, _I64, ctypes.c_int32, _P], _INT),
+    "pj_wpart_gather_dist": ([_P, _P, _P], _INT),
+    "pj_engine_bfs": ([_P, _P, _I64, ctypes.c_double, ctypes.c_double, _INT, _P], _INT),
+    "pj_engine_delta": ([_P, _P, _I64, ctypes.c_int32, _P], _INT),
 }
 for _name, (_args, _res) in _SIGS.items():
     _fn = getattr(_lib, _name)

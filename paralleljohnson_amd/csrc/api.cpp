@@ -10,6 +10,7 @@
 
 #include <sys/stat.h>
 
+#include "engine.h"
 #include "internal.h"
 
 namespace pj {
@@ -1072,5 +1073,259 @@ int pj_part_copy_dist(pj_part* p, int32_t* dist_out) {
 }
 
 const int32_t* pj_part_dist_device(pj_part* p) { return p ? part_dist_device(*reinterpret_cast<Part*>(p)) : nullptr; }
+
+}  // extern "C"
+
+// ---- transport and partitioned solves (comm.cpp, engine.cpp) ---------------
+
+struct pj_comm {
+    std::unique_ptr<pj::Comm> c;
+};
+
+namespace {
+
+struct CallbackBfsSteps final : BfsSteps {
+    pj_bfs_steps cb;
+    explicit CallbackBfsSteps(const pj_bfs_steps& s) : cb(s) {
+        n = s.n;
+        nnz_local = s.nnz_local;
+        bw = s.words_per_rank;
+        block = s.block;
+        rank = s.rank;
+        world = s.world;
+        vis = s.vis;
+        iso = s.iso;
+        zown = s.zown;
+        send = s.send;
+        recv = s.recv;
+    }
+    static void ok(int rc, const char* what) {
+        if (rc != 0) throw Error(PJ_ERR_STATE, std::string("step callback ") + what + " failed");
+    }
+    void zmask() override { ok(cb.zmask(cb.user), "zmask"); }
+    void begin(i64 source, i64* st3) override { ok(cb.begin(cb.user, source, st3), "begin"); }
+    void push(int level, i64* counts) override { ok(cb.push(cb.user, level, counts), "push"); }
+    void apply(int level, i64 nr) override { ok(cb.apply(cb.user, level, nr), "apply"); }
+    void pull(int level) override { ok(cb.pull(cb.user, level), "pull"); }
+    void end_level(i64* st3) override { ok(cb.end_level(cb.user, st3), "end_level"); }
+};
+
+struct CallbackDeltaSteps final : DeltaSteps {
+    pj_delta_steps cb;
+    explicit CallbackDeltaSteps(const pj_delta_steps& s) : cb(s) {
+        n = s.n;
+        rank = s.rank;
+        world = s.world;
+        send = s.send;
+        recv = s.recv;
+    }
+    static void ok(int rc, const char* what) {
+        if (rc != 0) throw Error(PJ_ERR_STATE, std::string("step callback ") + what + " failed");
+    }
+    int32_t begin(i64 source, int32_t delta) override {
+        int32_t d = 0;
+        ok(cb.begin(cb.user, source, delta, &d), "begin");
+        return d;
+    }
+    void select(int32_t lo, int32_t hi, i64* out2) override { ok(cb.select(cb.user, lo, hi, out2), "select"); }
+    void relax(int light, int32_t lo, int32_t hi, i64* counts) override {
+        ok(cb.relax(cb.user, light, lo, hi, counts), "relax");
+    }
+    void apply(i64 nr, int light, int32_t lo, int32_t hi) override { ok(cb.apply(cb.user, nr, light, lo, hi), "apply"); }
+    i64 end_round() override {
+        int64_t nf = 0;
+        ok(cb.end_round(cb.user, &nf), "end_round");
+        return nf;
+    }
+    void reach(i64* out2) override { ok(cb.reach(cb.user, out2), "reach"); }
+};
+
+// Run fn(r) on one host thread per rank; the first failure's status and message win.
+template <typename F>
+int run_group(int world, F&& fn) {
+    std::vector<int> rcs((size_t)world, PJ_OK);
+    std::vector<std::string> msgs((size_t)world);
+    std::vector<std::thread> th;
+    for (int r = 0; r < world; ++r)
+        th.emplace_back([&, r] {
+            rcs[(size_t)r] = guarded([&] { return fn(r); });
+            if (rcs[(size_t)r] != PJ_OK) msgs[(size_t)r] = pj_last_error();
+        });
+    for (auto& t : th) t.join();
+    // report the root cause, not a peer's "a peer rank failed"
+    int first = -1;
+    for (int r = 0; r < world; ++r)
+        if (rcs[(size_t)r] != PJ_OK && (first < 0 || (rcs[(size_t)first] == PJ_ERR_COMM && rcs[(size_t)r] != PJ_ERR_COMM)))
+            first = r;
+    if (first < 0) return PJ_OK;
+    set_error("rank " + std::to_string(first) + ": " + msgs[(size_t)first]);
+    return rcs[(size_t)first];
+}
+
+}  // namespace
+
+extern "C" {
+
+int pj_comm_unique_id(uint8_t id[128]) {
+    if (!id) return arg_error("pj_comm_unique_id: id is NULL");
+    return guarded([&] {
+        rccl_unique_id(id);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_comm_create_rank(pj_ctx* ctx, int world, int rank, const uint8_t id[128], pj_comm** out) {
+    if (!ctx || !out || world < 1 || rank < 0 || rank >= world || (world > 1 && !id))
+        return arg_error("pj_comm_create_rank: bad argument");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        auto c = std::make_unique<pj_comm>();
+        // world 1 with an id is a one-rank RCCL group (exercises the RCCL calls)
+        c->c = (world == 1 && !id) ? make_self_comm() : make_rccl_rank(ctx->c.device, world, rank, id);
+        *out = c.release();
+        return (int)PJ_OK;
+    });
+}
+
+int pj_comm_create_group(pj_ctx* const* ctxs, int world, int transport, pj_comm** out) {
+    if (!ctxs || !out || world < 1 || world > 64 || transport < 0 || transport > 2)
+        return arg_error("pj_comm_create_group: bad argument");
+    for (int r = 0; r < world; ++r) {
+        if (!ctxs[r]) return arg_error("pj_comm_create_group: a ctx is NULL");
+        out[r] = nullptr;
+    }
+    return guarded([&] {
+        std::vector<int> dev;
+        for (int r = 0; r < world; ++r) dev.push_back(ctxs[r]->c.device);
+        std::vector<int> sorted = dev;
+        std::sort(sorted.begin(), sorted.end());
+        const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+        std::vector<std::unique_ptr<Comm>> cs;
+        if (transport == PJ_TRANSPORT_RCCL || (transport == PJ_TRANSPORT_AUTO && distinct && world > 1))
+            cs = make_rccl_group(dev);
+        else if (world == 1) cs.push_back(make_self_comm());
+        else cs = make_thread_comms(world, dev);
+        for (int r = 0; r < world; ++r) {
+            auto c = std::make_unique<pj_comm>();
+            c->c = std::move(cs[(size_t)r]);
+            out[r] = c.release();
+        }
+        return (int)PJ_OK;
+    });
+}
+
+int pj_comm_create_callbacks(const pj_comm_callbacks* cb, pj_comm** out) {
+    if (!cb || !out) return arg_error("pj_comm_create_callbacks: bad argument");
+    *out = nullptr;
+    return guarded([&] {
+        auto c = std::make_unique<pj_comm>();
+        c->c = make_callback_comm(*cb);
+        *out = c.release();
+        return (int)PJ_OK;
+    });
+}
+
+int pj_comm_info(const pj_comm* c, int* rank, int* world, const char** kind) {
+    if (!c) return arg_error("pj_comm_info: comm is NULL");
+    if (rank) *rank = c->c->rank;
+    if (world) *world = c->c->world;
+    if (kind) *kind = c->c->kind();
+    return PJ_OK;
+}
+
+int pj_comm_destroy(pj_comm* c) {
+    if (!c) return PJ_OK;
+    return guarded([&] {
+        delete c;
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_set_option(pj_part* p, const char* key, double value) {
+    if (!p || !key) return arg_error("pj_part_set_option: bad argument");
+    BfsParams& prm = part_params(*reinterpret_cast<Part*>(p));
+    const std::string k(key);
+    if (k == "alpha" && value > 0) prm.alpha = value;
+    else if (k == "beta" && value > 0) prm.beta = value;
+    else if (k == "direction" && (value == 0 || value == 1 || value == 2)) prm.force = (int)value;
+    else return arg_error("pj_part_set_option: unknown key or bad value");
+    return PJ_OK;
+}
+
+int pj_part_bfs(pj_part* p, pj_comm* comm, int64_t source, pj_part_stats* st) {
+    if (!p || !comm) return arg_error("pj_part_bfs: bad argument");
+    return guarded([&] {
+        Part& P = *reinterpret_cast<Part*>(p);
+        BfsSteps& S = part_steps(P);
+        bool& iso = part_iso_ready(P, comm->c.get());
+        bfs_engine(S, *comm->c, source, part_params(P), iso, st);
+        iso = true;
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_bfs_group(int world, pj_part* const* parts, pj_comm* const* comms, int64_t source, pj_part_stats* st) {
+    if (world < 1 || !parts || !comms) return arg_error("pj_part_bfs_group: bad argument");
+    return run_group(world, [&](int r) { return pj_part_bfs(parts[r], comms[r], source, st ? st + r : nullptr); });
+}
+
+int pj_part_gather_dist(pj_part* p, pj_comm* comm, int32_t* dist_out) {
+    if (!p || !comm) return arg_error("pj_part_gather_dist: bad argument");
+    return guarded([&] {
+        part_gather_dist(*reinterpret_cast<Part*>(p), *comm->c, dist_out);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st) {
+    if (!p || !comm) return arg_error("pj_wpart_delta: bad argument");
+    return guarded([&] {
+        delta_engine(wpart_steps(*reinterpret_cast<WPart*>(p)), *comm->c, source, delta, st);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_delta_group(int world, pj_wpart* const* parts, pj_comm* const* comms, int64_t source, int32_t delta,
+                         pj_part_stats* st) {
+    if (world < 1 || !parts || !comms) return arg_error("pj_wpart_delta_group: bad argument");
+    return run_group(world,
+                     [&](int r) { return pj_wpart_delta(parts[r], comms[r], source, delta, st ? st + r : nullptr); });
+}
+
+int pj_wpart_gather_dist(pj_wpart* p, pj_comm* comm, int32_t* dist_out) {
+    if (!p || !comm) return arg_error("pj_wpart_gather_dist: bad argument");
+    return guarded([&] {
+        wpart_gather_dist(*reinterpret_cast<WPart*>(p), *comm->c, dist_out);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_engine_bfs(const pj_bfs_steps* steps, pj_comm* comm, int64_t source, double alpha, double beta, int force,
+                  pj_part_stats* st) {
+    if (!steps || !comm || !steps->zmask || !steps->begin || !steps->push || !steps->apply || !steps->pull ||
+        !steps->end_level || alpha <= 0 || beta <= 0 || force < 0 || force > 2)
+        return arg_error("pj_engine_bfs: bad argument");
+    return guarded([&] {
+        CallbackBfsSteps S(*steps);
+        BfsParams prm;
+        prm.alpha = alpha;
+        prm.beta = beta;
+        prm.force = force;
+        bfs_engine(S, *comm->c, source, prm, false, st);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_engine_delta(const pj_delta_steps* steps, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st) {
+    if (!steps || !comm || !steps->begin || !steps->select || !steps->relax || !steps->apply || !steps->end_round ||
+        !steps->reach)
+        return arg_error("pj_engine_delta: bad argument");
+    return guarded([&] {
+        CallbackDeltaSteps S(*steps);
+        delta_engine(S, *comm->c, source, delta, st);
+        return (int)PJ_OK;
+    });
+}
 
 }  // extern "C"

@@ -1,32 +1,41 @@
-// cli.cpp — `parallel_johnson webfile source_node sol_file`, the drop-in for
-// the reference's process boundary (README:9; parallel_johnson() :286-676,
-// main :678-684). Same arguments, same stderr progress lines, same stdout
-// `Time:` line and the same sol_file bytes; the work runs on the GPU through
-// libpj (include/pj.h).
+// cli.cpp — `[mpirun -np P] parallel_johnson webfile source_node sol_file`, the
+// drop-in for the reference's process boundary (README:9; parallel_johnson()
+// :286-676, main :678-684). Same arguments, same stderr progress lines, same
+// stdout `Time:` line and the same sol_file bytes; the work runs on the GPU
+// through libpj (include/pj.h).
 //
 // Differences that are not parity targets: lines the
 // reference reads as undefined behaviour are rejected with a message and exit
 // status 255 (the reference's error status, :35/:82/:302).
 //
-// Environment: PJ_DEVICE (HIP ordinal, default 0 or LOCAL_RANK), PJ_WEIGHTED=1
-// (third column = weight, delta-stepping), PJ_CSR_CACHE (binary CSR cache: "1"
-// for <webfile>.pjcsr, or a path; loaded instead of parsing when its stamp --
-// the text's size and mtime -- and weight mode match, else written after the
-// parse). Under an MPI-style launcher only rank 0 works; the other ranks exit 0.
+// Processes: P = PJ_GPUS, else the launcher's world size (OMPI_COMM_WORLD_SIZE,
+// PMI_SIZE, PMIX_SIZE), else 1. Under a launcher only rank 0 works (the other
+// ranks exit 0): it runs the P ranks of the 1D vertex partition itself, one
+// host thread and one pj_ctx each, rank r on GPU r mod (visible GPUs), over
+// RCCL when every rank has its own GPU and over device copies otherwise
+// (PJ_TRANSPORT=rccl|host overrides). P = 1 runs the single-GPU solver. The
+// `Time:` line reports P, as the reference does (:603-604).
+//
+// Environment: PJ_DEVICE (HIP ordinal for P = 1, default 0 or LOCAL_RANK),
+// PJ_WEIGHTED=1 (third column = weight, delta-stepping), PJ_CSR_CACHE (binary
+// CSR cache: "1" for <webfile>.pjcsr, or a path; loaded instead of parsing when
+// its stamp -- the text's size and mtime -- and weight mode match, else written
+// after the parse; P = 1 only), PJ_PHASES=1 (phase times on stderr).
 //
 // Multi-source (Johnson-style rows; no reference counterpart, the reference
 // takes one source per run, :448): PJ_SOURCES = a list of sources separated by
 // commas or blanks, or "@file" with one source per line (each read with atoi,
 // like argv[2]). argv[2] is then ignored and argv[3] is a pattern: "{s}" is
 // replaced by the source, "{i}" by its index (no token: argv[3].<source>). Each
-// file is byte-identical to a single-source run. With PJ_GPUS = P > 1 the
-// sources are sharded over P GPUs (source r, r+P, ... on GPU r), each holding a
-// copy of the graph.
+// file is byte-identical to a single-source run. With P > 1 the sources are
+// sharded over P GPUs (source i on GPU i mod P), each holding a copy of the
+// graph.
 #include <sys/stat.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <iostream>
 #include <sstream>
@@ -43,13 +52,41 @@ int env_int(const char* name, int dflt) {
     return v && *v ? std::atoi(v) : dflt;
 }
 
-int launcher_rank() {
-    for (const char* k : {"OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK", "RANK"}) {
+int launcher_value(std::initializer_list<const char*> keys, int dflt) {
+    for (const char* k : keys) {
         const char* v = std::getenv(k);
         if (v && *v) return std::atoi(v);
     }
-    return 0;
+    return dflt;
 }
+
+int launcher_rank() { return launcher_value({"OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK"}, 0); }
+
+int process_count() {
+    const int p = env_int("PJ_GPUS", 0);
+    if (p > 0) return p;
+    return std::max(1, launcher_value({"OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "PMIX_SIZE"}, 1));
+}
+
+int device_count() {
+    int n = 0;
+    pj_device_count(&n);
+    return n;
+}
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Phases {
+    bool on = env_int("PJ_PHASES", 0) != 0;
+    double t = now_s();
+    void mark(const char* name) {
+        const double u = now_s();
+        if (on) std::cerr << "phase " << name << ": " << (u - t) << " s" << std::endl;
+        t = u;
+    }
+};
 
 // The graph of `path`: from the binary CSR cache when PJ_CSR_CACHE names a fresh one,
 // else parsed (pj_load_snap) and, with PJ_CSR_CACHE set, cached for the next run.
@@ -73,23 +110,33 @@ int load_graph(pj_ctx* ctx, const char* path, int weighted, pj_graph** g) {
     return rc;
 }
 
-// print_msg :49-53
-void print_msg(const std::string& msg, int rank) {
-    if (rank == 0) std::cerr << msg << std::endl;
-}
+// print_msg :49-53 (rank 0 only; only rank 0 gets this far)
+void print_msg(const std::string& msg) { std::cerr << msg << std::endl; }
 
-[[noreturn]] void fail(const char* what, int rc) {
-    std::cerr << what << " failed (" << rc << "): " << pj_last_error() << std::endl;
+[[noreturn]] void fail(const std::string& what, int rc, const std::string& msg) {
+    std::cerr << what << " failed (" << rc << "): " << msg << std::endl;
     std::exit(-1);
 }
+[[noreturn]] void fail(const char* what, int rc) { fail(what, rc, pj_last_error()); }
 
-int device_count() {
-    static int n = -1;
-    if (n < 0) {
-        n = 0;
-        pj_device_count(&n);
-    }
-    return n;
+// fn(r) on one thread per rank; exits on the first failure (the root cause, not a peer's)
+template <typename F>
+void per_rank(int P, const char* what, F&& fn) {
+    std::vector<int> rcs((size_t)P, PJ_OK);
+    std::vector<std::string> msgs((size_t)P);
+    std::vector<std::thread> th;
+    for (int r = 0; r < P; ++r)
+        th.emplace_back([&, r] {
+            rcs[(size_t)r] = fn(r);
+            if (rcs[(size_t)r] != PJ_OK) msgs[(size_t)r] = pj_last_error();
+        });
+    for (auto& t : th) t.join();
+    for (int r = 0; r < P; ++r)
+        if (rcs[(size_t)r] != PJ_OK && rcs[(size_t)r] != PJ_ERR_COMM)
+            fail(std::string(what) + " (rank " + std::to_string(r) + ")", rcs[(size_t)r], msgs[(size_t)r]);
+    for (int r = 0; r < P; ++r)
+        if (rcs[(size_t)r] != PJ_OK)
+            fail(std::string(what) + " (rank " + std::to_string(r) + ")", rcs[(size_t)r], msgs[(size_t)r]);
 }
 
 // PJ_SOURCES: "a,b c" or "@file" (one per line); every token read with atoi (:448)
@@ -139,53 +186,161 @@ std::string sol_path(const std::string& pat, int64_t src, size_t idx) {
     return out;
 }
 
+std::vector<pj_ctx*> make_ctxs(int P) {
+    const int ndev = std::max(1, device_count());
+    std::vector<pj_ctx*> ctxs((size_t)P, nullptr);
+    for (int r = 0; r < P; ++r) {
+        const int rc = pj_create(r % ndev, &ctxs[(size_t)r]);
+        if (rc != PJ_OK) fail("pj_create", rc);
+    }
+    return ctxs;
+}
+
 // Source-sharded multi-source run: GPU r solves sources r, r+P, ... and writes their files.
-int run_multi_source(const char* webfile, const std::vector<int64_t>& sources, const char* pattern, int gpus,
+int run_multi_source(const char* webfile, const std::vector<int64_t>& sources, const char* pattern, int P,
                      int weighted) {
-    std::cerr << "compute shortest paths from " << sources.size() << " source nodes on " << gpus << " GPU(s)"
-              << std::endl;
-    std::cerr << "parallel Johnson's algorithm starts......" << std::endl;
-    std::vector<double> kms((size_t)gpus, 0.0);
-    std::vector<int> rcs((size_t)gpus, PJ_OK);
-    std::vector<std::string> errs((size_t)gpus);
-    std::vector<std::thread> th;
-    int64_t n_all = 0;
-    for (int r = 0; r < gpus; ++r)
-        th.emplace_back([&, r] {
-            pj_ctx* ctx = nullptr;
-            pj_graph* g = nullptr;
-            int rc = pj_create(r % std::max(1, device_count()), &ctx);
-            if (rc == PJ_OK) rc = load_graph(ctx, webfile, weighted, &g);
-            std::vector<int64_t> mine;
-            std::vector<std::string> paths;
-            for (size_t i = (size_t)r; i < sources.size(); i += (size_t)gpus) {
-                mine.push_back(sources[i]);
-                paths.push_back(sol_path(pattern, sources[i], i));
-            }
-            std::vector<const char*> pp;
-            for (auto& q : paths) pp.push_back(q.c_str());
-            if (rc == PJ_OK && r == 0) pj_graph_info(g, &n_all, nullptr, nullptr, nullptr);
-            if (rc == PJ_OK && !mine.empty()) {
-                rc = pj_sssp_batch_write(g, mine.data(), (int)mine.size(), pp.data(), 0);
-                pj_stats st{};
-                if (rc == PJ_OK && pj_last_stats(g, &st) == PJ_OK) kms[(size_t)r] = st.kernel_ms;
-            }
-            if (rc != PJ_OK) errs[(size_t)r] = pj_last_error();
-            rcs[(size_t)r] = rc;
-            pj_graph_destroy(g);
-            pj_destroy(ctx);
-        });
-    for (auto& t : th) t.join();
-    for (int r = 0; r < gpus; ++r)
-        if (rcs[(size_t)r] != PJ_OK) {
-            std::cerr << "GPU " << r << " failed (" << rcs[(size_t)r] << "): " << errs[(size_t)r] << std::endl;
-            std::exit(-1);
+    Phases ph;
+    std::vector<pj_ctx*> ctxs = make_ctxs(P);
+    std::vector<pj_graph*> gs((size_t)P, nullptr);
+    per_rank(P, "pj_load_snap", [&](int r) { return load_graph(ctxs[(size_t)r], webfile, weighted, &gs[(size_t)r]); });
+    int64_t n = 0;
+    pj_graph_info(gs[0], &n, nullptr, nullptr, nullptr);
+    std::cerr << "N = " << n << std::endl;
+    print_msg("read in the webgraph is done.");
+    ph.mark("load");
+    std::cerr << "compute shortest paths from " << sources.size() << " source nodes" << std::endl;
+    print_msg("parallel Johnson's algorithm starts......");
+    std::vector<double> kms((size_t)P, 0.0);
+    per_rank(P, "pj_sssp_batch_write", [&](int r) {
+        std::vector<int64_t> mine;
+        std::vector<std::string> paths;
+        for (size_t i = (size_t)r; i < sources.size(); i += (size_t)P) {
+            mine.push_back(sources[i]);
+            paths.push_back(sol_path(pattern, sources[i], i));
         }
-    std::cerr << "N = " << n_all << std::endl;
-    std::cerr << "parallel Johnson's algorithm completes." << std::endl;
+        if (mine.empty()) return (int)PJ_OK;
+        std::vector<const char*> pp;
+        for (auto& q : paths) pp.push_back(q.c_str());
+        int rc = pj_sssp_batch_write(gs[(size_t)r], mine.data(), (int)mine.size(), pp.data(), 0);
+        pj_stats st{};
+        if (rc == PJ_OK && pj_last_stats(gs[(size_t)r], &st) == PJ_OK) kms[(size_t)r] = st.kernel_ms;
+        return rc;
+    });
+    ph.mark("solve+write");
+    print_msg("parallel Johnson's algorithm completes.");
     const double t = *std::max_element(kms.begin(), kms.end()) / 1000.0;
-    std::cout << "Time: " << t << " seconds when using " << gpus << " processes." << std::endl;
+    std::cout << "Time: " << t << " seconds when using " << P << " processes." << std::endl;
     std::cerr << "the shortest path distance vectors have been saved in files " << pattern << std::endl;
+    for (int r = 0; r < P; ++r) {
+        pj_graph_destroy(gs[(size_t)r]);
+        pj_destroy(ctxs[(size_t)r]);
+    }
+    return 0;
+}
+
+int transport_from_env() {
+    const char* t = std::getenv("PJ_TRANSPORT");
+    if (!t || !*t || !std::strcmp(t, "auto")) return PJ_TRANSPORT_AUTO;
+    if (!std::strcmp(t, "rccl")) return PJ_TRANSPORT_RCCL;
+    if (!std::strcmp(t, "host")) return PJ_TRANSPORT_HOST;
+    std::cerr << "PJ_TRANSPORT must be auto, rccl or host" << std::endl;
+    std::exit(-1);
+}
+
+// The 1D vertex partition over P ranks in this process (the reference's np = P run).
+int run_partitioned(const char* webfile, int source, const char* out, int P, int weighted) {
+    Phases ph;
+    std::vector<pj_ctx*> ctxs = make_ctxs(P);
+    std::vector<pj_comm*> comms((size_t)P, nullptr);
+    int rc = pj_comm_create_group(ctxs.data(), P, transport_from_env(), comms.data());
+    if (rc != PJ_OK) fail("pj_comm_create_group", rc);
+    std::vector<pj_part*> parts((size_t)P, nullptr);
+    std::vector<pj_wpart*> wparts((size_t)P, nullptr);
+    // every rank builds its own rows on its GPU: no scatter (:344-410)
+    per_rank(P, "load", [&](int r) {
+        if (!weighted) return pj_part_load_snap(ctxs[(size_t)r], webfile, r, P, &parts[(size_t)r]);
+        pj_graph* g = nullptr;
+        int rc2 = pj_load_snap(ctxs[(size_t)r], webfile, 1, &g);
+        if (rc2 == PJ_OK) rc2 = pj_wpart_from_graph(g, r, P, &wparts[(size_t)r]);
+        pj_graph_destroy(g);
+        return rc2;
+    });
+    int64_t n = 0;
+    if (weighted) {
+        int64_t info[8];
+        pj_wpart_info(wparts[0], info);
+        n = info[0];
+    } else {
+        pj_part_info pi{};
+        pj_part_info_get(parts[0], &pi);
+        n = pi.n;
+    }
+    std::cerr << "N = " << n << std::endl;  // :320
+    print_msg("read in the webgraph is done.");
+    print_msg("distribute sparse matrix is done.");
+    ph.mark("load");
+    std::cerr << "compute shortest paths from source node: " << source << std::endl;
+    print_msg("parallel Johnson's algorithm starts......");
+    std::vector<pj_part_stats> st((size_t)P);
+    rc = weighted ? pj_wpart_delta_group(P, wparts.data(), comms.data(), source, 0, st.data())
+                  : pj_part_bfs_group(P, parts.data(), comms.data(), source, st.data());
+    if (rc != PJ_OK) fail(weighted ? "pj_wpart_delta_group" : "pj_part_bfs_group", rc);
+    double t = 0;
+    for (auto& s : st) t = std::max(t, s.solve_ms / 1000.0);  // max over ranks (:597-605)
+    ph.mark("solve");
+    std::vector<int32_t> dist((size_t)n);
+    per_rank(P, "gather", [&](int r) {  // MPI_Gatherv :612-614
+        int32_t* o = r == 0 ? dist.data() : nullptr;
+        return weighted ? pj_wpart_gather_dist(wparts[(size_t)r], comms[(size_t)r], o)
+                        : pj_part_gather_dist(parts[(size_t)r], comms[(size_t)r], o);
+    });
+    print_msg("parallel Johnson's algorithm completes.");
+    std::cout << "Time: " << t << " seconds when using " << P << " processes." << std::endl;
+    rc = pj_write_sol(dist.data(), n, out, 0);  // :615-618
+    if (rc != PJ_OK) fail("pj_write_sol", rc);
+    ph.mark("gather+write");
+    std::cerr << "the shortest path distance vector has been saved in file " << out << std::endl;
+    for (int r = 0; r < P; ++r) {
+        pj_part_destroy(parts[(size_t)r]);
+        pj_wpart_destroy(wparts[(size_t)r]);
+        pj_comm_destroy(comms[(size_t)r]);
+        pj_destroy(ctxs[(size_t)r]);
+    }
+    return 0;
+}
+
+int run_single(const char* webfile, int source, const char* out, int weighted) {
+    Phases ph;
+    pj_ctx* ctx = nullptr;
+    int rc = pj_create(env_int("PJ_DEVICE", env_int("LOCAL_RANK", 0)), &ctx);
+    if (rc != PJ_OK) fail("pj_create", rc);
+    ph.mark("init");
+    pj_graph* g = nullptr;
+    rc = load_graph(ctx, webfile, weighted, &g);
+    if (rc != PJ_OK) fail("pj_load_snap", rc);
+    int64_t n = 0;
+    pj_graph_info(g, &n, nullptr, nullptr, nullptr);
+    std::cerr << "N = " << n << std::endl;  // :320
+    print_msg("read in the webgraph is done.");
+    print_msg("distribute sparse matrix is done.");
+    ph.mark("load");
+    std::cerr << "compute shortest paths from source node: " << source << std::endl;
+    print_msg("parallel Johnson's algorithm starts......");
+    std::vector<int32_t> dist((size_t)n);
+    rc = pj_sssp(g, source, dist.data());
+    if (rc != PJ_OK) fail("pj_sssp", rc);
+    pj_stats st{};
+    pj_last_stats(g, &st);
+    const double t_elapsed = st.kernel_ms / 1000.0;  // device time of the solve (:597-605 analogue)
+    ph.mark("solve");
+    print_msg("parallel Johnson's algorithm completes.");
+    std::cout << "Time: " << t_elapsed << " seconds when using " << 1 << " processes." << std::endl;
+    rc = pj_write_sol(dist.data(), n, out, 0);  // :615-618
+    if (rc != PJ_OK) fail("pj_write_sol", rc);
+    ph.mark("write");
+    std::cerr << "the shortest path distance vector has been saved in file " << out << std::endl;
+    pj_graph_destroy(g);
+    pj_destroy(ctx);
     return 0;
 }
 
@@ -205,45 +360,13 @@ int main(int argc, char* argv[]) {
         std::exit(-1);
     }
     if (rank != 0) return 0;
+    const int P = process_count();
+    const int weighted = env_int("PJ_WEIGHTED", 0);
 
+    print_msg("process 0 reads in the web graph data......");
     const char* srcs = std::getenv("PJ_SOURCES");
-    if (srcs && *srcs) {
-        print_msg("process 0 reads in the web graph data......", rank);
-        const int gpus = std::max(1, env_int("PJ_GPUS", 1));
-        return run_multi_source(argv[1], parse_sources(srcs), argv[3], gpus, env_int("PJ_WEIGHTED", 0));
-    }
-
-    print_msg("process 0 reads in the web graph data......", rank);
-    pj_ctx* ctx = nullptr;
-    int rc = pj_create(env_int("PJ_DEVICE", env_int("LOCAL_RANK", 0)), &ctx);
-    if (rc != PJ_OK) fail("pj_create", rc);
-    pj_graph* g = nullptr;
-    rc = load_graph(ctx, argv[1], env_int("PJ_WEIGHTED", 0), &g);
-    if (rc != PJ_OK) fail("pj_load_snap", rc);
-    int64_t n = 0;
-    pj_graph_info(g, &n, nullptr, nullptr, nullptr);
-    std::cerr << "N = " << n << std::endl;  // :320
-    print_msg("read in the webgraph is done.", rank);
-    print_msg("distribute sparse matrix is done.", rank);
-
+    if (srcs && *srcs) return run_multi_source(argv[1], parse_sources(srcs), argv[3], P, weighted);
     const int source_node = std::atoi(argv[2]);  // :448
-    std::cerr << "compute shortest paths from source node: " << source_node << std::endl;
-    std::cerr << "parallel Johnson's algorithm starts......" << std::endl;
-
-    std::vector<int32_t> dist((size_t)n);
-    rc = pj_sssp(g, source_node, dist.data());
-    if (rc != PJ_OK) fail("pj_sssp", rc);
-    pj_stats st{};
-    pj_last_stats(g, &st);
-    const double t_elapsed = st.kernel_ms / 1000.0;  // device time of the solve (:597-605 analogue)
-    std::cerr << "parallel Johnson's algorithm completes." << std::endl;
-    std::cout << "Time: " << t_elapsed << " seconds when using " << 1 << " processes." << std::endl;
-
-    rc = pj_write_sol(dist.data(), n, argv[3], 0);  // :615-618
-    if (rc != PJ_OK) fail("pj_write_sol", rc);
-    std::cerr << "the shortest path distance vector has been saved in file " << argv[3] << std::endl;
-
-    pj_graph_destroy(g);
-    pj_destroy(ctx);
-    return 0;
+    if (P > 1) return run_partitioned(argv[1], source_node, argv[3], P, weighted);
+    return run_single(argv[1], source_node, argv[3], weighted);
 }

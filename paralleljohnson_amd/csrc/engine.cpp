@@ -1,0 +1,195 @@
+// engine.cpp — the rank-local protocol loops of the partitioned solves: the
+// MI355X form of the reference's bulk-synchronous round loop
+// (ParallelJohnson.cpp:488-594). Every rank runs the same loop; the only
+// cross-rank traffic is the Comm calls, made in the same order on every rank.
+//
+// BFS (unit weights, the reference's w = 1, :147): one level per round. A level
+// is a push (the owned frontier expands; ids owned elsewhere are sent to their
+// owner, the Alltoall + Alltoallv of :522-554) or a pull (owned unvisited
+// vertices probe their in-neighbours in a replicated visited bitmap that is
+// all-gathered around pull levels). Beamer's rule on all-reduced counts picks
+// the direction, identically on every rank; a zero global frontier ends the
+// solve (the termination Allreduce of :579-593).
+//
+// Delta-stepping (weighted): bands [lo, lo + delta) in order; light rounds
+// until no rank has a frontier, then one heavy step; candidates for remote
+// vertices are exchanged as (id | dist << 32). An empty band jumps to the band
+// of the all-reduced minimum pending distance; INT_INF everywhere ends it.
+#include <chrono>
+#include <cstring>
+
+#include "engine.h"
+
+namespace pj {
+
+namespace {
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// When a rank fails mid-protocol, its peers would wait forever at the next
+// collective: release them (thread groups) before rethrowing.
+template <typename F>
+void guarded_loop(Comm& comm, F&& f) {
+    try {
+        f();
+    } catch (...) {
+        comm.abort();
+        throw;
+    }
+}
+
+}  // namespace
+
+// A transport other than "self" exchanges even at world 1 (nothing is sent
+// then), so a one-GPU run exercises the same collective calls as a group.
+static bool exchanges(const Comm& comm) { return comm.world > 1 || std::strcmp(comm.kind(), "self") != 0; }
+
+void bfs_engine(BfsSteps& S, Comm& comm, i64 source, const BfsParams& prm, bool iso_ready, pj_part_stats* st) {
+    if (comm.world != S.world || comm.rank != S.rank)
+        throw Error(PJ_ERR_COMM, "transport rank/world differ from the partition's");
+    guarded_loop(comm, [&] {
+        hipStream_t s = S.stream();
+        const double t0 = now_ms();
+        const size_t slice = (size_t)S.bw * sizeof(u64);
+        if (!iso_ready) {  // replicated isolated-vertex mask: one all-gather per graph and transport
+            S.zmask();
+            comm.allgather(S.zown, S.iso, slice, s);
+        }
+        i64 nnz_global = S.nnz_local;
+        comm.allreduce(&nnz_global, 1, false, s);
+        auto gather_vis = [&] {
+            if (exchanges(comm))
+                comm.allgather(static_cast<char*>(S.vis) + (size_t)S.rank * slice, S.vis, slice, s);
+        };
+        i64 f[3];
+        S.begin(source, f);
+        comm.allreduce(f, 3, false, s);
+        i64 n_f = f[0], m_f = f[1];
+        i64 n_r = n_f, m_r = m_f, m_u = nnz_global - m_f;
+        int mode = 0, level = 0;
+        i64 td = 0, bu = 0, sent = 0;
+        if (prm.force == 2) {
+            mode = 1;
+            gather_vis();
+        }
+        std::vector<i64> counts((size_t)S.world), rcounts((size_t)S.world);
+        while (n_f > 0 && level + 1 < INT_INF) {
+            const i64 prev_n_f = n_f;
+            if (mode == 0) {
+                S.push(level, counts.data());
+                i64 nr = 0;
+                if (exchanges(comm)) {
+                    comm.alltoall_counts(counts.data(), rcounts.data(), s);
+                    comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u32), s);
+                    for (int q = 0; q < S.world; ++q) {
+                        sent += counts[(size_t)q];
+                        nr += rcounts[(size_t)q];
+                    }
+                }
+                S.apply(level, nr);
+                ++td;
+            } else {
+                S.pull(level);
+                ++bu;
+            }
+            S.end_level(f);
+            comm.allreduce(f, 3, false, s);
+            n_f = f[0];
+            m_f = f[1];
+            n_r += n_f;
+            m_r += m_f;
+            m_u -= m_f;
+            // Beamer: pull when the frontier's edges exceed the unexplored edges / alpha,
+            // back to push when the frontier is small and shrinking
+            int nxt = mode;
+            if (prm.force == 1) nxt = 0;
+            else if (prm.force == 2) nxt = 1;
+            else if (mode == 0 && (double)m_f > (double)m_u / prm.alpha) nxt = 1;
+            else if (mode == 1 && (double)n_f < (double)S.n / prm.beta && n_f < prev_n_f) nxt = 0;
+            if (n_f > 0 && (nxt == 1 || mode == 1)) gather_vis();
+            mode = nxt;
+            ++level;
+        }
+        if (s) PJ_HIP(hipStreamSynchronize(s));
+        if (st) {
+            *st = pj_part_stats{};
+            st->solve_ms = now_ms() - t0;
+            st->levels = level;
+            st->td_levels = td;
+            st->bu_levels = bu;
+            st->reached = n_r;
+            st->reached_edges = m_r;
+            st->sent = sent;
+        }
+    });
+}
+
+void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_part_stats* st) {
+    if (comm.world != S.world || comm.rank != S.rank)
+        throw Error(PJ_ERR_COMM, "transport rank/world differ from the partition's");
+    guarded_loop(comm, [&] {
+        hipStream_t s = S.stream();
+        const double t0 = now_ms();
+        const int32_t delta = S.begin(source, delta_in);
+        std::vector<i64> counts((size_t)S.world), rcounts((size_t)S.world);
+        i64 sent = 0, bands = 0, rounds = 0;
+        auto exchange_apply = [&](int light, int32_t lo, int32_t hi) {
+            S.relax(light, lo, hi, counts.data());
+            i64 nr = 0;
+            if (exchanges(comm)) {
+                comm.alltoall_counts(counts.data(), rcounts.data(), s);
+                comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u64), s);
+                for (int q = 0; q < S.world; ++q) {
+                    sent += counts[(size_t)q];
+                    nr += rcounts[(size_t)q];
+                }
+            }
+            S.apply(nr, light, lo, hi);
+        };
+        i64 lo = 0;
+        while (lo < INT_INF) {
+            const i64 hi = std::min<i64>(lo + delta, INT_INF);
+            i64 sel[2];
+            S.select((int32_t)lo, (int32_t)hi, sel);
+            i64 cnt = sel[0];
+            comm.allreduce(&cnt, 1, false, s);
+            if (cnt == 0) {
+                i64 mn = sel[1];
+                comm.allreduce(&mn, 1, true, s);
+                if (mn >= INT_INF) break;
+                lo = std::max<i64>(mn / delta * delta, hi);  // the next occupied band
+                continue;
+            }
+            ++bands;
+            for (;;) {  // light rounds until no rank has a frontier
+                exchange_apply(1, (int32_t)lo, (int32_t)hi);
+                ++rounds;
+                i64 nf = S.end_round();
+                comm.allreduce(&nf, 1, false, s);
+                if (nf == 0) break;
+            }
+            exchange_apply(0, (int32_t)lo, (int32_t)hi);  // heavy edges of the band's members
+            lo = hi;
+        }
+        if (s) PJ_HIP(hipStreamSynchronize(s));
+        const double t1 = now_ms();
+        i64 rc[2];
+        S.reach(rc);
+        comm.allreduce(rc, 2, false, s);
+        if (st) {
+            *st = pj_part_stats{};
+            st->solve_ms = t1 - t0;
+            st->levels = bands;
+            st->bands = bands;
+            st->rounds = rounds;
+            st->delta = delta;
+            st->reached = rc[0];
+            st->reached_edges = rc[1];
+            st->sent = sent;
+        }
+    });
+}
+
+}  // namespace pj

@@ -1,0 +1,108 @@
+// engine.h — the multi-GPU side of libpj (not part of the ABI): the transport
+// that replaces the reference's MPI collectives, and the rank-local protocol
+// loops that replace its BSP round loop (ParallelJohnson.cpp:488-594).
+//
+// A rank runs one of the loops (bfs_engine / delta_engine) against
+//  - its device steps (BfsSteps / DeltaSteps: part.hip / wpart.hip kernels,
+//    or caller callbacks), and
+//  - a Comm: RCCL over xGMI (one process per GPU, or one process driving
+//    several GPUs from one thread each), device copies between ranks that are
+//    threads of one process ("host" transport: several ranks per GPU, the
+//    SURVEY.md §4.3 fake cluster), or caller callbacks (e.g. MPI).
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+
+#include "internal.h"
+
+namespace pj {
+
+// ------------------------------------------------------------------ Comm ---
+// Collectives of one rank. Device pointers belong to the rank's device and are
+// ordered on stream `s` (callback transports get whatever pointers the steps
+// expose). Every rank of the group must make the same calls in the same order.
+struct Comm {
+    int rank = 0, world = 1;
+    virtual ~Comm() = default;
+    virtual const char* kind() const = 0;
+    // element-wise sum (or min) of k host values over the ranks (:589-590)
+    virtual void allreduce(i64* v, int k, bool is_min, hipStream_t s) = 0;
+    // recv[q] = what rank q sends to this rank (the counts MPI_Alltoall, :522-523)
+    virtual void alltoall_counts(const i64* send, i64* recv, hipStream_t s) = 0;
+    // owner-major segments of `elem`-byte items: send[...] holds scount[q] items for
+    // rank q in rank order; recv gets rcount[q] items from q in rank order (:553-554)
+    virtual void alltoallv(const void* send, const i64* scount, void* recv, const i64* rcount, size_t elem,
+                           hipStream_t s) = 0;
+    // all[q * bytes ...] := rank q's own bytes (own may alias all + rank * bytes)
+    virtual void allgather(const void* own, void* all, size_t bytes, hipStream_t s) = 0;
+    // release a group whose peer failed (threads of one process); no-op elsewhere
+    virtual void abort() {}
+};
+
+std::unique_ptr<Comm> make_self_comm();
+// world ranks in one process, one thread per rank: device copies between the
+// ranks' buffers (any devices, several ranks per device allowed)
+std::vector<std::unique_ptr<Comm>> make_thread_comms(int world, const std::vector<int>& devices);
+// world ranks in one process over RCCL (ncclCommInitAll; distinct devices)
+std::vector<std::unique_ptr<Comm>> make_rccl_group(const std::vector<int>& devices);
+// one rank of a multi-process RCCL group (ncclCommInitRank)
+std::unique_ptr<Comm> make_rccl_rank(int device, int world, int rank, const uint8_t* uid);
+void rccl_unique_id(uint8_t* out128);
+std::unique_ptr<Comm> make_callback_comm(const pj_comm_callbacks& cb);
+
+// --------------------------------------------------------- device steps ---
+// The pj_part_* steps of one rank (include/pj.h) and the buffers they share
+// with the transport: vis / iso (world * bw u64, replicated), send / recv
+// (world * block u32), zown (bw u64).
+struct BfsSteps {
+    i64 n = 0, nnz_local = 0, bw = 1, block = 64;
+    int rank = 0, world = 1;
+    void *vis = nullptr, *iso = nullptr, *zown = nullptr, *send = nullptr, *recv = nullptr;
+    virtual ~BfsSteps() = default;
+    virtual hipStream_t stream() { return nullptr; }
+    virtual void zmask() = 0;  // own isolated-vertex words -> zown
+    virtual void begin(i64 source, i64* st3) = 0;
+    virtual void push(int level, i64* counts) = 0;
+    virtual void apply(int level, i64 n_recv) = 0;
+    virtual void pull(int level) = 0;
+    virtual void end_level(i64* st3) = 0;
+};
+
+// The pj_wpart_* steps; send / recv hold world * block u64 (id | cand << 32).
+struct DeltaSteps {
+    i64 n = 0;
+    int rank = 0, world = 1;
+    void *send = nullptr, *recv = nullptr;
+    virtual ~DeltaSteps() = default;
+    virtual hipStream_t stream() { return nullptr; }
+    virtual int32_t begin(i64 source, int32_t delta) = 0;
+    virtual void select(int32_t lo, int32_t hi, i64* out2) = 0;
+    virtual void relax(int light, int32_t lo, int32_t hi, i64* counts) = 0;
+    virtual void apply(i64 n_recv, int light, int32_t lo, int32_t hi) = 0;
+    virtual i64 end_round() = 0;
+    virtual void reach(i64* out2) = 0;
+};
+
+struct BfsParams {
+    double alpha = 14.0, beta = 24.0;
+    int force = 0;  // 0 auto, 1 push only, 2 pull from level 1 on
+};
+
+// The rank-local loops. `iso_ready` says the replicated isolated mask in
+// steps.iso is current (it is gathered once per graph and transport).
+void bfs_engine(BfsSteps& steps, Comm& comm, i64 source, const BfsParams& prm, bool iso_ready, pj_part_stats* st);
+void delta_engine(DeltaSteps& steps, Comm& comm, i64 source, int32_t delta, pj_part_stats* st);
+
+// part.hip / wpart.hip: the GPU implementations (buffers owned by the part)
+BfsSteps& part_steps(Part& p);
+DeltaSteps& wpart_steps(WPart& p);
+bool& part_iso_ready(Part& p, const Comm* comm);
+BfsParams& part_params(Part& p);
+// every rank's slice of dist, gathered (n int32 to host; NULL: gather only)
+void part_gather_dist(Part& p, Comm& comm, int32_t* out);
+void wpart_gather_dist(WPart& p, Comm& comm, int32_t* out);
+
+}  // namespace pj

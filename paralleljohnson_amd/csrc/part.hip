@@ -37,6 +37,7 @@
 //          slices before pull levels.
 #include "kron.h"
 #include "lb.h"
+#include "engine.h"
 
 namespace pj {
 
@@ -502,6 +503,10 @@ struct Part {
     ScanWs scan;
     u64 nq = 0, mq = 0;  // push queue of the current frontier (host copy from end_level)
     int32_t level = 0;
+    std::unique_ptr<BfsSteps> steps;  // engine view with its own exchange buffers (lazy)
+    const Comm* iso_comm = nullptr;   // transport the replicated isolated mask was gathered over
+    bool iso_ok = false;
+    BfsParams prm;
 };
 
 void delete_part(Part* p) { delete p; }
@@ -796,5 +801,68 @@ void part_copy_dist(Part& p, int32_t* host) {
 }
 
 const int32_t* part_dist_device(const Part& p) { return p.dist.p; }
+
+// ------------------------------------------------------------ engine view ---
+namespace {
+
+struct PartGpuSteps final : BfsSteps {
+    Part& p;
+    DevBuf<u64> vis_b, iso_b, zown_b;
+    DevBuf<u32> send_b, recv_b;
+    explicit PartGpuSteps(Part& part) : p(part) {
+        n = p.n;
+        nnz_local = p.nnz_local;
+        bw = p.bw;
+        block = p.block;
+        rank = p.rank;
+        world = p.world;
+        vis_b.alloc((size_t)world * (size_t)bw);
+        iso_b.alloc((size_t)world * (size_t)bw);
+        zown_b.alloc((size_t)bw);
+        const size_t cap = world > 1 ? (size_t)world * (size_t)block : 1;
+        send_b.alloc(cap);
+        recv_b.alloc(cap);
+        vis = vis_b.p;
+        iso = iso_b.p;
+        zown = zown_b.p;
+        send = send_b.p;
+        recv = recv_b.p;
+    }
+    hipStream_t stream() override { return p.ctx->stream; }
+    void zmask() override { part_zmask(p, zown_b.p); }
+    void begin(i64 source, i64* st3) override { part_begin(p, source, iso_b.p, vis_b.p, st3); }
+    void push(int level, i64* counts) override { part_push(p, level, vis_b.p, send_b.p, counts); }
+    void apply(int level, i64 nr) override { part_apply(p, level, vis_b.p, recv_b.p, nr); }
+    void pull(int level) override { part_pull(p, level, vis_b.p); }
+    void end_level(i64* st3) override { part_end_level(p, vis_b.p, st3); }
+};
+
+}  // namespace
+
+BfsSteps& part_steps(Part& p) {
+    if (!p.steps) p.steps.reset(new PartGpuSteps(p));
+    return *p.steps;
+}
+
+BfsParams& part_params(Part& p) { return p.prm; }
+
+bool& part_iso_ready(Part& p, const Comm* comm) {
+    if (p.iso_comm != comm) {
+        p.iso_comm = comm;
+        p.iso_ok = false;
+    }
+    return p.iso_ok;
+}
+
+void part_gather_dist(Part& p, Comm& comm, int32_t* out) {
+    hipStream_t s = p.ctx->stream;
+    // every rank contributes a block of int32 (padded with INT_INF past its last vertex)
+    DevBuf<int32_t> own((size_t)p.block), all((size_t)p.world * (size_t)p.block);
+    PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(own.p), INT_INF, (size_t)p.block, s));
+    if (p.nl) PJ_HIP(hipMemcpyAsync(own.p, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToDevice, s));
+    comm.allgather(own.p, all.p, sizeof(int32_t) * (size_t)p.block, s);
+    if (out && p.n) PJ_HIP(hipMemcpyAsync(out, all.p, sizeof(int32_t) * (size_t)p.n, hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+}
 
 }  // namespace pj

@@ -35,6 +35,7 @@
 #include <cmath>
 
 #include "lb.h"
+#include "engine.h"
 
 namespace pj {
 
@@ -373,6 +374,7 @@ struct WPart {
     DevBuf<u32> lq_v;
     DevBuf<u64> lq_b, lq_e;
     std::vector<u64> hstat;
+    std::unique_ptr<DeltaSteps> steps;  // engine view with its own exchange buffers (lazy)
     unsigned grid() const { return (unsigned)ctx->cu_count * 8u; }
     WArgs args(int32_t dlo = 0, int32_t dhi = 0) {
         WArgs a{};
@@ -590,6 +592,50 @@ void wpart_reach(WPart& p, i64* out2) {
 
 void wpart_copy_dist(WPart& p, int32_t* host) {
     if (p.nl > 0) PJ_HIP(hipMemcpy(host, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToHost));
+}
+
+// ------------------------------------------------------------ engine view ---
+namespace {
+
+struct WPartGpuSteps final : DeltaSteps {
+    WPart& p;
+    DevBuf<u64> send_b, recv_b;
+    explicit WPartGpuSteps(WPart& part) : p(part) {
+        n = p.n;
+        rank = p.rank;
+        world = p.world;
+        const size_t cap = world > 1 ? (size_t)world * (size_t)p.block : 1;
+        send_b.alloc(cap);
+        recv_b.alloc(cap);
+        send = send_b.p;
+        recv = recv_b.p;
+    }
+    hipStream_t stream() override { return p.ctx->stream; }
+    int32_t begin(i64 source, int32_t delta) override { return wpart_begin(p, source, delta); }
+    void select(int32_t lo, int32_t hi, i64* out2) override { wpart_select(p, lo, hi, out2); }
+    void relax(int light, int32_t lo, int32_t hi, i64* counts) override {
+        wpart_relax(p, light, lo, hi, send_b.p, counts);
+    }
+    void apply(i64 nr, int light, int32_t lo, int32_t hi) override { wpart_apply(p, recv_b.p, nr, light, lo, hi); }
+    i64 end_round() override { return wpart_end_round(p); }
+    void reach(i64* out2) override { wpart_reach(p, out2); }
+};
+
+}  // namespace
+
+DeltaSteps& wpart_steps(WPart& p) {
+    if (!p.steps) p.steps.reset(new WPartGpuSteps(p));
+    return *p.steps;
+}
+
+void wpart_gather_dist(WPart& p, Comm& comm, int32_t* out) {
+    hipStream_t s = p.ctx->stream;
+    DevBuf<int32_t> own((size_t)p.block), all((size_t)p.world * (size_t)p.block);
+    PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(own.p), INT_INF, (size_t)p.block, s));
+    if (p.nl) PJ_HIP(hipMemcpyAsync(own.p, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToDevice, s));
+    comm.allgather(own.p, all.p, sizeof(int32_t) * (size_t)p.block, s);
+    if (out && p.n) PJ_HIP(hipMemcpyAsync(out, all.p, sizeof(int32_t) * (size_t)p.n, hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
 }
 
 }  // namespace pj

@@ -1,44 +1,99 @@
-"""1D vertex-partitioned BFS across GPUs, one process per GPU.
+"""1D vertex-partitioned solves across GPUs: Python binding of
+libpj's pj_comm / pj_part_* / pj_wpart_* (include/pj.h).
 
 The reference distributes contiguous vertex blocks over MPI ranks (nn2rank /
 get_start_nn, ParallelJohnson.cpp:169-200; row scatter :344-410) and, every
 round, exchanges (vertex, distance) pairs with MPI_Alltoall + MPI_Alltoallv
-(:522-554) and tests termination with MPI_Allreduce (:589-590). Here:
+(:522-554) and tests termination with MPI_Allreduce (:589-590). In libpj:
 
-  * each rank holds the rows of its block on its GPU (pj_part_* in libpj);
-  * a level is a top-down (push) or bottom-up (pull) step chosen with Beamer's
-    rule from global frontier counts, identical on every rank;
-  * push levels exchange the claimed target ids with all_to_all_single (the
-    analogue of :522-554; the distance is implicit: level + 1);
-  * the per-level counts are summed with all_reduce (the analogue of :589-590);
-  * pull levels read a replicated visited bitmap, refreshed by an all-gather of
-    the owned slices (N/8 bytes in total) before and after each pull level.
+  * each rank holds the rows of its block on its GPU (pj_part_load_* /
+    pj_wpart_from_graph: no scatter);
+  * the level loop (BFS) and the band loop (delta-stepping) run in C++
+    (engine.cpp), one call per rank: pj_part_bfs / pj_wpart_delta;
+  * the collectives go through a pj_comm (Comm below): RCCL over xGMI (one
+    process per GPU, or one process driving several GPUs), device copies
+    between ranks that are threads of one process (several ranks may share a
+    GPU), or caller callbacks (any transport: the CPU tests use gloo).
 
-Collectives go through torch.distributed: backend "nccl" is RCCL over xGMI on
-MI355X. With the gloo backend (CPU tests, or several ranks sharing one GPU for
-rehearsal) device tensors are staged through host memory.
-
-The device steps are an `ops` object (DevicePart: libpj kernels on the GPU).
-There is no CPU fallback in the product path; tests substitute a numpy
-restatement of the same steps to exercise the protocol on CPU.
+There is no torch and no CPU fallback on this path; the protocol loop is the
+same C++ code whatever the transport. `engine_bfs` / `engine_delta` run that
+loop over caller-supplied device steps (the CPU tests pass a numpy
+restatement, tests/part_numpy.py).
 """
 from __future__ import annotations
 
 import ctypes
 import os
-from typing import List, Optional
+from typing import List, Optional, Sequence
 
 import numpy as np
 
-from . import INT_INF, PJError, _check, _lib, _ptr
+from . import INT_INF, PJError, _check, _lib, _ptr  # noqa: F401
 
 _I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_INT = ctypes.c_int
+_P = ctypes.c_void_p
+_PP = ctypes.POINTER(ctypes.c_void_p)
+_PI64 = ctypes.POINTER(ctypes.c_int64)
 
 
 class PartInfo(ctypes.Structure):
     _fields_ = [("n", _I64), ("lo", _I64), ("hi", _I64), ("block", _I64), ("words_per_rank", _I64),
-                ("nnz_local", _I64), ("nnz_in_local", _I64), ("rank", ctypes.c_int32),
-                ("world", ctypes.c_int32), ("symmetric", ctypes.c_int32), ("off64", ctypes.c_int32)]
+                ("nnz_local", _I64), ("nnz_in_local", _I64), ("rank", _I32),
+                ("world", _I32), ("symmetric", _I32), ("off64", _I32)]
+
+
+class PartStats(ctypes.Structure):
+    _fields_ = [("solve_ms", ctypes.c_double), ("levels", _I64), ("td_levels", _I64), ("bu_levels", _I64),
+                ("bands", _I64), ("rounds", _I64), ("reached", _I64), ("reached_edges", _I64), ("sent", _I64),
+                ("delta", _I32), ("reserved", _I32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+_CB_ALLREDUCE = ctypes.CFUNCTYPE(_INT, _P, _PI64, _INT, _INT)
+_CB_A2A_COUNTS = ctypes.CFUNCTYPE(_INT, _P, _PI64, _PI64)
+_CB_A2AV = ctypes.CFUNCTYPE(_INT, _P, _P, _PI64, _P, _PI64, _I64)
+_CB_ALLGATHER = ctypes.CFUNCTYPE(_INT, _P, _P, _P, _I64)
+
+
+class CommCallbacks(ctypes.Structure):
+    _fields_ = [("user", _P), ("rank", _INT), ("world", _INT), ("allreduce", _CB_ALLREDUCE),
+                ("alltoall_counts", _CB_A2A_COUNTS), ("alltoallv", _CB_A2AV), ("allgather", _CB_ALLGATHER)]
+
+
+_ST_ZMASK = ctypes.CFUNCTYPE(_INT, _P)
+_ST_BEGIN = ctypes.CFUNCTYPE(_INT, _P, _I64, _PI64)
+_ST_PUSH = ctypes.CFUNCTYPE(_INT, _P, _INT, _PI64)
+_ST_APPLY = ctypes.CFUNCTYPE(_INT, _P, _INT, _I64)
+_ST_PULL = ctypes.CFUNCTYPE(_INT, _P, _INT)
+_ST_END = ctypes.CFUNCTYPE(_INT, _P, _PI64)
+
+
+class BfsSteps(ctypes.Structure):
+    _fields_ = [("user", _P), ("n", _I64), ("nnz_local", _I64), ("words_per_rank", _I64), ("block", _I64),
+                ("rank", _I32), ("world", _I32), ("vis", _P), ("iso", _P), ("zown", _P), ("send", _P), ("recv", _P),
+                ("zmask", _ST_ZMASK), ("begin", _ST_BEGIN), ("push", _ST_PUSH), ("apply", _ST_APPLY),
+                ("pull", _ST_PULL), ("end_level", _ST_END)]
+
+
+_DS_BEGIN = ctypes.CFUNCTYPE(_INT, _P, _I64, _I32, ctypes.POINTER(_I32))
+_DS_SELECT = ctypes.CFUNCTYPE(_INT, _P, _I32, _I32, _PI64)
+_DS_RELAX = ctypes.CFUNCTYPE(_INT, _P, _INT, _I32, _I32, _PI64)
+_DS_APPLY = ctypes.CFUNCTYPE(_INT, _P, _I64, _INT, _I32, _I32)
+_DS_END = ctypes.CFUNCTYPE(_INT, _P, _PI64)
+_DS_REACH = ctypes.CFUNCTYPE(_INT, _P, _PI64)
+
+
+class DeltaSteps(ctypes.Structure):
+    _fields_ = [("user", _P), ("n", _I64), ("rank", _I32), ("world", _I32), ("send", _P), ("recv", _P),
+                ("begin", _DS_BEGIN), ("select", _DS_SELECT), ("relax", _DS_RELAX), ("apply", _DS_APPLY),
+                ("end_round", _DS_END), ("reach", _DS_REACH)]
+
+
+TRANSPORTS = {"auto": 0, "rccl": 1, "host": 2}
 
 
 def block_geometry(n: int, world: int):
@@ -49,71 +104,108 @@ def block_geometry(n: int, world: int):
     return block, ranges
 
 
-class Exchange:
-    """The collectives of one level (torch.distributed; `None` group = default)."""
+def _host(ptr: int, nbytes: int) -> np.ndarray:
+    """uint8 view of nbytes of host memory at ptr (callback transports and steps)."""
+    if nbytes <= 0:
+        return np.zeros(0, np.uint8)
+    return np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(ptr))
 
-    def __init__(self, group=None):
-        import torch.distributed as dist
-        self.dist = dist
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        self.stage = dist.get_backend(group) == "gloo"
 
-    def _dev(self, like):
-        return "cpu" if self.stage else like.device
+# ---------------------------------------------------------------- transport ---
 
-    def allreduce_sum(self, vals: List[int], like) -> List[int]:
-        import torch
-        t = torch.tensor(vals, dtype=torch.int64, device=self._dev(like))
-        self.dist.all_reduce(t, group=self.group)
-        return t.tolist()
+class Comm:
+    """One rank's endpoint of a pj_comm group (the reference's MPI_COMM_WORLD)."""
 
-    def allreduce_min(self, vals: List[int], like) -> List[int]:
-        import torch
-        t = torch.tensor(vals, dtype=torch.int64, device=self._dev(like))
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
-        return t.tolist()
+    def __init__(self, handle, keep=None):
+        self._h = handle
+        self._keep = keep  # callback objects that must outlive the handle
+        r, w, k = _INT(), _INT(), ctypes.c_char_p()
+        _check(_lib.pj_comm_info(self._h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(k)))
+        self.rank, self.world, self.kind = r.value, w.value, k.value.decode()
 
-    def alltoall_counts(self, counts: List[int], like) -> List[int]:
-        import torch
-        s = torch.tensor(counts, dtype=torch.int64, device=self._dev(like))
-        r = torch.empty_like(s)
-        self.dist.all_to_all_single(r, s, group=self.group)
-        return r.tolist()
+    @staticmethod
+    def unique_id() -> bytes:
+        """RCCL group id made by rank 0 and handed to every rank by the launcher."""
+        buf = (ctypes.c_uint8 * 128)()
+        _check(_lib.pj_comm_unique_id(buf))
+        return bytes(buf)
 
-    def alltoall_ids(self, send, send_counts: List[int], recv, recv_counts: List[int]):
-        ns, nr = sum(send_counts), sum(recv_counts)
-        src = send[:ns]
-        dst = recv[:nr]
-        if self.stage and send.device.type != "cpu":
-            s_cpu = src.cpu()
-            r_cpu = dst.new_empty(nr, device="cpu")
-            self.dist.all_to_all_single(r_cpu, s_cpu, output_split_sizes=recv_counts,
-                                        input_split_sizes=send_counts, group=self.group)
-            dst.copy_(r_cpu)
-        else:
-            self.dist.all_to_all_single(dst, src, output_split_sizes=recv_counts,
-                                        input_split_sizes=send_counts, group=self.group)
+    @classmethod
+    def for_rank(cls, ctx, world: int, rank: int, uid: Optional[bytes] = None) -> "Comm":
+        """This process's rank of an RCCL group (one process per GPU); world 1
+        without an id is a single-rank transport with no RCCL."""
+        h = ctypes.c_void_p()
+        idb = None if uid is None else (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        _check(_lib.pj_comm_create_rank(ctx._h, int(world), int(rank), idb, ctypes.byref(h)))
+        return cls(h)
 
-    def allgather_slices(self, out, own):
-        """out (world * w words) := concatenation of every rank's `own` (w words)."""
-        if self.stage and out.device.type != "cpu":
-            o = out.cpu()
-            self.dist.all_gather_into_tensor(o, own.cpu().clone(), group=self.group)
-            out.copy_(o)
-        else:
-            self.dist.all_gather_into_tensor(out, own.clone(), group=self.group)
+    @classmethod
+    def group(cls, ctxs: Sequence, transport: str = "auto") -> List["Comm"]:
+        """world ranks in this process, rank r bound to ctxs[r] (one host thread per rank)."""
+        world = len(ctxs)
+        arr = (ctypes.c_void_p * world)(*[c._h.value for c in ctxs])
+        out = (ctypes.c_void_p * world)()
+        _check(_lib.pj_comm_create_group(arr, world, TRANSPORTS[transport], out))
+        return [cls(ctypes.c_void_p(out[r])) for r in range(world)]
 
+    @classmethod
+    def from_callbacks(cls, transport, rank: int, world: int) -> "Comm":
+        """A transport object with allreduce(vals, is_min), alltoall_counts(send, recv),
+        alltoallv(send_ptr, scounts, recv_ptr, rcounts, elem) and
+        allgather(own_ptr, all_ptr, nbytes) (int64 arrays in place, raw pointers)."""
+        err = []
+
+        def wrap(fn):
+            def call(*a):
+                try:
+                    fn(*a)
+                    return 0
+                except BaseException as e:  # noqa: BLE001 - reported through the status
+                    err.append(e)
+                    return 1
+            return call
+
+        def allreduce(_, vals, k, is_min):
+            v = np.ctypeslib.as_array(vals, shape=(k,))
+            transport.allreduce(v, bool(is_min))
+
+        def a2a(_, send, recv):
+            transport.alltoall_counts(np.ctypeslib.as_array(send, shape=(world,)),
+                                      np.ctypeslib.as_array(recv, shape=(world,)))
+
+        def a2av(_, send, scounts, recv, rcounts, elem):
+            transport.alltoallv(send or 0, np.ctypeslib.as_array(scounts, shape=(world,)).copy(), recv or 0,
+                                np.ctypeslib.as_array(rcounts, shape=(world,)).copy(), int(elem))
+
+        def allgather(_, own, all_, nbytes):
+            transport.allgather(own or 0, all_ or 0, int(nbytes))
+
+        cb = CommCallbacks(None, int(rank), int(world), _CB_ALLREDUCE(wrap(allreduce)),
+                           _CB_A2A_COUNTS(wrap(a2a)), _CB_A2AV(wrap(a2av)), _CB_ALLGATHER(wrap(allgather)))
+        h = ctypes.c_void_p()
+        _check(_lib.pj_comm_create_callbacks(ctypes.byref(cb), ctypes.byref(h)))
+        c = cls(h, keep=(cb, transport))
+        c.errors = err
+        return c
+
+    def close(self):
+        if self._h:
+            _check(_lib.pj_comm_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------- partitions ---
 
 class DevicePart:
-    """This rank's block on its GPU: libpj's pj_part_* kernels (the product path).
-
-    Device buffers shared with the collectives are torch tensors; libpj is put
-    on torch's current stream so kernels and RCCL calls are stream-ordered."""
+    """This rank's block of a unit-weight graph on its GPU (pj_part_*)."""
 
     def __init__(self, ctx, handle):
-        import torch
         self._ctx = ctx
         self._h = handle
         info = PartInfo()
@@ -123,50 +215,22 @@ class DevicePart:
         self.rank, self.world = info.rank, info.world
         self.nnz_local, self.symmetric = info.nnz_local, bool(info.symmetric)
         self.nl = self.hi - self.lo
-        dev = torch.device("cuda", ctx.device)
-        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-        self.vis = torch.zeros(self.world * self.bw, dtype=torch.int64, device=dev)
-        self.iso = torch.zeros_like(self.vis)
-        cap = self.world * self.block if self.world > 1 else 1
-        self.send = torch.empty(cap, dtype=torch.int32, device=dev)
-        self.recv = torch.empty(cap, dtype=torch.int32, device=dev)
-        self._counts = (_I64 * max(self.world, 1))()
-        self._st = (_I64 * 3)()
 
-    # buffers ---------------------------------------------------------------
-    def own_slice(self):
-        return self.vis[self.rank * self.bw:(self.rank + 1) * self.bw]
+    def set_option(self, key: str, value: float):
+        _check(_lib.pj_part_set_option(self._h, key.encode(), float(value)))
 
-    def zmask(self):
-        import torch
-        z = torch.empty(self.bw, dtype=torch.int64, device=self.vis.device)
-        _check(_lib.pj_part_zmask(self._h, ctypes.c_void_p(z.data_ptr())))
-        return z
+    def bfs(self, comm: Comm, source: int) -> dict:
+        """pj_part_bfs: every rank of comm calls it with the same source."""
+        st = PartStats()
+        _check(_lib.pj_part_bfs(self._h, comm._h, int(source), ctypes.byref(st)))
+        return st.as_dict()
 
-    @staticmethod
-    def _p(t):
-        return ctypes.c_void_p(t.data_ptr())
+    def gather_dist(self, comm: Comm, want: bool = True) -> Optional[np.ndarray]:
+        """The whole distance vector (every rank must call; the :612-614 Gatherv)."""
+        out = np.empty(max(self.n, 1), np.int32) if want else None
+        _check(_lib.pj_part_gather_dist(self._h, comm._h, _ptr(out)))
+        return out[: self.n] if want else None
 
-    # steps -------------------------------------------------------------------
-    def begin(self, source: int):
-        _check(_lib.pj_part_begin(self._h, int(source), self._p(self.iso), self._p(self.vis), self._st))
-        return list(self._st)
-
-    def push(self, level: int) -> List[int]:
-        _check(_lib.pj_part_push(self._h, int(level), self._p(self.vis), self._p(self.send), self._counts))
-        return list(self._counts)[: self.world]
-
-    def apply(self, level: int, n_recv: int):
-        _check(_lib.pj_part_apply(self._h, int(level), self._p(self.vis), self._p(self.recv), int(n_recv)))
-
-    def pull(self, level: int):
-        _check(_lib.pj_part_pull(self._h, int(level), self._p(self.vis)))
-
-    def end_level(self):
-        _check(_lib.pj_part_end_level(self._h, self._p(self.vis), self._st))
-        return list(self._st)
-
-    # results -----------------------------------------------------------------
     def reach(self):
         out = (_I64 * 2)()
         _check(_lib.pj_part_reach(self._h, out))
@@ -214,111 +278,10 @@ def load_coo(ctx, src, dst, n: int, rank: int, world: int, symmetric: bool = Fal
     return DevicePart(ctx, h)
 
 
-class PartitionedBFS:
-    """The level loop of one rank. Every rank calls solve() with the same source.
-
-    alpha / beta: Beamer's direction-switch parameters (as the single-GPU
-    solver's defaults); force: 0 auto, 1 push only, 2 pull from level 1 on."""
-
-    def __init__(self, ops, exchange: Optional[Exchange] = None, nnz_global: Optional[int] = None,
-                 alpha: float = 14.0, beta: float = 24.0, force: int = 0):
-        self.ops = ops
-        self.ex = exchange
-        self.alpha, self.beta, self.force = alpha, beta, force
-        self.world = 1 if exchange is None else exchange.world
-        if self.world != ops.world:
-            raise PJError(-9, f"exchange has {self.world} ranks, the partition {ops.world}")
-        if nnz_global is None:
-            nnz_global = self._sum([ops.nnz_local])[0]
-        self.nnz_global = nnz_global
-        # replicated isolated-vertex mask: one all-gather per graph
-        z = ops.zmask()
-        if self.ex is None:
-            ops.iso.copy_(z)
-        else:
-            self.ex.allgather_slices(ops.iso, z)
-        self.stats = {}
-
-    def _sum(self, vals):
-        return vals if self.ex is None else self.ex.allreduce_sum(vals, self.ops.vis)
-
-    def _allgather_vis(self):
-        if self.ex is not None:
-            self.ex.allgather_slices(self.ops.vis, self.ops.own_slice())
-
-    def solve(self, source: int) -> dict:
-        ops = self.ops
-        n_f, m_f, nz = self._sum(ops.begin(source))
-        n_r, m_r = n_f, m_f
-        m_u = self.nnz_global - m_f
-        mode, level, td, bu, sent = 0, 0, 0, 0, 0
-        if self.force == 2:
-            mode = 1
-            self._allgather_vis()
-        while n_f > 0 and level + 1 < INT_INF:
-            prev_n_f = n_f
-            if mode == 0:
-                counts = ops.push(level)
-                if self.ex is not None:
-                    rc = self.ex.alltoall_counts(counts, ops.vis)
-                    self.ex.alltoall_ids(ops.send, counts, ops.recv, rc)
-                    sent += sum(counts)
-                    ops.apply(level, sum(rc))
-                td += 1
-            else:
-                ops.pull(level)
-                bu += 1
-            n_f, m_f, nz = self._sum(ops.end_level())
-            n_r += n_f
-            m_r += m_f
-            m_u -= m_f
-            # Beamer: switch to pull when the frontier's edges exceed the unexplored
-            # edges / alpha, back to push when the frontier is small and shrinking
-            nxt = mode
-            if self.force == 1:
-                nxt = 0
-            elif self.force == 2:
-                nxt = 1
-            elif mode == 0 and m_f > m_u / self.alpha:
-                nxt = 1
-            elif mode == 1 and n_f < ops.n / self.beta and n_f < prev_n_f:
-                nxt = 0
-            if n_f > 0 and (nxt == 1 or mode == 1):
-                self._allgather_vis()
-            mode = nxt
-            level += 1
-        self.stats = dict(levels=level, td_levels=td, bu_levels=bu, reached=n_r, reached_edges=m_r,
-                          ids_sent=sent)
-        return self.stats
-
-
-def gather_dist(ops, exchange: Optional[Exchange]) -> np.ndarray:
-    """Full distance vector on every rank (test/CLI helper; not in the timed path)."""
-    import torch
-    local = ops.dist_local()
-    if exchange is None:
-        return local
-    block, ranges = block_geometry(ops.n, ops.world)
-    buf = torch.full((block,), INT_INF, dtype=torch.int32)
-    buf[: len(local)] = torch.from_numpy(local)
-    out = torch.empty(block * ops.world, dtype=torch.int32)
-    if exchange.stage:
-        exchange.dist.all_gather_into_tensor(out, buf, group=exchange.group)
-    else:
-        dev = (ops.vis if hasattr(ops, "vis") else ops.send).device
-        o = out.to(dev)
-        exchange.dist.all_gather_into_tensor(o, buf.to(dev), group=exchange.group)
-        out = o.cpu()
-    return out.numpy()[: ops.n]
-
-
-# ---- weighted SSSP over the 1D partition (delta-stepping; wpart.hip) --------
-
 class DeviceWPart:
-    """This rank's block of a weighted graph on its GPU (libpj pj_wpart_*)."""
+    """This rank's block of a weighted graph on its GPU (pj_wpart_*)."""
 
     def __init__(self, ctx, graph, rank: int, world: int):
-        import torch
         h = ctypes.c_void_p()
         _check(_lib.pj_wpart_from_graph(graph._h, int(rank), int(world), ctypes.byref(h)))
         self._ctx = ctx
@@ -327,42 +290,17 @@ class DeviceWPart:
         _check(_lib.pj_wpart_info(self._h, info))
         self.n, self.lo, self.hi, self.block, self.nnz_local, self.world, self.rank, self.nnz = list(info)
         self.nl = self.hi - self.lo
-        dev = torch.device("cuda", ctx.device)
-        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-        cap = self.world * self.block if self.world > 1 else 1
-        self.send = torch.empty(cap, dtype=torch.int64, device=dev)
-        self.recv = torch.empty(cap, dtype=torch.int64, device=dev)
-        self._counts = (_I64 * max(self.world, 1))()
-        self._o2 = (_I64 * 2)()
 
-    @staticmethod
-    def _p(t):
-        return ctypes.c_void_p(t.data_ptr())
+    def delta(self, comm: Comm, source: int, delta: int = 0) -> dict:
+        """pj_wpart_delta: every rank of comm calls it with the same source and delta."""
+        st = PartStats()
+        _check(_lib.pj_wpart_delta(self._h, comm._h, int(source), int(delta), ctypes.byref(st)))
+        return st.as_dict()
 
-    def begin(self, source: int, delta: int = 0) -> int:
-        d = ctypes.c_int32()
-        _check(_lib.pj_wpart_begin(self._h, int(source), int(delta), ctypes.byref(d)))
-        return d.value
-
-    def select(self, lo: int, hi: int):
-        _check(_lib.pj_wpart_select(self._h, int(lo), int(hi), self._o2))
-        return int(self._o2[0]), int(self._o2[1])
-
-    def relax(self, light: bool, lo: int, hi: int) -> List[int]:
-        _check(_lib.pj_wpart_relax(self._h, int(light), int(lo), int(hi), self._p(self.send), self._counts))
-        return list(self._counts)[: self.world]
-
-    def apply(self, n_recv: int, light: bool, lo: int, hi: int):
-        _check(_lib.pj_wpart_apply(self._h, self._p(self.recv), int(n_recv), int(light), int(lo), int(hi)))
-
-    def end_round(self) -> int:
-        nf = _I64()
-        _check(_lib.pj_wpart_end_round(self._h, ctypes.byref(nf)))
-        return nf.value
-
-    def reach(self):
-        _check(_lib.pj_wpart_reach(self._h, self._o2))
-        return int(self._o2[0]), int(self._o2[1])
+    def gather_dist(self, comm: Comm, want: bool = True) -> Optional[np.ndarray]:
+        out = np.empty(max(self.n, 1), np.int32) if want else None
+        _check(_lib.pj_wpart_gather_dist(self._h, comm._h, _ptr(out)))
+        return out[: self.n] if want else None
 
     def dist_local(self) -> np.ndarray:
         out = np.empty(max(self.nl, 1), np.int32)
@@ -381,67 +319,137 @@ class DeviceWPart:
             pass
 
 
-class PartitionedDelta:
-    """The band loop of one rank (delta-stepping, Meyer & Sanders) over a 1D
-    vertex partition; every rank calls solve() with the same source. The
-    reference's round loop (:488-594) with its exchange (:522-554) and its
-    termination all-reduce (:579-593); R9 makes the result independent of the
-    partition and of the band structure."""
-
-    def __init__(self, ops, exchange: Optional[Exchange] = None, delta: int = 0):
-        self.ops = ops
-        self.ex = exchange
-        self.delta = delta
-        self.world = 1 if exchange is None else exchange.world
-        if self.world != ops.world:
-            raise PJError(-9, f"exchange has {self.world} ranks, the partition {ops.world}")
-        self.stats = {}
-
-    def _sum(self, vals):
-        return vals if self.ex is None else self.ex.allreduce_sum(vals, self.ops.send)
-
-    def _min(self, vals):
-        return vals if self.ex is None else self.ex.allreduce_min(vals, self.ops.send)
-
-    def _exchange_apply(self, light, lo, hi):
-        ops = self.ops
-        counts = ops.relax(light, lo, hi)
-        nr = 0
-        if self.ex is not None:
-            rc = self.ex.alltoall_counts(counts, ops.send)
-            self.ex.alltoall_ids(ops.send, counts, ops.recv, rc)
-            nr = sum(rc)
-            self.sent += sum(counts)
-        ops.apply(nr, light, lo, hi)
-
-    def solve(self, source: int) -> dict:
-        ops = self.ops
-        delta = ops.begin(source, self.delta)
-        lo, bands, rounds = 0, 0, 0
-        self.sent = 0
-        while lo < INT_INF:
-            hi = min(lo + delta, INT_INF)
-            cnt, mn = ops.select(lo, hi)
-            cnt = self._sum([cnt])[0]
-            if cnt == 0:
-                mn = self._min([mn])[0]
-                if mn >= INT_INF:
-                    break
-                lo = max(mn // delta * delta, hi)  # jump to the next occupied band
-                continue
-            bands += 1
-            while True:  # light rounds until no rank has a frontier
-                self._exchange_apply(True, lo, hi)
-                rounds += 1
-                if self._sum([ops.end_round()])[0] == 0:
-                    break
-            self._exchange_apply(False, lo, hi)  # heavy edges of the band's members
-            lo = hi
-        r, m = self._sum(list(ops.reach()))
-        self.stats = dict(delta=delta, bands=bands, rounds=rounds, reached=r, reached_edges=m, sent=self.sent)
-        return self.stats
-
-
 def load_weighted(ctx, graph, rank: int, world: int) -> DeviceWPart:
     """The rank's block of a weighted pj Graph (the graph may be closed afterwards)."""
     return DeviceWPart(ctx, graph, rank, world)
+
+
+def bfs_group(parts: Sequence[DevicePart], comms: Sequence[Comm], source: int) -> List[dict]:
+    """pj_part_bfs_group: every rank of a one-process group at once (a host thread each)."""
+    w = len(parts)
+    st = (PartStats * w)()
+    _check(_lib.pj_part_bfs_group(w, (ctypes.c_void_p * w)(*[p._h.value for p in parts]),
+                                  (ctypes.c_void_p * w)(*[c._h.value for c in comms]), int(source), st))
+    return [s.as_dict() for s in st]
+
+
+def delta_group(parts: Sequence[DeviceWPart], comms: Sequence[Comm], source: int, delta: int = 0) -> List[dict]:
+    w = len(parts)
+    st = (PartStats * w)()
+    _check(_lib.pj_wpart_delta_group(w, (ctypes.c_void_p * w)(*[p._h.value for p in parts]),
+                                     (ctypes.c_void_p * w)(*[c._h.value for c in comms]), int(source), int(delta), st))
+    return [s.as_dict() for s in st]
+
+
+# ------------------------------------------- the loops over caller steps ---
+
+def _put(ptr, vals):
+    for i, v in enumerate(vals):
+        ptr[i] = int(v)
+
+
+def _step_call(err, fn):
+    def call(*a):
+        try:
+            fn(*a)
+            return 0
+        except BaseException as e:  # noqa: BLE001 - reported through the status
+            err.append(e)
+            return 1
+    return call
+
+
+def _raise_first(err, exc):
+    if err:
+        raise err[0]
+    raise exc
+
+
+def engine_bfs(steps, comm: Comm, source: int, alpha: float = 14.0, beta: float = 24.0, force: int = 0) -> dict:
+    """libpj's partitioned BFS loop (pj_engine_bfs) over caller steps: an object with
+    n, nnz_local, bw, block, rank, world, numpy buffers vis / iso / zown / send /
+    recv and the pj_part_* step methods zmask(), begin(source) -> [3],
+    push(level) -> counts, apply(level, n_recv), pull(level), end_level() -> [3]."""
+    err = []
+    world = int(steps.world)
+
+    def begin(_, s, st):
+        _put(st, steps.begin(int(s)))
+
+    def push(_, level, counts):
+        _put(counts, list(steps.push(int(level)))[:world])
+
+    def end_level(_, st):
+        _put(st, steps.end_level())
+
+    cs = BfsSteps(None, int(steps.n), int(steps.nnz_local), int(steps.bw), int(steps.block), int(steps.rank), world,
+                  steps.vis.ctypes.data, steps.iso.ctypes.data, steps.zown.ctypes.data, steps.send.ctypes.data,
+                  steps.recv.ctypes.data,
+                  _ST_ZMASK(_step_call(err, lambda _: steps.zmask())), _ST_BEGIN(_step_call(err, begin)),
+                  _ST_PUSH(_step_call(err, push)), _ST_APPLY(_step_call(err, lambda _, l, nr: steps.apply(l, nr))),
+                  _ST_PULL(_step_call(err, lambda _, l: steps.pull(l))), _ST_END(_step_call(err, end_level)))
+    st = PartStats()
+    rc = _lib.pj_engine_bfs(ctypes.byref(cs), comm._h, int(source), float(alpha), float(beta), int(force),
+                            ctypes.byref(st))
+    if rc != 0:
+        _raise_first(err + getattr(comm, "errors", []), PJError(rc, (_lib.pj_last_error() or b"").decode()))
+    return st.as_dict()
+
+
+def engine_delta(steps, comm: Comm, source: int, delta: int = 0) -> dict:
+    """libpj's partitioned delta-stepping loop (pj_engine_delta) over caller steps:
+    n, rank, world, numpy send / recv and the pj_wpart_* step methods begin(source,
+    delta) -> delta, select(lo, hi) -> (count, min), relax(light, lo, hi) -> counts,
+    apply(n_recv, light, lo, hi), end_round() -> n_f, reach() -> (n_r, m_r)."""
+    err = []
+    world = int(steps.world)
+
+    def begin(_, s, d, out):
+        out[0] = int(steps.begin(int(s), int(d)))
+
+    def select(_, lo, hi, out):
+        _put(out, steps.select(int(lo), int(hi)))
+
+    def relax(_, light, lo, hi, counts):
+        _put(counts, list(steps.relax(bool(light), int(lo), int(hi)))[:world])
+
+    def end_round(_, out):
+        out[0] = int(steps.end_round())
+
+    def reach(_, out):
+        _put(out, steps.reach())
+
+    cs = DeltaSteps(None, int(steps.n), int(steps.rank), world, steps.send.ctypes.data, steps.recv.ctypes.data,
+                    _DS_BEGIN(_step_call(err, begin)), _DS_SELECT(_step_call(err, select)),
+                    _DS_RELAX(_step_call(err, relax)),
+                    _DS_APPLY(_step_call(err, lambda _, nr, light, lo, hi: steps.apply(nr, bool(light), lo, hi))),
+                    _DS_END(_step_call(err, end_round)), _DS_REACH(_step_call(err, reach)))
+    st = PartStats()
+    rc = _lib.pj_engine_delta(ctypes.byref(cs), comm._h, int(source), int(delta), ctypes.byref(st))
+    if rc != 0:
+        _raise_first(err + getattr(comm, "errors", []), PJError(rc, (_lib.pj_last_error() or b"").decode()))
+    return st.as_dict()
+
+
+def gather_group(parts: Sequence, comms: Sequence[Comm]) -> np.ndarray:
+    """The whole distance vector of a one-process group: every rank gathers on its own
+    host thread (the collective needs all of them at once); rank 0's copy is returned."""
+    import threading
+    out, errs = [None], []
+
+    def run(r):
+        try:
+            d = parts[r].gather_dist(comms[r], want=(r == 0))
+            if r == 0:
+                out[0] = d
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(len(parts))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return out[0]

@@ -1,11 +1,13 @@
-"""Numpy restatement of the pj_part_* device steps (part.hip), for the CPU tests
-of the partitioned protocol (paralleljohnson_amd/partition.py) under gloo.
+"""Numpy restatement of the pj_part_* / pj_wpart_* device steps (part.hip,
+wpart.hip), for the CPU tests of libpj's partitioned protocol loops
+(engine.cpp, driven through pj_engine_bfs / pj_engine_delta) under gloo.
 
 Test infrastructure only: it lets the world_size > 1 exchange, termination and
-direction logic run without a GPU. The product path is DevicePart (libpj).
-Semantics per step are those documented in include/pj.h (pj_part_*)."""
+direction logic of the C++ loops run without a GPU. The product path runs the
+same loops over libpj's kernels (pj_part_bfs / pj_wpart_delta). Semantics per
+step are those documented in include/pj.h. The buffers the loop hands to the
+transport (vis, iso, zown, send, recv) are numpy arrays with fixed addresses."""
 import numpy as np
-import torch
 
 from paralleljohnson_amd.partition import block_geometry
 
@@ -34,18 +36,18 @@ class NumpyPart:
         self.row, self.col = rows(src, dst)
         self.crow, self.ccol = (self.row, self.col) if symmetric else rows(dst, src)
         self.nnz_local = len(self.col)
-        self.vis = torch.zeros(world * self.bw, dtype=torch.int64)
-        self.iso = torch.zeros_like(self.vis)
+        self.vis = np.zeros(world * self.bw, np.uint64)
+        self.iso = np.zeros_like(self.vis)
+        self.zown = np.zeros(self.bw, np.uint64)
         cap = world * self.block if world > 1 else 1
-        self.send = torch.zeros(cap, dtype=torch.int32)
-        self.recv = torch.zeros(cap, dtype=torch.int32)
+        self.send = np.zeros(cap, np.uint32)
+        self.recv = np.zeros(cap, np.uint32)
         self.dist = np.full(max(self.nl, 1), INF, np.int32)[: self.nl]
         self.fr = np.zeros(self.bw, np.uint64)
         self.frn = np.zeros(self.bw, np.uint64)
 
-    # bit helpers over the torch-owned visited words
     def _v(self):
-        return self.vis.numpy().view(np.uint64)
+        return self.vis
 
     @staticmethod
     def _get(words, ids):
@@ -57,16 +59,13 @@ class NumpyPart:
         ids = np.asarray(ids, np.int64)
         np.bitwise_or.at(words, ids >> 6, np.uint64(1) << (ids & 63).astype(np.uint64))
 
-    def own_slice(self):
-        return self.vis[self.rank * self.bw:(self.rank + 1) * self.bw]
-
     def zmask(self):
-        z = np.zeros(self.bw, np.uint64)
+        """Own isolated-vertex words -> zown (padding past the last owned vertex counts as isolated)."""
+        self.zown[:] = 0
         v = np.arange(self.block)
-        iso = np.ones(self.block, bool)  # padding past the last owned vertex counts as isolated
+        iso = np.ones(self.block, bool)
         iso[: self.nl] = (np.diff(self.row) == 0) & (np.diff(self.crow) == 0)
-        self._set(z, v[iso])
-        return torch.from_numpy(z.view(np.int64).copy())
+        self._set(self.zown, v[iso])
 
     def _settle(self, ids, level):
         """ids: global ids owned by this rank, newly claimed."""
@@ -75,7 +74,7 @@ class NumpyPart:
         self._set(self.frn, loc)
 
     def begin(self, s):
-        self._v()[:] = self.iso.numpy().view(np.uint64)
+        self._v()[:] = self.iso
         self.dist[:] = INF
         self.fr[:] = 0
         self.frn[:] = 0
@@ -107,12 +106,12 @@ class NumpyPart:
         counts = [int(np.sum(owner[~mine] == o)) for o in range(self.world)]
         packed = np.concatenate([out[owner[~mine] == o] for o in range(self.world)]) if len(out) else out
         if len(packed):
-            self.send[: len(packed)] = torch.from_numpy(packed.astype(np.int32))
+            self.send[: len(packed)] = packed.astype(np.uint32)
         return counts
 
     def apply(self, level, nr):
         vis = self._v()
-        ids = self.recv[:nr].numpy().astype(np.int64)
+        ids = self.recv[:nr].astype(np.int64)
         assert np.all((ids >= self.lo) & (ids < self.hi)), "received ids owned by another rank"
         ids = np.unique(ids[self._get(vis, ids) == 0])
         self._set(vis, ids)
@@ -146,7 +145,7 @@ class NumpyPart:
 
 class NumpyWPart:
     """Numpy restatement of the pj_wpart_* steps (wpart.hip; semantics as in
-    include/pj.h), driven by partition.PartitionedDelta under gloo on CPU.
+    include/pj.h), driven by libpj's band loop (pj_engine_delta) under gloo on CPU.
     Same block geometry; send/recv are int64 (id | cand << 32), owner-major."""
 
     def __init__(self, src, dst, w, n, rank, world):
@@ -167,8 +166,8 @@ class NumpyWPart:
         self.row, self.col, self.w = np.cumsum(row), dst[m][order], w[m][order]
         self.nnz_local = len(self.col)
         cap = world * self.block if world > 1 else 1
-        self.send = torch.zeros(cap, dtype=torch.int64)
-        self.recv = torch.zeros(cap, dtype=torch.int64)
+        self.send = np.zeros(cap, np.int64)
+        self.recv = np.zeros(cap, np.int64)
         self.dist = np.full(self.nl, INF, np.int64)
         self.cand = np.full(n, INF, np.int64)
         self.fr = np.zeros(self.nl, bool)
@@ -227,11 +226,11 @@ class NumpyWPart:
         counts = [int(np.sum(owner == o)) for o in range(self.world)]
         if len(ids):
             packed = ids | (self.cand[ids] << 32)  # ids are sorted, hence owner-major
-            self.send[: len(ids)] = torch.from_numpy(packed)
+            self.send[: len(ids)] = packed
         return counts
 
     def apply(self, nr, light, lo, hi):
-        rec = self.recv[:nr].numpy()
+        rec = self.recv[:nr]
         ids, cs = rec & 0xFFFFFFFF, rec >> 32
         assert np.all((ids >= self.lo) & (ids < self.hi)), "received ids owned by another rank"
         for v, c in zip(ids, cs):

@@ -387,14 +387,14 @@ def test_partitioned_bfs_s28_full_size(ctx):
     by the single-GPU loader (a different code path: kronecker -> radix sort -> CSR)."""
     import torch
     from helpers import sssp_certificate
-    from paralleljohnson_amd.partition import PartitionedBFS, gather_dist, load_kronecker
+    from paralleljohnson_amd.partition import Comm, load_kronecker
     ops = load_kronecker(ctx, 28, 16, 1, 0, 1)
-    bfs = PartitionedBFS(ops, None)
+    comm = Comm.for_rank(ctx, 1, 0)
     dists = {}
     for c in np.random.default_rng(8).integers(0, 1 << 28, 64):  # bench.py's root rule: reached > 1
-        st = bfs.solve(int(c))
+        st = ops.bfs(comm, int(c))
         if st["reached"] > 1:
-            dists[int(c)] = gather_dist(ops, None)
+            dists[int(c)] = ops.gather_dist(comm)
             assert st["reached"] == int((dists[int(c)] < INF).sum())
         if len(dists) == 2:
             break

@@ -1,12 +1,20 @@
-"""1D vertex-partitioned BFS: protocol tests on CPU (gloo,
-world_size 1-3, numpy restatement of the device steps) and parity of the HIP
-kernels (libpj pj_part_*) against the oracle on the GPU, at world_size 1 and
-at world_size 2 with both ranks sharing the one GPU (gloo, host-staged).
+"""1D vertex-partitioned solves: libpj's C++ protocol loops
+(engine.cpp: the BFS level loop and the delta-stepping band loop, the analogue of
+the reference's BSP round loop ParallelJohnson.cpp:488-594 with its
+Alltoall(v) / Allreduce exchange :522-554 / :589-590).
 
-Bar: bit-exact distances against the oracle BFS (the reference's R9 contract);
-partitioning is result-neutral."""
+CPU: the same C++ loops over a numpy restatement of the device steps
+(tests/part_numpy.py), at world 1 and over gloo at world 2-3 (pj_engine_bfs /
+pj_engine_delta with a callback transport). GPU: the product path -- libpj's
+kernels (pj_part_* / pj_wpart_*), the loops inside pj_part_bfs / pj_wpart_delta,
+over the in-process transports (ranks sharing the one GPU through device copies;
+RCCL at world 1) and through the CLI at P = 1, 2, 3.
+
+Bar: bit-exact distances against the oracle BFS / Dijkstra (the reference's R9
+contract); partitioning is result-neutral."""
 import os
 import socket
+import subprocess
 import sys
 import tempfile
 
@@ -14,7 +22,7 @@ import numpy as np
 import pytest
 
 from conftest import ROOT
-from helpers import random_graph
+from helpers import random_graph, to_text
 
 INF = 100000
 
@@ -27,8 +35,14 @@ def _free_port():
     return p
 
 
+def _csr(oracle, s, d, n, w=None):
+    return oracle.coo2csr(np.asarray(s, np.int64), np.asarray(d, np.int64), n, w)
+
+
 def _oracle_dist(oracle, src, dst, n, source):
-    row, col, _ = oracle.coo2csr(np.asarray(src, np.int64), np.asarray(dst, np.int64), n)
+    if not 0 <= source < n:
+        return np.full(n, INF, np.int32)
+    row, col, _ = _csr(oracle, src, dst, n)
     return oracle.bfs(row, col, source)
 
 
@@ -42,6 +56,37 @@ def _cases():
     s, d = random_graph(rng, "hub", 900)
     out.append(("sym", 900, np.concatenate([s, d]).astype(np.int64), np.concatenate([d, s]).astype(np.int64)))
     return out
+
+
+def _wcases():
+    rng = np.random.default_rng(99)
+    out = []
+    for kind, n, wmax in (("uniform", 500, 300), ("hub", 900, 40), ("chain", 300, 5), ("uniform", 64, 2)):
+        s, d = random_graph(rng, kind, n)
+        w = rng.integers(0 if kind == "uniform" else 1, wmax, len(s)).astype(np.uint32)
+        out.append((kind, n, s.astype(np.int64), d.astype(np.int64), w))
+    return out
+
+
+class LocalTransport:
+    """world 1: the collectives are copies (CPU tests of the loops without gloo)."""
+
+    def allreduce(self, vals, is_min):
+        pass
+
+    def alltoall_counts(self, send, recv):
+        recv[:] = send
+
+    def alltoallv(self, send_ptr, scounts, recv_ptr, rcounts, elem):
+        from paralleljohnson_amd.partition import _host
+        nb = int(scounts[0]) * elem
+        if nb:
+            _host(recv_ptr, nb)[:] = _host(send_ptr, nb)
+
+    def allgather(self, own_ptr, all_ptr, nbytes):
+        from paralleljohnson_amd.partition import _host
+        if own_ptr != all_ptr:
+            _host(all_ptr, nbytes)[:] = _host(own_ptr, nbytes)
 
 
 # ----------------------------------------------------------------- CPU ----
@@ -61,264 +106,81 @@ def test_block_geometry():
 
 
 @pytest.mark.parametrize("force", [0, 1, 2])
-def test_protocol_world1_numpy(oracle, force):
+def test_engine_world1_numpy(oracle, force):
+    """libpj's BFS level loop (pj_engine_bfs) over numpy steps, one rank."""
     from part_numpy import NumpyPart
-    from paralleljohnson_amd.partition import PartitionedBFS, gather_dist
+    from paralleljohnson_amd.partition import Comm, engine_bfs
+    comm = Comm.from_callbacks(LocalTransport(), 0, 1)
     for kind, n, s, d in _cases():
-        sym = kind == "sym"
-        ops = NumpyPart(s, d, n, 0, 1, symmetric=sym)
-        bfs = PartitionedBFS(ops, None, force=force)
+        ops = NumpyPart(s, d, n, 0, 1, symmetric=(kind == "sym"))
         for source in (0, n // 3, n - 1, n + 5, -1):
-            bfs.solve(source)
-            got = gather_dist(ops, None)
-            exp = _oracle_dist(oracle, s, d, n, source) if 0 <= source < n else np.full(n, INF, np.int32)
-            assert np.array_equal(got, exp), (kind, source, force)
+            st = engine_bfs(ops, comm, source, force=force)
+            exp = _oracle_dist(oracle, s, d, n, source)
+            assert np.array_equal(ops.dist_local(), exp), (kind, source, force)
+            assert st["reached"] == int((exp < INF).sum())
+            if force == 1:
+                assert st["bu_levels"] == 0
+            if force == 2 and st["levels"]:
+                assert st["td_levels"] == 0
 
 
-def _rank_main(rank, world, port, path, force, device, backend="gloo"):
-    """One rank of a gloo (or nccl) job: every case, every source; rank 0 saves the results."""
+def _rank_main(rank, world, port, path, force, weighted):
+    """One rank of a gloo job running libpj's C++ loop over numpy steps; rank 0 saves."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import torch
     import torch.distributed as dist
-    from paralleljohnson_amd.partition import Exchange, PartitionedBFS, gather_dist
-    if backend == "nccl":
-        torch.cuda.set_device(0)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
-    else:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    ex = Exchange()
+    from gloo_transport import GlooTransport, gather_blocks
+    from part_numpy import NumpyPart, NumpyWPart
+    from paralleljohnson_amd.partition import Comm, engine_bfs, engine_delta
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm.from_callbacks(GlooTransport(), rank, world)
     res = {}
-    if device:
-        import paralleljohnson_amd as pj
-        from paralleljohnson_amd.partition import load_coo, load_kronecker
-        ctx = pj.Context(0)
-        cases = [(k, n, s, d) for k, n, s, d in _cases()]
-        for ci, (kind, n, s, d) in enumerate(cases):
-            ops = load_coo(ctx, s, d, n, rank, world, symmetric=(kind == "sym"))
-            bfs = PartitionedBFS(ops, ex, force=force)
-            for source in (0, n // 3, n - 1):
-                st = bfs.solve(source)
-                res[f"{ci}_{source}"] = gather_dist(ops, ex)
-                res[f"{ci}_{source}_reached"] = np.array([st["reached"], st["reached_edges"]])
-            ops.close()
-        ops = load_kronecker(ctx, 14, 16, 7, rank, world)
-        bfs = PartitionedBFS(ops, ex, force=force)
-        for source in (1, 777, 12345):
-            bfs.solve(source)
-            res[f"k14_{source}"] = gather_dist(ops, ex)
-        ops.close()
-    else:
-        from part_numpy import NumpyPart
+    if not weighted:
         for ci, (kind, n, s, d) in enumerate(_cases()):
             ops = NumpyPart(s, d, n, rank, world, symmetric=(kind == "sym"))
-            bfs = PartitionedBFS(ops, ex, force=force)
             for source in (0, n // 3, n - 1, n + 5):
-                bfs.solve(source)
-                res[f"{ci}_{source}"] = gather_dist(ops, ex)
+                st = engine_bfs(ops, comm, source, force=force)
+                res[f"{ci}_{source}"] = gather_blocks(ops.dist_local(), ops.block, world, n)
+                res[f"{ci}_{source}_st"] = np.array([st["reached"], st["reached_edges"], st["sent"]])
+    else:
+        for i, (_, n, s, d, w) in enumerate(_wcases()):
+            ops = NumpyWPart(s, d, w, n, rank, world)
+            for delta in (0, 7, 60):
+                for source in (0, n // 3, n - 1, n + 2):
+                    st = engine_delta(ops, comm, source, delta)
+                    res[f"c{i}_{delta}_{source}"] = gather_blocks(ops.dist_local(), ops.block, world, n)
+                    res[f"c{i}_{delta}_{source}_reached"] = np.array([st["reached"], st["reached_edges"]])
     if rank == 0:
         np.savez(path, **res)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run_world(world, force, device=False, backend="gloo"):
+def _run_world(world, force=0, weighted=False):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "res.npz")
-        mp.spawn(_rank_main, args=(world, _free_port(), path, force, device, backend), nprocs=world, join=True)
+        mp.spawn(_rank_main, args=(world, _free_port(), path, force, weighted), nprocs=world, join=True)
         with np.load(path) as z:
             return {k: z[k] for k in z.files}
 
 
 @pytest.mark.parametrize("world,force", [(2, 0), (2, 1), (2, 2), (3, 0)])
-def test_protocol_gloo_numpy(oracle, world, force):
+def test_engine_gloo_numpy(oracle, world, force):
+    """The C++ level loop at world 2-3 over gloo: count exchange, Alltoallv of claimed ids,
+    all-gathered visited bitmaps around pull levels, sum termination."""
     res = _run_world(world, force)
     for ci, (kind, n, s, d) in enumerate(_cases()):
         for source in (0, n // 3, n - 1, n + 5):
-            exp = _oracle_dist(oracle, s, d, n, source) if source < n else np.full(n, INF, np.int32)
-            assert np.array_equal(res[f"{ci}_{source}"], exp), (world, force, kind, source)
-
-
-# ----------------------------------------------------------------- GPU ----
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("force", [0, 1, 2])
-def test_part_world1_gpu(ctx, oracle, force):
-    from paralleljohnson_amd.partition import PartitionedBFS, gather_dist, load_coo
-    for kind, n, s, d in _cases():
-        ops = load_coo(ctx, s, d, n, 0, 1, symmetric=(kind == "sym"))
-        bfs = PartitionedBFS(ops, None, force=force)
-        for source in (0, n // 3, n - 1, n + 5, -1):
-            st = bfs.solve(source)
-            got = gather_dist(ops, None)
-            exp = _oracle_dist(oracle, s, d, n, source) if 0 <= source < n else np.full(n, INF, np.int32)
-            assert np.array_equal(got, exp), (kind, source, force)
-            assert st["reached"] == int(np.sum(exp < INF))
-            assert ops.reach()[0] == st["reached"]
-        ops.close()
-
-
-@pytest.mark.gpu
-def test_part_kronecker_matches_single_gpu(ctx, pj, oracle):
-    """The partitioned generator yields the same graph: s16, world 1, vs pj.Graph and the oracle."""
-    from paralleljohnson_amd.partition import PartitionedBFS, gather_dist, load_kronecker
-    g = ctx.generate_kronecker(16, 16, 3)
-    row, col, _ = g.get_csr()
-    ops = load_kronecker(ctx, 16, 16, 3, 0, 1)
-    assert ops.nnz_local == g.nnz
-    bfs = PartitionedBFS(ops, None)
-    for r in g.sample_roots(5, 4):
-        st = bfs.solve(int(r))
-        got = gather_dist(ops, None)
-        assert np.array_equal(got, g.sssp(int(r))), r
-        assert np.array_equal(got, oracle.bfs(row, col.view(np.uint32), int(r))), r
-        rs = g.reach_stats()
-        assert (st["reached"], st["reached_edges"]) == (rs["reached"], rs["reached_edges"])
-        assert st["td_levels"] >= 1 and st["bu_levels"] >= 1  # both directions exercised
-    ops.close()
-    g.close()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("world,force,backend", [(2, 0, "gloo"), (2, 2, "gloo"), (1, 0, "nccl")])
-def test_part_world2_one_gpu(oracle, world, force, backend):
-    """Two ranks on the one GPU (gloo, host-staged): kernels + exchange end to end; and the
-    RCCL (nccl backend) code path of the exchange at world 1, device tensors, no staging."""
-    res = _run_world(world, force, device=True, backend=backend)
-    for ci, (kind, n, s, d) in enumerate(_cases()):
-        for source in (0, n // 3, n - 1):
             exp = _oracle_dist(oracle, s, d, n, source)
-            assert np.array_equal(res[f"{ci}_{source}"], exp), (kind, source)
-            row, col, _ = _csr(oracle, s, d, n)
+            assert np.array_equal(res[f"{ci}_{source}"], exp), (world, force, kind, source)
+            row, _, _ = _csr(oracle, s, d, n)
             reached = exp < INF
-            assert res[f"{ci}_{source}_reached"].tolist() == [int(reached.sum()),
-                                                             int(np.diff(row)[reached].sum())]
-    k = oracle.kronecker(14, 16, 7)
-    row, col, _ = oracle.coo2csr(k[0], k[1], 1 << 14)
-    for source in (1, 777, 12345):
-        assert np.array_equal(res[f"k14_{source}"], oracle.bfs(row, col, source)), source
-
-
-def _csr(oracle, s, d, n):
-    return oracle.coo2csr(np.asarray(s, np.int64), np.asarray(d, np.int64), n)
-
-
-@pytest.mark.gpu
-def test_run_module_matches_cli(pj, oracle, tmp_path):
-    """`python -m paralleljohnson_amd.run` (1 process, and 2 ranks on the one GPU under
-    torchrun with gloo) writes the same sol_file bytes as the single-GPU CLI and the oracle."""
-    import subprocess
-    from helpers import to_text
-    rng = np.random.default_rng(77)
-    s, d = random_graph(rng, "hub", 3000)
-    path = tmp_path / "g.txt"
-    path.write_bytes(to_text(s, d, style=1))
-    src = int(s[0])
-    env = dict(os.environ, PJ_DEVICE="0")
-    ref = tmp_path / "cli.sol"
-    subprocess.run([pj.cli_path(), str(path), str(src), str(ref)], check=True, capture_output=True, env=env)
-    row, col, _ = oracle.coo2csr(np.asarray(s, np.int64), np.asarray(d, np.int64), int(max(s.max(), d.max())) + 1)
-    assert ref.read_bytes() == oracle.format_sol(oracle.bfs(row, col, src))
-    one = tmp_path / "one.sol"
-    r = subprocess.run([sys.executable, "-m", "paralleljohnson_amd.run", str(path), str(src), str(one)],
-                       check=True, capture_output=True, text=True, env=env, cwd=ROOT)
-    assert one.read_bytes() == ref.read_bytes()
-    assert r.stdout.startswith("Time: ") and r.stdout.rstrip().endswith("seconds when using 1 processes.")
-    assert "parallel Johnson's algorithm completes." in r.stderr
-    two = tmp_path / "two.sol"
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        "-m", "paralleljohnson_amd.run", str(path), str(src), str(two)],
-                       capture_output=True, text=True, env=dict(env, PJ_BACKEND="gloo"), cwd=ROOT, timeout=200)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert two.read_bytes() == ref.read_bytes()
-    assert "when using 2 processes." in r.stdout
-
-
-@pytest.mark.gpu
-def test_run_module_weighted(pj, oracle, tmp_path):
-    """PJ_WEIGHTED=1: the single-GPU CLI (delta-stepping) and `python -m
-    paralleljohnson_amd.run` at 1 and 2 ranks (PartitionedDelta, gloo) write the
-    oracle Dijkstra's sol_file bytes."""
-    import subprocess
-    from helpers import to_text
-    rng = np.random.default_rng(78)
-    s, d = random_graph(rng, "hub", 2500)
-    w = rng.integers(1, 200, len(s)).astype(np.uint32)
-    text = to_text(s, d, w=w, style=1)
-    path = tmp_path / "gw.txt"
-    path.write_bytes(text)
-    src = int(s[0])
-    ps, pd, pw, n = oracle.parse_snap(text, weighted=True)
-    row, col, wc = oracle.coo2csr(ps, pd, n, pw)
-    exp = oracle.format_sol(oracle.dijkstra(row, col, wc, src))
-    env = dict(os.environ, PJ_DEVICE="0", PJ_WEIGHTED="1")
-    ref = tmp_path / "cli.sol"
-    subprocess.run([pj.cli_path(), str(path), str(src), str(ref)], check=True, capture_output=True, env=env)
-    assert ref.read_bytes() == exp
-    one = tmp_path / "one.sol"
-    subprocess.run([sys.executable, "-m", "paralleljohnson_amd.run", str(path), str(src), str(one)],
-                   check=True, capture_output=True, text=True, env=env, cwd=ROOT)
-    assert one.read_bytes() == exp
-    two = tmp_path / "two.sol"
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        "-m", "paralleljohnson_amd.run", str(path), str(src), str(two)],
-                       capture_output=True, text=True, env=dict(env, PJ_BACKEND="gloo"), cwd=ROOT, timeout=200)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert two.read_bytes() == exp
-    assert "when using 2 processes." in r.stdout
-
-
-# ------------------------------------------- weighted (delta-stepping) ----
-
-def _wcases():
-    rng = np.random.default_rng(99)
-    out = []
-    for kind, n, wmax in (("uniform", 500, 300), ("hub", 900, 40), ("chain", 300, 5), ("uniform", 64, 2)):
-        s, d = random_graph(rng, kind, n)
-        w = rng.integers(0 if kind == "uniform" else 1, wmax, len(s)).astype(np.uint32)
-        out.append((kind, n, s.astype(np.int64), d.astype(np.int64), w))
-    return out
-
-
-def _wrank_main(rank, world, port, path, backend):
-    """One rank: weighted delta-stepping over the partition for every case; rank 0 saves."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    sys.path.insert(0, ROOT)
-    import torch
-    import torch.distributed as dist
-    import paralleljohnson_amd as pj
-    from paralleljohnson_amd.partition import Exchange, PartitionedDelta, gather_dist, load_weighted
-    if backend == "nccl":
-        torch.cuda.set_device(0)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
-    else:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    ex = Exchange()
-    ctx = pj.Context(0)
-    res = {}
-    graphs = [(f"c{i}", ctx.load_coo(s, d, w=w, n=n)) for i, (_, n, s, d, w) in enumerate(_wcases())]
-    graphs.append(("k12", ctx.generate_kronecker(12, 16, 3, weighted=True)))
-    for name, g in graphs:
-        ops = load_weighted(ctx, g, rank, world)
-        n = g.n
-        g.close()
-        for delta in (0, 7, 60):
-            sp = PartitionedDelta(ops, ex, delta=delta)
-            for source in (0, n // 3, n - 1, n + 2):
-                st = sp.solve(source)
-                res[f"{name}_{delta}_{source}"] = gather_dist(ops, ex)
-                res[f"{name}_{delta}_{source}_reached"] = np.array([st["reached"], st["reached_edges"]])
-        ops.close()
-    if rank == 0:
-        np.savez(path, **res)
-    dist.barrier()
-    dist.destroy_process_group()
+            assert res[f"{ci}_{source}_st"][:2].tolist() == [int(reached.sum()), int(np.diff(row)[reached].sum())]
+    # push levels exchange ids between the ranks (the protocol is exercised, not bypassed)
+    assert any(res[k][2] > 0 for k in res if k.endswith("_st")) or force == 2
 
 
 def _wexpected(oracle):
@@ -341,89 +203,195 @@ def _wcheck(res, exp_graphs, oracle, deltas, world):
                     int(reached.sum()), int(np.diff(row)[reached].sum())], (name, delta, source)
 
 
-def _wrank_numpy(rank, world, port, path):
-    """One rank of the weighted protocol on CPU (gloo), device steps restated in numpy."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    sys.path.insert(0, ROOT)
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import torch.distributed as dist
+def test_wengine_world1_numpy(oracle):
+    """libpj's band loop (pj_engine_delta) without an exchange, numpy device steps."""
     from part_numpy import NumpyWPart
-    from paralleljohnson_amd.partition import Exchange, PartitionedDelta, gather_dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    ex = Exchange()
-    res = {}
-    for i, (_, n, s, d, w) in enumerate(_wcases()):
-        ops = NumpyWPart(s, d, w, n, rank, world)
-        for delta in (0, 7, 60):
-            sp = PartitionedDelta(ops, ex, delta=delta)
-            for source in (0, n // 3, n - 1, n + 2):
-                st = sp.solve(source)
-                res[f"c{i}_{delta}_{source}"] = gather_dist(ops, ex)
-                res[f"c{i}_{delta}_{source}_reached"] = np.array([st["reached"], st["reached_edges"]])
-    if rank == 0:
-        np.savez(path, **res)
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def test_wprotocol_world1_numpy(oracle):
-    """The band loop (PartitionedDelta) without an exchange, numpy device steps."""
-    from part_numpy import NumpyWPart
-    from paralleljohnson_amd.partition import PartitionedDelta, gather_dist
+    from paralleljohnson_amd.partition import Comm, engine_delta
+    comm = Comm.from_callbacks(LocalTransport(), 0, 1)
     res = {}
     for i, (_, n, s, d, w) in enumerate(_wcases()):
         ops = NumpyWPart(s, d, w, n, 0, 1)
         for delta in (0, 1, 7, 60):
-            sp = PartitionedDelta(ops, None, delta=delta)
             for source in (0, n // 3, n - 1, n + 2):
-                st = sp.solve(source)
-                res[f"c{i}_{delta}_{source}"] = gather_dist(ops, None)
+                st = engine_delta(ops, comm, source, delta)
+                res[f"c{i}_{delta}_{source}"] = ops.dist_local()
                 res[f"c{i}_{delta}_{source}_reached"] = np.array([st["reached"], st["reached_edges"]])
     _wcheck(res, _wexpected(oracle), oracle, (0, 1, 7, 60), 1)
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_wprotocol_gloo_numpy(oracle, world):
-    """Weighted band loop at world 2-3 over gloo: all_to_all of packed (id, cand)
-    pairs, all_reduce sum/min termination; bit-exact vs the oracle Dijkstra."""
-    import torch.multiprocessing as mp
-    with tempfile.TemporaryDirectory() as td:
-        path = os.path.join(td, "res.npz")
-        mp.spawn(_wrank_numpy, args=(world, _free_port(), path), nprocs=world, join=True)
-        with np.load(path) as z:
-            res = {k: z[k] for k in z.files}
+def test_wengine_gloo_numpy(oracle, world):
+    """The C++ band loop at world 2-3 over gloo: Alltoallv of packed (id, cand) pairs,
+    all-reduced sum/min termination; bit-exact vs the oracle Dijkstra."""
+    res = _run_world(world, weighted=True)
     _wcheck(res, _wexpected(oracle), oracle, (0, 7, 60), world)
 
 
+def test_engine_step_failure_is_reported(oracle):
+    """A failing step surfaces as an exception, not a hang or a wrong answer."""
+    from part_numpy import NumpyPart
+    from paralleljohnson_amd.partition import Comm, engine_bfs
+    kind, n, s, d = _cases()[0]
+    ops = NumpyPart(s, d, n, 0, 1)
+
+    def boom(level):
+        raise RuntimeError("step failed")
+    ops.push = boom
+    with pytest.raises(RuntimeError, match="step failed"):
+        engine_bfs(ops, Comm.from_callbacks(LocalTransport(), 0, 1), 0)
+
+
+# ----------------------------------------------------------------- GPU ----
+
+def _group(pj, world, transport="host"):
+    from paralleljohnson_amd.partition import Comm
+    ctxs = [pj.Context(0) for _ in range(world)]
+    return ctxs, Comm.group(ctxs, transport)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,backend", [(1, "nccl"), (2, "gloo"), (3, "gloo")])
-def test_wpart_delta_stepping(pj, oracle, world, backend):
-    """Weighted SSSP over the 1D partition (wpart.hip + PartitionedDelta): every
-    rank on the one GPU; distances bit-exact against the oracle Dijkstra, for
-    several band widths and sources (including one outside [0, n))."""
-    import torch.multiprocessing as mp
-    with tempfile.TemporaryDirectory() as td:
-        path = os.path.join(td, "res.npz")
-        mp.spawn(_wrank_main, args=(world, _free_port(), path, backend), nprocs=world, join=True)
-        with np.load(path) as z:
-            res = {k: z[k] for k in z.files}
-    exp_graphs = []
-    for i, (_, n, s, d, w) in enumerate(_wcases()):
-        row, col, wc = oracle.coo2csr(s.astype(np.uint32), d.astype(np.uint32), n, w)
-        exp_graphs.append((f"c{i}", n, row, col, wc))
-    ctx = pj.Context(0)
-    g = ctx.generate_kronecker(12, 16, 3, weighted=True)
-    row, col, wc = g.get_csr()
-    exp_graphs.append(("k12", g.n, row, col.astype(np.uint32), wc))
+@pytest.mark.parametrize("force", [0, 1, 2])
+@pytest.mark.parametrize("transport", ["self", "rccl"])
+def test_part_world1_gpu(ctx, oracle, force, transport):
+    """pj_part_bfs at world 1: no transport, and a one-rank RCCL group (the RCCL calls
+    of the loop -- allreduce, allgather, grouped send/recv -- with nothing to send)."""
+    from paralleljohnson_amd.partition import Comm, load_coo
+    comm = Comm.for_rank(ctx, 1, 0, Comm.unique_id() if transport == "rccl" else None)
+    assert comm.kind == transport
+    for kind, n, s, d in _cases():
+        ops = load_coo(ctx, s, d, n, 0, 1, symmetric=(kind == "sym"))
+        ops.set_option("direction", force)
+        for source in (0, n // 3, n - 1, n + 5, -1):
+            st = ops.bfs(comm, source)
+            got = ops.gather_dist(comm)
+            exp = _oracle_dist(oracle, s, d, n, source)
+            assert np.array_equal(got, exp), (kind, source, force)
+            assert st["reached"] == int(np.sum(exp < INF)) and ops.reach()[0] == st["reached"]
+        ops.close()
+    comm.close()
+
+
+@pytest.mark.gpu
+def test_part_kronecker_matches_single_gpu(ctx, pj, oracle):
+    """The partitioned generator yields the same graph: s16, world 1, vs pj.Graph and the oracle."""
+    from paralleljohnson_amd.partition import Comm, load_kronecker
+    g = ctx.generate_kronecker(16, 16, 3)
+    row, col, _ = g.get_csr()
+    ops = load_kronecker(ctx, 16, 16, 3, 0, 1)
+    comm = Comm.for_rank(ctx, 1, 0)
+    assert ops.nnz_local == g.nnz
+    for r in g.sample_roots(5, 4):
+        st = ops.bfs(comm, int(r))
+        got = ops.gather_dist(comm)
+        assert np.array_equal(got, g.sssp(int(r))), r
+        assert np.array_equal(got, oracle.bfs(row, col.view(np.uint32), int(r))), r
+        rs = g.reach_stats()
+        assert (st["reached"], st["reached_edges"]) == (rs["reached"], rs["reached_edges"])
+        assert st["td_levels"] >= 1 and st["bu_levels"] >= 1  # both directions exercised
+    ops.close()
     g.close()
-    ctx.close()
-    for name, n, row, col, wc in exp_graphs:
-        for source in (0, n // 3, n - 1, n + 2):
-            exp = oracle.dijkstra(row, col, wc, source) if source < n else np.full(n, INF, np.int32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,force", [(2, 0), (2, 1), (2, 2), (3, 0)])
+def test_part_group_one_gpu(pj, oracle, world, force):
+    """world ranks of one process sharing the one GPU (host transport: device copies between
+    the ranks' buffers, one host thread per rank): libpj kernels + the C++ level loop + the
+    exchange end to end, on random graphs and Kronecker s14."""
+    from paralleljohnson_amd.partition import bfs_group, gather_group, load_coo, load_kronecker
+    ctxs, comms = _group(pj, world)
+    assert all(c.kind == "host" for c in comms)
+    sent = 0
+    for kind, n, s, d in _cases():
+        parts = [load_coo(ctxs[r], s, d, n, r, world, symmetric=(kind == "sym")) for r in range(world)]
+        for p in parts:
+            p.set_option("direction", force)
+        row, _, _ = _csr(oracle, s, d, n)
+        for source in (0, n // 3, n - 1, n + 5):
+            st = bfs_group(parts, comms, source)
+            exp = _oracle_dist(oracle, s, d, n, source)
+            assert np.array_equal(gather_group(parts, comms), exp), (kind, source)
             reached = exp < INF
-            for delta in (0, 7, 60):
-                got = res[f"{name}_{delta}_{source}"]
-                assert np.array_equal(got, exp), (name, delta, source, world)
-                assert res[f"{name}_{delta}_{source}_reached"].tolist() == [
-                    int(reached.sum()), int(np.diff(row)[reached].sum())], (name, delta, source)
+            assert [st[0]["reached"], st[0]["reached_edges"]] == [int(reached.sum()),
+                                                                  int(np.diff(row)[reached].sum())]
+            assert len({x["levels"] for x in st}) == 1  # every rank ran the same levels
+            sent += sum(x["sent"] for x in st)
+        for p in parts:
+            p.close()
+    assert sent > 0 or force == 2
+    k = oracle.kronecker(14, 16, 7)
+    krow, kcol, _ = oracle.coo2csr(k[0], k[1], 1 << 14)
+    parts = [load_kronecker(ctxs[r], 14, 16, 7, r, world) for r in range(world)]
+    for source in (1, 777, 12345):
+        bfs_group(parts, comms, source)
+        assert np.array_equal(gather_group(parts, comms), oracle.bfs(krow, kcol, source)), source
+    for p in parts:
+        p.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,transport", [(1, "rccl"), (2, "host"), (3, "host")])
+def test_wpart_group(pj, oracle, world, transport):
+    """Weighted SSSP over the 1D partition (wpart.hip + the C++ band loop): every rank on the
+    one GPU; bit-exact against the oracle Dijkstra for several band widths and sources."""
+    from paralleljohnson_amd.partition import delta_group, gather_group, load_weighted
+    ctxs, comms = _group(pj, world, transport)
+    cases = [(f"c{i}", n, ctxs[0].load_coo(s, d, w=w, n=n)) for i, (_, n, s, d, w) in enumerate(_wcases())]
+    cases.append(("k12", 1 << 12, ctxs[0].generate_kronecker(12, 16, 3, weighted=True)))
+    for name, n, g0 in cases:
+        row, col, wc = g0.get_csr()
+        col = col.view(np.uint32)
+        parts = []
+        for r in range(world):
+            gr = g0 if r == 0 else None
+            if gr is None:  # each rank cuts its block from a graph on its own context
+                gr = ctxs[r].load_coo(np.repeat(np.arange(n), np.diff(row)), col, w=wc, n=n)
+            parts.append(load_weighted(ctxs[r], gr, r, world))
+            if r:
+                gr.close()
+        g0.close()
+        for delta in (0, 7, 60):
+            for source in (0, n // 3, n - 1, n + 2):
+                st = delta_group(parts, comms, source, delta)
+                exp = oracle.dijkstra(row, col, wc, source) if source < n else np.full(n, INF, np.int32)
+                assert np.array_equal(gather_group(parts, comms), exp), (name, delta, source, world)
+                reached = exp < INF
+                assert [st[0]["reached"], st[0]["reached_edges"]] == [int(reached.sum()),
+                                                                      int(np.diff(row)[reached].sum())]
+        for p in parts:
+            p.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("weighted", [False, True])
+def test_cli_processes_byte_identical(pj, oracle, tmp_path, weighted):
+    """`parallel_johnson` at P = 1 (single-GPU solver), P = 2 and 3 (PJ_GPUS: the 1D partition
+    in one process, ranks sharing the GPU over the host transport) and under an MPI-style
+    launcher (OMPI_COMM_WORLD_SIZE = 2: rank 0 runs both ranks, rank 1 exits): the same
+    sol_file bytes as the oracle, and the `Time:` line names P (:603-604)."""
+    rng = np.random.default_rng(77 + weighted)
+    s, d = random_graph(rng, "hub", 3000)
+    w = rng.integers(1, 200, len(s)).astype(np.uint32) if weighted else None
+    text = to_text(s, d, w=w, style=1)
+    path = tmp_path / "g.txt"
+    path.write_bytes(text)
+    src = int(s[0])
+    ps, pd, pw, n = oracle.parse_snap(text, weighted=weighted)
+    row, col, wc = oracle.coo2csr(ps, pd, n, pw)
+    exp = oracle.format_sol(oracle.dijkstra(row, col, wc, src) if weighted else oracle.bfs(row, col, src))
+    base = dict(os.environ, PJ_WEIGHTED=str(int(weighted)))
+    base.pop("PJ_GPUS", None)
+    runs = [("1", {}), ("2", {"PJ_GPUS": "2"}), ("3", {"PJ_GPUS": "3"}),
+            ("2", {"OMPI_COMM_WORLD_SIZE": "2", "OMPI_COMM_WORLD_RANK": "0"})]
+    for p, extra in runs:
+        out = tmp_path / f"sol_{p}_{len(extra)}.txt"
+        r = subprocess.run([pj.cli_path(), str(path), str(src), str(out)], capture_output=True, text=True,
+                           env=dict(base, **extra), timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert out.read_bytes() == exp, (p, extra)
+        assert r.stdout.startswith("Time: ") and r.stdout.endswith(f" seconds when using {p} processes.\n")
+        assert r.stderr.splitlines()[-1] == f"the shortest path distance vector has been saved in file {out}"
+    # the other launcher ranks do nothing and exit 0 (only rank 0 works)
+    r = subprocess.run([pj.cli_path(), str(path), str(src), str(tmp_path / "rank1.txt")], capture_output=True,
+                       env=dict(base, OMPI_COMM_WORLD_SIZE="2", OMPI_COMM_WORLD_RANK="1"), timeout=120)
+    assert r.returncode == 0 and not (tmp_path / "rank1.txt").exists()
