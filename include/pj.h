@@ -117,12 +117,28 @@ int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int
 int pj_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int weighted,
                           pj_graph** out);
 
+/* The same Kronecker tuples written as a SNAP text file in generation order
+ * (tuple i -> lines 2i and 2i+1, "u\tv[\tw]\n", after two '#' header lines):
+ * the text input of the ingestion benchmarks (the reference's read_webgraph
+ * :66-105 path at Graph500 sizes). No reference counterpart. */
+int pj_kronecker_write_snap(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int weighted, const char* path);
+
 /* web-Google-shaped synthetic graph (the SNAP file is not
  * available): n_ids ids (about 95.6% used, the largest always used, so
  * N = n_ids), n_edges directed edges with power-law out- and in-degrees and
  * 30% "same-site" links. Deterministic in (n_ids, n_edges, seed). Benchmark
  * input, no reference counterpart. */
 int pj_generate_webgraph(pj_ctx* ctx, int64_t n_ids, int64_t n_edges, uint64_t seed, pj_graph** out);
+
+/* How a graph was built (host wall times of the ingestion phases; 0 where a
+ * phase did not run): the file read (:66-105's getline passes), the copy of
+ * the text to the GPU, the GPU parse (line scan + field decode), and the CSR
+ * build (radix sort + row offsets, coord2csr :117-159). */
+typedef struct pj_load_stats {
+    double read_ms, h2d_ms, parse_ms, csr_ms;
+    int64_t text_bytes;
+} pj_load_stats;
+int pj_graph_load_stats(const pj_graph* g, pj_load_stats* out);
 
 int pj_graph_destroy(pj_graph* g);
 /* n = number of vertices, nnz = number of CSR entries, weighted = 0/1,

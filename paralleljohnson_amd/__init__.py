@@ -63,6 +63,11 @@ class Stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class LoadStats(ctypes.Structure):
+    _fields_ = [("read_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("parse_ms", ctypes.c_double),
+                ("csr_ms", ctypes.c_double), ("text_bytes", ctypes.c_int64)]
+
+
 _P = ctypes.c_void_p
 _PP = ctypes.POINTER(ctypes.c_void_p)
 _I64 = ctypes.c_int64
@@ -79,9 +84,11 @@ _SIGS = {
     "pj_load_coo": ([_P, _P, _P, _P, _I64, _I64, _PP], _INT),
     "pj_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _PP], _INT),
     "pj_generate_webgraph": ([_P, _I64, _I64, ctypes.c_uint64, _PP], _INT),
+    "pj_kronecker_write_snap": ([_P, _INT, _INT, ctypes.c_uint64, _INT, ctypes.c_char_p], _INT),
     "pj_graph_save": ([_P, ctypes.c_char_p, _I64, _I64], _INT),
     "pj_load_csr_file": ([_P, ctypes.c_char_p, _I64, _I64, _PP], _INT),
     "pj_graph_destroy": ([_P], _INT),
+    "pj_graph_load_stats": ([_P, _P], _INT),
     "pj_graph_info": ([_P, _P, _P, _P, _P], _INT),
     "pj_graph_get_csr": ([_P, _P, _P, _P], _INT),
     "pj_graph_out_degree": ([_P, _I64, _P], _INT),
@@ -222,6 +229,12 @@ class Graph:
         _check(_lib.pj_sssp_batch_write(self._h, _ptr(src), len(src), ctypes.cast(arr, ctypes.c_void_p),
                                         int(strict)))
 
+    def load_stats(self) -> dict:
+        """Ingestion phase times of this graph (pj_graph_load_stats)."""
+        st = LoadStats()
+        _check(_lib.pj_graph_load_stats(self._h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in st._fields_}
+
     def stats(self) -> dict:
         st = Stats()
         _check(_lib.pj_last_stats(self._h, ctypes.byref(st)))
@@ -319,6 +332,12 @@ class Context:
         g = ctypes.c_void_p()
         _check(_lib.pj_generate_webgraph(self._h, int(n_ids), int(n_edges), ctypes.c_uint64(seed), ctypes.byref(g)))
         return Graph(self, g)
+
+    def kronecker_write_snap(self, path: str, scale: int, edgefactor: int = 16, seed: int = 1,
+                             weighted: bool = False):
+        """The Kronecker tuples as a SNAP text file in generation order (ingestion benchmarks)."""
+        _check(_lib.pj_kronecker_write_snap(self._h, int(scale), int(edgefactor), ctypes.c_uint64(seed),
+                                            int(weighted), os.fsencode(path)))
 
     def generate_kronecker(self, scale: int, edgefactor: int = 16, seed: int = 1, weighted: bool = False) -> Graph:
         g = ctypes.c_void_p()

@@ -289,14 +289,26 @@ int pj_load_snap_buffer(pj_ctx* ctx, const char* text, int64_t len, int weighted
         }
         auto pg = std::make_unique<pj_graph>();
         pg->g.ctx = &ctx->c;
+        const auto t0 = std::chrono::steady_clock::now();
         build_graph_from_coo(pg->g, src, dst, weighted ? &w : nullptr, r.nnz, r.max_id + 1, false);
+        pg->g.load.csr_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        pg->g.load.h2d_ms = r.h2d_ms;
+        pg->g.load.parse_ms = r.parse_ms;
+        pg->g.load.text_bytes = len;
         return finish_graph(ctx, pg, out);
     });
+}
+
+int pj_graph_load_stats(const pj_graph* g, pj_load_stats* out) {
+    if (!g || !out) return arg_error("pj_graph_load_stats: bad argument");
+    *out = g->g.load;
+    return PJ_OK;
 }
 
 int pj_load_snap(pj_ctx* ctx, const char* path, int weighted, pj_graph** out) {
     if (!ctx || !path || !out) return arg_error("pj_load_snap: bad argument");
     return guarded([&] {
+        const auto t0 = std::chrono::steady_clock::now();
         std::vector<char> buf;
         struct stat sb;
         // A missing or unreadable file (or a directory) reads as empty, like the
@@ -310,7 +322,10 @@ int pj_load_snap(pj_ctx* ctx, const char* path, int weighted, pj_graph** out) {
             }
             std::fclose(f);
         }
-        return pj_load_snap_buffer(ctx, buf.data(), (int64_t)buf.size(), weighted, out);
+        const double read_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        const int rc = pj_load_snap_buffer(ctx, buf.data(), (int64_t)buf.size(), weighted, out);
+        if (rc == PJ_OK) (*out)->g.load.read_ms = read_ms;
+        return rc;
     });
 }
 
@@ -383,6 +398,70 @@ int pj_generate_webgraph(pj_ctx* ctx, int64_t n_ids, int64_t n_edges, uint64_t s
         pg->g.ctx = &ctx->c;
         build_graph_from_coo(pg->g, src, dst, nullptr, n_edges, n_ids, false);
         return finish_graph(ctx, pg, out);
+    });
+}
+
+int pj_kronecker_write_snap(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int weighted, const char* path) {
+    if (!ctx || !path || scale < 0 || scale > 31 || edgefactor < 1 || edgefactor > 1024)
+        return arg_error("pj_kronecker_write_snap: bad argument");
+    return guarded([&] {
+        bind(ctx->c);
+        DevBuf<u32> src, dst, w;
+        generate_kronecker_device(ctx->c, scale, edgefactor, seed, weighted != 0, src, dst, weighted ? &w : nullptr);
+        const i64 nnz = 2 * ((i64)edgefactor << scale);
+        FILE* f = std::fopen(path, "wb");
+        if (!f) {
+            set_error(std::string("pj_kronecker_write_snap: cannot open ") + path);
+            return (int)PJ_ERR_IO;
+        }
+        std::unique_ptr<FILE, int (*)(FILE*)> fc(f, std::fclose);
+        const char hdr[] = "# Graph500 Kronecker (A,B,C = 0.57,0.19,0.19), both directions\n# FromNodeId\tToNodeId\n";
+        std::fwrite(hdr, 1, sizeof(hdr) - 1, f);
+        const i64 chunk = (i64)1 << 24;
+        const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<u32> hs((size_t)chunk), hd((size_t)chunk), hw(weighted ? (size_t)chunk : 0);
+        std::vector<std::vector<char>> out(nt);
+        std::vector<size_t> lens(nt);
+        for (i64 c0 = 0; c0 < nnz; c0 += chunk) {
+            const i64 k = std::min(chunk, nnz - c0);
+            PJ_HIP(hipMemcpy(hs.data(), src.p + c0, 4 * (size_t)k, hipMemcpyDeviceToHost));
+            PJ_HIP(hipMemcpy(hd.data(), dst.p + c0, 4 * (size_t)k, hipMemcpyDeviceToHost));
+            if (weighted) PJ_HIP(hipMemcpy(hw.data(), w.p + c0, 4 * (size_t)k, hipMemcpyDeviceToHost));
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < nt; ++t)
+                th.emplace_back([&, t] {
+                    const i64 a = k * t / nt, b = k * (t + 1) / nt;
+                    out[t].resize((size_t)(b - a) * 36);
+                    char* o = out[t].data();
+                    size_t q = 0;
+                    auto put = [&](u32 x) {
+                        char rev[12];
+                        int r = 0;
+                        do {
+                            rev[r++] = (char)('0' + x % 10);
+                            x /= 10;
+                        } while (x);
+                        while (r) o[q++] = rev[--r];
+                    };
+                    for (i64 i = a; i < b; ++i) {
+                        put(hs[(size_t)i]);
+                        o[q++] = '\t';
+                        put(hd[(size_t)i]);
+                        if (weighted) {
+                            o[q++] = '\t';
+                            put(hw[(size_t)i]);
+                        }
+                        o[q++] = '\n';
+                    }
+                    lens[t] = q;
+                });
+            for (auto& t : th) t.join();
+            for (unsigned t = 0; t < nt; ++t)
+                if (std::fwrite(out[t].data(), 1, lens[t], f) != lens[t])
+                    throw Error(PJ_ERR_IO, "pj_kronecker_write_snap: write failed");
+        }
+        if (std::fclose(fc.release()) != 0) throw Error(PJ_ERR_IO, "pj_kronecker_write_snap: write failed");
+        return (int)PJ_OK;
     });
 }
 

@@ -324,6 +324,11 @@ int run_single(const char* webfile, int source, const char* out, int weighted) {
     print_msg("read in the webgraph is done.");
     print_msg("distribute sparse matrix is done.");
     ph.mark("load");
+    pj_load_stats ls{};
+    if (ph.on && pj_graph_load_stats(g, &ls) == PJ_OK)
+        std::cerr << "phase load: read " << ls.read_ms / 1000.0 << " s, h2d " << ls.h2d_ms / 1000.0 << " s, parse "
+                  << ls.parse_ms / 1000.0 << " s, csr " << ls.csr_ms / 1000.0 << " s (" << ls.text_bytes
+                  << " bytes of text)" << std::endl;
     std::cerr << "compute shortest paths from source node: " << source << std::endl;
     print_msg("parallel Johnson's algorithm starts......");
     std::vector<int32_t> dist((size_t)n);

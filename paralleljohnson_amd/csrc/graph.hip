@@ -13,12 +13,27 @@ namespace pj {
 
 namespace {
 
-__global__ void iota_k(u32* __restrict__ p, i64 n) {
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) p[i] = (u32)i;
+__global__ void pack_k(const u32* __restrict__ lo, const u32* __restrict__ hi, u64* __restrict__ out, i64 n) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
+        out[i] = (u64)lo[i] | ((u64)hi[i] << 32);
 }
 
-__global__ void gather_k(const u32* __restrict__ in, const u32* __restrict__ idx, u32* __restrict__ out, i64 n) {
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) out[i] = in[idx[i]];
+// (src | dst << 32) records in weight order, the sorted weights -> key src, record (dst | w << 32)
+__global__ void split_k(const u64* __restrict__ rec, const u32* __restrict__ wsorted, u32* __restrict__ key,
+                        u64* __restrict__ out, i64 n) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+        const u64 r = rec[i];
+        key[i] = (u32)r;
+        out[i] = (r >> 32) | ((u64)wsorted[i] << 32);
+    }
+}
+
+__global__ void unpack_k(const u64* __restrict__ rec, u32* __restrict__ lo, u32* __restrict__ hi, i64 n) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+        const u64 r = rec[i];
+        lo[i] = (u32)r;
+        hi[i] = (u32)(r >> 32);
+    }
 }
 
 __global__ void max_k(const u32* __restrict__ in, i64 n, u32* __restrict__ out) {
@@ -110,33 +125,38 @@ void build_graph_from_coo(Graph& g, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u
     } else {
         // Weighted: rows sorted by weight (ties in file order), so that for any
         // delta the light edges of a vertex are a prefix of its row. Two stable
-        // LSD sorts of a permutation: by weight, then by source.
-        DevBuf<u32> perm((size_t)nnz), palt((size_t)nnz), k2((size_t)nnz), kalt((size_t)nnz);
-        if (nnz) {
-            iota_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(perm.p, nnz);
-            PJ_LAUNCH_CHECK();
-            PJ_HIP(hipMemcpyAsync(k2.p, w->p, sizeof(u32) * (size_t)nnz, hipMemcpyDeviceToDevice, s));
-        }
+        // LSD sorts of whole records (no random gathers): by weight, carrying
+        // (src, dst), then by src, carrying (dst, w).
         const int wbits = max_bits_device(w->p, nnz, s);
-        u32 *kr, *pr;
-        radix_sort_pairs<u32>(k2.p, kalt.p, perm.p, palt.p, nnz, wbits, ws, s, &kr, &pr);
-        // keys := src[perm]
-        u32* keys = (kr == k2.p) ? kalt.p : k2.p;  // the free key buffer
-        u32* pfree = (pr == perm.p) ? palt.p : perm.p;
+        DevBuf<u64> rec((size_t)nnz), ralt((size_t)nnz);
+        DevBuf<u32> kalt((size_t)nnz);
+        u32* kr = w->p;
+        u64* rr = rec.p;
         if (nnz) {
-            gather_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(src.p, pr, keys, nnz);
+            pack_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(src.p, dst.p, rec.p, nnz);
+            PJ_LAUNCH_CHECK();
+            radix_sort_pairs<u64>(w->p, kalt.p, rec.p, ralt.p, nnz, wbits, ws, s, &kr, &rr);
+        }
+        // keys := src, records := (dst, w) in weight order
+        u32* skey = (kr == w->p) ? kalt.p : w->p;  // the free key buffer
+        u64* rfree = (rr == rec.p) ? ralt.p : rec.p;
+        if (nnz) {
+            split_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(rr, kr, skey, rfree, nnz);
             PJ_LAUNCH_CHECK();
         }
-        u32* kfree = (keys == k2.p) ? kalt.p : k2.p;
-        u32 *kr2, *pr2;
-        radix_sort_pairs<u32>(keys, kfree, pr, pfree, nnz, bits, ws, s, &kr2, &pr2);
+        PJ_HIP(hipStreamSynchronize(s));
+        src.release();
+        dst.release();
+        u32* kfree = (skey == kalt.p) ? w->p : kalt.p;
+        u64* rfree2 = (rfree == rec.p) ? ralt.p : rec.p;
+        u32* kr2 = skey;
+        u64* rr2 = rfree;
+        radix_sort_pairs<u64>(skey, kfree, rfree, rfree2, nnz, bits, ws, s, &kr2, &rr2);
         bounds(g, kr2, false);
         g.col.alloc((size_t)nnz);
         g.w.alloc((size_t)nnz);
         if (nnz) {
-            gather_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(dst.p, pr2, g.col.p, nnz);
-            PJ_LAUNCH_CHECK();
-            gather_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(w->p, pr2, g.w.p, nnz);
+            unpack_k<<<grid_for(nnz, 256, 8192), 256, 0, s>>>(rr2, g.col.p, g.w.p, nnz);
             PJ_LAUNCH_CHECK();
         }
         PJ_HIP(hipStreamSynchronize(s));

@@ -206,6 +206,7 @@ struct Graph {
 
     bool have_result = false;
     bool batch_stats = false;  // stats describe the last pj_sssp_batch
+    pj_load_stats load{};      // how the graph was built (pj_graph_load_stats)
     pj_stats stats{};
 
     const void* row_ptr() const { return off64 ? (const void*)row64.p : (const void*)row32.p; }
@@ -230,6 +231,7 @@ struct ParseResult {
     i64 nnz = 0;
     i64 max_id = -1;
     i64 bad_line = 0;  // 1-based, 0 = none
+    double h2d_ms = 0, parse_ms = 0;
 };
 // Parses `len` bytes of host text on the device; fills device COO.
 ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool weighted,

@@ -10,6 +10,8 @@
 // optional sign, digits; a non-numeric field reads as 0; extra columns are
 // ignored. Lines the reference turns into undefined behaviour (second field
 // missing, negative id, id overflow) are reported by byte offset.
+#include <chrono>
+
 #include "devutil.h"
 
 namespace pj {
@@ -136,11 +138,15 @@ ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool wei
                               DevBuf<u32>& dst, DevBuf<u32>& w) {
     hipStream_t s = ctx.stream;
     ParseResult r;
+    const auto t0 = std::chrono::steady_clock::now();
     const i64 nblocks = (len + PCHUNK - 1) / PCHUNK;
     const i64 padded = nblocks * PCHUNK + 64;
     DevBuf<uint8_t> text((size_t)padded);
-    PJ_HIP(hipMemsetAsync(text.p, 0, (size_t)padded, s));
+    PJ_HIP(hipMemsetAsync(text.p + len, 0, (size_t)(padded - len), s));
     if (len) PJ_HIP(hipMemcpyAsync(text.p, host_text, (size_t)len, hipMemcpyHostToDevice, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    const auto t1 = std::chrono::steady_clock::now();
+    r.h2d_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     DevBuf<u32> bcnt((size_t)(nblocks > 0 ? nblocks : 1));
     DevBuf<u64> boff((size_t)nblocks + 1);
     DevBuf<u64> scal(2);  // [0] = max id + 1, [1] = first bad byte offset
@@ -165,6 +171,7 @@ ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool wei
     }
     PJ_HIP(hipMemcpyAsync(h, scal.p, sizeof(h), hipMemcpyDeviceToHost, s));
     PJ_HIP(hipStreamSynchronize(s));
+    r.parse_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     r.nnz = (i64)total;
     r.max_id = (i64)h[0] - 1;
     if (h[1] != ~0ull) {

@@ -1,98 +1,136 @@
 // sort.hip — stable LSD radix sort of (key, value) pairs and CSR row bounds.
 //
 // This is the GPU form of coord2csr (ParallelJohnson.cpp:117-159): the
-// reference does a stable counting sort of the COO by src; here each 8-bit
-// digit pass is a stable counting sort over 4096-key tiles:
-//   hist    : per-tile digit histogram (LDS atomics)        -> hist[digit][tile]
-//   scan    : exclusive scan of hist in digit-major order     -> global offsets
-//   scatter : per tile, stable in-tile rank by wave64 ballot peer masks, then
-//             position = offset[digit][tile] + rank
-// Order inside a tile is (item j, wave, lane) = global index order, so every
-// pass is stable and the result keeps file order inside each row, exactly
-// like the reference's scatter loop :143-149.
+// reference does one stable counting sort of the COO by src; here the key is
+// split into P = ceil(bits / 8) digits of equal width (at most 8 bits: 22-bit
+// keys -> 8 + 7 + 7), and each digit pass is a stable counting sort over
+// tiles of TILE pairs:
+//   hist    : per-tile digit histogram (LDS atomics)          -> hist[digit][tile]
+//   scan    : exclusive scan of hist in digit-major order       -> global offsets
+//   scatter : the tile is ranked by digit inside each wave (ballot peer masks,
+//             wave-private running counters in LDS, no block barrier per
+//             item), reordered by digit in LDS, and written out in LDS order,
+//             so consecutive lanes store consecutive addresses of one digit's
+//             run: coalesced writes instead of 64 lanes hitting up to 256
+//             buckets.
+// Tile order is (wave, item, lane) = global index order, so every pass is
+// stable and the result keeps file order inside each row, exactly like the
+// reference's scatter loop :143-149.
 #include "devutil.h"
 
 namespace pj {
 
 namespace {
 
-constexpr int RB = 256;
-constexpr int RIPT = 16;
-constexpr int RTILE = RB * RIPT;
-constexpr int RW = RB / WAVE;
+constexpr int RB = 256;  // threads per tile block (4 waves)
+constexpr int RNW = RB / WAVE;
 
-__global__ __launch_bounds__(RB) void radix_hist_k(const u32* __restrict__ keys, i64 n, int shift,
+// pairs per thread: 32 with u32 values (8192-pair tiles, 64 KB of LDS), 16 with u64 values
+template <typename V>
+constexpr int ipt() {
+    return sizeof(V) == 8 ? 16 : 32;
+}
+template <typename V>
+constexpr int tile() {
+    return RB * ipt<V>();
+}
+
+template <int TILE>
+__global__ __launch_bounds__(RB) void radix_hist_k(const u32* __restrict__ keys, i64 n, int shift, u32 dmask,
                                                    u32* __restrict__ hist, i64 ntiles) {
     __shared__ u32 cnt[256];
     const int t = threadIdx.x;
     cnt[t] = 0;
     __syncthreads();
-    const i64 base = (i64)blockIdx.x * RTILE;
-#pragma unroll 4
-    for (int k = 0; k < RIPT; ++k) {
-        i64 i = base + (i64)k * RB + t;
-        if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255u], 1u);
-    }
+    const i64 base = (i64)blockIdx.x * TILE;
+    const i64 end = min(base + (i64)TILE, n);
+#pragma unroll 8
+    for (i64 i = base + t; i < end; i += RB) atomicAdd(&cnt[(keys[i] >> shift) & dmask], 1u);
     __syncthreads();
-    hist[(i64)t * ntiles + blockIdx.x] = cnt[t];
+    if ((u32)t <= dmask) hist[(i64)t * ntiles + blockIdx.x] = cnt[t];
 }
 
 template <typename V>
-__global__ __launch_bounds__(RB) void radix_scatter_k(const u32* __restrict__ keys,
-                                                      const V* __restrict__ vals,
-                                                      u32* __restrict__ kout, V* __restrict__ vout,
-                                                      i64 n, int shift, const u64* __restrict__ offs,
-                                                      i64 ntiles) {
-    __shared__ u32 cnt[RW][256];
-    __shared__ u32 pre[RW][256];
-    __shared__ u64 toff[256];
-    const int t = threadIdx.x, wid = wave_id();
-    const i64 base = (i64)blockIdx.x * RTILE;
-    toff[t] = offs[(i64)t * ntiles + blockIdx.x];
-#pragma unroll
-    for (int w = 0; w < RW; ++w) cnt[w][t] = 0;
+__global__ __launch_bounds__(RB) void radix_scatter_k(const u32* __restrict__ keys, const V* __restrict__ vals,
+                                                      u32* __restrict__ kout, V* __restrict__ vout, i64 n, int shift,
+                                                      int dbits, const u64* __restrict__ offs, i64 ntiles) {
+    constexpr int IPT = ipt<V>();
+    constexpr int TILE = tile<V>();
+    __shared__ u32 s_key[TILE];
+    __shared__ V s_val[TILE];
+    __shared__ u32 s_cnt[RNW][256];  // per-wave running counters, then per-wave exclusive bases
+    __shared__ u32 s_start[256];     // tile-local exclusive start of each digit
+    __shared__ u64 s_goff[256];      // global position of the tile's run of each digit
+    __shared__ u32 s_red[RNW];
+    const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+    const u32 dmask = (1u << dbits) - 1u;
+    const i64 base = (i64)blockIdx.x * TILE;
+    for (int d = lane; d < 256; d += WAVE) s_cnt[w][d] = 0;
+    if ((u32)t <= dmask) s_goff[t] = offs[(i64)t * ntiles + blockIdx.x];
 
-    u32 key[RIPT];
-    V val[RIPT];
+    // wave w owns tile items [w * 64 * IPT, (w + 1) * 64 * IPT), row j = 64 consecutive items
+    u32 key[IPT];
+    V val[IPT];
+    u32 rk[IPT];
+    const i64 wbase = base + (i64)w * WAVE * IPT + lane;
 #pragma unroll
-    for (int j = 0; j < RIPT; ++j) {
-        i64 i = base + (i64)j * RB + t;
+    for (int j = 0; j < IPT; ++j) {
+        const i64 i = wbase + (i64)j * WAVE;
         key[j] = i < n ? keys[i] : 0u;
         val[j] = i < n ? vals[i] : V(0);
     }
-    u32 run = 0;  // thread t owns digit t's running count inside this tile
-    __syncthreads();
-
-#pragma unroll 1
-    for (int j = 0; j < RIPT; ++j) {
-        const i64 i = base + (i64)j * RB + t;
-        const bool valid = i < n;
-        const u32 d = (key[j] >> shift) & 255u;
-        u64 peers = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
+    for (int j = 0; j < IPT; ++j) {
+        const bool valid = wbase + (i64)j * WAVE < n;
+        const u32 d = (key[j] >> shift) & dmask;
+        u64 peers = __ballot(valid);
+        for (int b = 0; b < dbits; ++b) {
             const bool bit = (d >> b) & 1u;
             const u64 m = __ballot(bit);
             peers &= bit ? m : ~m;
         }
-        const u32 rank_in = (u32)__popcll(peers & lanemask_lt());
-        if (valid && rank_in == 0) cnt[wid][d] = (u32)__popcll(peers);
-        __syncthreads();
-        {
-            u32 b = run;
-#pragma unroll
-            for (int w = 0; w < RW; ++w) {
-                pre[w][t] = b;
-                b += cnt[w][t];
-                cnt[w][t] = 0;
-            }
-            run = b;
+        const int leader = __ffsll((long long)peers) - 1;
+        u32 c = 0;
+        if (valid && lane == leader) {
+            c = s_cnt[w][d];
+            s_cnt[w][d] = c + (u32)__popcll(peers);
         }
-        __syncthreads();
-        if (valid) {
-            const u64 pos = toff[d] + pre[wid][d] + rank_in;
-            kout[pos] = key[j];
-            vout[pos] = val[j];
+        c = __shfl(c, leader < 0 ? 0 : leader, 64);
+        rk[j] = c + (u32)__popcll(peers & lanemask_lt());
+    }
+    __syncthreads();
+    // digit t: per-wave exclusive bases and the tile total, then the tile-local starts
+    u32 tot = 0;
+#pragma unroll
+    for (int q = 0; q < RNW; ++q) {
+        const u32 c = s_cnt[q][t];
+        s_cnt[q][t] = tot;
+        tot += c;
+    }
+    u32 all;
+    s_start[t] = block_excl_scan<RNW>(tot, s_red, all);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        if (wbase + (i64)j * WAVE < n) {
+            const u32 d = (key[j] >> shift) & dmask;
+            const u32 pos = s_start[d] + s_cnt[w][d] + rk[j];
+            s_key[pos] = key[j];
+            s_val[pos] = val[j];
+        }
+    }
+    __syncthreads();
+    // LDS order = digit-major, stable: lane-consecutive positions within a digit's run
+    const i64 count = min((i64)TILE, n - base);
+#pragma unroll 4
+    for (int k = 0; k < IPT; ++k) {
+        const int i = k * RB + t;
+        if (i < count) {
+            const u32 kk = s_key[i];
+            const u32 d = (kk >> shift) & dmask;
+            const u64 g = s_goff[d] + (u64)(i - (int)s_start[d]);
+            kout[g] = kk;
+            vout[g] = s_val[i];
         }
     }
 }
@@ -118,14 +156,20 @@ void radix_sort_pairs(u32* keys, u32* keys_alt, V* vals, V* vals_alt, i64 n, int
     u32 *kc = keys, *ka = keys_alt;
     V *vc = vals, *va = vals_alt;
     if (n > 0 && bits > 0) {
-        const i64 ntiles = (n + RTILE - 1) / RTILE;
+        constexpr i64 TILE = tile<V>();
+        const i64 ntiles = (n + TILE - 1) / TILE;
+        const int passes = (bits + 7) / 8;
+        const int dbits = (bits + passes - 1) / passes;  // equal digits: fewer buckets, longer runs
         ws.hist.ensure((size_t)(256 * ntiles));
         ws.offs.ensure((size_t)(256 * ntiles + 1));
-        for (int shift = 0; shift < bits; shift += 8) {
-            radix_hist_k<<<(unsigned)ntiles, RB, 0, s>>>(kc, n, shift, ws.hist.p, ntiles);
+        for (int shift = 0; shift < bits; shift += dbits) {
+            const int db = std::min(dbits, bits - shift);
+            const u32 dmask = (1u << db) - 1u;
+            const i64 nh = (i64)(dmask + 1) * ntiles;
+            radix_hist_k<tile<V>()><<<(unsigned)ntiles, RB, 0, s>>>(kc, n, shift, dmask, ws.hist.p, ntiles);
             PJ_LAUNCH_CHECK();
-            exclusive_scan_u32(ws.hist.p, ws.offs.p, 256 * ntiles, ws.scan, s);
-            radix_scatter_k<V><<<(unsigned)ntiles, RB, 0, s>>>(kc, vc, ka, va, n, shift, ws.offs.p, ntiles);
+            exclusive_scan_u32(ws.hist.p, ws.offs.p, nh, ws.scan, s);
+            radix_scatter_k<V><<<(unsigned)ntiles, RB, 0, s>>>(kc, vc, ka, va, n, shift, db, ws.offs.p, ntiles);
             PJ_LAUNCH_CHECK();
             std::swap(kc, ka);
             std::swap(vc, va);

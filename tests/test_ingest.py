@@ -1,0 +1,62 @@
+"""Ingestion (read_webgraph :66-105, coord2csr :117-159) at sizes
+where the radix sort runs several passes over many tiles: the CSR must equal a stable
+counting sort by src (file order inside rows, :143-149), and weighted rows must be
+ordered by (weight, file order) for delta-stepping. Also the Kronecker SNAP text
+writer used as the ingestion benchmark's input, round-tripped through the oracle
+parser and the CLI."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+INF = 100000
+
+
+@pytest.mark.parametrize("n,m,wmax", [(1 << 22, 20_000_000, 0), (3_000_000, 9_000_000, 70000),
+                                      (300, 100_000, 255), (70_000, 1_000_000, 1)])
+def test_csr_build_matches_stable_sort(ctx, n, m, wmax):
+    rng = np.random.default_rng(n + m)
+    src = rng.integers(0, n, m)
+    src[: m // 4] = rng.integers(0, 64, m // 4)  # heavy rows: long runs of one digit
+    dst = rng.integers(0, n, m)
+    w = rng.integers(1, wmax + 1, m).astype(np.uint32) if wmax else None
+    g = ctx.load_coo(src, dst, w=w, n=n)
+    row, col, wc = g.get_csr()
+    g.close()
+    order = np.lexsort((np.arange(m), w, src)) if wmax else np.argsort(src, kind="stable")
+    exp_row = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(src, minlength=n), out=exp_row[1:])
+    assert np.array_equal(row, exp_row)
+    assert np.array_equal(col.view(np.uint32), dst[order].astype(np.uint32))
+    if wmax:
+        assert np.array_equal(wc, w[order])
+
+
+def test_kronecker_text_roundtrip(ctx, pj, oracle, tmp_path):
+    """pj_kronecker_write_snap: the oracle parser reads back exactly the tuples of the
+    oracle's Kronecker restatement (generation order, both directions, weights), and the
+    CLI on that text equals the oracle BFS."""
+    for weighted in (False, True):
+        path = tmp_path / f"k10_{int(weighted)}.txt"
+        ctx.kronecker_write_snap(str(path), 10, 16, 5, weighted=weighted)
+        s, d, w, n = oracle.parse_snap(path.read_bytes(), weighted=weighted)
+        ks, kd, kw = oracle.kronecker(10, 16, 5, weighted=weighted)
+        assert np.array_equal(s, ks) and np.array_equal(d, kd)
+        if weighted:
+            assert np.array_equal(w, kw)
+    path = tmp_path / "k10_0.txt"
+    s, d, _, n = oracle.parse_snap(path.read_bytes())
+    row, col, _ = oracle.coo2csr(s, d, n)
+    out = tmp_path / "sol.txt"
+    r = subprocess.run([pj.cli_path(), str(path), str(int(s[0])), str(out)], capture_output=True, text=True,
+                       env=dict(os.environ, PJ_PHASES="1"), timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert out.read_bytes() == oracle.format_sol(oracle.bfs(row, col, int(s[0])))
+    assert "phase load: read" in r.stderr
+    g = ctx.load_snap(str(path))
+    st = g.load_stats()
+    assert st["text_bytes"] == path.stat().st_size and st["parse_ms"] > 0 and st["csr_ms"] > 0
+    g.close()
