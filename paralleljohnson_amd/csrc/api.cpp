@@ -8,7 +8,9 @@
 #include <cstdio>
 #include <thread>
 
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include "engine.h"
 #include "internal.h"
@@ -74,6 +76,49 @@ i64 out_degree(const Graph& g, i64 v) {
     u32 h[2];
     PJ_HIP(hipMemcpy(h, g.row32.p + v, sizeof(h), hipMemcpyDeviceToHost));
     return (i64)(h[1] - h[0]);
+}
+
+// The whole file in host memory, read by up to 16 threads with pread into an
+// uninitialised buffer (a zero-filled vector costs a second pass over the
+// bytes, and one reader thread page-faults the buffer alone). A missing or
+// unopenable file or a directory reads as empty (the reference does not check
+// its ifstream, :67); a file that shrinks while being read is PJ_ERR_IO.
+struct HostText {
+    std::unique_ptr<char[]> data;
+    int64_t len = 0;
+};
+
+HostText read_text_file(const char* path) {
+    HostText t;
+    struct stat sb;
+    if (stat(path, &sb) != 0 || !S_ISREG(sb.st_mode) || sb.st_size <= 0) return t;
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return t;
+    const int64_t size = (int64_t)sb.st_size;
+    t.data.reset(new char[(size_t)size]);
+    const int64_t piece = (int64_t)64 << 20;
+    const int64_t npieces = (size + piece - 1) / piece;
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(npieces, std::min(16u, std::thread::hardware_concurrency())));
+    std::atomic<int64_t> next{0}, got{0};
+    std::vector<std::thread> th;
+    for (int k = 0; k < nt; ++k)
+        th.emplace_back([&] {
+            for (int64_t c; (c = next.fetch_add(1)) < npieces;) {
+                const int64_t off = c * piece, want = std::min(piece, size - off);
+                int64_t done = 0;
+                while (done < want) {
+                    const ssize_t r = pread(fd, t.data.get() + off + done, (size_t)(want - done), (off_t)(off + done));
+                    if (r <= 0) break;
+                    done += r;
+                }
+                got.fetch_add(done);
+            }
+        });
+    for (auto& x : th) x.join();
+    close(fd);
+    if (got.load() != size) throw Error(PJ_ERR_IO, std::string("short read of ") + path);
+    t.len = size;
+    return t;
 }
 
 int finish_graph(pj_ctx* ctx, std::unique_ptr<pj_graph>& pg, pj_graph** out) {
@@ -309,21 +354,11 @@ int pj_load_snap(pj_ctx* ctx, const char* path, int weighted, pj_graph** out) {
     if (!ctx || !path || !out) return arg_error("pj_load_snap: bad argument");
     return guarded([&] {
         const auto t0 = std::chrono::steady_clock::now();
-        std::vector<char> buf;
-        struct stat sb;
         // A missing or unreadable file (or a directory) reads as empty, like the
         // reference's unchecked ifstream (:67): N = 0, header-only sol_file.
-        FILE* f = (stat(path, &sb) == 0 && S_ISREG(sb.st_mode)) ? std::fopen(path, "rb") : nullptr;
-        if (f) {
-            if (sb.st_size > 0) {
-                buf.resize((size_t)sb.st_size);
-                size_t got = std::fread(buf.data(), 1, (size_t)sb.st_size, f);
-                buf.resize(got);
-            }
-            std::fclose(f);
-        }
+        HostText text = read_text_file(path);
         const double read_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        const int rc = pj_load_snap_buffer(ctx, buf.data(), (int64_t)buf.size(), weighted, out);
+        const int rc = pj_load_snap_buffer(ctx, text.data.get(), text.len, weighted, out);
         if (rc == PJ_OK) (*out)->g.load.read_ms = read_ms;
         return rc;
     });
@@ -1032,19 +1067,9 @@ int pj_part_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_par
     *out = nullptr;
     return guarded([&] {
         bind(ctx->c);
-        std::vector<char> buf;
-        struct stat sb;
-        // missing / unreadable file: empty graph, as pj_load_snap (reference :67)
-        FILE* f = (stat(path, &sb) == 0 && S_ISREG(sb.st_mode)) ? std::fopen(path, "rb") : nullptr;
-        if (f) {
-            if (sb.st_size > 0) {
-                buf.resize((size_t)sb.st_size);
-                buf.resize(std::fread(buf.data(), 1, (size_t)sb.st_size, f));
-            }
-            std::fclose(f);
-        }
+        HostText text = read_text_file(path);  // missing file: empty graph, as pj_load_snap (:67)
         DevBuf<u32> src, dst, w;
-        ParseResult r = parse_snap_device(ctx->c, buf.data(), (i64)buf.size(), false, src, dst, w);
+        ParseResult r = parse_snap_device(ctx->c, text.data.get(), text.len, false, src, dst, w);
         if (r.bad_line) {
             set_error("edge list line " + std::to_string(r.bad_line) +
                       ": second field missing, negative id or id out of range "

@@ -21,6 +21,7 @@ namespace {
 constexpr int PB = 256;
 constexpr int PSEG = 64;
 constexpr i64 PCHUNK = (i64)PB * PSEG;
+constexpr i64 PTAIL = 512;  // bytes past the chunk staged with it (lines crossing the chunk end)
 constexpr i64 ID_LIMIT = 2147483646;  // N = max + 1 must fit the reference's int (:319)
 
 __device__ __forceinline__ bool is_digit(u32 c) { return (c - (u32)'0') < 10u; }
@@ -30,13 +31,12 @@ __device__ __forceinline__ bool is_blank(u32 c) {
 
 // Bitmask of positions p in [seg, seg+64) with text[p] a digit and
 // (p == 0 or text[p-1] == '\n'). The buffer is zero-padded to a multiple of
-// 64 bytes (+64), and '\0' is neither a digit nor a newline.
-__device__ __forceinline__ u64 line_start_mask(const uint8_t* __restrict__ text, i64 seg) {
-    const uint4* p4 = reinterpret_cast<const uint4*>(text + seg);
+// 64 bytes (+PTAIL), and '\0' is neither a digit nor a newline. `prev` is
+// text[seg - 1] ('\n' at seg 0).
+__device__ __forceinline__ u64 line_start_mask(const uint4* __restrict__ p4, u32 prev) {
     uint4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
     u32 words[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
                      a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-    u32 prev = seg == 0 ? (u32)'\n' : (u32)text[seg - 1];
     u64 mask = 0;
 #pragma unroll
     for (int k = 0; k < 64; ++k) {
@@ -47,9 +47,21 @@ __device__ __forceinline__ u64 line_start_mask(const uint8_t* __restrict__ text,
     return mask;
 }
 
+// Bytes of the text as one lane's parser sees them: the block's chunk and a tail
+// staged in LDS, anything further (a line running past the tail) from global.
+struct Bytes {
+    const uint8_t* __restrict__ lds;
+    const uint8_t* __restrict__ glob;
+    i64 base, staged;
+    __device__ __forceinline__ u32 operator[](i64 p) const {
+        const i64 q = p - base;
+        return q < staged ? (u32)lds[q] : (u32)glob[p];
+    }
+};
+
 // One `>> int` extraction. 1 = read, 0 = failed on a non-blank (value 0),
 // -1 = nothing but blanks before end of line, -2 = overflow.
-__device__ __forceinline__ int extract(const uint8_t* __restrict__ t, i64 len, i64& p, i64& out) {
+__device__ __forceinline__ int extract(const Bytes& t, i64 len, i64& p, i64& out) {
     while (p < len && is_blank(t[p])) ++p;
     if (p >= len || t[p] == '\n') return -1;
     bool neg = false;
@@ -64,13 +76,12 @@ __device__ __forceinline__ int extract(const uint8_t* __restrict__ t, i64 len, i
     }
     i64 acc = 0;
     bool ovf = false;
-    while (p < len && is_digit(t[p])) {
-        acc = acc * 10 + (t[p] - '0');
+    for (u32 d; p < len && is_digit(d = t[p]); ++p) {
+        acc = acc * 10 + (d - '0');
         if (acc > 4294967295ll) {
             ovf = true;
             acc = 4294967295ll;
         }
-        ++p;
     }
     if (ovf) return -2;
     out = neg ? -acc : acc;
@@ -82,19 +93,35 @@ __global__ __launch_bounds__(PB) void parse_count_k(const uint8_t* __restrict__ 
     __shared__ u32 lds[PB / WAVE];
     const i64 seg = (i64)blockIdx.x * PCHUNK + (i64)threadIdx.x * PSEG;
     u32 c = 0;
-    if (seg < len) c = (u32)__popcll(line_start_mask(text, seg));
+    if (seg < len)
+        c = (u32)__popcll(line_start_mask(reinterpret_cast<const uint4*>(text + seg),
+                                          seg == 0 ? (u32)'\n' : (u32)text[seg - 1]));
     c = block_sum<PB / WAVE>(c, lds);
     if (threadIdx.x == 0) block_cnt[blockIdx.x] = c;
 }
 
+// The block's 16 KiB chunk plus a PTAIL-byte tail is loaded into LDS with
+// coalesced 16-byte loads; every lane then parses the lines that start in its
+// 64-byte segment from LDS (byte loads from global were stride-64 across the
+// wave: one cache line per lane per byte).
 __global__ __launch_bounds__(PB) void parse_lines_k(const uint8_t* __restrict__ text, i64 len, int weighted,
                                                     const u64* __restrict__ block_off, u32* __restrict__ src,
                                                     u32* __restrict__ dst, u32* __restrict__ w,
                                                     u64* __restrict__ maxid, u64* __restrict__ errpos) {
     __shared__ u64 lds[PB / WAVE];
-    const i64 seg = (i64)blockIdx.x * PCHUNK + (i64)threadIdx.x * PSEG;
+    __shared__ uint4 stage[(PCHUNK + PTAIL) / 16];
+    const i64 base = (i64)blockIdx.x * PCHUNK;
+    const uint4* g4 = reinterpret_cast<const uint4*>(text + base);
+    for (int k = threadIdx.x; k < (int)((PCHUNK + PTAIL) / 16); k += PB) stage[k] = g4[k];
+    __syncthreads();
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage);
+    const Bytes t{sb, text, base, PCHUNK + PTAIL};
+    const i64 seg = base + (i64)threadIdx.x * PSEG;
     u64 mask = 0;
-    if (seg < len) mask = line_start_mask(text, seg);
+    if (seg < len) {
+        const u32 prev = seg == 0 ? (u32)'\n' : (threadIdx.x ? (u32)sb[threadIdx.x * PSEG - 1] : (u32)text[seg - 1]);
+        mask = line_start_mask(reinterpret_cast<const uint4*>(sb + threadIdx.x * PSEG), prev);
+    }
     u64 tot;
     u64 idx = block_off[blockIdx.x] + block_excl_scan<PB / WAVE>((u64)__popcll(mask), lds, tot);
     i64 mx = -1;
@@ -103,15 +130,15 @@ __global__ __launch_bounds__(PB) void parse_lines_k(const uint8_t* __restrict__ 
         mask &= mask - 1;
         const i64 start = seg + b;
         i64 p = start, u = 0, v = 0, wt = 1;
-        int r = extract(text, len, p, u);
+        int r = extract(t, len, p, u);
         bool bad = (r != 1) || u > ID_LIMIT;
         if (!bad) {
-            r = extract(text, len, p, v);
+            r = extract(t, len, p, v);
             bad = r < 0 || v < 0 || v > ID_LIMIT;
             if (!bad && weighted) {
                 if (r == 0) wt = 0;  // stream failed: the weight extraction stores nothing -> 0
                 else {
-                    int r3 = extract(text, len, p, wt);
+                    int r3 = extract(t, len, p, wt);
                     bad = r3 < 0 || wt < 0;
                 }
             }
@@ -140,7 +167,7 @@ ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool wei
     ParseResult r;
     const auto t0 = std::chrono::steady_clock::now();
     const i64 nblocks = (len + PCHUNK - 1) / PCHUNK;
-    const i64 padded = nblocks * PCHUNK + 64;
+    const i64 padded = nblocks * PCHUNK + PTAIL;
     DevBuf<uint8_t> text((size_t)padded);
     PJ_HIP(hipMemsetAsync(text.p + len, 0, (size_t)(padded - len), s));
     if (len) PJ_HIP(hipMemcpyAsync(text.p, host_text, (size_t)len, hipMemcpyHostToDevice, s));

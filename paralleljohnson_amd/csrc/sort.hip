@@ -5,7 +5,7 @@
 // split into P = ceil(bits / 8) digits of equal width (at most 8 bits: 22-bit
 // keys -> 8 + 7 + 7), and each digit pass is a stable counting sort over
 // tiles of TILE pairs:
-//   hist    : per-tile digit histogram (LDS atomics)          -> hist[digit][tile]
+//   hist    : per-tile digit histogram (wave ballot counting)  -> hist[digit][tile]
 //   scan    : exclusive scan of hist in digit-major order       -> global offsets
 //   scatter : the tile is ranked by digit inside each wave (ballot peer masks,
 //             wave-private running counters in LDS, no block barrier per
@@ -35,19 +35,39 @@ constexpr int tile() {
     return RB * ipt<V>();
 }
 
+// Per-tile digit histogram. Each wave counts 64 keys per step with ballot peer
+// masks (one LDS update per distinct digit, by its leader lane) into wave-private
+// counters: no LDS atomics, which serialise when many lanes share a digit (heavy
+// rows, presorted runs).
 template <int TILE>
-__global__ __launch_bounds__(RB) void radix_hist_k(const u32* __restrict__ keys, i64 n, int shift, u32 dmask,
+__global__ __launch_bounds__(RB) void radix_hist_k(const u32* __restrict__ keys, i64 n, int shift, int dbits,
                                                    u32* __restrict__ hist, i64 ntiles) {
-    __shared__ u32 cnt[256];
-    const int t = threadIdx.x;
-    cnt[t] = 0;
+    __shared__ u32 cnt[RNW][256];
+    const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+    const u32 dmask = (1u << dbits) - 1u;
+    for (int d = lane; d < 256; d += WAVE) cnt[w][d] = 0;
+    const i64 wbase = (i64)blockIdx.x * TILE + (i64)w * (TILE / RNW) + lane;
+    constexpr int ROWS = TILE / RB;
+#pragma unroll 4
+    for (int j = 0; j < ROWS; ++j) {
+        const i64 i = wbase + (i64)j * WAVE;
+        const bool valid = i < n;
+        const u32 d = valid ? (keys[i] >> shift) & dmask : 0u;
+        u64 peers = __ballot(valid);
+        for (int b = 0; b < dbits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const u64 m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        if (valid && lane == __ffsll((long long)peers) - 1) cnt[w][d] += (u32)__popcll(peers);
+    }
     __syncthreads();
-    const i64 base = (i64)blockIdx.x * TILE;
-    const i64 end = min(base + (i64)TILE, n);
-#pragma unroll 8
-    for (i64 i = base + t; i < end; i += RB) atomicAdd(&cnt[(keys[i] >> shift) & dmask], 1u);
-    __syncthreads();
-    if ((u32)t <= dmask) hist[(i64)t * ntiles + blockIdx.x] = cnt[t];
+    if ((u32)t <= dmask) {
+        u32 c = 0;
+#pragma unroll
+        for (int q = 0; q < RNW; ++q) c += cnt[q][t];
+        hist[(i64)t * ntiles + blockIdx.x] = c;
+    }
 }
 
 template <typename V>
@@ -166,7 +186,7 @@ void radix_sort_pairs(u32* keys, u32* keys_alt, V* vals, V* vals_alt, i64 n, int
             const int db = std::min(dbits, bits - shift);
             const u32 dmask = (1u << db) - 1u;
             const i64 nh = (i64)(dmask + 1) * ntiles;
-            radix_hist_k<tile<V>()><<<(unsigned)ntiles, RB, 0, s>>>(kc, n, shift, dmask, ws.hist.p, ntiles);
+            radix_hist_k<tile<V>()><<<(unsigned)ntiles, RB, 0, s>>>(kc, n, shift, db, ws.hist.p, ntiles);
             PJ_LAUNCH_CHECK();
             exclusive_scan_u32(ws.hist.p, ws.offs.p, nh, ws.scan, s);
             radix_scatter_k<V><<<(unsigned)ntiles, RB, 0, s>>>(kc, vc, ka, va, n, shift, db, ws.offs.p, ntiles);

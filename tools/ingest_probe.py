@@ -2,7 +2,7 @@
 path, :66-159): writes the web-Google-shaped synthetic and a Kronecker text file
 (generation order) to a scratch dir, then times `parallel_johnson` end to end with
 PJ_PHASES=1 and prints one JSON line per input.
-Usage: python tools/ingest_probe.py [kron_scale ...]   (default 22)"""
+Usage: python tools/ingest_probe.py [kron_scale ...] [--keep]   (default 22)"""
 import json
 import os
 import subprocess
@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.join(R, "tests"))
 import paralleljohnson_amd as pj  # noqa: E402
 from helpers import csr_to_text  # noqa: E402
 
-scales = [int(a) for a in sys.argv[1:]] or [22]
+keep = "--keep" in sys.argv  # leave the text files (and print their paths) for a profiler run
+scales = [int(a) for a in sys.argv[1:] if a.isdigit()] or [22]
 td = tempfile.mkdtemp(dir=os.environ.get("PJ_SCRATCH", "/tmp"))
 ctx = pj.Context(0)
 inputs = []
@@ -45,4 +46,7 @@ for name, path, src in inputs:
                       "time_to_solution_s": round(wall, 3), "time_line": r.stdout.strip(), "phases": phases}),
           flush=True)
     os.remove(out)
-    os.remove(path)
+    if keep:
+        print(f"# kept {path}", flush=True)
+    else:
+        os.remove(path)
