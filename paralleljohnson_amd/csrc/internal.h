@@ -106,8 +106,8 @@ void exclusive_scan_u64(const u64* in, u64* out, i64 n, ScanWs& ws, hipStream_t 
 // Stable LSD radix sort of (key, value) pairs by key; `bits` = key width to
 // sort. Returns through `*kout/*vout` which of the two buffers holds the result.
 struct SortWs {
-    DevBuf<u32> hist;
-    DevBuf<u64> offs;
+    DevBuf<u32> hist, csum;  // per-tile digit counts [tile][256], per-chunk digit sums [digit][chunk]
+    DevBuf<u64> offs, cpre;  // per-tile run starts [tile][256], scanned chunk sums
     ScanWs scan;
 };
 template <typename V>

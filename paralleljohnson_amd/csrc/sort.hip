@@ -5,8 +5,9 @@
 // split into P = ceil(bits / 8) digits of equal width (at most 8 bits: 22-bit
 // keys -> 8 + 7 + 7), and each digit pass is a stable counting sort over
 // tiles of TILE pairs:
-//   hist    : per-tile digit histogram (wave ballot counting)  -> hist[digit][tile]
-//   scan    : exclusive scan of hist in digit-major order       -> global offsets
+//   hist    : per-tile digit histograms (wave ballot counting)  -> hist[tile][digit],
+//             and per chunk of tiles                             -> csum[digit][chunk]
+//   scan    : exclusive scan of csum in digit-major order, then per tile -> offs[tile][digit]
 //   scatter : the tile is ranked by digit inside each wave (ballot peer masks,
 //             wave-private running counters in LDS, no block barrier per
 //             item), reordered by digit in LDS, and written out in LDS order,
@@ -24,49 +25,101 @@ namespace {
 
 constexpr int RB = 256;  // threads per tile block (4 waves)
 constexpr int RNW = RB / WAVE;
+#ifndef PJ_SORT_XCD
+#define PJ_SORT_XCD 1
+#endif
+#ifndef PJ_SORT_IPT32
+#define PJ_SORT_IPT32 16
+#endif
+#ifndef PJ_SORT_CHUNK
+#define PJ_SORT_CHUNK 16
+#endif
+constexpr int HC = PJ_SORT_CHUNK;  // tiles per histogram block (one chunk)
+#ifndef PJ_SORT_IPT64
+#define PJ_SORT_IPT64 16
+#endif
 
-// pairs per thread: 32 with u32 values (8192-pair tiles, 64 KB of LDS), 16 with u64 values
+// Tile of a block. With PJ_SORT_XCD, consecutive tiles go to blocks b, b + 8, ...
+// (one XCD under round-robin placement, speed only): the line shared by tile t's
+// run of a digit and tile t + 1's run is then written through one L2.
+__device__ __forceinline__ i64 tile_of(i64 ntiles) {
+    const i64 b = blockIdx.x;
+    if (!PJ_SORT_XCD || ntiles < 64) return b;
+    const i64 per = ntiles / 8, rem = ntiles % 8;  // XCD x gets per (+1 for x < rem) consecutive tiles
+    const i64 x = b % 8, k = b / 8;  // blocks with b % 8 == x number exactly per + (x < rem)
+    return x * per + (x < rem ? x : rem) + k;
+}
+
+// pairs per thread: 16 (4096-pair tiles; 32 KB of LDS with u32 values, 48 KB with u64):
+// 32 gave longer digit runs but half the resident tiles per CU and measured slower
 template <typename V>
 constexpr int ipt() {
-    return sizeof(V) == 8 ? 16 : 32;
+    return sizeof(V) == 8 ? PJ_SORT_IPT64 : PJ_SORT_IPT32;
 }
 template <typename V>
 constexpr int tile() {
     return RB * ipt<V>();
 }
 
-// Per-tile digit histogram. Each wave counts 64 keys per step with ballot peer
-// masks (one LDS update per distinct digit, by its leader lane) into wave-private
-// counters: no LDS atomics, which serialise when many lanes share a digit (heavy
-// rows, presorted runs).
+// Per-tile digit histograms of a chunk of HC consecutive tiles. Each wave counts
+// 64 keys per step with ballot peer masks (one LDS update per distinct digit, by
+// its leader lane) into wave-private counters: no LDS atomics, which serialise
+// when many lanes share a digit (heavy rows, presorted runs). Outputs are laid
+// out for coalesced stores: hist[tile][256] (tile-major) and the chunk's digit
+// sums csum[digit][chunk] (one scattered store per digit per HC tiles; a
+// digit-major hist[digit][tile] costs one partial-line store per digit per tile).
 template <int TILE>
 __global__ __launch_bounds__(RB) void radix_hist_k(const u32* __restrict__ keys, i64 n, int shift, int dbits,
-                                                   u32* __restrict__ hist, i64 ntiles) {
+                                                   u32* __restrict__ hist, u32* __restrict__ csum, i64 ntiles,
+                                                   i64 nchunks) {
     __shared__ u32 cnt[RNW][256];
     const int t = threadIdx.x, lane = lane_id(), w = wave_id();
     const u32 dmask = (1u << dbits) - 1u;
-    for (int d = lane; d < 256; d += WAVE) cnt[w][d] = 0;
-    const i64 wbase = (i64)blockIdx.x * TILE + (i64)w * (TILE / RNW) + lane;
     constexpr int ROWS = TILE / RB;
-#pragma unroll 4
-    for (int j = 0; j < ROWS; ++j) {
-        const i64 i = wbase + (i64)j * WAVE;
-        const bool valid = i < n;
-        const u32 d = valid ? (keys[i] >> shift) & dmask : 0u;
-        u64 peers = __ballot(valid);
-        for (int b = 0; b < dbits; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const u64 m = __ballot(bit);
-            peers &= bit ? m : ~m;
+    u32 chunk_sum = 0;
+    const i64 t0 = (i64)blockIdx.x * HC, t1 = min(t0 + HC, ntiles);
+    for (i64 tl = t0; tl < t1; ++tl) {
+        for (int d = lane; d < 256; d += WAVE) cnt[w][d] = 0;
+        const i64 wbase = tl * TILE + (i64)w * (TILE / RNW) + lane;
+        u32 key[ROWS];  // every load issued before the first ballot
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) {
+            const i64 i = wbase + (i64)j * WAVE;
+            key[j] = i < n ? keys[i] : 0u;
         }
-        if (valid && lane == __ffsll((long long)peers) - 1) cnt[w][d] += (u32)__popcll(peers);
-    }
-    __syncthreads();
-    if ((u32)t <= dmask) {
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) {
+            const bool valid = wbase + (i64)j * WAVE < n;
+            const u32 d = (key[j] >> shift) & dmask;
+            u64 peers = __ballot(valid);
+            for (int b = 0; b < dbits; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const u64 m = __ballot(bit);
+                peers &= bit ? m : ~m;
+            }
+            if (valid && lane == __ffsll((long long)peers) - 1) cnt[w][d] += (u32)__popcll(peers);
+        }
+        __syncthreads();
         u32 c = 0;
 #pragma unroll
         for (int q = 0; q < RNW; ++q) c += cnt[q][t];
-        hist[(i64)t * ntiles + blockIdx.x] = c;
+        hist[tl * 256 + t] = c;
+        chunk_sum += c;
+        __syncthreads();  // the counters are reset for the next tile
+    }
+    if ((u32)t <= dmask) csum[(i64)t * nchunks + blockIdx.x] = chunk_sum;
+}
+
+// offs[tile][digit] = (digit-major exclusive prefix of the chunk sums) + the digit's
+// counts in the chunk's earlier tiles: the global start of the tile's run of each digit.
+__global__ __launch_bounds__(RB) void radix_offs_k(const u32* __restrict__ hist, const u64* __restrict__ cpre,
+                                                   u64* __restrict__ offs, i64 ntiles, i64 nchunks) {
+    const int t = threadIdx.x;
+    const i64 t0 = (i64)blockIdx.x * HC, t1 = min(t0 + HC, ntiles);
+    u64 run = cpre[(i64)t * nchunks + blockIdx.x];
+    for (i64 tl = t0; tl < t1; ++tl) {
+        offs[tl * 256 + t] = run;
+        run += hist[tl * 256 + t];
     }
 }
 
@@ -84,9 +137,10 @@ __global__ __launch_bounds__(RB) void radix_scatter_k(const u32* __restrict__ ke
     __shared__ u32 s_red[RNW];
     const int t = threadIdx.x, lane = lane_id(), w = wave_id();
     const u32 dmask = (1u << dbits) - 1u;
-    const i64 base = (i64)blockIdx.x * TILE;
+    const i64 tl = tile_of(ntiles);
+    const i64 base = tl * TILE;
     for (int d = lane; d < 256; d += WAVE) s_cnt[w][d] = 0;
-    if ((u32)t <= dmask) s_goff[t] = offs[(i64)t * ntiles + blockIdx.x];
+    s_goff[t] = offs[tl * 256 + t];
 
     // wave w owns tile items [w * 64 * IPT, (w + 1) * 64 * IPT), row j = 64 consecutive items
     u32 key[IPT];
@@ -180,15 +234,20 @@ void radix_sort_pairs(u32* keys, u32* keys_alt, V* vals, V* vals_alt, i64 n, int
         const i64 ntiles = (n + TILE - 1) / TILE;
         const int passes = (bits + 7) / 8;
         const int dbits = (bits + passes - 1) / passes;  // equal digits: fewer buckets, longer runs
+        const i64 nchunks = (ntiles + HC - 1) / HC;
         ws.hist.ensure((size_t)(256 * ntiles));
-        ws.offs.ensure((size_t)(256 * ntiles + 1));
+        ws.csum.ensure((size_t)(256 * nchunks));
+        ws.offs.ensure((size_t)(256 * std::max(ntiles, nchunks) + 1));
+        ws.cpre.ensure((size_t)(256 * nchunks + 1));
         for (int shift = 0; shift < bits; shift += dbits) {
             const int db = std::min(dbits, bits - shift);
-            const u32 dmask = (1u << db) - 1u;
-            const i64 nh = (i64)(dmask + 1) * ntiles;
-            radix_hist_k<tile<V>()><<<(unsigned)ntiles, RB, 0, s>>>(kc, n, shift, db, ws.hist.p, ntiles);
+            const i64 nh = (i64)(1 << db) * nchunks;
+            radix_hist_k<tile<V>()><<<(unsigned)nchunks, RB, 0, s>>>(kc, n, shift, db, ws.hist.p, ws.csum.p, ntiles,
+                                                                     nchunks);
             PJ_LAUNCH_CHECK();
-            exclusive_scan_u32(ws.hist.p, ws.offs.p, nh, ws.scan, s);
+            exclusive_scan_u32(ws.csum.p, ws.cpre.p, nh, ws.scan, s);
+            radix_offs_k<<<(unsigned)nchunks, RB, 0, s>>>(ws.hist.p, ws.cpre.p, ws.offs.p, ntiles, nchunks);
+            PJ_LAUNCH_CHECK();
             radix_scatter_k<V><<<(unsigned)ntiles, RB, 0, s>>>(kc, vc, ka, va, n, shift, db, ws.offs.p, ntiles);
             PJ_LAUNCH_CHECK();
             std::swap(kc, ka);
