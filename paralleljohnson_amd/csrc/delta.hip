@@ -831,8 +831,8 @@ constexpr int V2_HTILE = DB * 4;
 #ifndef PJ_V2_PCH
 #define PJ_V2_PCH 256
 #endif
-constexpr u32 V2_PLMAX = PJ_V2_PLMAX;  // pull rounds: longer light rows go to v2_pull_long_k
-constexpr u32 V2_PCH = PJ_V2_PCH;      // light edges per v2_pull_long_k work item
+constexpr u32 V2_PLMAX = PJ_V2_PLMAX;  // pull rounds: longer light rows go to v2_pull_long_body
+constexpr u32 V2_PCH = PJ_V2_PCH;      // light edges per v2_pull_long_body work item
 
 struct alignas(64) V2Line {
     u64 v;
@@ -1017,7 +1017,7 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
         }
         if (v2_slot_sum(a.ctl->cnt[cin]) == 0) return;  // empty frontier (block-uniform)
         if (v2_slot_edges(a.ctl->cnt[cin]) > pull_thresh) {
-            // v2_pull_light_k relaxed this round; it could not clear fin (other waves
+            // v2_pull_round_k relaxed this round; it could not clear fin (other waves
             // were reading it), so clear it here
             for (i64 wi = (i64)blockIdx.x * DB + threadIdx.x; wi < a.nwords; wi += (i64)gridDim.x * DB) fin[wi] = 0;
             return;
@@ -1348,18 +1348,12 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
 // its own vertex. The wave owns its PSC words of fout (written whole) and of mb
 // (new members add their heavy / light degrees to ctl.mh).
 template <typename Off>
-__global__ __launch_bounds__(DB) void v2_pull_light_k(V2Args a, const Off* __restrict__ row,
-                                                      const u64* __restrict__ fin, u64* __restrict__ fout, int cin,
-                                                      u64 pull_thresh) {
+__device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* __restrict__ row,
+                                                   const u64* __restrict__ fin, u64* __restrict__ fout, u32* newb,
+                                                   u32& newc, u64& fe, u64& mh, u64& ml) {
     constexpr int NWV = DB / WAVE;
-    __shared__ u32 s_new[NWV][2 * PSC];
-    __shared__ u64 red[NWV];
-    if (v2_slot_sum(a.ctl->cnt[cin]) == 0 || v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) return;
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    u32* newb = s_new[wave_id()];
-    u32 newc = 0;
-    u64 fe = 0, mh = 0, ml = 0;
     const i64 nsc = (a.nwords + PSC - 1) / PSC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
         const i64 gbase = sc * PSC;
@@ -1412,7 +1406,7 @@ __global__ __launch_bounds__(DB) void v2_pull_light_k(V2Args a, const Off* __res
                 cur = d0;
                 k = (Off)a.lrow[v];
                 ls = (u32)(a.lrow[v + 1] - a.lrow[v]);
-                e = ls > V2_PLMAX ? k : k + (Off)ls;  // long rows: v2_pull_long_k
+                e = ls > V2_PLMAX ? k : k + (Off)ls;  // long rows: v2_pull_long_body
             }
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
             bool go = act && k < lim, done = !act || k >= e;
@@ -1467,30 +1461,26 @@ __global__ __launch_bounds__(DB) void v2_pull_light_k(V2Args a, const Off* __res
                 }
             }
         }
-        if (lane < PSC && gbase + lane < a.nwords)
-            fout[gbase + lane] = (u64)newb[2 * lane] | ((u64)newb[2 * lane + 1] << 32);
+        // fout is zero at the start of a round and v2_pull_long_body may set bits of
+        // the same words (long-row vertices) concurrently: OR the word in
+        if (lane < PSC && gbase + lane < a.nwords) {
+            const u64 word = (u64)newb[2 * lane] | ((u64)newb[2 * lane + 1] << 32);
+            if (word) atomicOr(fout + gbase + lane, word);
+        }
     }
-    v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
-    v2_flush2(mh, ml, a.ctl->mh, red);
 }
 
 // Long light rows (lsplit > V2_PLMAX, the high-degree vertices) are left out of
-// v2_pull_light_k: one lane scanning tens of thousands of edges would hold up
+// v2_pull_light_body: one lane scanning tens of thousands of edges would hold up
 // its wave. Their pull runs here instead, over a static list of (vertex, chunk
 // of V2_PCH light edges) built once per delta; a wave takes a chunk, skips it
 // when even its lightest edge cannot help, and folds the result in with
 // atomicMin (the vertex's chunks run in different waves).
-template <typename Off>
-__global__ __launch_bounds__(DB) void v2_pull_long_k(V2Args a, const Off* __restrict__ row,
-                                                     const u64* __restrict__ fin, u64* __restrict__ fout, int cin,
-                                                     u64 pull_thresh, const u32* __restrict__ lcv,
-                                                     const u32* __restrict__ lcc, u64 nlc) {
-    __shared__ u64 red[DB / WAVE];
-    if (v2_slot_sum(a.ctl->cnt[cin]) == 0 || v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) return;
+__device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __restrict__ fin, u64* __restrict__ fout,
+                                                  const u32* __restrict__ lcv, const u32* __restrict__ lcc, u64 nlc,
+                                                  u32& newc, u64& fe) {
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    u32 newc = 0;
-    u64 fe = 0;
     for (u64 it = (u64)blockIdx.x * (DB / WAVE) + wave_id(); it < nlc; it += (u64)gridDim.x * (DB / WAVE)) {
         const u32 v = lcv[it];
         const int32_t d0 = dist_now(a.dist + v);
@@ -1534,7 +1524,26 @@ __global__ __launch_bounds__(DB) void v2_pull_long_k(V2Args a, const Off* __rest
             }
         }
     }
+}
+
+// Pull form of a light round, one launch: the chunks of the long light rows
+// (v2_pull_long_body) and the short rows (v2_pull_light_body) over the whole
+// grid. The two touch disjoint vertices; frontier words are OR-ed in.
+template <typename Off>
+__global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __restrict__ row,
+                                                      const u64* __restrict__ fin, u64* __restrict__ fout, int cin,
+                                                      u64 pull_thresh, const u32* __restrict__ lcv,
+                                                      const u32* __restrict__ lcc, u64 nlc) {
+    constexpr int NWV = DB / WAVE;
+    __shared__ u32 s_new[NWV][2 * PSC];
+    __shared__ u64 red[NWV];
+    if (v2_slot_sum(a.ctl->cnt[cin]) == 0 || v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) return;
+    u32 newc = 0;
+    u64 fe = 0, mh = 0, ml = 0;
+    if (nlc) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe);
+    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml);
     v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+    v2_flush2(mh, ml, a.ctl->mh, red);
 }
 
 // static chunk list of the long light rows: count, then append (order is irrelevant)
@@ -1967,7 +1976,10 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             st.levels++;
             PJ_HIP(hipMemsetAsync(w.ctl.p->mh, 0, sizeof(w.ctl.p->mh), s));
             // light rounds until the band's frontier is empty
-            int K = PJ_V2_STATS ? 1 : 2;
+            // light rounds launched per host check: round_batch, doubling (starting
+            // each band at the previous band's round count, or at 4 or 8, measured slower:
+            // idle rounds cost more than the checks they save)
+            int K = PJ_V2_STATS ? 1 : g.round_batch;
             for (;;) {
                 const u64 pull_thresh = can_pull_light ? (u64)((double)light_left / g.light_pull) : ~0ull;
                 // launch the pull kernels (which decide on the device, per round) only
@@ -1975,13 +1987,9 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 const bool try_pull = can_pull_light && (double)last_fe * g.pull_grow > (double)pull_thresh;
                 for (int q = 0; q < K; ++q) {
                     if (try_pull) {
-                        v2_pull_light_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh);
+                        v2_pull_round_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh,
+                                                                    w.lcv.p, w.lcc.p, w.nlc);
                         PJ_LAUNCH_CHECK();
-                        if (w.nlc) {
-                            v2_pull_long_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh,
-                                                                       w.lcv.p, w.lcc.p, w.nlc);
-                            PJ_LAUNCH_CHECK();
-                        }
                     }
                     // (without the pull kernels the expand must push every round)
                     v2_expand_k<Off, true><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, hr,

@@ -199,6 +199,7 @@ struct Graph {
                                // of unsettled vertices < pull_factor x the members' heavy edges (0 = never)
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
     int level_batch = 0; // BFS levels enqueued per host check (0 = default 8, doubling)
+    int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
     int max_levels = 0;  // debug: truncate the BFS after this many levels (0 = off)
     int ms_width = 0;    // batch BFS: widest pass in 64-source words (0 = 4, i.e. 256 sources)
