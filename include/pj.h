@@ -104,7 +104,9 @@ int pj_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, const uint3
  * stamp the text the graph came from (-1: none); pj_load_csr_file with an
  * expected stamp other than -1 fails with PJ_ERR_STATE when the file's stamp
  * differs (a stale cache). A missing or unreadable file is PJ_ERR_IO; a bad
- * magic, version or size is PJ_ERR_PARSE. */
+ * magic, version or size is PJ_ERR_PARSE, and so is a payload that is not a
+ * valid CSR (checked on the device after loading: row[0] = 0, non-decreasing
+ * offsets, row[n] = nnz, every column id < n). */
 int pj_graph_save(const pj_graph* g, const char* path, int64_t src_size, int64_t src_mtime_ns);
 int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int64_t expect_src_mtime_ns,
                      pj_graph** out);
@@ -300,6 +302,10 @@ typedef struct pj_wpart pj_wpart;
  * Memory: the whole graph is resident on the rank's GPU while the block is cut
  * (the unit-weight pj_part_load_* keep only the rank's rows while building). */
 int pj_wpart_from_graph(pj_graph* g, int rank, int world, pj_wpart** out);
+/* The rank's block of a weighted SNAP file (third column = weight, the
+ * pj_load_snap grammar): every rank parses the file on its GPU and keeps only
+ * its block's rows, weight-sorted (no whole-graph CSR on any GPU). */
+int pj_wpart_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_wpart** out);
 int pj_wpart_destroy(pj_wpart* p);
 /* out[8] = (n, lo, hi, block, nnz_local, world, rank, nnz of the whole graph) */
 int pj_wpart_info(const pj_wpart* p, int64_t* out);

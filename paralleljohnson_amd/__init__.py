@@ -120,6 +120,7 @@ _SIGS = {
     "pj_part_copy_dist": ([_P, _P], _INT),
     "pj_part_dist_device": ([_P], _P),
     "pj_wpart_from_graph": ([_P, _INT, _INT, _PP], _INT),
+    "pj_wpart_load_snap": ([_P, ctypes.c_char_p, _INT, _INT, _PP], _INT),
     "pj_wpart_destroy": ([_P], _INT),
     "pj_wpart_info": ([_P, _P], _INT),
     "pj_wpart_begin": ([_P, _I64, ctypes.c_int32, _P], _INT),

@@ -854,6 +854,8 @@ int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int
             g.ccol.alloc((size_t)g.nnz);
             get_dev(f.get(), g.ccol.p, 4 * (size_t)g.nnz, st, s);
         }
+        check_csr_device(g.row_ptr(), g.off64, g.col.p, g.n, g.nnz, s);
+        if (!g.symmetric) check_csr_device(g.crow_ptr(), g.off64, g.ccol.p, g.n, g.nnz, s);
         return finish_graph(ctx, pg, out);
     });
 }
@@ -928,6 +930,27 @@ int pj_wpart_from_graph(pj_graph* g, int rank, int world, pj_wpart** out) {
     return guarded([&] {
         bind(*g->g.ctx);
         *out = reinterpret_cast<pj_wpart*>(wpart_from_graph(g->g, rank, world));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_wpart** out) {
+    if (!ctx || !path || !out) return arg_error("pj_wpart_load_snap: bad argument");
+    if (world < 1 || world > 64 || rank < 0 || rank >= world)
+        return arg_error("pj_wpart_load_snap: need 0 <= rank < world <= 64");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        HostText text = read_text_file(path);  // missing file: empty graph, as pj_load_snap (:67)
+        DevBuf<u32> src, dst, w;
+        ParseResult r = parse_snap_device(ctx->c, text.data.get(), text.len, true, src, dst, w);
+        if (r.bad_line) {
+            set_error("edge list line " + std::to_string(r.bad_line) +
+                      ": second field missing, negative id or id out of range "
+                      "(undefined behaviour in the reference's read_webgraph)");
+            return (int)PJ_ERR_PARSE;
+        }
+        *out = reinterpret_cast<pj_wpart*>(wpart_from_coo(ctx->c, src, dst, w, r.nnz, r.max_id + 1, rank, world));
         return (int)PJ_OK;
     });
 }

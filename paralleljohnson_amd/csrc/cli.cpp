@@ -258,12 +258,8 @@ int run_partitioned(const char* webfile, int source, const char* out, int P, int
     std::vector<pj_wpart*> wparts((size_t)P, nullptr);
     // every rank builds its own rows on its GPU: no scatter (:344-410)
     per_rank(P, "load", [&](int r) {
-        if (!weighted) return pj_part_load_snap(ctxs[(size_t)r], webfile, r, P, &parts[(size_t)r]);
-        pj_graph* g = nullptr;
-        int rc2 = pj_load_snap(ctxs[(size_t)r], webfile, 1, &g);
-        if (rc2 == PJ_OK) rc2 = pj_wpart_from_graph(g, r, P, &wparts[(size_t)r]);
-        pj_graph_destroy(g);
-        return rc2;
+        return weighted ? pj_wpart_load_snap(ctxs[(size_t)r], webfile, r, P, &wparts[(size_t)r])
+                        : pj_part_load_snap(ctxs[(size_t)r], webfile, r, P, &parts[(size_t)r]);
     });
     int64_t n = 0;
     if (weighted) {

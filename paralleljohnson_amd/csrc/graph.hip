@@ -85,6 +85,38 @@ void bounds(Graph& g, const u32* keys, bool csc) {
 
 }  // namespace
 
+namespace {
+
+// flags |= 1: row[0] != 0, a decreasing offset or row[n] != nnz; 2: a column id >= n
+template <typename Off>
+__global__ void csr_check_k(const Off* __restrict__ row, const u32* __restrict__ col, i64 n, i64 nnz,
+                            u32* __restrict__ flags) {
+    u32 f = 0;
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (i64)gridDim.x * blockDim.x) {
+        const u64 r = (u64)row[i];
+        if ((i == 0 && r != 0) || (i == n && r != (u64)nnz) || (i > 0 && (u64)row[i - 1] > r) || r > (u64)nnz) f |= 1u;
+    }
+    for (i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += (i64)gridDim.x * blockDim.x)
+        if ((i64)col[k] >= n) f |= 2u;
+    if (f) atomicOr(flags, f);
+}
+
+}  // namespace
+
+void check_csr_device(const void* row, bool off64, const u32* col, i64 n, i64 nnz, hipStream_t s) {
+    DevBuf<u32> flag(1);
+    PJ_HIP(hipMemsetAsync(flag.p, 0, sizeof(u32), s));
+    const unsigned grid = grid_for(std::max(n + 1, nnz), 256, 8192);
+    if (off64) csr_check_k<u64><<<grid, 256, 0, s>>>(static_cast<const u64*>(row), col, n, nnz, flag.p);
+    else csr_check_k<u32><<<grid, 256, 0, s>>>(static_cast<const u32*>(row), col, n, nnz, flag.p);
+    PJ_LAUNCH_CHECK();
+    u32 h = 0;
+    PJ_HIP(hipMemcpyAsync(&h, flag.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    if (h & 1u) throw Error(PJ_ERR_PARSE, "CSR file: row offsets are not a valid CSR (corrupted payload)");
+    if (h & 2u) throw Error(PJ_ERR_PARSE, "CSR file: a column id is out of range (corrupted payload)");
+}
+
 Graph::~Graph() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);

@@ -224,6 +224,10 @@ struct Graph {
 // Builds g.rl from g's CSR (weighted graphs).
 void build_relabeled(Graph& g);
 
+// Device check of CSR arrays read from a file: row[0] == 0, non-decreasing, row[n] ==
+// nnz, every col < n; PJ_ERR_PARSE otherwise (a corrupted cache must not fault a kernel).
+void check_csr_device(const void* row, bool off64, const u32* col, i64 n, i64 nnz, hipStream_t s);
+
 void build_graph_from_coo(Graph& g, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>* w, i64 nnz,
                           i64 n, bool symmetric);
 
@@ -258,6 +262,8 @@ void debug_bitmaps(Graph& g, u64* vis0, u64* vis1, u64* fnew);
 struct WPart;
 void delete_wpart(WPart* p);
 WPart* wpart_from_graph(Graph& g, int rank, int world);
+WPart* wpart_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w, i64 nnz, i64 n, int rank,
+                      int world);
 void wpart_info(const WPart& p, i64* out8);
 int32_t wpart_begin(WPart& p, i64 source, int32_t delta);
 void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2);

@@ -411,32 +411,52 @@ struct WPart {
 
 void delete_wpart(WPart* p) { delete p; }
 
-WPart* wpart_from_graph(Graph& g, int rank, int world) {
-    if (!g.weighted) throw Error(PJ_ERR_ARG, "pj_wpart_from_graph: the graph has no weights");
+namespace {
+
+u64 weight_sum(const u32* w, i64 m, unsigned grid, hipStream_t s) {
+    u64 wsum = 0;
+    if (m > 0) {
+        DevBuf<u64> acc(1);
+        PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
+        wsum_all_k<<<grid_for(m, 256, grid), 256, 0, s>>>(w, m, acc.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipMemcpyAsync(&wsum, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+    return wsum;
+}
+
+// Block geometry of rank / world over n vertices (the pj_part_* rule).
+std::unique_ptr<WPart> wpart_geometry(Ctx* ctx, i64 n, i64 nnz, int rank, int world) {
     if (world < 1 || world > WP_MAXW || rank < 0 || rank >= world) throw Error(PJ_ERR_ARG, "rank/world out of range");
-    hipStream_t s = g.ctx->stream;
     std::unique_ptr<WPart> p(new WPart());
-    p->ctx = g.ctx;
-    p->n = g.n;
-    p->nnz = g.nnz;
+    p->ctx = ctx;
+    p->n = n;
+    p->nnz = nnz;
     p->rank = rank;
     p->world = world;
-    const i64 per = (g.n + world - 1) / world;
+    const i64 per = (n + world - 1) / world;
     p->block = std::max<i64>(64, (per + 63) / 64 * 64);
     p->bw = p->block / 64;
-    p->lo = std::min<i64>((i64)rank * p->block, g.n);
-    p->hi = std::min<i64>(p->lo + p->block, g.n);
+    p->lo = std::min<i64>((i64)rank * p->block, n);
+    p->hi = std::min<i64>(p->lo + p->block, n);
     p->nl = p->hi - p->lo;
-    // rows [lo, hi) of the CSR: offsets rebased, edges and weights copied
+    return p;
+}
+
+// The block's weighted rows = rows [first, first + nl) of g (weight-sorted CSR, global
+// column ids): offsets rebased, edges and weights copied; then the per-solve state.
+void wpart_cut(WPart* p, const Graph& g, i64 first, double mean_w) {
+    hipStream_t s = p->ctx->stream;
     u64 eb = 0, ee = 0;
     if (g.n > 0) {
         if (g.off64) {
-            PJ_HIP(hipMemcpyAsync(&eb, g.row64.p + p->lo, sizeof(u64), hipMemcpyDeviceToHost, s));
-            PJ_HIP(hipMemcpyAsync(&ee, g.row64.p + p->hi, sizeof(u64), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipMemcpyAsync(&eb, g.row64.p + first, sizeof(u64), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipMemcpyAsync(&ee, g.row64.p + first + p->nl, sizeof(u64), hipMemcpyDeviceToHost, s));
         } else {
             u32 b32 = 0, e32 = 0;
-            PJ_HIP(hipMemcpyAsync(&b32, g.row32.p + p->lo, sizeof(u32), hipMemcpyDeviceToHost, s));
-            PJ_HIP(hipMemcpyAsync(&e32, g.row32.p + p->hi, sizeof(u32), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipMemcpyAsync(&b32, g.row32.p + first, sizeof(u32), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipMemcpyAsync(&e32, g.row32.p + first + p->nl, sizeof(u32), hipMemcpyDeviceToHost, s));
             PJ_HIP(hipStreamSynchronize(s));
             eb = b32;
             ee = e32;
@@ -446,7 +466,7 @@ WPart* wpart_from_graph(Graph& g, int rank, int world) {
     p->nnz_local = (i64)(ee - eb);
     p->row.alloc((size_t)p->nl + 1);
     if (g.n > 0) {
-        wp_rebase_k<<<grid_for(p->nl + 1, 256, p->grid()), 256, 0, s>>>(g.row_ptr(), g.off64, p->lo, p->nl, p->row.p);
+        wp_rebase_k<<<grid_for(p->nl + 1, 256, p->grid()), 256, 0, s>>>(g.row_ptr(), g.off64, first, p->nl, p->row.p);
         PJ_LAUNCH_CHECK();
     } else {
         PJ_HIP(hipMemsetAsync(p->row.p, 0, sizeof(u64), s));
@@ -457,17 +477,7 @@ WPart* wpart_from_graph(Graph& g, int rank, int world) {
         PJ_HIP(hipMemcpyAsync(p->col.p, g.col.p + eb, sizeof(u32) * (size_t)p->nnz_local, hipMemcpyDeviceToDevice, s));
         PJ_HIP(hipMemcpyAsync(p->w.p, g.w.p + eb, sizeof(u32) * (size_t)p->nnz_local, hipMemcpyDeviceToDevice, s));
     }
-    // mean weight over the whole graph (the default delta, as delta.hip)
-    u64 wsum = 0;
-    if (g.nnz > 0) {
-        DevBuf<u64> acc(1);
-        PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
-        wsum_all_k<<<grid_for(g.nnz, 256, p->grid()), 256, 0, s>>>(g.w.p, g.nnz, acc.p);
-        PJ_LAUNCH_CHECK();
-        PJ_HIP(hipMemcpyAsync(&wsum, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
-    }
-    PJ_HIP(hipStreamSynchronize(s));
-    p->mean_w = g.nnz > 0 ? (double)wsum / (double)g.nnz : 1.0;
+    p->mean_w = mean_w;
     const size_t nl1 = (size_t)std::max<i64>(p->nl, 1);
     p->lsplit.alloc(nl1);
     p->dist.alloc(nl1);
@@ -479,13 +489,90 @@ WPart* wpart_from_graph(Graph& g, int rank, int world) {
     p->lq_e.alloc(nl1);
     p->stat.alloc(ST_N);
     p->hstat.assign(ST_N, 0);
-    if (world > 1) {
-        p->cand.alloc((size_t)std::max<i64>(g.n, 1));
-        p->touched.alloc((size_t)std::max<i64>((g.n + 63) / 64, 1));
-        p->reg.alloc((size_t)world * (size_t)p->block);
+    if (p->world > 1) {
+        p->cand.alloc((size_t)std::max<i64>(p->n, 1));
+        p->touched.alloc((size_t)std::max<i64>((p->n + 63) / 64, 1));
+        p->reg.alloc((size_t)p->world * (size_t)p->block);
         PJ_HIP(hipMemsetAsync(p->touched.p, 0, p->touched.bytes(), s));
     }
     PJ_HIP(hipStreamSynchronize(s));
+}
+
+// keep the edges whose source lies in [lo, hi): count per block, scan, write (file order)
+__global__ void wp_filter_count_k(const u32* __restrict__ src, i64 m, u32 lo, u32 hi, u32* __restrict__ bcnt) {
+    __shared__ u32 red[4];
+    u32 c = 0;
+    const i64 b0 = (i64)blockIdx.x * 4096;
+    for (i64 i = b0 + threadIdx.x; i < min(b0 + 4096, m); i += 256) c += (src[i] >= lo && src[i] < hi) ? 1u : 0u;
+    c = block_sum<4>(c, red);
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = c;
+}
+__global__ void wp_filter_write_k(const u32* __restrict__ src, const u32* __restrict__ dst, const u32* __restrict__ w,
+                                  i64 m, u32 lo, u32 hi, const u64* __restrict__ boff, u32* __restrict__ os,
+                                  u32* __restrict__ od, u32* __restrict__ ow) {
+    __shared__ u64 red[4];
+    const i64 b0 = (i64)blockIdx.x * 4096;
+    u64 base = boff[blockIdx.x];
+    for (i64 i0 = b0; i0 < min(b0 + 4096, m); i0 += 256) {
+        const i64 i = i0 + threadIdx.x;
+        const bool keep = i < m && src[i] >= lo && src[i] < hi;
+        u64 tot;
+        const u64 ex = block_excl_scan<4>((u64)(keep ? 1 : 0), red, tot);
+        if (keep) {
+            os[base + ex] = src[i] - lo;
+            od[base + ex] = dst[i];
+            ow[base + ex] = w[i];
+        }
+        base += tot;
+    }
+}
+
+}  // namespace
+
+WPart* wpart_from_graph(Graph& g, int rank, int world) {
+    if (!g.weighted) throw Error(PJ_ERR_ARG, "pj_wpart_from_graph: the graph has no weights");
+    std::unique_ptr<WPart> p = wpart_geometry(g.ctx, g.n, g.nnz, rank, world);
+    const u64 wsum = weight_sum(g.w.p, g.nnz, p->grid(), g.ctx->stream);
+    wpart_cut(p.get(), g, p->lo, g.nnz > 0 ? (double)wsum / (double)g.nnz : 1.0);
+    return p.release();
+}
+
+// The rank's block from device COO (consumed): only the block's rows are sorted and
+// kept, so a rank holds its share of the graph plus the parsed COO while building.
+WPart* wpart_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w, i64 nnz, i64 n, int rank,
+                      int world) {
+    hipStream_t s = ctx.stream;
+    std::unique_ptr<WPart> p = wpart_geometry(&ctx, n, nnz, rank, world);
+    const u64 wsum = weight_sum(w.p, nnz, p->grid(), s);
+    const i64 nb = (nnz + 4095) / 4096;
+    i64 m = 0;
+    DevBuf<u32> ls, ld, lw;
+    if (nb > 0) {
+        DevBuf<u32> bcnt((size_t)nb);
+        DevBuf<u64> boff((size_t)nb + 1);
+        ScanWs ws;
+        wp_filter_count_k<<<(unsigned)nb, 256, 0, s>>>(src.p, nnz, (u32)p->lo, (u32)p->hi, bcnt.p);
+        PJ_LAUNCH_CHECK();
+        exclusive_scan_u32(bcnt.p, boff.p, nb, ws, s);
+        u64 tot = 0;
+        PJ_HIP(hipMemcpyAsync(&tot, boff.p + nb, sizeof(u64), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+        m = (i64)tot;
+        ls.alloc((size_t)std::max<i64>(m, 1));
+        ld.alloc((size_t)std::max<i64>(m, 1));
+        lw.alloc((size_t)std::max<i64>(m, 1));
+        wp_filter_write_k<<<(unsigned)nb, 256, 0, s>>>(src.p, dst.p, w.p, nnz, (u32)p->lo, (u32)p->hi, boff.p, ls.p,
+                                                       ld.p, lw.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+    src.release();
+    dst.release();
+    w.release();
+    Graph local;  // the block's rows, local ids, global columns, weight-sorted
+    local.ctx = &ctx;
+    build_graph_from_coo(local, ls, ld, &lw, m, p->nl, false);
+    wpart_cut(p.get(), local, 0, nnz > 0 ? (double)wsum / (double)nnz : 1.0);
     return p.release();
 }
 

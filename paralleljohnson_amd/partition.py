@@ -281,9 +281,11 @@ def load_coo(ctx, src, dst, n: int, rank: int, world: int, symmetric: bool = Fal
 class DeviceWPart:
     """This rank's block of a weighted graph on its GPU (pj_wpart_*)."""
 
-    def __init__(self, ctx, graph, rank: int, world: int):
-        h = ctypes.c_void_p()
-        _check(_lib.pj_wpart_from_graph(graph._h, int(rank), int(world), ctypes.byref(h)))
+    def __init__(self, ctx, graph, rank: int, world: int, handle=None):
+        h = handle
+        if h is None:
+            h = ctypes.c_void_p()
+            _check(_lib.pj_wpart_from_graph(graph._h, int(rank), int(world), ctypes.byref(h)))
         self._ctx = ctx
         self._h = h
         info = (_I64 * 8)()
@@ -322,6 +324,13 @@ class DeviceWPart:
 def load_weighted(ctx, graph, rank: int, world: int) -> DeviceWPart:
     """The rank's block of a weighted pj Graph (the graph may be closed afterwards)."""
     return DeviceWPart(ctx, graph, rank, world)
+
+
+def load_weighted_snap(ctx, path: str, rank: int, world: int) -> DeviceWPart:
+    """The rank's block of a weighted SNAP file (pj_wpart_load_snap: only the block's rows are kept)."""
+    h = ctypes.c_void_p()
+    _check(_lib.pj_wpart_load_snap(ctx._h, os.fsencode(path), int(rank), int(world), ctypes.byref(h)))
+    return DeviceWPart(ctx, None, rank, world, handle=h)
 
 
 def bfs_group(parts: Sequence[DevicePart], comms: Sequence[Comm], source: int) -> List[dict]:

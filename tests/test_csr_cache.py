@@ -100,3 +100,32 @@ def test_cli_csr_cache(pj, oracle, tmp_path):
     r2 = subprocess.run([pj.cli_path(), str(f), "3", str(tmp_path / "p.txt")], capture_output=True, text=True,
                         timeout=120)
     assert out.read_bytes() == (tmp_path / "p.txt").read_bytes()
+
+
+@pytest.mark.parametrize("where", ["row", "col", "csc"])
+def test_cache_corrupted_payload(ctx, pj, tmp_path, where):
+    """A cache file with a valid header but a corrupted payload fails with PJ_ERR_PARSE
+    (checked on the device) instead of faulting a kernel; the CLI then re-parses."""
+    n = 5000
+    rng = np.random.default_rng(3)
+    src, dst = random_graph(rng, "uniform", n)
+    g = ctx.load_coo(src, dst, n=n)
+    p = tmp_path / "c.pjcsr"
+    g.save(str(p))
+    raw = bytearray(p.read_bytes())
+    nnz = g.nnz
+    rowb = 4 * (n + 1)
+    if where == "row":  # a decreasing offset in the middle of the row array
+        off = 64 + 4 * (n // 2)
+        raw[off:off + 4] = (0xFFFFFF).to_bytes(4, "little")
+    elif where == "col":  # a column id past n
+        off = 64 + rowb + 4 * (nnz // 3)
+        raw[off:off + 4] = (n + 7).to_bytes(4, "little")
+    else:  # the in-edge CSC of a directed graph
+        off = 64 + rowb + 4 * nnz + rowb + 4 * (nnz // 2)
+        raw[off:off + 4] = (2 ** 31).to_bytes(4, "little")
+    p.write_bytes(bytes(raw))
+    with pytest.raises(pj.PJError) as e:
+        ctx.load_csr_file(str(p))
+    assert e.value.name == "PJ_ERR_PARSE"
+    g.close()

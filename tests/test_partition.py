@@ -395,3 +395,33 @@ def test_cli_processes_byte_identical(pj, oracle, tmp_path, weighted):
     r = subprocess.run([pj.cli_path(), str(path), str(src), str(tmp_path / "rank1.txt")], capture_output=True,
                        env=dict(base, OMPI_COMM_WORLD_SIZE="2", OMPI_COMM_WORLD_RANK="1"), timeout=120)
     assert r.returncode == 0 and not (tmp_path / "rank1.txt").exists()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_wpart_load_snap(pj, oracle, tmp_path, world):
+    """pj_wpart_load_snap: each rank parses the weighted text and keeps only its block's
+    rows; the band loop over the host transport equals the oracle Dijkstra, and the block
+    holds exactly the block's out-edges."""
+    from paralleljohnson_amd.partition import block_geometry, delta_group, gather_group, load_weighted_snap
+    rng = np.random.default_rng(41 + world)
+    n = 2000
+    s, d = random_graph(rng, "hub", n)
+    w = rng.integers(1, 120, len(s)).astype(np.uint32)
+    text = to_text(s, d, w=w, style=2)
+    path = tmp_path / "w.txt"
+    path.write_bytes(text)
+    ps, pd, pw, nn = oracle.parse_snap(text, weighted=True)
+    row, col, wc = oracle.coo2csr(ps, pd, nn, pw)
+    ctxs, comms = _group(pj, world)
+    parts = [load_weighted_snap(ctxs[r], str(path), r, world) for r in range(world)]
+    block, ranges = block_geometry(nn, world)
+    for r, p in enumerate(parts):
+        assert (p.lo, p.hi, p.n) == (ranges[r][0], ranges[r][1], nn)
+        assert p.nnz_local == int(row[ranges[r][1]] - row[ranges[r][0]])
+    for source in (int(ps[0]), 0, nn - 1, nn + 3):
+        delta_group(parts, comms, source)
+        exp = oracle.dijkstra(row, col, wc, source) if source < nn else np.full(nn, INF, np.int32)
+        assert np.array_equal(gather_group(parts, comms), exp), source
+    for p in parts:
+        p.close()
