@@ -334,7 +334,7 @@ def main():
         secondary["ms1024"] = {
             "workload": "web-google-shaped-synthetic, 1024 sources (smallest ids with out-degree >= 1), "
                         "up to 256 per batched pass (one 64-bit mask word per 64 sources), source-sharded over the ranks",
-            "sources_per_rank": ms["n_src"], "time_to_solution_ms": round(1000.0 * el, 3),
+            "sources_per_rank": ms["n_src"], "batch_ms": round(1000.0 * el, 3),
             "gteps": round(m / el / 1e9, 3), "scaling": "strong (1024 sources in total)",
         }
         if ms["cpu"]:
@@ -443,6 +443,24 @@ def run_wg_cli(ctx, args):
         t_line = r.stdout.strip()
         got = open(out, "rb").read()
         text_mb = os.path.getsize(path) / 1e6
+        # configs[4] through the drop-in: 1024 sources (PJ_SOURCES), one sol_file each
+        srcs = np.nonzero(np.diff(row) >= 1)[0][:1024]
+        lst, odir = os.path.join(td, "sources.txt"), os.path.join(td, "ms")
+        os.makedirs(odir)
+        with open(lst, "w") as f:
+            f.write("\n".join(map(str, srcs)) + "\n")
+        t0 = time.perf_counter()
+        r = subprocess.run([pj.cli_path(), path, "0", os.path.join(odir, "sol_{s}.txt")], capture_output=True, text=True,
+                           timeout=600, env=dict(os.environ, PJ_SOURCES="@" + lst))
+        ms_wall = time.perf_counter() - t0
+        if r.returncode != 0:
+            raise RuntimeError(f"parallel_johnson PJ_SOURCES failed: {r.stderr[-500:]}")
+        ms_files = os.listdir(odir)
+        ms_bytes = sum(os.path.getsize(os.path.join(odir, x)) for x in ms_files)
+        ms_first = open(os.path.join(odir, f"sol_{srcs[0]}.txt"), "rb").read()
+        ms_cli = {"sources": int(len(srcs)), "files": len(ms_files), "bytes_written": ms_bytes,
+                  "time_to_solution_s": round(ms_wall, 3), "time_line": r.stdout.strip()}
+    ms_cli["first_file_identical_to_oracle"] = ms_first == O.format_sol(O.bfs(row, col, int(srcs[0])))
     t0 = time.perf_counter()
     ref, st = O.reference_sssp(row, col, 0, 4)
     ref_s = time.perf_counter() - t0
@@ -467,6 +485,7 @@ def run_wg_cli(ctx, args):
         "reference_np4_gteps": round(m_r / st.solve_s / 1e9, 5), "reference_cores": 4,
         "reference_kind": "port (oracle restatement of the reference's BSP heap algorithm, 4 host threads)",
         "reference_solve_s_by_np": np_scan,
+        "ms1024_drop_in": ms_cli,
         **host_cpu(),
     }
 

@@ -6,6 +6,8 @@
  * and bench.py's cpu_baseline leg may load this library, and only as the
  * checker / the timed CPU baseline — never as the product path.
  *
+ * Status: PARITY UNPINNED against a run of the reference itself (see below).
+ *
  * Parity pinning: the reference ships no tests, fixtures or golden vectors
  *  and cannot be compiled here (Boost.Heap is absent from the
  * image; building it with a stand-in header is not allowed), so there is no
@@ -14,7 +16,9 @@
  * tests/golden/appendix_b/), (2) an independent implementation of the output
  * contract R9 (scipy.sparse.csgraph) and (3) agreement between its two
  * algorithms: the plain BFS/Dijkstra of the R9 contract and the restated
- * BSP heap algorithm of :466-594 at every partition count.
+ * BSP heap algorithm of :466-594 at every partition count. The Appendix B
+ * observations come from a survey build with a stand-in Boost.Heap header, so
+ * none of the three is a run of the unmodified reference: parity is unpinned.
  */
 #ifndef PJ_ORACLE_H
 #define PJ_ORACLE_H

@@ -47,21 +47,11 @@ __device__ __forceinline__ u64 line_start_mask(const uint4* __restrict__ p4, u32
     return mask;
 }
 
-// Bytes of the text as one lane's parser sees them: the block's chunk and a tail
-// staged in LDS, anything further (a line running past the tail) from global.
-struct Bytes {
-    const uint8_t* __restrict__ lds;
-    const uint8_t* __restrict__ glob;
-    i64 base, staged;
-    __device__ __forceinline__ u32 operator[](i64 p) const {
-        const i64 q = p - base;
-        return q < staged ? (u32)lds[q] : (u32)glob[p];
-    }
-};
-
-// One `>> int` extraction. 1 = read, 0 = failed on a non-blank (value 0),
-// -1 = nothing but blanks before end of line, -2 = overflow.
-__device__ __forceinline__ int extract(const Bytes& t, i64 len, i64& p, i64& out) {
+// One `>> int` extraction from bytes t[0, len) (t: the LDS window of the
+// block, or the whole text in global memory). 1 = read, 0 = failed on a
+// non-blank (value 0), -1 = nothing but blanks before end of line, -2 = overflow.
+template <typename T>
+__device__ __forceinline__ int extract(const T* __restrict__ t, int64_t len, int64_t& p, i64& out) {
     while (p < len && is_blank(t[p])) ++p;
     if (p >= len || t[p] == '\n') return -1;
     bool neg = false;
@@ -86,6 +76,30 @@ __device__ __forceinline__ int extract(const Bytes& t, i64 len, i64& p, i64& out
     if (ovf) return -2;
     out = neg ? -acc : acc;
     return 1;
+}
+
+// One line: `src dst [w]` with the reference's `>> int` semantics (:92-93).
+// Returns false when the line is undefined behaviour for the reference.
+template <typename T>
+__device__ __forceinline__ bool parse_line(const T* __restrict__ t, int64_t len, int64_t& p, bool weighted, i64& u,
+                                           i64& v, i64& wt) {
+    u = 0;
+    v = 0;
+    wt = 1;
+    int r = extract(t, len, p, u);
+    bool bad = (r != 1) || u > ID_LIMIT;
+    if (!bad) {
+        r = extract(t, len, p, v);
+        bad = r < 0 || v < 0 || v > ID_LIMIT;
+        if (!bad && weighted) {
+            if (r == 0) wt = 0;  // stream failed: the weight extraction stores nothing -> 0
+            else {
+                const int r3 = extract(t, len, p, wt);
+                bad = r3 < 0 || wt < 0;
+            }
+        }
+    }
+    return !bad;
 }
 
 __global__ __launch_bounds__(PB) void parse_count_k(const uint8_t* __restrict__ text, i64 len,
@@ -115,7 +129,9 @@ __global__ __launch_bounds__(PB) void parse_lines_k(const uint8_t* __restrict__ 
     for (int k = threadIdx.x; k < (int)((PCHUNK + PTAIL) / 16); k += PB) stage[k] = g4[k];
     __syncthreads();
     const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage);
-    const Bytes t{sb, text, base, PCHUNK + PTAIL};
+    // lines are parsed from the LDS window (ds_read_u8) up to its end; a line that
+    // reaches the end of the window is parsed again from global memory
+    const int64_t wlen = min((i64)(PCHUNK + PTAIL), len - base);
     const i64 seg = base + (i64)threadIdx.x * PSEG;
     u64 mask = 0;
     if (seg < len) {
@@ -129,21 +145,14 @@ __global__ __launch_bounds__(PB) void parse_lines_k(const uint8_t* __restrict__ 
         const int b = __ffsll((long long)mask) - 1;
         mask &= mask - 1;
         const i64 start = seg + b;
-        i64 p = start, u = 0, v = 0, wt = 1;
-        int r = extract(t, len, p, u);
-        bool bad = (r != 1) || u > ID_LIMIT;
-        if (!bad) {
-            r = extract(t, len, p, v);
-            bad = r < 0 || v < 0 || v > ID_LIMIT;
-            if (!bad && weighted) {
-                if (r == 0) wt = 0;  // stream failed: the weight extraction stores nothing -> 0
-                else {
-                    int r3 = extract(t, len, p, wt);
-                    bad = r3 < 0 || wt < 0;
-                }
-            }
+        int64_t q = start - base;
+        i64 u, v, wt;
+        bool ok = parse_line(sb, wlen, q, weighted != 0, u, v, wt);
+        if (q >= wlen && base + wlen < len) {  // ran into the window end: slow path
+            int64_t pg = start;
+            ok = parse_line(text, len, pg, weighted != 0, u, v, wt);
         }
-        if (bad) {
+        if (!ok) {
             atomicMin(errpos, (u64)start);
             u = 0;
             v = 0;
