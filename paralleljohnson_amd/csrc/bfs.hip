@@ -47,6 +47,9 @@ namespace {
 #ifndef PJ_PB2
 #define PJ_PB2 8
 #endif
+#ifndef PJ_SMALL_WG_ATOMIC
+#define PJ_SMALL_WG_ATOMIC 1  // small_levels claims: workgroup-scope atomics (one block is running)
+#endif
 constexpr int TB = 256;
 constexpr int NW = TB / WAVE;
 constexpr u32 HUBT = 256;     // out-degree above which a frontier vertex goes to the hub queue
@@ -61,6 +64,9 @@ constexpr int NSH = 16;       // shards of the summed counters
 constexpr int NQS = 8;        // normal-queue segments
 constexpr int SC = 16;        // pull levels: visited words a wave screens at once
 constexpr int RPI = PJ_RPI;   // pull levels: rounds of 64 candidates in flight per wave
+constexpr u32 SMALL_N = TB;   // one-workgroup levels: frontier vertices (one per thread)
+constexpr u32 SEPT = 8;       // one-workgroup levels: frontier edges per thread
+constexpr u32 SMALL_M = SEPT * TB;
 
 struct alignas(64) Line {
     u64 v;
@@ -91,6 +97,7 @@ struct BfsArgs {
     int eb;  // edge bits of the packed hub counter
     double alpha, beta;
     int force;  // 0 auto, 1 push only, 2 pull whenever possible
+    int small;  // one-workgroup levels for small push frontiers
     int32_t max_levels;  // debug: stop after this many levels
     int32_t* dist;
     u64* vis[2];
@@ -102,7 +109,7 @@ struct BfsArgs {
     LevelCnt* C;    // [3]
     LevelState* S;  // [2]
     u64* nmode;     // [2] push / pull levels run (device)
-    int64_t* host;  // mapped host words: [0] levels run (-1 while running), [1] push, [2] pull
+    int64_t* host;  // mapped host words: [0] levels run (-1 while running), [1] push, [2] pull, [3] launches
 };
 
 template <typename Off>
@@ -114,23 +121,30 @@ struct Graph_d {
 };
 
 struct Decision {
+    int32_t L;  // the level this launch computes
     int32_t mode, vsel, prev_mode;
     double m_u;
     u64 found;
     u64 nseg[NQS];
-    u64 nh, he;
+    u64 nh, he, mq;
 };
 
-// Decision for level L, identical in every block: 2 = run, 1 = the BFS ends at
-// this level, 0 = it ended before.
-__device__ __forceinline__ int decide(const BfsArgs& a, int32_t L, Decision& d) {
-    const LevelState& ps = a.S[(L + 1) & 1];
-    const LevelCnt& pc = a.C[(L + 2) % 3];
+// Decision of launch li, identical in every block: 2 = run level d.L, 1 = the BFS
+// ends at this level, 0 = it ended before. The counter / state rings are indexed
+// by launch, not by level, since one launch may run several levels (small_levels):
+// launch li reads C[(li + 2) % 3] and S[(li + 1) % 2], accumulates into C[li % 3],
+// publishes S[li % 2] and zeroes C[(li + 1) % 3] -- none of which it reads.
+__device__ __forceinline__ int decide(const BfsArgs& a, int32_t li, Decision& d) {
+    const LevelState& ps = a.S[(li + 1) & 1];
+    const LevelCnt& pc = a.C[(li + 2) % 3];
+    const int32_t L = ps.level + 1;
+    d.L = L;
     d.mode = ps.mode;
     d.prev_mode = ps.mode;
     d.vsel = ps.vsel;
     d.m_u = ps.m_u;
     d.found = ps.prev_found;
+    d.nh = d.he = d.mq = 0;
     if (ps.done) return 0;
     u64 nn = 0;
 #pragma unroll
@@ -150,6 +164,7 @@ __device__ __forceinline__ int decide(const BfsArgs& a, int32_t L, Decision& d) 
         fz += pc.fnz[k];
     }
     (void)nn;
+    d.mq = mq;
     d.found = fd;
     d.m_u = ps.m_u - (double)in;
     if (fz == 0 || L + 1 >= INT_INF || L >= a.max_levels) return 1;
@@ -177,7 +192,8 @@ struct Acc {
     u64 m = 0, f = 0, in = 0, fz = 0;
 };
 
-__device__ __forceinline__ void hub_direct(const BfsArgs& a, int32_t L, bool ish, u32 v, u32 deg, u64 beg) {
+__device__ __forceinline__ void hub_direct(const BfsArgs& a, LevelCnt* cacc, int32_t L, bool ish, u32 v, u32 deg,
+                                           u64 beg) {
     // staging full: publish this wave's hubs with one packed atomic
     const u64 hm = __ballot(ish);
     if (!hm) return;
@@ -187,7 +203,7 @@ __device__ __forceinline__ void hub_direct(const BfsArgs& a, int32_t L, bool ish
     const u64 tot = __shfl(incl, 63, 64);
     const int leader = __ffsll((long long)hm) - 1;
     u64 old = 0;
-    if (lane_id() == leader) old = atomicAdd(&a.C[L % 3].hub_packed.v, ((u64)__popcll(hm) << a.eb) + tot);
+    if (lane_id() == leader) old = atomicAdd(&cacc->hub_packed.v, ((u64)__popcll(hm) << a.eb) + tot);
     old = __shfl(old, leader, 64);
     if (ish) {
         const u64 hs = (old >> a.eb) + (u64)__popcll(hm & lanemask_lt());
@@ -199,8 +215,8 @@ __device__ __forceinline__ void hub_direct(const BfsArgs& a, int32_t L, bool ish
 
 // Stage one candidate per lane (whole wave calls). KNOWN: row bounds supplied.
 template <typename Off, bool SYM, bool KNOWN = false>
-__device__ __forceinline__ void stage(BlockQ& q, const BfsArgs& a, const Graph_d<Off>& g, int32_t L, bool pred,
-                                      u32 v, u64 in_deg, Acc& acc, Off kb = 0, Off ke = 0) {
+__device__ __forceinline__ void stage(BlockQ& q, const BfsArgs& a, LevelCnt* cacc, const Graph_d<Off>& g, int32_t L,
+                                      bool pred, u32 v, u64 in_deg, Acc& acc, Off kb = 0, Off ke = 0) {
     u32 deg = 0;
     u64 beg = 0;
     if (pred) {
@@ -231,28 +247,28 @@ __device__ __forceinline__ void stage(BlockQ& q, const BfsArgs& a, const Graph_d
         const int leader = __ffsll((long long)hm) - 1;
         u32 pos = 0;
         if (lane_id() == leader) pos = atomicAdd(&q.nh, (u32)__popcll(hm));
-        pos = __shfl(pos, leader, 64);
-        if (pos + (u32)__popcll(hm) <= (u32)HCAP) {
-            pos += (u32)__popcll(hm & lanemask_lt());
-            if (ish) {
-                q.hv[pos] = v;
-                q.hdeg[pos] = deg;
-                q.hbeg[pos] = beg;
-            }
-        } else {
-            if (lane_id() == leader) atomicSub(&q.nh, (u32)__popcll(hm));
-            hub_direct(a, L, ish, v, deg, beg);
+        pos = __shfl(pos, leader, 64) + (u32)__popcll(hm & lanemask_lt());
+        // q.nh only grows, so every staging slot below HCAP is taken exactly once; hubs past
+        // the end go straight to the global queue and flush() reads min(q.nh, HCAP). (Handing
+        // a whole overflowing wave back with a subtraction let a later wave's slots land above
+        // the restored count: lost hubs, seen as rare push-only mismatches on Kronecker.)
+        const bool fits = pos < (u32)HCAP;
+        if (ish && fits) {
+            q.hv[pos] = v;
+            q.hdeg[pos] = deg;
+            q.hbeg[pos] = beg;
         }
+        const bool over = ish && !fits;
+        if (__ballot(over)) hub_direct(a, cacc, L, over, v, deg, beg);
     }
 }
 
 // Block-uniform: publish everything staged (one atomic per queue).
-__device__ __forceinline__ void flush(BlockQ& q, const BfsArgs& a, int32_t L) {
+__device__ __forceinline__ void flush(BlockQ& q, const BfsArgs& a, LevelCnt* c, int32_t L) {
     __syncthreads();
-    const u32 n = q.n, nh = q.nh;
+    const u32 n = q.n, nh = min(q.nh, (u32)HCAP);
     if (!(n | nh)) return;
     const int np = (L + 1) & 1;
-    LevelCnt* c = a.C + (L % 3);
     const u32 t = threadIdx.x;
     const int seg = blockIdx.x % NQS;
     // hub edge offsets: block scan of the staged hub degrees (one per thread, HCAP == TB)
@@ -277,13 +293,12 @@ __device__ __forceinline__ void flush(BlockQ& q, const BfsArgs& a, int32_t L) {
     __syncthreads();
 }
 
-__device__ __forceinline__ void flush_acc(const BfsArgs& a, int32_t L, const Acc& acc, u64* red) {
+__device__ __forceinline__ void flush_acc(LevelCnt* c, const Acc& acc, u64* red) {
     const u64 m = block_sum<NW>(acc.m, red);
     const u64 f = block_sum<NW>(acc.f, red);
     const u64 in = block_sum<NW>(acc.in, red);
     const u64 fz = block_sum<NW>(acc.fz, red);
     if (threadIdx.x == 0) {
-        LevelCnt* c = a.C + (L % 3);
         const int sh = blockIdx.x % NSH;
         if (m) atomicAdd(&c->m_next[sh], m);
         if (f) atomicAdd(&c->found[sh], f);
@@ -300,25 +315,271 @@ __device__ __forceinline__ bool claim(u64* vis, u32 v) {
     return !(atomicOr(wp, bit) & bit);
 }
 
+struct LevelShared {
+    LbShared<HUB_TILE> sh;
+    BlockQ q;
+    u32 s_excl[TB];
+    u64 s_beg[TB];
+    u32 s_wex[TB];
+    u64 s_fw[TB];
+    u32 s_new[NW][2 * SC];
+};
+
+struct SmallShared {
+    u32 cv[SMALL_N];  // frontier of the current level: vertex, out-degree (>= 1), row begin
+    u32 cdeg[SMALL_N];
+    u64 cbeg[SMALL_N];
+    u32 cex[SMALL_N];  // exclusive scan of cdeg
+    u32 nv[SMALL_M];   // vertices the level claims with out-degree >= 1 (at most one per edge)
+    u32 ndeg[SMALL_M];
+    u64 nbeg[SMALL_M];
+    u32 nn;
+    u32 scan[NW];
+};
+
+// One-workgroup levels. While the frontier is small (<= SMALL_N vertices and
+// <= SMALL_M edges) and the decision is push, block 0 of the launch runs the levels
+// itself with the frontier in LDS: per level one edge-to-owner search in LDS, one
+// column load, one claim atomic (the row loads of the claimed vertices are issued
+// beside it) and the block barriers -- instead of a kernel boundary plus the
+// dependent global round trips of a grid level (decision counters, queue read,
+// staging and publication atomics). Small frontiers are where a web graph's BFS
+// spends its first and last levels. The loop leaves the queues, counters and state
+// exactly as the grid kernel would after its last level, or ends the BFS.
 template <typename Off, bool SYM>
-__global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int32_t L) {
-    __shared__ LbShared<HUB_TILE> sh;
-    __shared__ BlockQ q;
-    __shared__ u32 s_excl[TB];
-    __shared__ u64 s_beg[TB];
-    __shared__ u32 s_wex[TB];
-    __shared__ u64 s_fw[TB];
-    __shared__ u32 s_new[NW][2 * SC];
+__device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Decision& d, int32_t li, SmallShared& ss,
+                             u64* red) {
+    const u32 t = threadIdx.x;
+    u64 nn = 0;
+#pragma unroll
+    for (int k = 0; k < NQS; ++k) nn += d.nseg[k];
+    u32 F = (u32)(nn + d.nh);
+    if (t < F) {  // the frontier of level d.L, from the normal segments and the hub queue
+        const int cp = d.L & 1;
+        u32 v;
+        if (t < nn) {
+            u64 r = 0, pre = 0;
+            int k = 0;
+#pragma unroll
+            for (int j = 0; j < NQS; ++j) {  // unrolled: no dynamic index into d.nseg
+                if (t >= pre && t < pre + d.nseg[j]) {
+                    k = j;
+                    r = t - pre;
+                }
+                pre += d.nseg[j];
+            }
+            v = a.qv[cp][(u64)k * (u64)a.n + r];
+        } else {
+            v = a.hv[cp][t - nn];
+        }
+        const Off b = g.row[v], e = g.row[v + 1];
+        ss.cv[t] = v;
+        ss.cdeg[t] = (u32)(e - b);
+        ss.cbeg[t] = (u64)b;
+    }
+    u64* vis = a.vis[d.vsel];
+    int32_t L = d.L;
+    double m_u = d.m_u;
+    u64 fprev = d.found, nlev = 0;
+    for (;;) {
+        __syncthreads();
+        u32 E;
+        const u32 ex = block_excl_scan<NW>(t < F ? ss.cdeg[t] : 0u, ss.scan, E);
+        ss.cex[t] = ex;
+        if (t == 0) ss.nn = 0;
+        __syncthreads();
+        u32 vv[SEPT];
+        bool ok[SEPT];
+#pragma unroll
+        for (u32 k = 0; k < SEPT; ++k) {
+            const u32 e = k * TB + t;
+            ok[k] = e < E;
+            vv[k] = 0;
+            if (ok[k]) {
+                u32 lo = 0;  // owner: last entry with cex <= e (degrees >= 1: cex ascends strictly)
+#pragma unroll
+                for (u32 step = SMALL_N / 2; step > 0; step >>= 1)
+                    if (lo + step < F && ss.cex[lo + step] <= e) lo += step;
+                vv[k] = g.col[ss.cbeg[lo] + (e - ss.cex[lo])];
+            }
+        }
+        bool c[SEPT];
+        Off rb[SEPT], re[SEPT];
+        u64 ind[SEPT];
+#pragma unroll
+        for (u32 k = 0; k < SEPT; ++k) {
+            c[k] = false;
+            if (ok[k]) {
+                const u64 bit = 1ull << (vv[k] & 63);
+#if PJ_SMALL_WG_ATOMIC
+                // block 0 is the launch's only writer of vis: workgroup scope suffices, and the
+                // kernel's end publishes the words to the next launch
+                const u64 old = __hip_atomic_fetch_or(vis + (vv[k] >> 6), bit, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+                const u64 old = atomicOr(vis + (vv[k] >> 6), bit);
+#endif
+                c[k] = !(old & bit);
+            }
+        }
+#pragma unroll
+        for (u32 k = 0; k < SEPT; ++k) {  // issued beside the claims, needed only by the winners
+            rb[k] = re[k] = 0;
+            ind[k] = 0;
+            if (ok[k]) {
+                rb[k] = g.row[vv[k]];
+                re[k] = g.row[vv[k] + 1];
+                if (!SYM) ind[k] = (u64)(g.crow[vv[k] + 1] - g.crow[vv[k]]);
+            }
+        }
+        const int32_t nl = L + 1;
+        Acc acc;
+#pragma unroll
+        for (u32 k = 0; k < SEPT; ++k) {
+            const bool cl = ok[k] && c[k];
+            const u32 dg = cl ? (u32)(re[k] - rb[k]) : 0u;
+            if (cl) {
+                a.dist[vv[k]] = nl;
+                acc.f += 1;
+                acc.m += dg;
+                acc.fz += dg > 0;
+                acc.in += SYM ? (u64)dg : ind[k];
+            }
+            const bool app = cl && dg > 0;
+            const u64 m = __ballot(app);
+            if (m) {
+                const int leader = __ffsll((long long)m) - 1;
+                u32 pos = 0;
+                if (lane_id() == leader) pos = atomicAdd(&ss.nn, (u32)__popcll(m));
+                pos = __shfl(pos, leader, 64) + (u32)__popcll(m & lanemask_lt());
+                if (app) {
+                    ss.nv[pos] = vv[k];
+                    ss.ndeg[pos] = dg;
+                    ss.nbeg[pos] = (u64)rb[k];
+                }
+            }
+        }
+        const u64 mq = block_sum<NW>(acc.m, red);
+        const u64 f = block_sum<NW>(acc.f, red);
+        const u64 in = block_sum<NW>(acc.in, red);
+        const u32 NF = ss.nn;  // = the level's found vertices with out-degree > 0
+        ++nlev;
+        // decide() for level L + 1, from what level L would publish
+        const int32_t L2 = L + 1;
+        const double m_u2 = m_u - (double)in;
+        const bool end = NF == 0 || L2 + 1 >= INT_INF || L2 >= a.max_levels;
+        const bool pull = a.force == 2 || (a.force == 0 && (double)mq > m_u2 / a.alpha);
+        if (!end && !pull && NF <= SMALL_N && mq <= SMALL_M) {
+            if (t < NF) {
+                ss.cv[t] = ss.nv[t];
+                ss.cdeg[t] = ss.ndeg[t];
+                ss.cbeg[t] = ss.nbeg[t];
+            }
+            F = NF;
+            fprev = f;
+            m_u = m_u2;
+            L = L2;
+            continue;
+        }
+        if (end) {  // what the grid kernel publishes when decide() ends the BFS at L2
+            if (t == 0) {
+                a.nmode[0] += nlev;
+                LevelState& s = a.S[li & 1];
+                s.mode = 0;
+                s.done = 1;
+                s.vsel = d.vsel;
+                s.level = L2;
+                s.m_u = m_u2;
+                s.prev_found = f;
+                a.host[1] = (int64_t)a.nmode[0];
+                a.host[2] = (int64_t)a.nmode[1];
+                a.host[3] = (int64_t)li + 1;
+                __atomic_store_n(&a.host[0], (int64_t)L2, __ATOMIC_RELEASE);
+            }
+            return;
+        }
+        // hand level L2 to the grid: its frontier into normal segment 0 and the hub queue
+        // (thread t takes entries [t * SEPT, t * SEPT + SEPT), so slots keep one order),
+        // level L's counters into C[li % 3], level L's state into S[li % 2]
+        u32 cn = 0, ch = 0;
+        u64 che = 0;
+#pragma unroll
+        for (u32 k = 0; k < SEPT; ++k) {
+            const u32 j = t * SEPT + k;
+            if (j < NF) {
+                const u32 dg = ss.ndeg[j];
+                if (dg <= HUBT) ++cn;
+                else {
+                    ++ch;
+                    che += dg;
+                }
+            }
+        }
+        u32 tn, th;
+        u64 the;
+        u32 pn = block_excl_scan<NW>(cn, ss.scan, tn);
+        u32 ph = block_excl_scan<NW>(ch, ss.scan, th);
+        u64 pe = block_excl_scan<NW>(che, red, the);
+        const int np = L2 & 1;
+#pragma unroll
+        for (u32 k = 0; k < SEPT; ++k) {
+            const u32 j = t * SEPT + k;
+            if (j < NF) {
+                const u32 v = ss.nv[j], dg = ss.ndeg[j];
+                if (dg <= HUBT) {
+                    a.qv[np][pn++] = v;
+                } else {
+                    a.hv[np][ph] = v;
+                    a.hbeg[np][ph] = ss.nbeg[j];
+                    a.hoff[np][ph] = pe;
+                    ++ph;
+                    pe += dg;
+                }
+            }
+        }
+        if (t == 0) {
+            a.nmode[0] += nlev;
+            LevelCnt* c = a.C + li % 3;  // zeroed by launch li - 1
+            c->n_norm[0].v = tn;
+            c->hub_packed.v = ((u64)th << a.eb) | the;
+            c->m_next[0] = mq;
+            c->found[0] = f;
+            c->in_next[0] = in;
+            c->fnz[0] = NF;
+            LevelState& s = a.S[li & 1];
+            s.mode = 0;
+            s.done = 0;
+            s.vsel = d.vsel;
+            s.level = L;
+            s.m_u = m_u;
+            s.prev_found = fprev;
+        }
+        return;
+    }
+}
+
+template <typename Off, bool SYM>
+__global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int32_t li) {
+    __shared__ union {
+        LevelShared lv;
+        SmallShared sm;
+    } U;
     __shared__ u64 red[NW];
     Decision d;
-    const int dec = decide(a, L, d);
+    const int dec = decide(a, li, d);
     const bool go = dec == 2;
     const u32 t = threadIdx.x;
+    const int32_t L = d.L;
+    u64 nfr = d.nh;
+#pragma unroll
+    for (int k = 0; k < NQS; ++k) nfr += d.nseg[k];
+    // every block reaches the same verdict: the inputs are not written by this launch
+    const bool small = go && a.small && d.mode == 0 && d.prev_mode == 0 && nfr <= SMALL_N && d.mq <= SMALL_M;
     if (blockIdx.x == 0) {
-        u64* zp = reinterpret_cast<u64*>(a.C + (L + 1) % 3);
+        u64* zp = reinterpret_cast<u64*>(a.C + (li + 1) % 3);
         for (u32 i = t; i < sizeof(LevelCnt) / 8; i += TB) zp[i] = 0;
-        if (t == 0) {
-            LevelState& s = a.S[L & 1];
+        if (t == 0 && !small) {
+            LevelState& s = a.S[li & 1];
             s.mode = d.mode;
             s.done = go ? 0 : 1;
             s.vsel = (go && d.mode == 1) ? 1 - d.vsel : d.vsel;
@@ -329,11 +590,23 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
             if (dec == 1) {
                 a.host[1] = (int64_t)a.nmode[0];
                 a.host[2] = (int64_t)a.nmode[1];
+                a.host[3] = (int64_t)li + 1;
                 __atomic_store_n(&a.host[0], (int64_t)L, __ATOMIC_RELEASE);
             }
         }
     }
+    if (small) {
+        if (blockIdx.x == 0) small_levels<Off, SYM>(a, g, d, li, U.sm, red);
+        return;
+    }
     if (!go) return;
+    LbShared<HUB_TILE>& sh = U.lv.sh;
+    BlockQ& q = U.lv.q;
+    u32* s_excl = U.lv.s_excl;
+    u64* s_beg = U.lv.s_beg;
+    u32* s_wex = U.lv.s_wex;
+    u64* s_fw = U.lv.s_fw;
+    LevelCnt* cacc = a.C + li % 3;
     if (t == 0) q.n = q.nh = 0;
     const int32_t nl = L + 1;
     const int cp = L & 1;
@@ -371,9 +644,9 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
             }
 #pragma unroll
             for (int k = 0; k < HUB_TILE / TB; ++k)
-                stage<Off, SYM>(q, a, g, L, c[k], vv[k],
+                stage<Off, SYM>(q, a, cacc, g, L, c[k], vv[k],
                                 c[k] && !SYM ? (u64)(g.crow[vv[k] + 1] - g.crow[vv[k]]) : 0ull, acc);
-            flush(q, a, L);
+            flush(q, a, cacc, L);
         }
         // Walk the edges of up to 256 frontier vertices (one per thread: deg, beg) in
         // 256-edge steps; owner of an edge = binary search over the block's degree scan.
@@ -395,10 +668,10 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                     c = claim(vis, v);
                     if (c) a.dist[v] = nl;
                 }
-                stage<Off, SYM>(q, a, g, L, c, v, c && !SYM ? (u64)(g.crow[v + 1] - g.crow[v]) : 0ull, acc);
+                stage<Off, SYM>(q, a, cacc, g, L, c, v, c && !SYM ? (u64)(g.crow[v + 1] - g.crow[v]) : 0ull, acc);
                 __syncthreads();
                 // block-uniform: tot is uniform and q.n is read after the barrier
-                if (base + TB >= tot || q.n > (u32)(QCAP - TB)) flush(q, a, L);
+                if (base + TB >= tot || q.n > (u32)(QCAP - TB)) flush(q, a, cacc, L);
             }
         };
         if (d.prev_mode == 0) {
@@ -475,7 +748,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
         // at a time. Output is bitmaps only (vis_next, fnew): no queue, no block barrier.
         const u64* vis = a.vis[d.vsel];
         u64* vout = a.vis[1 - d.vsel];
-        u32* newb = s_new[wave_id()];  // found bits of the scw words, as 32-bit halves
+        u32* newb = U.lv.s_new[wave_id()];  // found bits of the scw words, as 32-bit halves
         // words per wave task: SC, halved while the tasks do not cover the grid's waves
         // (a small graph would otherwise leave most of the chip idle)
         u32 scw = SC;
@@ -631,8 +904,8 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
             }
         }
     }
-    flush(q, a, L);
-    flush_acc(a, L, acc, red);
+    flush(q, a, cacc, L);
+    flush_acc(cacc, acc, red);
 }
 
 // dist := INF, vis := isolated-vertex mask, then the source; level -1's counters
@@ -680,9 +953,11 @@ __global__ __launch_bounds__(TB) void bfs_init_k(BfsArgs a, Graph_d<Off> g, cons
         c.in_next[0] = (u64)(g.crow[s + 1] - g.crow[s]);
         LevelState& st = a.S[1];
         st = LevelState{};
+        st.level = -1;
         st.m_u = nnz;
         a.nmode[0] = a.nmode[1] = 0;
         a.host[0] = -1;
+        a.host[3] = 0;
     }
 }
 
@@ -739,7 +1014,7 @@ struct BfsWorkHolder {
     DevBuf<u64> fnew;   // frontier bitmap written by pull levels
     DevBuf<uint8_t> ctl;  // C[3] + S[2] + nmode[2]
     int64_t* host = nullptr;  // mapped pinned host words (see BfsArgs::host)
-    int32_t last_depth = 0;   // levels of the previous solve: sizes the first batch
+    int32_t last_launches = 0;  // level launches the previous solve used: sizes the first batch
     ~BfsWorkHolder() {
         if (host) (void)hipHostFree(host);
     }
@@ -763,6 +1038,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     a.alpha = g.alpha;
     a.beta = g.beta;
     a.force = g.force_mode;
+    a.small = g.bfs_small;
     a.max_levels = g.max_levels > 0 ? g.max_levels : INT_INF;
     a.dist = g.dist.p;
     a.vis[0] = g.visited.p;
@@ -796,25 +1072,25 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
         bfs_init_k<Off><<<grid_for(std::max(n / 4, nwords), TB, (unsigned)ctx.cu_count * 4u), TB, 0, s>>>(
             a, gd, w.zmask.p, source, (double)g.nnz);
         PJ_LAUNCH_CHECK();
-        int32_t L = 0;
-        // first batch: the previous solve's depth + 1 (+1 for the level that detects the
-        // end), so a repeated solve on the same graph usually needs one host check
-        int batch = g.level_batch > 0 ? g.level_batch : std::max(4, w.last_depth + 2);
+        int32_t li = 0;  // launch index (a launch runs one level, or several small ones)
+        // first batch: the previous solve's launches, so a repeated solve on the same graph
+        // usually needs one host check and no idle launch behind the last level
+        int batch = g.level_batch > 0 ? g.level_batch : std::max(2, w.last_launches);
         for (;;) {
-            for (int i = 0; i < batch && L < INT_INF; ++i, ++L) {
-                if (g.symmetric) bfs_level_k<Off, true><<<grid, TB, 0, s>>>(a, gd, L);
-                else bfs_level_k<Off, false><<<grid, TB, 0, s>>>(a, gd, L);
+            for (int i = 0; i < batch && li < INT_INF; ++i, ++li) {
+                if (g.symmetric) bfs_level_k<Off, true><<<grid, TB, 0, s>>>(a, gd, li);
+                else bfs_level_k<Off, false><<<grid, TB, 0, s>>>(a, gd, li);
                 PJ_LAUNCH_CHECK();
             }
             // end event right behind this batch's last level (re-recorded per batch), so the
             // device time does not include the host's done-word round trip
             PJ_HIP(hipEventRecord(g.ev1, s));
             PJ_HIP(hipStreamSynchronize(s));
-            if (*(volatile int64_t*)w.host >= 0 || L >= INT_INF) break;
+            if (*(volatile int64_t*)w.host >= 0 || li >= INT_INF) break;
             batch = batch < 1024 ? batch * 2 : batch;
         }
         st.levels = *(volatile int64_t*)w.host;
-        w.last_depth = (int32_t)st.levels;
+        w.last_launches = (int32_t)((volatile int64_t*)w.host)[3];
     }
     if (!valid) PJ_HIP(hipEventRecord(g.ev1, s));
     PJ_HIP(hipEventSynchronize(g.ev1));

@@ -186,7 +186,8 @@ struct Graph {
 
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;
-    double pull_factor = 4.0;
+    double pull_factor = 4.0;  // v1, symmetric: pull a band's heavy edges when the heavy edges of unsettled
+                               // vertices < pull_factor x the members' heavy edges (0 = never)
     double band_width = 0.0;   // v2: width of a band [lo, lo + band_width) (0 = delta, at most delta)
     double tail_delta = -1.0;  // v2: light threshold and band width of the tail (0 = off, < 0 = 64 x delta):
     int tail_after = 1;        // from the first band >= tail_after at which the edges of unsettled
@@ -195,12 +196,12 @@ struct Graph {
                                // frontier's light edges x pull_grow exceed the pull threshold
     double light_pull = 2.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
                                // the light edges of unsettled vertices / light_pull (0 = never)
-    int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based  // weighted, symmetric: pull a band's heavy edges when the heavy edges
-                               // of unsettled vertices < pull_factor x the members' heavy edges (0 = never)
+    int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
     int level_batch = 0; // BFS levels enqueued per host check (0 = default 8, doubling)
     int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
+    int bfs_small = 1;   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)
     int max_levels = 0;  // debug: truncate the BFS after this many levels (0 = off)
     int ms_width = 0;    // batch BFS: widest pass in 64-source words (0 = 4, i.e. 256 sources)
     double ms_alpha = 16.0;  // batch BFS: push levels while the frontier's out-edges < nnz / ms_alpha

@@ -77,15 +77,18 @@ def test_parse_weird_lines(ctx, oracle):
             ctx.load_snap_buffer(bad)
 
 
+@pytest.mark.parametrize("small", [0, 1])
 @pytest.mark.parametrize("kind", ["uniform", "hub", "chain"])
 @pytest.mark.parametrize("direction", [0, 1, 2])
-def test_bfs_random_graphs(ctx, oracle, kind, direction):
+def test_bfs_random_graphs(ctx, oracle, kind, direction, small):
+    """small = 1: levels with small push frontiers run on one workgroup (bfs.hip small_levels)."""
     rng = np.random.default_rng(100 + 7 * direction + len(kind))
     for trial in range(4):
         n = int(rng.integers(2, 60000))
         src, dst = random_graph(rng, kind, n)
         g = ctx.load_coo(src, dst, n=n)
         g.set_option("direction", direction)
+        g.set_option("bfs_small", small)
         row, col, _ = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n)
         roots = [int(src[0]) if len(src) else 0, int(rng.integers(0, n)), n, -5]
         for r in roots:
@@ -131,6 +134,13 @@ def test_bfs_kronecker_s22_full_size(ctx, oracle):
     assert (d == exp).all()
     st = g.stats()
     assert st["bu_levels"] > 0 and st["td_levels"] > 0  # direction switching exercised
+    # push-only levels of millions of vertices overflow the per-block hub staging (the
+    # overflow path once lost hubs in about 1 of 50 such solves), with and without the
+    # one-workgroup small levels
+    g.set_option("direction", 1)
+    for small in (1, 0, 1):
+        g.set_option("bfs_small", small)
+        assert (g.sssp(r) == exp).all(), small
     g.close()
 
 

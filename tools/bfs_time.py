@@ -1,5 +1,7 @@
-"""Unit-weight solve times: web-Google-shaped synthetic (configs[0], source 0) and Kronecker s22
-(configs[1], 8 sampled roots), median kernel ms per direction policy.
+"""Unit-weight solve times: web-Google-shaped synthetic (configs[0]: source 0 and 7 sampled roots) and
+Kronecker s22 (configs[1], 8 sampled roots), median kernel ms per direction policy, with and without
+the one-workgroup small-frontier levels (option bfs_small). Distances of every variant are checked
+against the first variant of the same root (bit-exact).
 Usage: python tools/bfs_time.py [key=value ...]   (libpj graph options)"""
 import os, sys
 import numpy as np
@@ -8,18 +10,35 @@ import paralleljohnson_amd as pj
 
 ctx = pj.Context(0)
 opts = [kv.split("=") for kv in sys.argv[1:]]
-for name, g, roots in (("wg", ctx.generate_webgraph(), [0]), ("k22", None, None)):
-    if g is None:
+for name in ("wg", "k22"):
+    if name == "wg":
+        g = ctx.generate_webgraph()
+        roots = [0] + [int(r) for r in g.sample_roots(7, 3)]
+    else:
         g = ctx.generate_kronecker(22, 16, 1)
         roots = [int(r) for r in g.sample_roots(7, 8)]
     for k, v in opts:
         g.set_option(k, float(v))
+    ref = {}
     for mode in (0, 1, 2):
         g.set_option("direction", mode)
-        ts = []
-        for _ in range(4):
-            for r in roots:
-                g.sssp(r, copy=False)
-                ts.append(g.stats()["kernel_ms"])
-        print(f"{name} direction={mode} median kernel_ms {np.median(ts):.4f} min {np.min(ts):.4f}", flush=True)
+        for small in (0, 1):
+            g.set_option("bfs_small", small)
+            ts, t0, lv = [], [], []
+            for rep in range(4):
+                for r in roots:
+                    d = g.sssp(r, copy=(rep == 0))
+                    st = g.stats()
+                    ts.append(st["kernel_ms"])
+                    if r == roots[0]:
+                        t0.append(st["kernel_ms"])
+                    if rep == 0:
+                        lv.append(st["levels"])
+                        if r in ref:
+                            assert np.array_equal(d, ref[r]), (name, mode, small, r)
+                        else:
+                            ref[r] = d
+            print(f"{name} direction={mode} small={small} median kernel_ms {np.median(ts):.4f} "
+                  f"min {np.min(ts):.4f} root0 {np.median(t0):.4f} levels {lv}", flush=True)
     g.close()
+print("bfs_time: all variants bit-identical", flush=True)
