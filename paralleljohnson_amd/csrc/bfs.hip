@@ -163,7 +163,6 @@ __device__ __forceinline__ int decide(const BfsArgs& a, int32_t li, Decision& d)
         in += pc.in_next[k];
         fz += pc.fnz[k];
     }
-    (void)nn;
     d.mq = mq;
     d.found = fd;
     d.m_u = ps.m_u - (double)in;
@@ -175,6 +174,11 @@ __device__ __forceinline__ int decide(const BfsArgs& a, int32_t li, Decision& d)
     } else if ((double)fd < (double)a.n / a.beta && fd < ps.prev_found) {
         d.mode = 0;
     }
+    // a queued frontier small enough for one workgroup stays push: a pull level costs a
+    // pass over the whole visited bitmap, small_levels a few dependent loads (web-graph
+    // tails, where the unvisited in-edges are few but the unvisited vertices are not)
+    if (a.small && a.force == 0 && d.mode == 1 && d.prev_mode == 0 && nn + d.nh <= SMALL_N && mq <= SMALL_M)
+        d.mode = 0;
     return 2;
 }
 
@@ -468,8 +472,8 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
         const int32_t L2 = L + 1;
         const double m_u2 = m_u - (double)in;
         const bool end = NF == 0 || L2 + 1 >= INT_INF || L2 >= a.max_levels;
-        const bool pull = a.force == 2 || (a.force == 0 && (double)mq > m_u2 / a.alpha);
-        if (!end && !pull && NF <= SMALL_N && mq <= SMALL_M) {
+        // (decide() keeps a frontier this small in push mode unless the caller forces pull)
+        if (!end && a.force != 2 && NF <= SMALL_N && mq <= SMALL_M) {
             if (t < NF) {
                 ss.cv[t] = ss.nv[t];
                 ss.cdeg[t] = ss.ndeg[t];
@@ -574,7 +578,8 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
 #pragma unroll
     for (int k = 0; k < NQS; ++k) nfr += d.nseg[k];
     // every block reaches the same verdict: the inputs are not written by this launch
-    const bool small = go && a.small && d.mode == 0 && d.prev_mode == 0 && nfr <= SMALL_N && d.mq <= SMALL_M;
+    const bool queued = d.prev_mode == 0;  // the frontier is in the queues (else in fnew)
+    const bool small = go && a.small && d.mode == 0 && queued && nfr <= SMALL_N && d.mq <= SMALL_M;
     if (blockIdx.x == 0) {
         u64* zp = reinterpret_cast<u64*>(a.C + (li + 1) % 3);
         for (u32 i = t; i < sizeof(LevelCnt) / 8; i += TB) zp[i] = 0;
@@ -674,7 +679,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                 if (base + TB >= tot || q.n > (u32)(QCAP - TB)) flush(q, a, cacc, L);
             }
         };
-        if (d.prev_mode == 0) {
+        if (queued) {
             // ---- normal queue: a block takes G entries. A block walks its group's edges
             // in dependent 256-edge steps, so a small frontier in 256-entry groups would run
             // on a handful of blocks; G shrinks while the groups still fit in one pass of the grid.

@@ -2,27 +2,31 @@
 Kronecker s22 (configs[1], 8 sampled roots), median kernel ms per direction policy, with and without
 the one-workgroup small-frontier levels (option bfs_small). Distances of every variant are checked
 against the first variant of the same root (bit-exact).
-Usage: python tools/bfs_time.py [key=value ...]   (libpj graph options)"""
+Usage: python tools/bfs_time.py [graphs=wg,k22] [dirs=0,1,2] [smalls=0,1] [key=value ...]  (libpj graph options)"""
 import os, sys
 import numpy as np
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
 import paralleljohnson_amd as pj
 
 ctx = pj.Context(0)
-opts = [kv.split("=") for kv in sys.argv[1:]]
-for name in ("wg", "k22"):
+opts = dict(kv.split("=") for kv in sys.argv[1:])
+graphs = opts.pop("graphs", "wg,k22").split(",")
+dirs = [int(x) for x in opts.pop("dirs", "0,1,2").split(",")]
+smalls = [int(x) for x in opts.pop("smalls", "0,1").split(",")]
+tag = " ".join(f"{k}={v}" for k, v in opts.items())
+for name in graphs:
     if name == "wg":
         g = ctx.generate_webgraph()
         roots = [0] + [int(r) for r in g.sample_roots(7, 3)]
     else:
         g = ctx.generate_kronecker(22, 16, 1)
         roots = [int(r) for r in g.sample_roots(7, 8)]
-    for k, v in opts:
+    for k, v in opts.items():
         g.set_option(k, float(v))
     ref = {}
-    for mode in (0, 1, 2):
+    for mode in dirs:
         g.set_option("direction", mode)
-        for small in (0, 1):
+        for small in smalls:
             g.set_option("bfs_small", small)
             ts, t0, lv = [], [], []
             for rep in range(4):
@@ -38,7 +42,7 @@ for name in ("wg", "k22"):
                             assert np.array_equal(d, ref[r]), (name, mode, small, r)
                         else:
                             ref[r] = d
-            print(f"{name} direction={mode} small={small} median kernel_ms {np.median(ts):.4f} "
+            print(f"{name} {tag} direction={mode} small={small} median kernel_ms {np.median(ts):.4f} "
                   f"min {np.min(ts):.4f} root0 {np.median(t0):.4f} levels {lv}", flush=True)
     g.close()
 print("bfs_time: all variants bit-identical", flush=True)
