@@ -187,8 +187,37 @@ int pj_sssp_batch_write(pj_graph* g, const int64_t* sources, int n_src, const ch
 int pj_last_stats(const pj_graph* g, pj_stats* out);
 int pj_reach_stats(pj_graph* g, pj_stats* out);
 /* Tuning knobs: alpha/beta of the direction switch (Beamer), delta for
- * delta-stepping (0 = automatic). Returns PJ_ERR_ARG on bad values. */
+ * delta-stepping (0 = automatic), direction (0 auto, 1 push, 2 pull),
+ * bfs_small (one-workgroup levels for small frontiers, 0/1) and the batch /
+ * grid knobs documented in DESIGN.md. Returns PJ_ERR_ARG on bad values. */
 int pj_set_option(pj_graph* g, const char* key, double value);
+
+/* ---- shortest-path tree (no reference counterpart:
+ * the reference writes distances only, output_vector :32-46) --------------- */
+
+/* Parent array of the last pj_sssp on g (host, n int64): parent[v] = the
+ * smallest u with an edge u -> v of weight w and dist[u] + w == dist[v],
+ * parent[source] = source, -1 where dist[v] = PJ_INT_INF. A function of the
+ * distances alone, so every solver path gives the same tree. PJ_ERR_STATE when
+ * the last solve was a batch or none ran. */
+int pj_parent_tree(pj_graph* g, int64_t* parent_out);
+
+/* Graph500-style validation of a parent array against the graph and the last
+ * pj_sssp's distances (which must be from `source`, else PJ_ERR_STATE). Each
+ * bad_* field counts violations; all zero = valid. */
+typedef struct pj_tree_report {
+    int64_t reached;        /* vertices with dist < PJ_INT_INF (the source included) */
+    int64_t bad_root;       /* 1 when parent[source] != source or dist[source] != 0 */
+    int64_t bad_reach;      /* parent[v] != -1 not exactly where dist[v] < PJ_INT_INF (or out of range) */
+    int64_t bad_tree_edge;  /* parent[v] = u with no edge u -> v of dist[u] + w == dist[v] */
+    int64_t bad_edge;       /* edges u -> v (dist[u] finite) with dist[v] > min(dist[u] + w, PJ_INT_INF) */
+    int64_t bad_cycle;      /* reached vertices whose parent chain does not end at the source */
+} pj_tree_report;
+int pj_validate_tree(pj_graph* g, int64_t source, const int64_t* parent, pj_tree_report* out);
+
+/* Write a parent array as text: "the parent tree is:\n", then parent[v] per
+ * line (-1 for unreached), in vertex order (the sol_file layout). */
+int pj_write_parents(const int64_t* parent, int64_t n, const char* path);
 
 /* ---- stream ---------------------------------------------------------------- */
 

@@ -63,6 +63,11 @@ class Stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class TreeReport(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int64) for k in ("reached", "bad_root", "bad_reach", "bad_tree_edge", "bad_edge",
+                                              "bad_cycle")]
+
+
 class LoadStats(ctypes.Structure):
     _fields_ = [("read_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("parse_ms", ctypes.c_double),
                 ("csr_ms", ctypes.c_double), ("text_bytes", ctypes.c_int64)]
@@ -105,6 +110,9 @@ _SIGS = {
     "pj_write_sol": ([_P, _I64, ctypes.c_char_p, _INT], _INT),
     "pj_format_sol": ([_P, _I64, _P, _I64, _P], _INT),
     "pj_set_stream": ([_P, _P], _INT),
+    "pj_parent_tree": ([_P, _P], _INT),
+    "pj_validate_tree": ([_P, _I64, _P, _P], _INT),
+    "pj_write_parents": ([_P, _I64, ctypes.c_char_p], _INT),
     "pj_part_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _INT, _PP], _INT),
     "pj_part_load_coo": ([_P, _P, _P, _I64, _I64, _INT, _INT, _INT, _PP], _INT),
     "pj_part_load_snap": ([_P, ctypes.c_char_p, _INT, _INT, _PP], _INT),
@@ -249,6 +257,22 @@ class Graph:
     def set_option(self, key: str, value: float):
         _check(_lib.pj_set_option(self._h, key.encode(), float(value)))
 
+    # -- shortest-path tree (pj_parent_tree / pj_validate_tree) --------------
+    def parent_tree(self) -> np.ndarray:
+        """Parents of the last single-source solve (int64, -1 = unreached)."""
+        out = np.empty(max(self.n, 1), np.int64)
+        _check(_lib.pj_parent_tree(self._h, _ptr(out)))
+        return out[: self.n]
+
+    def validate_tree(self, source: int, parent: np.ndarray) -> dict:
+        """Graph500-style checks of `parent` against the last solve from `source` (all bad_* 0 = valid)."""
+        p = np.ascontiguousarray(parent, dtype=np.int64)
+        if len(p) != self.n:
+            raise ValueError("one parent per vertex")
+        rep = TreeReport()
+        _check(_lib.pj_validate_tree(self._h, int(source), _ptr(p), ctypes.byref(rep)))
+        return {k: getattr(rep, k) for k, _ in rep._fields_}
+
     # -- inspection --------------------------------------------------------
     def save(self, path: str, src_size: int = -1, src_mtime_ns: int = -1):
         """Binary CSR cache of this graph (pj_graph_save)."""
@@ -360,6 +384,11 @@ def format_sol(dist) -> bytes:
 def write_sol(dist, path: str, strict: bool = False):
     d = np.ascontiguousarray(np.asarray(dist, dtype=np.int32))
     _check(_lib.pj_write_sol(_ptr(d), len(d), os.fsencode(path), int(strict)))
+
+
+def write_parents(parent, path: str):
+    p = np.ascontiguousarray(parent, dtype=np.int64)
+    _check(_lib.pj_write_parents(_ptr(p), len(p), os.fsencode(path)))
 
 
 def device_count() -> int:

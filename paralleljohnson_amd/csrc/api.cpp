@@ -577,6 +577,7 @@ int pj_sssp(pj_graph* pg, int64_t source, int32_t* dist_out) {
         g.batch_stats = false;
         if (g.weighted) delta_solve(g, source);
         else bfs_solve(g, source);
+        g.last_source = source;
         if (dist_out && g.n) PJ_HIP(hipMemcpy(dist_out, g.dist.p, 4 * (size_t)g.n, hipMemcpyDeviceToHost));
         g.stats.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         return (int)PJ_OK;
@@ -597,6 +598,62 @@ int pj_copy_dist(pj_graph* pg, int32_t* dist_out) {
 }
 
 const int32_t* pj_dist_device(pj_graph* pg) { return (pg && pg->g.have_result) ? pg->g.dist.p : nullptr; }
+
+// ---- shortest-path tree (tree.hip) ---------------------------------------------
+
+int pj_parent_tree(pj_graph* pg, int64_t* parent_out) {
+    if (!pg || (!parent_out && pg->g.n > 0)) return arg_error("pj_parent_tree: bad argument");
+    if (!pg->g.have_result) {
+        set_error("pj_parent_tree: no single-source solve has run on this graph");
+        return PJ_ERR_STATE;
+    }
+    return guarded([&] {
+        bind(*pg->g.ctx);
+        parent_tree(pg->g, pg->g.last_source, parent_out);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_validate_tree(pj_graph* pg, int64_t source, const int64_t* parent, pj_tree_report* out) {
+    if (!pg || !out || (!parent && pg->g.n > 0)) return arg_error("pj_validate_tree: bad argument");
+    if (!pg->g.have_result || pg->g.last_source != source) {
+        set_error("pj_validate_tree: the last solve on this graph is not a single-source solve from source");
+        return PJ_ERR_STATE;
+    }
+    return guarded([&] {
+        bind(*pg->g.ctx);
+        validate_tree(pg->g, source, parent, out);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_write_parents(const int64_t* parent, int64_t n, const char* path) {
+    if (!path || n < 0 || (n > 0 && !parent)) return arg_error("pj_write_parents: bad argument");
+    return guarded([&] {
+        FILE* f = std::fopen(path, "wb");
+        if (!f) {
+            set_error(std::string("cannot open ") + path);
+            return (int)PJ_ERR_IO;
+        }
+        static const char hdr[] = "the parent tree is:\n";
+        std::fwrite(hdr, 1, sizeof(hdr) - 1, f);
+        std::vector<char> buf((size_t)1 << 20);
+        size_t k = 0;
+        for (int64_t v = 0; v < n; ++v) {
+            if (k + 24 > buf.size()) {
+                std::fwrite(buf.data(), 1, k, f);
+                k = 0;
+            }
+            k += (size_t)std::snprintf(buf.data() + k, 24, "%lld\n", (long long)parent[v]);
+        }
+        std::fwrite(buf.data(), 1, k, f);
+        if (std::fclose(f) != 0) {
+            set_error(std::string("write failed: ") + path);
+            return (int)PJ_ERR_IO;
+        }
+        return (int)PJ_OK;
+    });
+}
 
 int pj_sssp_batch(pj_graph* pg, const int64_t* sources, int n_src, int32_t* dist_out) {
     if (!pg || (n_src > 0 && !sources) || n_src < 0) return arg_error("pj_sssp_batch: bad argument");

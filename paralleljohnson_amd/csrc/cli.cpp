@@ -305,6 +305,26 @@ int run_partitioned(const char* webfile, int source, const char* out, int P, int
     return 0;
 }
 
+// PJ_PARENTS=<path>: the shortest-path tree of the solve, validated by the Graph500
+// checks on the device (a failed check is an error, rc 255), written as one parent
+// id per line. No reference counterpart.
+void write_tree(pj_graph* g, int source, int64_t n, const char* path) {
+    std::vector<int64_t> parent((size_t)n);
+    int rc = pj_parent_tree(g, parent.data());
+    if (rc != PJ_OK) fail("pj_parent_tree", rc);
+    pj_tree_report r{};
+    rc = pj_validate_tree(g, source, parent.data(), &r);
+    if (rc != PJ_OK) fail("pj_validate_tree", rc);
+    const int64_t bad = r.bad_root + r.bad_reach + r.bad_tree_edge + r.bad_edge + r.bad_cycle;
+    std::cerr << "parent tree: " << r.reached << " vertices reached, validation "
+              << (bad ? "FAILED" : "passed") << " (root " << r.bad_root << ", reach " << r.bad_reach << ", tree edges "
+              << r.bad_tree_edge << ", edges " << r.bad_edge << ", cycles " << r.bad_cycle << ")" << std::endl;
+    if (bad) std::exit(-1);
+    rc = pj_write_parents(parent.data(), n, path);
+    if (rc != PJ_OK) fail("pj_write_parents", rc);
+    std::cerr << "the parent tree has been saved in file " << path << std::endl;
+}
+
 int run_single(const char* webfile, int source, const char* out, int weighted) {
     Phases ph;
     pj_ctx* ctx = nullptr;
@@ -340,6 +360,7 @@ int run_single(const char* webfile, int source, const char* out, int weighted) {
     if (rc != PJ_OK) fail("pj_write_sol", rc);
     ph.mark("write");
     std::cerr << "the shortest path distance vector has been saved in file " << out << std::endl;
+    if (const char* pp = std::getenv("PJ_PARENTS"); pp && *pp) write_tree(g, source, n, pp);
     pj_graph_destroy(g);
     pj_destroy(ctx);
     return 0;
@@ -366,6 +387,12 @@ int main(int argc, char* argv[]) {
 
     print_msg("process 0 reads in the web graph data......");
     const char* srcs = std::getenv("PJ_SOURCES");
+    const char* parents = std::getenv("PJ_PARENTS");
+    if (parents && *parents && (P > 1 || (srcs && *srcs))) {
+        std::cerr << "PJ_PARENTS: the parent tree needs a single-source run on one GPU (P = 1, no PJ_SOURCES)"
+                  << std::endl;
+        std::exit(-1);
+    }
     if (srcs && *srcs) return run_multi_source(argv[1], parse_sources(srcs), argv[3], P, weighted);
     const int source_node = std::atoi(argv[2]);  // :448
     if (P > 1) return run_partitioned(argv[1], source_node, argv[3], P, weighted);

@@ -207,6 +207,7 @@ struct Graph {
     double ms_alpha = 16.0;  // batch BFS: push levels while the frontier's out-edges < nnz / ms_alpha
 
     bool have_result = false;
+    i64 last_source = -1;      // source of the single-source result in dist (parent tree)
     bool batch_stats = false;  // stats describe the last pj_sssp_batch
     pj_load_stats load{};      // how the graph was built (pj_graph_load_stats)
     pj_stats stats{};
@@ -257,6 +258,9 @@ void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out)
 using MsPassFn = std::function<void(int, int, const int32_t*)>;
 void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_pass);
 void reach_stats(Graph& g, i64* n_r, i64* m_r);
+// shortest-path tree of g.dist (tree.hip)
+void parent_tree(Graph& g, i64 source, int64_t* host_out);
+void validate_tree(Graph& g, i64 source, const int64_t* host_parent, pj_tree_report* rep);
 void debug_bitmaps(Graph& g, u64* vis0, u64* vis1, u64* fnew);
 
 // 1D vertex partition (part.hip)

@@ -1,0 +1,205 @@
+// tree.hip — shortest-path tree of a single-source solve and its Graph500-style
+// validation (the reference has no counterpart: it writes
+// distances only, output_vector :32-46).
+//
+// parent[v] = the smallest u with an edge u -> v of weight w and dist[u] + w ==
+// dist[v] (< PJ_INT_INF), parent[source] = source, -1 for unreached vertices.
+// The smallest tight in-neighbour makes the tree a function of the distances
+// alone, so it is identical for every solver path (BFS levels, delta bands,
+// either direction) and for a CPU restatement.
+//
+// Validation (the Graph500 BFS / SSSP checks, restated for the capped int32
+// distances of the reference), against the graph's CSR and the
+// solve's distances:
+//   root   parent[source] == source and dist[source] == 0
+//   reach  parent[v] != -1 exactly when dist[v] < PJ_INT_INF
+//   tree   every parent edge u -> v exists with dist[u] + w == dist[v]
+//   edge   no edge u -> v with dist[u] < INF relaxes: dist[v] <= min(dist[u] + w, INF)
+//   cycle  every reached vertex's parent chain ends at the source (pointer
+//          jumping, ceil(log2 n) + 1 rounds)
+#include "devutil.h"
+
+namespace pj {
+
+namespace {
+
+constexpr int LONG_ROW = 32;  // rows longer than this are walked by the whole wave
+
+struct TreeCnt {
+    u64 reached, bad_root, bad_reach, bad_tree, bad_edge, bad_cycle;
+};
+
+// Every CSR edge u -> v of a reached row, visited once: short rows by their lane,
+// long rows by the whole wave (lanes over consecutive entries). f(u, du, v, w).
+template <typename Off, bool W, typename F>
+__device__ __forceinline__ void for_reached_edges(const Off* __restrict__ row, const u32* __restrict__ col,
+                                                  const u32* __restrict__ wt, const int32_t* __restrict__ dist,
+                                                  i64 n, F f) {
+    const int lane = lane_id();
+    const i64 stride = (i64)gridDim.x * blockDim.x;
+    for (i64 base = (i64)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < n; base += stride) {
+        const i64 u = base + lane;
+        const bool ok = u < n && dist[u] < INT_INF;
+        const int32_t du = ok ? dist[u] : 0;
+        const Off b = ok ? row[u] : 0, e = ok ? row[u + 1] : 0;
+        const bool lng = ok && e - b > (Off)LONG_ROW;
+        if (ok && !lng)
+            for (Off k = b; k < e; ++k) f(u, du, col[k], W ? wt[k] : 1u);
+        u64 m = __ballot(lng);
+        while (m) {
+            const int l = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const Off kb = __shfl(b, l, 64), ke = __shfl(e, l, 64);
+            const i64 ul = __shfl(u, l, 64);
+            const int32_t dl = __shfl(du, l, 64);
+            for (Off k = kb + (Off)lane; k < ke; k += WAVE) f(ul, dl, col[k], W ? wt[k] : 1u);
+        }
+    }
+}
+
+template <typename Off, bool W>
+__global__ __launch_bounds__(256) void parent_k(const Off* __restrict__ row, const u32* __restrict__ col,
+                                                const u32* __restrict__ wt, const int32_t* __restrict__ dist, i64 n,
+                                                u32* __restrict__ par) {
+    for_reached_edges<Off, W>(row, col, wt, dist, n, [&](i64 u, int32_t du, u32 v, u32 w) {
+        const int32_t dv = dist[v];
+        if (dv < INT_INF && (i64)du + (i64)w == (i64)dv && par[v] > (u32)u) atomicMin(&par[v], (u32)u);
+    });
+}
+
+__global__ void parent_out_k(const u32* __restrict__ par, i64 n, i64 source, int64_t* __restrict__ out) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x)
+        out[v] = v == source ? source : (par[v] == 0xffffffffu ? -1 : (int64_t)par[v]);
+}
+
+template <typename Off, bool W>
+__global__ __launch_bounds__(256) void tree_edges_k(const Off* __restrict__ row, const u32* __restrict__ col,
+                                                    const u32* __restrict__ wt, const int32_t* __restrict__ dist,
+                                                    i64 n, const int64_t* __restrict__ par, u32* __restrict__ ok,
+                                                    TreeCnt* __restrict__ c) {
+    u64 bad = 0;
+    for_reached_edges<Off, W>(row, col, wt, dist, n, [&](i64 u, int32_t du, u32 v, u32 w) {
+        const int32_t dv = dist[v];
+        const i64 via = (i64)du + (i64)w;
+        bad += (i64)dv > (via < INT_INF ? via : (i64)INT_INF);
+        if (dv < INT_INF && via == (i64)dv && par[v] == u) atomicOr(&ok[v >> 5], 1u << (v & 31));
+    });
+    if (bad) atomicAdd(&c->bad_edge, bad);
+}
+
+__global__ void tree_vertices_k(const int32_t* __restrict__ dist, i64 n, i64 source, const int64_t* __restrict__ par,
+                                const u32* __restrict__ ok, int64_t* __restrict__ anc, TreeCnt* __restrict__ c) {
+    u64 reached = 0, root = 0, reach = 0, tree = 0;
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
+        const int64_t p = par[v];
+        const int32_t d = dist[v];
+        int64_t a = -1;
+        if (v == source) {
+            root += p != source || d != 0;
+            reached += 1;
+            a = source;
+        } else if (d >= INT_INF) {
+            reach += p != -1;
+        } else {
+            reached += 1;
+            if (p < 0 || p >= n || p == v) reach += 1;
+            else {
+                tree += !((ok[v >> 5] >> (v & 31)) & 1u);
+                a = p;
+            }
+        }
+        anc[v] = a;
+    }
+    if (reached) atomicAdd(&c->reached, reached);
+    if (root) atomicAdd(&c->bad_root, root);
+    if (reach) atomicAdd(&c->bad_reach, reach);
+    if (tree) atomicAdd(&c->bad_tree, tree);
+}
+
+// one pointer-jumping round: anc[v] = anc[anc[v]] (in place: any ancestor stays an ancestor)
+__global__ void jump_k(int64_t* __restrict__ anc, i64 n) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
+        const int64_t a = anc[v];
+        if (a >= 0) anc[v] = anc[a];
+    }
+}
+
+__global__ void cycle_k(const int32_t* __restrict__ dist, const int64_t* __restrict__ anc, i64 n, i64 source,
+                        TreeCnt* __restrict__ c) {
+    u64 bad = 0;
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x)
+        bad += dist[v] < INT_INF && v != source && anc[v] != source;
+    if (bad) atomicAdd(&c->bad_cycle, bad);
+}
+
+unsigned grid_of(const Graph& g, i64 work) { return grid_for(work, 256, (unsigned)g.ctx->cu_count * 8u); }
+
+template <typename Off, bool W>
+void parent_run(Graph& g, u32* par) {
+    const Off* row = static_cast<const Off*>(g.row_ptr());
+    parent_k<Off, W><<<grid_of(g, g.n), 256, 0, g.ctx->stream>>>(row, g.col.p, g.w.p, g.dist.p, g.n, par);
+    PJ_LAUNCH_CHECK();
+}
+
+template <typename Off, bool W>
+void edges_run(Graph& g, const int64_t* par, u32* ok, TreeCnt* c) {
+    const Off* row = static_cast<const Off*>(g.row_ptr());
+    tree_edges_k<Off, W><<<grid_of(g, g.n), 256, 0, g.ctx->stream>>>(row, g.col.p, g.w.p, g.dist.p, g.n, par, ok, c);
+    PJ_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+void parent_tree(Graph& g, i64 source, int64_t* host_out) {
+    const i64 n = g.n;
+    if (n == 0) return;
+    hipStream_t s = g.ctx->stream;
+    DevBuf<u32> par((size_t)n);
+    DevBuf<int64_t> out((size_t)n);
+    PJ_HIP(hipMemsetAsync(par.p, 0xff, 4 * (size_t)n, s));
+    const bool w = g.weighted;
+    if (g.off64) w ? parent_run<u64, true>(g, par.p) : parent_run<u64, false>(g, par.p);
+    else w ? parent_run<u32, true>(g, par.p) : parent_run<u32, false>(g, par.p);
+    parent_out_k<<<grid_of(g, n), 256, 0, s>>>(par.p, n, source, out.p);
+    PJ_LAUNCH_CHECK();
+    PJ_HIP(hipMemcpyAsync(host_out, out.p, 8 * (size_t)n, hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+}
+
+void validate_tree(Graph& g, i64 source, const int64_t* host_parent, pj_tree_report* rep) {
+    const i64 n = g.n;
+    *rep = pj_tree_report{};
+    if (n == 0) return;
+    hipStream_t s = g.ctx->stream;
+    DevBuf<int64_t> par((size_t)n), anc((size_t)n);
+    DevBuf<u32> ok((size_t)((n + 31) / 32));
+    DevBuf<TreeCnt> cnt(1);
+    PJ_HIP(hipMemcpyAsync(par.p, host_parent, 8 * (size_t)n, hipMemcpyHostToDevice, s));
+    PJ_HIP(hipMemsetAsync(ok.p, 0, 4 * (size_t)((n + 31) / 32), s));
+    PJ_HIP(hipMemsetAsync(cnt.p, 0, sizeof(TreeCnt), s));
+    const bool w = g.weighted;
+    if (g.off64) w ? edges_run<u64, true>(g, par.p, ok.p, cnt.p) : edges_run<u64, false>(g, par.p, ok.p, cnt.p);
+    else w ? edges_run<u32, true>(g, par.p, ok.p, cnt.p) : edges_run<u32, false>(g, par.p, ok.p, cnt.p);
+    const unsigned gr = grid_of(g, n);
+    tree_vertices_k<<<gr, 256, 0, s>>>(g.dist.p, n, source, par.p, ok.p, anc.p, cnt.p);
+    PJ_LAUNCH_CHECK();
+    int rounds = 1;
+    while (((i64)1 << (rounds - 1)) < n) ++rounds;  // ceil(log2 n) + 1
+    for (int r = 0; r < rounds; ++r) {
+        jump_k<<<gr, 256, 0, s>>>(anc.p, n);
+        PJ_LAUNCH_CHECK();
+    }
+    cycle_k<<<gr, 256, 0, s>>>(g.dist.p, anc.p, n, source, cnt.p);
+    PJ_LAUNCH_CHECK();
+    TreeCnt h{};
+    PJ_HIP(hipMemcpyAsync(&h, cnt.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    rep->reached = (int64_t)h.reached;
+    rep->bad_root = (int64_t)h.bad_root;
+    rep->bad_reach = (int64_t)h.bad_reach;
+    rep->bad_tree_edge = (int64_t)h.bad_tree;
+    rep->bad_edge = (int64_t)h.bad_edge;
+    rep->bad_cycle = (int64_t)h.bad_cycle;
+}
+
+}  // namespace pj

@@ -95,3 +95,57 @@ def csr_to_text(row, col):
     body = np.char.add(np.char.add(src.astype(str), "\t"), np.asarray(col, dtype=np.int64).astype(str))
     return ("# Directed graph (synthetic, web-Google-shaped)\n# FromNodeId\tToNodeId\n" +
             "\n".join(body.tolist()) + "\n").encode()
+
+
+def tight_parents(row, col, w, dist, source, inf=100000):
+    """CPU restatement of pj_parent_tree: parent[v] = the smallest u with an edge u -> v of
+    weight w and dist[u] + w == dist[v] < inf, parent[source] = source, -1 when unreached."""
+    row = np.asarray(row, dtype=np.int64)
+    n = len(row) - 1
+    d = np.asarray(dist, dtype=np.int64)
+    u = np.repeat(np.arange(n, dtype=np.int64), np.diff(row))
+    v = np.asarray(col).view(np.uint32).astype(np.int64)
+    wt = np.ones_like(v) if w is None else np.asarray(w, dtype=np.int64)
+    tight = (d[u] < inf) & (d[v] < inf) & (d[u] + wt == d[v])
+    par = np.full(n, np.iinfo(np.int64).max, np.int64)
+    np.minimum.at(par, v[tight], u[tight])
+    par[par == np.iinfo(np.int64).max] = -1
+    if 0 <= source < n:
+        par[source] = source
+    return par
+
+
+def graph500_checks(row, col, w, dist, parent, source, inf=100000):
+    """CPU restatement of pj_validate_tree (the Graph500 BFS / SSSP validation, for the
+    capped int32 distances): counts per check, all bad_* zero = valid."""
+    row = np.asarray(row, dtype=np.int64)
+    n = len(row) - 1
+    d = np.asarray(dist, dtype=np.int64)
+    p = np.asarray(parent, dtype=np.int64)
+    u = np.repeat(np.arange(n, dtype=np.int64), np.diff(row))
+    v = np.asarray(col).view(np.uint32).astype(np.int64)
+    wt = np.ones_like(v) if w is None else np.asarray(w, dtype=np.int64)
+    reached = d < inf
+    out = dict(reached=int(reached.sum()), bad_root=0, bad_reach=0, bad_tree_edge=0, bad_edge=0, bad_cycle=0)
+    fu = reached[u]
+    via = d[u] + wt
+    out["bad_edge"] = int((d[v][fu] > np.minimum(via[fu], inf)).sum())
+    ok = np.zeros(n, bool)
+    t = fu & (d[v] < inf) & (via == d[v]) & (p[v] == u)
+    ok[v[t]] = True
+    idx = np.arange(n)
+    other = idx != source
+    out["bad_root"] = int(0 <= source < n and (p[source] != source or d[source] != 0))
+    out["bad_reach"] = int(((~reached) & other & (p != -1)).sum())
+    inner = reached & other
+    badp = inner & ((p < 0) | (p >= n) | (p == idx))
+    out["bad_reach"] += int(badp.sum())
+    good = inner & ~badp
+    out["bad_tree_edge"] = int((good & ~ok).sum())
+    anc = np.where(good, p, -1)
+    if 0 <= source < n:
+        anc[source] = source
+    for _ in range(max(1, int(np.ceil(np.log2(max(n, 2))))) + 1):
+        anc = np.where(anc >= 0, anc[np.maximum(anc, 0)], -1)
+    out["bad_cycle"] = int((inner & (anc != source)).sum())
+    return out
