@@ -1,7 +1,7 @@
 #!/bin/bash
 # BFS parity subset, WG stress, direction-auto timing and a WG kernel trace
 set -o pipefail
-OUT=gpurun_out/r2h; mkdir -p $OUT
+OUT=gpurun_out/${1:-bfs}; mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "random_graphs or s22_full or webgraph or kronecker" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 timeout -k 10 200 python3 -u tools/bfs_stress.py graph=wg reps=4 > $OUT/stress.txt 2>&1 || { grep -v amdgpu $OUT/stress.txt | cut -c1-300 | tail; exit 1; }
