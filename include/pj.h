@@ -133,9 +133,11 @@ int pj_kronecker_write_snap(pj_ctx* ctx, int scale, int edgefactor, uint64_t see
 int pj_generate_webgraph(pj_ctx* ctx, int64_t n_ids, int64_t n_edges, uint64_t seed, pj_graph** out);
 
 /* How a graph was built (host wall times of the ingestion phases; 0 where a
- * phase did not run): the file read (:66-105's getline passes), the copy of
- * the text to the GPU, the GPU parse (line scan + field decode), and the CSR
- * build (radix sort + row offsets, coord2csr :117-159). */
+ * phase did not run): read_ms = the file into HBM (pj_load_snap: pinned
+ * pieces, the read of each overlapped with the H2D copy of the previous;
+ * :66-105's getline passes), h2d_ms = a host buffer's copy to the GPU
+ * (pj_load_snap_buffer), the GPU parse (line scan + field decode), and the CSR
+ * build (radix sort + row offsets, coord2csr :117-159, kernels completed). */
 typedef struct pj_load_stats {
     double read_ms, h2d_ms, parse_ms, csr_ms;
     int64_t text_bytes;

@@ -78,47 +78,82 @@ i64 out_degree(const Graph& g, i64 v) {
     return (i64)(h[1] - h[0]);
 }
 
-// The whole file in host memory, read by up to 16 threads with pread into an
-// uninitialised buffer (a zero-filled vector costs a second pass over the
-// bytes, and one reader thread page-faults the buffer alone). A missing or
-// unopenable file or a directory reads as empty (the reference does not check
-// its ifstream, :67); a file that shrinks while being read is PJ_ERR_IO.
-struct HostText {
-    std::unique_ptr<char[]> data;
-    int64_t len = 0;
-};
+// The file straight into HBM: reader threads pread fixed pieces into pinned
+// staging slots (two per thread, kept in the ctx) and queue each piece's H2D copy
+// as soon as it is read, so the disk / page-cache read and the PCIe copy overlap
+// and no whole-file host buffer is allocated, faulted in and freed (the reference
+// reads the file line by line, :66-105). The device buffer is zero-padded to
+// padded_text_bytes(len) for the parser. A missing or unopenable file or a
+// directory reads as empty (the reference does not check its ifstream, :67); a
+// file that shrinks while being read is PJ_ERR_IO. Returns len.
+constexpr int64_t kStageSlot = (int64_t)8 << 20;
 
-HostText read_text_file(const char* path) {
-    HostText t;
+i64 read_file_to_device(Ctx& c, const char* path, DevBuf<uint8_t>& text) {
+    hipStream_t s = c.stream;
     struct stat sb;
-    if (stat(path, &sb) != 0 || !S_ISREG(sb.st_mode) || sb.st_size <= 0) return t;
-    const int fd = open(path, O_RDONLY);
-    if (fd < 0) return t;
-    const int64_t size = (int64_t)sb.st_size;
-    t.data.reset(new char[(size_t)size]);
-    const int64_t piece = (int64_t)64 << 20;
-    const int64_t npieces = (size + piece - 1) / piece;
-    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(npieces, std::min(16u, std::thread::hardware_concurrency())));
-    std::atomic<int64_t> next{0}, got{0};
+    int fd = -1;
+    int64_t size = 0;
+    if (stat(path, &sb) == 0 && S_ISREG(sb.st_mode) && sb.st_size > 0 && (fd = open(path, O_RDONLY)) >= 0)
+        size = (int64_t)sb.st_size;
+    const i64 padded = padded_text_bytes(size);
+    text.alloc((size_t)padded);
+    PJ_HIP(hipMemsetAsync(text.p + size, 0, (size_t)(padded - size), s));
+    if (size == 0) {
+        if (fd >= 0) close(fd);
+        PJ_HIP(hipStreamSynchronize(s));
+        return 0;
+    }
+    const int64_t npieces = (size + kStageSlot - 1) / kStageSlot;
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(npieces, std::min(8u, std::thread::hardware_concurrency())));
+    while ((int)c.stage.size() < 2 * nt) {
+        char* p = nullptr;
+        hipEvent_t e = nullptr;
+        PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), (size_t)kStageSlot, hipHostMallocDefault));
+        PJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c.stage.push_back(p);
+        c.stage_ev.push_back(e);
+    }
+    std::atomic<int64_t> got{0};
+    std::vector<std::exception_ptr> errs((size_t)nt);
     std::vector<std::thread> th;
-    for (int k = 0; k < nt; ++k)
-        th.emplace_back([&] {
-            for (int64_t c; (c = next.fetch_add(1)) < npieces;) {
-                const int64_t off = c * piece, want = std::min(piece, size - off);
-                int64_t done = 0;
-                while (done < want) {
-                    const ssize_t r = pread(fd, t.data.get() + off + done, (size_t)(want - done), (off_t)(off + done));
-                    if (r <= 0) break;
-                    done += r;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            try {
+                bind(c);
+                int k = 0;
+                for (int64_t piece = t; piece < npieces; piece += nt, ++k) {
+                    const int slot = 2 * t + (k & 1);
+                    if (k >= 2) PJ_HIP(hipEventSynchronize(c.stage_ev[(size_t)slot]));  // its last copy is done
+                    const int64_t off = piece * kStageSlot, want = std::min(kStageSlot, size - off);
+                    char* buf = c.stage[(size_t)slot];
+                    int64_t done = 0;
+                    while (done < want) {
+                        const ssize_t r = pread(fd, buf + done, (size_t)(want - done), (off_t)(off + done));
+                        if (r <= 0) break;
+                        done += r;
+                    }
+                    got.fetch_add(done);
+                    if (done < want) break;
+                    PJ_HIP(hipMemcpyAsync(text.p + off, buf, (size_t)want, hipMemcpyHostToDevice, s));
+                    PJ_HIP(hipEventRecord(c.stage_ev[(size_t)slot], s));
                 }
-                got.fetch_add(done);
+            } catch (...) {
+                errs[(size_t)t] = std::current_exception();
             }
         });
     for (auto& x : th) x.join();
     close(fd);
+    PJ_HIP(hipStreamSynchronize(s));
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
     if (got.load() != size) throw Error(PJ_ERR_IO, std::string("short read of ") + path);
-    t.len = size;
-    return t;
+    return size;
+}
+
+void parse_error(const ParseResult& r) {
+    set_error("edge list line " + std::to_string(r.bad_line) +
+              ": second field missing, negative id or id out of range "
+              "(undefined behaviour in the reference's read_webgraph)");
 }
 
 int finish_graph(pj_ctx* ctx, std::unique_ptr<pj_graph>& pg, pj_graph** out) {
@@ -301,6 +336,8 @@ int pj_destroy(pj_ctx* ctx) {
     if (!ctx) return PJ_OK;
     return guarded([&] {
         bind(ctx->c);
+        for (char* p : ctx->c.stage) (void)hipHostFree(p);
+        for (hipEvent_t e : ctx->c.stage_ev) (void)hipEventDestroy(e);
         if (ctx->c.own_stream) (void)hipStreamDestroy(ctx->c.own_stream);
         delete ctx;
         return (int)PJ_OK;
@@ -319,6 +356,29 @@ int pj_set_stream(pj_ctx* ctx, void* stream) {
     });
 }
 
+namespace {
+
+// COO from the parser -> CSR (+ CSC) on the device; csr_ms includes the kernels' completion
+int graph_from_parse(pj_ctx* ctx, const ParseResult& r, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w,
+                     int weighted, int64_t len, pj_graph** out) {
+    if (r.bad_line) {
+        parse_error(r);
+        return (int)PJ_ERR_PARSE;
+    }
+    auto pg = std::make_unique<pj_graph>();
+    pg->g.ctx = &ctx->c;
+    const auto t0 = std::chrono::steady_clock::now();
+    build_graph_from_coo(pg->g, src, dst, weighted ? &w : nullptr, r.nnz, r.max_id + 1, false);
+    PJ_HIP(hipStreamSynchronize(ctx->c.stream));
+    pg->g.load.csr_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    pg->g.load.h2d_ms = r.h2d_ms;
+    pg->g.load.parse_ms = r.parse_ms;
+    pg->g.load.text_bytes = len;
+    return finish_graph(ctx, pg, out);
+}
+
+}  // namespace
+
 int pj_load_snap_buffer(pj_ctx* ctx, const char* text, int64_t len, int weighted, pj_graph** out) {
     if (!ctx || !out || (len > 0 && !text) || len < 0) return arg_error("pj_load_snap_buffer: bad argument");
     *out = nullptr;
@@ -326,21 +386,7 @@ int pj_load_snap_buffer(pj_ctx* ctx, const char* text, int64_t len, int weighted
         bind(ctx->c);
         DevBuf<u32> src, dst, w;
         ParseResult r = parse_snap_device(ctx->c, text, len, weighted != 0, src, dst, w);
-        if (r.bad_line) {
-            set_error("edge list line " + std::to_string(r.bad_line) +
-                      ": second field missing, negative id or id out of range "
-                      "(undefined behaviour in the reference's read_webgraph)");
-            return (int)PJ_ERR_PARSE;
-        }
-        auto pg = std::make_unique<pj_graph>();
-        pg->g.ctx = &ctx->c;
-        const auto t0 = std::chrono::steady_clock::now();
-        build_graph_from_coo(pg->g, src, dst, weighted ? &w : nullptr, r.nnz, r.max_id + 1, false);
-        pg->g.load.csr_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        pg->g.load.h2d_ms = r.h2d_ms;
-        pg->g.load.parse_ms = r.parse_ms;
-        pg->g.load.text_bytes = len;
-        return finish_graph(ctx, pg, out);
+        return graph_from_parse(ctx, r, src, dst, w, weighted, len, out);
     });
 }
 
@@ -352,14 +398,20 @@ int pj_graph_load_stats(const pj_graph* g, pj_load_stats* out) {
 
 int pj_load_snap(pj_ctx* ctx, const char* path, int weighted, pj_graph** out) {
     if (!ctx || !path || !out) return arg_error("pj_load_snap: bad argument");
+    *out = nullptr;
     return guarded([&] {
+        bind(ctx->c);
         const auto t0 = std::chrono::steady_clock::now();
         // A missing or unreadable file (or a directory) reads as empty, like the
         // reference's unchecked ifstream (:67): N = 0, header-only sol_file.
-        HostText text = read_text_file(path);
+        DevBuf<uint8_t> text;
+        const i64 len = read_file_to_device(ctx->c, path, text);
         const double read_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        const int rc = pj_load_snap_buffer(ctx, text.data.get(), text.len, weighted, out);
-        if (rc == PJ_OK) (*out)->g.load.read_ms = read_ms;
+        DevBuf<u32> src, dst, w;
+        ParseResult r = parse_device_text(ctx->c, text.p, len, weighted != 0, src, dst, w);
+        text.release();
+        const int rc = graph_from_parse(ctx, r, src, dst, w, weighted, len, out);
+        if (rc == PJ_OK) (*out)->g.load.read_ms = read_ms;  // file -> HBM (read and H2D overlapped)
         return rc;
     });
 }
@@ -999,13 +1051,13 @@ int pj_wpart_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_wp
     *out = nullptr;
     return guarded([&] {
         bind(ctx->c);
-        HostText text = read_text_file(path);  // missing file: empty graph, as pj_load_snap (:67)
+        DevBuf<uint8_t> text;  // missing file: empty graph, as pj_load_snap (:67)
+        const i64 len = read_file_to_device(ctx->c, path, text);
         DevBuf<u32> src, dst, w;
-        ParseResult r = parse_snap_device(ctx->c, text.data.get(), text.len, true, src, dst, w);
+        ParseResult r = parse_device_text(ctx->c, text.p, len, true, src, dst, w);
+        text.release();
         if (r.bad_line) {
-            set_error("edge list line " + std::to_string(r.bad_line) +
-                      ": second field missing, negative id or id out of range "
-                      "(undefined behaviour in the reference's read_webgraph)");
+            parse_error(r);
             return (int)PJ_ERR_PARSE;
         }
         *out = reinterpret_cast<pj_wpart*>(wpart_from_coo(ctx->c, src, dst, w, r.nnz, r.max_id + 1, rank, world));
@@ -1149,13 +1201,13 @@ int pj_part_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_par
     *out = nullptr;
     return guarded([&] {
         bind(ctx->c);
-        HostText text = read_text_file(path);  // missing file: empty graph, as pj_load_snap (:67)
+        DevBuf<uint8_t> text;  // missing file: empty graph, as pj_load_snap (:67)
+        const i64 len = read_file_to_device(ctx->c, path, text);
         DevBuf<u32> src, dst, w;
-        ParseResult r = parse_snap_device(ctx->c, text.data.get(), text.len, false, src, dst, w);
+        ParseResult r = parse_device_text(ctx->c, text.p, len, false, src, dst, w);
+        text.release();
         if (r.bad_line) {
-            set_error("edge list line " + std::to_string(r.bad_line) +
-                      ": second field missing, negative id or id out of range "
-                      "(undefined behaviour in the reference's read_webgraph)");
+            parse_error(r);
             return (int)PJ_ERR_PARSE;
         }
         *out = reinterpret_cast<pj_part*>(part_from_coo(ctx->c, src, dst, r.nnz, r.max_id + 1, rank, world, false));

@@ -342,7 +342,7 @@ int run_single(const char* webfile, int source, const char* out, int weighted) {
     ph.mark("load");
     pj_load_stats ls{};
     if (ph.on && pj_graph_load_stats(g, &ls) == PJ_OK)
-        std::cerr << "phase load: read " << ls.read_ms / 1000.0 << " s, h2d " << ls.h2d_ms / 1000.0 << " s, parse "
+        std::cerr << "phase load: file->HBM " << ls.read_ms / 1000.0 << " s (read and H2D overlapped), parse "
                   << ls.parse_ms / 1000.0 << " s, csr " << ls.csr_ms / 1000.0 << " s (" << ls.text_bytes
                   << " bytes of text)" << std::endl;
     std::cerr << "compute shortest paths from source node: " << source << std::endl;

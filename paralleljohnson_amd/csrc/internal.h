@@ -124,6 +124,10 @@ struct Ctx {
     hipStream_t stream = nullptr;      // where work is launched (own or external)
     hipStream_t own_stream = nullptr;  // created by pj_create, destroyed by pj_destroy
     int cu_count = 256;
+    // pinned staging slots of the file loader (api.cpp read_file_to_device), kept for the
+    // ctx's lifetime; freed by pj_destroy
+    std::vector<char*> stage;
+    std::vector<hipEvent_t> stage_ev;
 };
 
 struct BfsWorkHolder;
@@ -243,6 +247,10 @@ struct ParseResult {
 // Parses `len` bytes of host text on the device; fills device COO.
 ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool weighted,
                               DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w);
+// The same from text already on the device (len bytes, zero-padded to padded_text_bytes(len)).
+i64 padded_text_bytes(i64 len);
+ParseResult parse_device_text(Ctx& ctx, const uint8_t* text, i64 len, bool weighted, DevBuf<u32>& src,
+                              DevBuf<u32>& dst, DevBuf<u32>& w);
 
 void generate_webgraph_device(Ctx& ctx, i64 n_ids, i64 n_edges, uint64_t seed, DevBuf<u32>& src,
                               DevBuf<u32>& dst);

@@ -170,25 +170,36 @@ __global__ __launch_bounds__(PB) void parse_lines_k(const uint8_t* __restrict__ 
 
 }  // namespace
 
+i64 padded_text_bytes(i64 len) { return (len + PCHUNK - 1) / PCHUNK * PCHUNK + PTAIL; }
+
 ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool weighted, DevBuf<u32>& src,
                               DevBuf<u32>& dst, DevBuf<u32>& w) {
     hipStream_t s = ctx.stream;
-    ParseResult r;
     const auto t0 = std::chrono::steady_clock::now();
-    const i64 nblocks = (len + PCHUNK - 1) / PCHUNK;
-    const i64 padded = nblocks * PCHUNK + PTAIL;
+    const i64 padded = padded_text_bytes(len);
     DevBuf<uint8_t> text((size_t)padded);
     PJ_HIP(hipMemsetAsync(text.p + len, 0, (size_t)(padded - len), s));
     if (len) PJ_HIP(hipMemcpyAsync(text.p, host_text, (size_t)len, hipMemcpyHostToDevice, s));
     PJ_HIP(hipStreamSynchronize(s));
+    const double h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ParseResult r = parse_device_text(ctx, text.p, len, weighted, src, dst, w);
+    r.h2d_ms = h2d_ms;
+    return r;
+}
+
+// text: len bytes on the device, zero-padded to padded_text_bytes(len)
+ParseResult parse_device_text(Ctx& ctx, const uint8_t* text, i64 len, bool weighted, DevBuf<u32>& src,
+                              DevBuf<u32>& dst, DevBuf<u32>& w) {
+    hipStream_t s = ctx.stream;
+    ParseResult r;
     const auto t1 = std::chrono::steady_clock::now();
-    r.h2d_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    const i64 nblocks = (len + PCHUNK - 1) / PCHUNK;
     DevBuf<u32> bcnt((size_t)(nblocks > 0 ? nblocks : 1));
     DevBuf<u64> boff((size_t)nblocks + 1);
     DevBuf<u64> scal(2);  // [0] = max id + 1, [1] = first bad byte offset
     ScanWs ws;
     if (nblocks) {
-        parse_count_k<<<(unsigned)nblocks, PB, 0, s>>>(text.p, len, bcnt.p);
+        parse_count_k<<<(unsigned)nblocks, PB, 0, s>>>(text, len, bcnt.p);
         PJ_LAUNCH_CHECK();
     }
     exclusive_scan_u32(bcnt.p, boff.p, nblocks, ws, s);
@@ -201,7 +212,7 @@ ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool wei
     dst.alloc((size_t)total);
     if (weighted) w.alloc((size_t)total);
     if (nblocks && total) {
-        parse_lines_k<<<(unsigned)nblocks, PB, 0, s>>>(text.p, len, weighted ? 1 : 0, boff.p, src.p, dst.p,
+        parse_lines_k<<<(unsigned)nblocks, PB, 0, s>>>(text, len, weighted ? 1 : 0, boff.p, src.p, dst.p,
                                                       weighted ? w.p : nullptr, scal.p, scal.p + 1);
         PJ_LAUNCH_CHECK();
     }
@@ -210,9 +221,11 @@ ParseResult parse_snap_device(Ctx& ctx, const char* host_text, i64 len, bool wei
     r.parse_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     r.nnz = (i64)total;
     r.max_id = (i64)h[0] - 1;
-    if (h[1] != ~0ull) {
+    if (h[1] != ~0ull) {  // error path: the line number from the text before the bad byte
+        std::vector<char> pre((size_t)h[1]);
+        if (h[1]) PJ_HIP(hipMemcpy(pre.data(), text, (size_t)h[1], hipMemcpyDeviceToHost));
         i64 line = 1;
-        for (i64 i = 0; i < (i64)h[1]; ++i) line += host_text[i] == '\n';
+        for (char c : pre) line += c == '\n';
         r.bad_line = line;
     }
     return r;

@@ -55,7 +55,7 @@ def test_kronecker_text_roundtrip(ctx, pj, oracle, tmp_path):
                        env=dict(os.environ, PJ_PHASES="1"), timeout=120)
     assert r.returncode == 0, r.stderr
     assert out.read_bytes() == oracle.format_sol(oracle.bfs(row, col, int(s[0])))
-    assert "phase load: read" in r.stderr
+    assert "phase load: file->HBM" in r.stderr
     g = ctx.load_snap(str(path))
     st = g.load_stats()
     assert st["text_bytes"] == path.stat().st_size and st["parse_ms"] > 0 and st["csr_ms"] > 0

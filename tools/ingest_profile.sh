@@ -12,6 +12,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export PJ_PHASES=1
 for t in "22 $K22 1" "wg $WG 0"; do
   set -- $t
+  mkdir -p $OUT/ing$1
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ing$1/kt -o run -- paralleljohnson_amd/bin/parallel_johnson $2 $3 /tmp/sol.txt > $OUT/ing$1/kt.log 2>&1 || { echo kt failed; tail $OUT/ing$1/kt.log; exit 1; }
   grep -E "phase|Time" $OUT/ing$1/kt.log
 done
