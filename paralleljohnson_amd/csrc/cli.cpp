@@ -348,12 +348,15 @@ int run_single(const char* webfile, int source, const char* out, int weighted) {
     std::cerr << "compute shortest paths from source node: " << source << std::endl;
     print_msg("parallel Johnson's algorithm starts......");
     std::vector<int32_t> dist((size_t)n);
-    rc = pj_sssp(g, source, dist.data());
+    rc = pj_sssp(g, source, nullptr);
     if (rc != PJ_OK) fail("pj_sssp", rc);
     pj_stats st{};
     pj_last_stats(g, &st);
     const double t_elapsed = st.kernel_ms / 1000.0;  // device time of the solve (:597-605 analogue)
     ph.mark("solve");
+    rc = pj_copy_dist(g, dist.data());  // :612-614's gather
+    if (rc != PJ_OK) fail("pj_copy_dist", rc);
+    ph.mark("d2h");
     print_msg("parallel Johnson's algorithm completes.");
     std::cout << "Time: " << t_elapsed << " seconds when using " << 1 << " processes." << std::endl;
     rc = pj_write_sol(dist.data(), n, out, 0);  // :615-618
