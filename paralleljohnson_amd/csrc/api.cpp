@@ -99,29 +99,48 @@ void ensure_stage(Ctx& c, int slots) {
     }
 }
 
-// Device -> pageable host copy through two of the ctx's pinned slots (piece k + 1
-// copies while the host moves piece k out). A plain hipMemcpy into pageable memory
-// took 38 ms for the first 16.8 MB (K22 distances) of a process.
+// Device -> pageable host copy through the ctx's pinned slots: up to 8 host threads,
+// each copying its pieces into its own two slots (piece k + 1 in flight while piece k
+// is moved out), so the PCIe copy and the host memcpy overlap. A plain hipMemcpy into
+// pageable memory took 38 ms for the first 16.8 MB (K22 distances) of a process.
 void copy_d2h_staged(Ctx& c, void* host, const void* dev, size_t bytes) {
     if (bytes < ((size_t)1 << 20)) {
         if (bytes) PJ_HIP(hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
         return;
     }
-    ensure_stage(c, 2);
-    hipStream_t s = c.stream;
     const size_t piece = (size_t)kStageSlot, np = (bytes + piece - 1) / piece;
-    auto issue = [&](size_t k) {
-        const size_t off = k * piece, len = std::min(piece, bytes - off);
-        PJ_HIP(hipMemcpyAsync(c.stage[k & 1], static_cast<const char*>(dev) + off, len, hipMemcpyDeviceToHost, s));
-        PJ_HIP(hipEventRecord(c.stage_ev[k & 1], s));
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>(np, std::min(8u, std::thread::hardware_concurrency())));
+    ensure_stage(c, 2 * nt);
+    hipStream_t s = c.stream;
+    std::vector<std::exception_ptr> errs((size_t)nt);
+    auto work = [&](int t) {
+        try {
+            bind(c);
+            auto issue = [&](size_t k, int slot) {
+                const size_t off = k * piece, len = std::min(piece, bytes - off);
+                PJ_HIP(hipMemcpyAsync(c.stage[(size_t)slot], static_cast<const char*>(dev) + off, len,
+                                      hipMemcpyDeviceToHost, s));
+                PJ_HIP(hipEventRecord(c.stage_ev[(size_t)slot], s));
+            };
+            int j = 0;
+            if ((size_t)t < np) issue((size_t)t, 2 * t);
+            for (size_t k = (size_t)t; k < np; k += (size_t)nt, ++j) {
+                if (k + (size_t)nt < np) issue(k + (size_t)nt, 2 * t + ((j + 1) & 1));
+                const int slot = 2 * t + (j & 1);
+                PJ_HIP(hipEventSynchronize(c.stage_ev[(size_t)slot]));
+                const size_t off = k * piece, len = std::min(piece, bytes - off);
+                std::memcpy(static_cast<char*>(host) + off, c.stage[(size_t)slot], len);
+            }
+        } catch (...) {
+            errs[(size_t)t] = std::current_exception();
+        }
     };
-    issue(0);
-    for (size_t k = 0; k < np; ++k) {
-        if (k + 1 < np) issue(k + 1);
-        PJ_HIP(hipEventSynchronize(c.stage_ev[k & 1]));
-        const size_t off = k * piece, len = std::min(piece, bytes - off);
-        std::memcpy(static_cast<char*>(host) + off, c.stage[k & 1], len);
-    }
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
 }
 
 i64 read_file_to_device(Ctx& c, const char* path, DevBuf<uint8_t>& text) {
@@ -149,10 +168,20 @@ i64 read_file_to_device(Ctx& c, const char* path, DevBuf<uint8_t>& text) {
         th.emplace_back([&, t] {
             try {
                 bind(c);
+                const bool warm = t == nt - 1 && npieces > 1;
+                if (warm) {
+                    // warm the device -> host copy path while the others read: the first D2H
+                    // of a process pays a one-time ~10 ms setup (the distances come back
+                    // this way after the solve)
+                    PJ_HIP(hipMemcpyAsync(c.stage[(size_t)(2 * t + 1)], text.p + size - 1, 1, hipMemcpyDeviceToHost, s));
+                    PJ_HIP(hipMemcpyAsync(c.stage[(size_t)(2 * t + 1)], text.p, std::min<int64_t>(size, (int64_t)2 << 20),
+                                          hipMemcpyDeviceToHost, s));
+                    PJ_HIP(hipEventRecord(c.stage_ev[(size_t)(2 * t + 1)], s));  // slot 2t+1 is busy until then
+                }
                 int k = 0;
                 for (int64_t piece = t; piece < npieces; piece += nt, ++k) {
                     const int slot = 2 * t + (k & 1);
-                    if (k >= 2) PJ_HIP(hipEventSynchronize(c.stage_ev[(size_t)slot]));  // its last copy is done
+                    if (k >= 2 || (k == 1 && warm)) PJ_HIP(hipEventSynchronize(c.stage_ev[(size_t)slot]));  // its last copy is done
                     const int64_t off = piece * kStageSlot, want = std::min(kStageSlot, size - off);
                     char* buf = c.stage[(size_t)slot];
                     int64_t done = 0;

@@ -1816,10 +1816,10 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
         }
     };
 
+    const bool valid = source >= 0 && source < g.n;
+    const i64 ls = valid ? relabeled_id(R, source, s) : -1;  // the source's new id (before the timed region)
     auto t_host0 = std::chrono::steady_clock::now();
     PJ_HIP(hipEventRecord(g.ev0, s));
-    const bool valid = source >= 0 && source < g.n;
-    const i64 ls = valid ? (i64)R.inv_h[(size_t)source] : -1;  // the source's new id
     if (n > 0) {
         PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(R.dist.p), INT_INF, (size_t)n, s));
         PJ_HIP(hipMemsetAsync(w.chg.p, 0, sizeof(u64) * (size_t)nwords, s));
@@ -1947,10 +1947,10 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     auto reset_minv = [&]() { PJ_HIP(hipMemsetAsync(&w.ctl.p->minv, 0xFF, sizeof(V2Line), s)); };
 
     pj_stats st{};
+    const bool valid = source >= 0 && source < g.n;
+    const i64 ls = valid ? relabeled_id(R, source, s) : -1;  // the source's new id (before the timed region)
     auto t_host0 = std::chrono::steady_clock::now();
     PJ_HIP(hipEventRecord(g.ev0, s));
-    const bool valid = source >= 0 && source < g.n;
-    const i64 ls = valid ? (i64)R.inv_h[(size_t)source] : -1;
     if (n > 0) {
         PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(R.dist.p), INT_INF, (size_t)n, s));
         PJ_HIP(hipMemsetAsync(w.f[0].p, 0, sizeof(u64) * (size_t)nwords, s));

@@ -153,7 +153,6 @@ struct DeltaWorkDeleter {
 struct Relabeled {
     i64 n_scan = 0;           // vertices with any edge: new ids [0, n_scan)
     DevBuf<u32> perm, inv;    // new -> old, old -> new
-    std::vector<u32> inv_h;   // host copy of inv (source lookup)
     DevBuf<u32> row32;
     DevBuf<u64> row64;
     DevBuf<u32> col, w;
@@ -259,6 +258,7 @@ void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t see
 
 // solvers
 void bfs_solve(Graph& g, i64 source);
+i64 relabeled_id(const Relabeled& R, i64 v, hipStream_t s);  // relabel.hip: inv[v]
 void delta_solve(Graph& g, i64 source);
 void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out);
 // Batched passes of up to 256 sources; after each pass on_pass(first source

@@ -135,14 +135,21 @@ void build(Graph& g) {
                                               n);
     PJ_LAUNCH_CHECK();
     R->dist.alloc((size_t)n);
-    R->inv_h.resize((size_t)n);
-    PJ_HIP(hipMemcpyAsync(R->inv_h.data(), R->inv.p, sizeof(u32) * (size_t)n, hipMemcpyDeviceToHost, s));
     PJ_HIP(hipStreamSynchronize(s));
     R->n_scan = h[1];
     g.rl = std::move(R);
 }
 
 }  // namespace
+
+// The relabeled id of one input vertex (4-byte read of inv; a whole host copy of
+// inv cost ~0.1 s of the first solve on a 2^26-vertex graph).
+i64 relabeled_id(const Relabeled& R, i64 v, hipStream_t s) {
+    u32 x = 0;
+    PJ_HIP(hipMemcpyAsync(&x, R.inv.p + v, sizeof(u32), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    return (i64)x;
+}
 
 void build_relabeled(Graph& g) {
     if (g.n == 0) {

@@ -60,3 +60,37 @@ def test_kronecker_text_roundtrip(ctx, pj, oracle, tmp_path):
     st = g.load_stats()
     assert st["text_bytes"] == path.stat().st_size and st["parse_ms"] > 0 and st["csr_ms"] > 0
     g.close()
+
+
+def test_file_loader_pieces(ctx, oracle, tmp_path):
+    """pj_load_snap streams the file into HBM in 8 MiB pinned pieces on several threads:
+    lines crossing piece boundaries, a last partial piece and comment lines must give the
+    same CSR as the in-memory path and the oracle parser; a directory and an empty file
+    read as an empty graph (the reference's unchecked ifstream, :67)."""
+    rng = np.random.default_rng(5)
+    m = 1_700_000  # ~21 MB of text: two full pieces and a partial one
+    src = rng.integers(0, 3_000_000, m)
+    dst = rng.integers(0, 3_000_000, m)
+    body = np.char.add(np.char.add(src.astype(str), "\t"), dst.astype(str))
+    text = ("# header\n" + "\n".join(body.tolist()) + "\n# trailer without newline").encode()
+    path = tmp_path / "big.txt"
+    path.write_bytes(text)
+    assert len(text) > 2 * (8 << 20)
+    g = ctx.load_snap(str(path))
+    row, col, _ = g.get_csr()
+    st = g.load_stats()
+    g.close()
+    h = ctx.load_snap_buffer(text)
+    hrow, hcol, _ = h.get_csr()
+    h.close()
+    assert np.array_equal(row, hrow) and np.array_equal(col, hcol)
+    s, d, _, n = oracle.parse_snap(text)
+    orow, ocol, _ = oracle.coo2csr(s, d, n)
+    assert np.array_equal(row, orow) and np.array_equal(col.view(np.uint32), ocol)
+    assert st["text_bytes"] == len(text) and st["read_ms"] > 0
+    empty = tmp_path / "empty.txt"
+    empty.write_bytes(b"")
+    for p in (tmp_path, empty, tmp_path / "missing.txt"):
+        e = ctx.load_snap(str(p))
+        assert e.n == 0 and e.nnz == 0
+        e.close()
