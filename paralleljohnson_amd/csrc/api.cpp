@@ -1052,15 +1052,31 @@ int pj_format_sol(const int32_t* dist, int64_t n, char* buf, int64_t cap, int64_
 int pj_write_sol(const int32_t* dist, int64_t n, const char* path, int strict) {
     if (!path || n < 0 || (n > 0 && !dist)) return arg_error("pj_write_sol: bad argument");
     return guarded([&] {
-        FILE* f = std::fopen(path, "wb");
-        if (!f) {
+        const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+        if (fd < 0) {
             if (strict) {
                 set_error(std::string("cannot open ") + path);
                 return (int)PJ_ERR_IO;
             }
             return (int)PJ_OK;  // the reference's ofstream fails silently (:617)
         }
-        std::fwrite(kHeader, 1, sizeof(kHeader) - 1, f);
+        // batches of chunks: formatted in parallel, then written in parallel at their
+        // offsets (pwrite), so the bytes equal the sequential writer's
+        std::atomic<bool> ok{true};
+        auto put = [&](const char* p, size_t len, int64_t off) {
+            while (len) {
+                const ssize_t r = pwrite(fd, p, len, (off_t)off);
+                if (r <= 0) {
+                    ok = false;
+                    return;
+                }
+                p += r;
+                len -= (size_t)r;
+                off += r;
+            }
+        };
+        put(kHeader, sizeof(kHeader) - 1, 0);
+        int64_t pos = (int64_t)sizeof(kHeader) - 1;
         unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         const int64_t chunk = 1 << 18;
         const int64_t nchunks = (n + chunk - 1) / chunk;
@@ -1068,6 +1084,7 @@ int pj_write_sol(const int32_t* dist, int64_t n, const char* path, int strict) {
         for (int64_t c0 = 0; c0 < nchunks; c0 += (int64_t)out.size()) {
             const int64_t cn = std::min<int64_t>((int64_t)out.size(), nchunks - c0);
             std::vector<size_t> lens((size_t)cn);
+            std::vector<int64_t> offs((size_t)cn);
             std::vector<std::thread> th;
             for (int64_t c = 0; c < cn; ++c) {
                 th.emplace_back([&, c] {
@@ -1077,9 +1094,16 @@ int pj_write_sol(const int32_t* dist, int64_t n, const char* path, int strict) {
                 });
             }
             for (auto& t : th) t.join();
-            for (int64_t c = 0; c < cn; ++c) std::fwrite(out[(size_t)c].data(), 1, lens[(size_t)c], f);
+            th.clear();
+            for (int64_t c = 0; c < cn; ++c) {
+                offs[(size_t)c] = pos;
+                pos += (int64_t)lens[(size_t)c];
+            }
+            for (int64_t c = 0; c < cn; ++c)
+                th.emplace_back([&, c] { put(out[(size_t)c].data(), lens[(size_t)c], offs[(size_t)c]); });
+            for (auto& t : th) t.join();
         }
-        const bool ok = std::fclose(f) == 0;
+        if (close(fd) != 0) ok = false;
         if (!ok && strict) {
             set_error(std::string("write failed: ") + path);
             return (int)PJ_ERR_IO;
