@@ -312,10 +312,14 @@ __device__ __forceinline__ void flush_acc(LevelCnt* c, const Acc& acc, u64* red)
 }
 
 // claim v for level L+1 through the visited bitmap (push levels)
-__device__ __forceinline__ bool claim(u64* vis, u32 v) {
+// prefilter (levels with at least n/4 edges): read the word first and skip the atomic
+// for visited targets, most of a big level's (K22 push-only 6.97 -> 2.52 ms); smaller
+// levels are latency-bound and take the atomic directly, one dependent round trip less
+// (web-Google-shaped 0.233 -> 0.217 ms, K22 0.194 -> 0.184 ms per solve)
+__device__ __forceinline__ bool claim(u64* vis, u32 v, bool prefilter) {
     u64* wp = vis + (v >> 6);
     const u64 bit = 1ull << (v & 63);
-    if (*wp & bit) return false;
+    if (prefilter && (*wp & bit)) return false;
     return !(atomicOr(wp, bit) & bit);
 }
 
@@ -620,6 +624,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
 
     if (d.mode == 0) {
         u64* vis = a.vis[d.vsel];
+        const bool prefilter = d.mq >= (u64)a.n / 4;  // block-uniform
         // ---- hub queue: 1024-edge tiles over monotonic edge offsets
         const u64 ntiles = (d.he + HUB_TILE - 1) / HUB_TILE;
         for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -643,7 +648,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
 #pragma unroll
             for (int k = 0; k < HUB_TILE / TB; ++k) {
                 if (e0 + (u64)k * TB + t < e1) {
-                    c[k] = claim(vis, vv[k]);
+                    c[k] = claim(vis, vv[k], prefilter);
                     if (c[k]) a.dist[vv[k]] = nl;
                 }
             }
@@ -670,7 +675,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                     for (u32 step = TB / 2; step > 0; step >>= 1)
                         if (s_excl[lo + step] <= e) lo += step;
                     v = g.col[s_beg[lo] + (e - s_excl[lo])];
-                    c = claim(vis, v);
+                    c = claim(vis, v, prefilter);
                     if (c) a.dist[v] = nl;
                 }
                 stage<Off, SYM>(q, a, cacc, g, L, c, v, c && !SYM ? (u64)(g.crow[v + 1] - g.crow[v]) : 0ull, acc);
