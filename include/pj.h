@@ -108,6 +108,13 @@ int pj_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, const uint3
  * valid CSR (checked on the device after loading: row[0] = 0, non-decreasing
  * offsets, row[n] = nnz, every column id < n). */
 int pj_graph_save(const pj_graph* g, const char* path, int64_t src_size, int64_t src_mtime_ns);
+/* pj_load_snap through a CSR cache file: when cache_path (may be NULL) holds a
+ * fresh cache of `path` (its size and mtime) in the same weight mode it is
+ * loaded instead of parsing; otherwise the text is parsed and, with
+ * write_back != 0, the cache is (re)written (a failed write is a warning on
+ * stderr, not an error). The CLI's PJ_CSR_CACHE. */
+int pj_load_snap_cached(pj_ctx* ctx, const char* path, int weighted, const char* cache_path, int write_back,
+                        pj_graph** out);
 int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int64_t expect_src_mtime_ns,
                      pj_graph** out);
 
@@ -467,6 +474,59 @@ typedef struct pj_delta_steps {
     int (*reach)(void* user, int64_t* out2);
 } pj_delta_steps;
 int pj_engine_delta(const pj_delta_steps* steps, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st);
+
+/* ---- n-GPU handle (SURVEY.md §8b `pj_create(int n_gpus, ...)`) ------------
+ *
+ * What `mpirun -np P parallel_johnson ...` gives a reference user, as one
+ * handle: P ranks in this process (one pj_ctx and one host thread each, rank r
+ * on GPU r mod the visible GPUs), the transport between them (pj_comm group:
+ * RCCL over xGMI when every rank has its own GPU, device copies otherwise) and
+ * the graph in one of two layouts:
+ *  - PJ_LAYOUT_PARTITIONED: the reference's 1D vertex partition (nn2rank
+ *    :169-200); every rank builds its own rows (no scatter, :344-410); a solve
+ *    runs the protocol loops of pj_part_bfs / pj_wpart_delta on all ranks
+ *    (exchange :522-554, termination allreduce :589-590) and gathers the
+ *    distances to the caller (:612-614);
+ *  - PJ_LAYOUT_REPLICATED: every rank holds the whole graph; batches of sources
+ *    are sharded over the ranks (source i on rank i mod P), no data-path
+ *    collective; a single source runs on rank 0.
+ * transport: PJ_TRANSPORT_AUTO / RCCL / HOST as pj_comm_create_group. The
+ * handle is driven from one caller thread. */
+typedef struct pj_multi pj_multi;
+enum pj_layout { PJ_LAYOUT_PARTITIONED = 0, PJ_LAYOUT_REPLICATED = 1 };
+typedef struct pj_multi_info_t {
+    int64_t n;             /* vertices of the loaded graph (0 before a load) */
+    int32_t world;         /* ranks (GPUs) */
+    int32_t layout;        /* PJ_LAYOUT_*, -1 before a load */
+    int32_t weighted;
+    const char* transport; /* "rccl", "host", "self", "replicated" or "none" */
+} pj_multi_info_t;
+
+int pj_multi_create(int n_gpus, int transport, pj_multi** out);
+int pj_multi_destroy(pj_multi* m);
+/* rank r's pj_ctx (owned by the handle) */
+int pj_multi_ctx(pj_multi* m, int rank, pj_ctx** out);
+/* The pj_load_snap grammar (weighted: third column = weight); replaces any
+ * graph loaded before. */
+int pj_multi_load_snap(pj_multi* m, const char* path, int weighted, int layout);
+/* CSR cache for later replicated loads (pj_load_snap_cached; rank 0 writes it);
+ * NULL or "" turns it off. Partitioned loads always parse. */
+int pj_multi_set_csr_cache(pj_multi* m, const char* cache_path);
+/* pj_generate_kronecker on every rank (partitioned + weighted: the whole graph
+ * is resident on each GPU while its block is cut, as pj_wpart_from_graph). */
+int pj_multi_generate_kronecker(pj_multi* m, int scale, int edgefactor, uint64_t seed, int weighted, int layout);
+int pj_multi_info(const pj_multi* m, pj_multi_info_t* out);
+/* One source: dist_out (n int32, host) may be NULL. st (may be NULL): rank 0's
+ * counts with solve_ms = the max over ranks (the reference's Time:, :597-605). */
+int pj_multi_sssp(pj_multi* m, int64_t source, int32_t* dist_out, pj_part_stats* st);
+/* n_src sources -> dist_out[n_src][n] (may be NULL). */
+int pj_multi_sssp_batch(pj_multi* m, const int64_t* sources, int n_src, int32_t* dist_out);
+/* n_src sources, one sol_file each (paths[i] for sources[i]), each byte-identical
+ * to a single-source run (pj_write_sol semantics, strict as there).
+ * *solve_ms (may be NULL): device solve time, max over ranks (replicated) or
+ * summed over the sources (partitioned). */
+int pj_multi_sssp_batch_write(pj_multi* m, const int64_t* sources, int n_src, const char* const* paths, int strict,
+                              double* solve_ms);
 
 /* ---- output (replaces output_vector :32-46 + the write at :615-620) ------ */
 

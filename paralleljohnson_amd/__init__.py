@@ -92,6 +92,7 @@ _SIGS = {
     "pj_kronecker_write_snap": ([_P, _INT, _INT, ctypes.c_uint64, _INT, ctypes.c_char_p], _INT),
     "pj_graph_save": ([_P, ctypes.c_char_p, _I64, _I64], _INT),
     "pj_load_csr_file": ([_P, ctypes.c_char_p, _I64, _I64, _PP], _INT),
+    "pj_load_snap_cached": ([_P, ctypes.c_char_p, _INT, ctypes.c_char_p, _INT, _PP], _INT),
     "pj_graph_destroy": ([_P], _INT),
     "pj_graph_load_stats": ([_P, _P], _INT),
     "pj_graph_info": ([_P, _P, _P, _P, _P], _INT),
@@ -154,6 +155,17 @@ _SIGS = {
     "pj_wpart_gather_dist": ([_P, _P, _P], _INT),
     "pj_engine_bfs": ([_P, _P, _I64, ctypes.c_double, ctypes.c_double, _INT, _P], _INT),
     "pj_engine_delta": ([_P, _P, _I64, ctypes.c_int32, _P], _INT),
+    # the n-GPU handle (partition.Multi wraps it)
+    "pj_multi_create": ([_INT, _INT, _PP], _INT),
+    "pj_multi_destroy": ([_P], _INT),
+    "pj_multi_ctx": ([_P, _INT, _PP], _INT),
+    "pj_multi_set_csr_cache": ([_P, ctypes.c_char_p], _INT),
+    "pj_multi_load_snap": ([_P, ctypes.c_char_p, _INT, _INT], _INT),
+    "pj_multi_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _INT], _INT),
+    "pj_multi_info": ([_P, _P], _INT),
+    "pj_multi_sssp": ([_P, _I64, _P, _P], _INT),
+    "pj_multi_sssp_batch": ([_P, _P, _INT, _P], _INT),
+    "pj_multi_sssp_batch_write": ([_P, _P, _INT, _P, _INT, _P], _INT),
 }
 for _name, (_args, _res) in _SIGS.items():
     _fn = getattr(_lib, _name)
@@ -344,6 +356,15 @@ class Context:
         g = ctypes.c_void_p()
         _check(_lib.pj_load_coo(self._h, _ptr(s), _ptr(d), _ptr(wa), len(s), int(n), ctypes.byref(g)))
         return Graph(self, g)
+
+    def load_snap_cached(self, path: str, cache_path: Optional[str], weighted: bool = False,
+                         write_back: bool = True) -> Graph:
+        """pj_load_snap through the CSR cache file cache_path (pj_load_snap_cached)."""
+        h = ctypes.c_void_p()
+        _check(_lib.pj_load_snap_cached(self._h, os.fsencode(path), int(weighted),
+                                        None if cache_path is None else os.fsencode(cache_path), int(write_back),
+                                        ctypes.byref(h)))
+        return Graph(self, h)
 
     def load_csr_file(self, path: str, expect_src_size: int = -1, expect_src_mtime_ns: int = -1) -> "Graph":
         """A graph saved by Graph.save (pj_load_csr_file): no parse, no sort."""

@@ -1028,6 +1028,25 @@ int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int
     });
 }
 
+int pj_load_snap_cached(pj_ctx* ctx, const char* path, int weighted, const char* cache_path, int write_back,
+                        pj_graph** out) {
+    if (!ctx || !path || !out) return arg_error("pj_load_snap_cached: bad argument");
+    *out = nullptr;
+    struct stat sb {};
+    if (!cache_path || !*cache_path || stat(path, &sb) != 0) return pj_load_snap(ctx, path, weighted, out);
+    const int64_t size = (int64_t)sb.st_size;
+    const int64_t mtime = (int64_t)sb.st_mtim.tv_sec * 1000000000ll + (int64_t)sb.st_mtim.tv_nsec;
+    if (pj_load_csr_file(ctx, cache_path, size, mtime, out) == PJ_OK) {
+        if ((*out)->g.weighted == (weighted != 0)) return PJ_OK;
+        pj_graph_destroy(*out);  // cached in the other weight mode: parse, and replace it
+        *out = nullptr;
+    }
+    const int rc = pj_load_snap(ctx, path, weighted, out);
+    if (rc == PJ_OK && write_back && pj_graph_save(*out, cache_path, size, mtime) != PJ_OK)
+        fprintf(stderr, "warning: could not write the CSR cache %s: %s\n", cache_path, pj_last_error());
+    return rc;
+}
+
 // ---------------------------------------------------------------- output --
 // output_vector (:32-46): header line, then one decimal or "inf" per vertex.
 // Formatting is split over host threads into per-chunk buffers and written

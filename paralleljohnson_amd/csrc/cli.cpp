@@ -10,8 +10,9 @@
 //
 // Processes: P = PJ_GPUS, else the launcher's world size (OMPI_COMM_WORLD_SIZE,
 // PMI_SIZE, PMIX_SIZE), else 1. Under a launcher only rank 0 works (the other
-// ranks exit 0): it runs the P ranks of the 1D vertex partition itself, one
-// host thread and one pj_ctx each, rank r on GPU r mod (visible GPUs), over
+// ranks exit 0): it runs the P ranks of the 1D vertex partition itself through
+// the n-GPU handle pj_multi (one host thread and one pj_ctx per rank, rank r on
+// GPU r mod (visible GPUs)), over
 // RCCL when every rank has its own GPU and over device copies otherwise
 // (PJ_TRANSPORT=rccl|host overrides). P = 1 runs the single-GPU solver. The
 // `Time:` line reports P, as the reference does (:603-604).
@@ -30,8 +31,6 @@
 // file is byte-identical to a single-source run. With P > 1 the sources are
 // sharded over P GPUs (source i on GPU i mod P), each holding a copy of the
 // graph.
-#include <sys/stat.h>
-
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -68,12 +67,6 @@ int process_count() {
     return std::max(1, launcher_value({"OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "PMIX_SIZE"}, 1));
 }
 
-int device_count() {
-    int n = 0;
-    pj_device_count(&n);
-    return n;
-}
-
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -88,26 +81,11 @@ struct Phases {
     }
 };
 
-// The graph of `path`: from the binary CSR cache when PJ_CSR_CACHE names a fresh one,
-// else parsed (pj_load_snap) and, with PJ_CSR_CACHE set, cached for the next run.
-int load_graph(pj_ctx* ctx, const char* path, int weighted, pj_graph** g) {
-    const char* cache = std::getenv("PJ_CSR_CACHE");
-    struct stat sb {};
-    if (!cache || !*cache || stat(path, &sb) != 0) return pj_load_snap(ctx, path, weighted, g);
-    const std::string cpath = std::string(cache) == "1" ? std::string(path) + ".pjcsr" : std::string(cache);
-    const int64_t size = (int64_t)sb.st_size;
-    const int64_t mtime = (int64_t)sb.st_mtim.tv_sec * 1000000000ll + (int64_t)sb.st_mtim.tv_nsec;
-    if (pj_load_csr_file(ctx, cpath.c_str(), size, mtime, g) == PJ_OK) {
-        int w = 0;
-        pj_graph_info(*g, nullptr, nullptr, &w, nullptr);
-        if (w == (weighted != 0)) return PJ_OK;
-        pj_graph_destroy(*g);
-        *g = nullptr;
-    }
-    const int rc = pj_load_snap(ctx, path, weighted, g);
-    if (rc == PJ_OK && pj_graph_save(*g, cpath.c_str(), size, mtime) != PJ_OK)
-        std::cerr << "warning: could not write the CSR cache " << cpath << ": " << pj_last_error() << std::endl;
-    return rc;
+// PJ_CSR_CACHE: "1" -> <webfile>.pjcsr, else the path given; unset -> no cache
+std::string cache_path(const char* webfile) {
+    const char* c = std::getenv("PJ_CSR_CACHE");
+    if (!c || !*c) return "";
+    return std::string(c) == "1" ? std::string(webfile) + ".pjcsr" : std::string(c);
 }
 
 // print_msg :49-53 (rank 0 only; only rank 0 gets this far)
@@ -118,26 +96,6 @@ void print_msg(const std::string& msg) { std::cerr << msg << std::endl; }
     std::exit(-1);
 }
 [[noreturn]] void fail(const char* what, int rc) { fail(what, rc, pj_last_error()); }
-
-// fn(r) on one thread per rank; exits on the first failure (the root cause, not a peer's)
-template <typename F>
-void per_rank(int P, const char* what, F&& fn) {
-    std::vector<int> rcs((size_t)P, PJ_OK);
-    std::vector<std::string> msgs((size_t)P);
-    std::vector<std::thread> th;
-    for (int r = 0; r < P; ++r)
-        th.emplace_back([&, r] {
-            rcs[(size_t)r] = fn(r);
-            if (rcs[(size_t)r] != PJ_OK) msgs[(size_t)r] = pj_last_error();
-        });
-    for (auto& t : th) t.join();
-    for (int r = 0; r < P; ++r)
-        if (rcs[(size_t)r] != PJ_OK && rcs[(size_t)r] != PJ_ERR_COMM)
-            fail(std::string(what) + " (rank " + std::to_string(r) + ")", rcs[(size_t)r], msgs[(size_t)r]);
-    for (int r = 0; r < P; ++r)
-        if (rcs[(size_t)r] != PJ_OK)
-            fail(std::string(what) + " (rank " + std::to_string(r) + ")", rcs[(size_t)r], msgs[(size_t)r]);
-}
 
 // PJ_SOURCES: "a,b c" or "@file" (one per line); every token read with atoi (:448)
 std::vector<int64_t> parse_sources(const char* spec) {
@@ -186,58 +144,6 @@ std::string sol_path(const std::string& pat, int64_t src, size_t idx) {
     return out;
 }
 
-std::vector<pj_ctx*> make_ctxs(int P) {
-    const int ndev = std::max(1, device_count());
-    std::vector<pj_ctx*> ctxs((size_t)P, nullptr);
-    for (int r = 0; r < P; ++r) {
-        const int rc = pj_create(r % ndev, &ctxs[(size_t)r]);
-        if (rc != PJ_OK) fail("pj_create", rc);
-    }
-    return ctxs;
-}
-
-// Source-sharded multi-source run: GPU r solves sources r, r+P, ... and writes their files.
-int run_multi_source(const char* webfile, const std::vector<int64_t>& sources, const char* pattern, int P,
-                     int weighted) {
-    Phases ph;
-    std::vector<pj_ctx*> ctxs = make_ctxs(P);
-    std::vector<pj_graph*> gs((size_t)P, nullptr);
-    per_rank(P, "pj_load_snap", [&](int r) { return load_graph(ctxs[(size_t)r], webfile, weighted, &gs[(size_t)r]); });
-    int64_t n = 0;
-    pj_graph_info(gs[0], &n, nullptr, nullptr, nullptr);
-    std::cerr << "N = " << n << std::endl;
-    print_msg("read in the webgraph is done.");
-    ph.mark("load");
-    std::cerr << "compute shortest paths from " << sources.size() << " source nodes" << std::endl;
-    print_msg("parallel Johnson's algorithm starts......");
-    std::vector<double> kms((size_t)P, 0.0);
-    per_rank(P, "pj_sssp_batch_write", [&](int r) {
-        std::vector<int64_t> mine;
-        std::vector<std::string> paths;
-        for (size_t i = (size_t)r; i < sources.size(); i += (size_t)P) {
-            mine.push_back(sources[i]);
-            paths.push_back(sol_path(pattern, sources[i], i));
-        }
-        if (mine.empty()) return (int)PJ_OK;
-        std::vector<const char*> pp;
-        for (auto& q : paths) pp.push_back(q.c_str());
-        int rc = pj_sssp_batch_write(gs[(size_t)r], mine.data(), (int)mine.size(), pp.data(), 0);
-        pj_stats st{};
-        if (rc == PJ_OK && pj_last_stats(gs[(size_t)r], &st) == PJ_OK) kms[(size_t)r] = st.kernel_ms;
-        return rc;
-    });
-    ph.mark("solve+write");
-    print_msg("parallel Johnson's algorithm completes.");
-    const double t = *std::max_element(kms.begin(), kms.end()) / 1000.0;
-    std::cout << "Time: " << t << " seconds when using " << P << " processes." << std::endl;
-    std::cerr << "the shortest path distance vectors have been saved in files " << pattern << std::endl;
-    for (int r = 0; r < P; ++r) {
-        pj_graph_destroy(gs[(size_t)r]);
-        pj_destroy(ctxs[(size_t)r]);
-    }
-    return 0;
-}
-
 int transport_from_env() {
     const char* t = std::getenv("PJ_TRANSPORT");
     if (!t || !*t || !std::strcmp(t, "auto")) return PJ_TRANSPORT_AUTO;
@@ -247,61 +153,73 @@ int transport_from_env() {
     std::exit(-1);
 }
 
+// P ranks in this process through the n-GPU handle of the C-ABI (pj_multi)
+pj_multi* make_multi(int P) {
+    pj_multi* m = nullptr;
+    const int rc = pj_multi_create(P, transport_from_env(), &m);
+    if (rc != PJ_OK) fail("pj_multi_create", rc);
+    return m;
+}
+
+// Source-sharded multi-source run: GPU r solves sources r, r+P, ... and writes their files.
+int run_multi_source(const char* webfile, const std::vector<int64_t>& sources, const char* pattern, int P,
+                     int weighted) {
+    Phases ph;
+    pj_multi* m = make_multi(P);
+    const std::string cache = cache_path(webfile);
+    pj_multi_set_csr_cache(m, cache.c_str());
+    int rc = pj_multi_load_snap(m, webfile, weighted, PJ_LAYOUT_REPLICATED);
+    if (rc != PJ_OK) fail("pj_load_snap", rc);
+    pj_multi_info_t mi{};
+    pj_multi_info(m, &mi);
+    std::cerr << "N = " << mi.n << std::endl;
+    print_msg("read in the webgraph is done.");
+    ph.mark("load");
+    std::cerr << "compute shortest paths from " << sources.size() << " source nodes" << std::endl;
+    print_msg("parallel Johnson's algorithm starts......");
+    std::vector<std::string> paths;
+    std::vector<const char*> pp;
+    for (size_t i = 0; i < sources.size(); ++i) paths.push_back(sol_path(pattern, sources[i], i));
+    for (auto& q : paths) pp.push_back(q.c_str());
+    double kms = 0;
+    rc = pj_multi_sssp_batch_write(m, sources.data(), (int)sources.size(), pp.data(), 0, &kms);
+    if (rc != PJ_OK) fail("pj_sssp_batch_write", rc);
+    ph.mark("solve+write");
+    print_msg("parallel Johnson's algorithm completes.");
+    std::cout << "Time: " << kms / 1000.0 << " seconds when using " << P << " processes." << std::endl;
+    std::cerr << "the shortest path distance vectors have been saved in files " << pattern << std::endl;
+    pj_multi_destroy(m);
+    return 0;
+}
+
 // The 1D vertex partition over P ranks in this process (the reference's np = P run).
 int run_partitioned(const char* webfile, int source, const char* out, int P, int weighted) {
     Phases ph;
-    std::vector<pj_ctx*> ctxs = make_ctxs(P);
-    std::vector<pj_comm*> comms((size_t)P, nullptr);
-    int rc = pj_comm_create_group(ctxs.data(), P, transport_from_env(), comms.data());
-    if (rc != PJ_OK) fail("pj_comm_create_group", rc);
-    std::vector<pj_part*> parts((size_t)P, nullptr);
-    std::vector<pj_wpart*> wparts((size_t)P, nullptr);
+    pj_multi* m = make_multi(P);
     // every rank builds its own rows on its GPU: no scatter (:344-410)
-    per_rank(P, "load", [&](int r) {
-        return weighted ? pj_wpart_load_snap(ctxs[(size_t)r], webfile, r, P, &wparts[(size_t)r])
-                        : pj_part_load_snap(ctxs[(size_t)r], webfile, r, P, &parts[(size_t)r]);
-    });
-    int64_t n = 0;
-    if (weighted) {
-        int64_t info[8];
-        pj_wpart_info(wparts[0], info);
-        n = info[0];
-    } else {
-        pj_part_info pi{};
-        pj_part_info_get(parts[0], &pi);
-        n = pi.n;
-    }
+    int rc = pj_multi_load_snap(m, webfile, weighted, PJ_LAYOUT_PARTITIONED);
+    if (rc != PJ_OK) fail("load", rc);
+    pj_multi_info_t mi{};
+    pj_multi_info(m, &mi);
+    const int64_t n = mi.n;
     std::cerr << "N = " << n << std::endl;  // :320
     print_msg("read in the webgraph is done.");
     print_msg("distribute sparse matrix is done.");
     ph.mark("load");
     std::cerr << "compute shortest paths from source node: " << source << std::endl;
     print_msg("parallel Johnson's algorithm starts......");
-    std::vector<pj_part_stats> st((size_t)P);
-    rc = weighted ? pj_wpart_delta_group(P, wparts.data(), comms.data(), source, 0, st.data())
-                  : pj_part_bfs_group(P, parts.data(), comms.data(), source, st.data());
-    if (rc != PJ_OK) fail(weighted ? "pj_wpart_delta_group" : "pj_part_bfs_group", rc);
-    double t = 0;
-    for (auto& s : st) t = std::max(t, s.solve_ms / 1000.0);  // max over ranks (:597-605)
-    ph.mark("solve");
     std::vector<int32_t> dist((size_t)n);
-    per_rank(P, "gather", [&](int r) {  // MPI_Gatherv :612-614
-        int32_t* o = r == 0 ? dist.data() : nullptr;
-        return weighted ? pj_wpart_gather_dist(wparts[(size_t)r], comms[(size_t)r], o)
-                        : pj_part_gather_dist(parts[(size_t)r], comms[(size_t)r], o);
-    });
+    pj_part_stats st{};
+    rc = pj_multi_sssp(m, source, dist.data(), &st);  // solve + MPI_Gatherv :612-614
+    if (rc != PJ_OK) fail(weighted ? "pj_wpart_delta_group" : "pj_part_bfs_group", rc);
+    ph.mark("solve+gather");
     print_msg("parallel Johnson's algorithm completes.");
-    std::cout << "Time: " << t << " seconds when using " << P << " processes." << std::endl;
+    std::cout << "Time: " << st.solve_ms / 1000.0 << " seconds when using " << P << " processes." << std::endl;
     rc = pj_write_sol(dist.data(), n, out, 0);  // :615-618
     if (rc != PJ_OK) fail("pj_write_sol", rc);
-    ph.mark("gather+write");
+    ph.mark("write");
     std::cerr << "the shortest path distance vector has been saved in file " << out << std::endl;
-    for (int r = 0; r < P; ++r) {
-        pj_part_destroy(parts[(size_t)r]);
-        pj_wpart_destroy(wparts[(size_t)r]);
-        pj_comm_destroy(comms[(size_t)r]);
-        pj_destroy(ctxs[(size_t)r]);
-    }
+    pj_multi_destroy(m);
     return 0;
 }
 
@@ -332,7 +250,8 @@ int run_single(const char* webfile, int source, const char* out, int weighted) {
     if (rc != PJ_OK) fail("pj_create", rc);
     ph.mark("init");
     pj_graph* g = nullptr;
-    rc = load_graph(ctx, webfile, weighted, &g);
+    const std::string cache = cache_path(webfile);
+    rc = pj_load_snap_cached(ctx, webfile, weighted, cache.empty() ? nullptr : cache.c_str(), 1, &g);
     if (rc != PJ_OK) fail("pj_load_snap", rc);
     int64_t n = 0;
     pj_graph_info(g, &n, nullptr, nullptr, nullptr);

@@ -462,3 +462,77 @@ def gather_group(parts: Sequence, comms: Sequence[Comm]) -> np.ndarray:
     if errs:
         raise errs[0]
     return out[0]
+
+
+class MultiInfo(ctypes.Structure):
+    _fields_ = [("n", _I64), ("world", _I32), ("layout", _I32), ("weighted", _I32), ("transport", ctypes.c_char_p)]
+
+
+PARTITIONED, REPLICATED = 0, 1
+TRANSPORTS = {"auto": 0, "rccl": 1, "host": 2}
+
+
+class Multi:
+    """The n-GPU handle (pj_multi_*, SURVEY.md §8b `pj_create(int n_gpus, ...)`):
+    P ranks in this process, one pj_ctx and host thread each, the transport
+    between them, and the graph partitioned (the reference's np = P run) or
+    replicated (sources sharded over the ranks)."""
+
+    def __init__(self, n_gpus: int, transport: str = "auto"):
+        h = ctypes.c_void_p()
+        _check(_lib.pj_multi_create(int(n_gpus), TRANSPORTS[transport], ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if self._h:
+            _check(_lib.pj_multi_destroy(self._h))
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def info(self) -> dict:
+        i = MultiInfo()
+        _check(_lib.pj_multi_info(self._h, ctypes.byref(i)))
+        return {"n": i.n, "world": i.world, "layout": i.layout, "weighted": bool(i.weighted),
+                "transport": (i.transport or b"").decode()}
+
+    def set_csr_cache(self, path: Optional[str]):
+        _check(_lib.pj_multi_set_csr_cache(self._h, None if path is None else os.fsencode(path)))
+
+    def load_snap(self, path: str, weighted: bool = False, layout: int = PARTITIONED):
+        _check(_lib.pj_multi_load_snap(self._h, os.fsencode(path), int(weighted), int(layout)))
+
+    def generate_kronecker(self, scale: int, edgefactor: int = 16, seed: int = 1, weighted: bool = False,
+                           layout: int = PARTITIONED):
+        _check(_lib.pj_multi_generate_kronecker(self._h, int(scale), int(edgefactor), ctypes.c_uint64(seed),
+                                                int(weighted), int(layout)))
+
+    def sssp(self, source: int):
+        """(distances, stats) of one solve from `source`."""
+        n = self.info()["n"]
+        out = np.empty(max(n, 1), np.int32)
+        st = PartStats()
+        _check(_lib.pj_multi_sssp(self._h, int(source), _ptr(out), ctypes.byref(st)))
+        return out[:n], st.as_dict()
+
+    def sssp_batch(self, sources: Sequence[int]) -> np.ndarray:
+        n = self.info()["n"]
+        src = np.ascontiguousarray(np.asarray(sources, dtype=np.int64))
+        out = np.empty((len(src), max(n, 1)), np.int32)
+        _check(_lib.pj_multi_sssp_batch(self._h, _ptr(src), len(src), _ptr(out)))
+        return out[:, :n]
+
+    def sssp_batch_write(self, sources: Sequence[int], paths: Sequence[str], strict: bool = True) -> float:
+        """One sol_file per source; returns the device solve time (ms)."""
+        src = np.ascontiguousarray(np.asarray(sources, dtype=np.int64))
+        if len(paths) != len(src):
+            raise ValueError("one path per source")
+        arr = (ctypes.c_char_p * max(len(paths), 1))(*[os.fsencode(p) for p in paths])
+        ms = ctypes.c_double()
+        _check(_lib.pj_multi_sssp_batch_write(self._h, _ptr(src), len(src), ctypes.cast(arr, ctypes.c_void_p),
+                                              int(strict), ctypes.byref(ms)))
+        return ms.value

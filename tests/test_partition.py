@@ -425,3 +425,69 @@ def test_wpart_load_snap(pj, oracle, tmp_path, world):
         assert np.array_equal(gather_group(parts, comms), exp), source
     for p in parts:
         p.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_multi_handle(pj, oracle, tmp_path, world):
+    """The n-GPU handle (pj_multi_*, SURVEY.md §8b `pj_create(n_gpus)`), ranks sharing the one
+    GPU over the host transport: partitioned single-source solves (unit and weighted) equal the
+    oracle; replicated batches (sources sharded over the ranks) equal per-source oracle rows;
+    batch_write files are byte-identical to the oracle's sol_files in both layouts; a CSR cache
+    written by rank 0 serves the next replicated load."""
+    from paralleljohnson_amd.partition import PARTITIONED, REPLICATED, Multi
+    rng = np.random.default_rng(90 + world)
+    s, d = random_graph(rng, "hub", 2500)
+    w = rng.integers(1, 150, len(s)).astype(np.uint32)
+    for weighted in (False, True):
+        text = to_text(s, d, w=w if weighted else None, style=1)
+        path = tmp_path / f"g{int(weighted)}.txt"
+        path.write_bytes(text)
+        ps, pd, pw, n = oracle.parse_snap(text, weighted=weighted)
+        row, col, wc = oracle.coo2csr(ps, pd, n, pw)
+
+        def ref(src):
+            if src < 0 or src >= n:
+                return np.full(n, INF, np.int32)
+            return oracle.dijkstra(row, col, wc, src) if weighted else oracle.bfs(row, col, src)
+
+        sources = [int(ps[0]), 0, n - 1, n + 5, int(ps[len(ps) // 2])]
+        with Multi(world, "host" if world > 1 else "auto") as m:
+            assert m.info()["layout"] == -1
+            with pytest.raises(pj.PJError):
+                m.sssp(0)
+            m.load_snap(str(path), weighted=weighted, layout=PARTITIONED)
+            info = m.info()
+            assert (info["n"], info["world"], info["layout"], info["weighted"]) == (n, world, PARTITIONED, weighted)
+            for src in sources:
+                dist, st = m.sssp(src)
+                exp = ref(src)
+                assert np.array_equal(dist, exp), (weighted, src)
+                assert st["reached"] == int((exp < INF).sum())
+            paths = [str(tmp_path / f"p{world}_{weighted}_{i}.txt") for i in range(len(sources))]
+            m.sssp_batch_write(sources, paths)
+            for src, p in zip(sources, paths):
+                assert open(p, "rb").read() == oracle.format_sol(ref(src)), (src, p)
+
+            cache = str(tmp_path / f"c{world}_{int(weighted)}.pjcsr")
+            m.set_csr_cache(cache)
+            m.load_snap(str(path), weighted=weighted, layout=REPLICATED)
+            assert m.info()["transport"] == "replicated" and os.path.exists(cache)
+            rows = m.sssp_batch(sources)
+            for i, src in enumerate(sources):
+                assert np.array_equal(rows[i], ref(src)), (weighted, src)
+            m.load_snap(str(path), weighted=weighted, layout=REPLICATED)  # from the cache now
+            paths = [str(tmp_path / f"r{world}_{weighted}_{i}.txt") for i in range(len(sources))]
+            m.sssp_batch_write(sources, paths)
+            for src, p in zip(sources, paths):
+                assert open(p, "rb").read() == oracle.format_sol(ref(src)), (src, p)
+            dist, _ = m.sssp(sources[0])
+            assert np.array_equal(dist, ref(sources[0]))
+    # Kronecker through the handle: partitioned (unit) equals the single-GPU solver
+    with Multi(world, "host" if world > 1 else "auto") as m:
+        m.generate_kronecker(11, 16, 5, layout=PARTITIONED)
+        with pj.Context(0) as c:
+            g = c.generate_kronecker(11, 16, 5)
+            for root in g.sample_roots(3, 2):
+                assert np.array_equal(m.sssp(int(root))[0], g.sssp(int(root)))
+            g.close()
