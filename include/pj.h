@@ -99,7 +99,7 @@ int pj_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, const uint3
  * reference re-parses the text on every run, read_webgraph :66-105 +
  * coord2csr :117-159). The file holds the graph's device arrays as they sit in
  * HBM -- a 64-byte header, row offsets (4 or 8 bytes), col, weights when
- * weighted, and the in-edge CSC when the graph is not symmetric -- so loading
+ * weighted, and the in-edge CSC when the graph is unit-weight and not symmetric -- so loading
  * it is file -> pinned staging -> HBM with no sort. src_size / src_mtime_ns
  * stamp the text the graph came from (-1: none); pj_load_csr_file with an
  * expected stamp other than -1 fails with PJ_ERR_STATE when the file's stamp

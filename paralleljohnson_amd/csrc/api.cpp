@@ -912,7 +912,7 @@ uint64_t csr_payload(int64_t n, int64_t nnz, uint32_t flags) {
     const uint64_t ob = (flags & 4) ? 8 : 4;
     uint64_t b = ob * (uint64_t)(n + 1) + 4ull * (uint64_t)nnz;
     if (flags & 1) b += 4ull * (uint64_t)nnz;
-    if (!(flags & 2)) b += ob * (uint64_t)(n + 1) + 4ull * (uint64_t)nnz;
+    if (flags & 8) b += ob * (uint64_t)(n + 1) + 4ull * (uint64_t)nnz;  // the in-edge CSC
     return b;
 }
 
@@ -927,7 +927,9 @@ int pj_graph_save(const pj_graph* pg, const char* path, int64_t src_size, int64_
         CsrFileHeader h{};
         std::memcpy(h.magic, kCsrMagic, 8);
         h.version = 1;
-        h.flags = (g.weighted ? 1u : 0u) | (g.symmetric ? 2u : 0u) | (g.off64 ? 4u : 0u);
+        // flag 8: the CSC follows (unit-weight non-symmetric graphs; weighted graphs have none)
+        const bool csc = !g.symmetric && !g.weighted;
+        h.flags = (g.weighted ? 1u : 0u) | (g.symmetric ? 2u : 0u) | (g.off64 ? 4u : 0u) | (csc ? 8u : 0u);
         h.n = g.n;
         h.nnz = g.nnz;
         h.src_size = src_size;
@@ -947,7 +949,7 @@ int pj_graph_save(const pj_graph* pg, const char* path, int64_t src_size, int64_
         put_dev(f.get(), g.row_ptr(), ob * (size_t)(g.n + 1), st, s);
         put_dev(f.get(), g.col.p, 4 * (size_t)g.nnz, st, s);
         if (g.weighted) put_dev(f.get(), g.w.p, 4 * (size_t)g.nnz, st, s);
-        if (!g.symmetric) {
+        if (csc) {
             put_dev(f.get(), g.crow_ptr(), ob * (size_t)(g.n + 1), st, s);
             put_dev(f.get(), g.ccol.p, 4 * (size_t)g.nnz, st, s);
         }
@@ -974,7 +976,7 @@ int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int
         CsrFileHeader h{};
         struct stat sb {};
         if (std::fread(&h, sizeof h, 1, f.get()) != 1 || std::memcmp(h.magic, kCsrMagic, 8) != 0 ||
-            h.version != 1 || (h.flags & ~7u) != 0 || h.n < 0 || h.n > 0xFFFFFFFFll || h.nnz < 0 ||
+            h.version != 1 || (h.flags & ~15u) != 0 || ((h.flags & 8) != 0) != ((h.flags & 3) == 0) || h.n < 0 || h.n > 0xFFFFFFFFll || h.nnz < 0 ||
             ((h.flags & 4) == 0 && (uint64_t)h.nnz > 0xFFFFFFFFull) ||
             h.payload != csr_payload(h.n, h.nnz, h.flags) || fstat(fileno(f.get()), &sb) != 0 ||
             (uint64_t)sb.st_size != sizeof h + h.payload) {
@@ -1011,7 +1013,7 @@ int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int
             g.w.alloc((size_t)g.nnz);
             get_dev(f.get(), g.w.p, 4 * (size_t)g.nnz, st, s);
         }
-        if (!g.symmetric) {
+        if (h.flags & 8) {
             if (g.off64) {
                 g.crow64.alloc(nr);
                 get_dev(f.get(), g.crow64.p, 8 * nr, st, s);
@@ -1023,7 +1025,7 @@ int pj_load_csr_file(pj_ctx* ctx, const char* path, int64_t expect_src_size, int
             get_dev(f.get(), g.ccol.p, 4 * (size_t)g.nnz, st, s);
         }
         check_csr_device(g.row_ptr(), g.off64, g.col.p, g.n, g.nnz, s);
-        if (!g.symmetric) check_csr_device(g.crow_ptr(), g.off64, g.ccol.p, g.n, g.nnz, s);
+        if (h.flags & 8) check_csr_device(g.crow_ptr(), g.off64, g.ccol.p, g.n, g.nnz, s);
         return finish_graph(ctx, pg, out);
     });
 }
