@@ -857,6 +857,7 @@ struct V2Args {
     const u64* cw;    // edges interleaved: col | w << 32 (the relabeled CSR)
     const u64* lrow;  // light CSR: the light prefixes of the rows, packed
     const u64* lcw;
+    const u64* hl;    // bit v: v has a light edge (lsplit[v] > 0) for this delta; null in the tail
     int ltail;        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
     const u64* sbits; // tail mode: settled-before-the-tail bitmap; relaxations skip its targets
     u64* swrite;      // the heavy step entering the tail writes that bitmap (pull / select)
@@ -1043,6 +1044,32 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
             }
         }
         if (!__ballot(mytodo != 0)) continue;
+        if (LIGHT && a.hl) {
+            // frontier vertices without light edges have nothing to relax: only a new
+            // member's heavy-edge count (its whole row) is accounted
+            const u64 hw = mytodo ? a.hl[wbase + lane] : 0ull;
+            const u64 nl = mynew & ~hw;
+            mytodo &= hw;
+            const u32 c2 = (u32)__popcll(nl);
+            const u32 i2 = wave_incl_scan(c2);
+            const u32 x2 = i2 - c2;
+            const u32 T2 = __shfl(i2, 63, 64);
+            for (u32 r0 = 0; r0 < T2; r0 += WAVE) {
+                const u32 c = r0 + lane;
+                u32 jw = 0;
+#pragma unroll
+                for (u32 step = V2_SC / 2; step > 0; step >>= 1) {
+                    const u32 x = __shfl(x2, jw + step, 64);
+                    if (x <= c) jw += step;
+                }
+                const u32 ex = __shfl(x2, jw, 64);
+                const u64 tw = __shfl(nl, jw, 64);
+                if (c < T2) {
+                    const u32 v = (u32)((wbase + jw) * 64 + select_bit(tw, c - ex));
+                    mh += (u64)row[v + 1] - (u64)row[v];
+                }
+            }
+        }
         const u32 cnt = (u32)__popcll(mytodo);
         const u32 incl = wave_incl_scan(cnt);
         const u32 myex = incl - cnt;
@@ -1381,6 +1408,8 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             const u64 m = __ballot(v < a.n && d > lo);
             if (lane == k) mytodo = m;
         }
+        // a vertex without light edges has no light in-edge (symmetric graph): not a candidate
+        if (a.hl && mytodo) mytodo &= a.hl[gbase + lane];
         if (lane < 2 * PSC) newb[lane] = 0;
         const u32 cnt = (u32)__popcll(mytodo);
         const u32 incl = wave_incl_scan(cnt);
@@ -1622,6 +1651,17 @@ __global__ void v2_source_k(V2Args a, i64 s, u64* __restrict__ f, int cin) {
     a.ctl->cnt[cin][0].v = 1;
 }
 
+// hl bit v = (lsplit[v] > 0): the vertices that have light edges for this delta
+__global__ void v2_haslight_k(const u32* __restrict__ lsplit, i64 n, u64* __restrict__ hl) {
+    const i64 nw = (n + 63) / 64;
+    for (i64 wi = ((i64)blockIdx.x * blockDim.x + threadIdx.x) / WAVE; wi < nw;
+         wi += (i64)gridDim.x * blockDim.x / WAVE) {
+        const i64 v = wi * 64 + lane_id();
+        const u64 m = __ballot(v < n && lsplit[v] > 0);
+        if (lane_id() == 0) hl[wi] = m;
+    }
+}
+
 }  // namespace
 
 struct DeltaWork {
@@ -1653,6 +1693,7 @@ struct DeltaWork {
     DevBuf<u64> cw;        // interleaved relabeled edges
     ScanWs lscan;
     DevBuf<u64> lrow, lcw; // light CSR (per delta)
+    DevBuf<u64> hl;        // has-light-edges bitmap (per delta)
     ~DeltaWork() {
         if (host) (void)hipHostFree(host);
         if (hctl) (void)hipHostFree(hctl);
@@ -1706,6 +1747,9 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
             v2_interleave_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.col.p, R.w.p, g.nnz, w.cw.p);
             PJ_LAUNCH_CHECK();
         }
+        w.hl.alloc((size_t)(n + 63) / 64);
+        v2_haslight_k<<<grid_for(n, 256, maxgrid), 256, 0, s>>>(w.lsplit.p, n, w.hl.p);
+        PJ_LAUNCH_CHECK();
         w.lrow.alloc((size_t)n + 1);
         exclusive_scan_u32(w.lsplit.p, w.lrow.p, n, w.lscan, s);
         w.lcw.alloc(std::max<u64>(light, 1));
@@ -1925,6 +1969,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     a.cw = w.cw.p;
     a.lrow = w.lrow.p;
     a.lcw = w.lcw.p;
+    a.hl = g.light_filter ? w.hl.p : nullptr;
     a.mb = w.mb.p;
     a.ctl = w.ctl.p;
     a.hv = w.hv.p;
@@ -2069,6 +2114,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             }
             if (enter_tail) {
                 tail = true;
+                a.hl = nullptr;  // the tail's light prefixes come from lsplit2
                 a.swrite = nullptr;
                 a.sbits = w.sb.p;
                 a.lsplit = w.lsplit2.p;
