@@ -1004,11 +1004,161 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const u64* __restrict
     return newc;
 }
 
+// Dense light round (the frontier holds more than dense_min vertices): the
+// workgroup takes a tile of V2_DT consecutive vertices, reads their frontier
+// words, row offsets and distances with coalesced loads (4 consecutive vertices
+// per thread), compacts the frontier vertices' light segments into LDS with one
+// block scan and relaxes the tile's edges edge-balanced, 4 independent edges per
+// thread (v2_relax_g), instead of one vertex per lane with a dependent chain of
+// loads per vertex. Segments longer than V2_DHT go to the hub queue.
+constexpr int V2_DT = DB * 4;     // vertices per dense tile (16 frontier words)
+constexpr u64 V2_DHT = 4096;      // dense mode: longer segments -> hub queue
+template <typename Off>
+struct V2Dense {
+    Off b[V2_DT];                 // segment begin (edge index into lcw, or cw in the tail)
+    u32 off[V2_DT];               // segment start inside the tile's edge range
+    int32_t du[V2_DT];
+    u64 f[V2_DT / 64], fnew[V2_DT / 64];
+    u64 red[DB / WAVE];
+};
+
+__device__ __forceinline__ u32 v2_dense_find(const u32* off, u32 ns, u32 e) {
+    u32 lo = 0, hi = ns - 1;
+    while (lo < hi) {
+        const u32 mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= e) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+template <typename Off>
+__device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __restrict__ row, u64* __restrict__ fin,
+                                              u64* __restrict__ fout, int hs, u32& newc, u64& fe, u64& mh, u64& ml,
+                                              V2Dense<Off>& sh) {
+    const int tid = threadIdx.x, lane = lane_id();
+    const u64 mask = (1ull << V2_EB) - 1ull;
+    const u64* ed = a.ltail ? a.cw : a.lcw;
+    const i64 ntiles = (a.n + V2_DT - 1) / V2_DT;
+    for (i64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const i64 w0 = tile * (V2_DT / 64);
+        if (tid < V2_DT / 64) {
+            u64 f = 0, nw = 0;
+            if (w0 + tid < a.nwords) {
+                f = fin[w0 + tid];
+                if (f) {
+                    fin[w0 + tid] = 0;
+                    const u64 old = a.mb[w0 + tid];  // the block owns these words of mb
+                    nw = f & ~old;
+                    if (nw) a.mb[w0 + tid] = old | f;
+                }
+            }
+            sh.f[tid] = f;
+            sh.fnew[tid] = nw;
+        }
+        __syncthreads();
+        u64 anyf = 0;
+#pragma unroll
+        for (int k = 0; k < V2_DT / 64; ++k) anyf |= sh.f[k];
+        if (!anyf) {  // block-uniform
+            __syncthreads();
+            continue;
+        }
+        const int i0 = tid * 4;
+        const i64 v0 = tile * V2_DT + i0;
+        const u32 nib = (u32)(sh.f[i0 >> 6] >> (i0 & 63)) & 15u;
+        const u32 nnew = (u32)(sh.fnew[i0 >> 6] >> (i0 & 63)) & 15u;
+        u64 b[4], e[4];
+        int32_t du[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            b[j] = e[j] = 0;
+            du[j] = 0;
+            if ((nib >> j) & 1u) {
+                const i64 v = v0 + j;
+                du[j] = a.dist[v];
+                if (a.ltail) {
+                    b[j] = (u64)row[v];
+                    e[j] = b[j] + a.lsplit[v];
+                } else {
+                    b[j] = a.lrow[v];
+                    e[j] = a.lrow[v + 1];
+                }
+                if ((nnew >> j) & 1u) {
+                    mh += (u64)row[v + 1] - (u64)row[v] - (e[j] - b[j]);
+                    ml += e[j] - b[j];
+                }
+            }
+        }
+        // long segments -> hub queue (wave-aggregated packed append, as v2_expand_k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool hub = e[j] - b[j] > V2_DHT;
+            const u64 hm = __ballot(hub);
+            if (hm) {
+                const u64 seg = hub ? e[j] - b[j] : 0;
+                const u64 ie = wave_incl_scan(seg);
+                const u64 tot = __shfl(ie, 63, 64);
+                const int leader = __ffsll((long long)hm) - 1;
+                u64 base = 0;
+                if (lane == leader) base = atomicAdd(&a.ctl->hub[hs].v, ((u64)__popcll(hm) << V2_EB) | tot);
+                base = __shfl(base, leader, 64);
+                if (hub) {
+                    const u64 slot = (base >> V2_EB) + (u64)__popcll(hm & lanemask_lt());
+                    const u64 q = (u64)hs * a.hcap + slot;
+                    a.hv[q] = (u32)(v0 + j);
+                    a.hbeg[q] = b[j];
+                    a.hoff[q] = (base & mask) + ie - seg;
+                    e[j] = b[j];
+                }
+            }
+        }
+        u64 cnt = 0, edges = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (e[j] > b[j]) {
+                ++cnt;
+                edges += e[j] - b[j];
+            }
+        u64 tot;
+        const u64 ex = block_excl_scan<DB / WAVE>((cnt << V2_EB) | edges, sh.red, tot);
+        u32 slot = (u32)(ex >> V2_EB);
+        u32 eo = (u32)(ex & mask);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (e[j] > b[j]) {
+                sh.b[slot] = (Off)b[j];
+                sh.du[slot] = du[j];
+                sh.off[slot] = eo;
+                ++slot;
+                eo += (u32)(e[j] - b[j]);
+            }
+        const u32 ns = (u32)(tot >> V2_EB), te = (u32)(tot & mask);
+        __syncthreads();
+        for (u32 e0 = 0; e0 < te; e0 += DB * 4) {
+            u64 idx[4];
+            int32_t dj[4];
+            bool val[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32 x = e0 + (u32)j * DB + (u32)tid;
+                val[j] = x < te;
+                const u32 sl = val[j] ? v2_dense_find(sh.off, ns, x) : 0u;
+                idx[j] = val[j] ? (u64)sh.b[sl] + (x - sh.off[sl]) : 0ull;
+                dj[j] = val[j] ? sh.du[sl] : 0;
+            }
+            newc += v2_relax_g<true, 4>(a, ed, idx, dj, val, fout, fe);
+        }
+        __syncthreads();
+    }
+}
+
 // LIGHT: relax the light prefixes of fin's vertices (a band round); HEAVY: the
 // heavy segments of fin = mb (push heavy step). fin words are cleared as read.
 template <typename Off, bool LIGHT>
 __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
-                                                  u64* __restrict__ fout, int cin, int hs, u64 pull_thresh) {
+                                                  u64* __restrict__ fout, int cin, int hs, u64 pull_thresh,
+                                                  u64 dense_min) {
     constexpr int NWV = DB / WAVE;
     __shared__ u64 red[NWV];
     if (LIGHT) {
@@ -1023,6 +1173,7 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
             for (i64 wi = (i64)blockIdx.x * DB + threadIdx.x; wi < a.nwords; wi += (i64)gridDim.x * DB) fin[wi] = 0;
             return;
         }
+        if (v2_slot_sum(a.ctl->cnt[cin]) > dense_min) return;  // v2_pull_round_k ran it tile-dense
     }
     const int lane = lane_id();
     const u64 mask = (1ull << V2_EB) - 1ull;
@@ -1559,14 +1710,25 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
 // (v2_pull_long_body) and the short rows (v2_pull_light_body) over the whole
 // grid. The two touch disjoint vertices; frontier words are OR-ed in.
 template <typename Off>
-__global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __restrict__ row,
-                                                      const u64* __restrict__ fin, u64* __restrict__ fout, int cin,
-                                                      u64 pull_thresh, const u32* __restrict__ lcv,
-                                                      const u32* __restrict__ lcc, u64 nlc) {
+__global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
+                                                      u64* __restrict__ fout, int cin, u64 pull_thresh,
+                                                      const u32* __restrict__ lcv, const u32* __restrict__ lcc, u64 nlc,
+                                                      int hs, u64 dense_min) {
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
     __shared__ u64 red[NWV];
-    if (v2_slot_sum(a.ctl->cnt[cin]) == 0 || v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) return;
+    const u64 fcount = v2_slot_sum(a.ctl->cnt[cin]);
+    if (fcount == 0) return;
+    if (v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) {
+        if (fcount <= dense_min) return;  // a sparse push round: v2_expand_k
+        __shared__ V2Dense<Off> dsh;
+        u32 newc = 0;
+        u64 mh = 0, ml = 0, fe = 0;
+        v2_dense_body<Off>(a, row, fin, fout, hs, newc, fe, mh, ml, dsh);
+        v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+        v2_flush2(mh, ml, a.ctl->mh, red);
+        return;
+    }
     u32 newc = 0;
     u64 fe = 0, mh = 0, ml = 0;
     if (nlc) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe);
@@ -1970,6 +2132,8 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     a.lrow = w.lrow.p;
     a.lcw = w.lcw.p;
     a.hl = g.light_filter ? w.hl.p : nullptr;
+    // light rounds whose frontier holds more than dense_frac x n vertices run tile-dense
+    const u64 dense_min = g.dense_frac > 0.0 ? (u64)(g.dense_frac * (double)n) : ~0ull;
     a.mb = w.mb.p;
     a.ctl = w.ctl.p;
     a.hv = w.hv.p;
@@ -2014,6 +2178,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         bool tail = false;
         const int32_t tdelta = (int32_t)std::min(65536.0, g.tail_delta < 0 ? 64.0 * delta : g.tail_delta);
         u64 last_fe = 1;  // light edges of the frontier at the last host sync (round 0: unknown)
+        u64 last_cnt = 1; // its vertex count
         while (lo < INT_INF) {
             const int32_t hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
             a.lo = (int32_t)lo;
@@ -2031,14 +2196,20 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 // when the last frontier seen could grow past the threshold in this batch
                 const bool try_pull = can_pull_light && (double)last_fe * g.pull_grow > (double)pull_thresh;
                 for (int q = 0; q < K; ++q) {
-                    if (try_pull) {
-                        v2_pull_round_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, pull_thresh,
-                                                                    w.lcv.p, w.lcc.p, w.nlc);
+                    // the round kernel also runs dense push rounds (v2_dense_body): whenever it
+                    // is launched for pulls, else for the first round of a batch whose last
+                    // seen frontier was dense
+                    const bool try_dense = dense_min != ~0ull && (try_pull || (q == 0 && last_cnt > dense_min));
+                    const u64 dmin = try_dense ? dense_min : ~0ull;
+                    if (try_pull || try_dense) {
+                        v2_pull_round_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs,
+                                                                    try_pull ? pull_thresh : ~0ull, w.lcv.p, w.lcc.p,
+                                                                    w.nlc, hr, dmin);
                         PJ_LAUNCH_CHECK();
                     }
-                    // (without the pull kernels the expand must push every round)
+                    // (without the round kernel the expand must push every round)
                     v2_expand_k<Off, true><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, hr,
-                                                                  try_pull ? pull_thresh : ~0ull);
+                                                                  try_pull ? pull_thresh : ~0ull, dmin);
                     PJ_LAUNCH_CHECK();
                     v2_hub_k<true><<<maxgrid, DB, 0, s>>>(a, w.f[1 - fi].p, cs, hr, (hr + 1) % 3);
                     PJ_LAUNCH_CHECK();
@@ -2050,6 +2221,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 sync_ctl();
                 last_fe = 0;
                 for (int i = 0; i < V2_NSH; ++i) last_fe += w.hctl->cnt[cs][i].pad[0];
+                last_cnt = slot(cs);
                 if (PJ_V2_STATS) {
                     fprintf(stderr, "band %d lo %lld rounds %d: frontier %llu edges %llu atomics %llu marks %llu next %llu\n",
                             (int)st.levels, lo, K, w.hctl->dbg[0].v, w.hctl->dbg[1].v, w.hctl->dbg[2].v,
@@ -2098,7 +2270,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 st.bu_levels++;
             } else {
                 if (mh > 0) {
-                    v2_expand_k<Off, false><<<maxgrid, DB, 0, s>>>(a, row, w.mb.p, nullptr, cs, hr, ~0ull);
+                    v2_expand_k<Off, false><<<maxgrid, DB, 0, s>>>(a, row, w.mb.p, nullptr, cs, hr, ~0ull, ~0ull);
                     PJ_LAUNCH_CHECK();
                     v2_hub_k<false><<<maxgrid, DB, 0, s>>>(a, nullptr, cs, hr, (hr + 1) % 3);
                     PJ_LAUNCH_CHECK();
@@ -2133,6 +2305,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             if (enter_tail && (long long)tdelta <= w.maxw) heavy_left = w.hctl->dbg[0].v;
             last_fe = 0;
             for (int i = 0; i < V2_NSH; ++i) last_fe += w.hctl->cnt[cs][i].pad[0];
+            last_cnt = slot(cs);
             if (slot(cs) == 0) {
                 const u64 mv = w.hctl->minv.v;
                 if (mv >= (u64)INT_INF) break;  // nothing reached beyond the settled bands

@@ -202,6 +202,8 @@ struct Graph {
     int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
     int level_batch = 0; // BFS levels enqueued per host check (0 = default 8, doubling)
+    double dense_frac = 0.1; // delta v2: a light round with a frontier above dense_frac x n runs tile-dense (0 = never;
+                             // swept 0 / 0.02 / 0.1 / 0.3 on k26w: 0.1 best)
     int light_filter = 1; // delta v2: skip vertices without light edges in light rounds (hl bitmap)
     int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)

@@ -203,6 +203,44 @@ def test_weighted_text_and_kronecker(ctx, oracle):
         assert (g.sssp(int(r)) == oracle.dijkstra(row, col, wc, int(r))).all()
 
 
+def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
+    """Tile-dense light rounds (dense_frac: never / whenever the frontier is non-empty /
+    the default threshold) and the has-light-edge filter (on / off), with and without
+    light pulls and the tail switch: directed random graphs (no pulls), a star whose
+    light segment exceeds the dense mode's hub threshold (4096), and Kronecker graphs.
+    Bit-exact against the oracle Dijkstra."""
+    rng = np.random.default_rng(33)
+    graphs = []
+    for kind, n in (("uniform", 30000), ("hub", 20000)):
+        src, dst = random_graph(rng, kind, n)
+        w = rng.integers(1, 200, len(src)).astype(np.uint32)
+        graphs.append((kind, ctx.load_coo(src, dst, w=w, n=n)))
+    fan = 9000  # vertex 1 -> 9000 leaves at weight 1: one light segment > 4096 edges
+    src = np.concatenate([[0], np.ones(fan, np.int64), 2 + rng.integers(0, fan, 20000)])
+    dst = np.concatenate([[1], 2 + np.arange(fan), 2 + rng.integers(0, fan, 20000)])
+    w = np.concatenate([[3], np.ones(fan), rng.integers(1, 90, 20000)]).astype(np.uint32)
+    graphs.append(("star", ctx.load_coo(src, dst, w=w, n=2 + fan)))
+    graphs.append(("k13", ctx.generate_kronecker(13, 16, 17, weighted=True)))
+    graphs.append(("k15ef4", ctx.generate_kronecker(15, 4, 18, weighted=True)))
+    for name, g in graphs:
+        row, col, wc = g.get_csr()
+        col = col.astype(np.uint32)
+        roots = [0] + [int(r) for r in g.sample_roots(4, 2)]
+        exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
+        for dense in (0.0, 1e-12, 0.02):
+            for lf in (0, 1):
+                for lp, tf in ((2.0, 0.1), (0.0, 0.1), (2.0, 0.0)):
+                    g.set_option("dense_frac", dense)
+                    g.set_option("light_filter", lf)
+                    g.set_option("light_pull", lp)
+                    g.set_option("tail_frac", tf)
+                    for delta in (0, 40):
+                        g.set_option("delta", delta)
+                        for r in roots:
+                            assert (g.sssp(r) == exp[r]).all(), (name, dense, lf, lp, tf, delta, r)
+        g.close()
+
+
 @pytest.mark.parametrize("scale,ef", [(13, 16), (15, 4)])
 def test_weighted_band_width(ctx, oracle, scale, ef):
     """Bands narrower than the light threshold (delta.hip band_width): light edges
