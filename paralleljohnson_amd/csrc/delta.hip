@@ -625,8 +625,25 @@ __device__ __forceinline__ bool pull_step_band_cw(const u64* __restrict__ ed, co
     k += (Off)nv;
     return stop;
 }
-template <typename Off>
-__device__ __forceinline__ bool pull_step_fin_cw(const u64* __restrict__ ed, const int32_t* __restrict__ dist,
+// Edge records read as u64 (col | w << 32): the interleaved CSR (cw), or the
+// light CSR packed in 32 bits (col | w << cb, when every light weight fits 32 - cb
+// bits and every id cb bits: half the bytes per light edge).
+struct ESrc {
+    const u64* e64;
+    const u32* e32;  // non-null: packed records
+    u32 cb;
+};
+__device__ __forceinline__ u64 eat(const u64* __restrict__ p, u64 k) { return p[k]; }
+__device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
+    if (s.e32) {
+        const u32 x = s.e32[k];
+        return (u64)(x & ((1u << s.cb) - 1u)) | ((u64)(x >> s.cb) << 32);
+    }
+    return s.e64[k];
+}
+
+template <typename Off, typename E>
+__device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __restrict__ dist,
                                                  const u64* __restrict__ fin, Off& k, Off lim, int32_t lo,
                                                  int32_t& cur) {
     u32 w[PU], u[PU];
@@ -634,7 +651,7 @@ __device__ __forceinline__ bool pull_step_fin_cw(const u64* __restrict__ ed, con
 #pragma unroll
     for (int j = 0; j < PU; ++j) {
         ok[j] = k + (Off)j < lim;
-        const u64 x = ok[j] ? ed[k + j] : 0ull;
+        const u64 x = ok[j] ? eat(ed, (u64)(k + j)) : 0ull;
         w[j] = (u32)(x >> 32);
         u[j] = (u32)x;
     }
@@ -857,8 +874,11 @@ struct V2Args {
     const u64* cw;    // edges interleaved: col | w << 32 (the relabeled CSR)
     const u64* lrow;  // light CSR: the light prefixes of the rows, packed
     const u64* lcw;
+    const u32* lcw32; // packed light CSR (col | w << lcb), or null
+    u32 lcb;
     const u64* hl;    // bit v: v has a light edge (lsplit[v] > 0) for this delta; null in the tail
-    int ltail;        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
+    int ltail;
+    int dense_pull;   // light pulls in tile-dense form (v2_dense_pull_body)        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
     const u64* sbits; // tail mode: settled-before-the-tail bitmap; relaxations skip its targets
     u64* swrite;      // the heavy step entering the tail writes that bitmap (pull / select)
     u64* mb;
@@ -868,6 +888,13 @@ struct V2Args {
     u64* hoff;   // [3][hcap]
     u64 hcap;
 };
+// the light edges of a band round (light CSR, or the light prefixes of cw in the tail)
+__device__ __forceinline__ ESrc v2_light_src(const V2Args& a) {
+    if (a.ltail) return ESrc{a.cw, nullptr, 0};
+    return ESrc{a.lcw, a.lcw32, a.lcb};
+}
+__device__ __forceinline__ ESrc v2_cw_src(const V2Args& a) { return ESrc{a.cw, nullptr, 0}; }
+
 
 __device__ __forceinline__ u64 v2_slot_sum(const V2Line* sl) {
     u64 t = 0;
@@ -878,9 +905,9 @@ __device__ __forceinline__ u64 v2_slot_sum(const V2Line* sl) {
 
 // one relaxation; LIGHT: a target lowered below hi is marked in fout (returns 1 if newly marked)
 template <bool LIGHT>
-__device__ __forceinline__ u32 v2_relax(const V2Args& a, const u64* __restrict__ ed, u64 k, int32_t du,
+__device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, int32_t du,
                                         u64* __restrict__ fout, u64& fe) {
-    const u64 x = ed[k];
+    const u64 x = eat(ed, k);
     const u32 t = (u32)x;
     const long long nd = (long long)du + (long long)(x >> 32);
     if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[1].v, 1ull);
@@ -917,7 +944,7 @@ __device__ __forceinline__ u64 v2_slot_edges(const V2Line* sl) {
 
 // PU consecutive edges [k, min(k + PU, lim)) of one source in one step (independent loads).
 template <bool LIGHT>
-__device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const u64* __restrict__ ed, u64 k, u64 lim, int32_t du,
+__device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const ESrc ed, u64 k, u64 lim, int32_t du,
                                           u64* __restrict__ fout, u64& fe) {
     u32 t[PU];
     long long nd[PU];
@@ -925,7 +952,7 @@ __device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const u64* __restrict
 #pragma unroll
     for (int j = 0; j < PU; ++j) {
         ok[j] = k + j < lim;
-        const u64 x = ok[j] ? ed[k + j] : 0ull;
+        const u64 x = ok[j] ? eat(ed, k + j) : 0ull;
         t[j] = (u32)x;
         nd[j] = (long long)du + (long long)(x >> 32);
         ok[j] = ok[j] && nd[j] < INT_INF;
@@ -964,7 +991,7 @@ __device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const u64* __restrict
 // this lane or another, so it belongs in the next frontier either way; the
 // atomicOr's old bit keeps the count of new frontier vertices exact.
 template <bool LIGHT, int N>
-__device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const u64* __restrict__ ed, const u64 (&idx)[N],
+__device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const u64 (&idx)[N],
                                           const int32_t (&du)[N], const bool (&val)[N], u64* __restrict__ fout,
                                           u64& fe) {
     u32 t[N];
@@ -972,7 +999,7 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const u64* __restrict
     bool ok[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        const u64 x = val[j] ? ed[idx[j]] : 0ull;
+        const u64 x = val[j] ? eat(ed, idx[j]) : 0ull;
         t[j] = (u32)x;
         nd[j] = (long long)du[j] + (long long)(x >> 32);
         ok[j] = val[j] && nd[j] < INT_INF;
@@ -1038,7 +1065,7 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
                                               V2Dense<Off>& sh) {
     const int tid = threadIdx.x, lane = lane_id();
     const u64 mask = (1ull << V2_EB) - 1ull;
-    const u64* ed = a.ltail ? a.cw : a.lcw;
+    const ESrc ed = v2_light_src(a);
     const i64 ntiles = (a.n + V2_DT - 1) / V2_DT;
     for (i64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const i64 w0 = tile * (V2_DT / 64);
@@ -1283,7 +1310,7 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
             bool go = k < lim;
             while (__ballot(go)) {
                 if (go) {
-                    newc += v2_relax_n<LIGHT>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, k, lim, du, fout, fe);
+                    newc += v2_relax_n<LIGHT>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), k, lim, du, fout, fe);
                     k = k + PU < lim ? k + PU : lim;
                     go = k < lim;
                 }
@@ -1305,7 +1332,7 @@ __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restric
                     const u64 kl = __shfl(k, l, 64), xl = __shfl(exc, l, 64);
                     const int32_t dl = __shfl(du, l, 64);
                     if (gi < tot)
-                        newc += v2_relax<LIGHT>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, kl + (gi - xl), dl, fout, fe);
+                        newc += v2_relax<LIGHT>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), kl + (gi - xl), dl, fout, fe);
                 }
             }
         }
@@ -1354,7 +1381,7 @@ __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout,
             idx[j] = val[j] ? s_b[sl] + (e - sh.off[sl]) : 0ull;
             du[j] = val[j] ? s_du[sl] : 0;
         }
-        newc += v2_relax_g<LIGHT, NJ>(a, (LIGHT && !a.ltail) ? a.lcw : a.cw, idx, du, val, fout, fe);
+        newc += v2_relax_g<LIGHT, NJ>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), idx, du, val, fout, fe);
         __syncthreads();
     }
     if (LIGHT) v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
@@ -1592,7 +1619,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             bool go = act && k < lim, done = !act || k >= e;
             while (__ballot(go)) {
                 if (go) {
-                    if (pull_step_fin_cw<Off>(a.lcw, a.dist, fin, k, lim, lo, cur)) {
+                    if (pull_step_fin_cw<Off>(v2_light_src(a), a.dist, fin, k, lim, lo, cur)) {
                         done = true;
                         go = false;
                     } else {
@@ -1610,7 +1637,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                 for (Off kk = kb; kk < ke; kk += WAVE) {
                     const Off k0 = kk + lane;
                     const bool valid = k0 < ke;
-                    const u64 x = valid ? a.lcw[k0] : 0ull;
+                    const u64 x = valid ? eat(v2_light_src(a), (u64)k0) : 0ull;
                     const u32 w = (u32)(x >> 32);
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
                     int32_t cand = INT_INF;
@@ -1669,12 +1696,12 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
         const u32 ls = (u32)(a.lrow[v + 1] - rb);
         const u64 kb = rb + (u64)lcc[it] * V2_PCH;
         const u64 ke = min(rb + ls, kb + V2_PCH);
-        if ((long long)lo + (a.lcw[kb] >> 32) >= (long long)d0) continue;
+        if ((long long)lo + (eat(v2_light_src(a), kb) >> 32) >= (long long)d0) continue;
         int32_t cur = d0;
         for (u64 kk = kb; kk < ke; kk += WAVE) {
             const u64 k0 = kk + lane;
             const bool valid = k0 < ke;
-            const u64 x = valid ? a.lcw[k0] : 0ull;
+            const u64 x = valid ? eat(v2_light_src(a), k0) : 0ull;
             const u32 w = (u32)(x >> 32);
             const bool stop = !valid || (long long)lo + w >= (long long)cur;
             int32_t cand = INT_INF;
@@ -1706,6 +1733,158 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
     }
 }
 
+// Tile-dense form of v2_pull_light_body (dense_pull): the workgroup takes V2_DT
+// consecutive vertices, 4 per thread with coalesced loads (distances, light-row
+// bounds, the new members' row bounds), compacts the candidates' light rows (dist
+// > lo, light edges, not a long row) into LDS with one block scan and scans all
+// their edges edge-balanced, 4 independent edges per thread: an edge can help only
+// when lo + w is below its vertex's best so far; a frontier in-neighbour's
+// dist + w is folded into the vertex's LDS minimum. The block owns its vertices:
+// improved distances are plain stores, the frontier words are OR-ed in (the long
+// rows' chunks run concurrently).
+template <typename Off>
+struct V2DensePull {
+    Off b[V2_DT];        // light-row begin (index into lcw)
+    u32 off[V2_DT + 1];  // row start inside the tile's edge range
+    int32_t best[V2_DT];
+    uint16_t vi[V2_DT];  // vertex index inside the tile
+    u32 newb[2 * (V2_DT / 64)];
+    u64 fnew[V2_DT / 64];
+    u64 red[DB / WAVE];
+};
+
+template <typename Off>
+__device__ __forceinline__ void v2_dense_pull_body(const V2Args& a, const Off* __restrict__ row,
+                                                   const u64* __restrict__ fin, u64* __restrict__ fout, u32& newc,
+                                                   u64& fe, u64& mh, u64& ml, V2DensePull<Off>& sh) {
+    const int tid = threadIdx.x;
+    const int32_t lo = a.lo, hi = a.hi;
+    const u64 mask = (1ull << V2_EB) - 1ull;
+    const i64 ntiles = (a.n + V2_DT - 1) / V2_DT;
+    for (i64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const i64 w0 = tile * (V2_DT / 64);
+        if (tid < V2_DT / 64) {
+            u64 nw = 0;
+            if (w0 + tid < a.nwords) {
+                const u64 f = fin[w0 + tid];
+                if (f) {
+                    const u64 old = a.mb[w0 + tid];  // the block owns these words of mb
+                    nw = f & ~old;
+                    if (nw) a.mb[w0 + tid] = old | f;
+                }
+            }
+            sh.fnew[tid] = nw;
+        }
+        if (tid < 2 * (V2_DT / 64)) sh.newb[tid] = 0;
+        __syncthreads();
+        const int i0 = tid * 4;
+        const i64 v0 = tile * V2_DT + i0;
+        const u32 nnew = (u32)(sh.fnew[i0 >> 6] >> (i0 & 63)) & 15u;
+        const u32 hlb = a.hl ? (u32)(a.hl[(v0 >> 6) < a.nwords ? (v0 >> 6) : 0] >> (v0 & 63)) & 15u : 15u;
+        u64 b[4], e[4];
+        int32_t d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const i64 v = v0 + j;
+            b[j] = e[j] = 0;
+            d[j] = 0;
+            if (v < a.n) {
+                d[j] = a.dist[v];
+                if ((nnew >> j) & 1u) {
+                    const u64 ls = a.lsplit[v];
+                    mh += (u64)row[v + 1] - (u64)row[v] - ls;
+                    ml += ls;
+                }
+                if (d[j] > lo && ((hlb >> j) & 1u)) {
+                    b[j] = a.lrow[v];
+                    e[j] = a.lrow[v + 1];
+                    if (e[j] - b[j] > V2_PLMAX) e[j] = b[j];  // long rows: v2_pull_long_body
+                }
+            }
+        }
+        u64 cnt = 0, edges = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (e[j] > b[j]) {
+                ++cnt;
+                edges += e[j] - b[j];
+            }
+        u64 tot;
+        const u64 ex = block_excl_scan<DB / WAVE>((cnt << V2_EB) | edges, sh.red, tot);
+        u32 slot = (u32)(ex >> V2_EB);
+        u32 eo = (u32)(ex & mask);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (e[j] > b[j]) {
+                sh.b[slot] = (Off)b[j];
+                sh.off[slot] = eo;
+                sh.best[slot] = d[j];
+                sh.vi[slot] = (uint16_t)(i0 + j);
+                ++slot;
+                eo += (u32)(e[j] - b[j]);
+            }
+        const u32 ns = (u32)(tot >> V2_EB), te = (u32)(tot & mask);
+        if (tid == 0) sh.off[ns] = te;
+        __syncthreads();
+        for (u32 e0 = 0; e0 < te; e0 += DB * 4) {
+            u32 sl[4], u[4], w[4];
+            bool ok[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32 x = e0 + (u32)j * DB + (u32)tid;
+                ok[j] = x < te;
+                sl[j] = ok[j] ? v2_dense_find(sh.off, ns, x) : 0u;
+                const u64 rec = ok[j] ? eat(v2_light_src(a), (u64)sh.b[sl[j]] + (x - sh.off[sl[j]])) : 0ull;
+                u[j] = (u32)rec;
+                w[j] = (u32)(rec >> 32);
+            }
+            u64 fw[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                ok[j] = ok[j] && (long long)lo + w[j] < (long long)sh.best[sl[j]];
+                fw[j] = ok[j] ? fin[u[j] >> 6] : 0ull;
+            }
+            int32_t du[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                ok[j] = ok[j] && ((fw[j] >> (u[j] & 63)) & 1ull);
+                du[j] = ok[j] ? a.dist[u[j]] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (ok[j]) {
+                    const long long nd = (long long)du[j] + w[j];
+                    if (nd < sh.best[sl[j]]) atomicMin(&sh.best[sl[j]], (int32_t)nd);
+                }
+        }
+        __syncthreads();
+        for (u32 q = tid; q < ns; q += DB) {
+            const u32 i = sh.vi[q];
+            const i64 v = tile * V2_DT + i;
+            const int32_t bq = sh.best[q];
+            if (bq < a.dist[v]) {  // (the block's own vertex: dist[v] is still d0)
+                a.dist[v] = bq;
+                if (bq < hi) {
+                    atomicOr(&sh.newb[i >> 5], 1u << (i & 31));
+                    ++newc;
+                    fe += sh.off[q + 1] - sh.off[q];
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < V2_DT / 64 && w0 + tid < a.nwords) {
+            const u64 word = (u64)sh.newb[2 * tid] | ((u64)sh.newb[2 * tid + 1] << 32);
+            if (word) atomicOr(fout + w0 + tid, word);
+        }
+    }
+}
+
+template <typename Off>
+union V2RoundLds {  // the round kernel's LDS: a dense push or a dense pull, never both
+    V2Dense<Off> push;
+    V2DensePull<Off> pull;
+};
+
 // Pull form of a light round, one launch: the chunks of the long light rows
 // (v2_pull_long_body) and the short rows (v2_pull_light_body) over the whole
 // grid. The two touch disjoint vertices; frontier words are OR-ed in.
@@ -1717,14 +1896,14 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
     __shared__ u64 red[NWV];
+    __shared__ V2RoundLds<Off> lds;
     const u64 fcount = v2_slot_sum(a.ctl->cnt[cin]);
     if (fcount == 0) return;
     if (v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) {
         if (fcount <= dense_min) return;  // a sparse push round: v2_expand_k
-        __shared__ V2Dense<Off> dsh;
         u32 newc = 0;
         u64 mh = 0, ml = 0, fe = 0;
-        v2_dense_body<Off>(a, row, fin, fout, hs, newc, fe, mh, ml, dsh);
+        v2_dense_body<Off>(a, row, fin, fout, hs, newc, fe, mh, ml, lds.push);
         v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
         v2_flush2(mh, ml, a.ctl->mh, red);
         return;
@@ -1732,7 +1911,11 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     u32 newc = 0;
     u64 fe = 0, mh = 0, ml = 0;
     if (nlc) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe);
-    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml);
+    if (a.dense_pull) {
+        v2_dense_pull_body<Off>(a, row, fin, fout, newc, fe, mh, ml, lds.pull);
+    } else {
+        v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml);
+    }
     v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
     v2_flush2(mh, ml, a.ctl->mh, red);
 }
@@ -1765,16 +1948,20 @@ __global__ void v2_interleave_k(const u32* __restrict__ col, const u32* __restri
 }
 // Light CSR: lcw[lrow[v] + j] = cw[row[v] + j] for j < lsplit[v] (a wave per vertex
 // for long prefixes, a lane per vertex otherwise).
-template <typename Off>
+__device__ __forceinline__ void v2_lput(u64* __restrict__ o, u64 k, u64 x, u32) { o[k] = x; }
+__device__ __forceinline__ void v2_lput(u32* __restrict__ o, u64 k, u64 x, u32 cb) {
+    o[k] = (u32)x | ((u32)(x >> 32) << cb);
+}
+template <typename Off, typename OutT>
 __global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restrict__ lsplit, const u64* __restrict__ lrow,
-                               const u64* __restrict__ cw, i64 n, u64* __restrict__ lcw) {
+                               const u64* __restrict__ cw, i64 n, OutT* __restrict__ lcw, u32 cb) {
     const int lane = lane_id();
     for (i64 v0 = ((i64)blockIdx.x * blockDim.x + threadIdx.x) & ~63ll; v0 < n; v0 += (i64)gridDim.x * blockDim.x) {
         const i64 v = v0 + lane;
         const u32 ls = v < n ? lsplit[v] : 0u;
         const bool longp = ls > 64;
         if (v < n && !longp)
-            for (u32 j = 0; j < ls; ++j) lcw[lrow[v] + j] = cw[(u64)row[v] + j];
+            for (u32 j = 0; j < ls; ++j) v2_lput(lcw, lrow[v] + j, cw[(u64)row[v] + j], cb);
         u64 lm = __ballot(longp);
         while (lm) {
             const int l = __ffsll((long long)lm) - 1;
@@ -1782,7 +1969,7 @@ __global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restric
             const i64 vl = v0 + l;
             const u64 src = (u64)row[vl], dst = lrow[vl];
             const u32 cnt = lsplit[vl];
-            for (u32 j = lane; j < cnt; j += WAVE) lcw[dst + j] = cw[src + j];
+            for (u32 j = lane; j < cnt; j += WAVE) v2_lput(lcw, dst + j, cw[src + j], cb);
         }
     }
 }
@@ -1855,6 +2042,9 @@ struct DeltaWork {
     DevBuf<u64> cw;        // interleaved relabeled edges
     ScanWs lscan;
     DevBuf<u64> lrow, lcw; // light CSR (per delta)
+    DevBuf<u32> lcw32;     // the light CSR packed (col | w << lcb), when it fits
+    u32 lcb = 0;
+    int packed_for = -1;   // g.light_pack the light CSR was built for
     DevBuf<u64> hl;        // has-light-edges bitmap (per delta)
     ~DeltaWork() {
         if (host) (void)hipHostFree(host);
@@ -1885,7 +2075,8 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         const double d = 3.5 * g.mean_weight / std::max(1.0, mean_deg);
         delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(d)));
     }
-    if (w.lsplit_delta != (u32)delta && n > 0) {
+    if ((w.lsplit_delta != (u32)delta || w.packed_for != g.light_pack) && n > 0) {
+        w.packed_for = g.light_pack;
         light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)delta, w.lsplit.p);
         PJ_LAUNCH_CHECK();
         w.lsplit_delta = (u32)delta;
@@ -1914,9 +2105,24 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         PJ_LAUNCH_CHECK();
         w.lrow.alloc((size_t)n + 1);
         exclusive_scan_u32(w.lsplit.p, w.lrow.p, n, w.lscan, s);
-        w.lcw.alloc(std::max<u64>(light, 1));
-        if (light)
-            v2_light_csr_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, n, w.lcw.p);
+        // packed light records when every light weight (< delta) fits the bits above the ids
+        int wb = 1;
+        while ((1ll << wb) < (long long)delta) ++wb;
+        const u32 cb = (u32)(32 - wb);
+        w.lcb = (g.light_pack && wb < 32 && (u64)n <= (1ull << cb)) ? cb : 0u;
+        w.lcw.release();
+        w.lcw32.release();
+        if (w.lcb) {
+            w.lcw32.alloc(std::max<u64>(light, 1));
+            if (light)
+                v2_light_csr_k<Off, u32><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, n,
+                                                                                   w.lcw32.p, w.lcb);
+        } else {
+            w.lcw.alloc(std::max<u64>(light, 1));
+            if (light)
+                v2_light_csr_k<Off, u64><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, n,
+                                                                                   w.lcw.p, 0u);
+        }
         PJ_LAUNCH_CHECK();
         w.lcv.alloc(std::max<u64>(w.nlc, 1));
         w.lcc.alloc(std::max<u64>(w.nlc, 1));
@@ -2131,7 +2337,10 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     a.cw = w.cw.p;
     a.lrow = w.lrow.p;
     a.lcw = w.lcw.p;
+    a.lcw32 = w.lcb ? w.lcw32.p : nullptr;
+    a.lcb = w.lcb;
     a.hl = g.light_filter ? w.hl.p : nullptr;
+    a.dense_pull = g.dense_pull;
     // light rounds whose frontier holds more than dense_frac x n vertices run tile-dense
     const u64 dense_min = g.dense_frac > 0.0 ? (u64)(g.dense_frac * (double)n) : ~0ull;
     a.mb = w.mb.p;

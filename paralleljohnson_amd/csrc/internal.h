@@ -204,7 +204,9 @@ struct Graph {
     int level_batch = 0; // BFS levels enqueued per host check (0 = default 8, doubling)
     double dense_frac = 0.1; // delta v2: a light round with a frontier above dense_frac x n runs tile-dense (0 = never;
                              // swept 0 / 0.02 / 0.1 / 0.3 on k26w: 0.1 best)
-    int light_filter = 1; // delta v2: skip vertices without light edges in light rounds (hl bitmap)
+    int light_filter = 1;
+    int dense_pull = 0;
+    int light_pack = 1;   // delta v2: light CSR records packed in 32 bits when they fit (0/1)   // delta v2: light pull rounds in tile-dense form (0/1) // delta v2: skip vertices without light edges in light rounds (hl bitmap)
     int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
     int bfs_small = 1;   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)

@@ -205,8 +205,9 @@ def test_weighted_text_and_kronecker(ctx, oracle):
 
 def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
     """Tile-dense light rounds (dense_frac: never / whenever the frontier is non-empty /
-    the default threshold) and the has-light-edge filter (on / off), with and without
-    light pulls and the tail switch: directed random graphs (no pulls), a star whose
+    the default threshold), tile-dense light pulls (dense_pull) and the has-light-edge
+    filter (on / off) and the packed 32-bit light CSR (on / off), with light pulls never / by the default rule / in every round and
+    with and without the tail switch: directed random graphs (no pulls), a star whose
     light segment exceeds the dense mode's hub threshold (4096), and Kronecker graphs.
     Bit-exact against the oracle Dijkstra."""
     rng = np.random.default_rng(33)
@@ -227,17 +228,19 @@ def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
         col = col.astype(np.uint32)
         roots = [0] + [int(r) for r in g.sample_roots(4, 2)]
         exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
-        for dense in (0.0, 1e-12, 0.02):
+        for dense, dp, pk in ((0.0, 0, 0), (1e-12, 1, 1), (0.02, 0, 1), (0.02, 1, 0), (0.1, 1, 1)):
             for lf in (0, 1):
-                for lp, tf in ((2.0, 0.1), (0.0, 0.1), (2.0, 0.0)):
+                for lp, tf in ((2.0, 0.1), (0.0, 0.1), (2.0, 0.0), (1e15, 0.1)):
                     g.set_option("dense_frac", dense)
+                    g.set_option("dense_pull", dp)
+                    g.set_option("light_pack", pk)
                     g.set_option("light_filter", lf)
                     g.set_option("light_pull", lp)
                     g.set_option("tail_frac", tf)
                     for delta in (0, 40):
                         g.set_option("delta", delta)
                         for r in roots:
-                            assert (g.sssp(r) == exp[r]).all(), (name, dense, lf, lp, tf, delta, r)
+                            assert (g.sssp(r) == exp[r]).all(), (name, dense, dp, pk, lf, lp, tf, delta, r)
         g.close()
 
 
