@@ -628,13 +628,17 @@ __device__ __forceinline__ bool pull_step_band_cw(const u64* __restrict__ ed, co
 // Edge records read as u64 (col | w << 32): the interleaved CSR (cw), or the
 // light CSR packed in 32 bits (col | w << cb, when every light weight fits 32 - cb
 // bits and every id cb bits: half the bytes per light edge).
+// Or split: u32 ids (e32) beside u8 weights (w8), 5 bytes per edge, when every
+// weight fits 8 bits (the heavy pull and the tail read the whole CSR this way).
 struct ESrc {
     const u64* e64;
-    const u32* e32;  // non-null: packed records
+    const u32* e32;  // non-null: packed records, or the ids when w8 is set
     u32 cb;
+    const uint8_t* w8;
 };
 __device__ __forceinline__ u64 eat(const u64* __restrict__ p, u64 k) { return p[k]; }
 __device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
+    if (s.w8) return (u64)s.e32[k] | ((u64)s.w8[k] << 32);
     if (s.e32) {
         const u32 x = s.e32[k];
         return (u64)(x & ((1u << s.cb) - 1u)) | ((u64)(x >> s.cb) << 32);
@@ -876,6 +880,8 @@ struct V2Args {
     const u64* lcw;
     const u32* lcw32; // packed light CSR (col | w << lcb), or null
     u32 lcb;
+    const u32* col;   // relabeled ids beside w8 (split records of the whole CSR), when w8 is set
+    const uint8_t* w8;
     const u64* hl;    // bit v: v has a light edge (lsplit[v] > 0) for this delta; null in the tail
     int ltail;
     int dense_pull;   // light pulls in tile-dense form (v2_dense_pull_body)        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
@@ -889,11 +895,14 @@ struct V2Args {
     u64 hcap;
 };
 // the light edges of a band round (light CSR, or the light prefixes of cw in the tail)
-__device__ __forceinline__ ESrc v2_light_src(const V2Args& a) {
-    if (a.ltail) return ESrc{a.cw, nullptr, 0};
-    return ESrc{a.lcw, a.lcw32, a.lcb};
+__device__ __forceinline__ ESrc v2_cw_src(const V2Args& a) {
+    if (a.w8) return ESrc{a.cw, a.col, 0, a.w8};
+    return ESrc{a.cw, nullptr, 0, nullptr};
 }
-__device__ __forceinline__ ESrc v2_cw_src(const V2Args& a) { return ESrc{a.cw, nullptr, 0}; }
+__device__ __forceinline__ ESrc v2_light_src(const V2Args& a) {
+    if (a.ltail) return v2_cw_src(a);
+    return ESrc{a.lcw, a.lcw32, a.lcb, nullptr};
+}
 
 
 __device__ __forceinline__ u64 v2_slot_sum(const V2Line* sl) {
@@ -1480,7 +1489,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                 if (go) {
                     // band members are exactly mb's bits: probe the (cache-resident)
                     // bitmap first, read dist only for members
-                    if (pull_step_fin_cw<Off>(a.cw, a.dist, a.mb, k, lim, lo, cur)) {
+                    if (pull_step_fin_cw<Off>(v2_cw_src(a), a.dist, a.mb, k, lim, lo, cur)) {
                         done = true;
                         go = false;
                     } else {
@@ -1498,7 +1507,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                 for (Off kk = kb; kk < ke; kk += WAVE) {
                     const Off k0 = kk + lane;
                     const bool valid = k0 < ke;
-                    const u64 x = valid ? a.cw[k0] : 0ull;
+                    const u64 x = valid ? eat(v2_cw_src(a), (u64)k0) : 0ull;
                     const u32 w = (u32)(x >> 32);
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
                     int32_t cand = INT_INF;
@@ -1946,6 +1955,10 @@ __global__ void v2_interleave_k(const u32* __restrict__ col, const u32* __restri
     for (i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (i64)gridDim.x * blockDim.x)
         cw[k] = (u64)col[k] | ((u64)w[k] << 32);
 }
+__global__ void v2_w8_k(const u32* __restrict__ w, i64 m, uint8_t* __restrict__ w8) {
+    for (i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (i64)gridDim.x * blockDim.x)
+        w8[k] = (uint8_t)w[k];
+}
 // Light CSR: lcw[lrow[v] + j] = cw[row[v] + j] for j < lsplit[v] (a wave per vertex
 // for long prefixes, a lane per vertex otherwise).
 __device__ __forceinline__ void v2_lput(u64* __restrict__ o, u64 k, u64 x, u32) { o[k] = x; }
@@ -2045,6 +2058,7 @@ struct DeltaWork {
     DevBuf<u32> lcw32;     // the light CSR packed (col | w << lcb), when it fits
     u32 lcb = 0;
     int packed_for = -1;   // g.light_pack the light CSR was built for
+    DevBuf<uint8_t> w8;    // u8 copy of the relabeled weights (max weight <= 255)
     DevBuf<u64> hl;        // has-light-edges bitmap (per delta)
     ~DeltaWork() {
         if (host) (void)hipHostFree(host);
@@ -2144,6 +2158,11 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
             PJ_HIP(hipStreamSynchronize(s));
         }
         w.maxw = (long long)h;
+    }
+    if (g.split_w && w.maxw <= 255 && !w.w8.p && g.nnz > 0) {  // u8 weights beside the ids
+        w.w8.alloc((size_t)g.nnz);
+        v2_w8_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.w.p, g.nnz, w.w8.p);
+        PJ_LAUNCH_CHECK();
     }
     return delta;
 }
@@ -2339,6 +2358,8 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     a.lcw = w.lcw.p;
     a.lcw32 = w.lcb ? w.lcw32.p : nullptr;
     a.lcb = w.lcb;
+    a.col = R.col.p;
+    a.w8 = (g.split_w && w.w8.p) ? w.w8.p : nullptr;
     a.hl = g.light_filter ? w.hl.p : nullptr;
     a.dense_pull = g.dense_pull;
     // light rounds whose frontier holds more than dense_frac x n vertices run tile-dense
