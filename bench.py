@@ -242,6 +242,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--part-scale", type=int, default=28, help="Kronecker scale of the partitioned run (configs[3])")
     ap.add_argument("--no-partitioned", action="store_true")
+    ap.add_argument("--part-timeout", type=float, default=240.0,
+                    help="watchdog of the partitioned leg (s): past it the line is emitted without that leg")
     ap.add_argument("--opt", action="append", default=[], help="libpj graph option key=value (tuning)")
     args = ap.parse_args()
 
@@ -348,10 +350,43 @@ def main():
         }
         if ms["cpu"]:
             secondary["ms1024"]["cpu_baseline"] = ms["cpu"]
-    if not args.no_partitioned and not args.scale and (world == 1 or backend == "nccl"):
+    mean_ms = 1000.0 * elapsed / args.steps
+
+    def emit():
+        if rank == 0:
+            print(json.dumps(line(main_res, wl, value, mean_ms, achieved, traffic, tts_s, tts_phases, cpu, secondary,
+                                  n_vertices, nnz, t_kernel, world, args)), flush=True)
+
+    force_part = os.environ.get("PJ_BENCH_FORCE_PART") == "1"  # (tests the guard under a gloo rehearsal)
+    if not args.no_partitioned and not args.scale and (world == 1 or backend == "nccl" or force_part):
         # (a gloo rehearsal shares one GPU between ranks; RCCL needs a GPU per rank)
-        pr = run_partitioned(ctx, args, rank, world, barrier)
-        el, _ = max_sum(pr["elapsed"], 0.0)
+        # The partitioned leg is the only one with a data-path collective (libpj's RCCL
+        # group). Guard it: an exception becomes an error entry, and a watchdog on every
+        # rank emits the line without it and ends the process if a collective hangs.
+        import threading
+
+        def on_timeout():
+            secondary["k28_partitioned"] = {"error": f"not finished within {args.part_timeout:.0f} s (watchdog)"}
+            emit()
+            os._exit(0)
+
+        wd = threading.Timer(args.part_timeout, on_timeout)
+        wd.daemon = True
+        wd.start()
+        try:
+            pr = run_partitioned(ctx, args, rank, world, barrier)
+        except Exception as e:  # noqa: BLE001 (reported in the line, not fatal to it)
+            pr = None
+            secondary["k28_partitioned"] = {"error": f"rank {rank}: {type(e).__name__}: {e}"[:300]}
+        # every rank reaches this collective (the watchdog covers a rank stuck in RCCL)
+        el, n_ok = max_sum(pr["elapsed"] if pr else 0.0, 1.0 if pr else 0.0)
+        wd.cancel()
+        if pr is not None and int(round(n_ok)) != world:
+            pr = None
+            secondary["k28_partitioned"] = {"error": f"failed on {world - int(round(n_ok))} rank(s)"}
+    else:
+        pr = None
+    if pr is not None:
         per = el / pr["roots"]
         secondary["k28_partitioned"] = {
             "workload": f"graph500-kronecker-s{args.part_scale}-ef{args.edgefactor}-unit-bfs, 1D vertex "
@@ -365,54 +400,59 @@ def main():
             "build_s": round(pr["build_s"], 2), "scaling": "strong (one graph, all ranks)",
         }
 
-    if rank == 0:
-        mean_ms = 1000.0 * elapsed / args.steps
-        lv = main_res["levels"][r0]
-        out = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "GTEPS",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(mean_ms, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int32",
-            "data": (f"synthetic: Graph500 Kronecker (A,B,C=0.57,0.19,0.19) generated on the device, seed "
-                     f"{args.seed}, both directions" + (", weights 1 + hash mod 255" if wl["weighted"] else "")
-                     if wl["kind"] == "kronecker" else "synthetic web-Google-shaped graph (SNAP file absent)"),
-            "config": {
-                "workload": wl["name"] if not args.scale else f"{wl['name']} (scale override {args.scale})",
-                "n_vertices": n_vertices, "nnz": nnz, "roots_per_rank": args.steps,
-                "parallelism": f"source-sharded x{world} (graph replicated, no data-path collective)",
-            },
-            "gteps_graph500": round(value / 2, 3),
-            "ms_per_sssp": round(mean_ms, 4),
-            "time_to_solution_s": tts_s,
-            "time_to_solution_phases": tts_phases,
-            "scaling_note": ("N>1: the graph is replicated and the roots are sharded (no exchange between GPUs), "
-                             "i.e. ideal weak scaling; the partitioned multi-GPU solve is secondary.k28_partitioned"),
-            "kernel_ms_mean": round(1000.0 * t_kernel / (args.steps * world), 4),
-            "bands_or_levels": lv[0], "relax_launches": lv[3],
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "scope": "one launch = one SSSP solve (every kernel of the solve); bytes = SURVEY.md §8d "
-                         "algorithmic bytes; time = HIP events on libpj's stream; traffic = PMC "
-                         "2*FETCH_SIZE + WRITE_SIZE per solve (profiles/)",
-            },
-            "cpu_baseline": cpu,
-            "secondary": secondary or None,
-        }
-        print(json.dumps(out), flush=True)
+    emit()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def line(main_res, wl, value, mean_ms, achieved, traffic, tts_s, tts_phases, cpu, secondary, n_vertices, nnz,
+         t_kernel, world, args):
+    """The one JSON line of the run (rank 0)."""
+    r0 = main_res["roots"][0]
+    lv = main_res["levels"][r0]
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GTEPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(mean_ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": (f"synthetic: Graph500 Kronecker (A,B,C=0.57,0.19,0.19) generated on the device, seed "
+                 f"{args.seed}, both directions" + (", weights 1 + hash mod 255" if wl["weighted"] else "")
+                 if wl["kind"] == "kronecker" else "synthetic web-Google-shaped graph (SNAP file absent)"),
+        "config": {
+            "workload": wl["name"] if not args.scale else f"{wl['name']} (scale override {args.scale})",
+            "n_vertices": n_vertices, "nnz": nnz, "roots_per_rank": args.steps,
+            "parallelism": f"source-sharded x{world} (graph replicated, no data-path collective)",
+        },
+        "gteps_graph500": round(value / 2, 3),
+        "ms_per_sssp": round(mean_ms, 4),
+        "time_to_solution_s": tts_s,
+        "time_to_solution_phases": tts_phases,
+        "scaling_note": ("N>1: the graph is replicated and the roots are sharded (no exchange between GPUs), "
+                         "i.e. ideal weak scaling; the partitioned multi-GPU solve is secondary.k28_partitioned"),
+        "kernel_ms_mean": round(1000.0 * t_kernel / (args.steps * world), 4),
+        "bands_or_levels": lv[0], "relax_launches": lv[3],
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "scope": "one launch = one SSSP solve (every kernel of the solve); bytes = SURVEY.md §8d "
+                     "algorithmic bytes; time = HIP events on libpj's stream; traffic = PMC "
+                     "2*FETCH_SIZE + WRITE_SIZE per solve (profiles/)",
+        },
+        "cpu_baseline": cpu,
+        "secondary": secondary or None,
+    }
+    return out
 
 
 def run_wg_cli(ctx, args):
