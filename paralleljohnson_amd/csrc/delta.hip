@@ -1049,6 +1049,10 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
 // loads per vertex. Segments longer than V2_DHT go to the hub queue.
 constexpr int V2_DT = DB * 4;     // vertices per dense tile (16 frontier words)
 constexpr u64 V2_DHT = 4096;      // dense mode: longer segments -> hub queue
+#ifndef PJ_V2_DNJ
+#define PJ_V2_DNJ 4
+#endif
+constexpr int V2_DNJ = PJ_V2_DNJ; // dense mode: independent edges per thread per relax step
 template <typename Off>
 struct V2Dense {
     Off b[V2_DT];                 // segment begin (edge index into lcw, or cw in the tail)
@@ -1171,19 +1175,19 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
             }
         const u32 ns = (u32)(tot >> V2_EB), te = (u32)(tot & mask);
         __syncthreads();
-        for (u32 e0 = 0; e0 < te; e0 += DB * 4) {
-            u64 idx[4];
-            int32_t dj[4];
-            bool val[4];
+        for (u32 e0 = 0; e0 < te; e0 += DB * V2_DNJ) {
+            u64 idx[V2_DNJ];
+            int32_t dj[V2_DNJ];
+            bool val[V2_DNJ];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < V2_DNJ; ++j) {
                 const u32 x = e0 + (u32)j * DB + (u32)tid;
                 val[j] = x < te;
                 const u32 sl = val[j] ? v2_dense_find(sh.off, ns, x) : 0u;
                 idx[j] = val[j] ? (u64)sh.b[sl] + (x - sh.off[sl]) : 0ull;
                 dj[j] = val[j] ? sh.du[sl] : 0;
             }
-            newc += v2_relax_g<true, 4>(a, ed, idx, dj, val, fout, fe);
+            newc += v2_relax_g<true, V2_DNJ>(a, ed, idx, dj, val, fout, fe);
         }
         __syncthreads();
     }
@@ -1620,9 +1624,15 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             if (act) {
                 d0 = a.dist[v];
                 cur = d0;
-                k = (Off)a.lrow[v];
-                ls = (u32)(a.lrow[v + 1] - a.lrow[v]);
-                e = ls > V2_PLMAX ? k : k + (Off)ls;  // long rows: v2_pull_long_body
+                if (a.ltail) {  // the tail: the light prefix of the row in the whole CSR, no long-row list
+                    k = row[v];
+                    ls = a.lsplit[v];
+                    e = k + (Off)ls;
+                } else {
+                    k = (Off)a.lrow[v];
+                    ls = (u32)(a.lrow[v + 1] - a.lrow[v]);
+                    e = ls > V2_PLMAX ? k : k + (Off)ls;  // long rows: v2_pull_long_body
+                }
             }
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
             bool go = act && k < lim, done = !act || k >= e;
@@ -1919,8 +1929,8 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     }
     u32 newc = 0;
     u64 fe = 0, mh = 0, ml = 0;
-    if (nlc) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe);
-    if (a.dense_pull) {
+    if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe);
+    if (a.dense_pull && !a.ltail) {
         v2_dense_pull_body<Off>(a, row, fin, fout, newc, fe, mh, ml, lds.pull);
     } else {
         v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml);
@@ -2406,6 +2416,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         const bool can_pull = g.symmetric && g.pull_factor > 0.0;
         bool can_pull_light = g.symmetric && g.light_pull > 0.0;
         bool tail = false;
+        u64 tail_unsettled = 0;
         const int32_t tdelta = (int32_t)std::min(65536.0, g.tail_delta < 0 ? 64.0 * delta : g.tail_delta);
         u64 last_fe = 1;  // light edges of the frontier at the last host sync (round 0: unknown)
         u64 last_cnt = 1; // its vertex count
@@ -2522,9 +2533,13 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 a.lsplit = w.lsplit2.p;
                 a.ltail = 1;
                 bw = tdelta;
-                can_pull_light = false;
+                // light pulls in the tail (tail_pull): rows are scanned in weight order and
+                // stop at the first w with lo + w >= the vertex's distance
+                can_pull_light = can_pull_light && g.tail_pull;
+                tail_unsettled = heavy_left + light_left;
                 if ((long long)tdelta > w.maxw) {
                     heavy_left = 0;  // every edge is light in the tail
+                    light_left = tail_unsettled;
                 } else {
                     PJ_HIP(hipMemsetAsync(&w.ctl.p->dbg[0], 0, sizeof(V2Line), s));
                     v2_heavy_left_k<Off><<<maxgrid, DB, 0, s>>>(row, a.lsplit, R.dist.p, n, hi, &w.ctl.p->dbg[0].v);
@@ -2532,7 +2547,10 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 }
             }
             sync_ctl();
-            if (enter_tail && (long long)tdelta <= w.maxw) heavy_left = w.hctl->dbg[0].v;
+            if (enter_tail && (long long)tdelta <= w.maxw) {
+                heavy_left = w.hctl->dbg[0].v;
+                light_left = tail_unsettled > heavy_left ? tail_unsettled - heavy_left : 0;
+            }
             last_fe = 0;
             for (int i = 0; i < V2_NSH; ++i) last_fe += w.hctl->cnt[cs][i].pad[0];
             last_cnt = slot(cs);
