@@ -1975,16 +1975,22 @@ __device__ __forceinline__ void v2_lput(u64* __restrict__ o, u64 k, u64 x, u32) 
 __device__ __forceinline__ void v2_lput(u32* __restrict__ o, u64 k, u64 x, u32 cb) {
     o[k] = (u32)x | ((u32)(x >> 32) << cb);
 }
+// (the edge records come from cw, or from the relabeled col / w arrays when cw is null)
+__device__ __forceinline__ u64 v2_rec(const u64* __restrict__ cw, const u32* __restrict__ col,
+                                      const u32* __restrict__ wt, u64 k) {
+    return cw ? cw[k] : (u64)col[k] | ((u64)wt[k] << 32);
+}
 template <typename Off, typename OutT>
 __global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restrict__ lsplit, const u64* __restrict__ lrow,
-                               const u64* __restrict__ cw, i64 n, OutT* __restrict__ lcw, u32 cb) {
+                               const u64* __restrict__ cw, const u32* __restrict__ col, const u32* __restrict__ wt,
+                               i64 n, OutT* __restrict__ lcw, u32 cb) {
     const int lane = lane_id();
     for (i64 v0 = ((i64)blockIdx.x * blockDim.x + threadIdx.x) & ~63ll; v0 < n; v0 += (i64)gridDim.x * blockDim.x) {
         const i64 v = v0 + lane;
         const u32 ls = v < n ? lsplit[v] : 0u;
         const bool longp = ls > 64;
         if (v < n && !longp)
-            for (u32 j = 0; j < ls; ++j) v2_lput(lcw, lrow[v] + j, cw[(u64)row[v] + j], cb);
+            for (u32 j = 0; j < ls; ++j) v2_lput(lcw, lrow[v] + j, v2_rec(cw, col, wt, (u64)row[v] + j), cb);
         u64 lm = __ballot(longp);
         while (lm) {
             const int l = __ffsll((long long)lm) - 1;
@@ -1992,7 +1998,7 @@ __global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restric
             const i64 vl = v0 + l;
             const u64 src = (u64)row[vl], dst = lrow[vl];
             const u32 cnt = lsplit[vl];
-            for (u32 j = lane; j < cnt; j += WAVE) v2_lput(lcw, dst + j, cw[src + j], cb);
+            for (u32 j = lane; j < cnt; j += WAVE) v2_lput(lcw, dst + j, v2_rec(cw, col, wt, src + j), cb);
         }
     }
 }
@@ -2099,6 +2105,31 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         const double d = 3.5 * g.mean_weight / std::max(1.0, mean_deg);
         delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(d)));
     }
+    if (w.maxw < 0) {  // largest weight: decides whether the tail has heavy edges at all
+        u32 h = 0;
+        if (g.nnz > 0) {
+            DevBuf<u32> m(1);
+            PJ_HIP(hipMemsetAsync(m.p, 0, sizeof(u32), s));
+            v2_wmax_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.w.p, g.nnz, m.p);
+            PJ_LAUNCH_CHECK();
+            PJ_HIP(hipMemcpyAsync(&h, m.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipStreamSynchronize(s));
+        }
+        w.maxw = (long long)h;
+    }
+    if (g.split_w && w.maxw <= 255 && !w.w8.p && g.nnz > 0) {  // u8 weights beside the ids
+        w.w8.alloc((size_t)g.nnz);
+        v2_w8_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.w.p, g.nnz, w.w8.p);
+        PJ_LAUNCH_CHECK();
+    }
+    // whole-CSR records: u32 ids + u8 weights (split) when every weight fits 8 bits,
+    // else the interleaved u64 copy
+    const bool split = g.split_w && w.maxw <= 255;
+    if (!split && !w.cw.p && g.nnz > 0) {
+        w.cw.alloc((size_t)g.nnz);
+        v2_interleave_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.col.p, R.w.p, g.nnz, w.cw.p);
+        PJ_LAUNCH_CHECK();
+    }
     if ((w.lsplit_delta != (u32)delta || w.packed_for != g.light_pack) && n > 0) {
         w.packed_for = g.light_pack;
         light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)delta, w.lsplit.p);
@@ -2118,12 +2149,7 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         PJ_LAUNCH_CHECK();
         PJ_HIP(hipMemcpyAsync(&w.nlc, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
         PJ_HIP(hipStreamSynchronize(s));
-        // interleaved edges (once) and the light CSR of this delta
-        if (!w.cw.p && g.nnz > 0) {
-            w.cw.alloc((size_t)g.nnz);
-            v2_interleave_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.col.p, R.w.p, g.nnz, w.cw.p);
-            PJ_LAUNCH_CHECK();
-        }
+        // the light CSR of this delta
         w.hl.alloc((size_t)(n + 63) / 64);
         v2_haslight_k<<<grid_for(n, 256, maxgrid), 256, 0, s>>>(w.lsplit.p, n, w.hl.p);
         PJ_LAUNCH_CHECK();
@@ -2139,13 +2165,13 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         if (w.lcb) {
             w.lcw32.alloc(std::max<u64>(light, 1));
             if (light)
-                v2_light_csr_k<Off, u32><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, n,
-                                                                                   w.lcw32.p, w.lcb);
+                v2_light_csr_k<Off, u32><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, R.col.p,
+                                                                                   R.w.p, n, w.lcw32.p, w.lcb);
         } else {
             w.lcw.alloc(std::max<u64>(light, 1));
             if (light)
-                v2_light_csr_k<Off, u64><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, n,
-                                                                                   w.lcw.p, 0u);
+                v2_light_csr_k<Off, u64><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, R.col.p,
+                                                                                   R.w.p, n, w.lcw.p, 0u);
         }
         PJ_LAUNCH_CHECK();
         w.lcv.alloc(std::max<u64>(w.nlc, 1));
@@ -2156,23 +2182,6 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
             PJ_LAUNCH_CHECK();
         }
         PJ_HIP(hipStreamSynchronize(s));
-    }
-    if (w.maxw < 0) {  // largest weight: decides whether the tail has heavy edges at all
-        u32 h = 0;
-        if (g.nnz > 0) {
-            DevBuf<u32> m(1);
-            PJ_HIP(hipMemsetAsync(m.p, 0, sizeof(u32), s));
-            v2_wmax_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.w.p, g.nnz, m.p);
-            PJ_LAUNCH_CHECK();
-            PJ_HIP(hipMemcpyAsync(&h, m.p, sizeof(u32), hipMemcpyDeviceToHost, s));
-            PJ_HIP(hipStreamSynchronize(s));
-        }
-        w.maxw = (long long)h;
-    }
-    if (g.split_w && w.maxw <= 255 && !w.w8.p && g.nnz > 0) {  // u8 weights beside the ids
-        w.w8.alloc((size_t)g.nnz);
-        v2_w8_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.w.p, g.nnz, w.w8.p);
-        PJ_LAUNCH_CHECK();
     }
     return delta;
 }

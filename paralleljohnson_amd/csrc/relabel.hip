@@ -26,7 +26,7 @@ __global__ void degree_k(const Off* __restrict__ row, i64 n, u32* __restrict__ d
 // touched[v] = 1 if v is the target of an edge (idempotent plain stores)
 __global__ void mark_targets_k(const u32* __restrict__ col, i64 nnz, uint8_t* __restrict__ touched) {
     for (i64 e = (i64)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (i64)gridDim.x * blockDim.x)
-        touched[col[e]] = 1;
+        if (!touched[col[e]]) touched[col[e]] = 1;  // (most targets repeat: skip the store)
 }
 
 __global__ void max_u32_k(const u32* __restrict__ in, i64 n, u32* __restrict__ out) {
@@ -70,6 +70,8 @@ __global__ __launch_bounds__(256) void copy_rows_k(const u32* __restrict__ perm,
                                                    const Off* __restrict__ orow, const u32* __restrict__ ocol,
                                                    const u32* __restrict__ ow, const Off* __restrict__ nrow,
                                                    u32* __restrict__ ncol, u32* __restrict__ nw, i64 nrows) {
+    // (bound by the random id lookups inv[ocol[k]]: a lane-per-row and an
+    // edge-parallel form over 64 rows per wave measured no faster, 50-56 ms at s26)
     const i64 nwaves = (i64)gridDim.x * (blockDim.x / WAVE);
     for (i64 i = (i64)blockIdx.x * (blockDim.x / WAVE) + wave_id(); i < nrows; i += nwaves) {
         const u32 o = perm[i];
@@ -95,7 +97,9 @@ void build(Graph& g) {
     PJ_HIP(hipMemsetAsync(touched.p, 0, (size_t)n + 1, s));
     PJ_HIP(hipMemsetAsync(scal.p, 0, 2 * sizeof(u32), s));
     degree_k<Off><<<grid_for(n, 256, grid), 256, 0, s>>>(orow, n, deg.p);
-    if (nnz) mark_targets_k<<<grid_for(nnz, 256, grid), 256, 0, s>>>(g.col.p, nnz, touched.p);
+    // vertices that are only targets also get an id below n_scan; a symmetric graph has
+    // none (every target has the reverse edge), so the random byte stores are skipped
+    if (nnz && !g.symmetric) mark_targets_k<<<grid_for(nnz, 256, grid), 256, 0, s>>>(g.col.p, nnz, touched.p);
     max_u32_k<<<grid_for(n, 256, grid), 256, 0, s>>>(deg.p, n, scal.p);
     PJ_LAUNCH_CHECK();
     u32 h[2] = {0, 0};
