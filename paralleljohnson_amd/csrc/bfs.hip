@@ -1086,6 +1086,10 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
         // first batch: the previous solve's launches, so a repeated solve on the same graph
         // usually needs one host check and no idle launch behind the last level
         int batch = g.level_batch > 0 ? g.level_batch : std::max(2, w.last_launches);
+        // a solve that outlasts the first batch usually needs one or two more levels:
+        // continue with 2, 4, 8, ... (doubling the first batch put up to a whole batch
+        // of idle ~7 us launches inside the timed region: K22, 14 behind an 8-level solve)
+        int next = 2;
         for (;;) {
             for (int i = 0; i < batch && li < INT_INF; ++i, ++li) {
                 if (g.symmetric) bfs_level_k<Off, true><<<grid, TB, 0, s>>>(a, gd, li);
@@ -1097,7 +1101,8 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
             PJ_HIP(hipEventRecord(g.ev1, s));
             PJ_HIP(hipStreamSynchronize(s));
             if (*(volatile int64_t*)w.host >= 0 || li >= INT_INF) break;
-            batch = batch < 1024 ? batch * 2 : batch;
+            batch = g.level_batch > 0 ? batch : next;
+            next = next < 1024 ? next * 2 : next;
         }
         st.levels = *(volatile int64_t*)w.host;
         w.last_launches = (int32_t)((volatile int64_t*)w.host)[3];

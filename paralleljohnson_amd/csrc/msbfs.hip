@@ -379,6 +379,7 @@ struct MsWork {
     DevBuf<int64_t> src;
     DevBuf<MsCtl> ctl;
     int64_t* host = nullptr;
+    int32_t last_levels = 0;  // level iterations the previous pass used: sizes the first batch
     ~MsWork() {
         if (host) (void)hipHostFree(host);
     }
@@ -414,7 +415,10 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double*
     ms_sources_k<Off><<<(ns + 255) / 256, 256, 0, s>>>(w.src.p, ns, W, n, row, w.V.p, w.F.p, w.dist.p, w.ctl.p);
     PJ_LAUNCH_CHECK();
     int32_t L = 0;
-    int batch = 16;
+    // first batch: the previous pass's levels (passes over one graph need about as many);
+    // then 2, 4, 8, ... (each idle level costs its 2-4 launches inside the timed region)
+    int batch = w.last_levels > 0 ? w.last_levels : 16;
+    int next = 2;
     u64* F = w.F.p;
     u64* Fn = w.Fn.p;
     for (;;) {
@@ -434,7 +438,8 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double*
         }
         PJ_HIP(hipStreamSynchronize(s));
         if (*(volatile int64_t*)w.host >= 0 || L >= INT_INF || !any) break;
-        batch = batch < 1024 ? batch * 2 : batch;
+        batch = next;
+        next = next < 1024 ? next * 2 : next;
     }
     PJ_HIP(hipEventRecord(g.ev1, s));
     PJ_HIP(hipEventSynchronize(g.ev1));
@@ -442,6 +447,7 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double*
     PJ_HIP(hipEventElapsedTime(&ms, g.ev0, g.ev1));
     *kernel_ms += ms;
     const i64 lv = (i64)*(volatile int64_t*)w.host;
+    if (any && lv >= 0) w.last_levels = (int32_t)lv + 1;
     *levels = std::max<i64>(*levels, lv);
 }
 
