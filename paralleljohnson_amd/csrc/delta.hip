@@ -2063,6 +2063,9 @@ struct DeltaWork {
     DevBuf<V2Ctl> ctl;
     V2Ctl* hctl = nullptr;  // mapped pinned host copy, written by v2_publish_k
     V2Ctl* hctl_dev = nullptr;
+    u64* hseq = nullptr;    // mapped pinned sequence word of v2_publish_k
+    u64* hseq_dev = nullptr;
+    u64 seq = 0;
     DevBuf<u32> hv;
     DevBuf<u64> hbeg, hoff;
     u64 hcap = 0;
@@ -2079,6 +2082,7 @@ struct DeltaWork {
     ~DeltaWork() {
         if (host) (void)hipHostFree(host);
         if (hctl) (void)hipHostFree(hctl);
+        if (hseq) (void)hipHostFree(hseq);
     }
 };
 
@@ -2336,8 +2340,16 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
     g.have_result = true;
 }
 
-__global__ __launch_bounds__(256) void v2_publish_k(const u64* __restrict__ ctl, u64* __restrict__ host, int nw) {
+// copies the counter block to mapped host memory, then (system-scope release) the
+// sequence number the host spins on
+__global__ __launch_bounds__(256) void v2_publish_k(const u64* __restrict__ ctl, u64* __restrict__ host, int nw,
+                                                    u64* seqp, u64 seq) {
     for (int i = threadIdx.x; i < nw; i += 256) host[i] = ctl[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(seqp, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 template <typename Off>
@@ -2366,6 +2378,10 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         w.hoff.alloc(3 * w.hcap);
         PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.hctl), sizeof(V2Ctl), hipHostMallocMapped));
         PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&w.hctl_dev), w.hctl, 0));
+        PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.hseq), 64, hipHostMallocMapped | hipHostMallocCoherent));
+        PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&w.hseq_dev), w.hseq, 0));
+        *w.hseq = 0;
+        w.seq = 0;
     }
     V2Args a{};
     a.n = n;
@@ -2391,11 +2407,25 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     a.hcap = w.hcap;
     // the host's view of the counters: one block copies them into mapped host memory
     // (a D2H hipMemcpyAsync of the same 3.3 KB ran as a ~30 us blit per sync)
+    // The host spins on the sequence number (wakes within ~1 us of the copy instead of
+    // the stream synchronization's latency); after 0.2 s of spinning it synchronizes the
+    // stream, which surfaces a failed kernel instead of spinning forever.
     auto sync_ctl = [&]() {
+        const u64 seq = ++w.seq;
         v2_publish_k<<<1, 256, 0, s>>>(reinterpret_cast<const u64*>(w.ctl.p), reinterpret_cast<u64*>(w.hctl_dev),
-                                       sizeof(V2Ctl) / sizeof(u64));
+                                       sizeof(V2Ctl) / sizeof(u64), w.hseq_dev, seq);
         PJ_LAUNCH_CHECK();
-        PJ_HIP(hipStreamSynchronize(s));
+        if (g.spin_sync) {
+            const auto t0 = std::chrono::steady_clock::now();
+            while (__atomic_load_n(w.hseq, __ATOMIC_ACQUIRE) != seq) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                    PJ_HIP(hipStreamSynchronize(s));
+                    break;
+                }
+            }
+        } else {
+            PJ_HIP(hipStreamSynchronize(s));
+        }
     };
     auto slot = [&](int c) {
         u64 t = 0;
