@@ -636,7 +636,6 @@ struct ESrc {
     u32 cb;
     const uint8_t* w8;
 };
-__device__ __forceinline__ u64 eat(const u64* __restrict__ p, u64 k) { return p[k]; }
 __device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
     if (s.w8) return (u64)s.e32[k] | ((u64)s.w8[k] << 32);
     if (s.e32) {
@@ -2023,11 +2022,6 @@ __global__ void v2_wmax_k(const u32* __restrict__ w, i64 m, u32* __restrict__ ou
     if (lane_id() == 0 && x) atomicMax(out, x);
 }
 
-__global__ void v2_source_k(V2Args a, i64 s, u64* __restrict__ f, int cin) {
-    a.dist[s] = 0;
-    f[s >> 6] = 1ull << (s & 63);
-    a.ctl->cnt[cin][0].v = 1;
-}
 
 // hl bit v = (lsplit[v] > 0): the vertices that have light edges for this delta
 __global__ void v2_haslight_k(const u32* __restrict__ lsplit, i64 n, u64* __restrict__ hl) {
@@ -2341,14 +2335,45 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
 }
 
 // copies the counter block to mapped host memory, then (system-scope release) the
-// sequence number the host spins on
-__global__ __launch_bounds__(256) void v2_publish_k(const u64* __restrict__ ctl, u64* __restrict__ host, int nw,
-                                                    u64* seqp, u64 seq) {
-    for (int i = threadIdx.x; i < nw; i += 256) host[i] = ctl[i];
+// sequence number the host spins on; then resets the counters the host consumes
+// per check (the members' degree sums mh, which the host accumulates over a band's
+// checks, and minv), so no memset launch precedes the next band or heavy step
+__global__ __launch_bounds__(256) void v2_publish_k(V2Ctl* __restrict__ ctl, u64* __restrict__ host, u64* seqp,
+                                                    u64 seq) {
+    const u64* c = reinterpret_cast<const u64*>(ctl);
+    constexpr int nw = sizeof(V2Ctl) / sizeof(u64);
+    for (int i = threadIdx.x; i < nw; i += 256) host[i] = c[i];
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence_system();
         __hip_atomic_store(seqp, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (threadIdx.x < V2_NSH) {
+        ctl->mh[threadIdx.x].v = 0;
+        ctl->mh[threadIdx.x].pad[0] = 0;
+    }
+    if (threadIdx.x == 0) ctl->minv.v = ~0ull;
+}
+
+// solve start in one launch: dist := INF (the source 0), frontier 0 := {source},
+// frontier 1 and the member bitmap := 0, counters := 0 with the source counted
+__global__ void v2_init_k(int32_t* __restrict__ dist, i64 n, i64 nwords, i64 src, u64* __restrict__ f0,
+                          u64* __restrict__ f1, u64* __restrict__ mb, V2Ctl* __restrict__ ctl) {
+    const i64 stride = (i64)gridDim.x * blockDim.x;
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += stride) dist[v] = v == src ? 0 : INT_INF;
+    for (i64 wi = (i64)blockIdx.x * blockDim.x + threadIdx.x; wi < nwords; wi += stride) {
+        f0[wi] = (src >= 0 && wi == (src >> 6)) ? 1ull << (src & 63) : 0ull;
+        f1[wi] = 0;
+        mb[wi] = 0;
+    }
+    if (blockIdx.x == 0) {
+        u64* c = reinterpret_cast<u64*>(ctl);
+        for (int i = threadIdx.x; i < (int)(sizeof(V2Ctl) / sizeof(u64)); i += blockDim.x) c[i] = 0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            ctl->minv.v = ~0ull;
+            if (src >= 0) ctl->cnt[0][0].v = 1;
+        }
     }
 }
 
@@ -2412,8 +2437,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     // stream, which surfaces a failed kernel instead of spinning forever.
     auto sync_ctl = [&]() {
         const u64 seq = ++w.seq;
-        v2_publish_k<<<1, 256, 0, s>>>(reinterpret_cast<const u64*>(w.ctl.p), reinterpret_cast<u64*>(w.hctl_dev),
-                                       sizeof(V2Ctl) / sizeof(u64), w.hseq_dev, seq);
+        v2_publish_k<<<1, 256, 0, s>>>(w.ctl.p, reinterpret_cast<u64*>(w.hctl_dev), w.hseq_dev, seq);
         PJ_LAUNCH_CHECK();
         if (g.spin_sync) {
             const auto t0 = std::chrono::steady_clock::now();
@@ -2432,7 +2456,6 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         for (int i = 0; i < V2_NSH; ++i) t += w.hctl->cnt[c][i].v;
         return t;
     };
-    auto reset_minv = [&]() { PJ_HIP(hipMemsetAsync(&w.ctl.p->minv, 0xFF, sizeof(V2Line), s)); };
 
     pj_stats st{};
     const bool valid = source >= 0 && source < g.n;
@@ -2440,16 +2463,12 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     auto t_host0 = std::chrono::steady_clock::now();
     PJ_HIP(hipEventRecord(g.ev0, s));
     if (n > 0) {
-        PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(R.dist.p), INT_INF, (size_t)n, s));
-        PJ_HIP(hipMemsetAsync(w.f[0].p, 0, sizeof(u64) * (size_t)nwords, s));
-        PJ_HIP(hipMemsetAsync(w.f[1].p, 0, sizeof(u64) * (size_t)nwords, s));
-        PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
-        PJ_HIP(hipMemsetAsync(w.ctl.p, 0, sizeof(V2Ctl), s));
+        v2_init_k<<<grid_for(n, 256, maxgrid), 256, 0, s>>>(R.dist.p, n, nwords, (valid && ls < n) ? ls : -1,
+                                                            w.f[0].p, w.f[1].p, w.mb.p, w.ctl.p);
+        PJ_LAUNCH_CHECK();
     }
     if (valid && ls < n) {
         int cs = 0, hr = 0, fi = 0;
-        v2_source_k<<<1, 1, 0, s>>>(a, ls, w.f[fi].p, cs);
-        PJ_LAUNCH_CHECK();
         long long lo = 0;
         u64 heavy_left = w.heavy_total, light_left = w.light_total;
         const bool can_pull = g.symmetric && g.pull_factor > 0.0;
@@ -2464,7 +2483,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             a.lo = (int32_t)lo;
             a.hi = hi;
             st.levels++;
-            PJ_HIP(hipMemsetAsync(w.ctl.p->mh, 0, sizeof(w.ctl.p->mh), s));
+            u64 mh = 0, ml = 0;  // members' heavy / light degree sums (reset by every publish)
             // light rounds until the band's frontier is empty
             // light rounds launched per host check: round_batch, doubling (starting
             // each band at the previous band's round count, or at 4 or 8, measured slower:
@@ -2499,6 +2518,10 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                     st.relax_rounds++;
                 }
                 sync_ctl();
+                for (int i = 0; i < V2_NSH; ++i) {
+                    mh += w.hctl->mh[i].v;
+                    ml += w.hctl->mh[i].pad[0];
+                }
                 last_fe = 0;
                 for (int i = 0; i < V2_NSH; ++i) last_fe += w.hctl->cnt[cs][i].pad[0];
                 last_cnt = slot(cs);
@@ -2511,14 +2534,8 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 if (slot(cs) == 0) break;
                 K = PJ_V2_STATS ? 1 : std::min(2 * K, 16);
             }
-            u64 mh = 0, ml = 0;
-            for (int i = 0; i < V2_NSH; ++i) {
-                mh += w.hctl->mh[i].v;
-                ml += w.hctl->mh[i].pad[0];
-            }
             heavy_left = heavy_left > mh ? heavy_left - mh : 0;
             light_left = light_left > ml ? light_left - ml : 0;
-            reset_minv();
             // Tail: past the dense first bands the remaining rows are short and the
             // bands sparse, so wide bands (few band steps) pay off. Once the edges of
             // the unsettled vertices drop below tail_frac x nnz, the bands after this
@@ -2599,7 +2616,6 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 lo = (long long)mv / bw * bw;  // jump to the next occupied band
                 a.lo = (int32_t)lo;
                 a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
-                reset_minv();
                 v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
                 PJ_LAUNCH_CHECK();
                 continue;
