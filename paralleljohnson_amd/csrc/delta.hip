@@ -1194,26 +1194,44 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
 
 // LIGHT: relax the light prefixes of fin's vertices (a band round); HEAVY: the
 // heavy segments of fin = mb (push heavy step). fin words are cleared as read.
+// Light rounds use a ring of three frontier bitmaps: round r reads f[r], writes
+// f[r+1] and clears f[r+2] (read by round r-1, written by nobody until round r+1),
+// so a pull round, whose probes read its input from every wave, never has to clear it.
+__device__ __forceinline__ void v2_clear_words(u64* __restrict__ f, i64 nwords) {
+    if (f)
+        for (i64 wi = (i64)blockIdx.x * DB + threadIdx.x; wi < nwords; wi += (i64)gridDim.x * DB) f[wi] = 0;
+}
+__device__ __forceinline__ void v2_zero_slot(const V2Args& a, int c) {
+    if (blockIdx.x == 0 && threadIdx.x < V2_NSH) {
+        a.ctl->cnt[c][threadIdx.x].v = 0;
+        a.ctl->cnt[c][threadIdx.x].pad[0] = 0;
+    }
+}
+
+template <typename Off, bool LIGHT>
+__device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __restrict__ row, u64* __restrict__ fin,
+                                               u64* __restrict__ fout, int cin, int hs, u64* red);
+
 template <typename Off, bool LIGHT>
 __global__ __launch_bounds__(DB) void v2_expand_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
                                                   u64* __restrict__ fout, int cin, int hs, u64 pull_thresh,
-                                                  u64 dense_min) {
+                                                  u64 dense_min, u64* __restrict__ fclr) {
     constexpr int NWV = DB / WAVE;
     __shared__ u64 red[NWV];
     if (LIGHT) {
-        if (blockIdx.x == 0 && threadIdx.x < V2_NSH) {
-            a.ctl->cnt[(cin + 2) & 3][threadIdx.x].v = 0;
-            a.ctl->cnt[(cin + 2) & 3][threadIdx.x].pad[0] = 0;
-        }
+        v2_zero_slot(a, (cin + 2) & 3);
+        v2_clear_words(fclr, a.nwords);
         if (v2_slot_sum(a.ctl->cnt[cin]) == 0) return;  // empty frontier (block-uniform)
-        if (v2_slot_edges(a.ctl->cnt[cin]) > pull_thresh) {
-            // v2_pull_round_k relaxed this round; it could not clear fin (other waves
-            // were reading it), so clear it here
-            for (i64 wi = (i64)blockIdx.x * DB + threadIdx.x; wi < a.nwords; wi += (i64)gridDim.x * DB) fin[wi] = 0;
-            return;
-        }
+        if (v2_slot_edges(a.ctl->cnt[cin]) > pull_thresh) return;  // v2_pull_round_k pulled this round
         if (v2_slot_sum(a.ctl->cnt[cin]) > dense_min) return;  // v2_pull_round_k ran it tile-dense
     }
+    v2_expand_body<Off, LIGHT>(a, row, fin, fout, cin, hs, red);
+}
+
+template <typename Off, bool LIGHT>
+__device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __restrict__ row, u64* __restrict__ fin,
+                                               u64* __restrict__ fout, int cin, int hs, u64* red) {
+    constexpr int NWV = DB / WAVE;
     const int lane = lane_id();
     const u64 mask = (1ull << V2_EB) - 1ull;
     u32 newc = 0;
@@ -1910,15 +1928,22 @@ template <typename Off>
 __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
                                                       u64* __restrict__ fout, int cin, u64 pull_thresh,
                                                       const u32* __restrict__ lcv, const u32* __restrict__ lcc, u64 nlc,
-                                                      int hs, u64 dense_min) {
+                                                      int hs, u64 dense_min, u64* __restrict__ fclr, int merged) {
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
     __shared__ u64 red[NWV];
     __shared__ V2RoundLds<Off> lds;
+    if (merged) {  // the whole round in this launch: no v2_expand_k behind it
+        v2_zero_slot(a, (cin + 2) & 3);
+        v2_clear_words(fclr, a.nwords);
+    }
     const u64 fcount = v2_slot_sum(a.ctl->cnt[cin]);
     if (fcount == 0) return;
     if (v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) {
-        if (fcount <= dense_min) return;  // a sparse push round: v2_expand_k
+        if (fcount <= dense_min) {  // a sparse push round
+            if (merged) v2_expand_body<Off, true>(a, row, fin, fout, cin, hs, red);
+            return;  // (else v2_expand_k)
+        }
         u32 newc = 0;
         u64 mh = 0, ml = 0, fe = 0;
         v2_dense_body<Off>(a, row, fin, fout, hs, newc, fe, mh, ml, lds.push);
@@ -2053,7 +2078,7 @@ struct DeltaWork {
     u64 heavy_total = 0;   // edges with w >= delta (for the pull decision)
     u64 light_total = 0;   // edges with w < delta
     // v2 band loop
-    DevBuf<u64> f[2], mb;
+    DevBuf<u64> f[3], mb;   // light-round frontier ring (v2_clear_words), band members
     DevBuf<V2Ctl> ctl;
     V2Ctl* hctl = nullptr;  // mapped pinned host copy, written by v2_publish_k
     V2Ctl* hctl_dev = nullptr;
@@ -2395,6 +2420,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         const size_t nw = nwords ? (size_t)nwords : 1;
         w.f[0].alloc(nw);
         w.f[1].alloc(nw);
+        w.f[2].alloc(nw);
         w.mb.alloc(nw);
         w.ctl.alloc(1);
         w.hcap = (u64)std::max<i64>(1, std::min<i64>(n, g.nnz / (i64)V2_HT + 1));
@@ -2495,24 +2521,36 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 // when the last frontier seen could grow past the threshold in this batch
                 const bool try_pull = can_pull_light && (double)last_fe * g.pull_grow > (double)pull_thresh;
                 for (int q = 0; q < K; ++q) {
-                    // the round kernel also runs dense push rounds (v2_dense_body): whenever it
-                    // is launched for pulls, else for the first round of a batch whose last
-                    // seen frontier was dense
-                    const bool try_dense = dense_min != ~0ull && (try_pull || (q == 0 && last_cnt > dense_min));
-                    const u64 dmin = try_dense ? dense_min : ~0ull;
-                    if (try_pull || try_dense) {
-                        v2_pull_round_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs,
-                                                                    try_pull ? pull_thresh : ~0ull, w.lcv.p, w.lcc.p,
-                                                                    w.nlc, hr, dmin);
+                    u64* fin = w.f[fi].p;
+                    u64* fout = w.f[(fi + 1) % 3].p;
+                    u64* fclr = w.f[(fi + 2) % 3].p;
+                    if (g.merged_round) {
+                        // one launch decides pull / tile-dense push / sparse push on the device
+                        v2_pull_round_k<Off><<<pullgrid, DB, 0, s>>>(a, row, fin, fout, cs,
+                                                                    can_pull_light ? pull_thresh : ~0ull, w.lcv.p,
+                                                                    w.lcc.p, w.nlc, hr, dense_min, fclr, 1);
+                        PJ_LAUNCH_CHECK();
+                    } else {
+                        // the round kernel also runs dense push rounds (v2_dense_body): whenever it
+                        // is launched for pulls, else for the first round of a batch whose last
+                        // seen frontier was dense
+                        const bool try_dense =
+                            dense_min != ~0ull && (try_pull || (q == 0 && last_cnt > dense_min));
+                        const u64 dmin = try_dense ? dense_min : ~0ull;
+                        if (try_pull || try_dense) {
+                            v2_pull_round_k<Off><<<pullgrid, DB, 0, s>>>(a, row, fin, fout, cs,
+                                                                        try_pull ? pull_thresh : ~0ull, w.lcv.p,
+                                                                        w.lcc.p, w.nlc, hr, dmin, nullptr, 0);
+                            PJ_LAUNCH_CHECK();
+                        }
+                        // (without the round kernel the expand must push every round)
+                        v2_expand_k<Off, true><<<maxgrid, DB, 0, s>>>(a, row, fin, fout, cs, hr,
+                                                                      try_pull ? pull_thresh : ~0ull, dmin, fclr);
                         PJ_LAUNCH_CHECK();
                     }
-                    // (without the round kernel the expand must push every round)
-                    v2_expand_k<Off, true><<<maxgrid, DB, 0, s>>>(a, row, w.f[fi].p, w.f[1 - fi].p, cs, hr,
-                                                                  try_pull ? pull_thresh : ~0ull, dmin);
+                    v2_hub_k<true><<<maxgrid, DB, 0, s>>>(a, fout, cs, hr, (hr + 1) % 3);
                     PJ_LAUNCH_CHECK();
-                    v2_hub_k<true><<<maxgrid, DB, 0, s>>>(a, w.f[1 - fi].p, cs, hr, (hr + 1) % 3);
-                    PJ_LAUNCH_CHECK();
-                    fi ^= 1;
+                    fi = (fi + 1) % 3;
                     cs = (cs + 1) & 3;
                     hr = (hr + 1) % 3;
                     st.relax_rounds++;
@@ -2567,7 +2605,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 st.bu_levels++;
             } else {
                 if (mh > 0) {
-                    v2_expand_k<Off, false><<<maxgrid, DB, 0, s>>>(a, row, w.mb.p, nullptr, cs, hr, ~0ull, ~0ull);
+                    v2_expand_k<Off, false><<<maxgrid, DB, 0, s>>>(a, row, w.mb.p, nullptr, cs, hr, ~0ull, ~0ull, nullptr);
                     PJ_LAUNCH_CHECK();
                     v2_hub_k<false><<<maxgrid, DB, 0, s>>>(a, nullptr, cs, hr, (hr + 1) % 3);
                     PJ_LAUNCH_CHECK();

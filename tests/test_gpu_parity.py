@@ -228,8 +228,8 @@ def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
         col = col.astype(np.uint32)
         roots = [0] + [int(r) for r in g.sample_roots(4, 2)]
         exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
-        for dense, dp, pk, tp in ((0.0, 0, 0, 0), (1e-12, 1, 1, 1), (0.02, 0, 1, 1), (0.02, 1, 0, 0), (0.1, 1, 1, 0),
-                                  (0.1, 0, 2, 1)):
+        for dense, dp, pk, tp, mr in ((0.0, 0, 0, 0, 0), (1e-12, 1, 1, 1, 1), (0.02, 0, 1, 1, 0), (0.02, 1, 0, 0, 1),
+                                      (0.1, 1, 1, 0, 0), (0.1, 0, 2, 1, 1), (0.0, 0, 1, 0, 1)):
             for lf in (0, 1):
                 for lp, tf in ((2.0, 0.1), (0.0, 0.1), (2.0, 0.0), (1e15, 0.1)):
                     g.set_option("dense_frac", dense)
@@ -237,13 +237,14 @@ def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
                     g.set_option("light_pack", min(pk, 1))
                     g.set_option("split_w", int(pk != 2))
                     g.set_option("tail_pull", tp)
+                    g.set_option("merged_round", mr)
                     g.set_option("light_filter", lf)
                     g.set_option("light_pull", lp)
                     g.set_option("tail_frac", tf)
                     for delta in (0, 40):
                         g.set_option("delta", delta)
                         for r in roots:
-                            assert (g.sssp(r) == exp[r]).all(), (name, dense, dp, pk, tp, lf, lp, tf, delta, r)
+                            assert (g.sssp(r) == exp[r]).all(), (name, dense, dp, pk, tp, mr, lf, lp, tf, delta, r)
         g.close()
 
 
