@@ -2412,6 +2412,10 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     const Off* row = static_cast<const Off*>(R.row_ptr(g.off64));
     const unsigned maxgrid = (unsigned)ctx.cu_count * (unsigned)PJ_V2_GPC;  // workgroups per CU of the v2 kernels (grid-stride)
     const unsigned pullgrid = (unsigned)ctx.cu_count * (unsigned)PJ_V2_GPC_PULL;
+    // light-round grids (grid-stride kernels): a launch that finds its round empty costs
+    // in proportion to its workgroups, so these may be sized to the resident capacity
+    const unsigned roundgrid = g.round_gpc > 0 ? (unsigned)ctx.cu_count * (unsigned)g.round_gpc : pullgrid;
+    const unsigned hubgrid = g.hub_gpc > 0 ? (unsigned)ctx.cu_count * (unsigned)g.hub_gpc : maxgrid;
     const int32_t delta = prepare_delta<Off>(g, w);
     // band width: at most the light threshold (an edge that can stay inside its
     // band must be light, so the band's light rounds see it)
@@ -2526,8 +2530,8 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                     u64* fclr = w.f[(fi + 2) % 3].p;
                     if (g.merged_round) {
                         // one launch decides pull / tile-dense push / sparse push on the device
-                        v2_pull_round_k<Off><<<pullgrid, DB, 0, s>>>(a, row, fin, fout, cs,
-                                                                    can_pull_light ? pull_thresh : ~0ull, w.lcv.p,
+                        v2_pull_round_k<Off><<<roundgrid, DB, 0, s>>>(a, row, fin, fout, cs,
+                                                                     can_pull_light ? pull_thresh : ~0ull, w.lcv.p,
                                                                     w.lcc.p, w.nlc, hr, dense_min, fclr, 1);
                         PJ_LAUNCH_CHECK();
                     } else {
@@ -2548,7 +2552,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                                                                       try_pull ? pull_thresh : ~0ull, dmin, fclr);
                         PJ_LAUNCH_CHECK();
                     }
-                    v2_hub_k<true><<<maxgrid, DB, 0, s>>>(a, fout, cs, hr, (hr + 1) % 3);
+                    v2_hub_k<true><<<hubgrid, DB, 0, s>>>(a, fout, cs, hr, (hr + 1) % 3);
                     PJ_LAUNCH_CHECK();
                     fi = (fi + 1) % 3;
                     cs = (cs + 1) & 3;
