@@ -16,7 +16,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for p in glob.glob(os.path.join(root, f"pmc_{c}", "*counter_collection.csv")):
         for r in csv.DictReader(open(p)):
             k = r["Kernel_Name"]
-            if "v2_source_k" in k:
+            if "v2_init_k" in k or "v2_source_k" in k:  # one per solve
                 solves += 1
             if any(s in k for s in PATTERNS) and not any(s in k for s in EXCLUDED):
                 tot += float(r["Counter_Value"])
