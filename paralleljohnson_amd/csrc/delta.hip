@@ -2508,12 +2508,22 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         const int32_t tdelta = (int32_t)std::min(65536.0, g.tail_delta < 0 ? 64.0 * delta : g.tail_delta);
         u64 last_fe = 1;  // light edges of the frontier at the last host sync (round 0: unknown)
         u64 last_cnt = 1; // its vertex count
-        while (lo < INT_INF) {
+        // Deferred band check (merged rounds): after a heavy step the host does not wait
+        // for its counters; it enqueues the next band's first rounds at once and learns at
+        // their check whether that band had any vertex (its start slot survives the first
+        // two rounds of the counter ring) and, if not, the next occupied band (minv of the
+        // heavy step, copied by the same publish before it resets minv).
+        const bool defer_ok = g.merged_round && g.defer_check && !PJ_V2_STATS && g.round_batch <= 2;
+        bool deferred = false;
+        bool finished = false;
+        while (lo < INT_INF && !finished) {
             const int32_t hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
             a.lo = (int32_t)lo;
             a.hi = hi;
             st.levels++;
             u64 mh = 0, ml = 0;  // members' heavy / light degree sums (reset by every publish)
+            const int cs_start = cs;
+            bool jumped = false;
             // light rounds until the band's frontier is empty
             // light rounds launched per host check: round_batch, doubling (starting
             // each band at the previous band's round count, or at 4 or 8, measured slower:
@@ -2560,6 +2570,24 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                     st.relax_rounds++;
                 }
                 sync_ctl();
+                if (deferred) {
+                    deferred = false;
+                    if (slot(cs_start) == 0) {  // the band was empty: its rounds were idle
+                        st.levels--;
+                        const u64 mv = w.hctl->minv.v;
+                        if (mv >= (u64)INT_INF) {  // nothing reached beyond the settled bands
+                            finished = true;
+                            break;
+                        }
+                        lo = (long long)mv / bw * bw;  // jump to the next occupied band
+                        a.lo = (int32_t)lo;
+                        a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
+                        v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
+                        PJ_LAUNCH_CHECK();
+                        jumped = true;
+                        break;
+                    }
+                }
                 for (int i = 0; i < V2_NSH; ++i) {
                     mh += w.hctl->mh[i].v;
                     ml += w.hctl->mh[i].pad[0];
@@ -2576,6 +2604,8 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 if (slot(cs) == 0) break;
                 K = PJ_V2_STATS ? 1 : std::min(2 * K, 16);
             }
+            if (finished) break;
+            if (jumped) continue;  // (the select of the jumped-to band is enqueued)
             heavy_left = heavy_left > mh ? heavy_left - mh : 0;
             light_left = light_left > ml ? light_left - ml : 0;
             // Tail: past the dense first bands the remaining rows are short and the
@@ -2643,6 +2673,11 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                     v2_heavy_left_k<Off><<<maxgrid, DB, 0, s>>>(row, a.lsplit, R.dist.p, n, hi, &w.ctl.p->dbg[0].v);
                     PJ_LAUNCH_CHECK();
                 }
+            }
+            if (defer_ok && !(enter_tail && (long long)tdelta <= w.maxw)) {
+                deferred = true;  // checked at the next band's first publish
+                lo = hi;
+                continue;
             }
             sync_ctl();
             if (enter_tail && (long long)tdelta <= w.maxw) {

@@ -211,6 +211,7 @@ struct Graph {
     int tail_pull = 0;
     int spin_sync = 1;
     int merged_round = 1;
+    int defer_check = 1;  // delta v2 (merged rounds): no host check right after a heavy step (0/1)
     int round_gpc = 12;   // delta v2: workgroups per CU of the light-round / hub launches (0 = the heavy
     int hub_gpc = 4;      // kernels' 24); swept (24,24) (6,7) (12,14) (12,7) (12,4) (16,7): (12,4) best // delta v2: one launch per light round decides pull / dense / sparse push (0/1)    // delta v2: the host spins on a published sequence word instead of a stream sync (0/1)    // delta v2: light pull rounds allowed in the tail too (0/1)      // delta v2: whole-CSR reads as u32 ids + u8 weights when every weight <= 255 (0/1)   // delta v2: light CSR records packed in 32 bits when they fit (0/1)   // delta v2: light pull rounds in tile-dense form (0/1) // delta v2: skip vertices without light edges in light rounds (hl bitmap)
     int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)

@@ -238,6 +238,7 @@ def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
                     g.set_option("split_w", int(pk != 2))
                     g.set_option("tail_pull", tp)
                     g.set_option("merged_round", mr)
+                    g.set_option("defer_check", int(dense != 0.02))
                     g.set_option("light_filter", lf)
                     g.set_option("light_pull", lp)
                     g.set_option("tail_frac", tf)
