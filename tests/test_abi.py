@@ -84,3 +84,26 @@ def test_cli_usage_contract(pj):
             "argv[3]---file to save the solution.",
         ]
         assert r.stdout == ""
+
+
+def test_multi_handle_argument_and_device_errors(pj):
+    """pj_multi_* on the host: bad arguments are PJ_ERR_ARG, and without a GPU the n-GPU
+    handle fails loudly (no CPU fallback) instead of returning a handle."""
+    import ctypes
+    lib = ctypes.CDLL(pj.LIB_PATH)
+    h = ctypes.c_void_p()
+    assert lib.pj_multi_create(0, 0, ctypes.byref(h)) == -1  # n_gpus < 1
+    assert lib.pj_multi_create(2, 7, ctypes.byref(h)) == -1  # unknown transport
+    assert lib.pj_multi_create(1, 0, None) == -1
+    assert lib.pj_multi_sssp(None, 0, None, None) == -1
+    assert lib.pj_multi_info(None, None) == -1
+    assert lib.pj_multi_destroy(None) == 0
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    from paralleljohnson_amd.partition import Multi
+    with pytest.raises(pj.PJError):
+        Multi(2, "host")
