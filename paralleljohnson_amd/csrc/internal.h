@@ -197,8 +197,9 @@ struct Graph {
     double tail_frac = 0.1;    // vertices are < tail_frac x nnz (profiles/r01/tail_sweep.txt)
     double pull_grow = 1e9;   // v2: launch the light-pull kernels in a batch of rounds when the last seen
                                // frontier's light edges x pull_grow exceed the pull threshold
-    double light_pull = 2.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
-                               // the light edges of unsettled vertices / light_pull (0 = never)
+    double light_pull = 3.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
+                               // the light edges of unsettled vertices / light_pull (0 = never; 2 -> 3 at
+                               // the end of round 2 with merged rounds: +1%, interleaved A/B)
     int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
     int level_batch = 0; // BFS levels enqueued per host check (0 = default 8, doubling)
