@@ -844,7 +844,10 @@ constexpr u64 V2_HT = PJ_V2_HT;  // longer segments: hub queue (edge-balanced). 
                                  // would carry a whole dense chunk of them alone (load imbalance).
 constexpr int V2_EB = 40;     // hub counter: (slots << V2_EB) | edges
 constexpr int V2_NSH = 8;     // shards of a count slot
-constexpr int V2_HTILE = DB * 4;
+#ifndef PJ_V2_HTM
+#define PJ_V2_HTM 2  // swept 1, 2, 4, 8 (round 2 end): 1-2 best, +0.7% over 4, 8 is 4% slower
+#endif
+constexpr int V2_HTILE = DB * PJ_V2_HTM;  // hub-queue tile: edges per workgroup step (PJ_V2_HTM per thread)
 #ifndef PJ_V2_PLMAX
 #define PJ_V2_PLMAX 64
 #endif
