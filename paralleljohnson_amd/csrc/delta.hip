@@ -1049,7 +1049,12 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
 // block scan and relaxes the tile's edges edge-balanced, 4 independent edges per
 // thread (v2_relax_g), instead of one vertex per lane with a dependent chain of
 // loads per vertex. Segments longer than V2_DHT go to the hub queue.
-constexpr int V2_DT = DB * 4;     // vertices per dense tile (16 frontier words)
+#ifndef PJ_V2_DV
+#define PJ_V2_DV 4  // swept 2, 4, 8 (round 2 end): 2 ~ 4, 8 is 8% slower
+#endif
+constexpr int V2_DV = PJ_V2_DV;   // dense tiles: consecutive vertices per thread
+constexpr int V2_DT = DB * V2_DV; // vertices per dense tile (V2_DV * 4 frontier words)
+constexpr u32 V2_DVM = (1u << V2_DV) - 1u;
 constexpr u64 V2_DHT = 4096;      // dense mode: longer segments -> hub queue
 #ifndef PJ_V2_DNJ
 #define PJ_V2_DNJ 4
@@ -1106,14 +1111,14 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
             __syncthreads();
             continue;
         }
-        const int i0 = tid * 4;
+        const int i0 = tid * V2_DV;
         const i64 v0 = tile * V2_DT + i0;
-        const u32 nib = (u32)(sh.f[i0 >> 6] >> (i0 & 63)) & 15u;
-        const u32 nnew = (u32)(sh.fnew[i0 >> 6] >> (i0 & 63)) & 15u;
-        u64 b[4], e[4];
-        int32_t du[4];
+        const u32 nib = (u32)(sh.f[i0 >> 6] >> (i0 & 63)) & V2_DVM;
+        const u32 nnew = (u32)(sh.fnew[i0 >> 6] >> (i0 & 63)) & V2_DVM;
+        u64 b[V2_DV], e[V2_DV];
+        int32_t du[V2_DV];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < V2_DV; ++j) {
             b[j] = e[j] = 0;
             du[j] = 0;
             if ((nib >> j) & 1u) {
@@ -1134,7 +1139,7 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
         }
         // long segments -> hub queue (wave-aggregated packed append, as v2_expand_k)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < V2_DV; ++j) {
             const bool hub = e[j] - b[j] > V2_DHT;
             const u64 hm = __ballot(hub);
             if (hm) {
@@ -1157,7 +1162,7 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
         }
         u64 cnt = 0, edges = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < V2_DV; ++j)
             if (e[j] > b[j]) {
                 ++cnt;
                 edges += e[j] - b[j];
@@ -1167,7 +1172,7 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
         u32 slot = (u32)(ex >> V2_EB);
         u32 eo = (u32)(ex & mask);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < V2_DV; ++j)
             if (e[j] > b[j]) {
                 sh.b[slot] = (Off)b[j];
                 sh.du[slot] = du[j];
@@ -1816,14 +1821,14 @@ __device__ __forceinline__ void v2_dense_pull_body(const V2Args& a, const Off* _
         }
         if (tid < 2 * (V2_DT / 64)) sh.newb[tid] = 0;
         __syncthreads();
-        const int i0 = tid * 4;
+        const int i0 = tid * V2_DV;
         const i64 v0 = tile * V2_DT + i0;
-        const u32 nnew = (u32)(sh.fnew[i0 >> 6] >> (i0 & 63)) & 15u;
-        const u32 hlb = a.hl ? (u32)(a.hl[(v0 >> 6) < a.nwords ? (v0 >> 6) : 0] >> (v0 & 63)) & 15u : 15u;
-        u64 b[4], e[4];
-        int32_t d[4];
+        const u32 nnew = (u32)(sh.fnew[i0 >> 6] >> (i0 & 63)) & V2_DVM;
+        const u32 hlb = a.hl ? (u32)(a.hl[(v0 >> 6) < a.nwords ? (v0 >> 6) : 0] >> (v0 & 63)) & V2_DVM : V2_DVM;
+        u64 b[V2_DV], e[V2_DV];
+        int32_t d[V2_DV];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < V2_DV; ++j) {
             const i64 v = v0 + j;
             b[j] = e[j] = 0;
             d[j] = 0;
@@ -1843,7 +1848,7 @@ __device__ __forceinline__ void v2_dense_pull_body(const V2Args& a, const Off* _
         }
         u64 cnt = 0, edges = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < V2_DV; ++j)
             if (e[j] > b[j]) {
                 ++cnt;
                 edges += e[j] - b[j];
@@ -1853,7 +1858,7 @@ __device__ __forceinline__ void v2_dense_pull_body(const V2Args& a, const Off* _
         u32 slot = (u32)(ex >> V2_EB);
         u32 eo = (u32)(ex & mask);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < V2_DV; ++j)
             if (e[j] > b[j]) {
                 sh.b[slot] = (Off)b[j];
                 sh.off[slot] = eo;
