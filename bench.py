@@ -185,7 +185,7 @@ def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
 
 
 def run_multisource(ctx, args, rank, world, barrier, n_src=1024):
-    """configs[4]: 1024 sources on the web-Google-shaped graph, batched (up to 256 per pass),
+    """configs[4]: 1024 sources on the web-Google-shaped graph, batched (up to 512 per pass),
     source batches sharded over the ranks (no data-path collective)."""
     g = ctx.generate_webgraph(seed=args.seed)
     row, _, _ = g.get_csr()
@@ -340,7 +340,7 @@ def main():
         _, bsum = max_sum(ms["elapsed"], ms["b"])
         secondary["ms1024"] = {
             "workload": "web-google-shaped-synthetic, 1024 sources (smallest ids with out-degree >= 1), "
-                        "up to 256 per batched pass (one 64-bit mask word per 64 sources), source-sharded over the ranks",
+                        "up to 512 per batched pass (one 64-bit mask word per 64 sources), source-sharded over the ranks",
             "sources_per_rank": ms["n_src"], "batch_ms": round(1000.0 * el, 3),
             "gteps": round(m / el / 1e9, 3), "scaling": "strong (1024 sources in total)",
             # B summed over the sources; the batched passes share the CSR reads,

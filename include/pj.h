@@ -178,7 +178,7 @@ int pj_copy_dist(pj_graph* g, int32_t* dist_out);
 const int32_t* pj_dist_device(pj_graph* g);
 /* Batched multi-source (Johnson-style all-pairs rows): dist_out is n_src x n
  * int32, row i = pj_sssp(g, sources[i]); NULL discards the rows (timing).
- * Unit-weight graphs run up to 256 sources per pass, one bit per source
+ * Unit-weight graphs run up to 512 sources per pass, one bit per source
  * (msbfs.hip; the option ms_width caps the pass at 64 x ms_width); weighted
  * graphs run one delta-stepping solve per source. Either way pj_last_stats
  * then describes the whole batch (kernel_ms and levels summed over passes or

@@ -34,7 +34,7 @@ constexpr int MS_SERIAL = PJ_MS_SERIAL;  // in-edges a lane scans alone before t
 #define PJ_MS_U 8
 #endif
 constexpr int MS_U = PJ_MS_U;  // pull: in-edges a lane loads per serial step
-constexpr int MS_WMAX = 4;  // widest pass: 256 sources
+constexpr int MS_WMAX = 8;  // widest pass: 512 sources
 
 struct MsCtl {
     u64 active[3];  // ring: level L reads [(L+2)%3] (level L-1), writes [L%3], block 0 zeroes [(L+1)%3]
@@ -60,7 +60,15 @@ struct Mask {
 template <int W>
 __device__ __forceinline__ Mask<W> mload(const u64* __restrict__ p, i64 v) {
     Mask<W> m;
-    if constexpr (W == 4) {
+    if constexpr (W == 8) {
+        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p + v * 8);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const ulonglong2 x = q[k];
+            m.w[2 * k] = x.x;
+            m.w[2 * k + 1] = x.y;
+        }
+    } else if constexpr (W == 4) {
         const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p + v * 4);
         const ulonglong2 x = q[0], y = q[1];
         m.w[0] = x.x; m.w[1] = x.y; m.w[2] = y.x; m.w[3] = y.y;
@@ -453,7 +461,8 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double*
 
 template <typename Off>
 static void ms_pass_w(int W, Graph& g, MsWork& w, const int64_t* sources, int ns, double* kernel_ms, i64* levels) {
-    if (W == 4) ms_pass<Off, 4>(g, w, sources, ns, kernel_ms, levels);
+    if (W == 8) ms_pass<Off, 8>(g, w, sources, ns, kernel_ms, levels);
+    else if (W == 4) ms_pass<Off, 4>(g, w, sources, ns, kernel_ms, levels);
     else if (W == 2) ms_pass<Off, 2>(g, w, sources, ns, kernel_ms, levels);
     else ms_pass<Off, 1>(g, w, sources, ns, kernel_ms, levels);
 }

@@ -25,7 +25,7 @@ def ms1024_sources(row, k=1024):
 def test_ms1024_full_size(ctx, oracle):
     """configs[4] exactly as bench.py times it: the web-Google-shaped graph (916,428 ids,
     5,105,039 edges, seed 1), the 1024 smallest ids with out-degree >= 1, the default
-    pass width (256 sources per pass); every one of the 1024 rows equals the oracle BFS."""
+    pass width (512 sources per pass); every one of the 1024 rows equals the oracle BFS."""
     g = ctx.generate_webgraph(916428, 5105039, 1)
     row, col, _ = g.get_csr()
     col = col.view(np.uint32)
