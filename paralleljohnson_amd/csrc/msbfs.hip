@@ -34,7 +34,8 @@ constexpr int MS_SERIAL = PJ_MS_SERIAL;  // in-edges a lane scans alone before t
 #define PJ_MS_U 8
 #endif
 constexpr int MS_U = PJ_MS_U;  // pull: in-edges a lane loads per serial step
-constexpr int MS_WMAX = 8;  // widest pass: 512 sources
+constexpr int MS_WMAX = 16;  // widest pass: 1024 sources (option ms_width)
+constexpr int MS_WDEF = 8;   // default widest pass: 512 sources
 
 struct MsCtl {
     u64 active[3];  // ring: level L reads [(L+2)%3] (level L-1), writes [L%3], block 0 zeroes [(L+1)%3]
@@ -60,10 +61,10 @@ struct Mask {
 template <int W>
 __device__ __forceinline__ Mask<W> mload(const u64* __restrict__ p, i64 v) {
     Mask<W> m;
-    if constexpr (W == 8) {
-        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p + v * 8);
+    if constexpr (W >= 8) {
+        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p + v * W);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < W / 2; ++k) {
             const ulonglong2 x = q[k];
             m.w[2 * k] = x.x;
             m.w[2 * k + 1] = x.y;
@@ -461,7 +462,8 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double*
 
 template <typename Off>
 static void ms_pass_w(int W, Graph& g, MsWork& w, const int64_t* sources, int ns, double* kernel_ms, i64* levels) {
-    if (W == 8) ms_pass<Off, 8>(g, w, sources, ns, kernel_ms, levels);
+    if (W == 16) ms_pass<Off, 16>(g, w, sources, ns, kernel_ms, levels);
+    else if (W == 8) ms_pass<Off, 8>(g, w, sources, ns, kernel_ms, levels);
     else if (W == 4) ms_pass<Off, 4>(g, w, sources, ns, kernel_ms, levels);
     else if (W == 2) ms_pass<Off, 2>(g, w, sources, ns, kernel_ms, levels);
     else ms_pass<Off, 1>(g, w, sources, ns, kernel_ms, levels);
@@ -471,7 +473,7 @@ static void ms_pass_w(int W, Graph& g, MsWork& w, const int64_t* sources, int ns
 // caps it), and the pass's distance block (64 W x n int32) kept under 16 GB.
 static int ms_words(const Graph& g, int n_src) {
     int W = 1;
-    const int cap = g.ms_width > 0 ? std::min(g.ms_width, MS_WMAX) : MS_WMAX;
+    const int cap = g.ms_width > 0 ? std::min(g.ms_width, MS_WMAX) : MS_WDEF;
     while (W < cap && 64 * W < n_src && (double)(128 * W) * 4.0 * (double)g.n <= 16e9) W *= 2;
     return W;
 }

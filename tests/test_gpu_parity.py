@@ -360,7 +360,7 @@ def test_msbfs_batch_rows(ctx, oracle, kind):
         assert (out[i] == oracle.bfs(row, col, r)).all(), (kind, i, r)
 
 
-@pytest.mark.parametrize("width,alpha", [(1, 16), (2, 0), (4, 16), (4, 1e9), (8, 16), (8, 0)])
+@pytest.mark.parametrize("width,alpha", [(1, 16), (2, 0), (4, 16), (4, 1e9), (8, 16), (8, 0), (16, 16)])
 def test_msbfs_pass_widths(ctx, oracle, width, alpha):
     """Passes of 64 x W sources (W words per vertex mask): 300 sources cross several
     passes and a partial last word; push and pull levels; rows equal single-source runs."""
@@ -371,7 +371,7 @@ def test_msbfs_pass_widths(ctx, oracle, width, alpha):
     g.set_option("ms_width", width)
     g.set_option("ms_alpha", alpha)  # push levels: default rule, never, always
     row, col, _ = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n)
-    sources = [int(x) for x in rng.integers(-2, n + 2, 300 if width < 8 else 700)]
+    sources = [int(x) for x in rng.integers(-2, n + 2, {8: 700, 16: 1100}.get(width, 300))]
     out = g.sssp_batch(sources)
     exp = {r: oracle.bfs(row, col, r) for r in set(sources)}
     for i, r in enumerate(sources):
