@@ -1085,7 +1085,9 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
         int32_t li = 0;  // launch index (a launch runs one level, or several small ones)
         // first batch: the previous solve's launches, so a repeated solve on the same graph
         // usually needs one host check and no idle launch behind the last level
-        int batch = g.level_batch > 0 ? g.level_batch : std::max(2, w.last_launches);
+        // (bfs_spare extra launches cover a solve one level longer than the previous one
+        // without a host round trip; measured slower, off by default)
+        int batch = g.level_batch > 0 ? g.level_batch : std::max(2, w.last_launches + g.bfs_spare);
         // a solve that outlasts the first batch usually needs one or two more levels:
         // continue with 2, 4, 8, ... (doubling the first batch put up to a whole batch
         // of idle ~7 us launches inside the timed region: K22, 14 behind an 8-level solve)

@@ -217,7 +217,9 @@ struct Graph {
     int hub_gpc = 4;      // kernels' 24); swept (24,24) (6,7) (12,14) (12,7) (12,4) (16,7): (12,4) best // delta v2: one launch per light round decides pull / dense / sparse push (0/1)    // delta v2: the host spins on a published sequence word instead of a stream sync (0/1)    // delta v2: light pull rounds allowed in the tail too (0/1)      // delta v2: whole-CSR reads as u32 ids + u8 weights when every weight <= 255 (0/1)   // delta v2: light CSR records packed in 32 bits when they fit (0/1)   // delta v2: light pull rounds in tile-dense form (0/1) // delta v2: skip vertices without light edges in light rounds (hl bitmap)
     int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
-    int bfs_small = 1;   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)
+    int bfs_small = 1;
+    int bfs_spare = 0;   // BFS: launches beyond the previous solve's count in the first batch (1 measured
+                         // 2-3% slower on K22: the spare launch costs more than the occasional round trip)   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)
     int max_levels = 0;  // debug: truncate the BFS after this many levels (0 = off)
     int ms_width = 0;    // batch BFS: widest pass in 64-source words (0 = 8, i.e. 512 sources;
                          // MS1024 on web-Google: 11.6 ms at 8 against 12.2-14.4 ms at 4; 16
