@@ -1,5 +1,6 @@
 // msbfs.hip — batched multi-source unit-weight SSSP (Johnson-style rows of
-// the all-pairs matrix), up to 64 x W sources per pass (W = 1, 2 or 4 words).
+// the all-pairs matrix), up to 64 x W sources per pass (W = 1, 2, 4, 8 or 16 words;
+// 8 by default).
 //
 // The reference answers one source per run (`atoi(argv[2])`, :448); a batch of
 // 64 W runs shares every CSR read here. Per vertex v the pass keeps three masks
@@ -15,8 +16,10 @@
 // MS_SERIAL in-edges in a wave-uniform loop (predicated body), then the whole wave
 // scans the rest of long rows (web-graph in-hubs) 64 edges at a time. The masks
 // are stored vertex-major (W words contiguous), so a probe of F[u] is one 8W-byte
-// access: wider passes do the same number of random probes for 4x the sources
-// (the levels are probe-latency-bound, profiles/r01).
+// access: wider passes do the same number of random probes for more sources
+// (the levels are probe-latency-bound, profiles/r01). W = 8 (512 sources) measured
+// best on MS1024; 16 is 3% slower (two passes' latency saved, but twice the mask
+// bytes per probe and per vertex).
 #include <chrono>
 
 #include "devutil.h"
