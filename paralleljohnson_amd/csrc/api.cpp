@@ -869,6 +869,7 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "defer_check" && (value == 0 || value == 1)) g.defer_check = (int)value;
     else if (k == "round_gpc" && value >= 0 && value <= 64) g.round_gpc = (int)value;
     else if (k == "hub_gpc" && value >= 0 && value <= 64) g.hub_gpc = (int)value;
+    else if (k == "heavy_gpc" && value >= 0 && value <= 64) g.heavy_gpc = (int)value;
     else if (k == "grid_per_cu" && value >= 0 && value <= 16) g.grid_per_cu = (int)value;
     else if (k == "max_levels" && value >= 0) g.max_levels = (int)value;
     else if (k == "bfs_small" && (value == 0 || value == 1)) g.bfs_small = (int)value;

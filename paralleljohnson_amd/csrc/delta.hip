@@ -2424,6 +2424,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     // in proportion to its workgroups, so these may be sized to the resident capacity
     const unsigned roundgrid = g.round_gpc > 0 ? (unsigned)ctx.cu_count * (unsigned)g.round_gpc : pullgrid;
     const unsigned hubgrid = g.hub_gpc > 0 ? (unsigned)ctx.cu_count * (unsigned)g.hub_gpc : maxgrid;
+    const unsigned heavygrid = g.heavy_gpc > 0 ? (unsigned)ctx.cu_count * (unsigned)g.heavy_gpc : pullgrid;
     const int32_t delta = prepare_delta<Off>(g, w);
     // band width: at most the light threshold (an edge that can stay inside its
     // band must be light, so the band's light rounds see it)
@@ -2641,7 +2642,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 a.swrite = w.sb.p;
             }
             if (can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh) {
-                v2_pull_k<Off><<<pullgrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi_t, cs);
+                v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi_t, cs);
                 PJ_LAUNCH_CHECK();
                 PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 st.bu_levels++;

@@ -202,24 +202,25 @@ struct Graph {
                                // the end of round 2 with merged rounds: +1%, interleaved A/B)
     int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
-    int level_batch = 0; // BFS levels enqueued per host check (0 = default 8, doubling)
+    int level_batch = 0; // BFS levels enqueued per host check (0 = the previous solve's count, then 2, 4, 8, ...)
     double dense_frac = 0.1; // delta v2: a light round with a frontier above dense_frac x n runs tile-dense (0 = never;
                              // swept 0 / 0.02 / 0.1 / 0.3 on k26w: 0.1 best)
-    int light_filter = 1;
-    int dense_pull = 0;
-    int light_pack = 1;
-    int split_w = 1;
-    int tail_pull = 0;
-    int spin_sync = 1;
-    int merged_round = 1;
-    int defer_check = 1;  // delta v2 (merged rounds): no host check right after a heavy step (0/1)
-    int round_gpc = 12;   // delta v2: workgroups per CU of the light-round / hub launches (0 = the heavy
-    int hub_gpc = 4;      // kernels' 24); swept (24,24) (6,7) (12,14) (12,7) (12,4) (16,7): (12,4) best // delta v2: one launch per light round decides pull / dense / sparse push (0/1)    // delta v2: the host spins on a published sequence word instead of a stream sync (0/1)    // delta v2: light pull rounds allowed in the tail too (0/1)      // delta v2: whole-CSR reads as u32 ids + u8 weights when every weight <= 255 (0/1)   // delta v2: light CSR records packed in 32 bits when they fit (0/1)   // delta v2: light pull rounds in tile-dense form (0/1) // delta v2: skip vertices without light edges in light rounds (hl bitmap)
+    int light_filter = 1;  // delta v2: skip vertices without light edges in light rounds (hl bitmap)
+    int dense_pull = 0;    // delta v2: light pull rounds in tile-dense form (0/1; measured equal)
+    int light_pack = 1;    // delta v2: light CSR records packed in 32 bits when they fit (0/1)
+    int split_w = 1;       // delta v2: whole-CSR reads as u32 ids + u8 weights when every weight <= 255 (0/1)
+    int tail_pull = 0;     // delta v2: light pull rounds allowed in the tail too (0/1; within noise)
+    int spin_sync = 1;     // delta v2: the host spins on a published sequence word instead of a stream sync (0/1)
+    int merged_round = 1;  // delta v2: one launch per light round decides pull / dense / sparse push (0/1)
+    int defer_check = 1;   // delta v2 (merged rounds): no host check right after a heavy step (0/1)
+    int round_gpc = 12;    // delta v2: workgroups per CU of the light-round / hub launches (0 = the heavy
+    int hub_gpc = 4;       // kernels' 24); swept (24,24) (6,7) (12,14) (12,7) (12,4) (16,7): (12,4) best
+    int heavy_gpc = 0;     // delta v2: workgroups per CU of the heavy pull (0 = 24; 7-32 swept, 12-32 equal)
     int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
-    int bfs_small = 1;
+    int bfs_small = 1;   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)
     int bfs_spare = 0;   // BFS: launches beyond the previous solve's count in the first batch (1 measured
-                         // 2-3% slower on K22: the spare launch costs more than the occasional round trip)   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)
+                         // 2-3% slower on K22: the spare launch costs more than the occasional round trip)
     int max_levels = 0;  // debug: truncate the BFS after this many levels (0 = off)
     int ms_width = 0;    // batch BFS: widest pass in 64-source words (0 = 8, i.e. 512 sources;
                          // MS1024 on web-Google: 11.6 ms at 8 against 12.2-14.4 ms at 4; 16
