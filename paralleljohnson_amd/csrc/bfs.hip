@@ -1069,7 +1069,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
 
     // workgroups per CU: 4, or 2 on small graphs (< 2^25 entries), whose levels are short and
     // latency-bound, so a smaller grid drains faster (web-Google-shaped: 0.297 -> 0.281 ms per
-    // solve; Kronecker s22 is fastest at 4: tools/gpu_wg_sweep.sh)
+    // solve; Kronecker s22 is fastest at 4: tools/probe_wg_opts.py grid_per_cu=...)
     const int gpc = g.grid_per_cu > 0 ? g.grid_per_cu : (g.nnz < ((i64)1 << 25) ? 2 : 4);
     const unsigned grid = (unsigned)ctx.cu_count * (unsigned)gpc;
     auto t_host0 = std::chrono::steady_clock::now();
