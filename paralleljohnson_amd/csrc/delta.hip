@@ -833,7 +833,7 @@ __global__ __launch_bounds__(DB) void wsum_k(const u32* __restrict__ w, i64 n, u
 // ---------------------------------------------------------------------------
 constexpr int V2_SC = 16;     // frontier words a wave screens at once
 #ifndef PJ_V2_LS
-#define PJ_V2_LS 2
+#define PJ_V2_LS 2  // swept 1, 2, 4 (round 2 end): 1 ~ 2, 4 is ~1% slower
 #endif
 constexpr int V2_LS = PJ_V2_LS;  // segment edges a lane relaxes alone
 #ifndef PJ_V2_HT
@@ -1055,7 +1055,10 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
 constexpr int V2_DV = PJ_V2_DV;   // dense tiles: consecutive vertices per thread
 constexpr int V2_DT = DB * V2_DV; // vertices per dense tile (V2_DV * 4 frontier words)
 constexpr u32 V2_DVM = (1u << V2_DV) - 1u;
-constexpr u64 V2_DHT = 4096;      // dense mode: longer segments -> hub queue
+#ifndef PJ_V2_DHT
+#define PJ_V2_DHT 4096  // swept 1024, 4096, 16384 (round 2 end): within the +-1% noise
+#endif
+constexpr u64 V2_DHT = PJ_V2_DHT; // dense mode: longer segments -> hub queue
 #ifndef PJ_V2_DNJ
 #define PJ_V2_DNJ 4
 #endif
