@@ -125,11 +125,14 @@ def run_workload(ctx, key, args, rank, world, barrier, steps, warmup):
                 roots=my_roots[:steps], reach=reach, levels=levels, gen_s=gen_s, build_s=build_s, prep_s=prep_s)
 
 
-def time_to_solution(ctx_s, res):
-    """One more SSSP of the main workload taken to a sol_file (D2H + pj_write_sol), and the
-    phases of a cold run summed: HIP context, graph build, solver preparation, solve, write
-    (process start -> sol_file closed; the graph comes from the on-device
-    generator, as the reference cannot read a 2^31-line file, :66/:117)."""
+def time_to_solution(ctx_s, res, args, wl):
+    """SURVEY.md §8d time-to-solution (process start -> sol_file closed) as ONE wall clock:
+    bin/pj_kron_tts, a fresh process through the C-ABI (pj_create, on-device Kronecker
+    generation + radix sort + CSR, the first solve with the solver's preparation, D2H,
+    pj_write_sol), timed by this process from launch to exit. The reference cannot read a
+    2^31-line text file (:66/:117), so the graph comes from the generator. The in-process
+    phases of this run are reported beside it as a breakdown."""
+    import subprocess
     import paralleljohnson_amd as pj
     g, r = res["g"], res["roots"][0]
     t0 = time.perf_counter()
@@ -137,11 +140,25 @@ def time_to_solution(ctx_s, res):
     t1 = time.perf_counter()
     with tempfile.TemporaryDirectory() as td:
         pj.write_sol(d, os.path.join(td, "sol.txt"))
-    t2 = time.perf_counter()
-    phases = {"hip_context_s": round(ctx_s, 4), "graph_build_s": round(res["build_s"], 4),
-              "solver_prep_s": round(res["prep_s"], 4), "solve_and_d2h_s": round(t1 - t0, 4),
-              "write_sol_s": round(t2 - t1, 4)}
-    return round(sum(phases.values()), 4), phases
+        t2 = time.perf_counter()
+        phases = {"hip_context_s": round(ctx_s, 4), "graph_build_s": round(res["build_s"], 4),
+                  "solver_prep_s": round(res["prep_s"], 4), "solve_and_d2h_s": round(t1 - t0, 4),
+                  "write_sol_s": round(t2 - t1, 4)}
+        tool = os.path.join(ROOT, "paralleljohnson_amd", "bin", "pj_kron_tts")
+        scale = args.scale if args.scale else wl["scale"]
+        out = os.path.join(td, "sol_tts.txt")
+        t3 = time.perf_counter()
+        p = subprocess.run([tool, str(scale), str(args.edgefactor), str(args.seed), str(int(wl["weighted"])), str(r),
+                            out], capture_output=True, text=True, timeout=300)
+        wall = time.perf_counter() - t3
+        if p.returncode != 0:
+            raise RuntimeError(f"pj_kron_tts failed: {p.stderr[-400:]}")
+        same = open(out, "rb").read() == open(os.path.join(td, "sol.txt"), "rb").read()
+    f = p.stdout.split()
+    tool_phases = dict(zip(("create_s", "build_s", "solve_prep_d2h_s", "write_s"), (float(x) for x in f[1:5])))
+    return round(wall, 4), {"wall_clock": "bin/pj_kron_tts, process launch -> exit (sol_file closed)",
+                            "process_phases": tool_phases, "sol_identical_to_bench_process": same,
+                            "in_process_breakdown": phases}
 
 
 def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
@@ -184,6 +201,53 @@ def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
     return res
 
 
+def run_partitioned_host(args, world_h=2, nroots=4):
+    """configs[3]'s exchange path on ONE GPU: the s{part_scale} 1D partition at world 2 with
+    both ranks in this process sharing the GPU over the host transport (device copies
+    between the ranks' buffers, host barriers; NOT xGMI/RCCL). Puts the per-level owner
+    exchange (:522-554) and termination allreduce (:589-590) cost on record at full size."""
+    import paralleljohnson_amd as pj
+    from paralleljohnson_amd.partition import Comm, bfs_group, load_kronecker
+    ctxs = [pj.Context(0) for _ in range(world_h)]
+    comms = Comm.group(ctxs, "host")
+    t0 = time.perf_counter()
+    parts = [load_kronecker(ctxs[r], args.part_scale, args.edgefactor, args.seed, r, world_h) for r in range(world_h)]
+    build_s = time.perf_counter() - t0
+    try:
+        rng = np.random.default_rng(args.seed + 7)  # run_partitioned's candidates
+        roots = []
+        for c in rng.integers(0, 1 << args.part_scale, 64):
+            st = bfs_group(parts, comms, int(c))
+            if st[0]["reached"] > 1:
+                roots.append((int(c), st))
+            if len(roots) == nroots:
+                break
+        t = time.perf_counter()
+        for r, _ in roots:
+            bfs_group(parts, comms, r)
+        elapsed = time.perf_counter() - t
+        m = float(sum(st[0]["reached_edges"] for _, st in roots))
+        st0 = roots[0][1]
+        return {
+            "workload": f"graph500-kronecker-s{args.part_scale}-ef{args.edgefactor}-unit-bfs, 1D vertex partition at "
+                        f"world {world_h}, both ranks on ONE GPU over the host transport (device copies + host "
+                        f"barriers; not xGMI/RCCL)",
+            "roots": len(roots), "ms_per_bfs": round(1000.0 * elapsed / len(roots), 3),
+            "gteps": round(m / elapsed / 1e9, 3),
+            "levels_td_bu": [st0[0]["td_levels"], st0[0]["bu_levels"]],
+            "ids_sent_per_bfs_by_rank": [x["sent"] for x in st0],
+            "nnz_local_by_rank": [p.nnz_local for p in parts],
+            "build_s": round(build_s, 2),
+        }
+    finally:
+        for p in parts:
+            p.close()
+        for c in comms:
+            c.close()
+        for c in ctxs:
+            c.close()
+
+
 def run_multisource(ctx, args, rank, world, barrier, n_src=1024):
     """configs[4]: 1024 sources on the web-Google-shaped graph, batched (up to 512 per pass),
     source batches sharded over the ranks (no data-path collective)."""
@@ -193,11 +257,15 @@ def run_multisource(ctx, args, rank, world, barrier, n_src=1024):
     sources = np.nonzero(deg >= 1)[0][:n_src]  # the smallest ids with out-degree >= 1
     mine = sources[rank::world]
     g.sssp_batch(mine[:64], copy=False)  # untimed warmup (workspace)
-    barrier()
-    t = time.perf_counter()
-    g.sssp_batch(mine, copy=False)
-    barrier()
-    elapsed = time.perf_counter() - t
+    g.sssp_batch(mine, copy=False)  # untimed: the pass level counts that size the launch batches
+    reps = []
+    for _ in range(args.ms_reps):  # every rep is the whole batch of this rank's sources
+        barrier()
+        t = time.perf_counter()
+        g.sssp_batch(mine, copy=False)
+        barrier()
+        reps.append(time.perf_counter() - t)
+    elapsed = float(np.median(reps))
     # m_r and n_r per source (untimed): every source's reached out-edge sum and reached count
     m, b = 0.0, 0.0
     for s0 in range(0, len(mine), 64):
@@ -224,7 +292,7 @@ def run_multisource(ctx, args, rank, world, barrier, n_src=1024):
                f"single-source solves timed ({solve_s:.3f} s), scaled to {len(sources)}", "cores": threads,
                "kind": "port"}
     g.close()
-    return dict(elapsed=elapsed, m=m, b=b, n_src=len(mine), cpu=cpu)
+    return dict(elapsed=elapsed, m=m, b=b, n_src=len(mine), cpu=cpu, reps=reps)
 
 
 def main():
@@ -244,6 +312,8 @@ def main():
     ap.add_argument("--no-partitioned", action="store_true")
     ap.add_argument("--part-timeout", type=float, default=240.0,
                     help="watchdog of the partitioned leg (s): past it the line is emitted without that leg")
+    ap.add_argument("--ms-reps", type=int, default=7, help="timed MS1024 batches (median reported)")
+    ap.add_argument("--no-part-host", action="store_true", help="skip the world-2 host-transport partitioned leg")
     ap.add_argument("--opt", action="append", default=[], help="libpj graph option key=value (tuning)")
     args = ap.parse_args()
 
@@ -296,7 +366,7 @@ def main():
         with open(tj_path) as f:
             traffic = json.load(f).get("hbm_bytes_per_sssp")
 
-    tts_s, tts_phases = time_to_solution(ctx_s, main_res) if rank == 0 else (None, None)
+    tts_s, tts_phases = time_to_solution(ctx_s, main_res, args, main_res["wl"]) if rank == 0 else (None, None)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(g, main_res, args)
@@ -342,6 +412,8 @@ def main():
             "workload": "web-google-shaped-synthetic, 1024 sources (smallest ids with out-degree >= 1), "
                         "up to 512 per batched pass (one 64-bit mask word per 64 sources), source-sharded over the ranks",
             "sources_per_rank": ms["n_src"], "batch_ms": round(1000.0 * el, 3),
+            "batch_ms_stat": f"median of {len(ms['reps'])} timed batches (max over ranks of each rank's median)",
+            "batch_ms_min_max_rank0": [round(1000.0 * min(ms["reps"]), 3), round(1000.0 * max(ms["reps"]), 3)],
             "gteps": round(m / el / 1e9, 3), "scaling": "strong (1024 sources in total)",
             # B summed over the sources; the batched passes share the CSR reads,
             # so this "effective" rate can exceed the HBM peak: a reuse factor, not a fraction
@@ -368,7 +440,7 @@ def main():
         def on_timeout():
             secondary["k28_partitioned"] = {"error": f"not finished within {args.part_timeout:.0f} s (watchdog)"}
             emit()
-            os._exit(0)
+            os._exit(3)  # the line is out; a hung collective still fails the run
 
         wd = threading.Timer(args.part_timeout, on_timeout)
         wd.daemon = True
@@ -386,6 +458,11 @@ def main():
             secondary["k28_partitioned"] = {"error": f"failed on {world - int(round(n_ok))} rank(s)"}
     else:
         pr = None
+    if world == 1 and pr is not None and not args.no_part_host:
+        try:
+            secondary["k28_partitioned_host_w2"] = run_partitioned_host(args)
+        except Exception as e:  # noqa: BLE001
+            secondary["k28_partitioned_host_w2"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if pr is not None:
         per = el / pr["roots"]
         secondary["k28_partitioned"] = {

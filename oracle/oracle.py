@@ -52,6 +52,11 @@ def lib():
         L.pjo_format_sol.restype = i64
         L.pjo_kronecker.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, P, P, P]
         L.pjo_kronecker.restype = None
+        L.pjo_kronecker_row_digest.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                               P, P]
+        L.pjo_kronecker_row_digest.restype = None
+        L.pjo_csr_row_digest.argtypes = [P, P, P, i64, ctypes.c_int, P, P]
+        L.pjo_csr_row_digest.restype = i64
         _lib = L
     return _lib
 
@@ -167,3 +172,25 @@ def kronecker(scale, edgefactor, seed, weighted=False):
     w = np.zeros(m, np.uint32)
     lib().pjo_kronecker(scale, edgefactor, seed, int(weighted), _p(src), _p(dst), _p(w))
     return src, dst, (w if weighted else None)
+
+
+def kronecker_row_digest(scale, edgefactor, seed, weighted=False, threads=8):
+    """Per-vertex (entries, order-free hash sum of (col, w)) of the Kronecker spec, both
+    directions, without building the COO or CSR (full-size cross-check of a GPU build)."""
+    n = 1 << scale
+    deg = np.zeros(n, np.uint32)
+    hs = np.zeros(n, np.uint64)
+    lib().pjo_kronecker_row_digest(scale, edgefactor, seed, int(weighted), int(threads), _p(deg), _p(hs))
+    return deg, hs
+
+
+def csr_row_digest(row, col, w=None, threads=8):
+    """The same digest of a CSR, plus the count of rows entries out of weight order."""
+    row = np.ascontiguousarray(row, np.int64)
+    n = len(row) - 1
+    deg = np.zeros(max(n, 1), np.uint32)
+    hs = np.zeros(max(n, 1), np.uint64)
+    col = np.ascontiguousarray(np.asarray(col).view(np.uint32))
+    wv = None if w is None else np.ascontiguousarray(w, np.uint32)
+    bad = lib().pjo_csr_row_digest(_p(row), _p(col), _p(wv), n, int(threads), _p(deg), _p(hs))
+    return deg[:n], hs[:n], int(bad)

@@ -505,3 +505,104 @@ void pjo_kronecker(int scale, int edgefactor, uint64_t seed, int weighted, uint3
         }
     }
 }
+
+/* ------------------------------------------------------------------------ */
+/* Row digests: an order-free fingerprint of every CSR row, computed from the  */
+/* generator spec directly (no sort, no CSR) and from a CSR, so a full-size    */
+/* GPU build (s26w: 2^31 entries) is checked against an independent path.     */
+/* digest(v) = (entries of row v, sum over them of splitmix64(col<<8 | w)).    */
+/* ------------------------------------------------------------------------ */
+
+static uint64_t entry_hash(uint32_t col, uint32_t w) {
+    return splitmix64(((uint64_t)col << 8 | (uint64_t)(w & 0xffu)) ^ 0x6A09E667F3BCC909ULL);
+}
+
+typedef struct {
+    int scale, weighted;
+    uint64_t seed, i0, i1;
+    uint32_t* deg;
+    uint64_t* hsum;
+} kdig_job;
+
+static void* kdig_worker(void* arg) {
+    kdig_job* J = (kdig_job*)arg;
+    const uint32_t TA = 2448131358u, TAB = 3264175144u, TABC = 4080218931u;
+    for (uint64_t i = J->i0; i < J->i1; i++) {
+        uint64_t u = 0, v = 0;
+        for (int l = 0; l < J->scale; l++) {
+            uint32_t r = (uint32_t)(splitmix64(J->seed ^ ((i << 6) | (uint64_t)l)) >> 32);
+            uint64_t bu = r >= TAB, bv = (r >= TA && r < TAB) || r >= TABC;
+            u = (u << 1) | bu;
+            v = (v << 1) | bv;
+        }
+        uint32_t pu = (uint32_t)kperm(u, J->scale, J->seed), pv = (uint32_t)kperm(v, J->scale, J->seed);
+        uint32_t wt = J->weighted ? 1u + (uint32_t)(splitmix64(J->seed ^ 0x5851F42D4C957F2DULL ^ i) % 255u) : 1u;
+        /* both directions, as pjo_kronecker writes them */
+        __atomic_fetch_add(&J->deg[pu], 1u, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&J->hsum[pu], entry_hash(pv, wt), __ATOMIC_RELAXED);
+        __atomic_fetch_add(&J->deg[pv], 1u, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&J->hsum[pv], entry_hash(pu, wt), __ATOMIC_RELAXED);
+    }
+    return NULL;
+}
+
+void pjo_kronecker_row_digest(int scale, int edgefactor, uint64_t seed, int weighted, int threads, uint32_t* deg,
+                              uint64_t* hsum) {
+    const uint64_t M = (uint64_t)edgefactor << scale, n = 1ULL << scale;
+    memset(deg, 0, sizeof(uint32_t) * n);
+    memset(hsum, 0, sizeof(uint64_t) * n);
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    kdig_job jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (kdig_job){scale, weighted, seed, M * (uint64_t)t / (uint64_t)threads,
+                             M * (uint64_t)(t + 1) / (uint64_t)threads, deg, hsum};
+        pthread_create(&th[t], NULL, kdig_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}
+
+typedef struct {
+    const int64_t* row;
+    const uint32_t* col;
+    const uint32_t* w;
+    int64_t v0, v1;
+    uint32_t* deg;
+    uint64_t* hsum;
+    int64_t unsorted;
+} cdig_job;
+
+static void* cdig_worker(void* arg) {
+    cdig_job* J = (cdig_job*)arg;
+    for (int64_t v = J->v0; v < J->v1; v++) {
+        uint64_t h = 0;
+        for (int64_t k = J->row[v]; k < J->row[v + 1]; k++) {
+            const uint32_t wk = J->w ? J->w[k] : 1u;
+            h += entry_hash(J->col[k], wk);
+            if (J->w && k > J->row[v] && J->w[k - 1] > wk) J->unsorted++;
+        }
+        J->deg[v] = (uint32_t)(J->row[v + 1] - J->row[v]);
+        J->hsum[v] = h;
+    }
+    return NULL;
+}
+
+/* returns the number of entries whose weight is below their predecessor's in the row */
+int64_t pjo_csr_row_digest(const int64_t* row, const uint32_t* col, const uint32_t* w, int64_t n, int threads,
+                           uint32_t* deg, uint64_t* hsum) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    cdig_job jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (cdig_job){row, col, w, n * t / threads, n * (t + 1) / threads, deg, hsum, 0};
+        pthread_create(&th[t], NULL, cdig_worker, &jobs[t]);
+    }
+    int64_t bad = 0;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        bad += jobs[t].unsorted;
+    }
+    return bad;
+}

@@ -87,6 +87,17 @@ int64_t pjo_format_sol(const int32_t* dist, int64_t n, char* buf);
 void pjo_kronecker(int scale, int edgefactor, uint64_t seed, int weighted, uint32_t* src,
                    uint32_t* dst, uint32_t* w);
 
+/* Order-free row digests (test infrastructure for full-size CSR builds):
+ * deg[v] = entries of row v, hsum[v] = sum of splitmix64((col << 8 | w) ^ K)
+ * over them. From the Kronecker spec directly (both directions, as
+ * pjo_kronecker), on `threads` host threads: */
+void pjo_kronecker_row_digest(int scale, int edgefactor, uint64_t seed, int weighted, int threads, uint32_t* deg,
+                              uint64_t* hsum);
+/* ... and from a CSR (w may be NULL = unit); returns the count of entries whose
+ * weight is below the previous entry's in the same row (0 = weight-sorted rows). */
+int64_t pjo_csr_row_digest(const int64_t* row, const uint32_t* col, const uint32_t* w, int64_t n, int threads,
+                           uint32_t* deg, uint64_t* hsum);
+
 #ifdef __cplusplus
 }
 #endif

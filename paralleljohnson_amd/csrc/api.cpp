@@ -1185,6 +1185,7 @@ int pj_wpart_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_wp
 int pj_wpart_destroy(pj_wpart* p) {
     if (!p) return PJ_OK;
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         delete_wpart(reinterpret_cast<WPart*>(p));
         return (int)PJ_OK;
     });
@@ -1199,6 +1200,7 @@ int pj_wpart_info(const pj_wpart* p, int64_t* out) {
 int pj_wpart_begin(pj_wpart* p, int64_t source, int32_t delta, int32_t* delta_out) {
     if (!p) return arg_error("pj_wpart_begin: bad argument");
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         const int32_t d = wpart_begin(*reinterpret_cast<WPart*>(p), source, delta);
         if (delta_out) *delta_out = d;
         return (int)PJ_OK;
@@ -1208,6 +1210,7 @@ int pj_wpart_begin(pj_wpart* p, int64_t source, int32_t delta, int32_t* delta_ou
 int pj_wpart_select(pj_wpart* p, int32_t lo, int32_t hi, int64_t* out) {
     if (!p || !out || lo < 0 || hi < lo) return arg_error("pj_wpart_select: bad argument");
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         wpart_select(*reinterpret_cast<WPart*>(p), lo, hi, out);
         return (int)PJ_OK;
     });
@@ -1216,6 +1219,7 @@ int pj_wpart_select(pj_wpart* p, int32_t lo, int32_t hi, int64_t* out) {
 int pj_wpart_relax(pj_wpart* p, int light, int32_t lo, int32_t hi, uint64_t* send, int64_t* counts) {
     if (!p || !counts || lo < 0 || hi < lo) return arg_error("pj_wpart_relax: bad argument");
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         wpart_relax(*reinterpret_cast<WPart*>(p), light, lo, hi, (u64*)send, counts);
         return (int)PJ_OK;
     });
@@ -1224,6 +1228,7 @@ int pj_wpart_relax(pj_wpart* p, int light, int32_t lo, int32_t hi, uint64_t* sen
 int pj_wpart_apply(pj_wpart* p, const uint64_t* recv, int64_t n_recv, int light, int32_t lo, int32_t hi) {
     if (!p || n_recv < 0 || (n_recv > 0 && !recv)) return arg_error("pj_wpart_apply: bad argument");
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         wpart_apply(*reinterpret_cast<WPart*>(p), (const u64*)recv, n_recv, light, lo, hi);
         return (int)PJ_OK;
     });
@@ -1232,6 +1237,7 @@ int pj_wpart_apply(pj_wpart* p, const uint64_t* recv, int64_t n_recv, int light,
 int pj_wpart_end_round(pj_wpart* p, int64_t* n_f) {
     if (!p || !n_f) return arg_error("pj_wpart_end_round: bad argument");
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         *n_f = wpart_end_round(*reinterpret_cast<WPart*>(p));
         return (int)PJ_OK;
     });
@@ -1240,6 +1246,7 @@ int pj_wpart_end_round(pj_wpart* p, int64_t* n_f) {
 int pj_wpart_reach(pj_wpart* p, int64_t* out) {
     if (!p || !out) return arg_error("pj_wpart_reach: bad argument");
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         wpart_reach(*reinterpret_cast<WPart*>(p), out);
         return (int)PJ_OK;
     });
@@ -1248,6 +1255,7 @@ int pj_wpart_reach(pj_wpart* p, int64_t* out) {
 int pj_wpart_copy_dist(pj_wpart* p, int32_t* dist_out) {
     if (!p || !dist_out) return arg_error("pj_wpart_copy_dist: bad argument");
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         wpart_copy_dist(*reinterpret_cast<WPart*>(p), dist_out);
         return (int)PJ_OK;
     });
@@ -1335,6 +1343,7 @@ int pj_part_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_par
 int pj_part_destroy(pj_part* p) {
     if (!p) return PJ_OK;
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         delete_part(reinterpret_cast<Part*>(p));
         return (int)PJ_OK;
     });
@@ -1361,6 +1370,7 @@ int pj_part_info_get(const pj_part* p, pj_part_info* out) {
 int pj_part_zmask(pj_part* p, uint64_t* own_words) {
     if (!p || !own_words) return arg_error("pj_part_zmask: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         part_zmask(*reinterpret_cast<Part*>(p), reinterpret_cast<u64*>(own_words));
         return (int)PJ_OK;
     });
@@ -1369,6 +1379,7 @@ int pj_part_zmask(pj_part* p, uint64_t* own_words) {
 int pj_part_begin(pj_part* p, int64_t source, const uint64_t* iso, uint64_t* vis, int64_t* stats) {
     if (!p || !iso || !vis || !stats) return arg_error("pj_part_begin: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         part_begin(*reinterpret_cast<Part*>(p), source, reinterpret_cast<const u64*>(iso), reinterpret_cast<u64*>(vis),
                    stats);
         return (int)PJ_OK;
@@ -1378,6 +1389,7 @@ int pj_part_begin(pj_part* p, int64_t source, const uint64_t* iso, uint64_t* vis
 int pj_part_push(pj_part* p, int level, uint64_t* vis, uint32_t* send, int64_t* counts) {
     if (!p || !vis || !counts || level < 0) return arg_error("pj_part_push: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         Part& P = *reinterpret_cast<Part*>(p);
         i64 info[11];
         part_info(P, info);
@@ -1390,6 +1402,7 @@ int pj_part_push(pj_part* p, int level, uint64_t* vis, uint32_t* send, int64_t* 
 int pj_part_apply(pj_part* p, int level, uint64_t* vis, const uint32_t* recv, int64_t n_recv) {
     if (!p || !vis || n_recv < 0 || (n_recv > 0 && !recv) || level < 0) return arg_error("pj_part_apply: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         part_apply(*reinterpret_cast<Part*>(p), level, reinterpret_cast<u64*>(vis), recv, n_recv);
         return (int)PJ_OK;
     });
@@ -1398,6 +1411,7 @@ int pj_part_apply(pj_part* p, int level, uint64_t* vis, const uint32_t* recv, in
 int pj_part_pull(pj_part* p, int level, uint64_t* vis) {
     if (!p || !vis || level < 0) return arg_error("pj_part_pull: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         part_pull(*reinterpret_cast<Part*>(p), level, reinterpret_cast<u64*>(vis));
         return (int)PJ_OK;
     });
@@ -1406,6 +1420,7 @@ int pj_part_pull(pj_part* p, int level, uint64_t* vis) {
 int pj_part_end_level(pj_part* p, uint64_t* vis, int64_t* stats) {
     if (!p || !vis || !stats) return arg_error("pj_part_end_level: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         part_end_level(*reinterpret_cast<Part*>(p), reinterpret_cast<u64*>(vis), stats);
         return (int)PJ_OK;
     });
@@ -1414,6 +1429,7 @@ int pj_part_end_level(pj_part* p, uint64_t* vis, int64_t* stats) {
 int pj_part_reach(pj_part* p, int64_t* out) {
     if (!p || !out) return arg_error("pj_part_reach: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         part_reach(*reinterpret_cast<Part*>(p), out);
         return (int)PJ_OK;
     });
@@ -1422,6 +1438,7 @@ int pj_part_reach(pj_part* p, int64_t* out) {
 int pj_part_copy_dist(pj_part* p, int32_t* dist_out) {
     if (!p || !dist_out) return arg_error("pj_part_copy_dist: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         part_copy_dist(*reinterpret_cast<Part*>(p), dist_out);
         return (int)PJ_OK;
     });
@@ -1515,6 +1532,13 @@ int run_group(int world, F&& fn) {
     if (first < 0) return PJ_OK;
     set_error("rank " + std::to_string(first) + ": " + msgs[(size_t)first]);
     return rcs[(size_t)first];
+}
+
+// after a failed group solve (every rank thread joined): host groups are usable
+// again; an aborted RCCL communicator stays unusable (pj_multi recreates its comms)
+void reset_group(int world, pj_comm* const* comms) {
+    for (int r = 0; r < world; ++r)
+        if (comms[r]) comms[r]->c->reset();
 }
 
 }  // namespace
@@ -1611,6 +1635,7 @@ int pj_part_set_option(pj_part* p, const char* key, double value) {
 int pj_part_bfs(pj_part* p, pj_comm* comm, int64_t source, pj_part_stats* st) {
     if (!p || !comm) return arg_error("pj_part_bfs: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         Part& P = *reinterpret_cast<Part*>(p);
         BfsSteps& S = part_steps(P);
         bool& iso = part_iso_ready(P, comm->c.get());
@@ -1622,12 +1647,15 @@ int pj_part_bfs(pj_part* p, pj_comm* comm, int64_t source, pj_part_stats* st) {
 
 int pj_part_bfs_group(int world, pj_part* const* parts, pj_comm* const* comms, int64_t source, pj_part_stats* st) {
     if (world < 1 || !parts || !comms) return arg_error("pj_part_bfs_group: bad argument");
-    return run_group(world, [&](int r) { return pj_part_bfs(parts[r], comms[r], source, st ? st + r : nullptr); });
+    const int rc = run_group(world, [&](int r) { return pj_part_bfs(parts[r], comms[r], source, st ? st + r : nullptr); });
+    if (rc != PJ_OK) reset_group(world, comms);
+    return rc;
 }
 
 int pj_part_gather_dist(pj_part* p, pj_comm* comm, int32_t* dist_out) {
     if (!p || !comm) return arg_error("pj_part_gather_dist: bad argument");
     return guarded([&] {
+        bind(part_ctx(*reinterpret_cast<Part*>(p)));
         part_gather_dist(*reinterpret_cast<Part*>(p), *comm->c, dist_out);
         return (int)PJ_OK;
     });
@@ -1636,6 +1664,7 @@ int pj_part_gather_dist(pj_part* p, pj_comm* comm, int32_t* dist_out) {
 int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st) {
     if (!p || !comm) return arg_error("pj_wpart_delta: bad argument");
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         delta_engine(wpart_steps(*reinterpret_cast<WPart*>(p)), *comm->c, source, delta, st);
         return (int)PJ_OK;
     });
@@ -1644,13 +1673,16 @@ int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj
 int pj_wpart_delta_group(int world, pj_wpart* const* parts, pj_comm* const* comms, int64_t source, int32_t delta,
                          pj_part_stats* st) {
     if (world < 1 || !parts || !comms) return arg_error("pj_wpart_delta_group: bad argument");
-    return run_group(world,
-                     [&](int r) { return pj_wpart_delta(parts[r], comms[r], source, delta, st ? st + r : nullptr); });
+    const int rc = run_group(
+        world, [&](int r) { return pj_wpart_delta(parts[r], comms[r], source, delta, st ? st + r : nullptr); });
+    if (rc != PJ_OK) reset_group(world, comms);
+    return rc;
 }
 
 int pj_wpart_gather_dist(pj_wpart* p, pj_comm* comm, int32_t* dist_out) {
     if (!p || !comm) return arg_error("pj_wpart_gather_dist: bad argument");
     return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
         wpart_gather_dist(*reinterpret_cast<WPart*>(p), *comm->c, dist_out);
         return (int)PJ_OK;
     });

@@ -15,6 +15,8 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 
 #include <rccl/rccl.h>
 
@@ -80,6 +82,12 @@ struct ThreadGroup {
         std::lock_guard<std::mutex> lk(mu);
         failed = true;
         cv.notify_all();
+    }
+    // after every rank has left the failed collective (the caller joined the rank threads)
+    void reset() {
+        std::lock_guard<std::mutex> lk(mu);
+        failed = false;
+        arrived = 0;
     }
 };
 
@@ -149,6 +157,7 @@ struct ThreadComm final : Comm {
     }
 
     void abort() override { g->abort(); }
+    void reset() override { g->reset(); }
 };
 
 }  // namespace
@@ -184,6 +193,8 @@ struct RcclApi {
     decltype(&ncclGroupStart) groupStart = nullptr;
     decltype(&ncclGroupEnd) groupEnd = nullptr;
     decltype(&ncclGetErrorString) errorString = nullptr;
+    decltype(&ncclCommAbort) commAbort = nullptr;
+    decltype(&ncclCommGetAsyncError) getAsyncError = nullptr;
 };
 
 const RcclApi& rccl() {
@@ -207,10 +218,13 @@ const RcclApi& rccl() {
         PJ_SYM(groupStart, ncclGroupStart);
         PJ_SYM(groupEnd, ncclGroupEnd);
         PJ_SYM(errorString, ncclGetErrorString);
+        PJ_SYM(commAbort, ncclCommAbort);
+        PJ_SYM(getAsyncError, ncclCommGetAsyncError);
 #undef PJ_SYM
     });
     if (!api.h || !api.getUniqueId || !api.commInitRank || !api.commInitAll || !api.allReduce || !api.allGather ||
-        !api.send || !api.recv || !api.groupStart || !api.groupEnd || !api.commDestroy || !api.errorString)
+        !api.send || !api.recv || !api.groupStart || !api.groupEnd || !api.commDestroy || !api.errorString ||
+        !api.commAbort || !api.getAsyncError)
         throw Error(PJ_ERR_COMM, "RCCL (librccl.so.1) is not available");
     return api;
 }
@@ -219,9 +233,18 @@ void nccl_check(ncclResult_t r, const char* what) {
     if (r != ncclSuccess) throw Error(PJ_ERR_COMM, std::string(what) + ": " + rccl().errorString(r));
 }
 
+// Failure state shared by the ranks of one process's RCCL group (ncclCommInitAll):
+// a rank that fails raises it, and every peer waiting on a collective aborts its
+// own communicator, so its blocked kernels exit instead of hanging the group.
+struct RcclGroupState {
+    std::atomic<bool> failed{false};
+};
+
 struct RcclComm final : Comm {
     ncclComm_t c = nullptr;
     int device = 0;
+    bool aborted = false;
+    std::shared_ptr<RcclGroupState> grp;  // null for one rank of a multi-process group
     DevBuf<i64> scratch;  // allreduce values / all-gathered count rows
     PinnedBuf<i64> host;
     const char* kind() const override { return "rccl"; }
@@ -233,21 +256,56 @@ struct RcclComm final : Comm {
         host.alloc(cap);
     }
     ~RcclComm() override {
-        if (c) (void)rccl().commDestroy(c);
+        if (c && !aborted) (void)rccl().commDestroy(c);
+    }
+    void usable() const {
+        if (aborted) throw Error(PJ_ERR_COMM, "the RCCL communicator was aborted after a rank failure");
+    }
+    void abort_local() {
+        if (c && !aborted) {
+            aborted = true;
+            (void)rccl().commAbort(c);
+        }
+    }
+    void abort() override {
+        if (grp) grp->failed = true;
+        abort_local();
+    }
+    // stream completion, polled so a peer's failure (group flag) or an RCCL async
+    // error ends the wait: hipStreamSynchronize would block forever on a dead peer
+    void wait(hipStream_t s) {
+        const RcclApi& api = rccl();
+        for (int spin = 0;; ++spin) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess) return;
+            if (e != hipErrorNotReady) PJ_HIP(e);
+            ncclResult_t ae = ncclSuccess;
+            if (api.getAsyncError(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                abort_local();
+                throw Error(PJ_ERR_COMM, std::string("RCCL async error: ") + api.errorString(ae));
+            }
+            if (grp && grp->failed) {
+                abort_local();
+                throw Error(PJ_ERR_COMM, "a peer rank of the RCCL group failed");
+            }
+            if (spin > 2000) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
     }
 
     void allreduce(i64* v, int k, bool is_min, hipStream_t s) override {
+        usable();
         if ((size_t)k > scratch.n) throw Error(PJ_ERR_ARG, "allreduce: too many values");
         std::copy(v, v + k, host.p);
         PJ_HIP(hipMemcpyAsync(scratch.p, host.p, sizeof(i64) * (size_t)k, hipMemcpyHostToDevice, s));
         nccl_check(rccl().allReduce(scratch.p, scratch.p, (size_t)k, ncclInt64, is_min ? ncclMin : ncclSum, c, s),
                    "ncclAllReduce");
         PJ_HIP(hipMemcpyAsync(host.p, scratch.p, sizeof(i64) * (size_t)k, hipMemcpyDeviceToHost, s));
-        PJ_HIP(hipStreamSynchronize(s));
+        wait(s);
         std::copy(host.p, host.p + k, v);
     }
 
     void alltoall_counts(const i64* send, i64* recv, hipStream_t s) override {
+        usable();
         // row r of a world x world matrix per rank; in place: own row at offset rank * world
         i64* rows = scratch.p;
         std::copy(send, send + world, host.p);
@@ -256,12 +314,13 @@ struct RcclComm final : Comm {
         nccl_check(rccl().allGather(rows + (size_t)rank * world, rows, (size_t)world, ncclInt64, c, s),
                    "ncclAllGather(counts)");
         PJ_HIP(hipMemcpyAsync(host.p, rows, sizeof(i64) * (size_t)world * world, hipMemcpyDeviceToHost, s));
-        PJ_HIP(hipStreamSynchronize(s));
+        wait(s);
         for (int q = 0; q < world; ++q) recv[q] = host.p[(size_t)q * world + rank];
     }
 
     void alltoallv(const void* send, const i64* scount, void* recv, const i64* rcount, size_t elem,
                    hipStream_t s) override {
+        usable();
         const char* sb = static_cast<const char*>(send);
         char* rb = static_cast<char*>(recv);
         size_t so = 0, ro = 0, self_s = 0, self_r = 0;
@@ -281,11 +340,16 @@ struct RcclComm final : Comm {
         }
         nccl_check(api.groupEnd(), "ncclGroupEnd");
         copy_on(rb + self_r, device, sb + self_s, device, (size_t)scount[rank] * elem, s);
+        wait(s);  // any later host wait of the steps is then on local work only
     }
 
     void allgather(const void* own, void* all, size_t bytes, hipStream_t s) override {
+        usable();
         nccl_check(rccl().allGather(own, all, bytes, ncclUint8, c, s), "ncclAllGather");
+        wait(s);
     }
+    // the loops' own stream waits after a collective (end of a solve, gathers)
+    void sync(hipStream_t s) override { wait(s); }
 };
 
 }  // namespace
@@ -318,6 +382,7 @@ std::vector<std::unique_ptr<Comm>> make_rccl_group(const std::vector<int>& devic
         throw Error(PJ_ERR_COMM, "RCCL needs one GPU per rank (use the host transport to share a GPU)");
     std::vector<ncclComm_t> cs((size_t)world);
     nccl_check(rccl().commInitAll(cs.data(), world, devices.data()), "ncclCommInitAll");
+    auto grp = std::make_shared<RcclGroupState>();
     std::vector<std::unique_ptr<Comm>> out;
     for (int r = 0; r < world; ++r) {
         auto c = std::make_unique<RcclComm>();
@@ -325,6 +390,7 @@ std::vector<std::unique_ptr<Comm>> make_rccl_group(const std::vector<int>& devic
         c->world = world;
         c->device = devices[(size_t)r];
         c->c = cs[(size_t)r];
+        c->grp = grp;
         c->init_buffers();
         out.push_back(std::move(c));
     }

@@ -112,7 +112,7 @@ void bfs_engine(BfsSteps& S, Comm& comm, i64 source, const BfsParams& prm, bool 
             mode = nxt;
             ++level;
         }
-        if (s) PJ_HIP(hipStreamSynchronize(s));
+        comm.sync(s);
         if (st) {
             *st = pj_part_stats{};
             st->solve_ms = now_ms() - t0;
@@ -173,7 +173,7 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             exchange_apply(0, (int32_t)lo, (int32_t)hi);  // heavy edges of the band's members
             lo = hi;
         }
-        if (s) PJ_HIP(hipStreamSynchronize(s));
+        comm.sync(s);
         const double t1 = now_ms();
         i64 rc[2];
         S.reach(rc);

@@ -38,8 +38,15 @@ struct Comm {
                            hipStream_t s) = 0;
     // all[q * bytes ...] := rank q's own bytes (own may alias all + rank * bytes)
     virtual void allgather(const void* own, void* all, size_t bytes, hipStream_t s) = 0;
-    // release a group whose peer failed (threads of one process); no-op elsewhere
+    // release a group whose peer failed (threads of one process: the host barrier;
+    // RCCL: ncclCommAbort, the group's peers abort theirs); no-op elsewhere
     virtual void abort() {}
+    // make a host group usable again once every rank has left a failed collective
+    virtual void reset() {}
+    // wait for the stream (RCCL: polled, so a failed peer ends the wait)
+    virtual void sync(hipStream_t s) {
+        if (s) PJ_HIP(hipStreamSynchronize(s));
+    }
 };
 
 std::unique_ptr<Comm> make_self_comm();
@@ -101,6 +108,10 @@ BfsSteps& part_steps(Part& p);
 DeltaSteps& wpart_steps(WPart& p);
 bool& part_iso_ready(Part& p, const Comm* comm);
 BfsParams& part_params(Part& p);
+// the context (device, stream) a part was built on: API entry points bind it first,
+// because the per-rank host threads start on device 0
+const Ctx& part_ctx(const Part& p);
+const Ctx& wpart_ctx(const WPart& p);
 // every rank's slice of dist, gathered (n int32 to host; NULL: gather only)
 void part_gather_dist(Part& p, Comm& comm, int32_t* out);
 void wpart_gather_dist(WPart& p, Comm& comm, int32_t* out);

@@ -108,7 +108,18 @@ int part_solve(pj_multi* m, int64_t source, int32_t* dist_out, pj_part_stats* st
     std::vector<pj_part_stats> rs((size_t)m->world);
     int rc = m->weighted ? pj_wpart_delta_group(m->world, m->wparts.data(), m->comms.data(), source, 0, rs.data())
                          : pj_part_bfs_group(m->world, m->parts.data(), m->comms.data(), source, rs.data());
-    if (rc != PJ_OK) return rc;
+    if (rc != PJ_OK) {
+        // a failed rank leaves an RCCL group aborted: recreate the comms so the handle
+        // stays usable (host groups were reset by the group call); keep the first error
+        const std::string err = pj_last_error();
+        std::string kind(m->kind);
+        if (kind == "rccl") {
+            for (auto*& c : m->comms) pj_comm_destroy(c), c = nullptr;
+            if (make_comms(m) != PJ_OK) m->drop_graph();  // unusable: the caller must load again
+        }
+        pj::set_error(err);
+        return rc;
+    }
     if (st) {  // the reference's Time: is rank 0's clock after the last round (:597-605); max over ranks here
         *st = rs[0];
         for (auto& s : rs) st->solve_ms = std::max(st->solve_ms, s.solve_ms);

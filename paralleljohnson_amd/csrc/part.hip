@@ -846,6 +846,8 @@ BfsSteps& part_steps(Part& p) {
 
 BfsParams& part_params(Part& p) { return p.prm; }
 
+const Ctx& part_ctx(const Part& p) { return *p.ctx; }
+
 bool& part_iso_ready(Part& p, const Comm* comm) {
     if (p.iso_comm != comm) {
         p.iso_comm = comm;

@@ -2,10 +2,16 @@
 // validation (the reference has no counterpart: it writes
 // distances only, output_vector :32-46).
 //
-// parent[v] = the smallest u with an edge u -> v of weight w and dist[u] + w ==
-// dist[v] (< PJ_INT_INF), parent[source] = source, -1 for unreached vertices.
-// The smallest tight in-neighbour makes the tree a function of the distances
-// alone, so it is identical for every solver path (BFS levels, delta bands,
+// parent[v] = the smallest u with an edge u -> v of weight w > 0 and dist[u] + w
+// == dist[v] (< PJ_INT_INF), parent[source] = source, -1 for unreached vertices.
+// A reached v with no such edge is entered only through zero-weight tight edges
+// from vertices of the same distance: those are parented level by level from
+// the vertices parented so far (hop depth h inside the zero-weight tight
+// subgraph, h = 0 for the source and every vertex with a positive tight
+// in-edge): parent[v] = the smallest u with a zero-weight edge u -> v,
+// dist[u] == dist[v] and h(u) == h(v) - 1. Every parent step lowers (dist, h),
+// so the tree is acyclic with zero weights too; it is a function of the
+// distances alone, identical for every solver path (BFS levels, delta bands,
 // either direction) and for a CPU restatement.
 //
 // Validation (the Graph500 BFS / SSSP checks, restated for the capped int32
@@ -57,14 +63,46 @@ __device__ __forceinline__ void for_reached_edges(const Off* __restrict__ row, c
     }
 }
 
+constexpr u32 NO_HOP = 0xffffffffu;
+
+// positive tight edges; zflag counts the zero-weight tight edges (the second phase runs only then)
 template <typename Off, bool W>
 __global__ __launch_bounds__(256) void parent_k(const Off* __restrict__ row, const u32* __restrict__ col,
                                                 const u32* __restrict__ wt, const int32_t* __restrict__ dist, i64 n,
-                                                u32* __restrict__ par) {
+                                                u32* __restrict__ par, u32* __restrict__ zflag) {
+    u32 zero = 0;
     for_reached_edges<Off, W>(row, col, wt, dist, n, [&](i64 u, int32_t du, u32 v, u32 w) {
         const int32_t dv = dist[v];
-        if (dv < INT_INF && (i64)du + (i64)w == (i64)dv && par[v] > (u32)u) atomicMin(&par[v], (u32)u);
+        if (dv < INT_INF && (i64)du + (i64)w == (i64)dv) {
+            if (w == 0) zero = 1;
+            else if (par[v] > (u32)u) atomicMin(&par[v], (u32)u);
+        }
     });
+    if (zero) atomicOr(zflag, 1u);
+}
+
+__global__ void hop_init_k(const u32* __restrict__ par, i64 n, i64 source, u32* __restrict__ hop) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x)
+        hop[v] = (v == source || par[v] != 0xffffffffu) ? 0u : NO_HOP;
+}
+
+// one level of the zero-weight phase: rows u with hop[u] == lvl parent their zero-weight tight
+// targets that have no hop yet (every writer stores lvl + 1)
+template <typename Off>
+__global__ __launch_bounds__(256) void parent_zero_k(const Off* __restrict__ row, const u32* __restrict__ col,
+                                                     const u32* __restrict__ wt, const int32_t* __restrict__ dist,
+                                                     i64 n, u32 lvl, u32* __restrict__ hop, u32* __restrict__ par,
+                                                     u32* __restrict__ changed) {
+    u32 any = 0;
+    for_reached_edges<Off, true>(row, col, wt, dist, n, [&](i64 u, int32_t du, u32 v, u32 w) {
+        if (w != 0 || hop[u] != lvl || dist[v] != du) return;
+        const u32 hv = hop[v];
+        if (hv != NO_HOP && hv != lvl + 1) return;
+        hop[v] = lvl + 1;
+        if (par[v] > (u32)u) atomicMin(&par[v], (u32)u);
+        any = 1;
+    });
+    if (any) atomicOr(changed, 1u);
 }
 
 __global__ void parent_out_k(const u32* __restrict__ par, i64 n, i64 source, int64_t* __restrict__ out) {
@@ -135,10 +173,32 @@ __global__ void cycle_k(const int32_t* __restrict__ dist, const int64_t* __restr
 unsigned grid_of(const Graph& g, i64 work) { return grid_for(work, 256, (unsigned)g.ctx->cu_count * 8u); }
 
 template <typename Off, bool W>
-void parent_run(Graph& g, u32* par) {
+void parent_run(Graph& g, i64 source, u32* par) {
     const Off* row = static_cast<const Off*>(g.row_ptr());
-    parent_k<Off, W><<<grid_of(g, g.n), 256, 0, g.ctx->stream>>>(row, g.col.p, g.w.p, g.dist.p, g.n, par);
+    hipStream_t s = g.ctx->stream;
+    DevBuf<u32> flag(1);
+    PinnedBuf<u32> hflag;
+    hflag.alloc(1);
+    PJ_HIP(hipMemsetAsync(flag.p, 0, sizeof(u32), s));
+    parent_k<Off, W><<<grid_of(g, g.n), 256, 0, s>>>(row, g.col.p, g.w.p, g.dist.p, g.n, par, flag.p);
     PJ_LAUNCH_CHECK();
+    if constexpr (W) {
+        PJ_HIP(hipMemcpyAsync(hflag.p, flag.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+        if (!hflag.p[0]) return;
+        DevBuf<u32> hop((size_t)g.n);
+        hop_init_k<<<grid_of(g, g.n), 256, 0, s>>>(par, g.n, source, hop.p);
+        PJ_LAUNCH_CHECK();
+        for (u32 lvl = 0;; ++lvl) {  // one level per pass; ends when a level parents nothing
+            PJ_HIP(hipMemsetAsync(flag.p, 0, sizeof(u32), s));
+            parent_zero_k<Off><<<grid_of(g, g.n), 256, 0, s>>>(row, g.col.p, g.w.p, g.dist.p, g.n, lvl, hop.p, par,
+                                                               flag.p);
+            PJ_LAUNCH_CHECK();
+            PJ_HIP(hipMemcpyAsync(hflag.p, flag.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipStreamSynchronize(s));
+            if (!hflag.p[0]) break;
+        }
+    }
 }
 
 template <typename Off, bool W>
@@ -158,8 +218,8 @@ void parent_tree(Graph& g, i64 source, int64_t* host_out) {
     DevBuf<int64_t> out((size_t)n);
     PJ_HIP(hipMemsetAsync(par.p, 0xff, 4 * (size_t)n, s));
     const bool w = g.weighted;
-    if (g.off64) w ? parent_run<u64, true>(g, par.p) : parent_run<u64, false>(g, par.p);
-    else w ? parent_run<u32, true>(g, par.p) : parent_run<u32, false>(g, par.p);
+    if (g.off64) w ? parent_run<u64, true>(g, source, par.p) : parent_run<u64, false>(g, source, par.p);
+    else w ? parent_run<u32, true>(g, source, par.p) : parent_run<u32, false>(g, source, par.p);
     parent_out_k<<<grid_of(g, n), 256, 0, s>>>(par.p, n, source, out.p);
     PJ_LAUNCH_CHECK();
     PJ_HIP(hipMemcpyAsync(host_out, out.p, 8 * (size_t)n, hipMemcpyDeviceToHost, s));

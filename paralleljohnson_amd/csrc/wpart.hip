@@ -710,6 +710,8 @@ struct WPartGpuSteps final : DeltaSteps {
 
 }  // namespace
 
+const Ctx& wpart_ctx(const WPart& p) { return *p.ctx; }
+
 DeltaSteps& wpart_steps(WPart& p) {
     if (!p.steps) p.steps.reset(new WPartGpuSteps(p));
     return *p.steps;

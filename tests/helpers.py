@@ -98,8 +98,12 @@ def csr_to_text(row, col):
 
 
 def tight_parents(row, col, w, dist, source, inf=100000):
-    """CPU restatement of pj_parent_tree: parent[v] = the smallest u with an edge u -> v of
-    weight w and dist[u] + w == dist[v] < inf, parent[source] = source, -1 when unreached."""
+    """CPU restatement of pj_parent_tree (tree.hip): parent[v] = the smallest u with an
+    edge u -> v of weight w > 0 and dist[u] + w == dist[v] < inf; a reached v without
+    one is parented through zero-weight tight edges, level by level from the vertices
+    parented so far (hop depth h, 0 for the source and every vertex with a positive tight
+    in-edge): the smallest u with w == 0, dist[u] == dist[v], h(u) == h(v) - 1.
+    parent[source] = source, -1 when unreached."""
     row = np.asarray(row, dtype=np.int64)
     n = len(row) - 1
     d = np.asarray(dist, dtype=np.int64)
@@ -107,9 +111,27 @@ def tight_parents(row, col, w, dist, source, inf=100000):
     v = np.asarray(col).view(np.uint32).astype(np.int64)
     wt = np.ones_like(v) if w is None else np.asarray(w, dtype=np.int64)
     tight = (d[u] < inf) & (d[v] < inf) & (d[u] + wt == d[v])
-    par = np.full(n, np.iinfo(np.int64).max, np.int64)
-    np.minimum.at(par, v[tight], u[tight])
-    par[par == np.iinfo(np.int64).max] = -1
+    big = np.iinfo(np.int64).max
+    par = np.full(n, big, np.int64)
+    pos = tight & (wt > 0)
+    np.minimum.at(par, v[pos], u[pos])
+    zero = tight & (wt == 0)
+    if zero.any():
+        hop = np.where(par != big, 0, -1)
+        if 0 <= source < n:
+            hop[source] = 0
+        zu, zv = u[zero], v[zero]
+        lvl = 0
+        while True:
+            e = (hop[zu] == lvl) & (hop[zv] < 0)
+            if 0 <= source < n:
+                e &= zv != source
+            if not e.any():
+                break
+            np.minimum.at(par, zv[e], zu[e])
+            hop[zv[e]] = lvl + 1
+            lvl += 1
+    par[par == big] = -1
     if 0 <= source < n:
         par[source] = source
     return par

@@ -107,6 +107,45 @@ def test_kronecker_generator_matches_spec(ctx, oracle):
         assert (grow == row).all() and (gcol.astype(np.uint32) == col).all()
 
 
+@pytest.mark.parametrize("weighted", [False, True])
+def test_kronecker_csr_s20_exact(ctx, oracle, weighted):
+    """The GPU Kronecker -> radix sort -> CSR build at s20 (2^25 entries) against the
+    oracle's independent pjo_kronecker + coord2csr (:117-159): identical row offsets and
+    columns; weighted rows are weight-sorted with ties in file order (a stable sort of the
+    oracle's file-order rows by weight)."""
+    g = ctx.generate_kronecker(20, 16, 1, weighted=weighted)
+    grow, gcol, gw = g.get_csr()
+    g.close()
+    s, d, w = oracle.kronecker(20, 16, 1, weighted=weighted)
+    row, col, wc = oracle.coo2csr(s, d, 1 << 20, w)
+    del s, d, w
+    assert (grow == row).all()
+    if weighted:
+        o = np.lexsort((wc, np.repeat(np.arange(1 << 20), np.diff(row))))
+        col, wc = col[o], wc[o]
+        assert (np.asarray(gw, np.uint32) == wc).all()
+    assert (gcol.view(np.uint32) == col).all()
+
+
+def test_kronecker_csr_s26w_full_size_digest(ctx, oracle):
+    """configs[2]'s graph at full size (s26, 2^31 entries, weights 1..255, built by two
+    radix sorts on the GPU): every row's entry count and order-free (col, w) hash sum
+    equal the digest computed on the host straight from the generator spec (no sort, no
+    CSR; symmetric with equal weights by construction), and every row is weight-sorted."""
+    import os
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8") or 8)))
+    g = ctx.generate_kronecker(26, 16, 1, weighted=True)
+    row, col, w = g.get_csr()
+    g.close()
+    assert len(col) == 1 << 31
+    gdeg, ghs, unsorted = oracle.csr_row_digest(row, col, w, threads=threads)
+    del col, w
+    assert unsorted == 0
+    deg, hs = oracle.kronecker_row_digest(26, 16, 1, True, threads=threads)
+    assert (gdeg == deg).all()
+    assert (ghs == hs).all()
+
+
 @pytest.mark.parametrize("scale", [10, 14, 16])
 def test_bfs_kronecker(ctx, oracle, scale):
     g = ctx.generate_kronecker(scale, 16, 2)
@@ -436,26 +475,52 @@ def test_weighted_kronecker_s26_full_size(ctx):
     torch.cuda.empty_cache()
 
 
-def test_partitioned_bfs_s28_full_size(ctx):
-    """BASELINE.json configs[3]'s solver (part.hip + partition.py, 1D vertex partition)
-    at world 1 on the full Kronecker s28 (2^33 entries, 64-bit row offsets): gathered
-    distances proven exact by the certificate against the CSR of the same graph built
-    by the single-GPU loader (a different code path: kronecker -> radix sort -> CSR)."""
+def test_partitioned_bfs_s28_full_size(ctx, pj):
+    """BASELINE.json configs[3] at full size: Kronecker s28 (2^33 entries, 64-bit row
+    offsets), 1D vertex partition at world 1 (no exchange), and at world 2 and 4 with
+    every rank on the one GPU over the host transport (each rank builds only its own
+    rows; per level: owner-packed send regions, the count exchange, the alltoallv of ids
+    (the reference's :522-554, buffers sized at :495-501), the visited all-gather around
+    pull levels and the termination allreduce :589-590). Every world must give the same
+    gathered distances, which are proven exact by the certificate against the CSR of the
+    same graph built by the single-GPU loader (kronecker -> radix sort -> CSR)."""
     import torch
     from helpers import sssp_certificate
-    from paralleljohnson_amd.partition import Comm, load_kronecker
+    from paralleljohnson_amd.partition import Comm, bfs_group, gather_group, load_kronecker
+    roots, dists = [], {}
     ops = load_kronecker(ctx, 28, 16, 1, 0, 1)
     comm = Comm.for_rank(ctx, 1, 0)
-    dists = {}
     for c in np.random.default_rng(8).integers(0, 1 << 28, 64):  # bench.py's root rule: reached > 1
         st = ops.bfs(comm, int(c))
         if st["reached"] > 1:
-            dists[int(c)] = ops.gather_dist(comm)
-            assert st["reached"] == int((dists[int(c)] < INF).sum())
-        if len(dists) == 2:
+            d = ops.gather_dist(comm)
+            assert st["reached"] == int((d < INF).sum())
+            roots.append(int(c))
+            dists[int(c)] = d
+        if len(roots) == 2:
             break
     ops.close()
+    comm.close()
     torch.cuda.empty_cache()
+    for world in (2, 4):
+        ctxs = [pj.Context(0) for _ in range(world)]
+        comms = Comm.group(ctxs, "host")
+        parts = [load_kronecker(ctxs[r], 28, 16, 1, r, world) for r in range(world)]
+        assert sum(p.nnz_local for p in parts) == 1 << 33
+        for r in roots:
+            st = bfs_group(parts, comms, r)
+            assert len({(x["levels"], x["td_levels"], x["bu_levels"]) for x in st}) == 1  # same loop on every rank
+            assert sum(x["sent"] for x in st) > 0  # the owner exchange ran
+            assert st[0]["reached"] == int((dists[r] < INF).sum()), (world, r)
+            got = gather_group(parts, comms)
+            assert np.array_equal(got, dists[r]), (world, r)
+        for p in parts:
+            p.close()
+        for c in comms:
+            c.close()
+        for c in ctxs:
+            c.close()
+        torch.cuda.empty_cache()
     g = ctx.generate_kronecker(28, 16, 1)
     assert g.nnz == 1 << 33
     row, col, _ = g.get_csr()
@@ -464,3 +529,39 @@ def test_partitioned_bfs_s28_full_size(ctx):
         assert sssp_certificate(row, col, None, d, r, device="cuda", chunk=1 << 28) == [], r
         assert (d < INF).sum() > (1 << 26)
     torch.cuda.empty_cache()
+
+
+def test_partitioned_weighted_s22_world2(ctx, pj):
+    """The weighted 1D partition (wpart.hip + the C++ band loop) on the full Kronecker s22
+    with weights 1..255 at world 2 (ranks sharing the GPU over the host transport):
+    gathered distances equal the single-GPU delta-stepping solver's and are proven exact
+    by the certificate; the remote-candidate exchange ran."""
+    import torch
+    from helpers import sssp_certificate
+    from paralleljohnson_amd.partition import Comm, delta_group, gather_group, load_weighted
+    world = 2
+    ctxs = [pj.Context(0) for _ in range(world)]
+    comms = Comm.group(ctxs, "host")
+    gs = [c.generate_kronecker(22, 16, 1, weighted=True) for c in ctxs]
+    parts = [load_weighted(ctxs[r], gs[r], r, world) for r in range(world)]
+    roots = [int(r) for r in gs[0].sample_roots(2, 2)]
+    for r in roots:
+        st = delta_group(parts, comms, r)
+        assert sum(x["sent"] for x in st) > 0
+        assert len({(x["bands"], x["rounds"]) for x in st}) == 1
+        got = gather_group(parts, comms)
+        exp = gs[0].sssp(r)
+        assert np.array_equal(got, exp), r
+        assert st[0]["reached"] == int((exp < INF).sum())
+    row, col, w = gs[0].get_csr()
+    for p in parts:
+        p.close()
+    for g in gs:
+        g.close()
+    for c in comms:
+        c.close()
+    for c in ctxs:
+        c.close()
+    torch.cuda.empty_cache()
+    # the certificate of the last solve's distances (got) against the single-GPU CSR
+    assert sssp_certificate(row, col, w, got, roots[-1], device="cuda", chunk=1 << 27) == []

@@ -129,6 +129,28 @@ def test_kronecker_spec(oracle):
     assert deg.max() > 20 * deg.mean()  # skewed (Kronecker), not uniform
 
 
+@pytest.mark.parametrize("weighted", [False, True])
+def test_row_digest_pins(oracle, weighted):
+    """The order-free row digest computed from the generator spec (no COO, no CSR) equals
+    the digest of coord2csr's CSR of pjo_kronecker's COO; a weight-sorted row order keeps
+    the digest and has no out-of-order entries; one changed entry changes the digest."""
+    s, d, w = oracle.kronecker(12, 16, 5, weighted=weighted)
+    row, col, wc = oracle.coo2csr(s, d, 1 << 12, w)
+    deg, hs = oracle.kronecker_row_digest(12, 16, 5, weighted, threads=3)
+    cdeg, chs, _ = oracle.csr_row_digest(row, col, wc, threads=2)
+    assert (deg == cdeg).all() and (hs == chs).all()
+    assert (deg == np.diff(row)).all()
+    if weighted:
+        rid = np.repeat(np.arange(1 << 12), np.diff(row))
+        o = np.lexsort((wc, rid))  # stable: ties keep file order
+        sdeg, shs, bad = oracle.csr_row_digest(row, col[o], wc[o])
+        assert bad == 0 and (shs == hs).all()
+        assert oracle.csr_row_digest(row, col, wc)[2] > 0  # file order is not weight order
+    col2 = col.copy()
+    col2[len(col2) // 2] ^= 1
+    assert (oracle.csr_row_digest(row, col2, wc)[1] != hs).sum() == 1
+
+
 def test_sssp_certificate_checker(oracle):
     """The full-size GPU tests prove exactness with helpers.sssp_certificate (no CPU
     solve at 2^31 entries); here the checker itself is pinned: it accepts the oracle's

@@ -96,6 +96,23 @@ def test_checks_weighted_cpu(oracle):
         assert sum(_bad(graph500_checks(row, col, wc, dist, p, int(s[0]))).values()) > 0, name
 
 
+def test_zero_weight_tree_is_acyclic(oracle):
+    """Zero-weight edges: two vertices at the same distance must not parent each other
+    (source 9 -> 2 (w 1), 1 <-> 2 (w 0), 2 -> 3 (w 0), 3 -> 1 (w 0)): 2 takes its positive
+    tight in-edge, 1 and 3 are parented by hop depth through the zero-weight edges."""
+    src = np.array([9, 1, 2, 2, 3], np.uint32)
+    dst = np.array([2, 2, 1, 3, 1], np.uint32)
+    w = np.array([1, 0, 0, 0, 0], np.uint32)
+    row, col, wc = oracle.coo2csr(src, dst, 10, w)
+    dist = oracle.dijkstra(row, col, wc, 9)
+    assert dist[[1, 2, 3, 9]].tolist() == [1, 1, 1, 0]
+    par = tight_parents(row, col, wc, dist, 9)
+    assert par[[1, 2, 3, 9]].tolist() == [2, 9, 2, 9]
+    assert _bad(graph500_checks(row, col, wc, dist, par, 9)) == ZERO
+    p = par.copy(); p[2] = 1  # the old smallest-tight-parent rule: 1 <-> 2 cycle
+    assert graph500_checks(row, col, wc, dist, p, 9)["bad_cycle"] > 0
+
+
 # ---------------------------------------------------------------------- GPU --
 
 def _check_graph(g, root, rng, corrupt=True):
@@ -124,6 +141,24 @@ def test_parent_tree_random_graphs(ctx, kind, weighted):
         w = rng.integers(1, 30, len(s)).astype(np.uint32) if weighted else None
         g = ctx.load_coo(s, d, w=w, n=n)
         _check_graph(g, int(s[0]) if len(s) else 0, rng)
+        g.close()
+
+
+@pytest.mark.gpu
+def test_parent_tree_zero_weights(ctx, oracle):
+    """Weights 0..3 (zero-weight cycles at equal distance): the tree is acyclic, equal to
+    the CPU restatement, and passes every Graph500 check (advisor case included)."""
+    rng = np.random.default_rng(77)
+    g = ctx.load_coo(np.array([9, 1, 2, 2, 3]), np.array([2, 2, 1, 3, 1]), w=np.array([1, 0, 0, 0, 0], np.uint32), n=10)
+    _check_graph(g, 9, rng, corrupt=False)
+    assert g.parent_tree()[[1, 2, 3, 9]].tolist() == [2, 9, 2, 9]
+    g.close()
+    for kind in ("uniform", "hub", "chain"):
+        n = int(rng.integers(1000, 30000))
+        s, d = random_graph(rng, kind, n)
+        w = rng.integers(0, 4, len(s)).astype(np.uint32)
+        g = ctx.load_coo(s, d, w=w, n=n)
+        _check_graph(g, int(s[0]), rng)
         g.close()
 
 
