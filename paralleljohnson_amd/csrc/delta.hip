@@ -889,6 +889,8 @@ struct V2Args {
     int dense_pull;   // light pulls in tile-dense form (v2_dense_pull_body)        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
     const u64* sbits; // tail mode: settled-before-the-tail bitmap; relaxations skip its targets
     u64* swrite;      // the heavy step entering the tail writes that bitmap (pull / select)
+    const u32* fesplit;  // the heavy step entering the tail counts the next frontier's edges with the
+                         // tail's light prefixes (lsplit2), so its first round sees its true push cost
     u64* mb;
     V2Ctl* ctl;
     u32* hv;     // [3][hcap]
@@ -1445,7 +1447,7 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fo
             if (lane == 0) a.swrite[wi] = sm;
         }
         if (d >= a.lo && d < mn) mn = d;
-        if (mem) fe += a.lsplit[v];
+        if (mem) fe += (a.fesplit ? a.fesplit : a.lsplit)[v];
         if (lane == 0) fout[wi] = m;
         c += lane == 0 ? (u32)__popcll(m) : 0u;
     }
@@ -1566,7 +1568,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                 if (cur < nhi) {  // cur >= hi always here
                     const i64 wl = (v >> 6) - gbase;
                     atomicOr(&newb[2 * wl + ((v >> 5) & 1)], 1u << (v & 31));
-                    fe += a.lsplit[v];
+                    fe += (a.fesplit ? a.fesplit : a.lsplit)[v];
                 }
             }
         }
@@ -2643,6 +2645,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 }
                 w.sb.ensure((size_t)nwords);
                 a.swrite = w.sb.p;
+                a.fesplit = w.lsplit2.p;
             }
             if (can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh) {
                 v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi_t, cs);
@@ -2669,6 +2672,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 tail = true;
                 a.hl = nullptr;  // the tail's light prefixes come from lsplit2
                 a.swrite = nullptr;
+                a.fesplit = nullptr;
                 a.sbits = w.sb.p;
                 a.lsplit = w.lsplit2.p;
                 a.ltail = 1;
