@@ -1229,7 +1229,9 @@ int pj_wpart_apply(pj_wpart* p, const uint64_t* recv, int64_t n_recv, int light,
     if (!p || n_recv < 0 || (n_recv > 0 && !recv)) return arg_error("pj_wpart_apply: bad argument");
     return guarded([&] {
         bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
-        wpart_apply(*reinterpret_cast<WPart*>(p), (const u64*)recv, n_recv, light, lo, hi);
+        WPart& P = *reinterpret_cast<WPart*>(p);
+        wpart_apply(P, (const u64*)recv, n_recv, light, lo, hi);
+        PJ_HIP(hipStreamSynchronize(wpart_ctx(P).stream));  // the caller may reuse recv on return
         return (int)PJ_OK;
     });
 }

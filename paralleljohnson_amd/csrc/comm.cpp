@@ -251,7 +251,7 @@ struct RcclComm final : Comm {
 
     void init_buffers() {
         PJ_HIP(hipSetDevice(device));
-        const size_t cap = std::max<size_t>(64, (size_t)world * (size_t)(world + 1));
+        const size_t cap = std::max<size_t>(64, (size_t)world * (size_t)(world + 8));
         scratch.alloc(cap);
         host.alloc(cap);
     }
@@ -350,6 +350,16 @@ struct RcclComm final : Comm {
     }
     // the loops' own stream waits after a collective (end of a solve, gathers)
     void sync(hipStream_t s) override { wait(s); }
+
+    bool rows_on_device() const override { return true; }
+    void allgather_rows_dev(const i64* dev_row, int k, i64* host_all, hipStream_t s) override {
+        usable();
+        if (k < 1 || (size_t)world * (size_t)k > scratch.n) throw Error(PJ_ERR_ARG, "allgather_rows_dev: row too long");
+        nccl_check(rccl().allGather(dev_row, scratch.p, (size_t)k, ncclInt64, c, s), "ncclAllGather(rows)");
+        PJ_HIP(hipMemcpyAsync(host.p, scratch.p, sizeof(i64) * (size_t)world * (size_t)k, hipMemcpyDeviceToHost, s));
+        wait(s);
+        std::copy(host.p, host.p + (size_t)world * (size_t)k, host_all);
+    }
 };
 
 }  // namespace

@@ -66,6 +66,23 @@ void bfs_engine(BfsSteps& S, Comm& comm, i64 source, const BfsParams& prm, bool 
         i64 f[3];
         S.begin(source, f);
         comm.allreduce(f, 3, false, s);
+        // device rows (RCCL): a level's counts exchange and its termination statistics
+        // each cost one collective and one host wait, with no readback by the step
+        const bool dev = comm.rows_on_device() && S.counts_dev() && S.stats_dev();
+        std::vector<i64> rows((size_t)S.world * (size_t)std::max(S.world, 5));
+        auto end_level = [&](i64* f3) {
+            if (!dev) {
+                S.end_level(f3);
+                comm.allreduce(f3, 3, false, s);
+                return;
+            }
+            S.end_level_async();
+            comm.allgather_rows_dev(S.stats_dev(), 5, rows.data(), s);
+            S.end_level_finish(rows.data() + 5 * (size_t)S.rank);
+            f3[0] = f3[1] = f3[2] = 0;
+            for (int q = 0; q < S.world; ++q)
+                for (int j = 0; j < 3; ++j) f3[j] += rows[5 * (size_t)q + (size_t)j];
+        };
         i64 n_f = f[0], m_f = f[1];
         i64 n_r = n_f, m_r = m_f, m_u = nnz_global - m_f;
         int mode = 0, level = 0;
@@ -78,10 +95,19 @@ void bfs_engine(BfsSteps& S, Comm& comm, i64 source, const BfsParams& prm, bool 
         while (n_f > 0 && level + 1 < INT_INF) {
             const i64 prev_n_f = n_f;
             if (mode == 0) {
-                S.push(level, counts.data());
                 i64 nr = 0;
+                if (dev) {
+                    S.push(level, nullptr);
+                    comm.allgather_rows_dev(S.counts_dev(), S.world, rows.data(), s);
+                    for (int q = 0; q < S.world; ++q) {
+                        counts[(size_t)q] = rows[(size_t)S.rank * S.world + (size_t)q];
+                        rcounts[(size_t)q] = rows[(size_t)q * S.world + (size_t)S.rank];
+                    }
+                } else {
+                    S.push(level, counts.data());
+                    if (exchanges(comm)) comm.alltoall_counts(counts.data(), rcounts.data(), s);
+                }
                 if (exchanges(comm)) {
-                    comm.alltoall_counts(counts.data(), rcounts.data(), s);
                     comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u32), s);
                     for (int q = 0; q < S.world; ++q) {
                         sent += counts[(size_t)q];
@@ -94,8 +120,7 @@ void bfs_engine(BfsSteps& S, Comm& comm, i64 source, const BfsParams& prm, bool 
                 S.pull(level);
                 ++bu;
             }
-            S.end_level(f);
-            comm.allreduce(f, 3, false, s);
+            end_level(f);
             n_f = f[0];
             m_f = f[1];
             n_r += n_f;
@@ -148,16 +173,34 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             }
             S.apply(nr, light, lo, hi);
         };
+        // device rows (RCCL): a band's size and min pending distance in one collective, a
+        // round's frontier size in one, each with one host wait
+        const bool dev = comm.rows_on_device() && S.select_dev() && S.nf_dev();
+        std::vector<i64> rows((size_t)S.world * 2);
         i64 lo = 0;
         while (lo < INT_INF) {
             const i64 hi = std::min<i64>(lo + delta, INT_INF);
-            i64 sel[2];
-            S.select((int32_t)lo, (int32_t)hi, sel);
-            i64 cnt = sel[0];
-            comm.allreduce(&cnt, 1, false, s);
+            i64 cnt = 0, mn = INT_INF;
+            if (dev) {
+                S.select_async((int32_t)lo, (int32_t)hi);
+                comm.allgather_rows_dev(S.select_dev(), 2, rows.data(), s);
+                S.select_finish();
+                for (int q = 0; q < S.world; ++q) {
+                    const u64 m = (u64)rows[2 * (size_t)q];
+                    mn = std::min<i64>(mn, m >= (u64)INT_INF ? (i64)INT_INF : (i64)m);
+                    cnt += rows[2 * (size_t)q + 1];
+                }
+            } else {
+                i64 sel[2];
+                S.select((int32_t)lo, (int32_t)hi, sel);
+                cnt = sel[0];
+                comm.allreduce(&cnt, 1, false, s);
+                if (cnt == 0) {
+                    mn = sel[1];
+                    comm.allreduce(&mn, 1, true, s);
+                }
+            }
             if (cnt == 0) {
-                i64 mn = sel[1];
-                comm.allreduce(&mn, 1, true, s);
                 if (mn >= INT_INF) break;
                 lo = std::max<i64>(mn / delta * delta, hi);  // the next occupied band
                 continue;
@@ -166,8 +209,15 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             for (;;) {  // light rounds until no rank has a frontier
                 exchange_apply(1, (int32_t)lo, (int32_t)hi);
                 ++rounds;
-                i64 nf = S.end_round();
-                comm.allreduce(&nf, 1, false, s);
+                i64 nf = 0;
+                if (dev) {
+                    S.end_round_async();
+                    comm.allgather_rows_dev(S.nf_dev(), 1, rows.data(), s);
+                    for (int q = 0; q < S.world; ++q) nf += rows[(size_t)q];
+                } else {
+                    nf = S.end_round();
+                    comm.allreduce(&nf, 1, false, s);
+                }
                 if (nf == 0) break;
             }
             exchange_apply(0, (int32_t)lo, (int32_t)hi);  // heavy edges of the band's members

@@ -47,6 +47,16 @@ struct Comm {
     virtual void sync(hipStream_t s) {
         if (s) PJ_HIP(hipStreamSynchronize(s));
     }
+    // Device rows (RCCL): every rank's k-value device row, gathered to the host
+    // (world x k values, rank-major) by one collective and one device->host copy.
+    // The loops use it for step results that stay on the device (the per-owner
+    // counts of a push, the level / band statistics), instead of a host readback
+    // by the step plus a host-staged collective: one host wait instead of two.
+    virtual bool rows_on_device() const { return false; }
+    virtual void allgather_rows_dev(const i64* dev_row, int k, i64* host_all, hipStream_t s) {
+        (void)dev_row, (void)k, (void)host_all, (void)s;
+        throw Error(PJ_ERR_COMM, "allgather_rows_dev: not supported by this transport");
+    }
 };
 
 std::unique_ptr<Comm> make_self_comm();
@@ -76,6 +86,15 @@ struct BfsSteps {
     virtual void apply(int level, i64 n_recv) = 0;
     virtual void pull(int level) = 0;
     virtual void end_level(i64* st3) = 0;
+    // Device-resident results (nullptr: host values only). push(level, nullptr)
+    // leaves the per-owner counts at counts_dev() (world values); end_level_async()
+    // leaves the 5-value level row (n_f, m_f, frontier vertices with edges, -, a
+    // nonzero "foreign id received" flag) at stats_dev(), and end_level_finish(own)
+    // consumes this rank's row once it is on the host.
+    virtual const i64* counts_dev() { return nullptr; }
+    virtual const i64* stats_dev() { return nullptr; }
+    virtual void end_level_async() {}
+    virtual void end_level_finish(const i64* own5) { (void)own5; }
 };
 
 // The pj_wpart_* steps; send / recv hold world * block u64 (id | cand << 32).
@@ -91,6 +110,14 @@ struct DeltaSteps {
     virtual void apply(i64 n_recv, int light, int32_t lo, int32_t hi) = 0;
     virtual i64 end_round() = 0;
     virtual void reach(i64* out2) = 0;
+    // Device-resident results (nullptr: host values only): select_async() leaves the
+    // row (min pending dist as u64, band size) at select_dev(); end_round_async() leaves
+    // the new frontier size at nf_dev(); the finish calls reset the step's counters.
+    virtual const i64* select_dev() { return nullptr; }
+    virtual const i64* nf_dev() { return nullptr; }
+    virtual void select_async(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
+    virtual void select_finish() {}
+    virtual void end_round_async() {}
 };
 
 struct BfsParams {

@@ -723,6 +723,19 @@ void part_end_level(Part& p, u64* vis, i64* out3) {
     read_stats(p, out3);
 }
 
+// device-row form of part_end_level: the kernel leaves stat[0..4]; the transport
+// gathers the rows; finish takes this rank's row (already on the host)
+static void part_end_level_async(Part& p, u64* vis) {
+    if (p.off64) end_level_impl<u64>(p, vis);
+    else end_level_impl<u32>(p, vis);
+}
+static void part_end_level_finish(Part& p, const i64* own5) {
+    if (own5[4]) throw Error(PJ_ERR_COMM, "received ids owned by another rank (corrupted exchange)");
+    p.nq = (u64)own5[2];
+    p.mq = (u64)own5[1];
+    PJ_HIP(hipMemsetAsync(p.stat.p, 0, sizeof(u64) * 8, p.ctx->stream));
+}
+
 void part_begin(Part& p, i64 source, const u64* iso, u64* vis, i64* out3) {
     hipStream_t s = p.ctx->stream;
     PartArgs a = part_args(p, vis);
@@ -752,8 +765,9 @@ void push_impl(Part& p, int level, u64* vis, u32* packed, i64* counts) {
     }
     part_pack_k<<<(unsigned)p.ctx->cu_count * 4, TB, 0, s>>>(a, packed);
     PJ_LAUNCH_CHECK();
-    PJ_HIP(hipMemcpyAsync(p.hstat.p + 8, p.stat.p + 8, sizeof(u64) * (size_t)p.world, hipMemcpyDeviceToHost, s));
     PJ_HIP(hipMemsetAsync(p.ctr.p, 0, p.ctr.bytes(), s));
+    if (!counts) return;  // device rows: the transport reads stat[8 ..] itself
+    PJ_HIP(hipMemcpyAsync(p.hstat.p + 8, p.stat.p + 8, sizeof(u64) * (size_t)p.world, hipMemcpyDeviceToHost, s));
     PJ_HIP(hipStreamSynchronize(s));
     for (int o = 0; o < p.world; ++o) counts[o] = (i64)p.hstat.p[8 + o];
 }
@@ -835,6 +849,10 @@ struct PartGpuSteps final : BfsSteps {
     void apply(int level, i64 nr) override { part_apply(p, level, vis_b.p, recv_b.p, nr); }
     void pull(int level) override { part_pull(p, level, vis_b.p); }
     void end_level(i64* st3) override { part_end_level(p, vis_b.p, st3); }
+    const i64* counts_dev() override { return reinterpret_cast<const i64*>(p.stat.p + 8); }
+    const i64* stats_dev() override { return reinterpret_cast<const i64*>(p.stat.p); }
+    void end_level_async() override { part_end_level_async(p, vis_b.p); }
+    void end_level_finish(const i64* own5) override { part_end_level_finish(p, own5); }
 };
 
 }  // namespace

@@ -609,12 +609,16 @@ int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
     return delta;
 }
 
-void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2) {
+static void wpart_select_async(WPart& p, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
     p.clear_stat();
     PJ_HIP(hipMemsetAsync(p.stat.p + ST_MIN, 0xFF, sizeof(u64), s));
     wp_select_k<<<grid_for(p.bw * 64, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi));
     PJ_LAUNCH_CHECK();
+}
+
+void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2) {
+    wpart_select_async(p, lo, hi);
     p.read_stat();
     out2[0] = (i64)p.hstat[ST_CNT];
     out2[1] = p.hstat[ST_MIN] >= (u64)INT_INF ? (i64)INT_INF : (i64)p.hstat[ST_MIN];
@@ -655,15 +659,20 @@ void wpart_apply(WPart& p, const u64* recv, i64 nr, int light, int32_t lo, int32
         wp_apply_k<<<grid_for(nr, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), recv, nr, light);
         PJ_LAUNCH_CHECK();
     }
-    PJ_HIP(hipStreamSynchronize(s));
+    // (no wait: the next step that needs the host -- end_round's counters or the
+    // transport's row gather -- waits for the stream after this kernel)
 }
 
 // The round's new frontier becomes current; returns its size on this rank (the
 // marks counted by the round's relax and apply: each vertex once, by the
 // atomicOr's old bit).
-i64 wpart_end_round(WPart& p) {
+static void wpart_end_round_async(WPart& p) {
     wp_swap_k<<<grid_for(p.bw, 256, p.grid()), 256, 0, p.ctx->stream>>>(p.args());
     PJ_LAUNCH_CHECK();
+}
+
+i64 wpart_end_round(WPart& p) {
+    wpart_end_round_async(p);
     p.read_stat();
     return (i64)p.hstat[ST_NF];
 }
@@ -706,6 +715,11 @@ struct WPartGpuSteps final : DeltaSteps {
     void apply(i64 nr, int light, int32_t lo, int32_t hi) override { wpart_apply(p, recv_b.p, nr, light, lo, hi); }
     i64 end_round() override { return wpart_end_round(p); }
     void reach(i64* out2) override { wpart_reach(p, out2); }
+    // device rows: [ST_MIN, ST_CNT] and ST_NF of the stat block
+    const i64* select_dev() override { return reinterpret_cast<const i64*>(p.stat.p + ST_MIN); }
+    const i64* nf_dev() override { return reinterpret_cast<const i64*>(p.stat.p + ST_NF); }
+    void select_async(int32_t lo, int32_t hi) override { wpart_select_async(p, lo, hi); }
+    void end_round_async() override { wpart_end_round_async(p); }
 };
 
 }  // namespace
