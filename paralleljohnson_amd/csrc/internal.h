@@ -209,7 +209,8 @@ struct Graph {
     int dense_pull = 0;    // delta v2: light pull rounds in tile-dense form (0/1; measured equal)
     int light_pack = 1;    // delta v2: light CSR records packed in 32 bits when they fit (0/1)
     int split_w = 1;       // delta v2: whole-CSR reads as u32 ids + u8 weights when every weight <= 255 (0/1)
-    int tail_pull = 0;     // delta v2: light pull rounds allowed in the tail too (0/1; within noise)
+    int tail_pull = 1;     // delta v2: light pull rounds allowed in the tail too (round 3: 391 -> 428 GTEPS, once
+                           // the tail-entry frontier counts its whole rows, fesplit)
     int spin_sync = 1;     // delta v2: the host spins on a published sequence word instead of a stream sync (0/1)
     int merged_round = 1;  // delta v2: one launch per light round decides pull / dense / sparse push (0/1)
     int defer_check = 1;   // delta v2 (merged rounds): no host check right after a heavy step (0/1)

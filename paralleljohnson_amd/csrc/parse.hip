@@ -33,7 +33,10 @@ __device__ __forceinline__ bool is_blank(u32 c) {
 // (p == 0 or text[p-1] == '\n'). The buffer is zero-padded to a multiple of
 // 64 bytes (+PTAIL), and '\0' is neither a digit nor a newline. `prev` is
 // text[seg - 1] ('\n' at seg 0).
-__device__ __forceinline__ u64 line_start_mask_w(const u32 (&words)[16], u32 prev) {
+__device__ __forceinline__ u64 line_start_mask(const uint4* __restrict__ p4, u32 prev) {
+    uint4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
+    u32 words[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                     a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
     u64 mask = 0;
 #pragma unroll
     for (int k = 0; k < 64; ++k) {
@@ -43,18 +46,12 @@ __device__ __forceinline__ u64 line_start_mask_w(const u32 (&words)[16], u32 pre
     }
     return mask;
 }
-__device__ __forceinline__ u64 line_start_mask(const uint4* __restrict__ p4, u32 prev) {
-    uint4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
-    const u32 words[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
-                           a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-    return line_start_mask_w(words, prev);
-}
 
 // One `>> int` extraction from bytes t[0, len) (t: the LDS window of the
 // block, or the whole text in global memory). 1 = read, 0 = failed on a
 // non-blank (value 0), -1 = nothing but blanks before end of line, -2 = overflow.
 template <typename T>
-__device__ __forceinline__ int extract(T t, int64_t len, int64_t& p, i64& out) {
+__device__ __forceinline__ int extract(const T* __restrict__ t, int64_t len, int64_t& p, i64& out) {
     while (p < len && is_blank(t[p])) ++p;
     if (p >= len || t[p] == '\n') return -1;
     bool neg = false;
@@ -84,7 +81,8 @@ __device__ __forceinline__ int extract(T t, int64_t len, int64_t& p, i64& out) {
 // One line: `src dst [w]` with the reference's `>> int` semantics (:92-93).
 // Returns false when the line is undefined behaviour for the reference.
 template <typename T>
-__device__ __forceinline__ bool parse_line(T t, int64_t len, int64_t& p, bool weighted, i64& u, i64& v, i64& wt) {
+__device__ __forceinline__ bool parse_line(const T* __restrict__ t, int64_t len, int64_t& p, bool weighted, i64& u,
+                                           i64& v, i64& wt) {
     u = 0;
     v = 0;
     wt = 1;
@@ -119,48 +117,26 @@ __global__ __launch_bounds__(PB) void parse_count_k(const uint8_t* __restrict__ 
 // The block's 16 KiB chunk plus a PTAIL-byte tail is loaded into LDS with
 // coalesced 16-byte loads; every lane then parses the lines that start in its
 // 64-byte segment from LDS (byte loads from global were stride-64 across the
-// wave: one cache line per lane per byte). In LDS every 64-byte segment is
-// followed by 4 bytes of padding (PSTRIDE = 68 bytes = 17 banks): the lanes of
-// a wave read their segments at about the same offset, and at a 64-byte stride
-// those reads all fell in the same bank (ds_read_u8 serialised across the
-// wave); at 17 dwords they spread over the banks.
-constexpr int PSTRIDE = PSEG + 4;
-constexpr int PWIN = (int)(PCHUNK + PTAIL);            // window bytes
-constexpr int PWIN_LDS = PWIN / PSEG * PSTRIDE;        // padded LDS bytes
-struct PadWin {  // byte i of the window, in the padded LDS layout
-    const uint8_t* p;
-    __device__ __forceinline__ u32 operator[](int64_t i) const { return p[i + ((i >> 6) << 2)]; }
-};
+// wave: one cache line per lane per byte).
 __global__ __launch_bounds__(PB) void parse_lines_k(const uint8_t* __restrict__ text, i64 len, int weighted,
                                                     const u64* __restrict__ block_off, u32* __restrict__ src,
                                                     u32* __restrict__ dst, u32* __restrict__ w,
                                                     u64* __restrict__ maxid, u64* __restrict__ errpos) {
     __shared__ u64 lds[PB / WAVE];
-    __shared__ u32 stage[PWIN_LDS / 4];
+    __shared__ uint4 stage[(PCHUNK + PTAIL) / 16];
     const i64 base = (i64)blockIdx.x * PCHUNK;
     const uint4* g4 = reinterpret_cast<const uint4*>(text + base);
-    for (int k = threadIdx.x; k < PWIN / 16; k += PB) {  // 16 window bytes -> 4 padded dwords
-        const uint4 x = g4[k];
-        u32* d = stage + (k * 16 + (k >> 2) * 4) / 4;
-        d[0] = x.x;
-        d[1] = x.y;
-        d[2] = x.z;
-        d[3] = x.w;
-    }
+    for (int k = threadIdx.x; k < (int)((PCHUNK + PTAIL) / 16); k += PB) stage[k] = g4[k];
     __syncthreads();
-    const PadWin sb{reinterpret_cast<const uint8_t*>(stage)};
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage);
     // lines are parsed from the LDS window (ds_read_u8) up to its end; a line that
     // reaches the end of the window is parsed again from global memory
-    const int64_t wlen = min((i64)PWIN, len - base);
+    const int64_t wlen = min((i64)(PCHUNK + PTAIL), len - base);
     const i64 seg = base + (i64)threadIdx.x * PSEG;
     u64 mask = 0;
     if (seg < len) {
-        const u32 prev = seg == 0 ? (u32)'\n' : (threadIdx.x ? sb[threadIdx.x * PSEG - 1] : (u32)text[seg - 1]);
-        const u32* sw = stage + threadIdx.x * (PSTRIDE / 4);
-        u32 words[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) words[k] = sw[k];
-        mask = line_start_mask_w(words, prev);
+        const u32 prev = seg == 0 ? (u32)'\n' : (threadIdx.x ? (u32)sb[threadIdx.x * PSEG - 1] : (u32)text[seg - 1]);
+        mask = line_start_mask(reinterpret_cast<const uint4*>(sb + threadIdx.x * PSEG), prev);
     }
     u64 tot;
     u64 idx = block_off[blockIdx.x] + block_excl_scan<PB / WAVE>((u64)__popcll(mask), lds, tot);

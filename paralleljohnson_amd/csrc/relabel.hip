@@ -76,12 +76,9 @@ __global__ __launch_bounds__(256) void copy_rows_k(const u32* __restrict__ perm,
     for (i64 i = (i64)blockIdx.x * (blockDim.x / WAVE) + wave_id(); i < nrows; i += nwaves) {
         const u32 o = perm[i];
         const Off b = orow[o], d = orow[o + 1] - b, nb = nrow[i];
-        // the edge streams are read and written once: nontemporal, so they do not
-        // evict inv (256 MB at s26, the random lookups) from the Infinity Cache
         for (Off k = (Off)lane_id(); k < d; k += WAVE) {
-            const u32 oc = __builtin_nontemporal_load(ocol + b + k);
-            __builtin_nontemporal_store(inv[oc], ncol + nb + k);
-            __builtin_nontemporal_store(__builtin_nontemporal_load(ow + b + k), nw + nb + k);
+            ncol[nb + k] = inv[ocol[b + k]];
+            nw[nb + k] = ow[b + k];
         }
     }
 }
