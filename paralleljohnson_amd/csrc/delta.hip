@@ -897,6 +897,7 @@ struct V2Args {
     u64* hbeg;   // [3][hcap]
     u64* hoff;   // [3][hcap]
     u64 hcap;
+    u64* rlog;   // round_log option: [0] = rounds logged, then (kind, frontier, its light edges) per round
 };
 // the light edges of a band round (light CSR, or the light prefixes of cw in the tail)
 __device__ __forceinline__ ESrc v2_cw_src(const V2Args& a) {
@@ -1951,6 +1952,15 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
         v2_clear_words(fclr, a.nwords);
     }
     const u64 fcount = v2_slot_sum(a.ctl->cnt[cin]);
+    if (a.rlog && merged && blockIdx.x == 0 && threadIdx.x == 0 && fcount) {  // (debug: round_log)
+        const u64 fe0 = v2_slot_edges(a.ctl->cnt[cin]);
+        const u64 i = atomicAdd(a.rlog, 1ull);
+        if (i < 255) {
+            a.rlog[1 + 3 * i] = fe0 > pull_thresh ? 2ull : (fcount > dense_min ? 1ull : 0ull);
+            a.rlog[2 + 3 * i] = fcount;
+            a.rlog[3 + 3 * i] = fe0 | ((u64)a.lo << 40);
+        }
+    }
     if (fcount == 0) return;
     if (v2_slot_edges(a.ctl->cnt[cin]) <= pull_thresh) {
         if (fcount <= dense_min) {  // a sparse push round
@@ -2474,6 +2484,12 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     a.hbeg = w.hbeg.p;
     a.hoff = w.hoff.p;
     a.hcap = w.hcap;
+    DevBuf<u64> rlog;
+    if (g.round_log) {
+        rlog.alloc(1 + 3 * 255);
+        PJ_HIP(hipMemsetAsync(rlog.p, 0, sizeof(u64), s));
+        a.rlog = rlog.p;
+    }
     // the host's view of the counters: one block copies them into mapped host memory
     // (a D2H hipMemcpyAsync of the same 3.3 KB ran as a ~30 us blit per sync)
     // The host spins on the sequence number (wakes within ~1 us of the copy instead of
@@ -2517,6 +2533,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         u64 heavy_left = w.heavy_total, light_left = w.light_total;
         const bool can_pull = g.symmetric && g.pull_factor > 0.0;
         bool can_pull_light = g.symmetric && g.light_pull > 0.0;
+        double light_pull = g.light_pull;  // (tail_light_pull once in the tail)
         bool tail = false;
         u64 tail_unsettled = 0;
         const int32_t tdelta = (int32_t)std::min(65536.0, g.tail_delta < 0 ? 64.0 * delta : g.tail_delta);
@@ -2544,7 +2561,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             // idle rounds cost more than the checks they save)
             int K = PJ_V2_STATS ? 1 : g.round_batch;
             for (;;) {
-                const u64 pull_thresh = can_pull_light ? (u64)((double)light_left / g.light_pull) : ~0ull;
+                const u64 pull_thresh = can_pull_light ? (u64)((double)light_left / light_pull) : ~0ull;
                 // launch the pull kernels (which decide on the device, per round) only
                 // when the last frontier seen could grow past the threshold in this batch
                 const bool try_pull = can_pull_light && (double)last_fe * g.pull_grow > (double)pull_thresh;
@@ -2679,7 +2696,8 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 bw = tdelta;
                 // light pulls in the tail (tail_pull): rows are scanned in weight order and
                 // stop at the first w with lo + w >= the vertex's distance
-                can_pull_light = can_pull_light && g.tail_pull;
+                can_pull_light = g.symmetric && g.tail_pull;
+                light_pull = g.tail_light_pull;
                 tail_unsettled = heavy_left + light_left;
                 if ((long long)tdelta > w.maxw) {
                     heavy_left = 0;  // every edge is light in the tail
@@ -2729,6 +2747,15 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
     g.stats = st;
     g.have_result = true;
+    if (g.round_log) {  // debug: one stderr line per non-empty light round
+        std::vector<u64> h(1 + 3 * 255);
+        PJ_HIP(hipMemcpy(h.data(), rlog.p, sizeof(u64) * h.size(), hipMemcpyDeviceToHost));
+        static const char* kind[3] = {"push", "dense", "pull"};
+        for (u64 i = 0; i < std::min<u64>(h[0], 255); ++i)
+            fprintf(stderr, "round %llu lo %llu %s frontier %llu light_edges %llu\n", (unsigned long long)i,
+                    (unsigned long long)(h[3 + 3 * i] >> 40), kind[h[1 + 3 * i] % 3], (unsigned long long)h[2 + 3 * i],
+                    (unsigned long long)(h[3 + 3 * i] & ((1ull << 40) - 1)));
+    }
 }
 
 }  // namespace

@@ -200,6 +200,8 @@ struct Graph {
     double light_pull = 3.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
                                // the light edges of unsettled vertices / light_pull (0 = never; 2 -> 3 at
                                // the end of round 2 with merged rounds: +1%, interleaved A/B)
+    double tail_light_pull = 3.0;  // the same rule in the tail's rounds
+    int round_log = 0;         // debug: per light round (kind, frontier, light edges) on stderr
     int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
     int level_batch = 0; // BFS levels enqueued per host check (0 = the previous solve's count, then 2, 4, 8, ...)
