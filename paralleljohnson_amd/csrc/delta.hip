@@ -832,6 +832,23 @@ __global__ __launch_bounds__(DB) void wsum_k(const u32* __restrict__ w, i64 n, u
 //                 once per batch of light rounds and once per band.
 // ---------------------------------------------------------------------------
 constexpr int V2_SC = 16;     // frontier words a wave screens at once
+#ifndef PJ_V2_ORPRE
+#define PJ_V2_ORPRE 0  // frontier marks: read the word first, atomicOr only when the bit is clear
+#endif
+#ifndef PJ_V2_NOATOM
+#define PJ_V2_NOATOM 0  // TIMING EXPERIMENT ONLY (wrong results): plain stores instead of atomicMin
+#endif
+// a light relaxation's dist update and frontier mark (1 = newly marked)
+__device__ __forceinline__ void v2_dmin(int32_t* p, int32_t v) {
+    if (PJ_V2_NOATOM) *p = v;
+    else atomicMin(p, v);
+}
+__device__ __forceinline__ bool v2_mark(u64* __restrict__ fout, u32 t) {
+    const u64 bit = 1ull << (t & 63);
+    if (PJ_V2_ORPRE && (__hip_atomic_load(fout + (t >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
+        return false;
+    return !(atomicOr(fout + (t >> 6), bit) & bit);
+}
 #ifndef PJ_V2_LS
 #define PJ_V2_LS 2  // swept 1, 2, 4 (round 2 end): 1 ~ 2, 4 is ~1% slower
 #endif
@@ -928,10 +945,9 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
     if (a.sbits && ((a.sbits[t >> 6] >> (t & 63)) & 1ull)) return 0u;
     if (nd < INT_INF && (int32_t)nd < dist_now(a.dist + t)) {
         if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
-        atomicMin(a.dist + t, (int32_t)nd);  // no return: see v2_relax_g
+        v2_dmin(a.dist + t, (int32_t)nd);  // no return: see v2_relax_g
         if (LIGHT && (int32_t)nd < a.hi) {
-            const u64 bit = 1ull << (t & 63);
-            const u32 nw = (atomicOr(fout + (t >> 6), bit) & bit) ? 0u : 1u;
+            const u32 nw = v2_mark(fout, t) ? 1u : 0u;
             if (PJ_V2_STATS && nw) atomicAdd(&a.ctl->dbg[3].v, 1ull);
             if (nw) fe += a.lsplit[t];  // the next round's push cost
             return nw;
@@ -985,10 +1001,9 @@ __device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const ESrc ed, u64 k,
 #pragma unroll
     for (int j = 0; j < PU; ++j) {
         if (ok[j] && (int32_t)nd[j] < cd[j]) {
-            atomicMin(a.dist + t[j], (int32_t)nd[j]);
+            v2_dmin(a.dist + t[j], (int32_t)nd[j]);
             if (LIGHT && (int32_t)nd[j] < a.hi) {
-                const u64 bit = 1ull << (t[j] & 63);
-                if (!(atomicOr(fout + (t[j] >> 6), bit) & bit)) {
+                if (v2_mark(fout, t[j])) {
                     ++newc;
                     fe += a.lsplit[t[j]];
                 }
@@ -1032,10 +1047,9 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         if (ok[j] && (int32_t)nd[j] < cd[j]) {
-            atomicMin(a.dist + t[j], (int32_t)nd[j]);
+            v2_dmin(a.dist + t[j], (int32_t)nd[j]);
             if (LIGHT && (int32_t)nd[j] < a.hi) {
-                const u64 bit = 1ull << (t[j] & 63);
-                if (!(atomicOr(fout + (t[j] >> 6), bit) & bit)) {
+                if (v2_mark(fout, t[j])) {
                     ++newc;
                     fe += a.lsplit[t[j]];
                 }
