@@ -852,6 +852,8 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "light_pull" && value >= 0) g.light_pull = value;
     else if (k == "tail_light_pull" && value > 0) g.tail_light_pull = value;
     else if (k == "round_log" && (value == 0 || value == 1)) g.round_log = (int)value;
+    else if (k == "bin_min" && value >= 0) g.bin_min = value;
+    else if (k == "bin_watch" && value >= 0) g.bin_watch = value;
     else if (k == "pull_grow" && value >= 0) g.pull_grow = value;
     else if (k == "band_width" && value >= 0) g.band_width = value;
     else if (k == "tail_delta") g.tail_delta = value;

@@ -2013,6 +2013,366 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     v2_flush2(mh, ml, a.ctl->mh, red);
 }
 
+// ---------------------------------------------------------------------------
+// Binned light rounds (host-decided, symmetric graphs, outside the tail).
+//
+// A big push round is bound by its random accesses: per light edge a 4-byte
+// probe of dist[t] (a 64-byte line from the Infinity Cache or HBM) and, when it
+// improves, a device-scope atomicMin executed at the memory side (round 3: 24M
+// and 32M light edges took 0.95 and 0.91 ms, 25-35 G edges/s; with the atomics
+// replaced by plain stores, a timing-only build, still ~0.5 ms). A binned round
+// has no random access and no global atomic per edge:
+//   gen    : the frontier's light edges become pairs (t << 32 | dist[u] + w),
+//            staged in LDS per coarse bucket (a vertex range holding ~1/64 of the
+//            light-edge mass) and flushed in runs, one cursor atomic per run;
+//            long segments go through the hub queue and v2_hub_k<BIN>
+//   fine   : each chunk of a coarse bucket's pairs is counting-sorted in LDS by
+//            fine bucket (2^14 vertices) and written out in runs
+//   reduce : one workgroup per fine bucket: dist of its range into LDS, an LDS
+//            atomicMin per pair, then improved distances and the next frontier's
+//            words stored whole (the workgroup owns the range)
+// Regions need no sizing pass: on a symmetric graph a vertex receives at most one
+// pair per light in-edge = light out-edge, so the pairs of a vertex range fit the
+// range's span of the light CSR, [lrow[a], lrow[b]), in both pair buffers.
+// ---------------------------------------------------------------------------
+constexpr int BIN_FLOG = 14;     // fine bucket: 2^14 vertices = 64 KB of LDS minima
+constexpr int BIN_FINE = 1 << BIN_FLOG;
+constexpr int BIN_NB1 = 128;     // most coarse buckets
+constexpr int BIN_SB = 32;       // pairs staged per coarse bucket before a flush
+constexpr int BIN_SPAN = 256;    // most fine buckets per coarse bucket
+constexpr int BIN_CH = 4096;     // pairs per chunk of the fine pass
+constexpr int BIN_MASS = 64;     // coarse buckets are cut at 1/BIN_MASS of the light-edge mass
+
+struct BinArgs {
+    u64* p1;             // pairs (t << 32 | nd) in coarse regions
+    u64* p2;             // pairs in fine regions
+    u64* c1;             // [BIN_NB1] coarse cursors (zeroed by the reduce)
+    u64* c2;             // [nfine] fine cursors (zeroed by the reduce)
+    const u64* r1;       // [nb1 + 1] coarse region starts
+    const u64* r2;       // [nfine + 1] fine region starts = lrow[f << BIN_FLOG]
+    const uint8_t* f2c;  // [nfine] coarse bucket of each fine bucket
+    const u32* cb;       // [nb1 + 1] first fine bucket of each coarse bucket
+    int nb1, nfine;
+};
+
+struct BinStage {
+    u64 p[BIN_NB1][BIN_SB];
+    u32 cnt[BIN_NB1];
+    u64 base[BIN_NB1];
+};
+
+__device__ __forceinline__ void bin_stage_init(BinStage& st) {
+    for (int c = threadIdx.x; c < BIN_NB1; c += blockDim.x) st.cnt[c] = 0;
+}
+
+// one pair into the block's staging (a full bucket goes straight to its region)
+__device__ __forceinline__ void bin_put(const BinArgs& b, BinStage& st, u32 t, u32 nd) {
+    const u32 c = b.f2c[t >> BIN_FLOG];
+    const u64 pr = ((u64)t << 32) | nd;
+    const u32 pos = atomicAdd(&st.cnt[c], 1u);
+    if (pos < (u32)BIN_SB) st.p[c][pos] = pr;
+    else b.p1[b.r1[c] + atomicAdd(&b.c1[c], 1ull)] = pr;
+}
+
+// collective: every staged run to its coarse region (one cursor atomic per run)
+__device__ __forceinline__ void bin_flush(const BinArgs& b, BinStage& st) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < b.nb1; c += blockDim.x) {
+        const u32 k = min(st.cnt[c], (u32)BIN_SB);
+        st.base[c] = k ? atomicAdd(&b.c1[c], (u64)k) : 0ull;
+    }
+    __syncthreads();
+    const int nwv = (int)blockDim.x / WAVE, lane = lane_id();
+    for (int c = wave_id(); c < b.nb1; c += nwv) {
+        const u32 k = min(st.cnt[c], (u32)BIN_SB);
+        if ((u32)lane < k) b.p1[b.r1[c] + st.base[c] + lane] = st.p[c][lane];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < b.nb1; c += blockDim.x) st.cnt[c] = 0;
+    __syncthreads();
+}
+
+// gen: tile-dense screening of the frontier (as v2_dense_body), pairs for the light
+// segments <= V2_DHT edges, longer ones to the hub queue; new members' degree sums
+template <typename Off>
+__global__ __launch_bounds__(DB) void v2_bin_gen_k(V2Args a, BinArgs b, const Off* __restrict__ row,
+                                                   u64* __restrict__ fin, int cin, int hs, u64* __restrict__ fclr) {
+    __shared__ V2Dense<Off> sh;
+    __shared__ BinStage st;
+    v2_zero_slot(a, (cin + 2) & 3);
+    v2_clear_words(fclr, a.nwords);
+    bin_stage_init(st);
+    const int tid = threadIdx.x, lane = lane_id();
+    const u64 mask = (1ull << V2_EB) - 1ull;
+    const ESrc ed = v2_light_src(a);
+    u64 mh = 0, ml = 0;
+    const i64 ntiles = (a.n + V2_DT - 1) / V2_DT;
+    for (i64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const i64 w0 = tile * (V2_DT / 64);
+        if (tid < V2_DT / 64) {
+            u64 f = 0, nw = 0;
+            if (w0 + tid < a.nwords) {
+                f = fin[w0 + tid];
+                if (f) {
+                    fin[w0 + tid] = 0;
+                    const u64 old = a.mb[w0 + tid];
+                    nw = f & ~old;
+                    if (nw) a.mb[w0 + tid] = old | f;
+                }
+            }
+            sh.f[tid] = f;
+            sh.fnew[tid] = nw;
+        }
+        __syncthreads();
+        u64 anyf = 0;
+#pragma unroll
+        for (int k = 0; k < V2_DT / 64; ++k) anyf |= sh.f[k];
+        if (!anyf) {  // block-uniform
+            __syncthreads();
+            continue;
+        }
+        const int i0 = tid * V2_DV;
+        const i64 v0 = tile * V2_DT + i0;
+        const u32 nib = (u32)(sh.f[i0 >> 6] >> (i0 & 63)) & V2_DVM;
+        const u32 nnew = (u32)(sh.fnew[i0 >> 6] >> (i0 & 63)) & V2_DVM;
+        u64 bb[V2_DV], e[V2_DV];
+        int32_t du[V2_DV];
+#pragma unroll
+        for (int j = 0; j < V2_DV; ++j) {
+            bb[j] = e[j] = 0;
+            du[j] = 0;
+            if ((nib >> j) & 1u) {
+                const i64 v = v0 + j;
+                du[j] = a.dist[v];
+                bb[j] = a.lrow[v];
+                e[j] = a.lrow[v + 1];
+                if ((nnew >> j) & 1u) {
+                    mh += (u64)row[v + 1] - (u64)row[v] - (e[j] - bb[j]);
+                    ml += e[j] - bb[j];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < V2_DV; ++j) {  // long segments -> hub queue (as v2_dense_body)
+            const bool hub = e[j] - bb[j] > V2_DHT;
+            const u64 hm = __ballot(hub);
+            if (hm) {
+                const u64 seg = hub ? e[j] - bb[j] : 0;
+                const u64 ie = wave_incl_scan(seg);
+                const u64 tot = __shfl(ie, 63, 64);
+                const int leader = __ffsll((long long)hm) - 1;
+                u64 base = 0;
+                if (lane == leader) base = atomicAdd(&a.ctl->hub[hs].v, ((u64)__popcll(hm) << V2_EB) | tot);
+                base = __shfl(base, leader, 64);
+                if (hub) {
+                    const u64 slot = (base >> V2_EB) + (u64)__popcll(hm & lanemask_lt());
+                    const u64 q = (u64)hs * a.hcap + slot;
+                    a.hv[q] = (u32)(v0 + j);
+                    a.hbeg[q] = bb[j];
+                    a.hoff[q] = (base & mask) + ie - seg;
+                    e[j] = bb[j];
+                }
+            }
+        }
+        u64 cnt = 0, edges = 0;
+#pragma unroll
+        for (int j = 0; j < V2_DV; ++j)
+            if (e[j] > bb[j]) {
+                ++cnt;
+                edges += e[j] - bb[j];
+            }
+        u64 tot;
+        const u64 ex = block_excl_scan<DB / WAVE>((cnt << V2_EB) | edges, sh.red, tot);
+        u32 slot = (u32)(ex >> V2_EB);
+        u32 eo = (u32)(ex & mask);
+#pragma unroll
+        for (int j = 0; j < V2_DV; ++j)
+            if (e[j] > bb[j]) {
+                sh.b[slot] = (Off)bb[j];
+                sh.du[slot] = du[j];
+                sh.off[slot] = eo;
+                ++slot;
+                eo += (u32)(e[j] - bb[j]);
+            }
+        const u32 ns = (u32)(tot >> V2_EB), te = (u32)(tot & mask);
+        __syncthreads();
+        for (u32 e0 = 0; e0 < te; e0 += DB * V2_DNJ) {  // (te is block-uniform: the flush is collective)
+#pragma unroll
+            for (int j = 0; j < V2_DNJ; ++j) {
+                const u32 x = e0 + (u32)j * DB + (u32)tid;
+                if (x < te) {
+                    const u32 sl = v2_dense_find(sh.off, ns, x);
+                    const u64 r = eat(ed, (u64)sh.b[sl] + (x - sh.off[sl]));
+                    const long long nd = (long long)sh.du[sl] + (long long)(r >> 32);
+                    if (nd < INT_INF) bin_put(b, st, (u32)r, (u32)nd);
+                }
+            }
+            bin_flush(b, st);
+        }
+        __syncthreads();
+    }
+    v2_flush2(mh, ml, a.ctl->mh, sh.red);
+}
+
+// hub segments of a binned round: the tiles of v2_hub_k, emitting pairs
+__global__ __launch_bounds__(DB) void v2_hub_bin_k(V2Args a, BinArgs b, int hs, int hz) {
+    __shared__ LbShared<V2_HTILE> sh;
+    __shared__ int32_t s_du[V2_HTILE];
+    __shared__ u64 s_b[V2_HTILE];
+    __shared__ BinStage st;
+    const u64 packed = a.ctl->hub[hs].v;
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->hub[hz].v = 0;
+    const u64 nq = packed >> V2_EB, total = packed & ((1ull << V2_EB) - 1ull);
+    if (nq == 0) return;
+    bin_stage_init(st);
+    const u32* hv = a.hv + (u64)hs * a.hcap;
+    const u64* hb = a.hbeg + (u64)hs * a.hcap;
+    const u64* ho = a.hoff + (u64)hs * a.hcap;
+    const ESrc ed = v2_light_src(a);
+    for (u64 e0 = (u64)blockIdx.x * V2_HTILE; e0 < total; e0 += (u64)gridDim.x * V2_HTILE) {
+        u64 s0;
+        u32 ns;
+        lb_tile_load<V2_HTILE>(ho, nq, e0, sh, s0, ns);
+        for (u32 i = threadIdx.x; i < ns; i += DB) {
+            s_du[i] = a.dist[hv[s0 + i]];
+            s_b[i] = hb[s0 + i];
+        }
+        __syncthreads();
+        for (u32 j = 0; j < (u32)V2_HTILE; j += DB) {
+            const u64 e = e0 + j + threadIdx.x;
+            if (e < total) {
+                const u32 sl = lb_find<V2_HTILE>(sh, ns, e);
+                const u64 r = eat(ed, s_b[sl] + (e - sh.off[sl]));
+                const long long nd = (long long)s_du[sl] + (long long)(r >> 32);
+                if (nd < INT_INF) bin_put(b, st, (u32)r, (u32)nd);
+            }
+        }
+        bin_flush(b, st);
+    }
+}
+
+// fine: counting sort of each BIN_CH chunk of a coarse bucket's pairs by fine bucket
+__global__ __launch_bounds__(DB) void v2_bin_fine_k(BinArgs b) {
+    __shared__ u64 sp[BIN_CH];
+    __shared__ u32 hist[BIN_SPAN], off[BIN_SPAN];
+    __shared__ u64 gbase[BIN_SPAN];
+    __shared__ u64 cpre[BIN_NB1 + 1];  // chunks before coarse bucket i
+    __shared__ u32 red[DB / WAVE];
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        u64 t = 0;
+        for (int i = 0; i < b.nb1; ++i) {
+            cpre[i] = t;
+            t += (b.c1[i] + BIN_CH - 1) / BIN_CH;
+        }
+        cpre[b.nb1] = t;
+    }
+    __syncthreads();
+    const u64 nchunks = cpre[b.nb1];
+    constexpr int PT = BIN_CH / DB;
+    for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        int i = 0;
+        while (cpre[i + 1] <= ch) ++i;  // (<= 128 buckets, LDS)
+        const u64 j0 = (ch - cpre[i]) * BIN_CH;
+        const u64 cnt1 = b.c1[i];
+        const u32 m = (u32)min((u64)BIN_CH, cnt1 - j0);
+        const u32 fb0 = b.cb[i], nfb = b.cb[i + 1] - fb0;
+        for (u32 k = tid; k < nfb; k += DB) hist[k] = 0;
+        __syncthreads();
+        u64 pr[PT];
+        u32 lf[PT], rk[PT];
+#pragma unroll
+        for (int q = 0; q < PT; ++q) {
+            const u32 x = (u32)q * DB + tid;
+            pr[q] = x < m ? b.p1[b.r1[i] + j0 + x] : 0ull;
+            lf[q] = x < m ? (u32)(pr[q] >> (32 + BIN_FLOG)) - fb0 : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < PT; ++q) rk[q] = ((u32)q * DB + tid < m) ? atomicAdd(&hist[lf[q]], 1u) : 0u;
+        __syncthreads();
+        // exclusive offsets of the fine buckets inside the chunk, and their global bases
+        u32 carry = 0;
+        for (u32 k0 = 0; k0 < nfb; k0 += DB) {
+            const u32 k = k0 + tid;
+            const u32 h = k < nfb ? hist[k] : 0u;
+            u32 tot;
+            const u32 ex = block_excl_scan<DB / WAVE>(h, red, tot);
+            if (k < nfb) {
+                off[k] = carry + ex;
+                gbase[k] = h ? atomicAdd(&b.c2[fb0 + k], (u64)h) : 0ull;
+            }
+            carry += tot;
+            __syncthreads();
+        }
+#pragma unroll
+        for (int q = 0; q < PT; ++q)
+            if ((u32)q * DB + tid < m) sp[off[lf[q]] + rk[q]] = pr[q];
+        __syncthreads();
+        // runs out in LDS order: consecutive threads, consecutive addresses of one fine region
+        for (u32 x = tid; x < m; x += DB) {
+            const u64 p = sp[x];
+            const u32 f = (u32)(p >> (32 + BIN_FLOG)), l = f - fb0;
+            b.p2[b.r2[f] + gbase[l] + (x - off[l])] = p;
+        }
+        __syncthreads();
+    }
+}
+
+// reduce: one workgroup per fine bucket (LDS minima), then the range's improved
+// distances and next-frontier words; zeroes the cursors for the next binned round
+__global__ __launch_bounds__(DB) void v2_bin_reduce_k(V2Args a, BinArgs b, u64* __restrict__ fout, int cin) {
+    __shared__ int32_t best[BIN_FINE];
+    __shared__ u64 words[BIN_FINE / 64];
+    __shared__ u64 red[DB / WAVE];
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0)
+        for (int c = tid; c < b.nb1; c += DB) b.c1[c] = 0;  // (the fine pass has read them)
+    u64 newc = 0, fe = 0;
+    for (int f = blockIdx.x; f < b.nfine; f += gridDim.x) {
+        const u64 np = b.c2[f];
+        if (np == 0) continue;  // block-uniform
+        const i64 v0 = (i64)f << BIN_FLOG;
+        const int nv = (int)min((i64)BIN_FINE, a.n - v0);
+        for (int x = tid; x < nv; x += DB) best[x] = a.dist[v0 + x];
+        __syncthreads();
+        const u64* pp = b.p2 + b.r2[f];
+        for (u64 k = tid; k < np; k += DB) {
+            const u64 p = pp[k];
+            const int32_t nd = (int32_t)(u32)p;
+            const int x = (int)((p >> 32) - (u64)v0);
+            if (nd < best[x]) atomicMin(&best[x], nd);
+        }
+        __syncthreads();
+        // improved distances (plain stores: the workgroup owns the range) and the
+        // range's next-frontier words, built in LDS and stored whole
+        for (int x = tid; x < BIN_FINE / 64; x += DB) words[x] = 0;
+        __syncthreads();
+        for (int x = tid; x < nv; x += DB) {
+            const int32_t bx = best[x];
+            const i64 v = v0 + x;
+            if (bx < a.dist[v]) {
+                a.dist[v] = bx;
+                if (bx < a.hi) {
+                    atomicOr(&words[x >> 6], 1ull << (x & 63));
+                    ++newc;
+                    fe += a.lsplit[v];
+                }
+            }
+        }
+        __syncthreads();
+        for (int x = tid; x < (nv + 63) / 64; x += DB) fout[(v0 >> 6) + x] = words[x];
+        __syncthreads();
+        if (tid == 0) b.c2[f] = 0;
+    }
+    v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+}
+
+// fine region starts: r2[f] = lrow[min(f << BIN_FLOG, n)]
+__global__ void v2_bin_r2_k(const u64* __restrict__ lrow, i64 n, int nfine, u64* __restrict__ r2) {
+    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f <= nfine; f += gridDim.x * blockDim.x)
+        r2[f] = lrow[min((i64)f << BIN_FLOG, n)];
+}
+
 // static chunk list of the long light rows: count, then append (order is irrelevant)
 __global__ void v2_long_count_k(const u32* __restrict__ lsplit, i64 n, u64* __restrict__ cnt) {
     u64 c = 0;
@@ -2054,11 +2414,6 @@ __device__ __forceinline__ u64 v2_rec(const u64* __restrict__ cw, const u32* __r
                                       const u32* __restrict__ wt, u64 k) {
     return cw ? cw[k] : (u64)col[k] | ((u64)wt[k] << 32);
 }
-// A wave takes 64 consecutive vertices, whose light prefixes are one contiguous
-// range of the light CSR, and copies that range edge-balanced: output entry o
-// finds its vertex by binary search over the lanes' inclusive prefix lengths,
-// so the stores are coalesced and no lane walks a prefix alone (a lane per
-// vertex measured 11.4 ms at s26, 0.77 TB/s).
 template <typename Off, typename OutT>
 __global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restrict__ lsplit, const u64* __restrict__ lrow,
                                const u64* __restrict__ cw, const u32* __restrict__ col, const u32* __restrict__ wt,
@@ -2066,19 +2421,18 @@ __global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restric
     const int lane = lane_id();
     for (i64 v0 = ((i64)blockIdx.x * blockDim.x + threadIdx.x) & ~63ll; v0 < n; v0 += (i64)gridDim.x * blockDim.x) {
         const i64 v = v0 + lane;
-        const u64 ls = v < n ? lsplit[v] : 0u;
-        const u64 src = v < n ? (u64)row[v] : 0u;
-        const u64 inc = wave_incl_scan(ls);
-        const u64 tot = __shfl(inc, 63, 64);
-        const u64 dst0 = lrow[v0];  // the group's light range starts here
-        for (u64 r0 = 0; r0 < tot; r0 += WAVE) {  // wave-uniform trip count: every lane shuffles
-            const u64 o = r0 + lane;
-            int l = 0;
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1)
-                if (__shfl(inc, l + step - 1, 64) <= o) l += step;
-            const u64 ex = __shfl(inc - ls, l, 64), sl = __shfl(src, l, 64);
-            if (o < tot) v2_lput(lcw, dst0 + o, v2_rec(cw, col, wt, sl + (o - ex)), cb);
+        const u32 ls = v < n ? lsplit[v] : 0u;
+        const bool longp = ls > 64;
+        if (v < n && !longp)
+            for (u32 j = 0; j < ls; ++j) v2_lput(lcw, lrow[v] + j, v2_rec(cw, col, wt, (u64)row[v] + j), cb);
+        u64 lm = __ballot(longp);
+        while (lm) {
+            const int l = __ffsll((long long)lm) - 1;
+            lm &= lm - 1;
+            const i64 vl = v0 + l;
+            const u64 src = (u64)row[vl], dst = lrow[vl];
+            const u32 cnt = lsplit[vl];
+            for (u32 j = lane; j < cnt; j += WAVE) v2_lput(lcw, dst + j, v2_rec(cw, col, wt, src + j), cb);
         }
     }
 }
@@ -2154,6 +2508,12 @@ struct DeltaWork {
     int packed_for = -1;   // g.light_pack the light CSR was built for
     DevBuf<uint8_t> w8;    // u8 copy of the relabeled weights (max weight <= 255)
     DevBuf<u64> hl;        // has-light-edges bitmap (per delta)
+    // binned light rounds (per delta): pair buffers, cursors, bucket tables
+    DevBuf<u64> bp1, bp2, bc1, bc2, br1, br2;
+    DevBuf<uint8_t> bf2c;
+    DevBuf<u32> bcb;
+    int bnb1 = 0, bnfine = 0;
+    u32 bin_for = 0;       // delta the tables were built for (0 = none)
     ~DeltaWork() {
         if (host) (void)hipHostFree(host);
         if (hctl) (void)hipHostFree(hctl);
@@ -2263,6 +2623,52 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         PJ_HIP(hipStreamSynchronize(s));
     }
     return delta;
+}
+
+// Binned-round tables of the current light CSR: fine region starts (lrow at every
+// 2^14-th vertex), coarse buckets cut greedily at 1/BIN_MASS of the light-edge mass
+// or BIN_SPAN fine buckets, and the two pair buffers (the light CSR's size each).
+// Returns false when the graph needs more than BIN_NB1 coarse buckets.
+bool prepare_bins(DeltaWork& w, i64 n, hipStream_t s) {
+    if (w.bin_for == w.lsplit_delta && w.bnb1 > 0) return true;
+    const int nfine = (int)((n + BIN_FINE - 1) / BIN_FINE);
+    w.br2.alloc((size_t)nfine + 1);
+    v2_bin_r2_k<<<grid_for(nfine + 1, 256, 1024), 256, 0, s>>>(w.lrow.p, n, nfine, w.br2.p);
+    PJ_LAUNCH_CHECK();
+    std::vector<u64> r2((size_t)nfine + 1);
+    PJ_HIP(hipMemcpyAsync(r2.data(), w.br2.p, sizeof(u64) * r2.size(), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    const u64 target = std::max<u64>(1, w.light_total / BIN_MASS);
+    std::vector<u32> cb{0};
+    for (int f = 0; f < nfine; ++f) {
+        const u64 mass = r2[(size_t)f + 1] - r2[cb.back()];
+        if (f + 1 < nfine && (mass >= target || (u32)(f + 1) - cb.back() >= (u32)BIN_SPAN)) cb.push_back((u32)f + 1);
+    }
+    cb.push_back((u32)nfine);
+    const int nb1 = (int)cb.size() - 1;
+    if (nb1 > BIN_NB1 || nfine == 0) return false;
+    std::vector<u64> r1((size_t)nb1 + 1);
+    std::vector<uint8_t> f2c((size_t)nfine);
+    for (int i = 0; i <= nb1; ++i) r1[(size_t)i] = r2[cb[(size_t)i]];
+    for (int i = 0; i < nb1; ++i)
+        for (u32 f = cb[(size_t)i]; f < cb[(size_t)i + 1]; ++f) f2c[f] = (uint8_t)i;
+    w.bcb.alloc(cb.size());
+    w.br1.alloc(r1.size());
+    w.bf2c.alloc(f2c.size());
+    PJ_HIP(hipMemcpyAsync(w.bcb.p, cb.data(), sizeof(u32) * cb.size(), hipMemcpyHostToDevice, s));
+    PJ_HIP(hipMemcpyAsync(w.br1.p, r1.data(), sizeof(u64) * r1.size(), hipMemcpyHostToDevice, s));
+    PJ_HIP(hipMemcpyAsync(w.bf2c.p, f2c.data(), f2c.size(), hipMemcpyHostToDevice, s));
+    w.bp1.ensure(std::max<u64>(w.light_total, 1));
+    w.bp2.ensure(std::max<u64>(w.light_total, 1));
+    w.bc1.ensure(BIN_NB1);
+    w.bc2.alloc((size_t)nfine);
+    PJ_HIP(hipMemsetAsync(w.bc1.p, 0, sizeof(u64) * BIN_NB1, s));
+    PJ_HIP(hipMemsetAsync(w.bc2.p, 0, sizeof(u64) * (size_t)nfine, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    w.bnb1 = nb1;
+    w.bnfine = nfine;
+    w.bin_for = w.lsplit_delta;
+    return true;
 }
 
 template <typename Off>
@@ -2572,6 +2978,23 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         const int32_t tdelta = (int32_t)std::min(65536.0, g.tail_delta < 0 ? 64.0 * delta : g.tail_delta);
         u64 last_fe = 1;  // light edges of the frontier at the last host sync (round 0: unknown)
         u64 last_cnt = 1; // its vertex count
+        bool fe_known = false;  // last_fe / last_cnt describe the next round's frontier
+        // binned light rounds: symmetric graphs with a light CSR, tables per delta
+        BinArgs ba{};
+        const bool bin_ok = g.bin_min > 0 && g.symmetric && !PJ_V2_STATS && w.light_total > 0 &&
+                            prepare_bins(w, n, s);
+        if (bin_ok) {
+            ba.p1 = w.bp1.p;
+            ba.p2 = w.bp2.p;
+            ba.c1 = w.bc1.p;
+            ba.c2 = w.bc2.p;
+            ba.r1 = w.br1.p;
+            ba.r2 = w.br2.p;
+            ba.f2c = w.bf2c.p;
+            ba.cb = w.bcb.p;
+            ba.nb1 = w.bnb1;
+            ba.nfine = w.bnfine;
+        }
         // Deferred band check (merged rounds): after a heavy step the host does not wait
         // for its counters; it enqueues the next band's first rounds at once and learns at
         // their check whether that band had any vertex (its start slot survives the first
@@ -2598,7 +3021,32 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 // launch the pull kernels (which decide on the device, per round) only
                 // when the last frontier seen could grow past the threshold in this batch
                 const bool try_pull = can_pull_light && (double)last_fe * g.pull_grow > (double)pull_thresh;
-                for (int q = 0; q < K; ++q) {
+                // binned round (host-decided, so the check before it must have seen the
+                // frontier): its light edges are many, it is not a pull; a growing frontier
+                // below that size gets single rounds, so the next big one is seen too
+                const bool bin_can = bin_ok && fe_known && !a.ltail && g.merged_round;
+                const bool pull_next = can_pull_light && last_fe > pull_thresh;
+                const bool bin_now = bin_can && !pull_next && last_fe >= (u64)g.bin_min;
+                const int k_now = (bin_can && !bin_now && last_fe >= (u64)g.bin_watch) ? 1 : K;
+                if (bin_now) {
+                    u64* fin = w.f[fi].p;
+                    u64* fout = w.f[(fi + 1) % 3].p;
+                    u64* fclr = w.f[(fi + 2) % 3].p;
+                    v2_bin_gen_k<Off><<<roundgrid, DB, 0, s>>>(a, ba, row, fin, cs, hr, fclr);
+                    PJ_LAUNCH_CHECK();
+                    v2_hub_bin_k<<<hubgrid, DB, 0, s>>>(a, ba, hr, (hr + 1) % 3);
+                    PJ_LAUNCH_CHECK();
+                    v2_bin_fine_k<<<roundgrid, DB, 0, s>>>(ba);
+                    PJ_LAUNCH_CHECK();
+                    v2_bin_reduce_k<<<(unsigned)std::min<i64>(w.bnfine, (i64)ctx.cu_count * 4), DB, 0, s>>>(
+                        a, ba, fout, cs);
+                    PJ_LAUNCH_CHECK();
+                    fi = (fi + 1) % 3;
+                    cs = (cs + 1) & 3;
+                    hr = (hr + 1) % 3;
+                    st.relax_rounds++;
+                }
+                for (int q = 0; q < (bin_now ? 0 : k_now); ++q) {
                     u64* fin = w.f[fi].p;
                     u64* fout = w.f[(fi + 1) % 3].p;
                     u64* fclr = w.f[(fi + 2) % 3].p;
@@ -2634,6 +3082,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                     st.relax_rounds++;
                 }
                 sync_ctl();
+                fe_known = true;
                 if (deferred) {
                     deferred = false;
                     if (slot(cs_start) == 0) {  // the band was empty: its rounds were idle
@@ -2648,6 +3097,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                         a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
                         v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
                         PJ_LAUNCH_CHECK();
+                        fe_known = false;
                         jumped = true;
                         break;
                     }
@@ -2666,7 +3116,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                     PJ_HIP(hipMemsetAsync(w.ctl.p->dbg, 0, sizeof(w.ctl.p->dbg), s));
                 }
                 if (slot(cs) == 0) break;
-                K = PJ_V2_STATS ? 1 : std::min(2 * K, 16);
+                if (!bin_now && k_now == K) K = PJ_V2_STATS ? 1 : std::min(2 * K, 16);
             }
             if (finished) break;
             if (jumped) continue;  // (the select of the jumped-to band is enqueued)
@@ -2743,6 +3193,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             }
             if (defer_ok && !(enter_tail && (long long)tdelta <= w.maxw)) {
                 deferred = true;  // checked at the next band's first publish
+                fe_known = false;
                 lo = hi;
                 continue;
             }
@@ -2762,6 +3213,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
                 v2_select_k<<<maxgrid, DB, 0, s>>>(a, w.f[fi].p, cs);
                 PJ_LAUNCH_CHECK();
+                fe_known = false;
                 continue;
             }
             lo = hi;

@@ -288,6 +288,30 @@ def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
         g.close()
 
 
+@pytest.mark.parametrize("scale,ef", [(12, 16), (16, 16), (18, 8)])
+def test_weighted_binned_rounds(ctx, oracle, scale, ef):
+    """Binned light rounds (delta.hip: the frontier's light edges as (target, dist) pairs,
+    bucketed by target range -- coarse, then 2^14-vertex fine buckets -- and reduced with
+    LDS minima per range) against the oracle Dijkstra: forced on every round after a
+    host check (bin_min 1), on mid-size rounds only, and off; with and without light
+    pulls; several deltas. s18 spans 16 fine buckets in several coarse ones."""
+    g = ctx.generate_kronecker(scale, ef, 40 + scale, weighted=True)
+    row, col, wc = g.get_csr()
+    col = col.astype(np.uint32)
+    roots = [0] + [int(r) for r in g.sample_roots(9, 3)]
+    exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
+    for bmin, bwatch in ((1, 0), (64, 1), (4096, 256), (0, 0)):
+        for lp in (0.0, 3.0):
+            for delta in (0, 5, 40):
+                g.set_option("bin_min", bmin)
+                g.set_option("bin_watch", bwatch)
+                g.set_option("light_pull", lp)
+                g.set_option("delta", delta)
+                for r in roots:
+                    assert (g.sssp(r) == exp[r]).all(), (scale, bmin, bwatch, lp, delta, r)
+    g.close()
+
+
 @pytest.mark.parametrize("scale,ef", [(13, 16), (15, 4)])
 def test_weighted_band_width(ctx, oracle, scale, ef):
     """Bands narrower than the light threshold (delta.hip band_width): light edges
