@@ -202,8 +202,9 @@ struct Graph {
                                // the end of round 2 with merged rounds: +1%, interleaved A/B)
     double tail_light_pull = 3.0;  // the same rule in the tail's rounds
     int round_log = 0;         // debug: per light round (kind, frontier, light edges) on stderr
-    double bin_min = 4194304;  // v2: binned light round when a check saw at least this many light edges
-                               // in the next (push) frontier (0 = never)
+    double bin_min = 0;        // v2: binned light round when a check saw at least this many light edges
+                               // in the next (push) frontier (0 = never; measured 10x slower on k26w:
+                               // degree-ordered ids send most pairs to the first buckets)
     double bin_watch = 524288; // v2: single rounds between checks while the frontier holds this many
     int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
