@@ -870,6 +870,7 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "tail_pull" && (value == 0 || value == 1)) g.tail_pull = (int)value;
     else if (k == "spin_sync" && (value == 0 || value == 1)) g.spin_sync = (int)value;
     else if (k == "merged_round" && (value == 0 || value == 1)) g.merged_round = (int)value;
+    else if (k == "fold_hub" && (value == 0 || value == 1)) g.fold_hub = (int)value;
     else if (k == "defer_check" && (value == 0 || value == 1)) g.defer_check = (int)value;
     else if (k == "round_gpc" && value >= 0 && value <= 64) g.round_gpc = (int)value;
     else if (k == "hub_gpc" && value >= 0 && value <= 64) g.hub_gpc = (int)value;

@@ -1099,6 +1099,9 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     if (!valid) {
         if (n > 0) PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.dist.p), INT_INF, (size_t)n, s));
     } else {
+        // the done word still holds the previous solve's level count until bfs_init_k runs;
+        // clear it here, or the first spin_wait sees it and ends the solve after one batch
+        *(volatile int64_t*)w.host = -1;
         bfs_init_k<Off><<<grid_for(std::max(n / 4, nwords), TB, (unsigned)ctx.cu_count * 4u), TB, 0, s>>>(
             a, gd, w.zmask.p, source, (double)g.nnz);
         PJ_LAUNCH_CHECK();

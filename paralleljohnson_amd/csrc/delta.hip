@@ -882,7 +882,7 @@ struct V2Ctl {
     V2Line cnt[4][V2_NSH];  // frontier vertices marked per light round (ring)
     V2Line hub[3];          // hub queue packed counters (ring)
     V2Line mh[V2_NSH];      // heavy edges of this band's members
-    V2Line minv;            // min dist >= lo of the last select / pull (next band search)
+    V2Line minv[V2_NSH];    // min dist >= lo of the last select / pull (next band search), per shard
     V2Line dbg[8];          // PJ_V2_STATS builds: vertices, edges, atomics, marks, hub edges
 };
 #ifndef PJ_V2_STATS
@@ -965,6 +965,23 @@ __device__ __forceinline__ void v2_flush2(u64 x, u64 e, V2Line* sl, u64* red) {
         if (x) atomicAdd(&sl[blockIdx.x % V2_NSH].v, x);
         if (e) atomicAdd(&sl[blockIdx.x % V2_NSH].pad[0], e);
     }
+}
+// min{mn} of the block into a minv shard: one atomic per workgroup (the heavy pull's
+// 24K waves taking one atomicMin each on one word serialized behind its ~88 per us)
+__device__ __forceinline__ void v2_flush_min(int32_t mn, V2Ctl* ctl, u64* red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int32_t y = __shfl_xor(mn, off, 64);
+        mn = y < mn ? y : mn;
+    }
+    if (lane_id() == 0) red[wave_id()] = (u64)(u32)mn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t m = INT_INF;
+        for (int w = 0; w < DB / WAVE; ++w) m = min(m, (int32_t)(u32)red[w]);
+        if (m < INT_INF) atomicMin(&ctl->minv[blockIdx.x % V2_NSH].v, (u64)m);
+    }
+    __syncthreads();
 }
 __device__ __forceinline__ u64 v2_slot_edges(const V2Line* sl) {
     u64 t = 0;
@@ -1415,29 +1432,26 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
 }
 
 // Edge-balanced relaxation of hub queue hs (slots' edge offsets are monotonic:
-// one packed atomic gave both). Zeroes the next ring slot hz for later appends.
+// one packed atomic gave both), over the whole grid (block-uniform).
+struct V2HubLds {
+    LbShared<V2_HTILE> sh;
+    int32_t s_du[V2_HTILE];
+    u64 s_b[V2_HTILE];
+};
 template <bool LIGHT>
-__global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout, int cin, int hs, int hz) {
-    __shared__ LbShared<V2_HTILE> sh;
-    __shared__ int32_t s_du[V2_HTILE];
-    __shared__ u64 s_b[V2_HTILE];
-    __shared__ u64 red[DB / WAVE];
-    const u64 packed = a.ctl->hub[hs].v;
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->hub[hz].v = 0;
+__device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ fout, int hs, u64 packed, u32& newc,
+                                            u64& fe, V2HubLds& L) {
     const u64 nq = packed >> V2_EB, total = packed & ((1ull << V2_EB) - 1ull);
-    if (nq == 0) return;
     const u32* hv = a.hv + (u64)hs * a.hcap;
     const u64* hb = a.hbeg + (u64)hs * a.hcap;
     const u64* ho = a.hoff + (u64)hs * a.hcap;
-    u32 newc = 0;
-    u64 fe = 0;
     for (u64 e0 = (u64)blockIdx.x * V2_HTILE; e0 < total; e0 += (u64)gridDim.x * V2_HTILE) {
         u64 s0;
         u32 ns;
-        lb_tile_load<V2_HTILE>(ho, nq, e0, sh, s0, ns);
+        lb_tile_load<V2_HTILE>(ho, nq, e0, L.sh, s0, ns);
         for (u32 i = threadIdx.x; i < ns; i += DB) {
-            s_du[i] = a.dist[hv[s0 + i]];
-            s_b[i] = hb[s0 + i];
+            L.s_du[i] = a.dist[hv[s0 + i]];
+            L.s_b[i] = hb[s0 + i];
         }
         __syncthreads();
         constexpr int NJ = V2_HTILE / DB;
@@ -1448,13 +1462,27 @@ __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout,
         for (int j = 0; j < NJ; ++j) {
             const u64 e = e0 + (u64)j * DB + threadIdx.x;
             val[j] = e < total;
-            const u32 sl = val[j] ? lb_find<V2_HTILE>(sh, ns, e) : 0u;
-            idx[j] = val[j] ? s_b[sl] + (e - sh.off[sl]) : 0ull;
-            du[j] = val[j] ? s_du[sl] : 0;
+            const u32 sl = val[j] ? lb_find<V2_HTILE>(L.sh, ns, e) : 0u;
+            idx[j] = val[j] ? L.s_b[sl] + (e - L.sh.off[sl]) : 0ull;
+            du[j] = val[j] ? L.s_du[sl] : 0;
         }
         newc += v2_relax_g<LIGHT, NJ>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), idx, du, val, fout, fe);
         __syncthreads();
     }
+}
+
+// The hub queue hs of one round in its own launch. Zeroes the next ring slot hz for
+// later appends.
+template <bool LIGHT>
+__global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout, int cin, int hs, int hz) {
+    __shared__ V2HubLds L;
+    __shared__ u64 red[DB / WAVE];
+    const u64 packed = a.ctl->hub[hs].v;
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->hub[hz].v = 0;
+    if ((packed >> V2_EB) == 0) return;
+    u32 newc = 0;
+    u64 fe = 0;
+    v2_hub_body<LIGHT>(a, fout, hs, packed, newc, fe, L);
     if (LIGHT) v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
 }
 
@@ -1480,12 +1508,7 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fo
         c += lane == 0 ? (u32)__popcll(m) : 0u;
     }
     v2_flush2(c, fe, a.ctl->cnt[cout], red);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const int32_t y = __shfl_xor(mn, off, 64);
-        mn = y < mn ? y : mn;
-    }
-    if (lane == 0 && mn < INT_INF) atomicMin(&a.ctl->minv.v, (u64)mn);
+    v2_flush_min(mn, a.ctl, red);
 }
 
 // Pull step of the heavy edges of band [lo, hi) fused with the selection of the
@@ -1607,12 +1630,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
         }
     }
     v2_flush2(ccount, fe, a.ctl->cnt[cout], red);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const int32_t y = __shfl_xor(mn, off, 64);
-        mn = y < mn ? y : mn;
-    }
-    if (lane == 0 && mn < INT_INF) atomicMin(&a.ctl->minv.v, (u64)mn);
+    v2_flush_min(mn, a.ctl, red);
 }
 
 // Pull form of a light round (symmetric graphs): every vertex that can still
@@ -1626,7 +1644,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
 template <typename Off>
 __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* __restrict__ row,
                                                    const u64* __restrict__ fin, u64* __restrict__ fout, u32* newb,
-                                                   u32& newc, u64& fe, u64& mh, u64& ml) {
+                                                   u32& newc, u64& fe, u64& mh, u64& ml, bool amin = false) {
     constexpr int NWV = DB / WAVE;
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
@@ -1735,8 +1753,10 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                 }
                 if (lane == l) cur = cl;
             }
-            if (act && cur < d0) {
-                a.dist[v] = cur;
+            // amin: hub tiles of the previous round relax concurrently (fold_hub), so a
+            // plain store could overwrite a lower distance they wrote
+            if (act && cur < d0 && (!amin || cur < atomicMin(a.dist + v, cur))) {
+                if (!amin) a.dist[v] = cur;
                 if (cur < hi) {
                     const i64 wl = (v >> 6) - gbase;
                     atomicOr(&newb[2 * wl + ((v >> 5) & 1)], 1u << (v & 31));
@@ -1957,9 +1977,10 @@ __device__ __forceinline__ void v2_dense_pull_body(const V2Args& a, const Off* _
 }
 
 template <typename Off>
-union V2RoundLds {  // the round kernel's LDS: a dense push or a dense pull, never both
+union V2RoundLds {  // the round kernel's LDS: the folded hub tiles, then a dense push or a dense pull
     V2Dense<Off> push;
     V2DensePull<Off> pull;
+    V2HubLds hub;
 };
 
 // Pull form of a light round, one launch: the chunks of the long light rows
@@ -1969,7 +1990,8 @@ template <typename Off>
 __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
                                                       u64* __restrict__ fout, int cin, u64 pull_thresh,
                                                       const u32* __restrict__ lcv, const u32* __restrict__ lcc, u64 nlc,
-                                                      int hs, u64 dense_min, u64* __restrict__ fclr, int merged) {
+                                                      int hs, u64 dense_min, u64* __restrict__ fclr, int merged,
+                                                      int fold, int hin) {
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
     __shared__ u64 red[NWV];
@@ -1977,6 +1999,23 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     if (merged) {  // the whole round in this launch: no v2_expand_k behind it
         v2_zero_slot(a, (cin + 2) & 3);
         v2_clear_words(fclr, a.nwords);
+    }
+    // fold_hub: no hub launch behind the round. The hub tiles of the previous round
+    // (queue hin, complete at this kernel boundary) are relaxed here first, into this
+    // round's output frontier -- a label-correcting delay of one round, exact in any
+    // order (R9). The round appends its own long segments to queue hs, which the next
+    // round relaxes; block 0 zeroes the ring slot after hs for the round after that.
+    bool hub_pending = false;
+    if (fold) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->hub[(hs + 1) % 3].v = 0;
+        const u64 packed = hin >= 0 ? a.ctl->hub[hin].v : 0ull;
+        if (packed >> V2_EB) {
+            hub_pending = true;
+            u32 hn = 0;
+            u64 hfe = 0;
+            v2_hub_body<true>(a, fout, hin, packed, hn, hfe, lds.hub);
+            v2_flush2(hn, hfe, a.ctl->cnt[(cin + 1) & 3], red);
+        }
     }
     const u64 fcount = v2_slot_sum(a.ctl->cnt[cin]);
     if (a.rlog && merged && blockIdx.x == 0 && threadIdx.x == 0 && fcount) {  // (debug: round_log)
@@ -2007,7 +2046,7 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     if (a.dense_pull && !a.ltail) {
         v2_dense_pull_body<Off>(a, row, fin, fout, newc, fe, mh, ml, lds.pull);
     } else {
-        v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml);
+        v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml, hub_pending);
     }
     v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
     v2_flush2(mh, ml, a.ctl->mh, red);
@@ -2839,7 +2878,7 @@ __global__ __launch_bounds__(256) void v2_publish_k(V2Ctl* __restrict__ ctl, u64
         ctl->mh[threadIdx.x].v = 0;
         ctl->mh[threadIdx.x].pad[0] = 0;
     }
-    if (threadIdx.x == 0) ctl->minv.v = ~0ull;
+    if (threadIdx.x < V2_NSH) ctl->minv[threadIdx.x].v = ~0ull;
 }
 
 // solve start in one launch: dist := INF (the source 0), frontier 0 := {source},
@@ -2857,10 +2896,8 @@ __global__ void v2_init_k(int32_t* __restrict__ dist, i64 n, i64 nwords, i64 src
         u64* c = reinterpret_cast<u64*>(ctl);
         for (int i = threadIdx.x; i < (int)(sizeof(V2Ctl) / sizeof(u64)); i += blockDim.x) c[i] = 0;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            ctl->minv.v = ~0ull;
-            if (src >= 0) ctl->cnt[0][0].v = 1;
-        }
+        if (threadIdx.x < V2_NSH) ctl->minv[threadIdx.x].v = ~0ull;
+        if (threadIdx.x == 0 && src >= 0) ctl->cnt[0][0].v = 1;
     }
 }
 
@@ -2955,6 +2992,11 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         for (int i = 0; i < V2_NSH; ++i) t += w.hctl->cnt[c][i].v;
         return t;
     };
+    auto hminv = [&]() {
+        u64 m = ~0ull;
+        for (int i = 0; i < V2_NSH; ++i) m = std::min<u64>(m, w.hctl->minv[i].v);
+        return m;
+    };
 
     pj_stats st{};
     const bool valid = source >= 0 && source < g.n;
@@ -3001,6 +3043,11 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         // two rounds of the counter ring) and, if not, the next occupied band (minv of the
         // heavy step, copied by the same publish before it resets minv).
         const bool defer_ok = g.merged_round && g.defer_check && !PJ_V2_STATS && g.round_batch <= 2;
+        // fold_hub: the hub tiles of light round r run inside round r + 1's launch (no hub
+        // launch per round); not with binned rounds (their own hub kernel) or tile-dense
+        // pulls (plain distance stores)
+        const bool fold = g.fold_hub && g.merged_round && !bin_ok && !g.dense_pull;
+        bool hub_pend = false;  // the last light round launched may have queued hub segments
         bool deferred = false;
         bool finished = false;
         while (lo < INT_INF && !finished) {
@@ -3054,7 +3101,8 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                         // one launch decides pull / tile-dense push / sparse push on the device
                         v2_pull_round_k<Off><<<roundgrid, DB, 0, s>>>(a, row, fin, fout, cs,
                                                                      can_pull_light ? pull_thresh : ~0ull, w.lcv.p,
-                                                                    w.lcc.p, w.nlc, hr, dense_min, fclr, 1);
+                                                                    w.lcc.p, w.nlc, hr, dense_min, fclr, 1,
+                                                                    fold ? 1 : 0, hub_pend ? (hr + 2) % 3 : -1);
                         PJ_LAUNCH_CHECK();
                     } else {
                         // the round kernel also runs dense push rounds (v2_dense_body): whenever it
@@ -3066,7 +3114,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                         if (try_pull || try_dense) {
                             v2_pull_round_k<Off><<<pullgrid, DB, 0, s>>>(a, row, fin, fout, cs,
                                                                         try_pull ? pull_thresh : ~0ull, w.lcv.p,
-                                                                        w.lcc.p, w.nlc, hr, dmin, nullptr, 0);
+                                                                        w.lcc.p, w.nlc, hr, dmin, nullptr, 0, 0, -1);
                             PJ_LAUNCH_CHECK();
                         }
                         // (without the round kernel the expand must push every round)
@@ -3074,8 +3122,12 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                                                                       try_pull ? pull_thresh : ~0ull, dmin, fclr);
                         PJ_LAUNCH_CHECK();
                     }
-                    v2_hub_k<true><<<hubgrid, DB, 0, s>>>(a, fout, cs, hr, (hr + 1) % 3);
-                    PJ_LAUNCH_CHECK();
+                    if (fold) {
+                        hub_pend = true;  // (the next round relaxes this round's hub queue)
+                    } else {
+                        v2_hub_k<true><<<hubgrid, DB, 0, s>>>(a, fout, cs, hr, (hr + 1) % 3);
+                        PJ_LAUNCH_CHECK();
+                    }
                     fi = (fi + 1) % 3;
                     cs = (cs + 1) & 3;
                     hr = (hr + 1) % 3;
@@ -3083,11 +3135,14 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 }
                 sync_ctl();
                 fe_known = true;
+                // fold_hub: the band's light work is done only when the last round's frontier
+                // AND its hub queue (relaxed by the next round) are empty
+                const bool hubs_left = hub_pend && (w.hctl->hub[(hr + 2) % 3].v >> V2_EB) != 0;
                 if (deferred) {
                     deferred = false;
                     if (slot(cs_start) == 0) {  // the band was empty: its rounds were idle
                         st.levels--;
-                        const u64 mv = w.hctl->minv.v;
+                        const u64 mv = hminv();
                         if (mv >= (u64)INT_INF) {  // nothing reached beyond the settled bands
                             finished = true;
                             break;
@@ -3099,6 +3154,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                         PJ_LAUNCH_CHECK();
                         fe_known = false;
                         jumped = true;
+                        hub_pend = false;  // (idle rounds: no hubs queued)
                         break;
                     }
                 }
@@ -3115,7 +3171,10 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                             w.hctl->dbg[4].v, w.hctl->dbg[3].v, slot(cs));
                     PJ_HIP(hipMemsetAsync(w.ctl.p->dbg, 0, sizeof(w.ctl.p->dbg), s));
                 }
-                if (slot(cs) == 0) break;
+                if (slot(cs) == 0 && !hubs_left) {
+                    hub_pend = false;
+                    break;
+                }
                 if (!bin_now && k_now == K) K = PJ_V2_STATS ? 1 : std::min(2 * K, 16);
             }
             if (finished) break;
@@ -3206,7 +3265,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             for (int i = 0; i < V2_NSH; ++i) last_fe += w.hctl->cnt[cs][i].pad[0];
             last_cnt = slot(cs);
             if (slot(cs) == 0) {
-                const u64 mv = w.hctl->minv.v;
+                const u64 mv = hminv();
                 if (mv >= (u64)INT_INF) break;  // nothing reached beyond the settled bands
                 lo = (long long)mv / bw * bw;  // jump to the next occupied band
                 a.lo = (int32_t)lo;

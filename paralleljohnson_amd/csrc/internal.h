@@ -218,6 +218,7 @@ struct Graph {
     int tail_pull = 1;     // delta v2: light pull rounds allowed in the tail too (round 3: 391 -> 428 GTEPS, once
                            // the tail-entry frontier counts its whole rows, fesplit)
     int spin_sync = 1;     // delta v2: the host spins on a published sequence word instead of a stream sync (0/1)
+    int fold_hub = 1;      // delta v2: a light round's hub tiles run in the next round's launch (0/1)
     int merged_round = 1;  // delta v2: one launch per light round decides pull / dense / sparse push (0/1)
     int defer_check = 1;   // delta v2 (merged rounds): no host check right after a heavy step (0/1)
     int round_gpc = 12;    // delta v2: workgroups per CU of the light-round / hub launches (0 = the heavy

@@ -40,17 +40,33 @@ constexpr int MS_U = PJ_MS_U;  // pull: in-edges a lane loads per serial step
 constexpr int MS_WMAX = 16;  // widest pass: 1024 sources (option ms_width)
 constexpr int MS_WDEF = 8;   // default widest pass: 512 sources
 
+constexpr int MS_NSH = 16;  // shards of the per-level edge counter (one 64-B line each)
+
 struct MsCtl {
     u64 active[3];  // ring: level L reads [(L+2)%3] (level L-1), writes [L%3], block 0 zeroes [(L+1)%3]
-    u64 fedges[3];  // same ring: out-edges of the vertices newly reached by a level (its frontier's push cost)
     u64 done;       // set once by block 0 of the first level that finds nothing to do
+    u64 pad[4];
+    // same ring: out-edges of the vertices newly reached by a level (its frontier's push
+    // cost), summed over MS_NSH shards: every workgroup of a level adds its count, and one
+    // word taking them all saturates at ~88 atomics per microsecond
+    u64 fedges[3][MS_NSH][8];
 };
+
+__device__ __forceinline__ u64 ms_fedges(const MsCtl* c, int slot) {
+    u64 t = 0;
+#pragma unroll
+    for (int i = 0; i < MS_NSH; ++i) t += c->fedges[slot][i][0];
+    return t;
+}
+__device__ __forceinline__ void ms_add_fedges(MsCtl* c, int slot, u64 x) {
+    atomicAdd(&c->fedges[slot][blockIdx.x % MS_NSH][0], x);
+}
 
 // Direction of level L, identical in every kernel of the level: push (top-down,
 // atomicOr of the frontier masks into the targets' next masks) while the last
 // frontier's out-edges are few, else pull over in-edges.
 __device__ __forceinline__ bool ms_is_push(const MsCtl* c, int32_t L, u64 push_max) {
-    return c->fedges[(L + 2) % 3] < push_max;
+    return ms_fedges(c, (L + 2) % 3) < push_max;
 }
 __device__ __forceinline__ bool ms_live(const MsCtl* c, int32_t L) {
     return c->active[(L + 2) % 3] != 0 && L + 1 < INT_INF;
@@ -113,6 +129,9 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
 #ifndef PJ_MS_GPC
 #define PJ_MS_GPC 4  // level-kernel workgroups per CU
 #endif
+// (filling the distance block here, ~0.43 ms per 512-source pass at 4.4 TB/s on the
+// web-Google-shaped graph, is cheaper than writing INT_INF for the unreached pairs at
+// the end of the pass, measured 0.72 ms: that loop's stores are mostly partial)
 __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __restrict__ F, i64 nw,
                                                 int32_t* __restrict__ dist, i64 nb_dist, MsCtl* ctl,
                                                 int64_t* host_done) {
@@ -120,7 +139,7 @@ __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __rest
     if (tid == 0) {
         for (int i = 0; i < 3; ++i) {
             ctl->active[i] = 0;
-            ctl->fedges[i] = 0;
+            for (int j = 0; j < MS_NSH; ++j) ctl->fedges[i][j][0] = 0;
         }
         ctl->done = 0;
         *host_done = -1;
@@ -147,7 +166,7 @@ __global__ void ms_sources_k(const int64_t* __restrict__ src, int ns, int W, i64
     atomicOr(&F[s * W + (i >> 6)], 1ull << (i & 63));
     dist[(i64)i * n + s] = 0;
     ctl->active[2] = 1;  // "level -1" found the sources
-    atomicAdd(&ctl->fedges[2], (u64)(row[s + 1] - row[s]));
+    atomicAdd(&ctl->fedges[2][0][0], (u64)(row[s + 1] - row[s]));
 }
 
 // First kernel of level L: ends the pass when level L-1 found nothing, zeroes
@@ -162,9 +181,9 @@ __global__ __launch_bounds__(MB) void ms_prep_k(i64 n, u64* __restrict__ Fn, int
         }
         return;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctl->active[(L + 1) % 3] = 0;
-        ctl->fedges[(L + 1) % 3] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < MS_NSH) {
+        if (threadIdx.x == 0) ctl->active[(L + 1) % 3] = 0;
+        ctl->fedges[(L + 1) % 3][threadIdx.x][0] = 0;
     }
     if (!ms_is_push(ctl, L, push_max)) return;
     ulonglong2* p = reinterpret_cast<ulonglong2*>(Fn);
@@ -274,7 +293,7 @@ __global__ __launch_bounds__(MB) void ms_fin_k(i64 n, const Off* __restrict__ ro
         ms_write_dist<W>(newb, dist, n, v, L + 1);
     }
     fe = block_sum<MB / WAVE>(fe, red);
-    if (threadIdx.x == 0 && fe) atomicAdd(&ctl->fedges[L % 3], fe);
+    if (threadIdx.x == 0 && fe) ms_add_fedges(ctl, L % 3, fe);
     if (__ballot(found_any != 0) && lane == 0) ctl->active[L % 3] = 1;
 }
 
@@ -378,7 +397,7 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
         ms_write_dist<W>(newb, dist, n, v, L + 1);
     }
     fe = block_sum<MB / WAVE>(fe, red);
-    if (threadIdx.x == 0 && fe) atomicAdd(&ctl->fedges[L % 3], fe);
+    if (threadIdx.x == 0 && fe) ms_add_fedges(ctl, L % 3, fe);
     if (__ballot(found_any != 0) && lane == 0) ctl->active[L % 3] = 1;
 }
 

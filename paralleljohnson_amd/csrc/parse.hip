@@ -64,17 +64,18 @@ __device__ __forceinline__ int extract(const T* __restrict__ t, int64_t len, int
         out = 0;
         return 0;
     }
-    i64 acc = 0;
+    // u32 accumulation: a value above 4294967295 is an overflow for every field
+    // (ids are limited to ID_LIMIT, weights to the int range), so the digits
+    // after it only need to be skipped
+    u32 acc = 0;
     bool ovf = false;
     for (u32 d; p < len && is_digit(d = t[p]); ++p) {
-        acc = acc * 10 + (d - '0');
-        if (acc > 4294967295ll) {
-            ovf = true;
-            acc = 4294967295ll;
-        }
+        d -= '0';
+        ovf |= acc > 429496729u || (acc == 429496729u && d > 5u);
+        acc = acc * 10u + d;
     }
     if (ovf) return -2;
-    out = neg ? -acc : acc;
+    out = neg ? -(i64)acc : (i64)acc;
     return 1;
 }
 
@@ -121,8 +122,9 @@ __global__ __launch_bounds__(PB) void parse_count_k(const uint8_t* __restrict__ 
 __global__ __launch_bounds__(PB) void parse_lines_k(const uint8_t* __restrict__ text, i64 len, int weighted,
                                                     const u64* __restrict__ block_off, u32* __restrict__ src,
                                                     u32* __restrict__ dst, u32* __restrict__ w,
-                                                    u64* __restrict__ maxid, u64* __restrict__ errpos) {
+                                                    u32* __restrict__ bmax, u64* __restrict__ errpos) {
     __shared__ u64 lds[PB / WAVE];
+    __shared__ u32 lmax[PB / WAVE];
     __shared__ uint4 stage[(PCHUNK + PTAIL) / 16];
     const i64 base = (i64)blockIdx.x * PCHUNK;
     const uint4* g4 = reinterpret_cast<const uint4*>(text + base);
@@ -164,8 +166,32 @@ __global__ __launch_bounds__(PB) void parse_lines_k(const uint8_t* __restrict__ 
         mx = u > mx ? u : mx;
         mx = v > mx ? v : mx;
     }
+    // the block's max id + 1 (0: no line) goes to its own slot: one word taking an
+    // atomic from every wave saturates at ~88 per microsecond, which bounded this
+    // kernel (K22 text: 524K waves, 6.1 ms)
     mx = wave_max(mx);
-    if (lane_id() == 0 && mx >= 0) atomicMax(maxid, (u64)(mx + 1));
+    if (lane_id() == 0) lmax[wave_id()] = (u32)(mx + 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u32 m = 0;
+#pragma unroll
+        for (int k = 0; k < PB / WAVE; ++k) m = max(m, lmax[k]);
+        bmax[blockIdx.x] = m;
+    }
+}
+
+// max over the per-block maxima (one block)
+__global__ __launch_bounds__(1024) void max_blocks_k(const u32* __restrict__ bmax, i64 n, u64* __restrict__ out) {
+    __shared__ u32 l[1024 / WAVE];
+    u32 m = 0;
+    for (i64 i = threadIdx.x; i < n; i += 1024) m = max(m, bmax[i]);
+    m = wave_max(m);
+    if (lane_id() == 0) l[wave_id()] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < 1024 / WAVE; ++k) m = max(m, l[k]);
+        out[0] = m;
+    }
 }
 
 }  // namespace
@@ -194,7 +220,7 @@ ParseResult parse_device_text(Ctx& ctx, const uint8_t* text, i64 len, bool weigh
     ParseResult r;
     const auto t1 = std::chrono::steady_clock::now();
     const i64 nblocks = (len + PCHUNK - 1) / PCHUNK;
-    DevBuf<u32> bcnt((size_t)(nblocks > 0 ? nblocks : 1));
+    DevBuf<u32> bcnt((size_t)(nblocks > 0 ? nblocks : 1));  // line counts, then the blocks' max id + 1
     DevBuf<u64> boff((size_t)nblocks + 1);
     DevBuf<u64> scal(2);  // [0] = max id + 1, [1] = first bad byte offset
     ScanWs ws;
@@ -213,7 +239,9 @@ ParseResult parse_device_text(Ctx& ctx, const uint8_t* text, i64 len, bool weigh
     if (weighted) w.alloc((size_t)total);
     if (nblocks && total) {
         parse_lines_k<<<(unsigned)nblocks, PB, 0, s>>>(text, len, weighted ? 1 : 0, boff.p, src.p, dst.p,
-                                                      weighted ? w.p : nullptr, scal.p, scal.p + 1);
+                                                      weighted ? w.p : nullptr, bcnt.p, scal.p + 1);
+        PJ_LAUNCH_CHECK();
+        max_blocks_k<<<1, 1024, 0, s>>>(bcnt.p, nblocks, scal.p);
         PJ_LAUNCH_CHECK();
     }
     PJ_HIP(hipMemcpyAsync(h, scal.p, sizeof(h), hipMemcpyDeviceToHost, s));

@@ -83,6 +83,92 @@ __global__ __launch_bounds__(256) void copy_rows_k(const u32* __restrict__ perm,
     }
 }
 
+#ifndef PJ_RL_COPY
+#define PJ_RL_COPY 1  // 0: one wave per new row; 1: edge tiles (below)
+#endif
+#ifndef PJ_RL_PASSES
+#define PJ_RL_PASSES 1  // target-id range passes of the tile copy
+#endif
+
+constexpr int CT = 256;          // threads of a tile block
+constexpr int CE = 8;            // edges per thread
+constexpr int CTILE = CT * CE;   // new-CSR entries per tile
+constexpr int CROWS = CTILE + 1; // rows staged per tile (more: per-edge global search)
+
+// tile_row[t] = the new row holding entry t * CTILE; tile_row[ntiles] = the row of
+// the last entry (only rows with entries are written)
+template <typename Off>
+__global__ void tile_rows_k(const Off* __restrict__ nrow, i64 n, i64 nnz, u32* __restrict__ tile_row) {
+    const i64 ntiles = (nnz + CTILE - 1) / CTILE;
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
+        const i64 b = (i64)nrow[v], e = (i64)nrow[v + 1];
+        if (e <= b) continue;
+        for (i64 t = (b + CTILE - 1) / CTILE; t * CTILE < e; ++t) tile_row[t] = (u32)v;
+        if (e == nnz) tile_row[ntiles] = (u32)v;
+    }
+}
+
+// Edge-balanced copy: a block takes CTILE consecutive entries of the new CSR, stages
+// the new and old row starts of the rows they belong to in LDS, and every thread
+// copies CE entries (stride CT: coalesced stores), each found by a binary search
+// over the staged starts. All CE loads of a thread are independent, so the random
+// id lookups inv[ocol[k]] overlap (the wave-per-row form walks short rows with
+// mostly idle lanes, one dependent row chain per wave). A pass renames only the
+// targets in [lo, hi) (PJ_RL_PASSES > 1: each pass's slice of inv stays cached).
+template <typename Off>
+__global__ __launch_bounds__(CT) void copy_tiles_k(const u32* __restrict__ perm, const u32* __restrict__ inv,
+                                                   const Off* __restrict__ orow, const u32* __restrict__ ocol,
+                                                   const u32* __restrict__ ow, const Off* __restrict__ nrow,
+                                                   u32* __restrict__ ncol, u32* __restrict__ nw, i64 nnz,
+                                                   const u32* __restrict__ tile_row, u32 lo, u32 hi, int first) {
+    __shared__ Off s_nb[CROWS], s_ob[CROWS];
+    const i64 ntiles = (nnz + CTILE - 1) / CTILE;
+    for (i64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const i64 e0 = t * CTILE, e1 = min(e0 + CTILE, nnz);
+        const u32 r0 = tile_row[t], r1 = tile_row[t + 1];
+        const i64 nr = (i64)r1 - r0 + 1;
+        const bool staged = nr <= CROWS;
+        if (staged)
+            for (i64 j = threadIdx.x; j < nr; j += CT) {
+                s_nb[j] = nrow[r0 + j];
+                s_ob[j] = orow[perm[r0 + j]];
+            }
+        __syncthreads();
+        i64 src[CE];
+#pragma unroll
+        for (int m = 0; m < CE; ++m) {
+            const i64 k = e0 + threadIdx.x + m * CT;
+            src[m] = -1;
+            if (k >= e1) continue;
+            i64 a = 0, b = nr - 1;  // largest j with start(j) <= k
+            while (a < b) {
+                const i64 mid = (a + b + 1) >> 1;
+                const Off st = staged ? s_nb[mid] : nrow[r0 + mid];
+                if ((i64)st <= k) a = mid;
+                else b = mid - 1;
+            }
+            const Off nb = staged ? s_nb[a] : nrow[r0 + a];
+            const Off ob = staged ? s_ob[a] : orow[perm[r0 + a]];
+            src[m] = (i64)ob + (k - (i64)nb);
+        }
+        u32 c[CE], wv[CE];
+#pragma unroll
+        for (int m = 0; m < CE; ++m)
+            if (src[m] >= 0) {
+                c[m] = ocol[src[m]];
+                if (first) wv[m] = ow[src[m]];
+            }
+#pragma unroll
+        for (int m = 0; m < CE; ++m)
+            if (src[m] >= 0) {
+                const i64 k = e0 + threadIdx.x + m * CT;
+                if (c[m] >= lo && c[m] < hi) ncol[k] = inv[c[m]];
+                if (first) nw[k] = wv[m];
+            }
+        __syncthreads();
+    }
+}
+
 template <typename Off>
 void build(Graph& g) {
     hipStream_t s = g.ctx->stream;
@@ -134,9 +220,25 @@ void build(Graph& g) {
     }
     R->col.alloc((size_t)(nnz ? nnz : 1));
     R->w.alloc((size_t)(nnz ? nnz : 1));
-    if (nnz)
+    if (nnz && PJ_RL_COPY == 0) {
         copy_rows_k<Off><<<grid, 256, 0, s>>>(R->perm.p, R->inv.p, orow, g.col.p, g.w.p, nrow, R->col.p, R->w.p,
                                               n);
+    } else if (nnz) {
+        const i64 ntiles = (nnz + CTILE - 1) / CTILE;
+        DevBuf<u32> trow((size_t)ntiles + 1);
+        tile_rows_k<Off><<<grid_for(n, 256, grid), 256, 0, s>>>(nrow, n, nnz, trow.p);
+        PJ_LAUNCH_CHECK();
+        const unsigned tgrid = (unsigned)std::min<i64>(ntiles, (i64)g.ctx->cu_count * 8);
+        const u64 span = ((u64)n + PJ_RL_PASSES - 1) / PJ_RL_PASSES;
+        for (int p = 0; p < PJ_RL_PASSES; ++p) {
+            const u64 lo = span * (u64)p, hi = std::min<u64>((u64)n, lo + span);
+            copy_tiles_k<Off><<<tgrid, CT, 0, s>>>(R->perm.p, R->inv.p, orow, g.col.p, g.w.p, nrow, R->col.p,
+                                                   R->w.p, nnz, trow.p, (u32)lo,
+                                                   p + 1 == PJ_RL_PASSES ? 0xFFFFFFFFu : (u32)hi, p == 0);
+            PJ_LAUNCH_CHECK();
+        }
+        PJ_HIP(hipStreamSynchronize(s));  // trow is freed on return
+    }
     PJ_LAUNCH_CHECK();
     R->dist.alloc((size_t)n);
     PJ_HIP(hipStreamSynchronize(s));

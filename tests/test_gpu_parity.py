@@ -245,7 +245,8 @@ def test_weighted_text_and_kronecker(ctx, oracle):
 def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
     """Tile-dense light rounds (dense_frac: never / whenever the frontier is non-empty /
     the default threshold), tile-dense light pulls (dense_pull) and the has-light-edge
-    filter (on / off) and the packed 32-bit light CSR (on / off), with light pulls never / by the default rule / in every round and
+    filter (on / off) and the packed 32-bit light CSR (on / off), hub tiles folded into the next
+    round's launch (fold_hub) or in their own, with light pulls never / by the default rule / in every round and
     with and without the tail switch: directed random graphs (no pulls), a star whose
     light segment exceeds the dense mode's hub threshold (4096), and Kronecker graphs.
     Bit-exact against the oracle Dijkstra."""
@@ -267,9 +268,11 @@ def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
         col = col.astype(np.uint32)
         roots = [0] + [int(r) for r in g.sample_roots(4, 2)]
         exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
-        for dense, dp, pk, tp, mr in ((0.0, 0, 0, 0, 0), (1e-12, 1, 1, 1, 1), (0.02, 0, 1, 1, 0), (0.02, 1, 0, 0, 1),
-                                      (0.1, 1, 1, 0, 0), (0.1, 0, 2, 1, 1), (0.0, 0, 1, 0, 1)):
+        for i, (dense, dp, pk, tp, mr) in enumerate(((0.0, 0, 0, 0, 0), (1e-12, 1, 1, 1, 1), (0.02, 0, 1, 1, 0),
+                                                     (0.02, 1, 0, 0, 1), (0.1, 1, 1, 0, 0), (0.1, 0, 2, 1, 1),
+                                                     (0.0, 0, 1, 0, 1))):
             for lf in (0, 1):
+                g.set_option("fold_hub", lf ^ (i & 1))  # hub tiles in the next round's launch, or their own
                 for lp, tf in ((2.0, 0.1), (0.0, 0.1), (2.0, 0.0), (1e15, 0.1)):
                     g.set_option("dense_frac", dense)
                     g.set_option("dense_pull", dp)
@@ -284,7 +287,8 @@ def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
                     for delta in (0, 40):
                         g.set_option("delta", delta)
                         for r in roots:
-                            assert (g.sssp(r) == exp[r]).all(), (name, dense, dp, pk, tp, mr, lf, lp, tf, delta, r)
+                            assert (g.sssp(r) == exp[r]).all(), (name, dense, dp, pk, tp, mr, lf, lp, tf, delta, r,
+                                                                 lf ^ (i & 1))
         g.close()
 
 
