@@ -871,6 +871,7 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "spin_sync" && (value == 0 || value == 1)) g.spin_sync = (int)value;
     else if (k == "merged_round" && (value == 0 || value == 1)) g.merged_round = (int)value;
     else if (k == "fold_hub" && (value == 0 || value == 1)) g.fold_hub = (int)value;
+    else if (k == "defer_heavy" && (value == 0 || value == 1)) g.defer_heavy = (int)value;
     else if (k == "defer_check" && (value == 0 || value == 1)) g.defer_check = (int)value;
     else if (k == "round_gpc" && value >= 0 && value <= 64) g.round_gpc = (int)value;
     else if (k == "hub_gpc" && value >= 0 && value <= 64) g.hub_gpc = (int)value;

@@ -804,6 +804,29 @@ __global__ void light_split_k(const Off* __restrict__ row, const u32* __restrict
     }
 }
 
+// sum (out[0]) and max (out[1]) of the edge weights in one pass: the auto delta's mean
+// weight and the v2 tail's "every edge is light" test (two passes over the 2^31 weights
+// of s26 cost 2.2 + 1.5 ms of the solver preparation)
+__global__ __launch_bounds__(DB) void wsummax_k(const u32* __restrict__ w, i64 n, u64* __restrict__ out) {
+    __shared__ u64 red[DB / WAVE];
+    u64 acc = 0;
+    u32 mx = 0;
+    for (i64 i = (i64)blockIdx.x * DB + threadIdx.x; i < n; i += (i64)gridDim.x * DB) {
+        const u32 x = w[i];
+        acc += x;
+        mx = max(mx, x);
+    }
+    acc = block_sum<DB / WAVE>(acc, red);
+    mx = wave_max(mx);
+    if (lane_id() == 0) red[wave_id()] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < DB / WAVE; ++k) mx = max(mx, (u32)red[k]);
+        if (acc) atomicAdd(&out[0], acc);
+        if (mx) atomicMax(&out[1], (u64)mx);
+    }
+}
+
 __global__ __launch_bounds__(DB) void wsum_k(const u32* __restrict__ w, i64 n, u64* __restrict__ out) {
     u64 acc = 0;
     for (i64 i = (i64)blockIdx.x * DB + threadIdx.x; i < n; i += (i64)gridDim.x * DB) acc += w[i];
@@ -1517,12 +1540,12 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fo
 // them), counts them into slot cout and folds min{new dist >= hi} into minv.
 template <typename Off>
 __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fout,
-                                                int32_t nhi, int cout) {
+                                                int32_t nhi, int cout, int32_t mlo, int32_t cap) {
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
     __shared__ u64 red[NWV];
     const int lane = lane_id();
-    const int32_t lo = a.lo, hi = a.hi;
+    const int32_t lo = mlo, hi = a.hi;  // lo: the smallest member distance (early stop)
     u32* newb = s_new[wave_id()];
     u32 ccount = 0;
     u64 fe = 0;
@@ -1560,11 +1583,12 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
             const u32 ex = __shfl(myex, jw, 64);
             const u64 tw = __shfl(mytodo, jw, 64);
             const i64 v = act ? (gbase + jw) * 64 + select_bit(tw, c - ex) : 0;
-            int32_t d0 = INT_INF, cur = INT_INF;
+            int32_t d0 = INT_INF, cur = INT_INF, bound = INT_INF;
             Off k = 0, e = 0;
             if (act) {
                 d0 = a.dist[v];
-                cur = d0;
+                bound = min(d0, cap);  // cap (defer_heavy): only values that can land in [hi, nhi)
+                cur = bound;
                 k = row[v] + (Off)a.lsplit[v];
                 e = row[v + 1];
             }  // (edges in a.cw)
@@ -1614,6 +1638,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                 if (lane == l) cur = cl;
             }
             if (act) {
+                if (cur == bound) cur = d0;  // nothing found below the bound
                 if (cur < d0) a.dist[v] = cur;
                 if (cur < mn) mn = cur;
                 if (cur < nhi) {  // cur >= hi always here
@@ -2476,6 +2501,54 @@ __global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restric
     }
 }
 
+// Edge-tiled light CSR build (the lane-per-vertex form above stored each lane's
+// prefix to its own place: uncoalesced, 11 ms at s26): a block takes LT_E consecutive
+// light-CSR positions, stages the light-row starts of the vertices they belong to in
+// LDS (tile table lt_row, like relabel.hip's copy tiles) and copies LT_E / 256 entries
+// per thread with coalesced stores, each row found by a binary search in LDS.
+constexpr int LT_E = 1024;   // light-CSR positions per tile
+constexpr int LT_R = 4096;   // light-row starts staged per tile (most vertices have no light edge)
+__global__ void v2_light_tiles_k(const u64* __restrict__ lrow, i64 n, u64 light, u32* __restrict__ trow) {
+    const i64 ntiles = (i64)((light + LT_E - 1) / LT_E);
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
+        const i64 b = (i64)lrow[v], e = (i64)lrow[v + 1];
+        if (e <= b) continue;
+        for (i64 t = (b + LT_E - 1) / LT_E; t * LT_E < e; ++t) trow[t] = (u32)v;
+        if (e == (i64)light) trow[ntiles] = (u32)v;
+    }
+}
+template <typename Off, typename OutT>
+__global__ __launch_bounds__(256) void v2_light_csr_tiled_k(const Off* __restrict__ row, const u64* __restrict__ lrow,
+                                                            const u64* __restrict__ cw, const u32* __restrict__ col,
+                                                            const u32* __restrict__ wt, u64 light,
+                                                            const u32* __restrict__ trow, OutT* __restrict__ lcw,
+                                                            u32 cb) {
+    __shared__ u64 s_lb[LT_R + 1];
+    const i64 ntiles = (i64)((light + LT_E - 1) / LT_E);
+    for (i64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const u64 e0 = (u64)t * LT_E, e1 = min(e0 + (u64)LT_E, light);
+        const u32 r0 = trow[t], r1 = trow[t + 1];
+        const u32 nr = r1 - r0 + 1;
+        const bool staged = nr <= (u32)LT_R + 1;
+        if (staged)
+            for (u32 j = threadIdx.x; j < nr; j += 256) s_lb[j] = lrow[r0 + j];
+        __syncthreads();
+#pragma unroll 4
+        for (u64 k = e0 + threadIdx.x; k < e1; k += 256) {
+            u32 a = 0, b = nr - 1;  // largest j with lrow[r0 + j] <= k
+            while (a < b) {
+                const u32 mid = (a + b + 1) >> 1;
+                if ((staged ? s_lb[mid] : lrow[r0 + mid]) <= k) a = mid;
+                else b = mid - 1;
+            }
+            const u64 lb = staged ? s_lb[a] : lrow[r0 + a];
+            const u64 rb = (u64)row[r0 + a];
+            v2_lput(lcw, k, v2_rec(cw, col, wt, rb + (k - lb)), cb);
+        }
+        __syncthreads();
+    }
+}
+
 // heavy edges (w >= the current light threshold) of the vertices not settled
 // below lo: the pull decision's heavy_left after a switch of the threshold
 template <typename Off>
@@ -2583,6 +2656,7 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         const double d = 3.5 * g.mean_weight / std::max(1.0, mean_deg);
         delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(d)));
     }
+    if (w.maxw < 0 && g.max_weight >= 0) w.maxw = g.max_weight;  // (the relabeled weights are the same)
     if (w.maxw < 0) {  // largest weight: decides whether the tail has heavy edges at all
         u32 h = 0;
         if (g.nnz > 0) {
@@ -2640,18 +2714,26 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         w.lcb = (g.light_pack && wb < 32 && (u64)n <= (1ull << cb)) ? cb : 0u;
         w.lcw.release();
         w.lcw32.release();
+        const i64 lt = (i64)((light + LT_E - 1) / LT_E);
+        DevBuf<u32> ltrow((size_t)lt + 1);
+        if (light) {
+            v2_light_tiles_k<<<grid_for(n, 256, maxgrid), 256, 0, s>>>(w.lrow.p, n, light, ltrow.p);
+            PJ_LAUNCH_CHECK();
+        }
+        const unsigned ltgrid = (unsigned)std::max<i64>(1, std::min<i64>(lt, (i64)ctx.cu_count * 8));
         if (w.lcb) {
             w.lcw32.alloc(std::max<u64>(light, 1));
             if (light)
-                v2_light_csr_k<Off, u32><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, R.col.p,
-                                                                                   R.w.p, n, w.lcw32.p, w.lcb);
+                v2_light_csr_tiled_k<Off, u32><<<ltgrid, 256, 0, s>>>(row, w.lrow.p, w.cw.p, R.col.p, R.w.p, light,
+                                                                       ltrow.p, w.lcw32.p, w.lcb);
         } else {
             w.lcw.alloc(std::max<u64>(light, 1));
             if (light)
-                v2_light_csr_k<Off, u64><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, w.lsplit.p, w.lrow.p, w.cw.p, R.col.p,
-                                                                                   R.w.p, n, w.lcw.p, 0u);
+                v2_light_csr_tiled_k<Off, u64><<<ltgrid, 256, 0, s>>>(row, w.lrow.p, w.cw.p, R.col.p, R.w.p, light,
+                                                                       ltrow.p, w.lcw.p, 0u);
         }
         PJ_LAUNCH_CHECK();
+        PJ_HIP(hipStreamSynchronize(s));  // (ltrow is freed on return)
         w.lcv.alloc(std::max<u64>(w.nlc, 1));
         w.lcc.alloc(std::max<u64>(w.nlc, 1));
         PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
@@ -3048,6 +3130,9 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
         // pulls (plain distance stores)
         const bool fold = g.fold_hub && g.merged_round && !bin_ok && !g.dense_pull;
         bool hub_pend = false;  // the last light round launched may have queued hub segments
+        bool owed = false;      // defer_heavy: mb still holds the last band's members, whose heavier
+        int32_t owed_lo = 0;    // edges (lo + w >= that band's nhi) are not relaxed yet; their lo
+        u64 mh_owed = 0;        // and heavy-edge count
         bool deferred = false;
         bool finished = false;
         while (lo < INT_INF && !finished) {
@@ -3206,13 +3291,32 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                 a.swrite = w.sb.p;
                 a.fesplit = w.lsplit2.p;
             }
-            if (can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh) {
-                v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi_t, cs);
+            // defer_heavy: a heavy pull whose next band is not the tail relaxes only what can
+            // land in the next band (lo + w < nhi: the lightest heavy edges) and keeps the
+            // members in mb; the heavy step after the next band relaxes the rest for the
+            // members of both bands in one pass over the heavy rows (R9: any relaxation
+            // order is exact as long as an edge is relaxed before the band it lands in runs)
+            const u64 mh_all = mh + mh_owed;
+            const bool pull_now = can_pull && mh_all > 0 && (double)heavy_left < g.pull_factor * (double)mh_all;
+            const bool medium = pull_now && g.defer_heavy && !owed && !enter_tail && nhi_t < INT_INF;
+            if (pull_now) {
+                v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi_t, cs, owed ? owed_lo : a.lo,
+                                                        medium ? nhi_t : INT_INF);
                 PJ_LAUNCH_CHECK();
-                PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
+                if (medium) {
+                    owed = true;
+                    owed_lo = a.lo;
+                    mh_owed = mh;
+                } else {
+                    PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
+                    owed = false;
+                    mh_owed = 0;
+                }
                 st.bu_levels++;
             } else {
-                if (mh > 0) {
+                owed = false;  // the push relaxes every heavy edge of mb's members (both bands)
+                mh_owed = 0;
+                if (mh_all > 0) {
                     v2_expand_k<Off, false><<<maxgrid, DB, 0, s>>>(a, row, w.mb.p, nullptr, cs, hr, ~0ull, ~0ull, nullptr);
                     PJ_LAUNCH_CHECK();
                     v2_hub_k<false><<<maxgrid, DB, 0, s>>>(a, nullptr, cs, hr, (hr + 1) % 3);
@@ -3250,13 +3354,27 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
                     PJ_LAUNCH_CHECK();
                 }
             }
-            if (defer_ok && !(enter_tail && (long long)tdelta <= w.maxw)) {
+            bool synced = false;
+            if (medium) {  // (no deferred check: an empty next band needs the owed edges first)
+                sync_ctl();
+                synced = true;
+                if (slot(cs) == 0) {  // the owed heavy edges decide where the solve goes on
+                    v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, w.f[fi].p, nhi_t, cs, owed_lo, INT_INF);
+                    PJ_LAUNCH_CHECK();
+                    PJ_HIP(hipMemsetAsync(w.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
+                    owed = false;
+                    mh_owed = 0;
+                    st.bu_levels++;
+                    sync_ctl();
+                }
+            }
+            if (!synced && defer_ok && !(enter_tail && (long long)tdelta <= w.maxw)) {
                 deferred = true;  // checked at the next band's first publish
                 fe_known = false;
                 lo = hi;
                 continue;
             }
-            sync_ctl();
+            if (!synced) sync_ctl();
             if (enter_tail && (long long)tdelta <= w.maxw) {
                 heavy_left = w.hctl->dbg[0].v;
                 light_left = tail_unsettled > heavy_left ? tail_unsettled - heavy_left : 0;
@@ -3336,17 +3454,19 @@ void delta_solve(Graph& g, i64 source) {
         PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.host), sizeof(DTot), hipHostMallocMapped));
     }
     if (g.mean_weight < 0.0) {
-        u64 sum = 0;
+        u64 h[2] = {0, 0};
         if (g.nnz > 0) {
             DevBuf<u64> acc;
-            acc.alloc(1);
-            PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), g.ctx->stream));
-            wsum_k<<<grid_for(g.nnz, DB, (unsigned)g.ctx->cu_count * 8u), DB, 0, g.ctx->stream>>>(g.w.p, g.nnz, acc.p);
+            acc.alloc(2);
+            PJ_HIP(hipMemsetAsync(acc.p, 0, 2 * sizeof(u64), g.ctx->stream));
+            wsummax_k<<<grid_for(g.nnz, DB, (unsigned)g.ctx->cu_count * 8u), DB, 0, g.ctx->stream>>>(g.w.p, g.nnz,
+                                                                                                     acc.p);
             PJ_LAUNCH_CHECK();
-            PJ_HIP(hipMemcpyAsync(&sum, acc.p, sizeof(u64), hipMemcpyDeviceToHost, g.ctx->stream));
+            PJ_HIP(hipMemcpyAsync(h, acc.p, 2 * sizeof(u64), hipMemcpyDeviceToHost, g.ctx->stream));
             PJ_HIP(hipStreamSynchronize(g.ctx->stream));
         }
-        g.mean_weight = g.nnz > 0 ? (double)sum / (double)g.nnz : 1.0;
+        g.mean_weight = g.nnz > 0 ? (double)h[0] / (double)g.nnz : 1.0;
+        g.max_weight = (long long)h[1];
     }
     if (g.delta_impl == 1) {
         if (g.off64) delta_run<u64>(g, *g.delta_work, source);

@@ -185,6 +185,7 @@ struct Graph {
     std::unique_ptr<MsWork, MsWorkDeleter> ms_work;
     std::unique_ptr<DeltaWork, DeltaWorkDeleter> delta_work;
     double mean_weight = -1.0;  // weighted: computed on first delta solve
+    long long max_weight = -1;  // weighted: with mean_weight (-1: not computed)
     std::unique_ptr<Relabeled> rl;  // weighted: built on the first delta solve
 
     // options
@@ -218,7 +219,8 @@ struct Graph {
     int tail_pull = 1;     // delta v2: light pull rounds allowed in the tail too (round 3: 391 -> 428 GTEPS, once
                            // the tail-entry frontier counts its whole rows, fesplit)
     int spin_sync = 1;     // delta v2: the host spins on a published sequence word instead of a stream sync (0/1)
-    int fold_hub = 1;      // delta v2: a light round's hub tiles run in the next round's launch (0/1)
+    int defer_heavy = 0;   // delta v2: a heavy pull before a non-tail band relaxes only edges landing in it (0/1; measured equal)
+    int fold_hub = 0;      // delta v2: a light round's hub tiles run in the next round's launch (0/1; measured 4% slower)
     int merged_round = 1;  // delta v2: one launch per light round decides pull / dense / sparse push (0/1)
     int defer_check = 1;   // delta v2 (merged rounds): no host check right after a heavy step (0/1)
     int round_gpc = 12;    // delta v2: workgroups per CU of the light-round / hub launches (0 = the heavy

@@ -34,7 +34,7 @@ constexpr int MB = 256;
 #endif
 constexpr int MS_SERIAL = PJ_MS_SERIAL;  // in-edges a lane scans alone before the wave helps
 #ifndef PJ_MS_U
-#define PJ_MS_U 8
+#define PJ_MS_U 4  // swept (round 3, MS1024): 2 / 4 / 8 at 4 workgroups per CU, 4 / 8 at 8: 4 at 8 best
 #endif
 constexpr int MS_U = PJ_MS_U;  // pull: in-edges a lane loads per serial step
 constexpr int MS_WMAX = 16;  // widest pass: 1024 sources (option ms_width)
@@ -127,7 +127,7 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
 }
 
 #ifndef PJ_MS_GPC
-#define PJ_MS_GPC 4  // level-kernel workgroups per CU
+#define PJ_MS_GPC 8  // level-kernel workgroups per CU (MS1024: 12.8 -> 12.4 ms with MS_U 4, round 3)
 #endif
 // (filling the distance block here, ~0.43 ms per 512-source pass at 4.4 TB/s on the
 // web-Google-shaped graph, is cheaper than writing INT_INF for the unreached pairs at

@@ -344,7 +344,9 @@ def test_weighted_band_width(ctx, oracle, scale, ef):
 @pytest.mark.parametrize("scale,ef", [(12, 16), (14, 4), (16, 1), (15, 16)])
 def test_weighted_pull_heavy(ctx, oracle, scale, ef):
     """Heavy edges by pull (symmetric graphs): never (push only), by the default
-    rule, and in every band; several deltas. Bit-exact against the oracle Dijkstra."""
+    rule, and in every band; several deltas; heavy pulls that defer the edges which
+    cannot land in the next band to the heavy step after it (defer_heavy) or not,
+    with and without the tail switch. Bit-exact against the oracle Dijkstra."""
     g = ctx.generate_kronecker(scale, ef, 9 + scale, weighted=True)
     row, col, wc = g.get_csr()
     col = col.astype(np.uint32)
@@ -356,10 +358,12 @@ def test_weighted_pull_heavy(ctx, oracle, scale, ef):
         g.set_option("delta_impl", impl)
         g.set_option("pull_factor", pf)
         g.set_option("light_pull", lp)
-        for delta in (0, 7, 60):
+        for delta, dh, tf in ((0, 1, 0.1), (7, 1, 0.0), (60, 1, 0.1), (0, 0, 0.1), (7, 0, 0.1), (60, 1, 0.0)):
             g.set_option("delta", delta)
+            g.set_option("defer_heavy", dh)
+            g.set_option("tail_frac", tf)
             for r in roots:
-                assert (g.sssp(r) == exp[r]).all(), (impl, pf, lp, delta, r)
+                assert (g.sssp(r) == exp[r]).all(), (impl, pf, lp, delta, dh, tf, r)
                 st = g.stats()
                 if pf == 0.0:
                     assert st["bu_levels"] == 0

@@ -1,4 +1,5 @@
-"""MS1024 on the web-Google-shaped graph: batched multi-source wall/kernel time per pass width."""
+"""MS1024 on the web-Google-shaped graph: batch wall time (median of 7) and kernel time under
+libpj option sets, interleaved. Usage: python tools/probe_ms.py "k=v,k=v" "k=v" ...  ("" = defaults)"""
 import os, sys, time
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
 import numpy as np
@@ -7,12 +8,21 @@ ctx = pj.Context(0)
 g = ctx.generate_webgraph()
 row, _, _ = g.get_csr()
 src = [int(x) for x in np.nonzero(np.diff(row) > 0)[0][:1024]]
-import itertools
-for wd, al in itertools.product((1, 4), (0, 4, 16, 64)):
-    g.set_option("ms_width", wd)
-    g.set_option("ms_alpha", al)
-    g.sssp_batch(src[:64], copy=False)
-    ts = []
-    for _ in range(3):
-        t = time.perf_counter(); g.sssp_batch(src, copy=False); ts.append(time.perf_counter() - t)
-    print(f"width {wd} alpha {al}: wall {1e3 * min(ts):.2f} ms kernel {g.stats()['kernel_ms']:.2f} ms levels {g.stats()['levels']}", flush=True)
+sets = sys.argv[1:] or [""]
+DEFAULTS = {"ms_width": 0, "ms_alpha": 16}
+for rep in range(2):
+    for o in sets:
+        opts = dict(DEFAULTS)
+        for kv in filter(None, o.split(",")):
+            k, v = kv.split("=")
+            opts[k] = float(v)
+        for k, v in opts.items():
+            g.set_option(k, v)
+        g.sssp_batch(src[:64], copy=False)
+        g.sssp_batch(src, copy=False)
+        ts, ks = [], []
+        for _ in range(7):
+            t = time.perf_counter(); g.sssp_batch(src, copy=False); ts.append(time.perf_counter() - t)
+            ks.append(g.stats()["kernel_ms"])
+        print(f"[{o}] pass {rep + 1}: batch {1e3 * np.median(ts):.2f} ms (min {1e3 * min(ts):.2f}) kernel "
+              f"{np.median(ks):.2f} ms levels {g.stats()['levels']}", flush=True)
