@@ -908,6 +908,9 @@ struct V2Ctl {
     V2Line minv[V2_NSH];    // min dist >= lo of the last select / pull (next band search), per shard
     V2Line dbg[8];          // PJ_V2_STATS builds: vertices, edges, atomics, marks, hub edges
 };
+#ifndef PJ_V2_PSTATS
+#define PJ_V2_PSTATS 0  // debug build: heavy-pull scan-length counters (printed per solve)
+#endif
 #ifndef PJ_V2_STATS
 #define PJ_V2_STATS 0
 #endif
@@ -1594,6 +1597,9 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
             }  // (edges in a.cw)
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
             bool go = act && k < lim, done = !act || k >= e;
+#if PJ_V2_PSTATS
+            const Off k0 = k;
+#endif
             while (__ballot(go)) {
                 if (go) {
                     // band members are exactly mb's bits: probe the (cache-resident)
@@ -1607,6 +1613,22 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                     }
                 }
             }
+#if PJ_V2_PSTATS  // (heavy-pull scan lengths: candidates, stopped within 2 / 4 / 8 / the serial part)
+            {
+                const u64 sc = (u64)(k - k0);
+                const u64 c0 = wave_sum((u64)act), c1 = wave_sum((u64)(act && done && sc <= 2)),
+                          c2 = wave_sum((u64)(act && done && sc <= 4)), c3 = wave_sum((u64)(act && done && sc <= 8)),
+                          c4 = wave_sum((u64)(act && done)), c5 = wave_sum(act ? (u64)(e - k0) : 0ull);
+                if (lane == 0) {
+                    atomicAdd(&a.ctl->dbg[2].v, c0);
+                    atomicAdd(&a.ctl->dbg[3].v, c1);
+                    atomicAdd(&a.ctl->dbg[4].v, c2);
+                    atomicAdd(&a.ctl->dbg[5].v, c3);
+                    atomicAdd(&a.ctl->dbg[6].v, c4);
+                    atomicAdd(&a.ctl->dbg[7].v, c5);
+                }
+            }
+#endif
             u64 open = __ballot(!done);
             while (open) {
                 const int l = __ffsll((long long)open) - 1;
@@ -3409,6 +3431,14 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
     g.stats = st;
     g.have_result = true;
+    if (PJ_V2_PSTATS) {
+        V2Ctl h;
+        PJ_HIP(hipMemcpy(&h, w.ctl.p, sizeof(V2Ctl), hipMemcpyDeviceToHost));
+        fprintf(stderr, "heavy pulls: candidates %llu stopped within 2 %llu, 4 %llu, 8 %llu, serial %llu; "
+                "heavy edges of the candidates %llu\n", (unsigned long long)h.dbg[2].v, (unsigned long long)h.dbg[3].v,
+                (unsigned long long)h.dbg[4].v, (unsigned long long)h.dbg[5].v, (unsigned long long)h.dbg[6].v,
+                (unsigned long long)h.dbg[7].v);
+    }
     if (g.round_log) {  // debug: one stderr line per non-empty light round
         std::vector<u64> h(1 + 3 * 255);
         PJ_HIP(hipMemcpy(h.data(), rlog.p, sizeof(u64) * h.size(), hipMemcpyDeviceToHost));
