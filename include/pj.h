@@ -437,6 +437,11 @@ int pj_part_gather_dist(pj_part* p, pj_comm* comm, int32_t* dist_out);
 /* Weighted partitioned solve (delta-stepping, wpart.hip + engine.cpp);
  * delta <= 0 picks the single-GPU default. */
 int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st);
+/* pj_wpart_set_option keys: "tail_frac" (switch to the tail threshold once the edges of
+ * the vertices not settled yet, over all ranks, drop below tail_frac x all edges; 0 = off;
+ * default 0.1) and "tail_mult" (tail threshold and band width = tail_mult x delta,
+ * default 64). Every rank must use the same values. */
+int pj_wpart_set_option(pj_wpart* p, const char* key, double value);
 int pj_wpart_delta_group(int world, pj_wpart* const* parts, pj_comm* const* comms, int64_t source, int32_t delta,
                          pj_part_stats* st);
 int pj_wpart_gather_dist(pj_wpart* p, pj_comm* comm, int32_t* dist_out);

@@ -151,6 +151,7 @@ _SIGS = {
     "pj_part_bfs_group": ([_INT, _P, _P, _I64, _P], _INT),
     "pj_part_gather_dist": ([_P, _P, _P], _INT),
     "pj_wpart_delta": ([_P, _P, _I64, ctypes.c_int32, _P], _INT),
+    "pj_wpart_set_option": ([_P, ctypes.c_char_p, ctypes.c_double], _INT),
     "pj_wpart_delta_group": ([_INT, _P, _P, _I64, ctypes.c_int32, _P], _INT),
     "pj_wpart_gather_dist": ([_P, _P, _P], _INT),
     "pj_engine_bfs": ([_P, _P, _I64, ctypes.c_double, ctypes.c_double, _INT, _P], _INT),

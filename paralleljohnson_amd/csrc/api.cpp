@@ -1669,6 +1669,16 @@ int pj_part_gather_dist(pj_part* p, pj_comm* comm, int32_t* dist_out) {
     });
 }
 
+int pj_wpart_set_option(pj_wpart* p, const char* key, double value) {
+    if (!p || !key) return arg_error("pj_wpart_set_option: bad argument");
+    WPart& P = *reinterpret_cast<WPart*>(p);
+    const std::string k(key);
+    if (k == "tail_frac" && value >= 0) wpart_tail_params(P)[0] = value;
+    else if (k == "tail_mult" && value >= 1) wpart_tail_params(P)[1] = value;
+    else return arg_error("pj_wpart_set_option: unknown key or bad value");
+    return PJ_OK;
+}
+
 int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st) {
     if (!p || !comm) return arg_error("pj_wpart_delta: bad argument");
     return guarded([&] {

@@ -157,7 +157,17 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
     guarded_loop(comm, [&] {
         hipStream_t s = S.stream();
         const double t0 = now_ms();
-        const int32_t delta = S.begin(source, delta_in);
+        int32_t delta = S.begin(source, delta_in);
+        const int32_t delta0 = delta;
+        // tail switch: every rank takes the same decision from the all-reduced counts
+        const double tfrac = S.tail_frac();
+        const int32_t tdelta = S.tail_delta(delta);
+        i64 all_edges = 0;
+        bool tail_on = tfrac > 0.0 && tdelta > delta;
+        if (tail_on) {
+            all_edges = S.local_edges();
+            comm.allreduce(&all_edges, 1, false, s);
+        }
         std::vector<i64> counts((size_t)S.world), rcounts((size_t)S.world);
         i64 sent = 0, bands = 0, rounds = 0;
         auto exchange_apply = [&](int light, int32_t lo, int32_t hi) {
@@ -221,6 +231,19 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
                 if (nf == 0) break;
             }
             exchange_apply(0, (int32_t)lo, (int32_t)hi);  // heavy edges of the band's members
+            if (tail_on) {
+                i64 ue = S.unsettled_edges((int32_t)hi);
+                if (ue < 0) {
+                    tail_on = false;  // (not supported: the same on every rank)
+                } else {
+                    comm.allreduce(&ue, 1, false, s);
+                    if ((double)ue < tfrac * (double)all_edges) {
+                        delta = tdelta;
+                        S.set_delta(delta);
+                        tail_on = false;
+                    }
+                }
+            }
             lo = hi;
         }
         comm.sync(s);
@@ -234,7 +257,7 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             st->levels = bands;
             st->bands = bands;
             st->rounds = rounds;
-            st->delta = delta;
+            st->delta = delta0;
             st->reached = rc[0];
             st->reached_edges = rc[1];
             st->sent = sent;

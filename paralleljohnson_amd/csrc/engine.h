@@ -118,6 +118,17 @@ struct DeltaSteps {
     virtual void select_async(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
     virtual void select_finish() {}
     virtual void end_round_async() {}
+    // Tail switch (optional; the defaults disable it): once the out-edges of the vertices
+    // not settled below hi, summed over the ranks, drop under tail_frac x all edges, the
+    // bands after this one use the light threshold and width tail_delta (64 x delta by
+    // default: every edge light, bands of Bellman-Ford rounds). Exact at a band boundary:
+    // everything below hi is settled and relaxed. unsettled_edges(hi) returns this rank's
+    // sum (-1: not supported, on every rank alike), local_edges() this rank's edges.
+    virtual double tail_frac() { return 0.0; }
+    virtual int32_t tail_delta(int32_t delta) { return delta; }
+    virtual i64 unsettled_edges(int32_t hi) { (void)hi; return -1; }
+    virtual i64 local_edges() { return 0; }
+    virtual void set_delta(int32_t delta) { (void)delta; }
 };
 
 struct BfsParams {
@@ -139,6 +150,7 @@ BfsParams& part_params(Part& p);
 // because the per-rank host threads start on device 0
 const Ctx& part_ctx(const Part& p);
 const Ctx& wpart_ctx(const WPart& p);
+double* wpart_tail_params(WPart& p);  // [0] tail_frac, [1] tail_mult (pj_wpart_set_option)
 // every rank's slice of dist, gathered (n int32 to host; NULL: gather only)
 void part_gather_dist(Part& p, Comm& comm, int32_t* out);
 void wpart_gather_dist(WPart& p, Comm& comm, int32_t* out);

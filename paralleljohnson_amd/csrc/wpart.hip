@@ -336,6 +336,16 @@ __global__ void wp_lsplit_k(const u64* __restrict__ row, const u32* __restrict__
     }
 }
 
+// out-edges of the owned vertices not settled below hi (dist >= hi, unreached included)
+__global__ __launch_bounds__(WB) void wp_unsettled_k(WArgs a, int32_t hi, u64* __restrict__ out) {
+    __shared__ u64 red[WB / WAVE];
+    u64 acc = 0;
+    for (i64 v = (i64)blockIdx.x * WB + threadIdx.x; v < a.nl; v += (i64)gridDim.x * WB)
+        if (a.dist[v] >= hi) acc += a.row[v + 1] - a.row[v];
+    acc = block_sum<WB / WAVE>(acc, red);
+    if (threadIdx.x == 0 && acc) atomicAdd(out, acc);
+}
+
 __global__ __launch_bounds__(WB) void wp_reach_k(WArgs a) {
     __shared__ u64 red[WB / WAVE];
     u64 c = 0, m = 0;
@@ -367,6 +377,7 @@ struct WPart {
     int rank = 0, world = 1;
     double mean_w = 1.0;
     int32_t delta = 0;
+    double tail[2] = {0.1, 64.0};  // tail switch (engine.h DeltaSteps): tail_frac (0 = off), threshold / delta
     DevBuf<u64> row;
     DevBuf<u32> col, w, lsplit;
     DevBuf<int32_t> dist, cand;
@@ -587,6 +598,30 @@ void wpart_info(const WPart& p, i64* out) {
     out[7] = p.nnz;
 }
 
+i64 wpart_unsettled(WPart& p, int32_t hi) {
+    hipStream_t s = p.ctx->stream;
+    u64 h = 0;
+    if (p.nl > 0) {
+        DevBuf<u64> acc(1);
+        PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
+        wp_unsettled_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(), hi, acc.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipMemcpyAsync(&h, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+    return (i64)h;
+}
+
+// a new light threshold at a band boundary (the tail switch): the light prefixes follow it
+void wpart_set_delta(WPart& p, int32_t delta) {
+    if (delta != p.delta && p.nl > 0) {
+        wp_lsplit_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, p.ctx->stream>>>(p.row.p, p.w.p, p.nl, (u32)delta,
+                                                                              p.lsplit.p);
+        PJ_LAUNCH_CHECK();
+    }
+    p.delta = delta;
+}
+
 int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
     hipStream_t s = p.ctx->stream;
     if (delta <= 0) {
@@ -720,11 +755,20 @@ struct WPartGpuSteps final : DeltaSteps {
     const i64* nf_dev() override { return reinterpret_cast<const i64*>(p.stat.p + ST_NF); }
     void select_async(int32_t lo, int32_t hi) override { wpart_select_async(p, lo, hi); }
     void end_round_async() override { wpart_end_round_async(p); }
+    double tail_frac() override { return p.tail[0]; }
+    int32_t tail_delta(int32_t delta) override {
+        return (int32_t)std::min(65536.0, std::max((double)delta, std::round(p.tail[1] * delta)));
+    }
+    i64 unsettled_edges(int32_t hi) override { return wpart_unsettled(p, hi); }
+    i64 local_edges() override { return p.nnz_local; }
+    void set_delta(int32_t delta) override { wpart_set_delta(p, delta); }
 };
 
 }  // namespace
 
 const Ctx& wpart_ctx(const WPart& p) { return *p.ctx; }
+
+double* wpart_tail_params(WPart& p) { return p.tail; }
 
 DeltaSteps& wpart_steps(WPart& p) {
     if (!p.steps) p.steps.reset(new WPartGpuSteps(p));

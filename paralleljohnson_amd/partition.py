@@ -293,6 +293,10 @@ class DeviceWPart:
         self.n, self.lo, self.hi, self.block, self.nnz_local, self.world, self.rank, self.nnz = list(info)
         self.nl = self.hi - self.lo
 
+    def set_option(self, key: str, value: float):
+        """pj_wpart_set_option ("tail_frac", "tail_mult"); the same on every rank."""
+        _check(_lib.pj_wpart_set_option(self._h, key.encode(), float(value)))
+
     def delta(self, comm: Comm, source: int, delta: int = 0) -> dict:
         """pj_wpart_delta: every rank of comm calls it with the same source and delta."""
         st = PartStats()

@@ -333,7 +333,9 @@ def test_part_group_one_gpu(pj, oracle, world, force):
 @pytest.mark.parametrize("world,transport", [(1, "rccl"), (2, "host"), (3, "host")])
 def test_wpart_group(pj, oracle, world, transport):
     """Weighted SSSP over the 1D partition (wpart.hip + the C++ band loop): every rank on the
-    one GPU; bit-exact against the oracle Dijkstra for several band widths and sources."""
+    one GPU; bit-exact against the oracle Dijkstra for several band widths and sources, with
+    the tail switch (all-reduced unsettled-edge count, then a 64x / 3x light threshold) at its
+    default, forced right after the first band, and off."""
     from paralleljohnson_amd.partition import delta_group, gather_group, load_weighted
     ctxs, comms = _group(pj, world, transport)
     cases = [(f"c{i}", n, ctxs[0].load_coo(s, d, w=w, n=n)) for i, (_, n, s, d, w) in enumerate(_wcases())]
@@ -350,11 +352,14 @@ def test_wpart_group(pj, oracle, world, transport):
             if r:
                 gr.close()
         g0.close()
-        for delta in (0, 7, 60):
+        for delta, tf, tm in ((0, 0.1, 64), (7, 2.0, 3), (60, 0.0, 64), (7, 0.1, 64)):
+            for p in parts:
+                p.set_option("tail_frac", tf)
+                p.set_option("tail_mult", tm)
             for source in (0, n // 3, n - 1, n + 2):
                 st = delta_group(parts, comms, source, delta)
                 exp = oracle.dijkstra(row, col, wc, source) if source < n else np.full(n, INF, np.int32)
-                assert np.array_equal(gather_group(parts, comms), exp), (name, delta, source, world)
+                assert np.array_equal(gather_group(parts, comms), exp), (name, delta, tf, tm, source, world)
                 reached = exp < INF
                 assert [st[0]["reached"], st[0]["reached_edges"]] == [int(reached.sum()),
                                                                       int(np.diff(row)[reached].sum())]

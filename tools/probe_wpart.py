@@ -1,0 +1,35 @@
+"""Weighted partitioned solve (wpart.hip + engine.cpp) on Kronecker s{scale} weights 1..255 at
+world 1 (no transport) and world 2 (both ranks on this GPU, host transport): per-solve time
+with the tail switch at its default and off. Usage: python tools/probe_wpart.py [scale=26]"""
+import os, sys, time
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
+import numpy as np
+import paralleljohnson_amd as pj
+from paralleljohnson_amd.partition import Comm, delta_group, load_weighted
+
+scale = int(sys.argv[1]) if len(sys.argv) > 1 else 26
+for world in (1, 2):
+    ctxs = [pj.Context(0) for _ in range(world)]
+    comms = Comm.group(ctxs, "host") if world > 1 else [Comm.for_rank(ctxs[0], 1, 0)]
+    parts, roots = [], None
+    for r in range(world):  # each rank cuts its block from a graph on its own context
+        g = ctxs[r].generate_kronecker(scale, 16, 1, weighted=True)
+        if roots is None:
+            roots = [int(x) for x in g.sample_roots(2, 3)]
+        parts.append(load_weighted(ctxs[r], g, r, world))
+        g.close()
+    for tf in (0.1, 0.0, 0.1, 0.0):
+        for p in parts:
+            p.set_option("tail_frac", tf)
+        ms = []
+        for r in roots:
+            st = delta_group(parts, comms, r)
+            ms.append(max(s["solve_ms"] for s in st))
+        print(f"world {world} s{scale}w tail_frac {tf}: solve ms {[round(x, 2) for x in ms]} bands {st[0]['bands']} "
+              f"rounds {st[0]['rounds']} sent {[s['sent'] for s in st]}", flush=True)
+    for p in parts:
+        p.close()
+    for c in comms:
+        c.close()
+    for c in ctxs:
+        c.close()
