@@ -418,7 +418,8 @@ typedef struct pj_part_stats {
     int64_t bands, rounds; /* delta-stepping: non-empty bands, light rounds */
     int64_t reached, reached_edges;
     int64_t sent;         /* ids (BFS) or (id, dist) pairs (delta) this rank sent */
-    int32_t delta, reserved;
+    int32_t delta;        /* delta-stepping: the light threshold the solve started with */
+    int32_t heavy_pulls;  /* delta-stepping: heavy steps done by pull (pj_wpart_set_option "pull_factor") */
 } pj_part_stats;
 
 /* The partitioned BFS of this rank (part.hip + the level loop of engine.cpp,
@@ -440,7 +441,10 @@ int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj
 /* pj_wpart_set_option keys: "tail_frac" (switch to the tail threshold once the edges of
  * the vertices not settled yet, over all ranks, drop below tail_frac x all edges; 0 = off;
  * default 0.1) and "tail_mult" (tail threshold and band width = tail_mult x delta,
- * default 64). Every rank must use the same values. */
+ * default 64) and "pull_factor" (heavy steps by pull -- the unsettled vertices scan their
+ * heavy rows for band members through an all-gathered byte map -- when the unsettled
+ * vertices' heavy edges are fewer than pull_factor x the members'; symmetric graphs only;
+ * 0 = always push; default 4). Every rank must use the same values. */
 int pj_wpart_set_option(pj_wpart* p, const char* key, double value);
 int pj_wpart_delta_group(int world, pj_wpart* const* parts, pj_comm* const* comms, int64_t source, int32_t delta,
                          pj_part_stats* st);

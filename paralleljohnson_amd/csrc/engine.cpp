@@ -169,7 +169,7 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             comm.allreduce(&all_edges, 1, false, s);
         }
         std::vector<i64> counts((size_t)S.world), rcounts((size_t)S.world);
-        i64 sent = 0, bands = 0, rounds = 0;
+        i64 sent = 0, bands = 0, rounds = 0, pulls = 0;
         auto exchange_apply = [&](int light, int32_t lo, int32_t hi) {
             S.relax(light, lo, hi, counts.data());
             i64 nr = 0;
@@ -230,7 +230,28 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
                 }
                 if (nf == 0) break;
             }
-            exchange_apply(0, (int32_t)lo, (int32_t)hi);  // heavy edges of the band's members
+            // heavy edges of the band's members: pulled by the unsettled vertices when those
+            // have fewer heavy edges than pull_factor x the members' (v2's rule, §4.2), else pushed
+            bool pulled = false;
+            const double pf = S.pull_factor();
+            if (pf >= 0.0 && hi - lo <= 255) {  // (member offsets are bytes)
+                // every rank must agree: a rank whose rows are not its in-edges (or with the
+                // pull off) vetoes it through the third count
+                i64 hc[3] = {0, 0, pf > 0.0 ? 1 : 0};
+                if (pf > 0.0) S.heavy_counts((int32_t)lo, (int32_t)hi, hc);
+                comm.allreduce(hc, 3, false, s);
+                if (hc[2] == S.world && hc[0] > 0 && (double)hc[1] < pf * (double)hc[0]) {
+                    S.member_slice((int32_t)lo, (int32_t)hi);
+                    if (S.world > 1) {
+                        const size_t sl = S.member_bytes();
+                        comm.allgather(static_cast<char*>(S.member_map()) + (size_t)S.rank * sl, S.member_map(), sl, s);
+                    }
+                    S.heavy_pull((int32_t)lo, (int32_t)hi);
+                    pulled = true;
+                    ++pulls;
+                }
+            }
+            if (!pulled) exchange_apply(0, (int32_t)lo, (int32_t)hi);
             if (tail_on) {
                 i64 ue = S.unsettled_edges((int32_t)hi);
                 if (ue < 0) {
@@ -261,6 +282,7 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             st->reached = rc[0];
             st->reached_edges = rc[1];
             st->sent = sent;
+            st->heavy_pulls = (int32_t)pulls;
         }
     });
 }

@@ -129,6 +129,18 @@ struct DeltaSteps {
     virtual i64 unsettled_edges(int32_t hi) { (void)hi; return -1; }
     virtual i64 local_edges() { return 0; }
     virtual void set_delta(int32_t delta) { (void)delta; }
+    // Heavy pull (optional; symmetric graphs): instead of the members pushing their heavy
+    // edges (relax / exchange / apply), every rank's unsettled vertices scan their own heavy
+    // rows for members, read from a replicated byte map (dist - lo of a member, 0xFF
+    // otherwise): member_slice() writes this rank's slice of member_map() (member_bytes()
+    // bytes at rank x member_bytes()), the engine all-gathers it, heavy_pull() relaxes.
+    // heavy_counts(): this rank's (members' heavy edges, unsettled vertices' heavy edges).
+    virtual double pull_factor() { return -1.0; }  // -1: no heavy pull (callback steps); 0: off on this rank
+    virtual void heavy_counts(int32_t lo, int32_t hi, i64* out2) { (void)lo, (void)hi, out2[0] = out2[1] = 0; }
+    virtual void member_slice(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
+    virtual void* member_map() { return nullptr; }
+    virtual size_t member_bytes() { return 0; }
+    virtual void heavy_pull(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
 };
 
 struct BfsParams {
@@ -151,6 +163,7 @@ BfsParams& part_params(Part& p);
 const Ctx& part_ctx(const Part& p);
 const Ctx& wpart_ctx(const WPart& p);
 double* wpart_tail_params(WPart& p);  // [0] tail_frac, [1] tail_mult (pj_wpart_set_option)
+double& wpart_pull_factor(WPart& p);  // heavy pull rule (pj_wpart_set_option "pull_factor")
 // every rank's slice of dist, gathered (n int32 to host; NULL: gather only)
 void part_gather_dist(Part& p, Comm& comm, int32_t* out);
 void wpart_gather_dist(WPart& p, Comm& comm, int32_t* out);

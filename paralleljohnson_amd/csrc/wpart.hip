@@ -336,6 +336,95 @@ __global__ void wp_lsplit_k(const u64* __restrict__ row, const u32* __restrict__
     }
 }
 
+// Heavy pull (engine.h DeltaSteps): (members' heavy edges, unsettled vertices' heavy edges)
+__global__ __launch_bounds__(WB) void wp_heavy_counts_k(WArgs a, int32_t hi, u64* __restrict__ out) {
+    __shared__ u64 red[WB / WAVE];
+    u64 m = 0, u = 0;
+    for (i64 v = (i64)blockIdx.x * WB + threadIdx.x; v < a.nl; v += (i64)gridDim.x * WB) {
+        const u64 hd = a.row[v + 1] - a.row[v] - a.lsplit[v];
+        if ((a.mb[v >> 6] >> (v & 63)) & 1ull) m += hd;
+        else if (a.dist[v] >= hi) u += hd;
+    }
+    m = block_sum<WB / WAVE>(m, red);
+    u = block_sum<WB / WAVE>(u, red);
+    if (threadIdx.x == 0) {
+        if (m) atomicAdd(&out[0], m);
+        if (u) atomicAdd(&out[1], u);
+    }
+}
+// this rank's slice of the member map: dist - lo of a band member, 0xFF otherwise
+__global__ void wp_member_slice_k(WArgs a, uint8_t* __restrict__ own) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < a.block; v += (i64)gridDim.x * blockDim.x) {
+        uint8_t x = 0xFF;
+        if (v < a.nl && ((a.mb[v >> 6] >> (v & 63)) & 1ull)) x = (uint8_t)(a.dist[v] - a.dlo);
+        own[v] = x;
+    }
+}
+// every unsettled owned vertex scans its heavy row (ascending weight) for band members
+// (any rank's, through the replicated map) and stops once lo + w >= its best value; the
+// first WP_PSERIAL edges by the lane alone, the rest of a long row by the whole wave
+constexpr int WP_PSERIAL = 16;
+__global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __restrict__ mmap) {
+    const int lane = lane_id();
+    const int32_t lo = a.dlo, hi = a.dhi;
+    const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
+    for (i64 b0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; b0 < a.nl; b0 += nwaves * 64) {
+        const i64 v = b0 + lane;
+        int32_t d0 = INT_INF, cur = INT_INF;
+        u64 k = 0, e = 0;
+        bool act = false;
+        if (v < a.nl) {
+            d0 = a.dist[v];
+            act = d0 >= hi;
+            if (act) {
+                cur = d0;
+                k = a.row[v] + a.lsplit[v];
+                e = a.row[v + 1];
+            }
+        }
+        const u64 lim = e - k > (u64)WP_PSERIAL ? k + WP_PSERIAL : e;
+        bool done = !act || k >= e;
+        while (act && k < lim) {
+            const u32 w = a.w[k];
+            if ((long long)lo + w >= (long long)cur) {
+                done = true;
+                break;
+            }
+            const uint8_t m = mmap[a.col[k]];
+            if (m != 0xFF) cur = min(cur, lo + (int32_t)m + (int32_t)w);
+            ++k;
+        }
+        if (k >= e) done = true;
+        u64 open = __ballot(!done);
+        while (open) {  // long rows: 64 edges per wave step, early stop when any lane may
+            const int l = __ffsll((long long)open) - 1;
+            open &= open - 1;
+            const u64 kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
+            int32_t cl = __shfl(cur, l, 64);
+            for (u64 kk = kb; kk < ke; kk += WAVE) {
+                const u64 k0 = kk + lane;
+                const bool valid = k0 < ke;
+                const u32 w = valid ? a.w[k0] : 0u;
+                const bool stop = !valid || (long long)lo + w >= (long long)cl;
+                int32_t cand = INT_INF;
+                if (!stop) {
+                    const uint8_t m = mmap[a.col[k0]];
+                    if (m != 0xFF) cand = lo + (int32_t)m + (int32_t)w;
+                }
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) {
+                    const int32_t y = __shfl_xor(cand, off, 64);
+                    cand = y < cand ? y : cand;
+                }
+                cl = cand < cl ? cand : cl;
+                if (__ballot(stop)) break;
+            }
+            if (lane == l) cur = cl;
+        }
+        if (act && cur < d0) a.dist[v] = cur;  // (the vertex's own rank is its only writer here)
+    }
+}
+
 // out-edges of the owned vertices not settled below hi (dist >= hi, unreached included)
 __global__ __launch_bounds__(WB) void wp_unsettled_k(WArgs a, int32_t hi, u64* __restrict__ out) {
     __shared__ u64 red[WB / WAVE];
@@ -378,6 +467,9 @@ struct WPart {
     double mean_w = 1.0;
     int32_t delta = 0;
     double tail[2] = {0.1, 64.0};  // tail switch (engine.h DeltaSteps): tail_frac (0 = off), threshold / delta
+    double pull_factor = 4.0;      // heavy pull when unsettled heavy edges < pull_factor x members' (0 = push)
+    bool symmetric = false;        // rows are also the in-edges (Kronecker graphs): the heavy pull applies
+    DevBuf<uint8_t> mmap;          // replicated member map of the heavy pull (world x block bytes)
     DevBuf<u64> row;
     DevBuf<u32> col, w, lsplit;
     DevBuf<int32_t> dist, cand;
@@ -545,6 +637,7 @@ WPart* wpart_from_graph(Graph& g, int rank, int world) {
     std::unique_ptr<WPart> p = wpart_geometry(g.ctx, g.n, g.nnz, rank, world);
     const u64 wsum = weight_sum(g.w.p, g.nnz, p->grid(), g.ctx->stream);
     wpart_cut(p.get(), g, p->lo, g.nnz > 0 ? (double)wsum / (double)g.nnz : 1.0);
+    p->symmetric = g.symmetric;
     return p.release();
 }
 
@@ -596,6 +689,37 @@ void wpart_info(const WPart& p, i64* out) {
     out[5] = p.world;
     out[6] = p.rank;
     out[7] = p.nnz;
+}
+
+void wpart_heavy_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
+    hipStream_t s = p.ctx->stream;
+    u64 h[2] = {0, 0};
+    if (p.nl > 0) {
+        DevBuf<u64> acc(2);
+        PJ_HIP(hipMemsetAsync(acc.p, 0, 2 * sizeof(u64), s));
+        wp_heavy_counts_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), hi, acc.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipMemcpyAsync(h, acc.p, 2 * sizeof(u64), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+    out2[0] = (i64)h[0];
+    out2[1] = (i64)h[1];
+}
+
+void wpart_member_slice(WPart& p, int32_t lo, int32_t hi) {
+    if (!p.mmap.p) p.mmap.alloc((size_t)p.world * (size_t)p.block);
+    wp_member_slice_k<<<grid_for(p.block, 256, p.grid()), 256, 0, p.ctx->stream>>>(
+        p.args(lo, hi), p.mmap.p + (size_t)p.rank * (size_t)p.block);
+    PJ_LAUNCH_CHECK();
+}
+
+void wpart_heavy_pull(WPart& p, int32_t lo, int32_t hi) {
+    hipStream_t s = p.ctx->stream;
+    if (p.nl > 0) {
+        wp_pull_heavy_k<<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.mmap.p);
+        PJ_LAUNCH_CHECK();
+    }
+    PJ_HIP(hipStreamSynchronize(s));
 }
 
 i64 wpart_unsettled(WPart& p, int32_t hi) {
@@ -762,6 +886,12 @@ struct WPartGpuSteps final : DeltaSteps {
     i64 unsettled_edges(int32_t hi) override { return wpart_unsettled(p, hi); }
     i64 local_edges() override { return p.nnz_local; }
     void set_delta(int32_t delta) override { wpart_set_delta(p, delta); }
+    double pull_factor() override { return p.symmetric ? p.pull_factor : 0.0; }  // (0: this rank vetoes)
+    void heavy_counts(int32_t lo, int32_t hi, i64* out2) override { wpart_heavy_counts(p, lo, hi, out2); }
+    void member_slice(int32_t lo, int32_t hi) override { wpart_member_slice(p, lo, hi); }
+    void* member_map() override { return p.mmap.p; }
+    size_t member_bytes() override { return (size_t)p.block; }
+    void heavy_pull(int32_t lo, int32_t hi) override { wpart_heavy_pull(p, lo, hi); }
 };
 
 }  // namespace
@@ -769,6 +899,7 @@ struct WPartGpuSteps final : DeltaSteps {
 const Ctx& wpart_ctx(const WPart& p) { return *p.ctx; }
 
 double* wpart_tail_params(WPart& p) { return p.tail; }
+double& wpart_pull_factor(WPart& p) { return p.pull_factor; }
 
 DeltaSteps& wpart_steps(WPart& p) {
     if (!p.steps) p.steps.reset(new WPartGpuSteps(p));

@@ -47,10 +47,10 @@ class PartInfo(ctypes.Structure):
 class PartStats(ctypes.Structure):
     _fields_ = [("solve_ms", ctypes.c_double), ("levels", _I64), ("td_levels", _I64), ("bu_levels", _I64),
                 ("bands", _I64), ("rounds", _I64), ("reached", _I64), ("reached_edges", _I64), ("sent", _I64),
-                ("delta", _I32), ("reserved", _I32)]
+                ("delta", _I32), ("heavy_pulls", _I32)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 _CB_ALLREDUCE = ctypes.CFUNCTYPE(_INT, _P, _PI64, _INT, _INT)

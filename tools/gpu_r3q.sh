@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 3: tail switch of the weighted partition (engine.cpp + wpart.hip): partition tests, then
-# per-solve times of the weighted partition at world 1 / 2 with the tail on and off (s24w, s26w)
+# per-solve times of the weighted partition at world 1 / 2 with the tail and heavy pull on and off (s24w, s26w)
 set -o pipefail
 OUT=gpurun_out/r3q; mkdir -p $OUT
 timeout -k 10 500 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_partition.py tests/test_gpu_parity.py -k "wpart or weighted_s22 or partition or cli_processes or multi" > $OUT/tests.log 2>&1 || { echo tests failed; tail -40 $OUT/tests.log; exit 1; }
