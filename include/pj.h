@@ -414,7 +414,7 @@ typedef struct pj_part_stats {
     double solve_ms;      /* host wall time of the solve on this rank, device work included
                              (the reference's timed region :459-462 ... :597-605) */
     int64_t levels;       /* BFS levels, or delta-stepping bands */
-    int64_t td_levels, bu_levels;
+    int64_t td_levels, bu_levels; /* BFS: push / pull levels; delta-stepping: -, light rounds run as pulls */
     int64_t bands, rounds; /* delta-stepping: non-empty bands, light rounds */
     int64_t reached, reached_edges;
     int64_t sent;         /* ids (BFS) or (id, dist) pairs (delta) this rank sent */
@@ -444,7 +444,10 @@ int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj
  * default 64) and "pull_factor" (heavy steps by pull -- the unsettled vertices scan their
  * heavy rows for band members through an all-gathered byte map -- when the unsettled
  * vertices' heavy edges are fewer than pull_factor x the members'; symmetric graphs only;
- * 0 = always push; default 4). Every rank must use the same values. */
+ * 0 = always push; default 4) and "light_pull" (a light round whose frontier has more light
+ * edges than the vertices above the band start / light_pull runs as a pull through an
+ * all-gathered frontier map; symmetric graphs; 0 = push; default 3). Every rank must use the
+ * same values. */
 int pj_wpart_set_option(pj_wpart* p, const char* key, double value);
 int pj_wpart_delta_group(int world, pj_wpart* const* parts, pj_comm* const* comms, int64_t source, int32_t delta,
                          pj_part_stats* st);

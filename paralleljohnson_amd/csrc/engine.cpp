@@ -169,7 +169,7 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             comm.allreduce(&all_edges, 1, false, s);
         }
         std::vector<i64> counts((size_t)S.world), rcounts((size_t)S.world);
-        i64 sent = 0, bands = 0, rounds = 0, pulls = 0;
+        i64 sent = 0, bands = 0, rounds = 0, pulls = 0, lpulls = 0;
         auto exchange_apply = [&](int light, int32_t lo, int32_t hi) {
             S.relax(light, lo, hi, counts.data());
             i64 nr = 0;
@@ -216,8 +216,29 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
                 continue;
             }
             ++bands;
+            i64 fsize = cnt;  // the round's frontier, all ranks
+            const double lpf = S.light_pull_factor();
             for (;;) {  // light rounds until no rank has a frontier
-                exchange_apply(1, (int32_t)lo, (int32_t)hi);
+                // a big round may pull (the gate keeps the counts off small rounds; every rank
+                // sees the same fsize, and any rank can veto through the third count)
+                bool lpulled = false;
+                if (lpf >= 0.0 && hi - lo <= 255 && fsize * 64 >= S.n) {
+                    i64 lc[3] = {0, 0, lpf > 0.0 ? 1 : 0};
+                    if (lpf > 0.0) S.light_counts((int32_t)lo, (int32_t)hi, lc);
+                    comm.allreduce(lc, 3, false, s);
+                    if (lc[2] == S.world && lc[0] > 0 && (double)lc[0] * lpf > (double)lc[1]) {
+                        S.frontier_slice((int32_t)lo, (int32_t)hi);
+                        if (S.world > 1) {
+                            const size_t sl = S.member_bytes();
+                            comm.allgather(static_cast<char*>(S.member_map()) + (size_t)S.rank * sl, S.member_map(),
+                                           sl, s);
+                        }
+                        S.light_pull((int32_t)lo, (int32_t)hi);
+                        lpulled = true;
+                        ++lpulls;
+                    }
+                }
+                if (!lpulled) exchange_apply(1, (int32_t)lo, (int32_t)hi);
                 ++rounds;
                 i64 nf = 0;
                 if (dev) {
@@ -229,6 +250,7 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
                     comm.allreduce(&nf, 1, false, s);
                 }
                 if (nf == 0) break;
+                fsize = nf;
             }
             // heavy edges of the band's members: pulled by the unsettled vertices when those
             // have fewer heavy edges than pull_factor x the members' (v2's rule, §4.2), else pushed
@@ -283,6 +305,7 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             st->reached_edges = rc[1];
             st->sent = sent;
             st->heavy_pulls = (int32_t)pulls;
+            st->bu_levels = lpulls;  // (delta-stepping: light rounds run as pulls)
         }
     });
 }

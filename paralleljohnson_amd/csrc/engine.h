@@ -141,6 +141,16 @@ struct DeltaSteps {
     virtual void* member_map() { return nullptr; }
     virtual size_t member_bytes() { return 0; }
     virtual void heavy_pull(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
+    // Light pull rounds (optional; symmetric graphs): a round whose frontier's light edges
+    // exceed the light edges of the vertices above lo / light_pull_factor() runs as a pull:
+    // frontier_slice() writes this rank's slice of member_map() (dist - lo of a frontier
+    // vertex, 0xFF otherwise), the engine all-gathers it, light_pull() lets every owned vertex
+    // above lo scan its light row for frontier vertices and marks the improved ones below hi.
+    // light_counts(): this rank's (frontier light edges, light edges of vertices above lo).
+    virtual double light_pull_factor() { return -1.0; }
+    virtual void light_counts(int32_t lo, int32_t hi, i64* out2) { (void)lo, (void)hi, out2[0] = out2[1] = 0; }
+    virtual void frontier_slice(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
+    virtual void light_pull(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
 };
 
 struct BfsParams {
@@ -164,6 +174,7 @@ const Ctx& part_ctx(const Part& p);
 const Ctx& wpart_ctx(const WPart& p);
 double* wpart_tail_params(WPart& p);  // [0] tail_frac, [1] tail_mult (pj_wpart_set_option)
 double& wpart_pull_factor(WPart& p);  // heavy pull rule (pj_wpart_set_option "pull_factor")
+double& wpart_light_pull(WPart& p);   // light pull rule (pj_wpart_set_option "light_pull")
 // every rank's slice of dist, gathered (n int32 to host; NULL: gather only)
 void part_gather_dist(Part& p, Comm& comm, int32_t* out);
 void wpart_gather_dist(WPart& p, Comm& comm, int32_t* out);

@@ -425,6 +425,110 @@ __global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __
     }
 }
 
+// Light pull rounds (engine.h DeltaSteps): (frontier light edges, light edges of vertices above lo)
+__global__ __launch_bounds__(WB) void wp_light_counts_k(WArgs a, u64* __restrict__ out) {
+    __shared__ u64 red[WB / WAVE];
+    u64 f = 0, u = 0;
+    for (i64 v = (i64)blockIdx.x * WB + threadIdx.x; v < a.nl; v += (i64)gridDim.x * WB) {
+        const u64 ls = a.lsplit[v];
+        if ((a.fr[v >> 6] >> (v & 63)) & 1ull) f += ls;
+        if (a.dist[v] > a.dlo) u += ls;
+    }
+    f = block_sum<WB / WAVE>(f, red);
+    u = block_sum<WB / WAVE>(u, red);
+    if (threadIdx.x == 0) {
+        if (f) atomicAdd(&out[0], f);
+        if (u) atomicAdd(&out[1], u);
+    }
+}
+// this rank's slice of the frontier map: dist - lo of a frontier vertex, 0xFF otherwise
+__global__ void wp_frontier_slice_k(WArgs a, uint8_t* __restrict__ own) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < a.block; v += (i64)gridDim.x * blockDim.x) {
+        uint8_t x = 0xFF;
+        if (v < a.nl && ((a.fr[v >> 6] >> (v & 63)) & 1ull)) x = (uint8_t)(a.dist[v] - a.dlo);
+        own[v] = x;
+    }
+}
+// every owned vertex above lo scans its light row (ascending weight) for frontier vertices
+// (any rank's, through the map; frozen at the slice: a label-correcting round) and stops
+// once lo + w >= its best value; improved vertices below hi join the next frontier. The
+// wave owns its 64 vertices' words: the frontier word moves into mb (the round consumed
+// it) and the next-frontier word is OR-ed in whole.
+__global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const uint8_t* __restrict__ fmap) {
+    __shared__ u64 red[WB / WAVE];
+    const int lane = lane_id();
+    const int32_t lo = a.dlo, hi = a.dhi;
+    const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
+    u64 marks = 0;
+    for (i64 b0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; b0 < a.nl; b0 += nwaves * 64) {
+        const i64 v = b0 + lane;
+        if (lane == 0) {
+            const u64 f = a.fr[b0 >> 6];
+            if (f) a.mb[b0 >> 6] |= f;
+        }
+        int32_t d0 = INT_INF, cur = INT_INF;
+        u64 k = 0, e = 0;
+        bool act = false;
+        if (v < a.nl) {
+            d0 = a.dist[v];
+            act = d0 > lo;
+            if (act) {
+                cur = d0;
+                k = a.row[v];
+                e = k + a.lsplit[v];
+            }
+        }
+        const u64 lim = e - k > (u64)WP_PSERIAL ? k + WP_PSERIAL : e;
+        bool done = !act || k >= e;
+        while (act && k < lim) {
+            const u32 w = a.w[k];
+            if ((long long)lo + w >= (long long)cur) {
+                done = true;
+                break;
+            }
+            const uint8_t m = fmap[a.col[k]];
+            if (m != 0xFF) cur = min(cur, lo + (int32_t)m + (int32_t)w);
+            ++k;
+        }
+        if (k >= e) done = true;
+        u64 open = __ballot(!done);
+        while (open) {
+            const int l = __ffsll((long long)open) - 1;
+            open &= open - 1;
+            const u64 kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
+            int32_t cl = __shfl(cur, l, 64);
+            for (u64 kk = kb; kk < ke; kk += WAVE) {
+                const u64 k0 = kk + lane;
+                const bool valid = k0 < ke;
+                const u32 w = valid ? a.w[k0] : 0u;
+                const bool stop = !valid || (long long)lo + w >= (long long)cl;
+                int32_t cand = INT_INF;
+                if (!stop) {
+                    const uint8_t m = fmap[a.col[k0]];
+                    if (m != 0xFF) cand = lo + (int32_t)m + (int32_t)w;
+                }
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) {
+                    const int32_t y = __shfl_xor(cand, off, 64);
+                    cand = y < cand ? y : cand;
+                }
+                cl = cand < cl ? cand : cl;
+                if (__ballot(stop)) break;
+            }
+            if (lane == l) cur = cl;
+        }
+        const bool imp = act && cur < d0;
+        if (imp) a.dist[v] = cur;
+        const u64 nb = __ballot(imp && cur < hi);
+        if (lane == 0 && nb) {
+            a.frn[b0 >> 6] |= nb;
+            marks += (u64)__popcll(nb);
+        }
+    }
+    marks = block_sum<WB / WAVE>(marks, red);
+    if (threadIdx.x == 0 && marks) atomicAdd(&a.stat[ST_NF], marks);
+}
+
 // out-edges of the owned vertices not settled below hi (dist >= hi, unreached included)
 __global__ __launch_bounds__(WB) void wp_unsettled_k(WArgs a, int32_t hi, u64* __restrict__ out) {
     __shared__ u64 red[WB / WAVE];
@@ -468,6 +572,8 @@ struct WPart {
     int32_t delta = 0;
     double tail[2] = {0.1, 64.0};  // tail switch (engine.h DeltaSteps): tail_frac (0 = off), threshold / delta
     double pull_factor = 4.0;      // heavy pull when unsettled heavy edges < pull_factor x members' (0 = push)
+    double light_pull = 3.0;       // light pull round when the frontier's light edges > the light edges
+                                   // of the vertices above lo / light_pull (0 = push)
     bool symmetric = false;        // rows are also the in-edges (Kronecker graphs): the heavy pull applies
     DevBuf<uint8_t> mmap;          // replicated member map of the heavy pull (world x block bytes)
     DevBuf<u64> row;
@@ -706,6 +812,38 @@ void wpart_heavy_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
     out2[1] = (i64)h[1];
 }
 
+void wpart_light_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
+    hipStream_t s = p.ctx->stream;
+    u64 h[2] = {0, 0};
+    if (p.nl > 0) {
+        DevBuf<u64> acc(2);
+        PJ_HIP(hipMemsetAsync(acc.p, 0, 2 * sizeof(u64), s));
+        wp_light_counts_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), acc.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipMemcpyAsync(h, acc.p, 2 * sizeof(u64), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+    out2[0] = (i64)h[0];
+    out2[1] = (i64)h[1];
+}
+
+void wpart_frontier_slice(WPart& p, int32_t lo, int32_t hi) {
+    if (!p.mmap.p) p.mmap.alloc((size_t)p.world * (size_t)p.block);
+    wp_frontier_slice_k<<<grid_for(p.block, 256, p.grid()), 256, 0, p.ctx->stream>>>(
+        p.args(lo, hi), p.mmap.p + (size_t)p.rank * (size_t)p.block);
+    PJ_LAUNCH_CHECK();
+}
+
+// one light round by pull (the counters ST_NF as a push round leaves them)
+void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
+    hipStream_t s = p.ctx->stream;
+    p.clear_stat();
+    if (p.nl > 0) {
+        wp_pull_light_k<<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.mmap.p);
+        PJ_LAUNCH_CHECK();
+    }
+}
+
 void wpart_member_slice(WPart& p, int32_t lo, int32_t hi) {
     if (!p.mmap.p) p.mmap.alloc((size_t)p.world * (size_t)p.block);
     wp_member_slice_k<<<grid_for(p.block, 256, p.grid()), 256, 0, p.ctx->stream>>>(
@@ -892,6 +1030,10 @@ struct WPartGpuSteps final : DeltaSteps {
     void* member_map() override { return p.mmap.p; }
     size_t member_bytes() override { return (size_t)p.block; }
     void heavy_pull(int32_t lo, int32_t hi) override { wpart_heavy_pull(p, lo, hi); }
+    double light_pull_factor() override { return p.symmetric ? p.light_pull : 0.0; }
+    void light_counts(int32_t lo, int32_t hi, i64* out2) override { wpart_light_counts(p, lo, hi, out2); }
+    void frontier_slice(int32_t lo, int32_t hi) override { wpart_frontier_slice(p, lo, hi); }
+    void light_pull(int32_t lo, int32_t hi) override { wpart_light_pull(p, lo, hi); }
 };
 
 }  // namespace
@@ -900,6 +1042,7 @@ const Ctx& wpart_ctx(const WPart& p) { return *p.ctx; }
 
 double* wpart_tail_params(WPart& p) { return p.tail; }
 double& wpart_pull_factor(WPart& p) { return p.pull_factor; }
+double& wpart_light_pull(WPart& p) { return p.light_pull; }
 
 DeltaSteps& wpart_steps(WPart& p) {
     if (!p.steps) p.steps.reset(new WPartGpuSteps(p));

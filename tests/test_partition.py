@@ -337,7 +337,8 @@ def test_wpart_group(pj, oracle, world, transport):
     the tail switch (all-reduced unsettled-edge count, then a 64x / 3x light threshold) at its
     default, forced right after the first band, and off; heavy steps pushed, pulled (the
     Kronecker case: unsettled vertices scan their heavy rows through the all-gathered member
-    map) by the default rule, and pulled whenever the graph allows."""
+    map) by the default rule, and pulled whenever the graph allows; light rounds pushed, pulled by
+    the default rule and pulled whenever the frontier is big enough."""
     from paralleljohnson_amd.partition import delta_group, gather_group, load_weighted
     ctxs, comms = _group(pj, world, transport)
     cases = [(f"c{i}", n, ctxs[0].load_coo(s, d, w=w, n=n)) for i, (_, n, s, d, w) in enumerate(_wcases())]
@@ -354,16 +355,17 @@ def test_wpart_group(pj, oracle, world, transport):
             if r:
                 gr.close()
         g0.close()
-        for delta, tf, tm, pf in ((0, 0.1, 64, 4), (7, 2.0, 3, 1e9), (60, 0.0, 64, 0), (7, 0.1, 64, 1e9),
-                                  (0, 0.0, 64, 4)):
+        for delta, tf, tm, pf, lp in ((0, 0.1, 64, 4, 3), (7, 2.0, 3, 1e9, 1e9), (60, 0.0, 64, 0, 0),
+                                      (7, 0.1, 64, 1e9, 3), (0, 0.0, 64, 4, 1e9)):
             for p in parts:
                 p.set_option("tail_frac", tf)
                 p.set_option("tail_mult", tm)
                 p.set_option("pull_factor", pf)
+                p.set_option("light_pull", lp)
             for source in (0, n // 3, n - 1, n + 2):
                 st = delta_group(parts, comms, source, delta)
                 exp = oracle.dijkstra(row, col, wc, source) if source < n else np.full(n, INF, np.int32)
-                assert np.array_equal(gather_group(parts, comms), exp), (name, delta, tf, tm, pf, source, world)
+                assert np.array_equal(gather_group(parts, comms), exp), (name, delta, tf, tm, pf, lp, source, world)
                 reached = exp < INF
                 assert [st[0]["reached"], st[0]["reached_edges"]] == [int(reached.sum()),
                                                                       int(np.diff(row)[reached].sum())]

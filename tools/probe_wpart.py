@@ -1,6 +1,6 @@
 """Weighted partitioned solve (wpart.hip + engine.cpp) on Kronecker s{scale} weights 1..255 at
 world 1 (no transport) and world 2 (both ranks on this GPU, host transport): per-solve time
-with the tail switch and the heavy pull at their defaults and off. Usage: python tools/probe_wpart.py [scale=26]"""
+with the tail switch, the heavy pull and the light pull rounds at their defaults and off. Usage: python tools/probe_wpart.py [scale=26]"""
 import os, sys, time
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
 import numpy as np
@@ -18,16 +18,18 @@ for world in (1, 2):
             roots = [int(x) for x in g.sample_roots(2, 3)]
         parts.append(load_weighted(ctxs[r], g, r, world))
         g.close()
-    for tf, pf in ((0.1, 4), (0.1, 0), (0.0, 0), (0.1, 4), (0.1, 0), (0.0, 0)):
+    for tf, pf, lp in ((0.1, 4, 3), (0.1, 4, 0), (0.1, 0, 0), (0.1, 4, 3), (0.1, 4, 0), (0.1, 0, 0)):
         for p in parts:
             p.set_option("tail_frac", tf)
             p.set_option("pull_factor", pf)
+            p.set_option("light_pull", lp)
         ms = []
         for r in roots:
             st = delta_group(parts, comms, r)
             ms.append(max(s["solve_ms"] for s in st))
-        print(f"world {world} s{scale}w tail_frac {tf} pull_factor {pf}: solve ms {[round(x, 2) for x in ms]} "
-              f"bands {st[0]['bands']} rounds {st[0]['rounds']} heavy pulls {st[0]['heavy_pulls']} "
+        print(f"world {world} s{scale}w tail_frac {tf} pull_factor {pf} light_pull {lp}: solve ms "
+              f"{[round(x, 2) for x in ms]} bands {st[0]['bands']} rounds {st[0]['rounds']} heavy pulls "
+              f"{st[0]['heavy_pulls']} light pulls {st[0]['bu_levels']} "
               f"sent {[s['sent'] for s in st]}", flush=True)
     for p in parts:
         p.close()
