@@ -125,40 +125,47 @@ def run_workload(ctx, key, args, rank, world, barrier, steps, warmup):
                 roots=my_roots[:steps], reach=reach, levels=levels, gen_s=gen_s, build_s=build_s, prep_s=prep_s)
 
 
-def time_to_solution(ctx_s, res, args, wl):
+def tts_process(args, wl, td):
     """SURVEY.md §8d time-to-solution (process start -> sol_file closed) as ONE wall clock:
     bin/pj_kron_tts, a fresh process through the C-ABI (pj_create, on-device Kronecker
     generation + radix sort + CSR, the first solve with the solver's preparation, D2H,
-    pj_write_sol), timed by this process from launch to exit. The reference cannot read a
-    2^31-line text file (:66/:117), so the graph comes from the generator. The in-process
-    phases of this run are reported beside it as a breakdown."""
+    pj_write_sol), timed by this process from launch to exit, for the bench's first root
+    (picked inside the tool). Run before this process builds anything, so the tool has
+    the GPU to itself, as a user's run would. The reference cannot read a 2^31-line text
+    file (:66/:117), so the graph comes from the generator."""
     import subprocess
-    import paralleljohnson_amd as pj
-    g, r = res["g"], res["roots"][0]
-    t0 = time.perf_counter()
-    d = g.sssp(r)
-    t1 = time.perf_counter()
-    with tempfile.TemporaryDirectory() as td:
-        pj.write_sol(d, os.path.join(td, "sol.txt"))
-        t2 = time.perf_counter()
-        phases = {"hip_context_s": round(ctx_s, 4), "graph_build_s": round(res["build_s"], 4),
-                  "solver_prep_s": round(res["prep_s"], 4), "solve_and_d2h_s": round(t1 - t0, 4),
-                  "write_sol_s": round(t2 - t1, 4)}
-        tool = os.path.join(ROOT, "paralleljohnson_amd", "bin", "pj_kron_tts")
-        scale = args.scale if args.scale else wl["scale"]
-        out = os.path.join(td, "sol_tts.txt")
-        t3 = time.perf_counter()
-        p = subprocess.run([tool, str(scale), str(args.edgefactor), str(args.seed), str(int(wl["weighted"])), str(r),
-                            out], capture_output=True, text=True, timeout=300)
-        wall = time.perf_counter() - t3
-        if p.returncode != 0:
-            raise RuntimeError(f"pj_kron_tts failed: {p.stderr[-400:]}")
-        same = open(out, "rb").read() == open(os.path.join(td, "sol.txt"), "rb").read()
+    tool = os.path.join(ROOT, "paralleljohnson_amd", "bin", "pj_kron_tts")
+    scale = args.scale if args.scale else wl["scale"]
+    out = os.path.join(td, "sol_tts.txt")
+    t3 = time.perf_counter()
+    p = subprocess.run([tool, str(scale), str(args.edgefactor), str(args.seed), str(int(wl["weighted"])),
+                        f"sample:{args.seed + 1}", out], capture_output=True, text=True, timeout=300)
+    wall = time.perf_counter() - t3
+    if p.returncode != 0:
+        raise RuntimeError(f"pj_kron_tts failed: {p.stderr[-400:]}")
     f = p.stdout.split()
-    tool_phases = dict(zip(("create_s", "build_s", "solve_prep_d2h_s", "write_s"), (float(x) for x in f[1:5])))
-    return round(wall, 4), {"wall_clock": "bin/pj_kron_tts, process launch -> exit (sol_file closed)",
-                            "process_phases": tool_phases, "sol_identical_to_bench_process": same,
-                            "in_process_breakdown": phases}
+    phases = dict(zip(("create_s", "build_s", "solve_prep_d2h_s", "write_s"), (float(x) for x in f[1:5])))
+    return {"wall": round(wall, 4), "phases": phases, "root": int(f[6]), "sol": out}
+
+
+def time_to_solution(ctx_s, res, tts, td):
+    """The tool's wall clock (tts_process) with this process's phases as a breakdown, and
+    whether the tool's sol_file equals this process's for the same root."""
+    import paralleljohnson_amd as pj
+    g = res["g"]
+    t0 = time.perf_counter()
+    d = g.sssp(tts["root"])
+    t1 = time.perf_counter()
+    pj.write_sol(d, os.path.join(td, "sol.txt"))
+    t2 = time.perf_counter()
+    phases = {"hip_context_s": round(ctx_s, 4), "graph_build_s": round(res["build_s"], 4),
+              "solver_prep_s": round(res["prep_s"], 4), "solve_and_d2h_s": round(t1 - t0, 4),
+              "write_sol_s": round(t2 - t1, 4)}
+    same = open(tts["sol"], "rb").read() == open(os.path.join(td, "sol.txt"), "rb").read()
+    return tts["wall"], {"wall_clock": "bin/pj_kron_tts, process launch -> exit (sol_file closed), run before "
+                                       "this process built its graph",
+                         "process_phases": tts["phases"], "root": tts["root"], "sol_identical_to_bench_process": same,
+                         "in_process_breakdown": phases}
 
 
 def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
@@ -295,6 +302,52 @@ def run_multisource(ctx, args, rank, world, barrier, n_src=1024):
     return dict(elapsed=elapsed, m=m, b=b, n_src=len(mine), cpu=cpu, reps=reps)
 
 
+def run_wpartitioned_host(args, world_h=2, nroots=3, scale=26):
+    """The weighted 1D partition (wpart.hip + libpj's band loop: tail switch, heavy and light
+    pulls through all-gathered byte maps) on configs[2]'s graph (Kronecker s26, weights
+    1..255) at world 2, both ranks in this process on ONE GPU over the host transport (device
+    copies + host barriers; not xGMI/RCCL): the reference's only mode (:344-594) for a graph
+    split over ranks, timed per solve."""
+    import paralleljohnson_amd as pj
+    from paralleljohnson_amd.partition import Comm, delta_group, load_weighted
+    ctxs = [pj.Context(0) for _ in range(world_h)]
+    comms = Comm.group(ctxs, "host")
+    parts, roots = [], None
+    t0 = time.perf_counter()
+    try:
+        for r in range(world_h):  # each rank cuts its block from the graph generated on its context
+            g = ctxs[r].generate_kronecker(scale, args.edgefactor, args.seed, weighted=True)
+            if roots is None:
+                roots = [int(x) for x in g.sample_roots(args.seed + 1, nroots)]
+            parts.append(load_weighted(ctxs[r], g, r, world_h))
+            g.close()
+        build_s = time.perf_counter() - t0
+        delta_group(parts, comms, roots[0])  # warm-up (workspace)
+        sts = []
+        t = time.perf_counter()
+        for r in roots:
+            sts.append(delta_group(parts, comms, r))
+        elapsed = time.perf_counter() - t
+        m = float(sum(st[0]["reached_edges"] for st in sts))
+        st0 = sts[0]
+        return {
+            "workload": f"graph500-kronecker-s{scale}-ef{args.edgefactor}-w1..255-delta-stepping, 1D vertex partition "
+                        f"at world {world_h}, both ranks on ONE GPU over the host transport (not xGMI/RCCL)",
+            "roots": len(roots), "ms_per_sssp": round(1000.0 * elapsed / len(roots), 3),
+            "gteps": round(m / elapsed / 1e9, 3), "bands": st0[0]["bands"], "light_rounds": st0[0]["rounds"],
+            "heavy_pulls": st0[0]["heavy_pulls"], "light_pulls": st0[0]["bu_levels"],
+            "solve_ms_max_rank": [round(max(x["solve_ms"] for x in st), 2) for st in sts],
+            "pairs_sent_per_sssp_by_rank": [x["sent"] for x in st0], "build_s": round(build_s, 2),
+        }
+    finally:
+        for p in parts:
+            p.close()
+        for c in comms:
+            c.close()
+        for c in ctxs:
+            c.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -346,6 +399,10 @@ def main():
     t_ctx = time.perf_counter()
     ctx = pj.Context(local)
     ctx_s = time.perf_counter() - t_ctx
+    tts_dir = tempfile.TemporaryDirectory()
+    tts = None
+    if rank == 0 and WORKLOADS[args.workload]["kind"] == "kronecker":
+        tts = tts_process(args, WORKLOADS[args.workload], tts_dir.name)
     main_res = run_workload(ctx, args.workload, args, rank, world, barrier, args.steps, args.warmup)
     elapsed, m_sum, b_sum, t_kernel = main_res["elapsed"], main_res["m_sum"], main_res["b_sum"], main_res["t_kernel"]
     if dist is not None:
@@ -366,7 +423,8 @@ def main():
         with open(tj_path) as f:
             traffic = json.load(f).get("hbm_bytes_per_sssp")
 
-    tts_s, tts_phases = time_to_solution(ctx_s, main_res, args, main_res["wl"]) if rank == 0 else (None, None)
+    tts_s, tts_phases = time_to_solution(ctx_s, main_res, tts, tts_dir.name) if tts else (None, None)
+    tts_dir.cleanup()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(g, main_res, args)
@@ -463,6 +521,10 @@ def main():
             secondary["k28_partitioned_host_w2"] = run_partitioned_host(args)
         except Exception as e:  # noqa: BLE001
             secondary["k28_partitioned_host_w2"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        try:
+            secondary["k26w_partitioned_host_w2"] = run_wpartitioned_host(args)
+        except Exception as e:  # noqa: BLE001
+            secondary["k26w_partitioned_host_w2"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if pr is not None:
         per = el / pr["roots"]
         secondary["k28_partitioned"] = {

@@ -47,6 +47,9 @@ namespace {
 #ifndef PJ_PB2
 #define PJ_PB2 8
 #endif
+#ifndef PJ_BFS_STAMPS
+#define PJ_BFS_STAMPS 0  // diagnostic build: block 0 stamps s_memrealtime per launch / small level (stderr)
+#endif
 #ifndef PJ_SMALL_WG_ATOMIC
 #define PJ_SMALL_WG_ATOMIC 1  // small_levels claims: workgroup-scope atomics (one block is running)
 #endif
@@ -110,7 +113,20 @@ struct BfsArgs {
     LevelState* S;  // [2]
     u64* nmode;     // [2] push / pull levels run (device)
     int64_t* host;  // mapped host words: [0] levels run (-1 while running), [1] push, [2] pull, [3] launches
+    u64* stamps;    // PJ_BFS_STAMPS builds: [launch * 64 + slot] 100 MHz timestamps of block 0
 };
+
+// (PJ_BFS_STAMPS) thread 0 of block 0 records the real-time counter in slot k of launch li
+__device__ __forceinline__ void bfs_stamp(const BfsArgs& a, int32_t li, int k) {
+#if PJ_BFS_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x == 0 && li < 64 && k < 64)
+        a.stamps[(u64)li * 64 + (u64)k] = __builtin_amdgcn_s_memrealtime();
+#else
+    (void)a;
+    (void)li;
+    (void)k;
+#endif
+}
 
 template <typename Off>
 struct Graph_d {
@@ -391,6 +407,7 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
     u64 fprev = d.found, nlev = 0;
     for (;;) {
         __syncthreads();
+        bfs_stamp(a, li, 2 + 3 * (int)nlev);
         u32 E;
         const u32 ex = block_excl_scan<NW>(t < F ? ss.cdeg[t] : 0u, ss.scan, E);
         ss.cex[t] = ex;
@@ -468,9 +485,11 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
             }
         }
         const u64 mq = block_sum<NW>(acc.m, red);
+        bfs_stamp(a, li, 3 + 3 * (int)nlev);
         const u64 f = block_sum<NW>(acc.f, red);
         const u64 in = block_sum<NW>(acc.in, red);
         const u32 NF = ss.nn;  // = the level's found vertices with out-degree > 0
+        bfs_stamp(a, li, 4 + 3 * (int)nlev);
         ++nlev;
         // decide() for level L + 1, from what level L would publish
         const int32_t L2 = L + 1;
@@ -574,7 +593,9 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
     } U;
     __shared__ u64 red[NW];
     Decision d;
+    bfs_stamp(a, li, 0);
     const int dec = decide(a, li, d);
+    bfs_stamp(a, li, 1);
     const bool go = dec == 2;
     const u32 t = threadIdx.x;
     const int32_t L = d.L;
@@ -916,6 +937,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
     }
     flush(q, a, cacc, L);
     flush_acc(cacc, acc, red);
+    bfs_stamp(a, li, 63);
 }
 
 // dist := INF, vis := isolated-vertex mask, then the source; level -1's counters
@@ -1086,6 +1108,12 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.host), w.host, 0));
     Graph_d<Off> gd{static_cast<const Off*>(g.row_ptr()), g.col.p, static_cast<const Off*>(g.crow_ptr()),
                     g.ccol_ptr()};
+#if PJ_BFS_STAMPS
+    static DevBuf<u64> stamps;
+    stamps.ensure(64 * 64);
+    PJ_HIP(hipMemsetAsync(stamps.p, 0, 64 * 64 * sizeof(u64), s));
+    a.stamps = stamps.p;
+#endif
 
     // workgroups per CU: 4, or 2 on small graphs (< 2^25 entries), whose levels are short and
     // latency-bound, so a smaller grid drains faster (web-Google-shaped: 0.297 -> 0.281 ms per
@@ -1144,6 +1172,20 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     }
     g.stats = st;
     g.have_result = true;
+#if PJ_BFS_STAMPS
+    {  // per launch: decide, then per small level (start, edges done, counters done), block 0's end
+        std::vector<u64> h(64 * 64);
+        PJ_HIP(hipMemcpy(h.data(), stamps.p, h.size() * sizeof(u64), hipMemcpyDeviceToHost));
+        const u64 t0 = h[0];
+        for (int l = 0; l < 64 && h[(size_t)l * 64]; ++l) {
+            std::fprintf(stderr, "stamps launch %d:", l);
+            for (int k = 0; k < 64; ++k)
+                if (h[(size_t)l * 64 + k])
+                    std::fprintf(stderr, " %d@%.2f", k, (double)(h[(size_t)l * 64 + k] - t0) / 100.0);
+            std::fprintf(stderr, "\n");
+        }
+    }
+#endif
 }
 
 void bfs_workspace(Graph& g) {

@@ -789,8 +789,8 @@ __global__ __launch_bounds__(DB) void d_pull_heavy_k(const Off* __restrict__ row
     }
 }
 
-template <typename Off>
-__global__ void light_split_k(const Off* __restrict__ row, const u32* __restrict__ w, i64 n, u32 delta,
+template <typename Off, typename WT>
+__global__ void light_split_k(const Off* __restrict__ row, const WT* __restrict__ w, i64 n, u32 delta,
                               u32* __restrict__ lsplit) {
     for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
         Off lo = row[v], hi = row[v + 1];
@@ -2485,46 +2485,23 @@ __global__ void v2_interleave_k(const u32* __restrict__ col, const u32* __restri
     for (i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (i64)gridDim.x * blockDim.x)
         cw[k] = (u64)col[k] | ((u64)w[k] << 32);
 }
-__global__ void v2_w8_k(const u32* __restrict__ w, i64 m, uint8_t* __restrict__ w8) {
-    for (i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (i64)gridDim.x * blockDim.x)
-        w8[k] = (uint8_t)w[k];
+__global__ void widen_k(const uint8_t* __restrict__ w8, i64 m, u32* __restrict__ w) {
+    for (i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (i64)gridDim.x * blockDim.x) w[k] = w8[k];
 }
-// Light CSR: lcw[lrow[v] + j] = cw[row[v] + j] for j < lsplit[v] (a wave per vertex
-// for long prefixes, a lane per vertex otherwise).
+// Light CSR: lcw[lrow[v] + j] = the record of row[v] + j for j < lsplit[v], packed
+// (col | w << cb) in 32 bits when it fits.
 __device__ __forceinline__ void v2_lput(u64* __restrict__ o, u64 k, u64 x, u32) { o[k] = x; }
 __device__ __forceinline__ void v2_lput(u32* __restrict__ o, u64 k, u64 x, u32 cb) {
     o[k] = (u32)x | ((u32)(x >> 32) << cb);
 }
 // (the edge records come from cw, or from the relabeled col / w arrays when cw is null)
+template <typename WT>
 __device__ __forceinline__ u64 v2_rec(const u64* __restrict__ cw, const u32* __restrict__ col,
-                                      const u32* __restrict__ wt, u64 k) {
+                                      const WT* __restrict__ wt, u64 k) {
     return cw ? cw[k] : (u64)col[k] | ((u64)wt[k] << 32);
 }
-template <typename Off, typename OutT>
-__global__ void v2_light_csr_k(const Off* __restrict__ row, const u32* __restrict__ lsplit, const u64* __restrict__ lrow,
-                               const u64* __restrict__ cw, const u32* __restrict__ col, const u32* __restrict__ wt,
-                               i64 n, OutT* __restrict__ lcw, u32 cb) {
-    const int lane = lane_id();
-    for (i64 v0 = ((i64)blockIdx.x * blockDim.x + threadIdx.x) & ~63ll; v0 < n; v0 += (i64)gridDim.x * blockDim.x) {
-        const i64 v = v0 + lane;
-        const u32 ls = v < n ? lsplit[v] : 0u;
-        const bool longp = ls > 64;
-        if (v < n && !longp)
-            for (u32 j = 0; j < ls; ++j) v2_lput(lcw, lrow[v] + j, v2_rec(cw, col, wt, (u64)row[v] + j), cb);
-        u64 lm = __ballot(longp);
-        while (lm) {
-            const int l = __ffsll((long long)lm) - 1;
-            lm &= lm - 1;
-            const i64 vl = v0 + l;
-            const u64 src = (u64)row[vl], dst = lrow[vl];
-            const u32 cnt = lsplit[vl];
-            for (u32 j = lane; j < cnt; j += WAVE) v2_lput(lcw, dst + j, v2_rec(cw, col, wt, src + j), cb);
-        }
-    }
-}
-
-// Edge-tiled light CSR build (the lane-per-vertex form above stored each lane's
-// prefix to its own place: uncoalesced, 11 ms at s26): a block takes LT_E consecutive
+// Edge-tiled light CSR build (a lane-per-vertex form stored each lane's prefix to
+// its own place: uncoalesced, 11 ms at s26): a block takes LT_E consecutive
 // light-CSR positions, stages the light-row starts of the vertices they belong to in
 // LDS (tile table lt_row, like relabel.hip's copy tiles) and copies LT_E / 256 entries
 // per thread with coalesced stores, each row found by a binary search in LDS.
@@ -2539,10 +2516,10 @@ __global__ void v2_light_tiles_k(const u64* __restrict__ lrow, i64 n, u64 light,
         if (e == (i64)light) trow[ntiles] = (u32)v;
     }
 }
-template <typename Off, typename OutT>
+template <typename Off, typename OutT, typename WT>
 __global__ __launch_bounds__(256) void v2_light_csr_tiled_k(const Off* __restrict__ row, const u64* __restrict__ lrow,
                                                             const u64* __restrict__ cw, const u32* __restrict__ col,
-                                                            const u32* __restrict__ wt, u64 light,
+                                                            const WT* __restrict__ wt, u64 light,
                                                             const u32* __restrict__ trow, OutT* __restrict__ lcw,
                                                             u32 cb) {
     __shared__ u64 s_lb[LT_R + 1];
@@ -2584,12 +2561,6 @@ __global__ __launch_bounds__(DB) void v2_heavy_left_k(const Off* __restrict__ ro
     if (lane_id() == 0 && acc) atomicAdd(out, acc);
 }
 
-__global__ void v2_wmax_k(const u32* __restrict__ w, i64 m, u32* __restrict__ out) {
-    u32 x = 0;
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x) x = max(x, w[i]);
-    x = wave_max(x);
-    if (lane_id() == 0 && x) atomicMax(out, x);
-}
 
 
 // hl bit v = (lsplit[v] > 0): the vertices that have light edges for this delta
@@ -2640,7 +2611,6 @@ struct DeltaWork {
     DevBuf<u32> lcw32;     // the light CSR packed (col | w << lcb), when it fits
     u32 lcb = 0;
     int packed_for = -1;   // g.light_pack the light CSR was built for
-    DevBuf<uint8_t> w8;    // u8 copy of the relabeled weights (max weight <= 255)
     DevBuf<u64> hl;        // has-light-edges bitmap (per delta)
     // binned light rounds (per delta): pair buffers, cursors, bucket tables
     DevBuf<u64> bp1, bp2, bc1, bc2, br1, br2;
@@ -2658,6 +2628,44 @@ struct DeltaWork {
 void delete_delta_work(DeltaWork* p) { delete p; }
 
 namespace {
+
+}  // namespace
+
+void preload_delta_module() {
+    hipFuncAttributes fa;
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&light_split_k<u32, uint8_t>));
+}
+
+namespace {
+
+// u32 relabeled weights, widened from the relabel copy's u8 weights on first use
+// (the v1 band loop and the interleaved records read u32)
+void ensure_w32(Graph& g) {
+    Relabeled& R = *g.rl;
+    if (R.w.p || !R.w8.p || g.nnz == 0) return;
+    R.w.alloc((size_t)g.nnz);
+    widen_k<<<grid_for(g.nnz, 256, (unsigned)g.ctx->cu_count * 8u), 256, 0, g.ctx->stream>>>(R.w8.p, g.nnz, R.w.p);
+    PJ_LAUNCH_CHECK();
+}
+
+template <typename Off>
+void launch_light_split(const Relabeled& R, const Off* row, i64 n, u32 delta, u32* out, unsigned maxgrid,
+                        hipStream_t s) {
+    if (R.w8.p) light_split_k<Off, uint8_t><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w8.p, n, delta, out);
+    else light_split_k<Off, u32><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, delta, out);
+    PJ_LAUNCH_CHECK();
+}
+
+template <typename Off, typename OutT>
+void light_csr_tiled(const Relabeled& R, const Off* row, const DeltaWork& w, u64 light, const u32* ltrow, OutT* out,
+                     u32 cb, unsigned grid, hipStream_t s) {
+    if (R.w8.p)
+        v2_light_csr_tiled_k<Off, OutT, uint8_t><<<grid, 256, 0, s>>>(row, w.lrow.p, w.cw.p, R.col.p, R.w8.p, light,
+                                                                      ltrow, out, cb);
+    else
+        v2_light_csr_tiled_k<Off, OutT, u32><<<grid, 256, 0, s>>>(row, w.lrow.p, w.cw.p, R.col.p, R.w.p, light,
+                                                                  ltrow, out, cb);
+}
 
 // delta (explicit option, else 3.5 * mean weight / mean out-degree over all input
 // ids: light edges are then ~5% of a row; swept on Kronecker s26 with weights
@@ -2678,36 +2686,19 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         const double d = 3.5 * g.mean_weight / std::max(1.0, mean_deg);
         delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(d)));
     }
-    if (w.maxw < 0 && g.max_weight >= 0) w.maxw = g.max_weight;  // (the relabeled weights are the same)
-    if (w.maxw < 0) {  // largest weight: decides whether the tail has heavy edges at all
-        u32 h = 0;
-        if (g.nnz > 0) {
-            DevBuf<u32> m(1);
-            PJ_HIP(hipMemsetAsync(m.p, 0, sizeof(u32), s));
-            v2_wmax_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.w.p, g.nnz, m.p);
-            PJ_LAUNCH_CHECK();
-            PJ_HIP(hipMemcpyAsync(&h, m.p, sizeof(u32), hipMemcpyDeviceToHost, s));
-            PJ_HIP(hipStreamSynchronize(s));
-        }
-        w.maxw = (long long)h;
-    }
-    if (g.split_w && w.maxw <= 255 && !w.w8.p && g.nnz > 0) {  // u8 weights beside the ids
-        w.w8.alloc((size_t)g.nnz);
-        v2_w8_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.w.p, g.nnz, w.w8.p);
-        PJ_LAUNCH_CHECK();
-    }
-    // whole-CSR records: u32 ids + u8 weights (split) when every weight fits 8 bits,
-    // else the interleaved u64 copy
-    const bool split = g.split_w && w.maxw <= 255;
+    w.maxw = std::max(0ll, g.max_weight);  // (the relabel copy's reduction; the relabeled weights are the same)
+    // whole-CSR records: u32 ids + u8 weights (split) when every weight fits 8 bits (the
+    // relabel copy then wrote them as u8), else the interleaved u64 copy
+    const bool split = g.split_w && R.w8.p;
     if (!split && !w.cw.p && g.nnz > 0) {
+        ensure_w32(g);
         w.cw.alloc((size_t)g.nnz);
         v2_interleave_k<<<grid_for(g.nnz, 256, maxgrid), 256, 0, s>>>(R.col.p, R.w.p, g.nnz, w.cw.p);
         PJ_LAUNCH_CHECK();
     }
     if ((w.lsplit_delta != (u32)delta || w.packed_for != g.light_pack) && n > 0) {
         w.packed_for = g.light_pack;
-        light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)delta, w.lsplit.p);
-        PJ_LAUNCH_CHECK();
+        launch_light_split<Off>(R, row, n, (u32)delta, w.lsplit.p, maxgrid, s);
         w.lsplit_delta = (u32)delta;
         DevBuf<u64> acc(1);
         PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
@@ -2745,14 +2736,10 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         const unsigned ltgrid = (unsigned)std::max<i64>(1, std::min<i64>(lt, (i64)ctx.cu_count * 8));
         if (w.lcb) {
             w.lcw32.alloc(std::max<u64>(light, 1));
-            if (light)
-                v2_light_csr_tiled_k<Off, u32><<<ltgrid, 256, 0, s>>>(row, w.lrow.p, w.cw.p, R.col.p, R.w.p, light,
-                                                                       ltrow.p, w.lcw32.p, w.lcb);
+            if (light) light_csr_tiled<Off, u32>(R, row, w, light, ltrow.p, w.lcw32.p, w.lcb, ltgrid, s);
         } else {
             w.lcw.alloc(std::max<u64>(light, 1));
-            if (light)
-                v2_light_csr_tiled_k<Off, u64><<<ltgrid, 256, 0, s>>>(row, w.lrow.p, w.cw.p, R.col.p, R.w.p, light,
-                                                                       ltrow.p, w.lcw.p, 0u);
+            if (light) light_csr_tiled<Off, u64>(R, row, w, light, ltrow.p, w.lcw.p, 0u, ltgrid, s);
         }
         PJ_LAUNCH_CHECK();
         PJ_HIP(hipStreamSynchronize(s));  // (ltrow is freed on return)
@@ -2825,6 +2812,7 @@ void delta_run(Graph& g, DeltaWork& w, i64 source) {
     const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
 
     const int32_t delta = prepare_delta<Off>(g, w);
+    ensure_w32(g);
 
     SelArgs a{};
     a.n = n;
@@ -3053,7 +3041,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
     a.lcw32 = w.lcb ? w.lcw32.p : nullptr;
     a.lcb = w.lcb;
     a.col = R.col.p;
-    a.w8 = (g.split_w && w.w8.p) ? w.w8.p : nullptr;
+    a.w8 = g.split_w ? R.w8.p : nullptr;
     a.hl = g.light_filter ? w.hl.p : nullptr;
     a.dense_pull = g.dense_pull;
     // light rounds whose frontier holds more than dense_frac x n vertices run tile-dense
@@ -3304,9 +3292,7 @@ void delta2_run(Graph& g, DeltaWork& w, i64 source) {
             if (enter_tail) {
                 if (w.lsplit2_delta != (u32)tdelta) {
                     w.lsplit2.ensure((size_t)n);
-                    light_split_k<Off><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, (u32)tdelta,
-                                                                                 w.lsplit2.p);
-                    PJ_LAUNCH_CHECK();
+                    launch_light_split<Off>(R, row, n, (u32)tdelta, w.lsplit2.p, maxgrid, s);
                     w.lsplit2_delta = (u32)tdelta;
                 }
                 w.sb.ensure((size_t)nwords);

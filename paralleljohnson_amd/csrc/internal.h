@@ -155,7 +155,9 @@ struct Relabeled {
     DevBuf<u32> perm, inv;    // new -> old, old -> new
     DevBuf<u32> row32;
     DevBuf<u64> row64;
-    DevBuf<u32> col, w;
+    DevBuf<u32> col;
+    DevBuf<uint8_t> w8;       // weights as u8 when every weight fits (the copy's form), else
+    DevBuf<u32> w;            // u32 (also widened from w8 on demand: v1, interleaved records)
     DevBuf<int32_t> dist;     // solver distances in new ids
     const void* row_ptr(bool off64) const { return off64 ? (const void*)row64.p : (const void*)row32.p; }
 };
@@ -256,6 +258,9 @@ struct Graph {
 // used as sort scratch). n must already be known.
 // Builds g.rl from g's CSR (weighted graphs).
 void build_relabeled(Graph& g);
+// Loads delta.hip's code object on this host thread (HIP loads a module on the first use
+// of one of its kernels, ~2.5 ms for delta.hip), so the relabel can do it behind its copy.
+void preload_delta_module();
 
 // Device check of CSR arrays read from a file: row[0] == 0, non-decreasing, row[n] ==
 // nnz, every col < n; PJ_ERR_PARSE otherwise (a corrupted cache must not fault a kernel).

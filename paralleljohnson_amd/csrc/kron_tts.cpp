@@ -7,11 +7,14 @@
 // includes the solver's preparation) -> D2H -> pj_write_sol.
 //
 //   pj_kron_tts scale edgefactor seed weighted source sol_file
-// stdout: one line "phases_s <create> <build> <solve+d2h> <write>" (the parent
-// times the whole process itself).
+// source "sample:<seed>": the first root pj_sample_roots(seed) picks on the built graph
+// (the bench's first root), chosen inside the timed process.
+// stdout: one line "phases_s <create> <build> <solve+d2h> <write> root <source>" (the
+// parent times the whole process itself).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../../include/pj.h"
@@ -42,11 +45,19 @@ int main(int argc, char** argv) {
     int64_t n = 0;
     pj_graph_info(g, &n, nullptr, nullptr, nullptr);
     std::vector<int32_t> dist((size_t)n);
-    if (pj_sssp(g, std::atoll(argv[5]), dist.data()) != PJ_OK) return fail("pj_sssp");
+    int64_t source = 0;
+    if (std::strncmp(argv[5], "sample:", 7) == 0) {
+        int found = 0;
+        if (pj_sample_roots(g, std::strtoull(argv[5] + 7, nullptr, 10), 1, &source, &found) != PJ_OK || found != 1)
+            return fail("pj_sample_roots");
+    } else {
+        source = std::atoll(argv[5]);
+    }
+    if (pj_sssp(g, source, dist.data()) != PJ_OK) return fail("pj_sssp");
     const double t3 = now_s();
     if (pj_write_sol(dist.data(), n, argv[6], 1) != PJ_OK) return fail("pj_write_sol");
     const double t4 = now_s();
-    std::printf("phases_s %.4f %.4f %.4f %.4f\n", t1 - t0, t2 - t1, t3 - t2, t4 - t3);
+    std::printf("phases_s %.4f %.4f %.4f %.4f root %lld\n", t1 - t0, t2 - t1, t3 - t2, t4 - t3, (long long)source);
     pj_graph_destroy(g);
     pj_destroy(ctx);
     return 0;

@@ -64,32 +64,6 @@ __global__ void narrow_k(const u64* __restrict__ in, i64 n, u32* __restrict__ ou
         out[i] = (u32)in[i];
 }
 
-// one wave per new row: copy the old row in order, targets renamed
-template <typename Off>
-__global__ __launch_bounds__(256) void copy_rows_k(const u32* __restrict__ perm, const u32* __restrict__ inv,
-                                                   const Off* __restrict__ orow, const u32* __restrict__ ocol,
-                                                   const u32* __restrict__ ow, const Off* __restrict__ nrow,
-                                                   u32* __restrict__ ncol, u32* __restrict__ nw, i64 nrows) {
-    // (bound by the random id lookups inv[ocol[k]]: a lane-per-row and an
-    // edge-parallel form over 64 rows per wave measured no faster, 50-56 ms at s26)
-    const i64 nwaves = (i64)gridDim.x * (blockDim.x / WAVE);
-    for (i64 i = (i64)blockIdx.x * (blockDim.x / WAVE) + wave_id(); i < nrows; i += nwaves) {
-        const u32 o = perm[i];
-        const Off b = orow[o], d = orow[o + 1] - b, nb = nrow[i];
-        for (Off k = (Off)lane_id(); k < d; k += WAVE) {
-            ncol[nb + k] = inv[ocol[b + k]];
-            nw[nb + k] = ow[b + k];
-        }
-    }
-}
-
-#ifndef PJ_RL_COPY
-#define PJ_RL_COPY 1  // 0: one wave per new row; 1: edge tiles (below)
-#endif
-#ifndef PJ_RL_PASSES
-#define PJ_RL_PASSES 1  // target-id range passes of the tile copy
-#endif
-
 constexpr int CT = 256;          // threads of a tile block
 constexpr int CE = 8;            // edges per thread
 constexpr int CTILE = CT * CE;   // new-CSR entries per tile
@@ -112,17 +86,24 @@ __global__ void tile_rows_k(const Off* __restrict__ nrow, i64 n, i64 nnz, u32* _
 // the new and old row starts of the rows they belong to in LDS, and every thread
 // copies CE entries (stride CT: coalesced stores), each found by a binary search
 // over the staged starts. All CE loads of a thread are independent, so the random
-// id lookups inv[ocol[k]] overlap (the wave-per-row form walks short rows with
-// mostly idle lanes, one dependent row chain per wave). A pass renames only the
-// targets in [lo, hi) (PJ_RL_PASSES > 1: each pass's slice of inv stays cached).
-template <typename Off>
+// id lookups inv[ocol[k]] overlap (a wave-per-row form walked short rows with mostly
+// idle lanes, one dependent row chain per wave: 53.7 against 43.7 ms at s26, and
+// target-range passes that keep a slice of inv cached measured 49-61 ms,
+// profiles/r03/relabel_copy_variants.txt). The weights are written as WT (u8 when
+// every weight fits, the solver's split records) and their sum and maximum reduced on
+// the way (wacc[0], wacc[1]: the auto delta's mean weight and the u8 test), so no
+// separate pass reads the 2^31 input weights again.
+template <typename Off, typename WT>
 __global__ __launch_bounds__(CT) void copy_tiles_k(const u32* __restrict__ perm, const u32* __restrict__ inv,
                                                    const Off* __restrict__ orow, const u32* __restrict__ ocol,
                                                    const u32* __restrict__ ow, const Off* __restrict__ nrow,
-                                                   u32* __restrict__ ncol, u32* __restrict__ nw, i64 nnz,
-                                                   const u32* __restrict__ tile_row, u32 lo, u32 hi, int first) {
+                                                   u32* __restrict__ ncol, WT* __restrict__ nw, i64 nnz,
+                                                   const u32* __restrict__ tile_row, u64* __restrict__ wacc) {
     __shared__ Off s_nb[CROWS], s_ob[CROWS];
+    __shared__ u64 red[CT / WAVE];
     const i64 ntiles = (nnz + CTILE - 1) / CTILE;
+    u64 wsum = 0;
+    u32 wmax = 0;
     for (i64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const i64 e0 = t * CTILE, e1 = min(e0 + CTILE, nnz);
         const u32 r0 = tile_row[t], r1 = tile_row[t + 1];
@@ -156,16 +137,27 @@ __global__ __launch_bounds__(CT) void copy_tiles_k(const u32* __restrict__ perm,
         for (int m = 0; m < CE; ++m)
             if (src[m] >= 0) {
                 c[m] = ocol[src[m]];
-                if (first) wv[m] = ow[src[m]];
+                wv[m] = ow[src[m]];
             }
 #pragma unroll
         for (int m = 0; m < CE; ++m)
             if (src[m] >= 0) {
                 const i64 k = e0 + threadIdx.x + m * CT;
-                if (c[m] >= lo && c[m] < hi) ncol[k] = inv[c[m]];
-                if (first) nw[k] = wv[m];
+                ncol[k] = inv[c[m]];
+                nw[k] = (WT)wv[m];
+                wsum += wv[m];
+                wmax = max(wmax, wv[m]);
             }
         __syncthreads();
+    }
+    wsum = block_sum<CT / WAVE>(wsum, red);
+    wmax = wave_max(wmax);
+    if (lane_id() == 0) red[wave_id()] = wmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < CT / WAVE; ++k) wmax = max(wmax, (u32)red[k]);
+        if (wsum) atomicAdd(&wacc[0], wsum);
+        if (wmax) atomicMax(&wacc[1], (u64)wmax);
     }
 }
 
@@ -176,68 +168,94 @@ void build(Graph& g) {
     const Off* orow = static_cast<const Off*>(g.row_ptr());
     std::unique_ptr<Relabeled> R(new Relabeled());
     const unsigned grid = (unsigned)g.ctx->cu_count * 16u;
-    DevBuf<u32> deg((size_t)n + 1), key((size_t)n + 1), kalt((size_t)n + 1), ids((size_t)n + 1),
-        ialt((size_t)n + 1);
-    DevBuf<uint8_t> touched((size_t)n + 1);
-    DevBuf<u32> scal(2);
-    PJ_HIP(hipMemsetAsync(touched.p, 0, (size_t)n + 1, s));
-    PJ_HIP(hipMemsetAsync(scal.p, 0, 2 * sizeof(u32), s));
-    degree_k<Off><<<grid_for(n, 256, grid), 256, 0, s>>>(orow, n, deg.p);
+    // the temporaries in ONE allocation: a hipFree costs ~0.19 ms of host time at s26
+    // (it waits for the device), and there were twelve of them behind the copy
+    const i64 ntiles = (nnz + CTILE - 1) / CTILE;
+    const size_t nb = ((size_t)n + 1) * sizeof(u32), al = 256;
+    auto up = [&](size_t b) { return (b + al - 1) / al * al; };
+    const size_t sz_off = sizeof(Off) == 8 ? 0 : up(((size_t)n + 1) * sizeof(u64));
+    DevBuf<uint8_t> arena(5 * up(nb) + up((size_t)n + 1) + up(4 * sizeof(u64)) + sz_off +
+                          up(((size_t)ntiles + 1) * sizeof(u32)));
+    uint8_t* cur = arena.p;
+    auto carve = [&](size_t b) {
+        uint8_t* q = cur;
+        cur += up(b);
+        return q;
+    };
+    u32* deg = reinterpret_cast<u32*>(carve(nb));
+    u32* key = reinterpret_cast<u32*>(carve(nb));
+    u32* kalt = reinterpret_cast<u32*>(carve(nb));
+    u32* ids = reinterpret_cast<u32*>(carve(nb));
+    u32* ialt = reinterpret_cast<u32*>(carve(nb));
+    uint8_t* touched = carve((size_t)n + 1);
+    u64* scal64 = reinterpret_cast<u64*>(carve(4 * sizeof(u64)));  // [0] max degree, [1] n_scan (u32), [2..3] wacc
+    u32* scal = reinterpret_cast<u32*>(scal64);
+    u64* wacc = scal64 + 2;
+    PJ_HIP(hipMemsetAsync(touched, 0, (size_t)n + 1, s));
+    PJ_HIP(hipMemsetAsync(scal64, 0, 4 * sizeof(u64), s));
+    degree_k<Off><<<grid_for(n, 256, grid), 256, 0, s>>>(orow, n, deg);
     // vertices that are only targets also get an id below n_scan; a symmetric graph has
     // none (every target has the reverse edge), so the random byte stores are skipped
-    if (nnz && !g.symmetric) mark_targets_k<<<grid_for(nnz, 256, grid), 256, 0, s>>>(g.col.p, nnz, touched.p);
-    max_u32_k<<<grid_for(n, 256, grid), 256, 0, s>>>(deg.p, n, scal.p);
+    if (nnz && !g.symmetric) mark_targets_k<<<grid_for(nnz, 256, grid), 256, 0, s>>>(g.col.p, nnz, touched);
+    max_u32_k<<<grid_for(n, 256, grid), 256, 0, s>>>(deg, n, scal);
     PJ_LAUNCH_CHECK();
     u32 h[2] = {0, 0};
-    PJ_HIP(hipMemcpyAsync(h, scal.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipMemcpyAsync(h, scal, sizeof(u32), hipMemcpyDeviceToHost, s));
     PJ_HIP(hipStreamSynchronize(s));
     const u32 maxdeg = h[0];
-    order_key_k<<<grid_for(n, 256, grid), 256, 0, s>>>(deg.p, touched.p, n, maxdeg, key.p, ids.p, scal.p + 1);
+    order_key_k<<<grid_for(n, 256, grid), 256, 0, s>>>(deg, touched, n, maxdeg, key, ids, scal + 1);
     PJ_LAUNCH_CHECK();
-    PJ_HIP(hipMemcpyAsync(h + 1, scal.p + 1, sizeof(u32), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipMemcpyAsync(h + 1, scal + 1, sizeof(u32), hipMemcpyDeviceToHost, s));
     int bits = 0;
     while (bits < 32 && ((u64)1 << bits) < (u64)maxdeg + 2) ++bits;
     SortWs ws;
     u32 *kr, *pr;
-    radix_sort_pairs<u32>(key.p, kalt.p, ids.p, ialt.p, n, bits, ws, s, &kr, &pr);
+    radix_sort_pairs<u32>(key, kalt, ids, ialt, n, bits, ws, s, &kr, &pr);
     R->perm.alloc((size_t)n);
     R->inv.alloc((size_t)n);
     PJ_HIP(hipMemcpyAsync(R->perm.p, pr, sizeof(u32) * (size_t)n, hipMemcpyDeviceToDevice, s));
-    u32* ndeg = kr == key.p ? kalt.p : key.p;  // free buffer
-    invert_k<<<grid_for(n, 256, grid), 256, 0, s>>>(R->perm.p, n, R->inv.p, deg.p, ndeg);
+    u32* ndeg = kr == key ? kalt : key;  // free buffer
+    invert_k<<<grid_for(n, 256, grid), 256, 0, s>>>(R->perm.p, n, R->inv.p, deg, ndeg);
     PJ_LAUNCH_CHECK();
-    DevBuf<u64> off((size_t)n + 1);
-    exclusive_scan_u32(ndeg, off.p, n, g.scan, s);
     Off* nrow;
-    if (sizeof(Off) == 8) {
-        R->row64 = std::move(off);
+    if (sizeof(Off) == 8) {  // the scan writes the 64-bit row offsets in place
+        R->row64.alloc((size_t)n + 1);
+        exclusive_scan_u32(ndeg, R->row64.p, n, g.scan, s);
         nrow = reinterpret_cast<Off*>(R->row64.p);
     } else {
+        u64* off = reinterpret_cast<u64*>(carve(((size_t)n + 1) * sizeof(u64)));
+        exclusive_scan_u32(ndeg, off, n, g.scan, s);
         R->row32.alloc((size_t)n + 1);
-        narrow_k<<<grid_for(n + 1, 256, grid), 256, 0, s>>>(off.p, n + 1, R->row32.p);
+        narrow_k<<<grid_for(n + 1, 256, grid), 256, 0, s>>>(off, n + 1, R->row32.p);
         PJ_LAUNCH_CHECK();
         nrow = reinterpret_cast<Off*>(R->row32.p);
     }
     R->col.alloc((size_t)(nnz ? nnz : 1));
-    R->w.alloc((size_t)(nnz ? nnz : 1));
-    if (nnz && PJ_RL_COPY == 0) {
-        copy_rows_k<Off><<<grid, 256, 0, s>>>(R->perm.p, R->inv.p, orow, g.col.p, g.w.p, nrow, R->col.p, R->w.p,
-                                              n);
-    } else if (nnz) {
-        const i64 ntiles = (nnz + CTILE - 1) / CTILE;
-        DevBuf<u32> trow((size_t)ntiles + 1);
-        tile_rows_k<Off><<<grid_for(n, 256, grid), 256, 0, s>>>(nrow, n, nnz, trow.p);
+    R->w8.alloc((size_t)(nnz ? nnz : 1));
+    if (nnz) {
+        u32* trow = reinterpret_cast<u32*>(carve(((size_t)ntiles + 1) * sizeof(u32)));
+        tile_rows_k<Off><<<grid_for(n, 256, grid), 256, 0, s>>>(nrow, n, nnz, trow);
         PJ_LAUNCH_CHECK();
         const unsigned tgrid = (unsigned)std::min<i64>(ntiles, (i64)g.ctx->cu_count * 8);
-        const u64 span = ((u64)n + PJ_RL_PASSES - 1) / PJ_RL_PASSES;
-        for (int p = 0; p < PJ_RL_PASSES; ++p) {
-            const u64 lo = span * (u64)p, hi = std::min<u64>((u64)n, lo + span);
-            copy_tiles_k<Off><<<tgrid, CT, 0, s>>>(R->perm.p, R->inv.p, orow, g.col.p, g.w.p, nrow, R->col.p,
-                                                   R->w.p, nnz, trow.p, (u32)lo,
-                                                   p + 1 == PJ_RL_PASSES ? 0xFFFFFFFFu : (u32)hi, p == 0);
+        copy_tiles_k<Off, uint8_t><<<tgrid, CT, 0, s>>>(R->perm.p, R->inv.p, orow, g.col.p, g.w.p, nrow, R->col.p,
+                                                       R->w8.p, nnz, trow, wacc);
+        PJ_LAUNCH_CHECK();
+        preload_delta_module();  // host work hidden behind the copy
+        u64 hw[2] = {0, 0};
+        PJ_HIP(hipMemcpyAsync(hw, wacc, sizeof(hw), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+        if (hw[1] > 255) {  // wide weights: the copy again with u32 weights (ids rewritten unchanged)
+            R->w8.release();
+            R->w.alloc((size_t)nnz);
+            PJ_HIP(hipMemsetAsync(wacc, 0, 2 * sizeof(u64), s));
+            copy_tiles_k<Off, u32><<<tgrid, CT, 0, s>>>(R->perm.p, R->inv.p, orow, g.col.p, g.w.p, nrow, R->col.p,
+                                                       R->w.p, nnz, trow, wacc);
             PJ_LAUNCH_CHECK();
         }
-        PJ_HIP(hipStreamSynchronize(s));  // trow is freed on return
+        if (g.mean_weight < 0.0) {
+            g.mean_weight = (double)hw[0] / (double)nnz;
+            g.max_weight = (long long)hw[1];
+        }
     }
     PJ_LAUNCH_CHECK();
     R->dist.alloc((size_t)n);
