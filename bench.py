@@ -367,6 +367,7 @@ def main():
                     help="watchdog of the partitioned leg (s): past it the line is emitted without that leg")
     ap.add_argument("--ms-reps", type=int, default=7, help="timed MS1024 batches (median reported)")
     ap.add_argument("--no-part-host", action="store_true", help="skip the world-2 host-transport partitioned leg")
+    ap.add_argument("--no-tts", action="store_true", help="skip the time-to-solution process (tuning runs)")
     ap.add_argument("--opt", action="append", default=[], help="libpj graph option key=value (tuning)")
     args = ap.parse_args()
 
@@ -401,7 +402,7 @@ def main():
     ctx_s = time.perf_counter() - t_ctx
     tts_dir = tempfile.TemporaryDirectory()
     tts = None
-    if rank == 0 and WORKLOADS[args.workload]["kind"] == "kronecker":
+    if rank == 0 and WORKLOADS[args.workload]["kind"] == "kronecker" and not args.no_tts:
         tts = tts_process(args, WORKLOADS[args.workload], tts_dir.name)
         # the driver reclaims the tool's ~40 GB of device memory after it exits; allocations
         # made right then wait for it (seen as 1-3 s of "graph build" in whichever process
