@@ -507,6 +507,8 @@ __global__ void d_source_k(i64 s, int32_t* __restrict__ dist) { dist[s] = 0; }
 // distances back to input ids: out[v] = dist'[inv[v]] (INT_INF past n_scan)
 __global__ void unlabel_k(const u32* __restrict__ inv, const int32_t* __restrict__ dl, i64 n, i64 n_scan,
                           int32_t* __restrict__ out) {
+    // (bound by the gathered distance lines: 8 ids per thread step measured 192.5 against
+    // 200.6 us at s26, profiles/r03/experiments_r3ab_select.txt)
     for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
         const u32 x = inv[v];
         out[v] = (i64)x < n_scan ? dl[x] : INT_INF;
@@ -1513,25 +1515,44 @@ __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout,
 }
 
 // Next band [lo, hi): fout words = members, count into slot cout, min dist >= lo.
+// A wave takes V2_SELW consecutive words per step with their distance loads issued
+// together (one 256-byte load per step and wave left each wave one load in flight:
+// 42.5 us for the 134 MB of s26 distances; 28 us with 4, profiles/r03/experiments_r3ab_select.txt).
+#ifndef PJ_V2_SELW
+#define PJ_V2_SELW 4
+#endif
+constexpr int V2_SELW = PJ_V2_SELW;
 __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fout, int cout) {
     __shared__ u64 red[DB / WAVE];
     const int lane = lane_id();
     u32 c = 0;
     u64 fe = 0;
     int32_t mn = INT_INF;
-    for (i64 wi = (i64)blockIdx.x * (DB / WAVE) + wave_id(); wi < a.nwords; wi += (i64)gridDim.x * (DB / WAVE)) {
-        const i64 v = wi * 64 + lane;
-        const int32_t d = v < a.n ? a.dist[v] : INT_INF;
-        const bool mem = d >= a.lo && d < a.hi;
-        const u64 m = __ballot(mem);
-        if (a.swrite) {
-            const u64 sm = __ballot(v < a.n && d < a.lo);
-            if (lane == 0) a.swrite[wi] = sm;
+    for (i64 w0 = ((i64)blockIdx.x * (DB / WAVE) + wave_id()) * V2_SELW; w0 < a.nwords;
+         w0 += (i64)gridDim.x * (DB / WAVE) * V2_SELW) {
+        int32_t dd[V2_SELW];
+#pragma unroll
+        for (int j = 0; j < V2_SELW; ++j) {
+            const i64 v = (w0 + j) * 64 + lane;
+            dd[j] = v < a.n ? a.dist[v] : INT_INF;
         }
-        if (d >= a.lo && d < mn) mn = d;
-        if (mem) fe += (a.fesplit ? a.fesplit : a.lsplit)[v];
-        if (lane == 0) fout[wi] = m;
-        c += lane == 0 ? (u32)__popcll(m) : 0u;
+#pragma unroll
+        for (int j = 0; j < V2_SELW; ++j) {
+            const i64 wi = w0 + j;
+            if (wi >= a.nwords) break;
+            const i64 v = wi * 64 + lane;
+            const int32_t d = dd[j];
+            const bool mem = d >= a.lo && d < a.hi;
+            const u64 m = __ballot(mem);
+            if (a.swrite) {
+                const u64 sm = __ballot(v < a.n && d < a.lo);
+                if (lane == 0) a.swrite[wi] = sm;
+            }
+            if (d >= a.lo && d < mn) mn = d;
+            if (mem) fe += (a.fesplit ? a.fesplit : a.lsplit)[v];
+            if (lane == 0) fout[wi] = m;
+            c += lane == 0 ? (u32)__popcll(m) : 0u;
+        }
     }
     v2_flush2(c, fe, a.ctl->cnt[cout], red);
     v2_flush_min(mn, a.ctl, red);
