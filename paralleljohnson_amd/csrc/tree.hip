@@ -122,7 +122,8 @@ __global__ __launch_bounds__(256) void tree_edges_k(const Off* __restrict__ row,
         bad += (i64)dv > (via < INT_INF ? via : (i64)INT_INF);
         if (dv < INT_INF && via == (i64)dv && par[v] == u) atomicOr(&ok[v >> 5], 1u << (v & 31));
     });
-    if (bad) atomicAdd(&c->bad_edge, bad);
+    bad = wave_sum(bad);  // (one atomic per wave: a per-thread add on one word serializes)
+    if (lane_id() == 0 && bad) atomicAdd(&c->bad_edge, bad);
 }
 
 __global__ void tree_vertices_k(const int32_t* __restrict__ dist, i64 n, i64 source, const int64_t* __restrict__ par,
@@ -148,10 +149,16 @@ __global__ void tree_vertices_k(const int32_t* __restrict__ dist, i64 n, i64 sou
         }
         anc[v] = a;
     }
-    if (reached) atomicAdd(&c->reached, reached);
-    if (root) atomicAdd(&c->bad_root, root);
-    if (reach) atomicAdd(&c->bad_reach, reach);
-    if (tree) atomicAdd(&c->bad_tree, tree);
+    reached = wave_sum(reached);
+    root = wave_sum(root);
+    reach = wave_sum(reach);
+    tree = wave_sum(tree);
+    if (lane_id() == 0) {
+        if (reached) atomicAdd(&c->reached, reached);
+        if (root) atomicAdd(&c->bad_root, root);
+        if (reach) atomicAdd(&c->bad_reach, reach);
+        if (tree) atomicAdd(&c->bad_tree, tree);
+    }
 }
 
 // one pointer-jumping round: anc[v] = anc[anc[v]] (in place: any ancestor stays an ancestor)
@@ -167,7 +174,8 @@ __global__ void cycle_k(const int32_t* __restrict__ dist, const int64_t* __restr
     u64 bad = 0;
     for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x)
         bad += dist[v] < INT_INF && v != source && anc[v] != source;
-    if (bad) atomicAdd(&c->bad_cycle, bad);
+    bad = wave_sum(bad);
+    if (lane_id() == 0 && bad) atomicAdd(&c->bad_cycle, bad);
 }
 
 unsigned grid_of(const Graph& g, i64 work) { return grid_for(work, 256, (unsigned)g.ctx->cu_count * 8u); }

@@ -83,21 +83,31 @@ struct WArgs {
     u64* stat;
 };
 
-__device__ __forceinline__ void wp_edge(const WArgs& a, bool light, u32 t, long long nd) {
-    if (nd >= INT_INF) return;
+// one relaxation; returns 1 when it adds t to the next frontier (the callers count
+// these per thread and add the block's sum to ST_NF once: an atomicAdd per marked
+// vertex on that one word serialized the light rounds behind its atomic rate)
+__device__ __forceinline__ u32 wp_edge(const WArgs& a, bool light, u32 t, long long nd) {
+    if (nd >= INT_INF) return 0u;
     const i64 tl = (i64)t - a.lo;
     if (tl >= 0 && tl < a.nl) {
         if ((int32_t)nd < wp_now(a.dist + tl)) {
             atomicMin(a.dist + tl, (int32_t)nd);
             if (light && (int32_t)nd < a.dhi) {
                 const u64 bit = 1ull << (tl & 63);
-                if (!(atomicOr(a.frn + (tl >> 6), bit) & bit)) atomicAdd(&a.stat[ST_NF], 1ull);
+                if (!(atomicOr(a.frn + (tl >> 6), bit) & bit)) return 1u;
             }
         }
     } else if ((int32_t)nd < wp_now(a.cand + t)) {
         atomicMin(a.cand + t, (int32_t)nd);
         atomicOr(a.touched + (t >> 6), 1ull << (t & 63));
     }
+    return 0u;
+}
+
+// the block's newly marked frontier vertices into ST_NF (one atomic per block)
+__device__ __forceinline__ void wp_flush_nf(const WArgs& a, u32 nf, u64* red) {
+    const u64 t = block_sum<WB / WAVE>((u64)nf, red);
+    if (threadIdx.x == 0 && t) atomicAdd(&a.stat[ST_NF], t);
 }
 
 __global__ void wp_seed_k(WArgs a, i64 s) {
@@ -130,14 +140,23 @@ __global__ __launch_bounds__(WB) void wp_select_k(WArgs a) {
         const int32_t y = __shfl_xor(mn, off, 64);
         mn = y < mn ? y : mn;
     }
-    if (lane == 0 && mn < INT_INF) atomicMin(&a.stat[ST_MIN], (u64)mn);
+    // one atomicMin per block, not per wave
+    if (lane == 0) red[wave_id()] = (u64)(u32)mn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t m = INT_INF;
+        for (int k = 0; k < WB / WAVE; ++k) m = min(m, (int32_t)(u32)red[k]);
+        if (m < INT_INF) atomicMin(&a.stat[ST_MIN], (u64)m);
+    }
 }
 
 // LIGHT: the frontier fr relaxes its light prefixes (fr words are cleared as
 // read, members join mb); HEAVY: mb relaxes its heavy suffixes.
 template <bool LIGHT>
 __global__ __launch_bounds__(WB) void wp_relax_k(WArgs a) {
+    __shared__ u64 red[WB / WAVE];
     const int lane = lane_id();
+    u32 nf = 0;
     const i64 nsc = (a.bw + WSC - 1) / WSC;
     for (i64 sc = (i64)blockIdx.x * (WB / WAVE) + wave_id(); sc < nsc; sc += (i64)gridDim.x * (WB / WAVE)) {
         const i64 wbase = sc * WSC;
@@ -201,7 +220,7 @@ __global__ __launch_bounds__(WB) void wp_relax_k(WArgs a) {
             }
             u64 k = b;
             const u64 lim = (e - b > (u64)WP_SERIAL) ? b + WP_SERIAL : e;
-            for (; k < lim; ++k) wp_edge(a, LIGHT, a.col[k], (long long)du + a.w[k]);
+            for (; k < lim; ++k) nf += wp_edge(a, LIGHT, a.col[k], (long long)du + a.w[k]);
             // the rest, edge-balanced over the wave
             if (__ballot(k < e)) {
                 const u64 rem = k < e ? e - k : 0;
@@ -218,12 +237,13 @@ __global__ __launch_bounds__(WB) void wp_relax_k(WArgs a) {
                     const int32_t dl = __shfl(du, l, 64);
                     if (gi < tot) {
                         const u64 kk = kl + (gi - xl);
-                        wp_edge(a, LIGHT, a.col[kk], (long long)dl + a.w[kk]);
+                        nf += wp_edge(a, LIGHT, a.col[kk], (long long)dl + a.w[kk]);
                     }
                 }
             }
         }
     }
+    if (LIGHT) wp_flush_nf(a, nf, red);
 }
 
 // the long segments queued by wp_relax_k, edge-balanced: 1024-edge tiles over
@@ -233,6 +253,8 @@ __global__ __launch_bounds__(WB) void wp_long_k(WArgs a) {
     __shared__ LbShared<WP_TILE> sh;
     __shared__ int32_t s_du[WP_TILE];
     __shared__ u64 s_b[WP_TILE];
+    __shared__ u64 red[WB / WAVE];
+    u32 nf = 0;
     const u64 packed = a.stat[ST_LONGQ];
     const u64 nq = packed >> WP_EB, total = packed & ((1ull << WP_EB) - 1ull);
     if (nq == 0) return;
@@ -251,11 +273,12 @@ __global__ __launch_bounds__(WB) void wp_long_k(WArgs a) {
             if (e < total) {
                 const u32 sl = lb_find<WP_TILE>(sh, ns, e);
                 const u64 k = s_b[sl] + (e - sh.off[sl]);
-                wp_edge(a, LIGHT, a.col[k], (long long)s_du[sl] + a.w[k]);
+                nf += wp_edge(a, LIGHT, a.col[k], (long long)s_du[sl] + a.w[k]);
             }
         }
         __syncthreads();
     }
+    if (LIGHT) wp_flush_nf(a, nf, red);
 }
 
 // Touched remote targets -> (id | cand << 32) in the owner's region of `reg`
@@ -302,10 +325,13 @@ __global__ __launch_bounds__(WB) void wp_pack_k(WArgs a, i64 nwords, u64* __rest
 
 // received (id | cand << 32) for this rank
 __global__ __launch_bounds__(WB) void wp_apply_k(WArgs a, const u64* __restrict__ recv, i64 nr, int light) {
+    __shared__ u64 red[WB / WAVE];
+    u32 nf = 0;
     for (i64 i = (i64)blockIdx.x * WB + threadIdx.x; i < nr; i += (i64)gridDim.x * WB) {
         const u64 x = recv[i];
-        wp_edge(a, light != 0, (u32)x, (long long)(int32_t)(u32)(x >> 32));
+        nf += wp_edge(a, light != 0, (u32)x, (long long)(int32_t)(u32)(x >> 32));
     }
+    if (light) wp_flush_nf(a, nf, red);
 }
 
 // fr := frn, frn := 0 (the round's new frontier becomes current)

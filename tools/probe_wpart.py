@@ -1,6 +1,7 @@
 """Weighted partitioned solve (wpart.hip + engine.cpp) on Kronecker s{scale} weights 1..255 at
 world 1 (no transport) and world 2 (both ranks on this GPU, host transport): per-solve time
-with the tail switch, the heavy pull and the light pull rounds at their defaults and off. Usage: python tools/probe_wpart.py [scale=26]"""
+with the tail switch, the heavy pull and the light pull rounds at their defaults and off, or under the
+given (tail_frac, pull_factor, light_pull) sets. Usage: python tools/probe_wpart.py [scale=26] ["tf,pf,lp;tf,pf,lp..."]"""
 import os, sys, time
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
 import numpy as np
@@ -18,7 +19,10 @@ for world in (1, 2):
             roots = [int(x) for x in g.sample_roots(2, 3)]
         parts.append(load_weighted(ctxs[r], g, r, world))
         g.close()
-    for tf, pf, lp in ((0.1, 4, 3), (0.1, 4, 0), (0.1, 0, 0), (0.1, 4, 3), (0.1, 4, 0), (0.1, 0, 0)):
+    sets = ((0.1, 4, 3), (0.1, 4, 0), (0.1, 0, 0), (0.1, 4, 3), (0.1, 4, 0), (0.1, 0, 0))
+    if len(sys.argv) > 2:
+        sets = [tuple(float(x) for x in t.split(",")) for t in sys.argv[2].split(";")]
+    for tf, pf, lp in sets:
         for p in parts:
             p.set_option("tail_frac", tf)
             p.set_option("pull_factor", pf)
