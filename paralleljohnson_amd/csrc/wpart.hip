@@ -598,8 +598,10 @@ struct WPart {
     int32_t delta = 0;
     double tail[2] = {0.1, 64.0};  // tail switch (engine.h DeltaSteps): tail_frac (0 = off), threshold / delta
     double pull_factor = 4.0;      // heavy pull when unsettled heavy edges < pull_factor x members' (0 = push)
-    double light_pull = 3.0;       // light pull round when the frontier's light edges > the light edges
-                                   // of the vertices above lo / light_pull (0 = push)
+    double light_pull = 0.0;       // light pull round when the frontier's light edges > the light edges
+                                   // of the vertices above lo / light_pull (0 = push; 3 was the default
+                                   // until the push rounds counted their frontier per workgroup: then
+                                   // 0 measured best at s24w / s26w, world 1 and 2, r3ad)
     bool symmetric = false;        // rows are also the in-edges (Kronecker graphs): the heavy pull applies
     DevBuf<uint8_t> mmap;          // replicated member map of the heavy pull (world x block bytes)
     DevBuf<u64> row;
