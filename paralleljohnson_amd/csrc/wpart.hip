@@ -104,6 +104,50 @@ __device__ __forceinline__ u32 wp_edge(const WArgs& a, bool light, u32 t, long l
     return 0u;
 }
 
+// WP_PU edges of one source in one step: the target reads of all of them issued before
+// any atomic (wp_edge one by one is a dependent chain of read, atomicMin and atomicOr per
+// edge); same rule as wp_edge, returns the number of newly marked frontier vertices
+#ifndef PJ_WP_PU
+#define PJ_WP_PU 2
+#endif
+constexpr int WP_PU = PJ_WP_PU;
+__device__ __forceinline__ u32 wp_edges(const WArgs& a, bool light, u64 k, u64 lim, int32_t du) {
+    u32 t[WP_PU];
+    long long nd[WP_PU];
+    bool ok[WP_PU], loc[WP_PU];
+    int32_t cur[WP_PU];
+#pragma unroll
+    for (int j = 0; j < WP_PU; ++j) {
+        ok[j] = k + j < lim;
+        t[j] = ok[j] ? a.col[k + j] : 0u;
+        nd[j] = (long long)du + (ok[j] ? a.w[k + j] : 0u);
+        ok[j] = ok[j] && nd[j] < INT_INF;
+    }
+#pragma unroll
+    for (int j = 0; j < WP_PU; ++j) {
+        const i64 tl = (i64)t[j] - a.lo;
+        loc[j] = tl >= 0 && tl < a.nl;
+        cur[j] = !ok[j] ? 0 : (loc[j] ? wp_now(a.dist + tl) : wp_now(a.cand + t[j]));
+    }
+    u32 nf = 0;
+#pragma unroll
+    for (int j = 0; j < WP_PU; ++j) {
+        if (!ok[j] || (int32_t)nd[j] >= cur[j]) continue;
+        if (loc[j]) {
+            const i64 tl = (i64)t[j] - a.lo;
+            atomicMin(a.dist + tl, (int32_t)nd[j]);
+            if (light && (int32_t)nd[j] < a.dhi) {
+                const u64 bit = 1ull << (tl & 63);
+                if (!(atomicOr(a.frn + (tl >> 6), bit) & bit)) ++nf;
+            }
+        } else {
+            atomicMin(a.cand + t[j], (int32_t)nd[j]);
+            atomicOr(a.touched + (t[j] >> 6), 1ull << (t[j] & 63));
+        }
+    }
+    return nf;
+}
+
 // the block's newly marked frontier vertices into ST_NF (one atomic per block)
 __device__ __forceinline__ void wp_flush_nf(const WArgs& a, u32 nf, u64* red) {
     const u64 t = block_sum<WB / WAVE>((u64)nf, red);
@@ -121,16 +165,29 @@ __global__ __launch_bounds__(WB) void wp_select_k(WArgs a) {
     const int lane = lane_id();
     u64 c = 0;
     int32_t mn = INT_INF;
-    for (i64 wi = (i64)blockIdx.x * (WB / WAVE) + wave_id(); wi < a.bw; wi += (i64)gridDim.x * (WB / WAVE)) {
-        const i64 v = wi * 64 + lane;
-        const int32_t d = v < a.nl ? a.dist[v] : INT_INF;
-        const u64 m = __ballot(d >= a.dlo && d < a.dhi);
-        if (d >= a.dlo && d < mn) mn = d;
-        if (lane == 0) {
-            a.fr[wi] = m;
-            a.frn[wi] = 0;
-            a.mb[wi] = 0;
-            c += (u64)__popcll(m);
+    // (4 words per wave step, loads issued together, as delta.hip's v2_select_k)
+    constexpr int SELW = 4;
+    for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * SELW; w0 < a.bw;
+         w0 += (i64)gridDim.x * (WB / WAVE) * SELW) {
+        int32_t dd[SELW];
+#pragma unroll
+        for (int j = 0; j < SELW; ++j) {
+            const i64 v = (w0 + j) * 64 + lane;
+            dd[j] = v < a.nl ? a.dist[v] : INT_INF;
+        }
+#pragma unroll
+        for (int j = 0; j < SELW; ++j) {
+            const i64 wi = w0 + j;
+            if (wi >= a.bw) break;
+            const int32_t d = dd[j];
+            const u64 m = __ballot(d >= a.dlo && d < a.dhi);
+            if (d >= a.dlo && d < mn) mn = d;
+            if (lane == 0) {
+                a.fr[wi] = m;
+                a.frn[wi] = 0;
+                a.mb[wi] = 0;
+                c += (u64)__popcll(m);
+            }
         }
     }
     c = block_sum<WB / WAVE>(c, red);
@@ -220,7 +277,8 @@ __global__ __launch_bounds__(WB) void wp_relax_k(WArgs a) {
             }
             u64 k = b;
             const u64 lim = (e - b > (u64)WP_SERIAL) ? b + WP_SERIAL : e;
-            for (; k < lim; ++k) nf += wp_edge(a, LIGHT, a.col[k], (long long)du + a.w[k]);
+            for (; k < lim; k += WP_PU) nf += wp_edges(a, LIGHT, k, lim, du);
+            k = k < lim ? k : lim;
             // the rest, edge-balanced over the wave
             if (__ballot(k < e)) {
                 const u64 rem = k < e ? e - k : 0;
@@ -596,6 +654,7 @@ struct WPart {
     int rank = 0, world = 1;
     double mean_w = 1.0;
     int32_t delta = 0;
+    int32_t delta_alt = 0;         // the light threshold lsplit_alt was computed for (0 = none)
     double tail[2] = {0.1, 64.0};  // tail switch (engine.h DeltaSteps): tail_frac (0 = off), threshold / delta
     double pull_factor = 4.0;      // heavy pull when unsettled heavy edges < pull_factor x members' (0 = push)
     double light_pull = 0.0;       // light pull round when the frontier's light edges > the light edges
@@ -606,6 +665,8 @@ struct WPart {
     DevBuf<uint8_t> mmap;          // replicated member map of the heavy pull (world x block bytes)
     DevBuf<u64> row;
     DevBuf<u32> col, w, lsplit;
+    DevBuf<u32> lsplit_alt;        // the other light threshold's prefixes (delta and the tail's are
+                                   // used in turn by every solve: each was recomputed per solve)
     DevBuf<int32_t> dist, cand;
     DevBuf<u64> touched, fr, frn, mb, reg, stat;
     DevBuf<u32> lq_v;
@@ -902,15 +963,25 @@ i64 wpart_unsettled(WPart& p, int32_t hi) {
     return (i64)h;
 }
 
-// a new light threshold at a band boundary (the tail switch): the light prefixes follow it
-void wpart_set_delta(WPart& p, int32_t delta) {
-    if (delta != p.delta && p.nl > 0) {
-        wp_lsplit_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, p.ctx->stream>>>(p.row.p, p.w.p, p.nl, (u32)delta,
-                                                                              p.lsplit.p);
-        PJ_LAUNCH_CHECK();
+// the light prefixes of light threshold delta in p.lsplit: the current buffer, the other
+// cached one (swapped in), or computed into the buffer of the older threshold
+void wpart_use_delta(WPart& p, int32_t delta) {
+    if (delta == p.delta || p.nl <= 0) {
+        p.delta = delta;
+        return;
     }
+    std::swap(p.lsplit, p.lsplit_alt);
+    std::swap(p.delta, p.delta_alt);
+    if (delta == p.delta) return;
+    if (!p.lsplit.p) p.lsplit.alloc((size_t)p.nl);
+    wp_lsplit_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, p.ctx->stream>>>(p.row.p, p.w.p, p.nl, (u32)delta,
+                                                                          p.lsplit.p);
+    PJ_LAUNCH_CHECK();
     p.delta = delta;
 }
+
+// a new light threshold at a band boundary (the tail switch): the light prefixes follow it
+void wpart_set_delta(WPart& p, int32_t delta) { wpart_use_delta(p, delta); }
 
 int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
     hipStream_t s = p.ctx->stream;
@@ -918,11 +989,7 @@ int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
         const double mean_deg = p.n ? (double)p.nnz / (double)p.n : 1.0;
         delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(3.5 * p.mean_w / std::max(1.0, mean_deg))));
     }
-    if (delta != p.delta && p.nl > 0) {
-        wp_lsplit_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, s>>>(p.row.p, p.w.p, p.nl, (u32)delta, p.lsplit.p);
-        PJ_LAUNCH_CHECK();
-    }
-    p.delta = delta;
+    wpart_use_delta(p, delta);
     if (p.nl > 0) PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.dist.p), INT_INF, (size_t)p.nl, s));
     if (p.world > 1 && p.n > 0)
         PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.cand.p), INT_INF, (size_t)p.n, s));
