@@ -448,6 +448,10 @@ __global__ void wp_member_slice_k(WArgs a, uint8_t* __restrict__ own) {
 // (any rank's, through the replicated map) and stops once lo + w >= its best value; the
 // first WP_PSERIAL edges by the lane alone, the rest of a long row by the whole wave
 constexpr int WP_PSERIAL = 16;
+#ifndef PJ_WP_HPU
+#define PJ_WP_HPU 1
+#endif
+constexpr int WP_HPU = PJ_WP_HPU;
 __global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __restrict__ mmap) {
     const int lane = lane_id();
     const int32_t lo = a.dlo, hi = a.dhi;
@@ -468,15 +472,35 @@ __global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __
         }
         const u64 lim = e - k > (u64)WP_PSERIAL ? k + WP_PSERIAL : e;
         bool done = !act || k >= e;
+        // WP_HPU edges per step: their weight, id and map loads issued together, then taken
+        // in row order with the same early stop (the probes past a stop are wasted only)
         while (act && k < lim) {
-            const u32 w = a.w[k];
-            if ((long long)lo + w >= (long long)cur) {
+            u32 w[WP_HPU], c[WP_HPU];
+            uint8_t m[WP_HPU];
+#pragma unroll
+            for (int j = 0; j < WP_HPU; ++j) {
+                const bool in = k + j < lim;
+                w[j] = in ? a.w[k + j] : 0u;
+                c[j] = in ? a.col[k + j] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < WP_HPU; ++j)
+                m[j] = (k + j < lim && (long long)lo + w[j] < (long long)cur) ? mmap[c[j]] : (uint8_t)0xFF;
+            bool stop = false;
+#pragma unroll
+            for (int j = 0; j < WP_HPU; ++j) {
+                if (stop || k >= lim) continue;
+                if ((long long)lo + w[j] >= (long long)cur) {
+                    stop = true;
+                    continue;
+                }
+                if (m[j] != 0xFF) cur = min(cur, lo + (int32_t)m[j] + (int32_t)w[j]);
+                ++k;
+            }
+            if (stop) {
                 done = true;
                 break;
             }
-            const uint8_t m = mmap[a.col[k]];
-            if (m != 0xFF) cur = min(cur, lo + (int32_t)m + (int32_t)w);
-            ++k;
         }
         if (k >= e) done = true;
         u64 open = __ballot(!done);
