@@ -449,7 +449,7 @@ __global__ void wp_member_slice_k(WArgs a, uint8_t* __restrict__ own) {
 // first WP_PSERIAL edges by the lane alone, the rest of a long row by the whole wave
 constexpr int WP_PSERIAL = 16;
 #ifndef PJ_WP_HPU
-#define PJ_WP_HPU 1
+#define PJ_WP_HPU 1  // 2 and 4 measured no faster at s26w (13.0-13.5 against 12.8-13.2 ms at world 1, r3ai)
 #endif
 constexpr int WP_HPU = PJ_WP_HPU;
 __global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __restrict__ mmap) {
