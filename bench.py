@@ -137,15 +137,21 @@ def tts_process(args, wl, td):
     tool = os.path.join(ROOT, "paralleljohnson_amd", "bin", "pj_kron_tts")
     scale = args.scale if args.scale else wl["scale"]
     out = os.path.join(td, "sol_tts.txt")
+    env = dict(os.environ)
+    env["PJ_TTS_LAUNCH_NS"] = str(time.monotonic_ns())  # (CLOCK_MONOTONIC, as the tool's steady_clock)
     t3 = time.perf_counter()
     p = subprocess.run([tool, str(scale), str(args.edgefactor), str(args.seed), str(int(wl["weighted"])),
-                        f"sample:{args.seed + 1}", out], capture_output=True, text=True, timeout=300)
+                        f"sample:{args.seed + 1}", out], capture_output=True, text=True, timeout=300, env=env)
     wall = time.perf_counter() - t3
+    t_end = time.monotonic_ns()
     if p.returncode != 0:
         raise RuntimeError(f"pj_kron_tts failed: {p.stderr[-400:]}")
     f = p.stdout.split()
-    phases = dict(zip(("create_s", "build_s", "solve_prep_d2h_s", "write_s"), (float(x) for x in f[1:5])))
-    return {"wall": round(wall, 4), "phases": phases, "root": int(f[6]), "sol": out}
+    phases = dict(zip(("create_s", "build_s", "solve_prep_s", "d2h_s", "write_s", "launch_s", "teardown_s"),
+                      (float(x) for x in f[1:8])))
+    phases["exit_s"] = round((t_end - int(f[11])) * 1e-9, 4)
+    phases["unaccounted_s"] = round(wall - sum(v for v in phases.values() if v > 0), 4)
+    return {"wall": round(wall, 4), "phases": phases, "root": int(f[9]), "sol": out}
 
 
 def time_to_solution(ctx_s, res, tts, td):
@@ -302,6 +308,31 @@ def run_multisource(ctx, args, rank, world, barrier, n_src=1024):
     return dict(elapsed=elapsed, m=m, b=b, n_src=len(mine), cpu=cpu, reps=reps)
 
 
+def run_weighted_batch(g, args, n_roots=16, reps=3):
+    """Johnson-style weighted rows on configs[2]'s graph: pj_sssp_batch over n_roots roots with
+    1 (the serial loop), 2 and 3 delta-stepping solves in flight (delta.hip delta_batch: one
+    stream, frontier ring and counter block per slot, the graph and light CSR shared); rows
+    stay on the device (copy=False), median of `reps` timed batches each."""
+    roots = [int(x) for x in g.sample_roots(args.seed + 7, n_roots)]
+    out = {"workload": f"{n_roots} roots of configs[2]'s graph (sample_roots seed {args.seed + 7}), "
+                       "one pj_sssp_batch call, rows left in HBM", "ms_per_root_by_streams": {}}
+    for slots in (1, 2, 3):
+        g.set_option("batch_streams", slots)
+        g.sssp_batch(roots[:slots], copy=False)  # untimed: the slots' workspaces
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            g.sssp_batch(roots, copy=False)
+            ts.append(time.perf_counter() - t)
+        out["ms_per_root_by_streams"][str(slots)] = round(1000.0 * float(np.median(ts)) / n_roots, 4)
+    g.set_option("batch_streams", 2)
+    by = out["ms_per_root_by_streams"]
+    out["default_streams"] = 2
+    out["speedup_default_vs_serial"] = round(by["1"] / by["2"], 3)
+    out["speedup_best_vs_serial"] = round(by["1"] / min(by.values()), 3)
+    return out
+
+
 def run_wpartitioned_host(args, world_h=2, nroots=3, scale=26):
     """The weighted 1D partition (wpart.hip + libpj's band loop: tail switch, heavy and light
     pulls through all-gathered byte maps) on configs[2]'s graph (Kronecker s26, weights
@@ -435,9 +466,14 @@ def main():
         cpu = cpu_baseline(g, main_res, args)
     n_vertices, nnz = g.n, g.nnz
     r0 = main_res["roots"][0]
+    k26w_batch = None
+    if world == 1 and not args.no_secondary and not args.scale and wl["weighted"]:
+        k26w_batch = run_weighted_batch(g, args)
     g.close()
 
     secondary = {}
+    if k26w_batch:
+        secondary["k26w_batch"] = k26w_batch
     if world == 1 and not args.no_secondary and not args.scale:
         for key in ("k22", "wg"):
             if key == args.workload:

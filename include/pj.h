@@ -180,7 +180,10 @@ const int32_t* pj_dist_device(pj_graph* g);
  * int32, row i = pj_sssp(g, sources[i]); NULL discards the rows (timing).
  * Unit-weight graphs run up to 512 sources per pass, one bit per source
  * (msbfs.hip; the option ms_width caps the pass at 64 x ms_width); weighted
- * graphs run one delta-stepping solve per source. Either way pj_last_stats
+ * graphs run delta-stepping solves with `batch_streams` (default 2, 1-8) of
+ * them in flight at once, each on its own stream and host thread with its own
+ * frontiers and counters, the graph shared (delta.hip delta_batch; rows in
+ * source order whatever finishes first). Either way pj_last_stats
  * then describes the whole batch (kernel_ms and levels summed over passes or
  * solves) and pj_copy_dist / pj_reach_stats fail with PJ_ERR_STATE until the
  * next pj_sssp. No reference counterpart: the reference answers one source
@@ -197,8 +200,9 @@ int pj_last_stats(const pj_graph* g, pj_stats* out);
 int pj_reach_stats(pj_graph* g, pj_stats* out);
 /* Tuning knobs: alpha/beta of the direction switch (Beamer), delta for
  * delta-stepping (0 = automatic), direction (0 auto, 1 push, 2 pull),
- * bfs_small (one-workgroup levels for small frontiers, 0/1) and the batch /
- * grid knobs documented in DESIGN.md. Returns PJ_ERR_ARG on bad values. */
+ * bfs_small (one-workgroup levels for small frontiers, 0/1), batch_streams
+ * (weighted batches: solves in flight, 1-8) and the batch / grid knobs
+ * documented in DESIGN.md. Returns PJ_ERR_ARG on bad values. */
 int pj_set_option(pj_graph* g, const char* key, double value);
 
 /* ---- shortest-path tree (no reference counterpart:

@@ -220,23 +220,6 @@ int finish_graph(pj_ctx* ctx, std::unique_ptr<pj_graph>& pg, pj_graph** out) {
     return PJ_OK;
 }
 
-// Weighted batch: one delta-stepping solve per source (no shared passes);
-// stats are summed over the batch like the unit-weight msbfs path.
-template <typename F>
-void weighted_batch(Graph& g, const int64_t* sources, int n_src, F&& on_row) {
-    auto t0 = std::chrono::steady_clock::now();
-    pj_stats sum{};
-    for (int i = 0; i < n_src; ++i) {
-        delta_solve(g, sources[i]);
-        sum.kernel_ms += g.stats.kernel_ms;
-        sum.levels += g.stats.levels;
-        sum.relax_rounds += g.stats.relax_rounds;
-        on_row(i, g.dist.p);
-    }
-    sum.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    g.stats = sum;
-}
-
 size_t format_rows(const int32_t* d, int64_t a, int64_t b, char* o) {
     size_t k = 0;
     for (int64_t i = a; i < b; ++i) {
@@ -277,9 +260,12 @@ class BatchWriter {
         nthreads_ = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     }
     ~BatchWriter() { join(); }
-    void add_row(int idx, const int32_t* dev_row) {
+    void add_row(int idx, const int32_t* dev_row, hipStream_t s = nullptr) {
         if (fill_ == 0) join_slot(cur_);
-        if (n_) PJ_HIP(hipMemcpy(buf_[cur_].p + (size_t)fill_ * n_, dev_row, 4 * n_, hipMemcpyDeviceToHost));
+        if (n_) {
+            PJ_HIP(hipMemcpyAsync(buf_[cur_].p + (size_t)fill_ * n_, dev_row, 4 * n_, hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipStreamSynchronize(s));
+        }
         paths_[cur_].push_back(paths_in_[idx]);
         if (++fill_ == group_) flush();
     }
@@ -771,9 +757,12 @@ int pj_sssp_batch(pj_graph* pg, const int64_t* sources, int n_src, int32_t* dist
         Graph& g = pg->g;
         bind(*g.ctx);
         if (g.weighted) {
-            weighted_batch(g, sources, n_src, [&](int i, const int32_t* dev) {
-                if (dist_out && g.n)
-                    PJ_HIP(hipMemcpy(dist_out + (size_t)i * (size_t)g.n, dev, 4 * (size_t)g.n, hipMemcpyDeviceToHost));
+            delta_batch(g, sources, n_src, g.batch_streams, [&](int i, const int32_t* dev, hipStream_t s) {
+                if (dist_out && g.n) {
+                    PJ_HIP(hipMemcpyAsync(dist_out + (size_t)i * (size_t)g.n, dev, 4 * (size_t)g.n,
+                                          hipMemcpyDeviceToHost, s));
+                    PJ_HIP(hipStreamSynchronize(s));
+                }
             });
         } else {
             msbfs_solve(g, sources, n_src, dist_out);
@@ -795,8 +784,9 @@ int pj_sssp_batch_write(pj_graph* pg, const int64_t* sources, int n_src, const c
         std::atomic<int> err{PJ_OK};
         BatchWriter wr(n, paths, strict != 0, &err);
         if (g.weighted) {
-            // one solve per source; rows are gathered into host groups and written by the pool
-            weighted_batch(g, sources, n_src, [&](int i, const int32_t* dev) { wr.add_row(i, dev); });
+            // concurrent solves (delta_batch); rows are gathered into host groups and written by the pool
+            delta_batch(g, sources, n_src, g.batch_streams,
+                        [&](int i, const int32_t* dev, hipStream_t s) { wr.add_row(i, dev, s); });
         } else {
             msbfs_each(g, sources, n_src, [&](int off, int ns, const int32_t* rows) {
                 for (int k = 0; k < ns; ++k) wr.add_row(off + k, rows + (size_t)k * n);
@@ -848,13 +838,9 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "beta" && value > 0) g.beta = value;
     else if (k == "delta" && value >= 0) g.delta = value;
     else if (k == "pull_factor" && value >= 0) g.pull_factor = value;
-    else if (k == "delta_impl" && (value == 1 || value == 2)) g.delta_impl = (int)value;
     else if (k == "light_pull" && value >= 0) g.light_pull = value;
     else if (k == "tail_light_pull" && value > 0) g.tail_light_pull = value;
     else if (k == "round_log" && (value == 0 || value == 1)) g.round_log = (int)value;
-    else if (k == "bin_min" && value >= 0) g.bin_min = value;
-    else if (k == "bin_watch" && value >= 0) g.bin_watch = value;
-    else if (k == "pull_grow" && value >= 0) g.pull_grow = value;
     else if (k == "band_width" && value >= 0) g.band_width = value;
     else if (k == "tail_delta") g.tail_delta = value;
     else if (k == "tail_after" && value >= 0 && value < 1e6) g.tail_after = (int)value;
@@ -862,16 +848,13 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "direction" && (value == 0 || value == 1 || value == 2)) g.force_mode = (int)value;
     else if (k == "level_batch" && value >= 0 && value <= 4096) g.level_batch = (int)value;
     else if (k == "round_batch" && value >= 1 && value <= 64) g.round_batch = (int)value;
+    else if (k == "batch_streams" && value >= 1 && value <= 8) g.batch_streams = (int)value;
     else if (k == "light_filter" && (value == 0 || value == 1)) g.light_filter = (int)value;
     else if (k == "dense_frac" && value >= 0 && value <= 1) g.dense_frac = value;
-    else if (k == "dense_pull" && (value == 0 || value == 1)) g.dense_pull = (int)value;
     else if (k == "light_pack" && (value == 0 || value == 1)) g.light_pack = (int)value;
     else if (k == "split_w" && (value == 0 || value == 1)) g.split_w = (int)value;
     else if (k == "tail_pull" && (value == 0 || value == 1)) g.tail_pull = (int)value;
     else if (k == "spin_sync" && (value == 0 || value == 1)) g.spin_sync = (int)value;
-    else if (k == "merged_round" && (value == 0 || value == 1)) g.merged_round = (int)value;
-    else if (k == "fold_hub" && (value == 0 || value == 1)) g.fold_hub = (int)value;
-    else if (k == "defer_heavy" && (value == 0 || value == 1)) g.defer_heavy = (int)value;
     else if (k == "defer_check" && (value == 0 || value == 1)) g.defer_check = (int)value;
     else if (k == "round_gpc" && value >= 0 && value <= 64) g.round_gpc = (int)value;
     else if (k == "hub_gpc" && value >= 0 && value <= 64) g.hub_gpc = (int)value;

@@ -37,6 +37,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -266,19 +267,26 @@ int run_single(const char* webfile, int source, const char* out, int weighted) {
                   << " bytes of text)" << std::endl;
     std::cerr << "compute shortest paths from source node: " << source << std::endl;
     print_msg("parallel Johnson's algorithm starts......");
-    std::vector<int32_t> dist((size_t)n);
+    // the distance buffer: not zero-filled; a host thread faults its pages in while the
+    // GPU solves, so the D2H copy lands in resident memory
+    std::unique_ptr<int32_t[]> dist(new int32_t[(size_t)std::max<int64_t>(n, 1)]);
+    std::thread warm([&] {
+        char* b = reinterpret_cast<char*>(dist.get());
+        for (size_t o = 0; o < (size_t)n * sizeof(int32_t); o += 4096) b[o] = 0;
+    });
     rc = pj_sssp(g, source, nullptr);
+    warm.join();
     if (rc != PJ_OK) fail("pj_sssp", rc);
     pj_stats st{};
     pj_last_stats(g, &st);
     const double t_elapsed = st.kernel_ms / 1000.0;  // device time of the solve (:597-605 analogue)
     ph.mark("solve");
-    rc = pj_copy_dist(g, dist.data());  // :612-614's gather
+    rc = pj_copy_dist(g, dist.get());  // :612-614's gather
     if (rc != PJ_OK) fail("pj_copy_dist", rc);
     ph.mark("d2h");
     print_msg("parallel Johnson's algorithm completes.");
     std::cout << "Time: " << t_elapsed << " seconds when using " << 1 << " processes." << std::endl;
-    rc = pj_write_sol(dist.data(), n, out, 0);  // :615-618
+    rc = pj_write_sol(dist.get(), n, out, 0);  // :615-618
     if (rc != PJ_OK) fail("pj_write_sol", rc);
     ph.mark("write");
     std::cerr << "the shortest path distance vector has been saved in file " << out << std::endl;

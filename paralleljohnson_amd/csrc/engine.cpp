@@ -78,6 +78,12 @@ void bfs_engine(BfsSteps& S, Comm& comm, i64 source, const BfsParams& prm, bool 
             }
             S.end_level_async();
             comm.allgather_rows_dev(S.stats_dev(), 5, rows.data(), s);
+            // a foreign id received by any rank fails every rank at the same level (a peer
+            // of a multi-process group would otherwise wait in the next collective)
+            for (int q = 0; q < S.world; ++q)
+                if (q != S.rank && rows[5 * (size_t)q + 4])
+                    throw Error(PJ_ERR_COMM, "rank " + std::to_string(q) +
+                                                 " received ids owned by another rank (corrupted exchange)");
             S.end_level_finish(rows.data() + 5 * (size_t)S.rank);
             f3[0] = f3[1] = f3[2] = 0;
             for (int q = 0; q < S.world; ++q)
@@ -168,6 +174,12 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             all_edges = S.local_edges();
             comm.allreduce(&all_edges, 1, false, s);
         }
+        // the pull rules: agreed once per solve (any rank vetoes: a rank whose rows are not
+        // its in-edges, or with a pull off), so a vetoed pull costs no per-band collective
+        const double pf = S.pull_factor(), lpf = S.light_pull_factor();
+        i64 allow[2] = {pf > 0.0 ? 1 : 0, lpf > 0.0 ? 1 : 0};
+        comm.allreduce(allow, 2, false, s);
+        const bool heavy_pull_ok = allow[0] == S.world, light_pull_ok = allow[1] == S.world;
         std::vector<i64> counts((size_t)S.world), rcounts((size_t)S.world);
         i64 sent = 0, bands = 0, rounds = 0, pulls = 0, lpulls = 0;
         auto exchange_apply = [&](int light, int32_t lo, int32_t hi) {
@@ -217,16 +229,15 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             }
             ++bands;
             i64 fsize = cnt;  // the round's frontier, all ranks
-            const double lpf = S.light_pull_factor();
             for (;;) {  // light rounds until no rank has a frontier
                 // a big round may pull (the gate keeps the counts off small rounds; every rank
-                // sees the same fsize, and any rank can veto through the third count)
+                // sees the same fsize)
                 bool lpulled = false;
-                if (lpf >= 0.0 && hi - lo <= 255 && fsize * 64 >= S.n) {
-                    i64 lc[3] = {0, 0, lpf > 0.0 ? 1 : 0};
-                    if (lpf > 0.0) S.light_counts((int32_t)lo, (int32_t)hi, lc);
-                    comm.allreduce(lc, 3, false, s);
-                    if (lc[2] == S.world && lc[0] > 0 && (double)lc[0] * lpf > (double)lc[1]) {
+                if (light_pull_ok && hi - lo <= 255 && fsize * 64 >= S.n) {
+                    i64 lc[2] = {0, 0};
+                    S.light_counts((int32_t)lo, (int32_t)hi, lc);
+                    comm.allreduce(lc, 2, false, s);
+                    if (lc[0] > 0 && (double)lc[0] * lpf > (double)lc[1]) {
                         S.frontier_slice((int32_t)lo, (int32_t)hi);
                         if (S.world > 1) {
                             const size_t sl = S.member_bytes();
@@ -255,14 +266,11 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             // heavy edges of the band's members: pulled by the unsettled vertices when those
             // have fewer heavy edges than pull_factor x the members' (v2's rule, §4.2), else pushed
             bool pulled = false;
-            const double pf = S.pull_factor();
-            if (pf >= 0.0 && hi - lo <= 255) {  // (member offsets are bytes)
-                // every rank must agree: a rank whose rows are not its in-edges (or with the
-                // pull off) vetoes it through the third count
-                i64 hc[3] = {0, 0, pf > 0.0 ? 1 : 0};
-                if (pf > 0.0) S.heavy_counts((int32_t)lo, (int32_t)hi, hc);
-                comm.allreduce(hc, 3, false, s);
-                if (hc[2] == S.world && hc[0] > 0 && (double)hc[1] < pf * (double)hc[0]) {
+            if (heavy_pull_ok && hi - lo <= 255) {  // (member offsets are bytes)
+                i64 hc[2] = {0, 0};
+                S.heavy_counts((int32_t)lo, (int32_t)hi, hc);
+                comm.allreduce(hc, 2, false, s);
+                if (hc[0] > 0 && (double)hc[1] < pf * (double)hc[0]) {
                     S.member_slice((int32_t)lo, (int32_t)hi);
                     if (S.world > 1) {
                         const size_t sl = S.member_bytes();

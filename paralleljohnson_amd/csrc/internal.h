@@ -192,43 +192,33 @@ struct Graph {
 
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;
-    double pull_factor = 4.0;  // v1, symmetric: pull a band's heavy edges when the heavy edges of unsettled
+    double pull_factor = 4.0;  // symmetric: pull a band's heavy edges when the heavy edges of unsettled
                                // vertices < pull_factor x the members' heavy edges (0 = never)
     double band_width = 0.0;   // v2: width of a band [lo, lo + band_width) (0 = delta, at most delta)
     double tail_delta = -1.0;  // v2: light threshold and band width of the tail (0 = off, < 0 = 64 x delta):
     int tail_after = 1;        // from the first band >= tail_after at which the edges of unsettled
     double tail_frac = 0.1;    // vertices are < tail_frac x nnz (profiles/r01/tail_sweep.txt)
-    double pull_grow = 1e9;   // v2: launch the light-pull kernels in a batch of rounds when the last seen
-                               // frontier's light edges x pull_grow exceed the pull threshold
     double light_pull = 3.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
                                // the light edges of unsettled vertices / light_pull (0 = never; 2 -> 3 at
                                // the end of round 2 with merged rounds: +1%, interleaved A/B)
     double tail_light_pull = 3.0;  // the same rule in the tail's rounds
     int round_log = 0;         // debug: per light round (kind, frontier, light edges) on stderr
-    double bin_min = 0;        // v2: binned light round when a check saw at least this many light edges
-                               // in the next (push) frontier (0 = never; measured 10x slower on k26w:
-                               // degree-ordered ids send most pairs to the first buckets)
-    double bin_watch = 524288; // v2: single rounds between checks while the frontier holds this many
-    int delta_impl = 2;        // weighted band loop: 2 = bitmap frontiers (delta.hip v2), 1 = list-based
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
     int level_batch = 0; // BFS levels enqueued per host check (0 = the previous solve's count, then 2, 4, 8, ...)
     double dense_frac = 0.1; // delta v2: a light round with a frontier above dense_frac x n runs tile-dense (0 = never;
                              // swept 0 / 0.02 / 0.1 / 0.3 on k26w: 0.1 best)
     int light_filter = 1;  // delta v2: skip vertices without light edges in light rounds (hl bitmap)
-    int dense_pull = 0;    // delta v2: light pull rounds in tile-dense form (0/1; measured equal)
     int light_pack = 1;    // delta v2: light CSR records packed in 32 bits when they fit (0/1)
     int split_w = 1;       // delta v2: whole-CSR reads as u32 ids + u8 weights when every weight <= 255 (0/1)
     int tail_pull = 1;     // delta v2: light pull rounds allowed in the tail too (round 3: 391 -> 428 GTEPS, once
                            // the tail-entry frontier counts its whole rows, fesplit)
     int spin_sync = 1;     // delta v2: the host spins on a published sequence word instead of a stream sync (0/1)
-    int defer_heavy = 0;   // delta v2: a heavy pull before a non-tail band relaxes only edges landing in it (0/1; measured equal)
-    int fold_hub = 0;      // delta v2: a light round's hub tiles run in the next round's launch (0/1; measured 4% slower)
-    int merged_round = 1;  // delta v2: one launch per light round decides pull / dense / sparse push (0/1)
-    int defer_check = 1;   // delta v2 (merged rounds): no host check right after a heavy step (0/1)
+    int defer_check = 1;   // delta v2: no host check right after a heavy step (0/1)
     int round_gpc = 12;    // delta v2: workgroups per CU of the light-round / hub launches (0 = the heavy
     int hub_gpc = 4;       // kernels' 24); swept (24,24) (6,7) (12,14) (12,7) (12,4) (16,7): (12,4) best
     int heavy_gpc = 0;     // delta v2: workgroups per CU of the heavy pull (0 = 24; 7-32 swept, 12-32 equal)
     int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)
+    int batch_streams = 2; // weighted batches (pj_sssp_batch*): solves in flight at once, one stream each
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
     int bfs_small = 1;   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)
     int bfs_spare = 0;   // BFS: launches beyond the previous solve's count in the first batch (1 measured
@@ -293,6 +283,10 @@ void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t see
 void bfs_solve(Graph& g, i64 source);
 i64 relabeled_id(const Relabeled& R, i64 v, hipStream_t s);  // relabel.hip: inv[v]
 void delta_solve(Graph& g, i64 source);
+// Weighted batch with `slots` concurrent solves (delta.hip); on_row(i, device row, stream)
+// is called once per source, serialised.
+void delta_batch(Graph& g, const i64* sources, int n_src, int slots,
+                 const std::function<void(int, const int32_t*, hipStream_t)>& on_row);
 void msbfs_solve(Graph& g, const int64_t* sources, int n_src, int32_t* dist_out);
 // Batched passes of up to 256 sources; after each pass on_pass(first source
 // index, sources in the pass, device rows [ns][n]) runs with the device idle.

@@ -294,7 +294,11 @@ class DeviceWPart:
         self.nl = self.hi - self.lo
 
     def set_option(self, key: str, value: float):
-        """pj_wpart_set_option ("tail_frac", "tail_mult"); the same on every rank."""
+        """pj_wpart_set_option: "tail_frac", "tail_mult", "pull_factor" or "light_pull".
+
+        Every rank of a group must set the same values (the ranks take the tail switch and
+        the pull decisions from all-reduced counts, and agree once per solve whether every
+        rank allows each pull)."""
         _check(_lib.pj_wpart_set_option(self._h, key.encode(), float(value)))
 
     def delta(self, comm: Comm, source: int, delta: int = 0) -> dict:

@@ -197,20 +197,16 @@ def test_weighted_delta_stepping(ctx, oracle):
         perm = np.lexsort((wc, rid))
         assert (grow == row).all()
         assert (gcol.astype(np.uint32) == col[perm]).all() and (gw == wc[perm]).all()
-        for impl in (1, 2):  # list-based and bitmap-frontier band loops (delta.hip)
-            g.set_option("delta_impl", impl)
-            for delta in (0, 1, 37):
-                g.set_option("delta", delta)
-                for r in (int(src[0]) if len(src) else 0, int(rng.integers(0, n))):
-                    assert (g.sssp(r) == oracle.dijkstra(row, col, wc, r)).all(), (trial, impl, delta, r)
+        for delta in (0, 1, 37):
+            g.set_option("delta", delta)
+            for r in (int(src[0]) if len(src) else 0, int(rng.integers(0, n))):
+                assert (g.sssp(r) == oracle.dijkstra(row, col, wc, r)).all(), (trial, delta, r)
         g.close()
 
 
-def test_weighted_deferral_paths(ctx, oracle):
-    """In-band vertices that a relax workgroup cannot finish itself: a row longer
-    than LOCAL_MAX (4096) reached by a light edge, and more in-band improvements
-    than the LDS worklist holds (2048). Both go through the `chg` bitmap and the
-    follow-up rounds of delta.hip."""
+def test_weighted_fan_cascades(ctx, oracle):
+    """A light row longer than the hub threshold reached by a light edge, followed by
+    thousands of in-band improvements in one round (hub queue, tile-dense rounds)."""
     rng = np.random.default_rng(5)
     fan = 9000
     leaves = np.arange(2, 2 + fan)
@@ -222,11 +218,9 @@ def test_weighted_deferral_paths(ctx, oracle):
         w = rng.integers(0, wmax, len(src)).astype(np.uint32)
         g = ctx.load_coo(src, dst, w=w, n=n)
         row, col, wc = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n, w)
-        for impl in (1, 2):
-            g.set_option("delta_impl", impl)
-            for delta in (0, 8, 1000):
-                g.set_option("delta", delta)
-                assert (g.sssp(0) == oracle.dijkstra(row, col, wc, 0)).all(), (wmax, impl, delta)
+        for delta in (0, 8, 1000):
+            g.set_option("delta", delta)
+            assert (g.sssp(0) == oracle.dijkstra(row, col, wc, 0)).all(), (wmax, delta)
         g.close()
 
 
@@ -244,10 +238,10 @@ def test_weighted_text_and_kronecker(ctx, oracle):
 
 def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
     """Tile-dense light rounds (dense_frac: never / whenever the frontier is non-empty /
-    the default threshold), tile-dense light pulls (dense_pull) and the has-light-edge
-    filter (on / off) and the packed 32-bit light CSR (on / off), hub tiles folded into the next
-    round's launch (fold_hub) or in their own, with light pulls never / by the default rule / in every round and
-    with and without the tail switch: directed random graphs (no pulls), a star whose
+    the default threshold), the has-light-edge filter (on / off), the packed 32-bit light
+    CSR (on / off) and the split whole-CSR records, light pulls in the tail (on / off), the
+    deferred band check (on / off), with light pulls never / by the default rule / in every
+    round and with and without the tail switch: directed random graphs (no pulls), a star whose
     light segment exceeds the dense mode's hub threshold (4096), and Kronecker graphs.
     Bit-exact against the oracle Dijkstra."""
     rng = np.random.default_rng(33)
@@ -268,52 +262,22 @@ def test_weighted_dense_rounds_and_light_filter(ctx, oracle):
         col = col.astype(np.uint32)
         roots = [0] + [int(r) for r in g.sample_roots(4, 2)]
         exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
-        for i, (dense, dp, pk, tp, mr) in enumerate(((0.0, 0, 0, 0, 0), (1e-12, 1, 1, 1, 1), (0.02, 0, 1, 1, 0),
-                                                     (0.02, 1, 0, 0, 1), (0.1, 1, 1, 0, 0), (0.1, 0, 2, 1, 1),
-                                                     (0.0, 0, 1, 0, 1))):
-            for lf in (0, 1):
-                g.set_option("fold_hub", lf ^ (i & 1))  # hub tiles in the next round's launch, or their own
-                for lp, tf in ((2.0, 0.1), (0.0, 0.1), (2.0, 0.0), (1e15, 0.1)):
-                    g.set_option("dense_frac", dense)
-                    g.set_option("dense_pull", dp)
-                    g.set_option("light_pack", min(pk, 1))
-                    g.set_option("split_w", int(pk != 2))
-                    g.set_option("tail_pull", tp)
-                    g.set_option("merged_round", mr)
-                    g.set_option("defer_check", int(dense != 0.02))
-                    g.set_option("light_filter", lf)
-                    g.set_option("light_pull", lp)
-                    g.set_option("tail_frac", tf)
-                    for delta in (0, 40):
-                        g.set_option("delta", delta)
-                        for r in roots:
-                            assert (g.sssp(r) == exp[r]).all(), (name, dense, dp, pk, tp, mr, lf, lp, tf, delta, r,
-                                                                 lf ^ (i & 1))
-        g.close()
-
-
-@pytest.mark.parametrize("scale,ef", [(12, 16), (16, 16), (18, 8)])
-def test_weighted_binned_rounds(ctx, oracle, scale, ef):
-    """Binned light rounds (delta.hip: the frontier's light edges as (target, dist) pairs,
-    bucketed by target range -- coarse, then 2^14-vertex fine buckets -- and reduced with
-    LDS minima per range) against the oracle Dijkstra: forced on every round after a
-    host check (bin_min 1), on mid-size rounds only, and off; with and without light
-    pulls; several deltas. s18 spans 16 fine buckets in several coarse ones."""
-    g = ctx.generate_kronecker(scale, ef, 40 + scale, weighted=True)
-    row, col, wc = g.get_csr()
-    col = col.astype(np.uint32)
-    roots = [0] + [int(r) for r in g.sample_roots(9, 3)]
-    exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
-    for bmin, bwatch in ((1, 0), (64, 1), (4096, 256), (0, 0)):
-        for lp in (0.0, 3.0):
-            for delta in (0, 5, 40):
-                g.set_option("bin_min", bmin)
-                g.set_option("bin_watch", bwatch)
+        for i, (dense, pk, tp) in enumerate(((0.0, 0, 0), (1e-12, 1, 1), (0.02, 1, 1), (0.1, 2, 0), (0.1, 0, 1))):
+            lf = i & 1
+            for lp, tf in ((2.0, 0.1), (0.0, 0.1), (2.0, 0.0), (1e15, 0.1)):
+                g.set_option("dense_frac", dense)
+                g.set_option("light_pack", min(pk, 1))
+                g.set_option("split_w", int(pk != 2))
+                g.set_option("tail_pull", tp)
+                g.set_option("defer_check", int(dense != 0.02))
+                g.set_option("light_filter", lf)
                 g.set_option("light_pull", lp)
-                g.set_option("delta", delta)
-                for r in roots:
-                    assert (g.sssp(r) == exp[r]).all(), (scale, bmin, bwatch, lp, delta, r)
-    g.close()
+                g.set_option("tail_frac", tf)
+                for delta in (0, 40):
+                    g.set_option("delta", delta)
+                    for r in roots:
+                        assert (g.sssp(r) == exp[r]).all(), (name, dense, pk, tp, lf, lp, tf, delta, r)
+        g.close()
 
 
 @pytest.mark.parametrize("scale,ef", [(13, 16), (15, 4)])
@@ -344,26 +308,21 @@ def test_weighted_band_width(ctx, oracle, scale, ef):
 @pytest.mark.parametrize("scale,ef", [(12, 16), (14, 4), (16, 1), (15, 16)])
 def test_weighted_pull_heavy(ctx, oracle, scale, ef):
     """Heavy edges by pull (symmetric graphs): never (push only), by the default
-    rule, and in every band; several deltas; heavy pulls that defer the edges which
-    cannot land in the next band to the heavy step after it (defer_heavy) or not,
-    with and without the tail switch. Bit-exact against the oracle Dijkstra."""
+    rule, and in every band; several deltas, with and without the tail switch. Bit-exact against the oracle Dijkstra."""
     g = ctx.generate_kronecker(scale, ef, 9 + scale, weighted=True)
     row, col, wc = g.get_csr()
     col = col.astype(np.uint32)
     roots = [int(r) for r in g.sample_roots(3 + ef, 3)]
     exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
-    # (band loop, heavy pull factor, light pull factor): list-based; bitmap with
-    # push only, default rules, pull whenever possible
-    for impl, pf, lp in ((1, 1.0, 0.0), (2, 0.0, 0.0), (2, 4.0, 2.0), (2, 1e15, 1e15)):
-        g.set_option("delta_impl", impl)
+    # (heavy pull factor, light pull factor): push only, default rules, pull whenever possible
+    for pf, lp in ((0.0, 0.0), (4.0, 2.0), (1e15, 1e15)):
         g.set_option("pull_factor", pf)
         g.set_option("light_pull", lp)
-        for delta, dh, tf in ((0, 1, 0.1), (7, 1, 0.0), (60, 1, 0.1), (0, 0, 0.1), (7, 0, 0.1), (60, 1, 0.0)):
+        for delta, tf in ((0, 0.1), (7, 0.0), (60, 0.1), (7, 0.1), (60, 0.0)):
             g.set_option("delta", delta)
-            g.set_option("defer_heavy", dh)
             g.set_option("tail_frac", tf)
             for r in roots:
-                assert (g.sssp(r) == exp[r]).all(), (impl, pf, lp, delta, dh, tf, r)
+                assert (g.sssp(r) == exp[r]).all(), (pf, lp, delta, tf, r)
                 st = g.stats()
                 if pf == 0.0:
                     assert st["bu_levels"] == 0

@@ -1,0 +1,53 @@
+#!/bin/bash
+# One parameterised GPU-box cycle (replaces the per-cycle gpu_r3*.sh scripts of round 3).
+#   bash tools/cycle.sh TAG STEPS [bench args...]
+# STEPS: comma-separated, run in order, stopping at the first failure:
+#   tests         every -m gpu test           tests:<pytest args>  e.g. tests:tests/test_gpu_parity.py
+#   smoke         __graft_entry__.smoke()
+#   bench         the default bench line (bench args appended) -> bench.json
+#   kt            rocprofv3 kernel trace + stats of a short k26w bench run
+#   pmc           FETCH_SIZE / WRITE_SIZE passes over tools/traffic_probe.py (one counter per run)
+#   table         the per-kernel PMC table and traffic json from kt + pmc
+#   probe:<cmd>   any python command line under a 240 s limit (e.g. probe:tools/stats_probe.py 26 3)
+# Output under gpurun_out/TAG.
+set -o pipefail
+TAG=${1:?tag}; STEPS=${2:?steps}; shift 2
+OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+IFS=',' read -ra LIST <<< "$STEPS"
+for st in "${LIST[@]}"; do
+  name=${st%%:*}; arg=""; [[ "$st" == *:* ]] && arg=${st#*:}
+  echo "== $name $arg"
+  case $name in
+    tests)
+      timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu ${arg:-tests} \
+        > "$OUT/pytest_gpu.log" 2>&1 || { echo "tests failed"; tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+      tail -1 "$OUT/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || { echo "smoke failed"; tail "$OUT/smoke.log"; exit 1; }
+      tail -2 "$OUT/smoke.log" ;;
+    bench)
+      timeout -k 10 500 python -u bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" \
+        || { echo "bench failed"; tail -20 "$OUT/bench.err"; exit 1; }
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); s=d.get('secondary',{}); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d.get('time_to_solution_s'), (d.get('time_to_solution_phases') or {}).get('process_phases'), s.get('wg',{}).get('ms_per_sssp'), s.get('ms1024',{}).get('batch_ms'))" "$OUT/bench.json" ;;
+    kt)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
+        python3 bench.py --no-cpu-baseline --no-secondary --no-partitioned --no-tts --steps 8 --warmup 1 "$@" \
+        > "$OUT/kt.log" 2>&1 || { echo "kt failed"; tail "$OUT/kt.log"; exit 1; } ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o run -- \
+          python3 tools/traffic_probe.py 26 4 1 > "$OUT/pmc_$c.log" 2>&1 || { echo "pmc $c failed"; exit 1; }
+      done ;;
+    table)
+      python3 tools/pmc_solve_table.py "$OUT" > "$OUT/pmc_table.txt" 2>&1 || { echo "table failed"; exit 1; }
+      python3 tools/traffic_json.py "$OUT" > "$OUT/traffic_k26w.json" 2>&1 || { echo "traffic failed"; exit 1; }
+      cat "$OUT/pmc_table.txt" ;;
+    probe)
+      timeout -k 10 240 python3 -u $arg > "$OUT/probe_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-40).log" 2>&1 \
+        || { echo "probe failed: $arg"; exit 1; } ;;
+    *) echo "unknown step $name"; exit 2 ;;
+  esac
+done
+echo "cycle ok"

@@ -1,4 +1,4 @@
-"""Per-kernel time and PMC bytes per k26w SSSP from one round cycle (tools/gpu_round.sh layout):
+"""Per-kernel time and PMC bytes per k26w SSSP from one round cycle (tools/cycle.sh kt + pmc layout):
 launches and time per solve from the bench's kernel trace (TAG/kt, solves = v2_init_k launches),
 2*FETCH_SIZE + WRITE_SIZE per solve from the traffic_probe passes (TAG/pmc_FETCH_SIZE,
 TAG/pmc_WRITE_SIZE, solves = v2_init_k dispatches). Usage: python tools/pmc_solve_table.py gpurun_out/TAG"""

@@ -1,4 +1,4 @@
-"""HBM traffic per solve from the FETCH_SIZE / WRITE_SIZE passes of tools/gpu_round.sh
+"""HBM traffic per solve from the FETCH_SIZE / WRITE_SIZE passes of tools/cycle.sh (pmc step)
 (rocprofv3 --pmc over tools/traffic_probe.py): sum of the solve kernels' counters (KB)
 per solve, 2 x FETCH_SIZE + WRITE_SIZE in bytes (MI355X_MICROARCH.md HBM section).
 Usage: python tools/traffic_json.py gpurun_out/TAG > profiles/traffic_k26w.json"""
