@@ -274,6 +274,11 @@ typedef struct pj_part_info {
     int64_t nnz_local;      /* out-edges of the owned block */
     int64_t nnz_in_local;   /* in-edges of the owned block (== nnz_local if symmetric) */
     int32_t rank, world, symmetric, off64;
+    /* device bytes held by this rank: its rows (CSR, and CSC when not symmetric),
+     * the O(block) vertex state, the N-bit bitmaps (the level's claimed remote ids,
+     * and the engine's replicated visited / isolated masks once pj_part_bfs ran) and
+     * the exchange buffers (sized to the largest level's ids sent / received) */
+    int64_t bytes_rows, bytes_state, bytes_bitmaps, bytes_exchange;
 } pj_part_info;
 
 /* The rank's share of pj_generate_kronecker(scale, edgefactor, seed, unit
@@ -298,8 +303,9 @@ int pj_part_zmask(pj_part* p, uint64_t* own_words);
  * (n_f, m_f, frontier vertices with out-edges) of level 0, this rank's share. */
 int pj_part_begin(pj_part* p, int64_t source, const uint64_t* iso, uint64_t* vis, int64_t* stats);
 /* Top-down expansion of level `level` (this rank's frontier). Owned targets are
- * settled at distance level+1; the others are written to send (device,
- * capacity world * block u32) owner-major, counts[world] (host) per owner. */
+ * settled at distance level+1; the others are written to send (device, room for
+ * the sum of the counts; world * block u32 always suffices) owner-major,
+ * counts[world] (host) per owner. */
 int pj_part_push(pj_part* p, int level, uint64_t* vis, uint32_t* send, int64_t* counts);
 /* Settle the ids received for this rank after the exchange of a push level. */
 int pj_part_apply(pj_part* p, int level, uint64_t* vis, const uint32_t* recv, int64_t n_recv);
@@ -351,6 +357,11 @@ int pj_wpart_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_wp
 int pj_wpart_destroy(pj_wpart* p);
 /* out[8] = (n, lo, hi, block, nnz_local, world, rank, nnz of the whole graph) */
 int pj_wpart_info(const pj_wpart* p, int64_t* out);
+/* out[4] = this rank's device bytes: its rows; the O(block) vertex state; the
+ * N-sized tables (remote candidates, int32 per vertex, with their touched bitmap,
+ * and the pull rounds' replicated byte map); the exchange buffers, sized to the
+ * largest round's (id, candidate) traffic once pj_wpart_delta ran. */
+int pj_wpart_device_bytes(const pj_wpart* p, int64_t* out);
 /* Start a solve from `source` (dist := INF, then the source); delta <= 0 picks
  * the single-GPU default (3.5 x mean weight / mean degree). *delta_out = delta. */
 int pj_wpart_begin(pj_wpart* p, int64_t source, int32_t delta, int32_t* delta_out);

@@ -1180,6 +1180,12 @@ int pj_wpart_destroy(pj_wpart* p) {
     });
 }
 
+int pj_wpart_device_bytes(const pj_wpart* p, int64_t* out) {
+    if (!p || !out) return arg_error("pj_wpart_device_bytes: bad argument");
+    wpart_device_bytes(*reinterpret_cast<const WPart*>(p), out);
+    return PJ_OK;
+}
+
 int pj_wpart_info(const pj_wpart* p, int64_t* out) {
     if (!p || !out) return arg_error("pj_wpart_info: bad argument");
     wpart_info(*reinterpret_cast<const WPart*>(p), out);
@@ -1342,7 +1348,7 @@ int pj_part_destroy(pj_part* p) {
 
 int pj_part_info_get(const pj_part* p, pj_part_info* out) {
     if (!p || !out) return arg_error("pj_part_info_get: bad argument");
-    i64 v[11];
+    i64 v[15];
     part_info(*reinterpret_cast<const Part*>(p), v);
     out->n = v[0];
     out->lo = v[1];
@@ -1355,6 +1361,10 @@ int pj_part_info_get(const pj_part* p, pj_part_info* out) {
     out->rank = (int32_t)v[8];
     out->world = (int32_t)v[9];
     out->nnz_in_local = v[10];
+    out->bytes_rows = v[11];
+    out->bytes_state = v[12];
+    out->bytes_bitmaps = v[13];
+    out->bytes_exchange = v[14];
     return PJ_OK;
 }
 
@@ -1382,7 +1392,7 @@ int pj_part_push(pj_part* p, int level, uint64_t* vis, uint32_t* send, int64_t* 
     return guarded([&] {
         bind(part_ctx(*reinterpret_cast<Part*>(p)));
         Part& P = *reinterpret_cast<Part*>(p);
-        i64 info[11];
+        i64 info[15];
         part_info(P, info);
         if (info[9] > 1 && !send) throw Error(PJ_ERR_ARG, "pj_part_push: send is NULL");
         part_push(P, level, reinterpret_cast<u64*>(vis), send, counts);

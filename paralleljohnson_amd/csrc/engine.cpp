@@ -114,11 +114,14 @@ void bfs_engine(BfsSteps& S, Comm& comm, i64 source, const BfsParams& prm, bool 
                     if (exchanges(comm)) comm.alltoall_counts(counts.data(), rcounts.data(), s);
                 }
                 if (exchanges(comm)) {
-                    comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u32), s);
+                    i64 ns = 0;
                     for (int q = 0; q < S.world; ++q) {
-                        sent += counts[(size_t)q];
+                        ns += q == S.rank ? 0 : counts[(size_t)q];
                         nr += rcounts[(size_t)q];
                     }
+                    S.exchange_buffers(ns, nr);
+                    comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u32), s);
+                    sent += ns;
                 }
                 S.apply(level, nr);
                 ++td;
@@ -187,11 +190,14 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
             i64 nr = 0;
             if (exchanges(comm)) {
                 comm.alltoall_counts(counts.data(), rcounts.data(), s);
-                comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u64), s);
+                i64 ns = 0;
                 for (int q = 0; q < S.world; ++q) {
-                    sent += counts[(size_t)q];
+                    ns += counts[(size_t)q];
                     nr += rcounts[(size_t)q];
                 }
+                S.exchange_buffers(ns, nr);
+                comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u64), s);
+                sent += ns;
             }
             S.apply(nr, light, lo, hi);
         };

@@ -72,8 +72,9 @@ std::unique_ptr<Comm> make_callback_comm(const pj_comm_callbacks& cb);
 
 // --------------------------------------------------------- device steps ---
 // The pj_part_* steps of one rank (include/pj.h) and the buffers they share
-// with the transport: vis / iso (world * bw u64, replicated), send / recv
-// (world * block u32), zown (bw u64).
+// with the transport: vis / iso (world * bw u64, replicated), send / recv (u32
+// ids; caller steps: world * block, libpj's steps: sized to the traffic by
+// exchange_buffers), zown (bw u64).
 struct BfsSteps {
     i64 n = 0, nnz_local = 0, bw = 1, block = 64;
     int rank = 0, world = 1;
@@ -95,9 +96,14 @@ struct BfsSteps {
     virtual const i64* stats_dev() { return nullptr; }
     virtual void end_level_async() {}
     virtual void end_level_finish(const i64* own5) { (void)own5; }
+    // Called after a push level's counts are known on every rank, before the exchange:
+    // send must then hold the packed ids (nsend of them) and recv room for nrecv. The
+    // default (callback steps) keeps the caller's buffers, packed by push itself.
+    virtual void exchange_buffers(i64 nsend, i64 nrecv) { (void)nsend, (void)nrecv; }
 };
 
-// The pj_wpart_* steps; send / recv hold world * block u64 (id | cand << 32).
+// The pj_wpart_* steps; send / recv hold u64 (id | cand << 32): world * block for
+// caller steps, sized to the traffic by exchange_buffers for libpj's steps.
 struct DeltaSteps {
     i64 n = 0;
     int rank = 0, world = 1;
@@ -110,6 +116,8 @@ struct DeltaSteps {
     virtual void apply(i64 n_recv, int light, int32_t lo, int32_t hi) = 0;
     virtual i64 end_round() = 0;
     virtual void reach(i64* out2) = 0;
+    // after relax's counts are exchanged, before the alltoallv (as BfsSteps)
+    virtual void exchange_buffers(i64 nsend, i64 nrecv) { (void)nsend, (void)nrecv; }
     // Device-resident results (nullptr: host values only): select_async() leaves the
     // row (min pending dist as u64, band size) at select_dev(); end_round_async() leaves
     // the new frontier size at nf_dev(); the finish calls reset the step's counters.

@@ -308,6 +308,8 @@ void wpart_info(const WPart& p, i64* out8);
 int32_t wpart_begin(WPart& p, i64 source, int32_t delta);
 void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2);
 void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts);
+void wpart_pack(WPart& p, u64* send);
+void wpart_device_bytes(const WPart& p, i64* out4);
 void wpart_apply(WPart& p, const u64* recv, i64 nr, int light, int32_t lo, int32_t hi);
 i64 wpart_end_round(WPart& p);
 void wpart_reach(WPart& p, i64* out2);
@@ -318,7 +320,7 @@ void delete_part(Part* p);
 Part* part_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, int rank, int world);
 Part* part_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, i64 nnz, i64 n, int rank, int world,
                     bool symmetric);
-void part_info(const Part& p, i64* out);  // n lo hi block bw nnz_local sym off64 rank world nnz_in_local
+void part_info(const Part& p, i64* out);  // n lo hi block bw nnz_local sym off64 rank world nnz_in_local, bytes x4
 void part_zmask(Part& p, u64* out_dev);
 void part_begin(Part& p, i64 source, const u64* iso, u64* vis, i64* out3);
 void part_push(Part& p, int level, u64* vis, u32* packed, i64* counts);

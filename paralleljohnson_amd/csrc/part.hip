@@ -18,14 +18,20 @@
 //               world slices of bw = block/64 words; exact for the owned slice,
 //               exact everywhere after the per-level all-gather of slices
 //   fr / frn    own-slice bitmaps: current and next frontier
-//   send        world x SH regions of `block` ids (targets for owner o, shard s);
-//               one rank claims a target at most once, so a region cannot overflow
+//   sent        replicated-size bitmap (world x bw words) of the remote targets this
+//               rank claimed in the current push level; the pack turns it into the
+//               owner-major id list and clears it. With it, the exchange buffers are
+//               sized to the traffic (the ids actually sent / received, grown to the
+//               largest level), not to the partition: per-rank state is the owned
+//               rows + O(N/P) vertex state + three N-bit bitmaps (vis, iso, sent)
+//               + the traffic (round 3: world x 8 x block u32 send regions and world x
+//               block u32 send / recv buffers, ~40 N bytes per rank at every world)
 //
 // A level (driven by paralleljohnson_amd/partition.py):
 //   push : queue := fr (vertices with out-degree >= 1), edge-balanced expansion;
 //          a target is claimed with atomicOr on vis; owned targets are settled
-//          at once, others are appended to the owner's send region, then packed
-//          owner-major for all_to_all_single; pj_part_apply settles the received
+//          at once, others are marked in `sent` and counted per owner, then packed
+//          owner-major for the exchange; pj_part_apply settles the received
 //          ids (claim on the owner's exact slice). This is the analogue of the
 //          reference's per-owner send buffers and MPI_Alltoall(v) at :522-554.
 //   pull : every unvisited owned vertex probes its in-neighbours in the exact
@@ -192,8 +198,9 @@ struct PartArgs {
     u32* q;     // frontier queue (local ids)
     u32* qdeg;
     u64* qoff;
-    u32* send;  // world * SH * block
-    u64* ctr;   // world * SH counters, 8 words apart
+    u64* sent;  // world * bw: remote targets claimed by this push level
+    u64* ctr;   // world * SH counters, 8 words apart (this level's remote claims per owner)
+    u64* cur;   // world cursors, 8 words apart (pack)
     u64* stat;  // [0] n_f, [1] m_f, [2] frontier with out-edges, [3] queue fill, [4] bad ids, [8..8+world) packed counts
 };
 
@@ -293,7 +300,6 @@ template <typename Off>
 __global__ __launch_bounds__(TB) void part_push_k(PartArgs a, PartD<Off> g, u64 nq, u64 mq, int32_t nlev) {
     __shared__ LbShared<PTILE> sh;
     __shared__ u32 lcnt[MAXW];
-    __shared__ u64 lbase[MAXW];
     const int shard = blockIdx.x % SH;
     const u32 blk = (u32)a.block;
     for (u64 e0 = (u64)blockIdx.x * PTILE; e0 < mq; e0 += (u64)gridDim.x * PTILE) {
@@ -302,25 +308,22 @@ __global__ __launch_bounds__(TB) void part_push_k(PartArgs a, PartD<Off> g, u64 
         lb_tile_load<PTILE>(a.qoff, nq, e0, sh, s0, ns);
         if (threadIdx.x < (u32)a.world) lcnt[threadIdx.x] = 0;
         __syncthreads();
-        u32 tgt[EPT], own[EPT], rk[EPT];
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
-            own[j] = 0xFFFFFFFFu;
             const u64 e = e0 + (u64)j * TB + threadIdx.x;
             if (e < mq) {
                 const u32 slot = lb_find<PTILE>(sh, ns, e);
                 const u32 u = a.q[s0 + slot];
                 const u32 t = g.col[(u64)g.row[u] + (e - sh.off[slot])];
-                tgt[j] = t;
                 if (claim(a.vis, t)) {
                     const u32 o = t / blk;
                     if ((int)o == a.rank) {
                         const u32 l = t - (u32)a.lo;
                         a.dist[l] = nlev;
                         atomicOr(&a.frn[l >> 6], 1ull << (l & 63));
-                    } else {
-                        own[j] = o;
-                        rk[j] = atomicAdd(&lcnt[o], 1u);
+                    } else {  // (the claim is this rank's only one of t: the bit is new)
+                        atomicOr(&a.sent[t >> 6], 1ull << (t & 63));
+                        atomicAdd(&lcnt[o], 1u);
                     }
                 }
             }
@@ -328,42 +331,59 @@ __global__ __launch_bounds__(TB) void part_push_k(PartArgs a, PartD<Off> g, u64 
         __syncthreads();
         if (threadIdx.x < (u32)a.world) {
             const u32 c = lcnt[threadIdx.x];
-            lbase[threadIdx.x] = c ? atomicAdd(&a.ctr[((u64)threadIdx.x * SH + shard) * 8], (u64)c) : 0;
+            if (c) atomicAdd(&a.ctr[((u64)threadIdx.x * SH + shard) * 8], (u64)c);
         }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < EPT; ++j)
-            if (own[j] != 0xFFFFFFFFu)
-                a.send[((u64)own[j] * SH + shard) * a.block + lbase[own[j]] + rk[j]] = tgt[j];
         __syncthreads();
     }
 }
 
-// Pack the send regions owner-major: packed = [owner 0 | owner 1 | ...], shards
-// in order inside an owner; stat[8 + o] = ids for owner o.
-__global__ __launch_bounds__(TB) void part_pack_k(PartArgs a, u32* __restrict__ packed) {
-    __shared__ u64 pre[MAXW * SH + 1];
-    const int ns = a.world * SH;
-    if (threadIdx.x == 0) {
-        u64 s = 0;
-        for (int i = 0; i < ns; ++i) {
-            pre[i] = s;
-            s += a.ctr[(u64)i * 8];
+// Per-owner counts of the level's remote claims: stat[8 + o] = sum of o's shards;
+// the shards and the pack cursors are cleared for the next level (one block).
+__global__ void part_counts_k(PartArgs a) {
+    for (int o = threadIdx.x; o < a.world; o += blockDim.x) {
+        u64 c = 0;
+        for (int sh = 0; sh < SH; ++sh) {
+            c += a.ctr[((u64)o * SH + sh) * 8];
+            a.ctr[((u64)o * SH + sh) * 8] = 0;
         }
-        pre[ns] = s;
-        if (blockIdx.x == 0)
-            for (int o = 0; o < a.world; ++o) a.stat[8 + o] = pre[(o + 1) * SH] - pre[o * SH];
+        a.stat[8 + o] = c;
+        a.cur[(u64)o * 8] = 0;
     }
-    __syncthreads();
-    const u64 T = pre[ns];
-    for (u64 i = (u64)blockIdx.x * TB + threadIdx.x; i < T; i += (u64)gridDim.x * TB) {
-        int lo = 0, hi = ns - 1;  // last segment with pre[seg] <= i
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (pre[mid] <= i) lo = mid;
-            else hi = mid - 1;
+}
+
+// Pack: the `sent` bits of every remote slice become the owner-major id list
+// packed = [owner 0 | owner 1 | ...] (owner offsets from stat[8 ..]); a wave takes 64
+// words of one owner's slice, places its ids with one cursor atomic and clears the
+// words. (Order inside an owner's segment is free: the owner settles ids in any order.)
+__global__ __launch_bounds__(TB) void part_pack_k(PartArgs a, u32* __restrict__ packed) {
+    const int lane = lane_id();
+    const i64 cpo = (a.bw + 63) / 64;  // chunks per owner slice
+    const i64 nch = cpo * a.world;
+    for (i64 c = (i64)blockIdx.x * NW + wave_id(); c < nch; c += (i64)gridDim.x * NW) {
+        const int o = (int)(c / cpo);
+        if (o == a.rank) continue;  // (wave-uniform)
+        const i64 wi = (c - (i64)o * cpo) * 64 + lane;
+        u64 bits = 0;
+        if (wi < a.bw) {
+            bits = a.sent[(i64)o * a.bw + wi];
+            if (bits) a.sent[(i64)o * a.bw + wi] = 0;
         }
-        packed[i] = a.send[(u64)lo * a.block + (i - pre[lo])];
+        const u32 cnt = (u32)__popcll(bits);
+        const u32 incl = wave_incl_scan(cnt);
+        const u32 tot = __shfl(incl, 63, 64);
+        if (!tot) continue;
+        u64 base = 0;
+        if (lane == 63) base = atomicAdd(&a.cur[(u64)o * 8], (u64)tot);
+        base = __shfl(base, 63, 64);
+        u64 off = 0;  // owner o's segment start
+        for (int q = 0; q < o; ++q) off += a.stat[8 + q];
+        u64 p = off + base + incl - cnt;
+        const u64 w0 = ((u64)((i64)o * a.bw + wi)) << 6;
+        while (bits) {
+            const int b = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            packed[p++] = (u32)(w0 + (u64)b);
+        }
     }
 }
 
@@ -497,11 +517,12 @@ struct Part {
     DevBuf<u32> row32, crow32, col, ccol;
     DevBuf<u64> row64, crow64;
     DevBuf<int32_t> dist;
-    DevBuf<u64> zmask, fr, frn, qoff, ctr, stat;
-    DevBuf<u32> q, qdeg, send;
+    DevBuf<u64> zmask, fr, frn, qoff, ctr, cur, stat, sent;
+    DevBuf<u32> q, qdeg;
     PinnedBuf<u64> hstat;
     ScanWs scan;
     u64 nq = 0, mq = 0;  // push queue of the current frontier (host copy from end_level)
+    i64 exch_bytes = 0;  // the engine view's send + recv buffers (sized to the largest level)
     int32_t level = 0;
     std::unique_ptr<BfsSteps> steps;  // engine view with its own exchange buffers (lazy)
     const Comm* iso_comm = nullptr;   // transport the replicated isolated mask was gathered over
@@ -544,8 +565,9 @@ PartArgs part_args(Part& p, u64* vis) {
     a.q = p.q.p;
     a.qdeg = p.qdeg.p;
     a.qoff = p.qoff.p;
-    a.send = p.send.p;
+    a.sent = p.sent.p;
     a.ctr = p.ctr.p;
+    a.cur = p.cur.p;
     a.stat = p.stat.p;
     return a;
 }
@@ -624,8 +646,13 @@ void build_part(Part& p, const S& src, i64 items, bool symmetric) {
     p.q.alloc((size_t)std::max<i64>(p.nl, 1));
     p.qdeg.alloc((size_t)std::max<i64>(p.nl, 1));
     p.qoff.alloc((size_t)std::max<i64>(p.nl, 1) + 1);
-    if (p.world > 1) p.send.alloc((size_t)p.world * SH * (size_t)p.block);
+    if (p.world > 1) {
+        p.sent.alloc((size_t)p.world * (size_t)p.bw);
+        PJ_HIP(hipMemsetAsync(p.sent.p, 0, p.sent.bytes(), s));
+    }
     p.ctr.alloc((size_t)p.world * SH * 8);
+    p.cur.alloc((size_t)p.world * 8);
+    PJ_HIP(hipMemsetAsync(p.cur.p, 0, p.cur.bytes(), s));
     p.stat.alloc(64);
     p.hstat.alloc(64);
     p.scan.ensure(std::max<i64>(p.nl, 1));
@@ -698,6 +725,14 @@ void part_info(const Part& p, i64* out) {
     out[8] = p.rank;
     out[9] = p.world;
     out[10] = p.nnz_in_local;
+    // device bytes of this rank: owned rows; O(N/P) vertex state; the N-bit bitmaps
+    // (sent, and the engine view's replicated vis / iso); the exchange buffers
+    out[11] = (i64)(p.row32.bytes() + p.row64.bytes() + p.col.bytes() + p.crow32.bytes() + p.crow64.bytes() +
+                    p.ccol.bytes());
+    out[12] = (i64)(p.dist.bytes() + p.zmask.bytes() + p.fr.bytes() + p.frn.bytes() + p.q.bytes() + p.qdeg.bytes() +
+                    p.qoff.bytes() + p.ctr.bytes() + p.cur.bytes() + p.stat.bytes());
+    out[13] = (i64)p.sent.bytes() + (p.steps ? 2 * (i64)p.world * p.bw * 8 + p.bw * 8 : 0);
+    out[14] = p.exch_bytes;
 }
 
 void part_zmask(Part& p, u64* out_dev) {
@@ -748,6 +783,16 @@ void part_begin(Part& p, i64 source, const u64* iso, u64* vis, i64* out3) {
     part_end_level(p, vis, out3);
 }
 
+// The level's remote claims (marked in `sent` by the push) as the owner-major id list;
+// packed holds at least the sum of the level's counts.
+void part_pack(Part& p, u64* vis, u32* packed) {
+    if (p.world < 2) return;
+    PartArgs a = part_args(p, vis);
+    const i64 nch = (p.bw + 63) / 64 * p.world;
+    part_pack_k<<<grid_for(nch, NW, (unsigned)p.ctx->cu_count * 8), TB, 0, p.ctx->stream>>>(a, packed);
+    PJ_LAUNCH_CHECK();
+}
+
 namespace {
 template <typename Off>
 void push_impl(Part& p, int level, u64* vis, u32* packed, i64* counts) {
@@ -763,9 +808,9 @@ void push_impl(Part& p, int level, u64* vis, u32* packed, i64* counts) {
         part_push_k<Off><<<grid, TB, 0, s>>>(a, part_d<Off>(p), p.nq, p.mq, level + 1);
         PJ_LAUNCH_CHECK();
     }
-    part_pack_k<<<(unsigned)p.ctx->cu_count * 4, TB, 0, s>>>(a, packed);
+    part_counts_k<<<1, 64, 0, s>>>(a);
     PJ_LAUNCH_CHECK();
-    PJ_HIP(hipMemsetAsync(p.ctr.p, 0, p.ctr.bytes(), s));
+    if (packed) part_pack(p, vis, packed);
     if (!counts) return;  // device rows: the transport reads stat[8 ..] itself
     PJ_HIP(hipMemcpyAsync(p.hstat.p + 8, p.stat.p + 8, sizeof(u64) * (size_t)p.world, hipMemcpyDeviceToHost, s));
     PJ_HIP(hipStreamSynchronize(s));
@@ -819,6 +864,9 @@ const int32_t* part_dist_device(const Part& p) { return p.dist.p; }
 // ------------------------------------------------------------ engine view ---
 namespace {
 
+// The exchange buffers are sized to the traffic: the level's counts are known (on the
+// host) before the exchange, so exchange_buffers grows send / recv to the largest level
+// seen so far and packs the claimed ids into send.
 struct PartGpuSteps final : BfsSteps {
     Part& p;
     DevBuf<u64> vis_b, iso_b, zown_b;
@@ -833,9 +881,8 @@ struct PartGpuSteps final : BfsSteps {
         vis_b.alloc((size_t)world * (size_t)bw);
         iso_b.alloc((size_t)world * (size_t)bw);
         zown_b.alloc((size_t)bw);
-        const size_t cap = world > 1 ? (size_t)world * (size_t)block : 1;
-        send_b.alloc(cap);
-        recv_b.alloc(cap);
+        send_b.alloc(1);
+        recv_b.alloc(1);
         vis = vis_b.p;
         iso = iso_b.p;
         zown = zown_b.p;
@@ -845,7 +892,19 @@ struct PartGpuSteps final : BfsSteps {
     hipStream_t stream() override { return p.ctx->stream; }
     void zmask() override { part_zmask(p, zown_b.p); }
     void begin(i64 source, i64* st3) override { part_begin(p, source, iso_b.p, vis_b.p, st3); }
-    void push(int level, i64* counts) override { part_push(p, level, vis_b.p, send_b.p, counts); }
+    void push(int level, i64* counts) override { part_push(p, level, vis_b.p, nullptr, counts); }
+    void exchange_buffers(i64 nsend, i64 nrecv) override {
+        if ((size_t)nsend > send_b.n) {
+            send_b.ensure((size_t)nsend + (size_t)nsend / 4);
+            send = send_b.p;
+        }
+        if ((size_t)nrecv > recv_b.n) {
+            recv_b.ensure((size_t)nrecv + (size_t)nrecv / 4);
+            recv = recv_b.p;
+        }
+        p.exch_bytes = (i64)(send_b.bytes() + recv_b.bytes());
+        part_pack(p, vis_b.p, send_b.p);
+    }
     void apply(int level, i64 nr) override { part_apply(p, level, vis_b.p, recv_b.p, nr); }
     void pull(int level) override { part_pull(p, level, vis_b.p); }
     void end_level(i64* st3) override { part_end_level(p, vis_b.p, st3); }

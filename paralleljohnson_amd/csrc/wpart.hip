@@ -16,8 +16,10 @@
 //                        target is lowered with atomicMin and joins the next
 //                        frontier when it lands below hi; a remote target's
 //                        candidate is folded into a full-size `cand` array
-//                        (atomicMin) and its `touched` bit set. pack: every
-//                        touched remote target once, as (id, cand) owner-major —
+//                        (atomicMin) and its `touched` bit set. count: touched
+//                        remote targets per owner; pack (into a send buffer sized
+//                        to that count): every touched remote target once, as
+//                        (id, cand) owner-major —
 //                        the per-owner send buffers of :537-542 — exchanged with
 //                        all_to_all_single (:522-554); apply: the owner folds the
 //                        received candidates in the same way. A round ends with
@@ -61,7 +63,8 @@ constexpr int ST_NF = 65;      // vertices marked in the next frontier
 constexpr int ST_MIN = 66;     // min owned dist >= lo (select)
 constexpr int ST_CNT = 67;     // selected frontier size
 constexpr int ST_REACH = 68;   // reached vertices, [69] their out-edges
-constexpr int ST_N = 72;
+constexpr int ST_CUR = 72;     // [72, 72 + 64): pack cursors per owner
+constexpr int ST_N = 72 + WP_MAXW;
 
 struct WArgs {
     i64 n, lo, nl, block, bw;
@@ -339,11 +342,31 @@ __global__ __launch_bounds__(WB) void wp_long_k(WArgs a) {
     if (LIGHT) wp_flush_nf(a, nf, red);
 }
 
-// Touched remote targets -> (id | cand << 32) in the owner's region of `reg`
-// (region o at o * block; one entry per distinct target, so no region
-// overflows). Bits are cleared as read. A lane owns one touched word (64 ids
-// of one owner); per-owner counts are wave-aggregated.
-__global__ __launch_bounds__(WB) void wp_pack_k(WArgs a, i64 nwords, u64* __restrict__ reg) {
+// Touched remote targets per owner -> stat[o] (wave-aggregated: one atomic per
+// (wave, owner)). A lane owns one touched word (64 ids of one owner).
+__global__ __launch_bounds__(WB) void wp_count_k(WArgs a, i64 nwords) {
+    const int lane = lane_id();
+    const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
+    for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; w0 < nwords; w0 += nwaves * 64) {
+        const i64 wi = w0 + lane;
+        const u32 cnt = wi < nwords ? (u32)__popcll(a.touched[wi]) : 0u;
+        const int owner = wi < nwords ? (int)((wi * 64) / a.block) : -1;
+        u64 pending = __ballot(cnt != 0);
+        while (pending) {
+            const int l = __ffsll((long long)pending) - 1;
+            const int o = __shfl(owner, l, 64);
+            const bool mine = cnt != 0 && owner == o;
+            pending &= ~__ballot(mine);
+            const u32 tot = wave_sum(mine ? cnt : 0u);
+            if (lane == l) atomicAdd(&a.stat[o], (u64)tot);
+        }
+    }
+}
+
+// Pack: touched remote targets -> (id | cand << 32) at their owner's segment of send
+// (segments owner-major, sizes stat[o] from wp_count_k; a cursor per owner). Bits are
+// cleared as read.
+__global__ __launch_bounds__(WB) void wp_pack_k(WArgs a, i64 nwords, int world, u64* __restrict__ send) {
     const int lane = lane_id();
     const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
     for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; w0 < nwords; w0 += nwaves * 64) {
@@ -367,11 +390,14 @@ __global__ __launch_bounds__(WB) void wp_pack_k(WArgs a, i64 nwords, u64* __rest
             const u32 inc = wave_incl_scan(x);
             const u32 tot = __shfl(inc, 63, 64);
             u64 ob = 0;
-            if (lane == l) ob = atomicAdd(&a.stat[o], (u64)tot);
+            if (lane == l) {
+                ob = atomicAdd(&a.stat[ST_CUR + o], (u64)tot);
+                for (int q = 0; q < o && q < world; ++q) ob += a.stat[q];
+            }
             ob = __shfl(ob, l, 64);
             if (mine) base = ob + (inc - x);
         }
-        u64* out = cnt ? reg + (i64)owner * a.block + base : nullptr;
+        u64* out = cnt ? send + base : nullptr;
         while (bits) {
             const int bb = __ffsll((long long)bits) - 1;
             bits &= bits - 1;
@@ -692,7 +718,8 @@ struct WPart {
     DevBuf<u32> lsplit_alt;        // the other light threshold's prefixes (delta and the tail's are
                                    // used in turn by every solve: each was recomputed per solve)
     DevBuf<int32_t> dist, cand;
-    DevBuf<u64> touched, fr, frn, mb, reg, stat;
+    DevBuf<u64> touched, fr, frn, mb, stat;
+    i64 exch_bytes = 0;  // the engine view's send + recv buffers (sized to the largest round)
     DevBuf<u32> lq_v;
     DevBuf<u64> lq_b, lq_e;
     std::vector<u64> hstat;
@@ -814,7 +841,6 @@ void wpart_cut(WPart* p, const Graph& g, i64 first, double mean_w) {
     if (p->world > 1) {
         p->cand.alloc((size_t)std::max<i64>(p->n, 1));
         p->touched.alloc((size_t)std::max<i64>((p->n + 63) / 64, 1));
-        p->reg.alloc((size_t)p->world * (size_t)p->block);
         PJ_HIP(hipMemsetAsync(p->touched.p, 0, p->touched.bytes(), s));
     }
     PJ_HIP(hipStreamSynchronize(s));
@@ -908,6 +934,17 @@ void wpart_info(const WPart& p, i64* out) {
     out[5] = p.world;
     out[6] = p.rank;
     out[7] = p.nnz;
+}
+
+// device bytes of this rank: rows, O(block) vertex state, the N-sized tables (the remote
+// candidates `cand` (int32 per vertex) with their touched bitmap, and the pull rounds'
+// replicated byte map), the exchange buffers (sized to the largest round's traffic)
+void wpart_device_bytes(const WPart& p, i64* out4) {
+    out4[0] = (i64)(p.row.bytes() + p.col.bytes() + p.w.bytes());
+    out4[1] = (i64)(p.lsplit.bytes() + p.lsplit_alt.bytes() + p.dist.bytes() + p.fr.bytes() + p.frn.bytes() +
+                    p.mb.bytes() + p.lq_v.bytes() + p.lq_b.bytes() + p.lq_e.bytes() + p.stat.bytes());
+    out4[2] = (i64)(p.cand.bytes() + p.touched.bytes() + p.mmap.bytes());
+    out4[3] = p.exch_bytes;
 }
 
 void wpart_heavy_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
@@ -1040,6 +1077,10 @@ void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2) {
     out2[1] = p.hstat[ST_MIN] >= (u64)INT_INF ? (i64)INT_INF : (i64)p.hstat[ST_MIN];
 }
 
+// Relax the frontier's light (or the members' heavy) edges; counts[o] = the distinct
+// remote targets improved for owner o. send != NULL (room for their sum; world x block
+// always suffices) also packs them (wpart_pack); else the caller packs once it has
+// sized its buffer.
 void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts) {
     hipStream_t s = p.ctx->stream;
     p.clear_stat();
@@ -1051,21 +1092,20 @@ void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* co
     else wp_long_k<false><<<p.grid(), WB, 0, s>>>(a);
     PJ_LAUNCH_CHECK();
     if (p.world > 1) {
-        const i64 nwords = (p.n + 63) / 64;
-        wp_pack_k<<<p.grid(), WB, 0, s>>>(a, nwords, p.reg.p);
+        wp_count_k<<<p.grid(), WB, 0, s>>>(a, (p.n + 63) / 64);
         PJ_LAUNCH_CHECK();
     }
     p.read_stat();
-    u64 off = 0;
-    for (int o = 0; o < p.world; ++o) {
-        const u64 c = p.world > 1 ? p.hstat[o] : 0;
-        counts[o] = (i64)c;
-        if (c) {
-            PJ_HIP(hipMemcpyAsync(send + off, p.reg.p + (size_t)o * (size_t)p.block, sizeof(u64) * c,
-                                  hipMemcpyDeviceToDevice, s));
-            off += c;
-        }
-    }
+    for (int o = 0; o < p.world; ++o) counts[o] = p.world > 1 ? (i64)p.hstat[o] : 0;
+    if (send) wpart_pack(p, send);
+}
+
+// The touched remote targets as (id | cand << 32), owner-major, into send.
+void wpart_pack(WPart& p, u64* send) {
+    if (p.world < 2) return;
+    hipStream_t s = p.ctx->stream;
+    wp_pack_k<<<p.grid(), WB, 0, s>>>(p.args(), (p.n + 63) / 64, p.world, send);
+    PJ_LAUNCH_CHECK();
     PJ_HIP(hipStreamSynchronize(s));
 }
 
@@ -1109,6 +1149,9 @@ void wpart_copy_dist(WPart& p, int32_t* host) {
 // ------------------------------------------------------------ engine view ---
 namespace {
 
+// The exchange buffers follow the traffic: relax leaves the improved remote targets in
+// `touched` and their per-owner counts on the host; exchange_buffers grows send / recv
+// to the largest round seen so far and packs.
 struct WPartGpuSteps final : DeltaSteps {
     WPart& p;
     DevBuf<u64> send_b, recv_b;
@@ -1116,17 +1159,28 @@ struct WPartGpuSteps final : DeltaSteps {
         n = p.n;
         rank = p.rank;
         world = p.world;
-        const size_t cap = world > 1 ? (size_t)world * (size_t)p.block : 1;
-        send_b.alloc(cap);
-        recv_b.alloc(cap);
+        send_b.alloc(1);
+        recv_b.alloc(1);
         send = send_b.p;
         recv = recv_b.p;
+    }
+    void exchange_buffers(i64 nsend, i64 nrecv) override {
+        if ((size_t)nsend > send_b.n) {
+            send_b.ensure((size_t)nsend + (size_t)nsend / 4);
+            send = send_b.p;
+        }
+        if ((size_t)nrecv > recv_b.n) {
+            recv_b.ensure((size_t)nrecv + (size_t)nrecv / 4);
+            recv = recv_b.p;
+        }
+        p.exch_bytes = (i64)(send_b.bytes() + recv_b.bytes());
+        wpart_pack(p, send_b.p);
     }
     hipStream_t stream() override { return p.ctx->stream; }
     int32_t begin(i64 source, int32_t delta) override { return wpart_begin(p, source, delta); }
     void select(int32_t lo, int32_t hi, i64* out2) override { wpart_select(p, lo, hi, out2); }
     void relax(int light, int32_t lo, int32_t hi, i64* counts) override {
-        wpart_relax(p, light, lo, hi, send_b.p, counts);
+        wpart_relax(p, light, lo, hi, nullptr, counts);
     }
     void apply(i64 nr, int light, int32_t lo, int32_t hi) override { wpart_apply(p, recv_b.p, nr, light, lo, hi); }
     i64 end_round() override { return wpart_end_round(p); }

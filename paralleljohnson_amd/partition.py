@@ -41,7 +41,8 @@ _PI64 = ctypes.POINTER(ctypes.c_int64)
 class PartInfo(ctypes.Structure):
     _fields_ = [("n", _I64), ("lo", _I64), ("hi", _I64), ("block", _I64), ("words_per_rank", _I64),
                 ("nnz_local", _I64), ("nnz_in_local", _I64), ("rank", _I32),
-                ("world", _I32), ("symmetric", _I32), ("off64", _I32)]
+                ("world", _I32), ("symmetric", _I32), ("off64", _I32), ("bytes_rows", _I64),
+                ("bytes_state", _I64), ("bytes_bitmaps", _I64), ("bytes_exchange", _I64)]
 
 
 class PartStats(ctypes.Structure):
@@ -216,6 +217,14 @@ class DevicePart:
         self.nnz_local, self.symmetric = info.nnz_local, bool(info.symmetric)
         self.nl = self.hi - self.lo
 
+    def device_bytes(self) -> dict:
+        """pj_part_info_get's per-rank device bytes (rows, vertex state, N-bit bitmaps,
+        exchange buffers sized to the largest level's traffic)."""
+        info = PartInfo()
+        _check(_lib.pj_part_info_get(self._h, ctypes.byref(info)))
+        return {"rows": info.bytes_rows, "state": info.bytes_state, "bitmaps": info.bytes_bitmaps,
+                "exchange": info.bytes_exchange}
+
     def set_option(self, key: str, value: float):
         _check(_lib.pj_part_set_option(self._h, key.encode(), float(value)))
 
@@ -292,6 +301,12 @@ class DeviceWPart:
         _check(_lib.pj_wpart_info(self._h, info))
         self.n, self.lo, self.hi, self.block, self.nnz_local, self.world, self.rank, self.nnz = list(info)
         self.nl = self.hi - self.lo
+
+    def device_bytes(self) -> dict:
+        """pj_wpart_device_bytes: rows, vertex state, N-sized tables, exchange buffers."""
+        out = np.zeros(4, np.int64)
+        _check(_lib.pj_wpart_device_bytes(self._h, _ptr(out)))
+        return {"rows": int(out[0]), "state": int(out[1]), "tables": int(out[2]), "exchange": int(out[3])}
 
     def set_option(self, key: str, value: float):
         """pj_wpart_set_option: "tail_frac", "tail_mult", "pull_factor" or "light_pull".

@@ -468,9 +468,10 @@ def test_weighted_kronecker_s26_full_size(ctx):
 
 def test_partitioned_bfs_s28_full_size(ctx, pj):
     """BASELINE.json configs[3] at full size: Kronecker s28 (2^33 entries, 64-bit row
-    offsets), 1D vertex partition at world 1 (no exchange), and at world 2 and 4 with
+    offsets), 1D vertex partition at world 1 (no exchange), and at world 2, 4 and 8 with
     every rank on the one GPU over the host transport (each rank builds only its own
-    rows; per level: owner-packed send regions, the count exchange, the alltoallv of ids
+    rows; per level: the claimed remote ids packed owner-major into traffic-sized
+    buffers, the count exchange, the alltoallv of ids
     (the reference's :522-554, buffers sized at :495-501), the visited all-gather around
     pull levels and the termination allreduce :589-590). Every world must give the same
     gathered distances, which are proven exact by the certificate against the CSR of the
@@ -493,11 +494,13 @@ def test_partitioned_bfs_s28_full_size(ctx, pj):
     ops.close()
     comm.close()
     torch.cuda.empty_cache()
-    for world in (2, 4):
+    mem = {}
+    for world in (2, 4, 8):
         ctxs = [pj.Context(0) for _ in range(world)]
         comms = Comm.group(ctxs, "host")
         parts = [load_kronecker(ctxs[r], 28, 16, 1, r, world) for r in range(world)]
         assert sum(p.nnz_local for p in parts) == 1 << 33
+        sent = [0] * world
         for r in roots:
             st = bfs_group(parts, comms, r)
             assert len({(x["levels"], x["td_levels"], x["bu_levels"]) for x in st}) == 1  # same loop on every rank
@@ -505,6 +508,15 @@ def test_partitioned_bfs_s28_full_size(ctx, pj):
             assert st[0]["reached"] == int((dists[r] < INF).sum()), (world, r)
             got = gather_group(parts, comms)
             assert np.array_equal(got, dists[r]), (world, r)
+            sent = [max(a, x["sent"]) for a, x in zip(sent, st)]
+        # per-rank device bytes: the exchange buffers follow the traffic (at most the ids one
+        # BFS sends / receives, x1.25 growth slack, x2 for send + recv), no longer world x block
+        # sized regions (round 3: 40 N bytes per rank at every world)
+        b = [p.device_bytes() for p in parts]
+        mem[world] = {k: max(x[k] for x in b) for k in b[0]}
+        n = 1 << 28
+        assert mem[world]["exchange"] <= 2 * 1.25 * 4 * max(sent) * world + 64, (world, mem[world], sent)
+        assert mem[world]["exchange"] < 40 * n / 16, (world, mem[world])
         for p in parts:
             p.close()
         for c in comms:
@@ -512,6 +524,11 @@ def test_partitioned_bfs_s28_full_size(ctx, pj):
         for c in ctxs:
             c.close()
         torch.cuda.empty_cache()
+    # rows and vertex state shrink with the world size; the N-bit bitmaps stay
+    assert mem[8]["rows"] < mem[2]["rows"] / 3 and mem[8]["state"] < mem[2]["state"] / 3, mem
+    assert mem[8]["exchange"] <= mem[2]["exchange"], mem
+    total = {w: sum(m.values()) for w, m in mem.items()}
+    assert total[8] < total[4] < total[2], mem
     g = ctx.generate_kronecker(28, 16, 1)
     assert g.nnz == 1 << 33
     row, col, _ = g.get_csr()
@@ -526,7 +543,7 @@ def test_partitioned_weighted_s22_world2(ctx, pj):
     """The weighted 1D partition (wpart.hip + the C++ band loop) on the full Kronecker s22
     with weights 1..255 at world 2 (ranks sharing the GPU over the host transport):
     gathered distances equal the single-GPU delta-stepping solver's and are proven exact
-    by the certificate; the remote-candidate exchange ran."""
+    by the certificate; the remote-candidate exchange ran, in buffers sized to its traffic."""
     import torch
     from helpers import sssp_certificate
     from paralleljohnson_amd.partition import Comm, delta_group, gather_group, load_weighted
@@ -536,6 +553,7 @@ def test_partitioned_weighted_s22_world2(ctx, pj):
     gs = [c.generate_kronecker(22, 16, 1, weighted=True) for c in ctxs]
     parts = [load_weighted(ctxs[r], gs[r], r, world) for r in range(world)]
     roots = [int(r) for r in gs[0].sample_roots(2, 2)]
+    sent = 0
     for r in roots:
         st = delta_group(parts, comms, r)
         assert sum(x["sent"] for x in st) > 0
@@ -544,6 +562,13 @@ def test_partitioned_weighted_s22_world2(ctx, pj):
         exp = gs[0].sssp(r)
         assert np.array_equal(got, exp), r
         assert st[0]["reached"] == int((exp < INF).sum())
+        sent = max(sent, max(x["sent"] for x in st))
+    # the (id, candidate) exchange buffers follow the traffic (at most a solve's pairs, x1.25
+    # growth slack, send + recv), not world x block regions (round 3: 24 N bytes per rank)
+    for p in parts:
+        b = p.device_bytes()
+        assert 0 < b["exchange"] <= 2 * 1.25 * 8 * sent * world + 64, (b, sent)
+        assert b["exchange"] < 24 * (1 << 22) / 4, b
     row, col, w = gs[0].get_csr()
     for p in parts:
         p.close()
