@@ -250,6 +250,7 @@ def run_partitioned_host(args, world_h=2, nroots=4):
             "levels_td_bu": [st0[0]["td_levels"], st0[0]["bu_levels"]],
             "ids_sent_per_bfs_by_rank": [x["sent"] for x in st0],
             "nnz_local_by_rank": [p.nnz_local for p in parts],
+            "device_bytes_by_rank": [p.device_bytes() for p in parts],
             "build_s": round(build_s, 2),
         }
     finally:
@@ -340,18 +341,17 @@ def run_wpartitioned_host(args, world_h=2, nroots=3, scale=26):
     copies + host barriers; not xGMI/RCCL): the reference's only mode (:344-594) for a graph
     split over ranks, timed per solve."""
     import paralleljohnson_amd as pj
-    from paralleljohnson_amd.partition import Comm, delta_group, load_weighted
+    from paralleljohnson_amd.partition import Comm, delta_group, load_weighted_kronecker
     ctxs = [pj.Context(0) for _ in range(world_h)]
     comms = Comm.group(ctxs, "host")
     parts, roots = [], None
-    t0 = time.perf_counter()
     try:
-        for r in range(world_h):  # each rank cuts its block from the graph generated on its context
-            g = ctxs[r].generate_kronecker(scale, args.edgefactor, args.seed, weighted=True)
-            if roots is None:
-                roots = [int(x) for x in g.sample_roots(args.seed + 1, nroots)]
-            parts.append(load_weighted(ctxs[r], g, r, world_h))
-            g.close()
+        g = ctxs[0].generate_kronecker(scale, args.edgefactor, args.seed, weighted=True)  # (the bench's roots)
+        roots = [int(x) for x in g.sample_roots(args.seed + 1, nroots)]
+        g.close()
+        t0 = time.perf_counter()
+        for r in range(world_h):  # each rank generates only its block's rows (pj_wpart_generate_kronecker)
+            parts.append(load_weighted_kronecker(ctxs[r], scale, args.edgefactor, args.seed, r, world_h))
         build_s = time.perf_counter() - t0
         delta_group(parts, comms, roots[0])  # warm-up (workspace)
         sts = []
@@ -368,7 +368,9 @@ def run_wpartitioned_host(args, world_h=2, nroots=3, scale=26):
             "gteps": round(m / elapsed / 1e9, 3), "bands": st0[0]["bands"], "light_rounds": st0[0]["rounds"],
             "heavy_pulls": st0[0]["heavy_pulls"], "light_pulls": st0[0]["bu_levels"],
             "solve_ms_max_rank": [round(max(x["solve_ms"] for x in st), 2) for st in sts],
-            "pairs_sent_per_sssp_by_rank": [x["sent"] for x in st0], "build_s": round(build_s, 2),
+            "pairs_sent_per_sssp_by_rank": [x["sent"] for x in st0],
+            "build_s": round(build_s, 2), "build": "per block (pj_wpart_generate_kronecker)",
+            "device_bytes_by_rank": [p.device_bytes() for p in parts],
         }
     finally:
         for p in parts:

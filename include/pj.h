@@ -354,6 +354,13 @@ int pj_wpart_from_graph(pj_graph* g, int rank, int world, pj_wpart** out);
  * pj_load_snap grammar): every rank parses the file on its GPU and keeps only
  * its block's rows, weight-sorted (no whole-graph CSR on any GPU). */
 int pj_wpart_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_wpart** out);
+/* The rank's block of pj_generate_kronecker(scale, edgefactor, seed, weighted = 1):
+ * every rank enumerates the generator's tuples on its GPU and keeps only its block's
+ * rows (weight-sorted, the same rows as the single-GPU graph's), so the weighted
+ * graph never has to fit whole on one device (the reference's split graph,
+ * :344-410). The automatic delta uses the whole graph's mean weight on every rank. */
+int pj_wpart_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int rank, int world,
+                                pj_wpart** out);
 int pj_wpart_destroy(pj_wpart* p);
 /* out[8] = (n, lo, hi, block, nnz_local, world, rank, nnz of the whole graph) */
 int pj_wpart_info(const pj_wpart* p, int64_t* out);

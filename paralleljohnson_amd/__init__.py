@@ -133,6 +133,7 @@ _SIGS = {
     "pj_wpart_destroy": ([_P], _INT),
     "pj_wpart_info": ([_P, _P], _INT),
     "pj_wpart_device_bytes": ([_P, _P], _INT),
+    "pj_wpart_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _INT, _PP], _INT),
     "pj_wpart_begin": ([_P, _I64, ctypes.c_int32, _P], _INT),
     "pj_wpart_select": ([_P, ctypes.c_int32, ctypes.c_int32, _P], _INT),
     "pj_wpart_relax": ([_P, _INT, ctypes.c_int32, ctypes.c_int32, _P, _P], _INT),

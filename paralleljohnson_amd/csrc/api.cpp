@@ -1150,6 +1150,20 @@ int pj_wpart_from_graph(pj_graph* g, int rank, int world, pj_wpart** out) {
     });
 }
 
+int pj_wpart_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t seed, int rank, int world,
+                                pj_wpart** out) {
+    if (!ctx || !out || scale < 0 || scale > 31 || edgefactor < 1 || edgefactor > 1024)
+        return arg_error("pj_wpart_generate_kronecker: scale must be in [0,31], edgefactor in [1,1024]");
+    if (world < 1 || world > 64 || rank < 0 || rank >= world)
+        return arg_error("pj_wpart_generate_kronecker: need 0 <= rank < world <= 64");
+    *out = nullptr;
+    return guarded([&] {
+        bind(ctx->c);
+        *out = reinterpret_cast<pj_wpart*>(wpart_from_kronecker(ctx->c, scale, edgefactor, seed, rank, world));
+        return (int)PJ_OK;
+    });
+}
+
 int pj_wpart_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_wpart** out) {
     if (!ctx || !path || !out) return arg_error("pj_wpart_load_snap: bad argument");
     if (world < 1 || world > 64 || rank < 0 || rank >= world)

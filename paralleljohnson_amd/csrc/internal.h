@@ -302,6 +302,7 @@ void debug_bitmaps(Graph& g, u64* vis0, u64* vis1, u64* fnew);
 struct WPart;
 void delete_wpart(WPart* p);
 WPart* wpart_from_graph(Graph& g, int rank, int world);
+WPart* wpart_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, int rank, int world);
 WPart* wpart_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w, i64 nnz, i64 n, int rank,
                       int world);
 void wpart_info(const WPart& p, i64* out8);

@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <cmath>
 
+#include "kron.h"
 #include "lb.h"
 #include "engine.h"
 
@@ -875,7 +876,107 @@ __global__ void wp_filter_write_k(const u32* __restrict__ src, const u32* __rest
     }
 }
 
+// Per-block weighted Kronecker build: every rank enumerates the tuples of the
+// generator spec (kron.h, both directions, the tuple's weight on each), keeps the
+// entries whose source lies in its block, in enumeration order (= the single-GPU
+// generator's file order, so the rows sort to the same weight-sorted rows), and sums
+// every entry's weight for the whole graph's mean (each rank sees all tuples, so every
+// rank derives the same automatic delta). 2048 tuples per block.
+constexpr int WK_IPT = 8;
+__global__ __launch_bounds__(256) void wp_kron_count_k(int scale, u64 seed, PermKeys pk, u64 M, u32 lo, u32 hi,
+                                                       u32* __restrict__ bcnt, u64* __restrict__ wsum) {
+    __shared__ u64 red[4];
+    const u64 base = (u64)blockIdx.x * 256 * WK_IPT;
+    u32 c = 0;
+    u64 ws = 0;
+    for (int k = 0; k < WK_IPT; ++k) {
+        const u64 i = base + (u64)k * 256 + threadIdx.x;
+        if (i < M) {
+            u32 pu, pv;
+            kron_tuple(scale, seed, pk, i, pu, pv);
+            c += (pu >= lo && pu < hi) + (pv >= lo && pv < hi);
+            ws += 2ull * kron_weight(seed, i, true);
+        }
+    }
+    c = (u32)block_sum<4>((u64)c, red);
+    ws = block_sum<4>(ws, red);
+    if (threadIdx.x == 0) {
+        bcnt[blockIdx.x] = c;
+        atomicAdd(wsum, ws);
+    }
+}
+__global__ __launch_bounds__(256) void wp_kron_write_k(int scale, u64 seed, PermKeys pk, u64 M, u32 lo, u32 hi,
+                                                       const u64* __restrict__ boff, u32* __restrict__ os,
+                                                       u32* __restrict__ od, u32* __restrict__ ow) {
+    __shared__ u64 red[4];
+    const u64 b0 = (u64)blockIdx.x * 256 * WK_IPT;
+    u64 pos = boff[blockIdx.x];
+    for (int k = 0; k < WK_IPT; ++k) {
+        const u64 i = b0 + (u64)k * 256 + threadIdx.x;
+        u32 pu = 0, pv = 0, w = 0;
+        bool k0 = false, k1 = false;
+        if (i < M) {
+            kron_tuple(scale, seed, pk, i, pu, pv);
+            w = kron_weight(seed, i, true);
+            k0 = pu >= lo && pu < hi;  // entry 2i: pu -> pv
+            k1 = pv >= lo && pv < hi;  // entry 2i + 1: pv -> pu
+        }
+        u64 tot;
+        u64 p = pos + block_excl_scan<4>((u64)k0 + (u64)k1, red, tot);
+        if (k0) {
+            os[p] = pu - lo;
+            od[p] = pv;
+            ow[p] = w;
+            ++p;
+        }
+        if (k1) {
+            os[p] = pv - lo;
+            od[p] = pu;
+            ow[p] = w;
+        }
+        pos += tot;
+    }
+}
+
 }  // namespace
+
+WPart* wpart_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, int rank, int world) {
+    hipStream_t s = ctx.stream;
+    const u64 M = (u64)edgefactor << scale;
+    std::unique_ptr<WPart> p = wpart_geometry(&ctx, (i64)1 << scale, (i64)(2 * M), rank, world);
+    const PermKeys pk = make_perm_keys(scale, seed);
+    const i64 nb = (i64)((M + 256 * WK_IPT - 1) / (256 * WK_IPT));
+    i64 m = 0;
+    u64 wsum = 0;
+    DevBuf<u32> ls, ld, lw;
+    if (nb > 0) {
+        DevBuf<u32> bcnt((size_t)nb);
+        DevBuf<u64> boff((size_t)nb + 1), acc(1);
+        ScanWs ws;
+        PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
+        wp_kron_count_k<<<(unsigned)nb, 256, 0, s>>>(scale, seed, pk, M, (u32)p->lo, (u32)p->hi, bcnt.p, acc.p);
+        PJ_LAUNCH_CHECK();
+        exclusive_scan_u32(bcnt.p, boff.p, nb, ws, s);
+        u64 tot = 0;
+        PJ_HIP(hipMemcpyAsync(&tot, boff.p + nb, sizeof(u64), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipMemcpyAsync(&wsum, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+        m = (i64)tot;
+        ls.alloc((size_t)std::max<i64>(m, 1));
+        ld.alloc((size_t)std::max<i64>(m, 1));
+        lw.alloc((size_t)std::max<i64>(m, 1));
+        wp_kron_write_k<<<(unsigned)nb, 256, 0, s>>>(scale, seed, pk, M, (u32)p->lo, (u32)p->hi, boff.p, ls.p, ld.p,
+                                                     lw.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+    Graph local;  // the block's rows, local ids, global columns, weight-sorted
+    local.ctx = &ctx;
+    build_graph_from_coo(local, ls, ld, &lw, m, p->nl, false);
+    wpart_cut(p.get(), local, 0, M > 0 ? (double)wsum / (double)(2 * M) : 1.0);
+    p->symmetric = true;  // both directions of every tuple, same weight
+    return p.release();
+}
 
 WPart* wpart_from_graph(Graph& g, int rank, int world) {
     if (!g.weighted) throw Error(PJ_ERR_ARG, "pj_wpart_from_graph: the graph has no weights");

@@ -349,6 +349,15 @@ def load_weighted(ctx, graph, rank: int, world: int) -> DeviceWPart:
     return DeviceWPart(ctx, graph, rank, world)
 
 
+def load_weighted_kronecker(ctx, scale: int, edgefactor: int, seed: int, rank: int, world: int) -> DeviceWPart:
+    """The rank's block of the weighted Kronecker graph, generated per block on its GPU
+    (pj_wpart_generate_kronecker: no rank ever holds the whole graph)."""
+    h = ctypes.c_void_p()
+    _check(_lib.pj_wpart_generate_kronecker(ctx._h, int(scale), int(edgefactor), ctypes.c_uint64(seed), int(rank),
+                                            int(world), ctypes.byref(h)))
+    return DeviceWPart(ctx, None, rank, world, handle=h)
+
+
 def load_weighted_snap(ctx, path: str, rank: int, world: int) -> DeviceWPart:
     """The rank's block of a weighted SNAP file (pj_wpart_load_snap: only the block's rows are kept)."""
     h = ctypes.c_void_p()

@@ -541,17 +541,20 @@ def test_partitioned_bfs_s28_full_size(ctx, pj):
 
 def test_partitioned_weighted_s22_world2(ctx, pj):
     """The weighted 1D partition (wpart.hip + the C++ band loop) on the full Kronecker s22
-    with weights 1..255 at world 2 (ranks sharing the GPU over the host transport):
+    with weights 1..255 at world 2 (ranks sharing the GPU over the host transport), each
+    rank generating only its own block's rows:
     gathered distances equal the single-GPU delta-stepping solver's and are proven exact
     by the certificate; the remote-candidate exchange ran, in buffers sized to its traffic."""
     import torch
     from helpers import sssp_certificate
-    from paralleljohnson_amd.partition import Comm, delta_group, gather_group, load_weighted
+    from paralleljohnson_amd.partition import Comm, delta_group, gather_group, load_weighted_kronecker
     world = 2
     ctxs = [pj.Context(0) for _ in range(world)]
     comms = Comm.group(ctxs, "host")
-    gs = [c.generate_kronecker(22, 16, 1, weighted=True) for c in ctxs]
-    parts = [load_weighted(ctxs[r], gs[r], r, world) for r in range(world)]
+    gs = [ctxs[0].generate_kronecker(22, 16, 1, weighted=True)]  # (the single-GPU reference solve)
+    # each rank generates only its block's rows (pj_wpart_generate_kronecker)
+    parts = [load_weighted_kronecker(ctxs[r], 22, 16, 1, r, world) for r in range(world)]
+    assert sum(p.nnz_local for p in parts) == gs[0].nnz and all(p.nnz == gs[0].nnz for p in parts)
     roots = [int(r) for r in gs[0].sample_roots(2, 2)]
     sent = 0
     for r in roots:

@@ -374,6 +374,36 @@ def test_wpart_group(pj, oracle, world, transport):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_wpart_generate_kronecker_blocks(pj, oracle, world):
+    """pj_wpart_generate_kronecker: each rank enumerates the weighted generator and keeps its
+    block's rows only. The blocks' entry counts are the single-GPU CSR's row sums over the
+    block, every rank has the whole graph's nnz (the automatic delta's mean weight), and the
+    gathered distances equal the oracle Dijkstra on the single-GPU CSR; the exchange buffers
+    stay traffic-sized."""
+    from paralleljohnson_amd.partition import delta_group, gather_group, load_weighted_kronecker
+    ctxs, comms = _group(pj, world, "host")
+    for scale, ef, seed in ((10, 16, 5), (12, 8, 6)):
+        g0 = ctxs[0].generate_kronecker(scale, ef, seed, weighted=True)
+        row, col, wc = g0.get_csr()
+        col = col.view(np.uint32)
+        n = g0.n
+        g0.close()
+        parts = [load_weighted_kronecker(ctxs[r], scale, ef, seed, r, world) for r in range(world)]
+        for p in parts:
+            assert p.nnz == row[-1] and p.nnz_local == row[p.hi] - row[p.lo], (scale, p.rank)
+        for source in (0, n // 3, n - 1):
+            st = delta_group(parts, comms, source)
+            exp = oracle.dijkstra(row, col, wc, source)
+            assert np.array_equal(gather_group(parts, comms), exp), (scale, world, source)
+            assert st[0]["reached"] == int((exp < INF).sum())
+        for p in parts:
+            b = p.device_bytes()
+            assert b["rows"] > 0 and b["exchange"] < 8 * 2 * n, b
+            p.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("weighted", [False, True])
 def test_cli_processes_byte_identical(pj, oracle, tmp_path, weighted):
     """`parallel_johnson` at P = 1 (single-GPU solver), P = 2 and 3 (PJ_GPUS: the 1D partition
