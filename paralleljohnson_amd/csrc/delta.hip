@@ -297,29 +297,6 @@ __device__ __forceinline__ u64 v2_slot_sum(const V2Line* sl) {
     return t;
 }
 
-// one relaxation; LIGHT: a target lowered below hi is marked in fout (returns 1 if newly marked)
-template <bool LIGHT>
-__device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, int32_t du,
-                                        u64* __restrict__ fout, u64& fe) {
-    const u64 x = eat(ed, k);
-    const u32 t = (u32)x;
-    const long long nd = (long long)du + (long long)(x >> 32);
-    if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[1].v, 1ull);
-    if (a.sbits && ((a.sbits[t >> 6] >> (t & 63)) & 1ull)) return 0u;
-    if (nd < INT_INF && (int32_t)nd < dist_now(a.dist + t)) {
-        if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
-        v2_dmin(a.dist + t, (int32_t)nd);  // no return: see v2_relax_g
-        if (LIGHT && (int32_t)nd < a.hi) {
-            if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[4].v, 1ull);
-            const u32 nw = v2_mark(fout, t) ? 1u : 0u;
-            if (PJ_V2_STATS && nw) atomicAdd(&a.ctl->dbg[3].v, 1ull);
-            if (nw) fe += a.lsplit[t];  // the next round's push cost
-            return nw;
-        }
-    }
-    return 0u;
-}
-
 // (vertices, their light edges) into a count slot: .v and .pad[0]
 __device__ __forceinline__ void v2_flush2(u64 x, u64 e, V2Line* sl, u64* red) {
     x = block_sum<DB / WAVE>(x, red);
@@ -353,59 +330,28 @@ __device__ __forceinline__ u64 v2_slot_edges(const V2Line* sl) {
     return t;
 }
 
-// PU consecutive edges [k, min(k + PU, lim)) of one source in one step (independent loads).
-template <bool LIGHT>
-__device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const ESrc ed, u64 k, u64 lim, int32_t du,
-                                          u64* __restrict__ fout, u64& fe) {
-    u32 t[PU];
-    long long nd[PU];
-    bool ok[PU];
-#pragma unroll
-    for (int j = 0; j < PU; ++j) {
-        ok[j] = k + j < lim;
-        const u64 x = ok[j] ? eat(ed, k + j) : 0ull;
-        t[j] = (u32)x;
-        nd[j] = (long long)du + (long long)(x >> 32);
-        ok[j] = ok[j] && nd[j] < INT_INF;
-    }
-    if (a.sbits) {  // tail: skip targets settled before the tail (a cache-resident bit, not dist)
-        u64 sw[PU];
-#pragma unroll
-        for (int j = 0; j < PU; ++j) sw[j] = ok[j] ? a.sbits[t[j] >> 6] : 0ull;
-#pragma unroll
-        for (int j = 0; j < PU; ++j) ok[j] = ok[j] && !((sw[j] >> (t[j] & 63)) & 1ull);
-    }
-    int32_t cd[PU];
-#pragma unroll
-    for (int j = 0; j < PU; ++j) cd[j] = ok[j] ? dist_now(a.dist + t[j]) : 0;
-    if (PJ_V2_STATS)
-        for (int j = 0; j < PU; ++j)
-            if (ok[j]) atomicAdd(&a.ctl->dbg[1].v, 1ull);
-    u32 newc = 0;
-#pragma unroll
-    for (int j = 0; j < PU; ++j) {
-        if (ok[j] && (int32_t)nd[j] < cd[j]) {
-            v2_dmin(a.dist + t[j], (int32_t)nd[j]);
-            if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
-            if (LIGHT && (int32_t)nd[j] < a.hi) {
-                if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[4].v, 1ull);
-                if (v2_mark(fout, t[j])) {
-                    if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[3].v, 1ull);
-                    ++newc;
-                    fe += a.lsplit[t[j]];
-                }
-            }
-        }
-    }
-    return newc;
-}
-
 // N independent edges (any positions, own source distances) with the loads
 // issued together: edge words, then target distances, then the atomics. The
 // atomicMin is issued without a return value (nothing waits for it): a target
 // whose read distance was above nd has been lowered to <= nd this round, by
-// this lane or another, so it belongs in the next frontier either way; the
-// atomicOr's old bit keeps the count of new frontier vertices exact.
+// this lane or another, so it belongs in the next frontier either way. The
+// frontier mark counts the new frontier vertex and its light edges (the next
+// round's push cost, read from lsplit):
+//   PJ_V2_MARK 0: a returning atomicOr, then the lsplit read of a newly marked
+//                 target (two dependent round trips after the distance);
+//   PJ_V2_MARK 1: the lsplit read issued beside the returning atomicOr (one);
+//   PJ_V2_MARK 2: the mark word read (agent scope) beside the distance, a
+//                 returnless atomicOr when the bit is clear, the lsplit read beside
+//                 it: the count may include a target two lanes marked at once
+//                 (a pull-decision estimate; never zero for a non-empty frontier).
+#ifndef PJ_V2_MARK
+#define PJ_V2_MARK 0
+#endif
+// hub queue slots carry the source's distance read by the producing round (PJ_V2_HUBDU 1)
+// instead of its id (0: the hub kernel reads dist[v], one dependent load per slot)
+#ifndef PJ_V2_HUBDU
+#define PJ_V2_HUBDU 0
+#endif
 template <bool LIGHT, int N>
 __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const u64 (&idx)[N],
                                           const int32_t (&du)[N], const bool (&val)[N], u64* __restrict__ fout,
@@ -420,7 +366,7 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
         nd[j] = (long long)du[j] + (long long)(x >> 32);
         ok[j] = val[j] && nd[j] < INT_INF;
     }
-    if (a.sbits) {
+    if (a.sbits) {  // tail: skip targets settled before the tail (a cache-resident bit, not dist)
         u64 sw[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) sw[j] = ok[j] ? a.sbits[t[j] >> 6] : 0ull;
@@ -428,18 +374,61 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
         for (int j = 0; j < N; ++j) ok[j] = ok[j] && !((sw[j] >> (t[j] & 63)) & 1ull);
     }
     int32_t cd[N];
+    u64 fw[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) cd[j] = ok[j] ? dist_now(a.dist + t[j]) : 0;
+    for (int j = 0; j < N; ++j) {
+        cd[j] = ok[j] ? dist_now(a.dist + t[j]) : 0;
+        if (LIGHT && PJ_V2_MARK == 2)
+            fw[j] = ok[j] && (int32_t)nd[j] < a.hi
+                        ? __hip_atomic_load(fout + (t[j] >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : ~0ull;
+    }
     if (PJ_V2_STATS)
         for (int j = 0; j < N; ++j)
             if (ok[j]) atomicAdd(&a.ctl->dbg[1].v, 1ull);
-    u32 newc = 0;
+    bool mk[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        if (ok[j] && (int32_t)nd[j] < cd[j]) {
+        const bool imp = ok[j] && (int32_t)nd[j] < cd[j];
+        if (imp) {
             v2_dmin(a.dist + t[j], (int32_t)nd[j]);
             if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
-            if (LIGHT && (int32_t)nd[j] < a.hi) {
+        }
+        mk[j] = LIGHT && imp && (int32_t)nd[j] < a.hi;
+    }
+    if (!LIGHT) return 0u;
+    u32 newc = 0;
+    if (PJ_V2_MARK == 2) {
+        u32 ls[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            mk[j] = mk[j] && !((fw[j] >> (t[j] & 63)) & 1ull);
+            if (mk[j]) atomicOr(fout + (t[j] >> 6), 1ull << (t[j] & 63));
+            ls[j] = mk[j] ? a.lsplit[t[j]] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            newc += mk[j];
+            fe += ls[j];
+        }
+    } else if (PJ_V2_MARK == 1) {
+        u64 old[N];
+        u32 ls[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            old[j] = mk[j] ? atomicOr(fout + (t[j] >> 6), 1ull << (t[j] & 63)) : ~0ull;
+            ls[j] = mk[j] ? a.lsplit[t[j]] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (!((old[j] >> (t[j] & 63)) & 1ull)) {
+                ++newc;
+                fe += ls[j];
+            }
+    } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (mk[j]) {
                 if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[4].v, 1ull);
                 if (v2_mark(fout, t[j])) {
                     if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[3].v, 1ull);
@@ -447,9 +436,34 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
                     fe += a.lsplit[t[j]];
                 }
             }
-        }
     }
     return newc;
+}
+
+// PU consecutive edges [k, min(k + PU, lim)) of one source in one step
+template <bool LIGHT>
+__device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const ESrc ed, u64 k, u64 lim, int32_t du,
+                                          u64* __restrict__ fout, u64& fe) {
+    u64 idx[PU];
+    int32_t d[PU];
+    bool val[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        idx[j] = k + j;
+        d[j] = du;
+        val[j] = k + j < lim;
+    }
+    return v2_relax_g<LIGHT, PU>(a, ed, idx, d, val, fout, fe);
+}
+
+// one relaxation
+template <bool LIGHT>
+__device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, int32_t du, u64* __restrict__ fout,
+                                        u64& fe) {
+    const u64 idx[1] = {k};
+    const int32_t d[1] = {du};
+    const bool val[1] = {true};
+    return v2_relax_g<LIGHT, 1>(a, ed, idx, d, val, fout, fe);
 }
 
 // Dense light round (the frontier holds more than dense_min vertices): the
@@ -566,7 +580,7 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
                 if (hub) {
                     const u64 slot = (base >> V2_EB) + (u64)__popcll(hm & lanemask_lt());
                     const u64 q = (u64)hs * a.hcap + slot;
-                    a.hv[q] = (u32)(v0 + j);
+                    a.hv[q] = PJ_V2_HUBDU ? (u32)du[j] : (u32)(v0 + j);
                     a.hbeg[q] = b[j];
                     a.hoff[q] = (base & mask) + ie - seg;
                     e[j] = b[j];
@@ -741,7 +755,7 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
                 if (hub) {
                     const u64 slot = (base >> V2_EB) + (u64)__popcll(hm & lanemask_lt());
                     const u64 q = (u64)hs * a.hcap + slot;
-                    a.hv[q] = v;
+                    a.hv[q] = PJ_V2_HUBDU ? (u32)du : v;
                     a.hbeg[q] = b;
                     a.hoff[q] = (base & mask) + ie - seg;
                     e = b;  // the hub kernel relaxes this segment
@@ -805,7 +819,7 @@ __device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ f
         u32 ns;
         lb_tile_load<V2_HTILE>(ho, nq, e0, L.sh, s0, ns);
         for (u32 i = threadIdx.x; i < ns; i += DB) {
-            L.s_du[i] = a.dist[hv[s0 + i]];
+            L.s_du[i] = PJ_V2_HUBDU ? (int32_t)hv[s0 + i] : a.dist[hv[s0 + i]];
             L.s_b[i] = hb[s0 + i];
         }
         __syncthreads();

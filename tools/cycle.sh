@@ -9,6 +9,9 @@
 #   pmc           FETCH_SIZE / WRITE_SIZE passes over tools/traffic_probe.py (one counter per run)
 #   table         the per-kernel PMC table and traffic json from kt + pmc
 #   probe:<cmd>   any python command line under a 240 s limit (e.g. probe:tools/stats_probe.py 26 3)
+#   ktp:<cmd>     rocprofv3 kernel trace + stats of any python command line -> kt_<name>/
+#   ab:<v1+v2..>  interleaved A/B (AB_PASSES times, default 2) of the k26w bench line under libpj
+#                 build variants (lib/variants/<v>/libpj.so; "default" = the main build)
 # Output under gpurun_out/TAG.
 set -o pipefail
 TAG=${1:?tag}; STEPS=${2:?steps}; shift 2
@@ -47,6 +50,21 @@ for st in "${LIST[@]}"; do
     probe)
       timeout -k 10 240 python3 -u $arg > "$OUT/probe_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-40).log" 2>&1 \
         || { echo "probe failed: $arg"; exit 1; } ;;
+    ktp)
+      kn=kt_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-30)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$kn" -o run -- python3 -u $arg \
+        > "$OUT/$kn.log" 2>&1 || { echo "ktp failed: $arg"; tail "$OUT/$kn.log"; exit 1; } ;;
+    ab)
+      IFS='+' read -ra VS <<< "$arg"
+      for pass in $(seq 1 ${AB_PASSES:-2}); do
+        for v in "${VS[@]}"; do
+          if [ "$v" != default ]; then export PJ_LIB_OVERRIDE=$PWD/paralleljohnson_amd/lib/variants/$v/libpj.so; else unset PJ_LIB_OVERRIDE; fi
+          timeout -k 10 200 python3 -u bench.py --no-secondary --no-partitioned --no-tts --no-cpu-baseline --steps 32 --warmup 4 "$@" \
+            > "$OUT/ab_$v.$pass.json" 2> "$OUT/ab_$v.$pass.err" || { echo "ab $v failed"; tail -5 "$OUT/ab_$v.$pass.err"; exit 1; }
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3], d['value'], d['ms_per_step'], d['roofline']['frac'])" "$OUT/ab_$v.$pass.json" $v $pass
+        done
+      done
+      unset PJ_LIB_OVERRIDE ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done

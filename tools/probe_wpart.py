@@ -6,20 +6,18 @@ import os, sys, time
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
 import numpy as np
 import paralleljohnson_amd as pj
-from paralleljohnson_amd.partition import Comm, delta_group, load_weighted
+from paralleljohnson_amd.partition import Comm, delta_group, load_weighted_kronecker
 
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 26
 for world in (1, 2):
     ctxs = [pj.Context(0) for _ in range(world)]
     comms = Comm.group(ctxs, "host") if world > 1 else [Comm.for_rank(ctxs[0], 1, 0)]
-    parts, roots = [], None
-    for r in range(world):  # each rank cuts its block from a graph on its own context
-        g = ctxs[r].generate_kronecker(scale, 16, 1, weighted=True)
-        if roots is None:
-            roots = [int(x) for x in g.sample_roots(2, 3)]
-        parts.append(load_weighted(ctxs[r], g, r, world))
-        g.close()
-    sets = ((0.1, 4, 3), (0.1, 4, 0), (0.1, 0, 0), (0.1, 4, 3), (0.1, 4, 0), (0.1, 0, 0))
+    g = ctxs[0].generate_kronecker(scale, 16, 1, weighted=True)  # (the roots)
+    roots = [int(x) for x in g.sample_roots(2, 3)]
+    g.close()
+    # each rank generates only its block's rows (pj_wpart_generate_kronecker)
+    parts = [load_weighted_kronecker(ctxs[r], scale, 16, 1, r, world) for r in range(world)]
+    sets = ((0.1, 4, 0), (0.1, 4, 0))
     if len(sys.argv) > 2:
         sets = [tuple(float(x) for x in t.split(",")) for t in sys.argv[2].split(";")]
     for tf, pf, lp in sets:
