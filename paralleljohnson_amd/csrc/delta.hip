@@ -277,6 +277,8 @@ struct V2Args {
     u64* hbeg;   // [3][hcap]
     u64* hoff;   // [3][hcap]
     u64 hcap;
+    uint4* hq;   // PJ_V2_HCH > 0: [3][hqcap] chunk descriptors (row position lo / hi, source dist, edges)
+    u64 hqcap;
     u64* rlog;   // round_log option: [0] = rounds logged, then (kind, frontier, its light edges) per round
 };
 // the light edges of a band round (light CSR, or the light prefixes of cw in the tail)
@@ -466,6 +468,67 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
     return v2_relax_g<LIGHT, 1>(a, ed, idx, d, val, fout, fe);
 }
 
+// Hub queue appends (whole wave; lanes with hub = true hand their segment [b, e) to the
+// queue of ring slot hs and get e = b back).
+//   PJ_V2_HCH 0: one slot per segment, (source, row position, edge offset) from ONE packed
+//                atomic, relaxed by v2_hub_body in edge-balanced block tiles (an LDS binary
+//                search per edge, the tile's slot offsets and source distances staged in LDS);
+//   PJ_V2_HCH > 0: the segment cut into chunks of HCH edges, one 16-byte descriptor each
+//                (row position, the source's distance, edge count), appended with one atomic
+//                per wave and written by the whole wave; v2_hub_chunks gives a wave one
+//                descriptor at a time: one load, then the chunk's edges in coalesced runs,
+//                no search, no block barrier.
+#ifndef PJ_V2_HCH
+#define PJ_V2_HCH 0
+#endif
+constexpr u32 V2_HCH = PJ_V2_HCH > 0 ? PJ_V2_HCH : 256;
+__device__ __forceinline__ void v2_hub_append(const V2Args& a, int hs, bool hub, u32 v, int32_t du, u64 b, u64& e) {
+    const int lane = lane_id();
+    const u64 hm = __ballot(hub);
+    if (!hm) return;
+    if (PJ_V2_HCH > 0) {
+        const u32 nc = hub ? (u32)((e - b + V2_HCH - 1) / V2_HCH) : 0u;
+        const u32 inc = wave_incl_scan(nc);
+        const u32 tot = __shfl(inc, 63, 64);
+        u64 base = 0;
+        if (lane == 63) base = atomicAdd(&a.ctl->hub[hs].v, (u64)tot);
+        base = __shfl(base, 63, 64);
+        uint4* q = a.hq + (u64)hs * a.hqcap;
+        u64 m = hm;
+        while (m) {  // the wave writes each hub's descriptors
+            const int l = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const u32 ncl = __shfl(nc, l, 64);
+            const u64 bl = __shfl(b, l, 64), el = __shfl(e, l, 64);
+            const int32_t dl = __shfl(du, l, 64);
+            const u64 qb = base + __shfl(inc, l, 64) - ncl;
+            for (u32 c = (u32)lane; c < ncl; c += WAVE) {
+                const u64 cb = bl + (u64)c * V2_HCH;
+                const u32 cn = (u32)min((u64)V2_HCH, el - cb);
+                q[qb + c] = make_uint4((u32)cb, (u32)(cb >> 32), (u32)dl, cn);
+            }
+        }
+        if (hub) e = b;
+        return;
+    }
+    const u64 mask = (1ull << V2_EB) - 1ull;
+    const u64 seg = hub ? e - b : 0;
+    const u64 ie = wave_incl_scan(seg);
+    const u64 tot = __shfl(ie, 63, 64);
+    const int leader = __ffsll((long long)hm) - 1;
+    u64 base = 0;
+    if (lane == leader) base = atomicAdd(&a.ctl->hub[hs].v, ((u64)__popcll(hm) << V2_EB) | tot);
+    base = __shfl(base, leader, 64);
+    if (hub) {
+        const u64 slot = (base >> V2_EB) + (u64)__popcll(hm & lanemask_lt());
+        const u64 q = (u64)hs * a.hcap + slot;
+        a.hv[q] = PJ_V2_HUBDU ? (u32)du : v;
+        a.hbeg[q] = b;
+        a.hoff[q] = (base & mask) + ie - seg;
+        e = b;
+    }
+}
+
 // Dense light round (the frontier holds more than dense_min vertices): the
 // workgroup takes a tile of V2_DT consecutive vertices, reads their frontier
 // words, row offsets and distances with coalesced loads (4 consecutive vertices
@@ -510,7 +573,7 @@ template <typename Off>
 __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __restrict__ row, u64* __restrict__ fin,
                                               u64* __restrict__ fout, int hs, u32& newc, u64& fe, u64& mh, u64& ml,
                                               V2Dense<Off>& sh) {
-    const int tid = threadIdx.x, lane = lane_id();
+    const int tid = threadIdx.x;
     const u64 mask = (1ull << V2_EB) - 1ull;
     const ESrc ed = v2_light_src(a);
     const i64 ntiles = (a.n + V2_DT - 1) / V2_DT;
@@ -564,29 +627,9 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
                 }
             }
         }
-        // long segments -> hub queue (wave-aggregated packed append, as v2_expand_body)
+        // long segments -> hub queue (wave-aggregated append, v2_hub_append)
 #pragma unroll
-        for (int j = 0; j < V2_DV; ++j) {
-            const bool hub = e[j] - b[j] > V2_DHT;
-            const u64 hm = __ballot(hub);
-            if (hm) {
-                const u64 seg = hub ? e[j] - b[j] : 0;
-                const u64 ie = wave_incl_scan(seg);
-                const u64 tot = __shfl(ie, 63, 64);
-                const int leader = __ffsll((long long)hm) - 1;
-                u64 base = 0;
-                if (lane == leader) base = atomicAdd(&a.ctl->hub[hs].v, ((u64)__popcll(hm) << V2_EB) | tot);
-                base = __shfl(base, leader, 64);
-                if (hub) {
-                    const u64 slot = (base >> V2_EB) + (u64)__popcll(hm & lanemask_lt());
-                    const u64 q = (u64)hs * a.hcap + slot;
-                    a.hv[q] = PJ_V2_HUBDU ? (u32)du[j] : (u32)(v0 + j);
-                    a.hbeg[q] = b[j];
-                    a.hoff[q] = (base & mask) + ie - seg;
-                    e[j] = b[j];
-                }
-            }
-        }
+        for (int j = 0; j < V2_DV; ++j) v2_hub_append(a, hs, e[j] - b[j] > V2_DHT, (u32)(v0 + j), du[j], b[j], e[j]);
         u64 cnt = 0, edges = 0;
 #pragma unroll
         for (int j = 0; j < V2_DV; ++j)
@@ -660,7 +703,6 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
                                                u64* __restrict__ fout, int cin, int hs, u64* red) {
     constexpr int NWV = DB / WAVE;
     const int lane = lane_id();
-    const u64 mask = (1ull << V2_EB) - 1ull;
     u32 newc = 0;
     u64 mh = 0, ml = 0, fe = 0;
     const i64 nsc = (a.nwords + V2_SC - 1) / V2_SC;
@@ -741,26 +783,8 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
                     e = (u64)row[v + 1];
                 }
             }
-            // long segment -> hub queue (wave-aggregated packed append; all lanes here)
-            const bool hub = e - b > V2_HT;
-            const u64 hm = __ballot(hub);
-            if (hm) {
-                const u64 seg = hub ? e - b : 0;
-                const u64 ie = wave_incl_scan(seg);
-                const u64 tot = __shfl(ie, 63, 64);
-                const int leader = __ffsll((long long)hm) - 1;
-                u64 base = 0;
-                if (lane == leader) base = atomicAdd(&a.ctl->hub[hs].v, ((u64)__popcll(hm) << V2_EB) | tot);
-                base = __shfl(base, leader, 64);
-                if (hub) {
-                    const u64 slot = (base >> V2_EB) + (u64)__popcll(hm & lanemask_lt());
-                    const u64 q = (u64)hs * a.hcap + slot;
-                    a.hv[q] = PJ_V2_HUBDU ? (u32)du : v;
-                    a.hbeg[q] = b;
-                    a.hoff[q] = (base & mask) + ie - seg;
-                    e = b;  // the hub kernel relaxes this segment
-                }
-            }
+            // long segment -> hub queue (wave-aggregated append; all lanes here)
+            v2_hub_append(a, hs, e - b > V2_HT, v, du, b, e);
             // lane-serial part
             u64 k = b;
             const u64 lim = (e - b > (u64)V2_LS) ? b + V2_LS : e;
@@ -842,16 +866,45 @@ __device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ f
 
 // The hub queue hs of one round in its own launch. Zeroes the next ring slot hz for
 // later appends.
+// PJ_V2_HCH > 0: a wave takes one chunk descriptor at a time (grid-stride over the
+// chunks); lane l relaxes edges l, l + 64, ... of the chunk, HCH / 64 per lane with the
+// loads issued together (v2_relax_g).
+template <bool LIGHT>
+__device__ __forceinline__ void v2_hub_chunks(const V2Args& a, u64* __restrict__ fout, int hs, u64 nch, u32& newc,
+                                              u64& fe) {
+    constexpr int NJ = (int)(V2_HCH / WAVE);
+    const int lane = lane_id();
+    const uint4* q = a.hq + (u64)hs * a.hqcap;
+    const ESrc ed = LIGHT ? v2_light_src(a) : v2_cw_src(a);
+    const u64 nwv = (u64)gridDim.x * (DB / WAVE);
+    for (u64 c = (u64)blockIdx.x * (DB / WAVE) + wave_id(); c < nch; c += nwv) {
+        const uint4 d = q[c];
+        const u64 cb = (u64)d.x | ((u64)d.y << 32);
+        u64 idx[NJ];
+        int32_t du[NJ];
+        bool val[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const u32 o = (u32)lane + (u32)j * WAVE;
+            val[j] = o < d.w;
+            idx[j] = cb + o;
+            du[j] = (int32_t)d.z;
+        }
+        newc += v2_relax_g<LIGHT, NJ>(a, ed, idx, du, val, fout, fe);
+    }
+}
+
 template <bool LIGHT>
 __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout, int cin, int hs, int hz) {
     __shared__ V2HubLds L;
     __shared__ u64 red[DB / WAVE];
     const u64 packed = a.ctl->hub[hs].v;
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->hub[hz].v = 0;
-    if ((packed >> V2_EB) == 0) return;
+    if (PJ_V2_HCH > 0 ? packed == 0 : (packed >> V2_EB) == 0) return;
     u32 newc = 0;
     u64 fe = 0;
-    v2_hub_body<LIGHT>(a, fout, hs, packed, newc, fe, L);
+    if (PJ_V2_HCH > 0) v2_hub_chunks<LIGHT>(a, fout, hs, packed, newc, fe);
+    else v2_hub_body<LIGHT>(a, fout, hs, packed, newc, fe, L);
     if (LIGHT) v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
 }
 
@@ -1433,6 +1486,8 @@ struct DeltaSolve {
     DevBuf<u32> hv;
     DevBuf<u64> hbeg, hoff;
     u64 hcap = 0;
+    DevBuf<uint4> hq;          // (PJ_V2_HCH > 0) hub chunk descriptors, [3][hqcap]
+    u64 hqcap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     pj_stats st{};
     ~DeltaSolve() {
@@ -1660,9 +1715,18 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     v.sb.alloc(nw);
     v.ctl.alloc(1);
     v.hcap = (u64)std::max<i64>(1, std::min<i64>(n, g.nnz / (i64)V2_HT + 1));
-    v.hv.alloc(3 * v.hcap);
-    v.hbeg.alloc(3 * v.hcap);
-    v.hoff.alloc(3 * v.hcap);
+    if (PJ_V2_HCH > 0) {
+        // every segment has more than V2_HT edges: at most nnz / V2_HCH + nnz / V2_HT chunks a round
+        v.hqcap = (u64)std::max<i64>(1, g.nnz / (i64)V2_HCH + g.nnz / (i64)V2_HT + 1);
+        v.hq.alloc(3 * v.hqcap);
+        v.hv.alloc(1);
+        v.hbeg.alloc(1);
+        v.hoff.alloc(1);
+    } else {
+        v.hv.alloc(3 * v.hcap);
+        v.hbeg.alloc(3 * v.hcap);
+        v.hoff.alloc(3 * v.hcap);
+    }
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hctl), sizeof(V2Ctl), hipHostMallocMapped));
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&v.hctl_dev), v.hctl, 0));
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hseq), 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -1716,6 +1780,8 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     a.hbeg = v.hbeg.p;
     a.hoff = v.hoff.p;
     a.hcap = v.hcap;
+    a.hq = v.hq.p;
+    a.hqcap = v.hqcap;
     DevBuf<u64> rlog;
     if (g.round_log) {
         rlog.alloc(1 + 3 * 255);

@@ -9,6 +9,7 @@
 #   pmc           FETCH_SIZE / WRITE_SIZE passes over tools/traffic_probe.py (one counter per run)
 #   table         the per-kernel PMC table and traffic json from kt + pmc
 #   probe:<cmd>   any python command line under a 240 s limit (e.g. probe:tools/stats_probe.py 26 3)
+#   vtests:<v>:<pytest args>  -m gpu tests under the libpj build variant <v>
 #   ktp:<cmd>     rocprofv3 kernel trace + stats of any python command line -> kt_<name>/
 #   ab:<v1+v2..>  interleaved A/B (AB_PASSES times, default 2) of the k26w bench line under libpj
 #                 build variants (lib/variants/<v>/libpj.so; "default" = the main build)
@@ -50,6 +51,12 @@ for st in "${LIST[@]}"; do
     probe)
       timeout -k 10 240 python3 -u $arg > "$OUT/probe_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-40).log" 2>&1 \
         || { echo "probe failed: $arg"; exit 1; } ;;
+    vtests)
+      v=${arg%%:*}; targs=${arg#*:}
+      PJ_LIB_OVERRIDE=$PWD/paralleljohnson_amd/lib/variants/$v/libpj.so timeout -k 10 600 python -u -m pytest -x -q \
+        --timeout 300 --timeout-method thread -m gpu $targs > "$OUT/vtests_$v.log" 2>&1 \
+        || { echo "vtests $v failed"; tail -30 "$OUT/vtests_$v.log"; exit 1; }
+      tail -1 "$OUT/vtests_$v.log" ;;
     ktp)
       kn=kt_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-30)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$kn" -o run -- python3 -u $arg \
