@@ -266,6 +266,8 @@ struct V2Args {
     const u32* col;   // relabeled ids beside w8 (split records of the whole CSR), when w8 is set
     const uint8_t* w8;
     const u64* hl;    // bit v: v has a light edge (lsplit[v] > 0) for this delta; null in the tail
+    const uint8_t* hw;  // (PJ_V2_HWF) weight of v's first heavy edge for the current threshold (capped
+                        // at 255; 0 = no heavy edge), or null: the heavy pull's candidate filter
     int ltail;        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
     const u64* sbits; // tail mode: settled-before-the-tail bitmap; relaxations skip its targets
     u64* swrite;      // the heavy step entering the tail writes that bitmap (pull / select)
@@ -480,6 +482,10 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
 //                no search, no block barrier.
 #ifndef PJ_V2_HCH
 #define PJ_V2_HCH 0
+#endif
+// heavy pull candidates filtered by the row's first heavy weight (V2Args::hw)
+#ifndef PJ_V2_HWF
+#define PJ_V2_HWF 0
 #endif
 constexpr u32 V2_HCH = PJ_V2_HCH > 0 ? PJ_V2_HCH : 256;
 __device__ __forceinline__ void v2_hub_append(const V2Args& a, int hs, bool hub, u32 v, int32_t du, u64 b, u64& e) {
@@ -986,14 +992,30 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
         for (int k = 0; k < PSC; ++k) {
             const i64 v = (gbase + k) * 64 + lane;
             const int32_t d = v < a.n ? a.dist[v] : 0;
-            const u64 m = __ballot(v < a.n && d >= hi);
-            if (lane == k) mytodo = m;
+            const bool up = v < a.n && d >= hi;
+            // heavy-head filter: no band member can lower d below lo + (the row's lightest
+            // heavy weight); such vertices (and those without heavy edges) are not scanned,
+            // but still join the next band / its minimum
+            const int h = (a.hw && up) ? (int)a.hw[v] : 1;
+            const bool cand = up && h != 0 && (long long)lo + h < (long long)d;
+            const u64 m = __ballot(cand);
+            u64 nm = 0;
+            if (a.hw) {
+                const bool sk = up && !cand;
+                if (sk && d < mn) mn = d;
+                nm = __ballot(sk && d < nhi);
+                if (sk && d < nhi) fe += (a.fesplit ? a.fesplit : a.lsplit)[v];
+            }
+            if (lane == k) {
+                mytodo = m;
+                newb[2 * k] = (u32)nm;
+                newb[2 * k + 1] = (u32)(nm >> 32);
+            }
             if (a.swrite) {
                 const u64 sm = __ballot(v < a.n && d < hi);
                 if (lane == k && gbase + k < a.nwords) a.swrite[gbase + k] = sm;
             }
         }
-        if (lane < 2 * PSC) newb[lane] = 0;
         const u32 cnt = (u32)__popcll(mytodo);
         const u32 incl = wave_incl_scan(cnt);
         const u32 myex = incl - cnt;
@@ -1452,6 +1474,17 @@ __global__ __launch_bounds__(DB) void v2_heavy_left_k(const Off* __restrict__ ro
 
 
 
+// hw[v] = the weight of v's first heavy edge (row[v] + lsplit[v]; rows are weight-sorted),
+// capped at 255, or 0 when v has no heavy edge (heavy weights are >= the threshold >= 1)
+template <typename Off, typename WT>
+__global__ void v2_hw_k(const Off* __restrict__ row, const u32* __restrict__ lsplit, const WT* __restrict__ w, i64 n,
+                        uint8_t* __restrict__ hw) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
+        const u64 b = (u64)row[v] + lsplit[v], e = (u64)row[v + 1];
+        hw[v] = b < e ? (uint8_t)max(1u, min(255u, (u32)w[b])) : (uint8_t)0;
+    }
+}
+
 // hl bit v = (lsplit[v] > 0): the vertices that have light edges for this delta
 __global__ void v2_haslight_k(const u32* __restrict__ lsplit, i64 n, u64* __restrict__ hl) {
     const i64 nw = (n + 63) / 64;
@@ -1519,6 +1552,7 @@ struct DeltaWork {
     u32 lcb = 0;
     int packed_for = -1;   // g.light_pack the light CSR was built for
     DevBuf<u64> hl;        // has-light-edges bitmap (per delta)
+    DevBuf<uint8_t> hw, hw2;  // (PJ_V2_HWF) first heavy weight per vertex for delta / the tail threshold
     DeltaSolve main;
     std::vector<std::unique_ptr<DeltaSolve>> extra;  // concurrent batch solves
 };
@@ -1547,6 +1581,15 @@ void launch_light_split(const Relabeled& R, const Off* row, i64 n, u32 delta, u3
                         hipStream_t s) {
     if (R.w8.p) light_split_k<Off, uint8_t><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w8.p, n, delta, out);
     else light_split_k<Off, u32><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, delta, out);
+    PJ_LAUNCH_CHECK();
+}
+
+template <typename Off>
+void launch_hw(const Relabeled& R, const Off* row, const u32* lsplit, i64 n, DevBuf<uint8_t>& out, unsigned maxgrid,
+               hipStream_t s) {
+    out.ensure((size_t)std::max<i64>(n, 1));
+    if (R.w8.p) v2_hw_k<Off, uint8_t><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, lsplit, R.w8.p, n, out.p);
+    else v2_hw_k<Off, u32><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, lsplit, R.w.p, n, out.p);
     PJ_LAUNCH_CHECK();
 }
 
@@ -1612,6 +1655,7 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         PJ_LAUNCH_CHECK();
         PJ_HIP(hipMemcpyAsync(&w.nlc, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
         PJ_HIP(hipStreamSynchronize(s));
+        if (PJ_V2_HWF) launch_hw<Off>(R, row, w.lsplit.p, n, w.hw, maxgrid, s);
         // the light CSR of this delta
         w.hl.alloc((size_t)(n + 63) / 64);
         v2_haslight_k<<<grid_for(n, 256, maxgrid), 256, 0, s>>>(w.lsplit.p, n, w.hl.p);
@@ -1655,6 +1699,7 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
     if (tdelta > delta && w.lsplit2_delta != (u32)tdelta && n > 0) {
         w.lsplit2.ensure((size_t)n);
         launch_light_split<Off>(R, row, n, (u32)tdelta, w.lsplit2.p, maxgrid, s);
+        if (PJ_V2_HWF) launch_hw<Off>(R, row, w.lsplit2.p, n, w.hw2, maxgrid, s);
         w.lsplit2_delta = (u32)tdelta;
         PJ_HIP(hipStreamSynchronize(s));
     }
@@ -1772,6 +1817,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     a.col = R.col.p;
     a.w8 = g.split_w ? R.w8.p : nullptr;
     a.hl = g.light_filter ? w.hl.p : nullptr;
+    a.hw = PJ_V2_HWF ? w.hw.p : nullptr;
     // light rounds whose frontier holds more than dense_frac x n vertices run tile-dense
     const u64 dense_min = g.dense_frac > 0.0 ? (u64)(g.dense_frac * (double)n) : ~0ull;
     a.mb = v.mb.p;
@@ -1959,6 +2005,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 a.fesplit = nullptr;
                 a.sbits = v.sb.p;
                 a.lsplit = w.lsplit2.p;
+                a.hw = PJ_V2_HWF ? w.hw2.p : nullptr;
                 a.ltail = 1;
                 bw = tdelta;
                 // light pulls in the tail (tail_pull): rows are scanned in weight order and
