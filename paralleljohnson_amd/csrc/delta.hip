@@ -266,6 +266,8 @@ struct V2Args {
     const u32* col;   // relabeled ids beside w8 (split records of the whole CSR), when w8 is set
     const uint8_t* w8;
     const u64* hl;    // bit v: v has a light edge (lsplit[v] > 0) for this delta; null in the tail
+    const uint8_t* w1;  // (PJ_V2_LWF) the lightest weight of v's row (capped at 255), or null: the light
+                        // pull's candidate filter
     const uint8_t* hw;  // (PJ_V2_HWF) weight of v's first heavy edge for the current threshold (capped
                         // at 255; 0 = no heavy edge), or null: the heavy pull's candidate filter
     int ltail;        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
@@ -486,6 +488,10 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
 // heavy pull candidates filtered by the row's first heavy weight (V2Args::hw)
 #ifndef PJ_V2_HWF
 #define PJ_V2_HWF 0
+#endif
+// light pull candidates filtered by the row's lightest weight (V2Args::w1)
+#ifndef PJ_V2_LWF
+#define PJ_V2_LWF 0
 #endif
 constexpr u32 V2_HCH = PJ_V2_HCH > 0 ? PJ_V2_HCH : 256;
 __device__ __forceinline__ void v2_hub_append(const V2Args& a, int hs, bool hub, u32 v, int32_t du, u64 b, u64& e) {
@@ -1163,7 +1169,9 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
         for (int k = 0; k < PSC; ++k) {
             const i64 v = (gbase + k) * 64 + lane;
             const int32_t d = v < a.n ? a.dist[v] : 0;
-            const u64 m = __ballot(v < a.n && d > lo);
+            // (w1 filter: a frontier in-neighbour offers at least lo + the row's lightest weight)
+            const int w1 = (a.w1 && v < a.n && d > lo) ? (int)a.w1[v] : 0;
+            const u64 m = __ballot(v < a.n && d > lo && (long long)lo + w1 < (long long)d);
             if (lane == k) mytodo = m;
         }
         // a vertex without light edges has no light in-edge (symmetric graph): not a candidate
@@ -1476,6 +1484,15 @@ __global__ __launch_bounds__(DB) void v2_heavy_left_k(const Off* __restrict__ ro
 
 // hw[v] = the weight of v's first heavy edge (row[v] + lsplit[v]; rows are weight-sorted),
 // capped at 255, or 0 when v has no heavy edge (heavy weights are >= the threshold >= 1)
+// w1[v] = the lightest weight of v's row (its first: rows are weight-sorted), capped at 255
+template <typename Off, typename WT>
+__global__ void v2_w1_k(const Off* __restrict__ row, const WT* __restrict__ w, i64 n, uint8_t* __restrict__ w1) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
+        const u64 b = (u64)row[v], e = (u64)row[v + 1];
+        w1[v] = b < e ? (uint8_t)min(255u, (u32)w[b]) : (uint8_t)255;
+    }
+}
+
 template <typename Off, typename WT>
 __global__ void v2_hw_k(const Off* __restrict__ row, const u32* __restrict__ lsplit, const WT* __restrict__ w, i64 n,
                         uint8_t* __restrict__ hw) {
@@ -1553,6 +1570,7 @@ struct DeltaWork {
     int packed_for = -1;   // g.light_pack the light CSR was built for
     DevBuf<u64> hl;        // has-light-edges bitmap (per delta)
     DevBuf<uint8_t> hw, hw2;  // (PJ_V2_HWF) first heavy weight per vertex for delta / the tail threshold
+    DevBuf<uint8_t> w1;       // (PJ_V2_LWF) lightest weight per vertex (any threshold)
     DeltaSolve main;
     std::vector<std::unique_ptr<DeltaSolve>> extra;  // concurrent batch solves
 };
@@ -1656,6 +1674,12 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         PJ_HIP(hipMemcpyAsync(&w.nlc, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
         PJ_HIP(hipStreamSynchronize(s));
         if (PJ_V2_HWF) launch_hw<Off>(R, row, w.lsplit.p, n, w.hw, maxgrid, s);
+        if (PJ_V2_LWF && !w.w1.p) {
+            w.w1.alloc((size_t)std::max<i64>(n, 1));
+            if (R.w8.p) v2_w1_k<Off, uint8_t><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w8.p, n, w.w1.p);
+            else v2_w1_k<Off, u32><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, w.w1.p);
+            PJ_LAUNCH_CHECK();
+        }
         // the light CSR of this delta
         w.hl.alloc((size_t)(n + 63) / 64);
         v2_haslight_k<<<grid_for(n, 256, maxgrid), 256, 0, s>>>(w.lsplit.p, n, w.hl.p);
@@ -1818,6 +1842,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     a.w8 = g.split_w ? R.w8.p : nullptr;
     a.hl = g.light_filter ? w.hl.p : nullptr;
     a.hw = PJ_V2_HWF ? w.hw.p : nullptr;
+    a.w1 = PJ_V2_LWF ? w.w1.p : nullptr;
     // light rounds whose frontier holds more than dense_frac x n vertices run tile-dense
     const u64 dense_min = g.dense_frac > 0.0 ? (u64)(g.dense_frac * (double)n) : ~0ull;
     a.mb = v.mb.p;
