@@ -489,6 +489,10 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
 #ifndef PJ_V2_HWF
 #define PJ_V2_HWF 0
 #endif
+// light pull rounds: new members' degree sums with a lane per vertex (v2_pull_light_body)
+#ifndef PJ_V2_MBPAR
+#define PJ_V2_MBPAR 0
+#endif
 // light pull candidates filtered by the row's lightest weight (V2Args::w1)
 #ifndef PJ_V2_LWF
 #define PJ_V2_LWF 0
@@ -1148,20 +1152,50 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
     const i64 nsc = (a.nwords + PSC - 1) / PSC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
         const i64 gbase = sc * PSC;
+        // the frontier joins the members; new members add their heavy / light degrees.
+        // PJ_V2_MBPAR 1: lane = vertex of each of the PSC words (the loads of all words
+        // issued together); 0: a lane walks the bits of its word serially (one dependent
+        // round trip per new member: ~35 per word in a band-start pull of the tail)
+        u64 nmw = 0;
         if (lane < PSC && gbase + lane < a.nwords) {
             const u64 f = fin[gbase + lane];
             if (f) {
                 const u64 old = a.mb[gbase + lane];
-                u64 nm = f & ~old;
-                if (nm) a.mb[gbase + lane] = old | f;
-                while (nm) {
-                    const int b = __ffsll((long long)nm) - 1;
-                    nm &= nm - 1;
-                    const i64 v = (gbase + lane) * 64 + b;
-                    const u64 rb = (u64)row[v], ls = a.lsplit[v];
-                    mh += (u64)row[v + 1] - rb - ls;
-                    ml += ls;
+                nmw = f & ~old;
+                if (nmw) a.mb[gbase + lane] = old | f;
+            }
+        }
+        if (PJ_V2_MBPAR) {
+            if (__ballot(nmw != 0)) {
+                constexpr int MB4 = 4;
+#pragma unroll
+                for (int k0 = 0; k0 < PSC; k0 += MB4) {
+                    u64 rb[MB4], re[MB4], ls[MB4];
+                    bool on[MB4];
+#pragma unroll
+                    for (int j = 0; j < MB4; ++j) {
+                        const u64 w = __shfl(nmw, k0 + j, 64);
+                        on[j] = (w >> lane) & 1ull;
+                        const i64 v = (gbase + k0 + j) * 64 + lane;
+                        rb[j] = on[j] ? (u64)row[v] : 0;
+                        re[j] = on[j] ? (u64)row[v + 1] : 0;
+                        ls[j] = on[j] ? a.lsplit[v] : 0;
+                    }
+#pragma unroll
+                    for (int j = 0; j < MB4; ++j) {
+                        mh += re[j] - rb[j] - ls[j];
+                        ml += ls[j];
+                    }
                 }
+            }
+        } else {
+            while (nmw) {
+                const int b = __ffsll((long long)nmw) - 1;
+                nmw &= nmw - 1;
+                const i64 v = (gbase + lane) * 64 + b;
+                const u64 rb = (u64)row[v], ls = a.lsplit[v];
+                mh += (u64)row[v + 1] - rb - ls;
+                ml += ls;
             }
         }
         u64 mytodo = 0;
