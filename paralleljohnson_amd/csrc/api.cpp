@@ -866,6 +866,7 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "ms_width" && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16))
         g.ms_width = (int)value;
     else if (k == "ms_alpha" && value >= 0) g.ms_alpha = value;
+    else if (k == "ms_streams" && value >= 1 && value <= 4) g.ms_streams = (int)value;
     else return arg_error("pj_set_option: unknown key or bad value");
     return PJ_OK;
 }

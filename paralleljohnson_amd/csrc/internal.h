@@ -227,6 +227,7 @@ struct Graph {
     int ms_width = 0;    // batch BFS: widest pass in 64-source words (0 = 8, i.e. 512 sources;
                          // MS1024 on web-Google: 11.6 ms at 8 against 12.2-14.4 ms at 4; 16
                          // (1024 sources) 3% slower than 8)
+    int ms_streams = 2;      // batch BFS: passes in flight at once (one stream + host thread each)
     double ms_alpha = 16.0;  // batch BFS: push levels while the frontier's out-edges < nnz / ms_alpha
 
     bool have_result = false;

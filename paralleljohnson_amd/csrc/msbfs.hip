@@ -20,7 +20,11 @@
 // (the levels are probe-latency-bound, profiles/r01). W = 8 (512 sources) measured
 // best on MS1024; 16 is 3% slower (two passes' latency saved, but twice the mask
 // bytes per probe and per vertex).
+#include <atomic>
 #include <chrono>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "devutil.h"
 
@@ -403,24 +407,38 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
 
 }  // namespace
 
-struct MsWork {
-    int W = 0;  // words per vertex mask of the allocation
+// One pass in flight: its masks, distance block, control block, stream and events.
+// Slot 0 runs on the ctx stream; further slots (option ms_streams) own a stream, and
+// passes of one batch run on the slots at once, one host thread each: a pass is a chain
+// of latency-bound levels, so two of them interleave on the CUs.
+struct MsSlot {
     DevBuf<u64> V, F, Fn;
     DevBuf<int32_t> dist;
     DevBuf<int64_t> src;
     DevBuf<MsCtl> ctl;
     int64_t* host = nullptr;
     int32_t last_levels = 0;  // level iterations the previous pass used: sizes the first batch
-    ~MsWork() {
+    hipStream_t s = nullptr;
+    bool own_stream = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    ~MsSlot() {
         if (host) (void)hipHostFree(host);
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (own_stream && s) (void)hipStreamDestroy(s);
     }
+};
+
+struct MsWork {
+    int W = 0;  // words per vertex mask of the allocation
+    std::vector<std::unique_ptr<MsSlot>> slots;
 };
 
 void delete_ms_work(MsWork* p) { delete p; }
 
 template <typename Off, int W>
-static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double* kernel_ms, i64* levels) {
-    hipStream_t s = g.ctx->stream;
+static void ms_pass(Graph& g, MsSlot& w, const int64_t* sources, int ns, double* kernel_ms, i64* levels) {
+    hipStream_t s = w.s;
     const i64 n = g.n;
     const Off* crow = static_cast<const Off*>(g.crow_ptr());
     const u32* ccol = g.ccol_ptr();
@@ -439,7 +457,7 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double*
     const u32* col = g.col.p;
     // push while the frontier's out-edges are below nnz / ms_alpha (0: never)
     const u64 push_max = g.ms_alpha > 0 ? (u64)((double)g.nnz / g.ms_alpha) : 0ull;
-    PJ_HIP(hipEventRecord(g.ev0, s));
+    PJ_HIP(hipEventRecord(w.ev0, s));
     ms_init_k<<<grid_for(std::max<i64>(n * W, (i64)ns * n / 4), MB, (unsigned)g.ctx->cu_count * 8u), MB, 0, s>>>(
         w.V.p, w.F.p, n * W, w.dist.p, (i64)ns * n, w.ctl.p, host_dev);
     PJ_LAUNCH_CHECK();
@@ -472,10 +490,10 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double*
         batch = next;
         next = next < 1024 ? next * 2 : next;
     }
-    PJ_HIP(hipEventRecord(g.ev1, s));
-    PJ_HIP(hipEventSynchronize(g.ev1));
+    PJ_HIP(hipEventRecord(w.ev1, s));
+    PJ_HIP(hipEventSynchronize(w.ev1));
     float ms = 0.f;
-    PJ_HIP(hipEventElapsedTime(&ms, g.ev0, g.ev1));
+    PJ_HIP(hipEventElapsedTime(&ms, w.ev0, w.ev1));
     *kernel_ms += ms;
     const i64 lv = (i64)*(volatile int64_t*)w.host;
     if (any && lv >= 0) w.last_levels = (int32_t)lv + 1;
@@ -483,7 +501,7 @@ static void ms_pass(Graph& g, MsWork& w, const int64_t* sources, int ns, double*
 }
 
 template <typename Off>
-static void ms_pass_w(int W, Graph& g, MsWork& w, const int64_t* sources, int ns, double* kernel_ms, i64* levels) {
+static void ms_pass_w(int W, Graph& g, MsSlot& w, const int64_t* sources, int ns, double* kernel_ms, i64* levels) {
     if (W == 16) ms_pass<Off, 16>(g, w, sources, ns, kernel_ms, levels);
     else if (W == 8) ms_pass<Off, 8>(g, w, sources, ns, kernel_ms, levels);
     else if (W == 4) ms_pass<Off, 4>(g, w, sources, ns, kernel_ms, levels);
@@ -500,33 +518,84 @@ static int ms_words(const Graph& g, int n_src) {
     return W;
 }
 
-void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_pass) {
+static void ms_slot_alloc(Graph& g, MsSlot& sl, int W, bool own_stream) {
     const size_t n = (size_t)g.n;
+    sl.V.alloc(n ? n * W : 1);
+    sl.F.alloc(n ? n * W : 1);
+    sl.Fn.alloc(n ? n * W : 1);
+    sl.dist.alloc(n ? 64 * W * n : 1);
+    sl.src.alloc(64 * W);
+    sl.ctl.alloc(1);
+    PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&sl.host), sizeof(int64_t), hipHostMallocMapped));
+    PJ_HIP(hipEventCreate(&sl.ev0));
+    PJ_HIP(hipEventCreate(&sl.ev1));
+    if (own_stream) {
+        PJ_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
+        sl.own_stream = true;
+    }
+}
+
+void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_pass) {
     const int W = ms_words(g, n_src);
+    const int per = 64 * W;
+    const int npass = (n_src + per - 1) / per;
+    const int nslots = std::max(1, std::min(g.ms_streams, npass));
     if (!g.ms_work || g.ms_work->W < W) {
         g.ms_work.reset(new MsWork());
-        MsWork& w = *g.ms_work;
-        w.W = W;
-        w.V.alloc(n ? n * W : 1);
-        w.F.alloc(n ? n * W : 1);
-        w.Fn.alloc(n ? n * W : 1);
-        w.dist.alloc(n ? 64 * W * n : 1);
-        w.src.alloc(64 * W);
-        w.ctl.alloc(1);
-        PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.host), sizeof(int64_t), hipHostMallocMapped));
+        g.ms_work->W = W;
     }
-    if (!g.ev0) PJ_HIP(hipEventCreate(&g.ev0));
-    if (!g.ev1) PJ_HIP(hipEventCreate(&g.ev1));
+    MsWork& mw = *g.ms_work;
+    while ((int)mw.slots.size() < nslots) {
+        std::unique_ptr<MsSlot> sl(new MsSlot());
+        ms_slot_alloc(g, *sl, mw.W, !mw.slots.empty());
+        mw.slots.push_back(std::move(sl));
+    }
+    mw.slots[0]->s = g.ctx->stream;  // (pj_set_stream may change it)
     auto t0 = std::chrono::steady_clock::now();
     pj_stats st{};
     double kms = 0;
     i64 levels = 0;
-    const int per = 64 * W;
-    for (int off = 0; off < n_src; off += per) {
+    auto run = [&](MsSlot& sl, int off, double* k, i64* lv) {
         const int ns = std::min(per, n_src - off);
-        if (g.off64) ms_pass_w<u64>(W, g, *g.ms_work, sources + off, ns, &kms, &levels);
-        else ms_pass_w<u32>(W, g, *g.ms_work, sources + off, ns, &kms, &levels);
-        if (on_pass) on_pass(off, ns, g.ms_work->dist.p);
+        if (g.off64) ms_pass_w<u64>(W, g, sl, sources + off, ns, k, lv);
+        else ms_pass_w<u32>(W, g, sl, sources + off, ns, k, lv);
+        return ns;
+    };
+    if (nslots == 1) {
+        for (int off = 0; off < n_src; off += per) {
+            const int ns = run(*mw.slots[0], off, &kms, &levels);
+            if (on_pass) on_pass(off, ns, mw.slots[0]->dist.p);
+        }
+    } else {
+        PJ_HIP(hipStreamSynchronize(g.ctx->stream));
+        std::atomic<int> next{0};
+        std::mutex mu;
+        std::vector<std::exception_ptr> errs((size_t)nslots);
+        auto work = [&](int k) {
+            try {
+                PJ_HIP(hipSetDevice(g.ctx->device));
+                MsSlot& sl = *mw.slots[(size_t)k];
+                for (int p; (p = next.fetch_add(1)) < npass;) {
+                    double km = 0;
+                    i64 lv = 0;
+                    const int off = p * per;
+                    const int ns = run(sl, off, &km, &lv);
+                    std::lock_guard<std::mutex> lk(mu);
+                    kms += km;
+                    levels = std::max(levels, lv);
+                    if (on_pass) on_pass(off, ns, sl.dist.p);
+                }
+            } catch (...) {
+                errs[(size_t)k] = std::current_exception();
+                next.store(npass);
+            }
+        };
+        std::vector<std::thread> th;
+        for (int k = 1; k < nslots; ++k) th.emplace_back(work, k);
+        work(0);
+        for (auto& t : th) t.join();
+        for (auto& e : errs)
+            if (e) std::rethrow_exception(e);
     }
     st.kernel_ms = kms;
     st.levels = levels;

@@ -390,6 +390,33 @@ def test_msbfs_batch_rows(ctx, oracle, kind):
         assert (out[i] == oracle.bfs(row, col, r)).all(), (kind, i, r)
 
 
+@pytest.mark.parametrize("streams", [1, 2, 3])
+def test_msbfs_stream_slots(ctx, oracle, tmp_path, streams):
+    """Batched BFS passes on 1-3 concurrent slots (msbfs.hip: one stream, mask set and distance
+    block per slot, a host thread each): 64-source passes (ms_width 1), every row of a
+    300-source batch with duplicates and out-of-range sources equals the oracle BFS, and the
+    sol_files of the drop-in equal the rows."""
+    rng = np.random.default_rng(900 + streams)
+    n = 12000
+    src, dst = random_graph(rng, "hub", n)
+    g = ctx.load_coo(src, dst, n=n)
+    row, col, _ = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n)
+    g.set_option("ms_width", 1)
+    g.set_option("ms_streams", streams)
+    sources = [int(x) for x in rng.integers(0, n, 290)] + [-1, n, int(src[0]), int(src[0])] + list(range(6))
+    out = g.sssp_batch(sources)
+    exp = {s: oracle.bfs(row, col, s) for s in set(sources)}
+    for i, s in enumerate(sources):
+        assert (out[i] == exp[s]).all(), (streams, i, s)
+    paths = [str(tmp_path / f"m_{i}.txt") for i in range(0, len(sources), 37)]
+    g.sssp_batch_write(sources[::37], paths)
+    for p, s in zip(paths, sources[::37]):
+        assert open(p, "rb").read() == oracle.format_sol(exp[s]), (streams, s)
+    with pytest.raises(Exception):
+        g.set_option("ms_streams", 5)
+    g.close()
+
+
 @pytest.mark.parametrize("width,alpha", [(1, 16), (2, 0), (4, 16), (4, 1e9), (8, 16), (8, 0), (16, 16)])
 def test_msbfs_pass_widths(ctx, oracle, width, alpha):
     """Passes of 64 x W sources (W words per vertex mask): 300 sources cross several
