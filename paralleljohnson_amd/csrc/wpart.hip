@@ -53,7 +53,10 @@ __device__ __forceinline__ int32_t wp_now(const int32_t* p) {
 constexpr int WB = 256;
 constexpr int WSC = 16;        // frontier words a wave screens at once
 constexpr int WP_SERIAL = 8;   // edges a lane relaxes alone
-constexpr u64 WP_LONG = 1024;  // longer row segments: the grid-wide queue
+#ifndef PJ_WP_LONG
+#define PJ_WP_LONG 1024
+#endif
+constexpr u64 WP_LONG = PJ_WP_LONG;  // longer row segments: the grid-wide queue
 constexpr int WP_MAXW = 64;    // largest world size
 constexpr int WP_EB = 40;      // long queue counter: (slots << WP_EB) | edges
 constexpr int WP_TILE = WB * 4;
