@@ -37,15 +37,16 @@ struct TreeCnt {
 
 // Every CSR edge u -> v of a reached row, visited once: short rows by their lane,
 // long rows by the whole wave (lanes over consecutive entries). f(u, du, v, w).
+// (hop != null: only the rows u with hop[u] == lvl, the frontier of a zero-weight level)
 template <typename Off, bool W, typename F>
 __device__ __forceinline__ void for_reached_edges(const Off* __restrict__ row, const u32* __restrict__ col,
                                                   const u32* __restrict__ wt, const int32_t* __restrict__ dist,
-                                                  i64 n, F f) {
+                                                  i64 n, F f, const u32* __restrict__ hop = nullptr, u32 lvl = 0) {
     const int lane = lane_id();
     const i64 stride = (i64)gridDim.x * blockDim.x;
     for (i64 base = (i64)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < n; base += stride) {
         const i64 u = base + lane;
-        const bool ok = u < n && dist[u] < INT_INF;
+        const bool ok = u < n && (!hop || hop[u] == lvl) && dist[u] < INT_INF;
         const int32_t du = ok ? dist[u] : 0;
         const Off b = ok ? row[u] : 0, e = ok ? row[u + 1] : 0;
         const bool lng = ok && e - b > (Off)LONG_ROW;
@@ -86,23 +87,28 @@ __global__ void hop_init_k(const u32* __restrict__ par, i64 n, i64 source, u32* 
         hop[v] = (v == source || par[v] != 0xffffffffu) ? 0u : NO_HOP;
 }
 
-// one level of the zero-weight phase: rows u with hop[u] == lvl parent their zero-weight tight
-// targets that have no hop yet (every writer stores lvl + 1)
+// one level of the zero-weight phase: the rows u with hop[u] == lvl (only those rows'
+// edges are read) parent their zero-weight tight targets that have no hop yet (every
+// writer stores lvl + 1). Levels are enqueued in batches: flags is a ring of 3, level lvl
+// sets flags[lvl % 3] when it parents anything, exits at once when level lvl - 1
+// (flags[(lvl + 2) % 3]) parented nothing, and clears flags[(lvl + 1) % 3] for level lvl + 1.
 template <typename Off>
 __global__ __launch_bounds__(256) void parent_zero_k(const Off* __restrict__ row, const u32* __restrict__ col,
                                                      const u32* __restrict__ wt, const int32_t* __restrict__ dist,
                                                      i64 n, u32 lvl, u32* __restrict__ hop, u32* __restrict__ par,
-                                                     u32* __restrict__ changed) {
+                                                     u32* __restrict__ flags) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) flags[(lvl + 1) % 3] = 0;
+    if (flags[(lvl + 2) % 3] == 0) return;  // (block-uniform)
     u32 any = 0;
     for_reached_edges<Off, true>(row, col, wt, dist, n, [&](i64 u, int32_t du, u32 v, u32 w) {
-        if (w != 0 || hop[u] != lvl || dist[v] != du) return;
+        if (w != 0 || dist[v] != du) return;
         const u32 hv = hop[v];
         if (hv != NO_HOP && hv != lvl + 1) return;
         hop[v] = lvl + 1;
         if (par[v] > (u32)u) atomicMin(&par[v], (u32)u);
         any = 1;
-    });
-    if (any) atomicOr(changed, 1u);
+    }, hop, lvl);
+    if (any) atomicOr(&flags[lvl % 3], 1u);
 }
 
 __global__ void parent_out_k(const u32* __restrict__ par, i64 n, i64 source, int64_t* __restrict__ out) {
@@ -194,15 +200,20 @@ void parent_run(Graph& g, i64 source, u32* par) {
         PJ_HIP(hipMemcpyAsync(hflag.p, flag.p, sizeof(u32), hipMemcpyDeviceToHost, s));
         PJ_HIP(hipStreamSynchronize(s));
         if (!hflag.p[0]) return;
-        DevBuf<u32> hop((size_t)g.n);
+        DevBuf<u32> hop((size_t)g.n), flags(3);
         hop_init_k<<<grid_of(g, g.n), 256, 0, s>>>(par, g.n, source, hop.p);
         PJ_LAUNCH_CHECK();
-        for (u32 lvl = 0;; ++lvl) {  // one level per pass; ends when a level parents nothing
-            PJ_HIP(hipMemsetAsync(flag.p, 0, sizeof(u32), s));
-            parent_zero_k<Off><<<grid_of(g, g.n), 256, 0, s>>>(row, g.col.p, g.w.p, g.dist.p, g.n, lvl, hop.p, par,
-                                                               flag.p);
-            PJ_LAUNCH_CHECK();
-            PJ_HIP(hipMemcpyAsync(hflag.p, flag.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+        const u32 f0[3] = {0, 0, 1};  // "level -1" parented something
+        PJ_HIP(hipMemcpyAsync(flags.p, f0, sizeof(f0), hipMemcpyHostToDevice, s));
+        // levels in batches of 8 between host checks (a level whose predecessor parented
+        // nothing exits at once); ends when a level parents nothing
+        for (u32 lvl = 0;;) {
+            for (int b = 0; b < 8; ++b, ++lvl) {
+                parent_zero_k<Off><<<grid_of(g, g.n), 256, 0, s>>>(row, g.col.p, g.w.p, g.dist.p, g.n, lvl, hop.p,
+                                                                   par, flags.p);
+                PJ_LAUNCH_CHECK();
+            }
+            PJ_HIP(hipMemcpyAsync(hflag.p, flags.p + (lvl - 1) % 3, sizeof(u32), hipMemcpyDeviceToHost, s));
             PJ_HIP(hipStreamSynchronize(s));
             if (!hflag.p[0]) break;
         }
