@@ -723,6 +723,7 @@ struct WPart {
                                    // used in turn by every solve: each was recomputed per solve)
     DevBuf<int32_t> dist, cand;
     DevBuf<u64> touched, fr, frn, mb, stat;
+    DevBuf<u32> rl_inv;   // (relabeled blocks) old local id -> new local id; empty: input ids
     i64 exch_bytes = 0;  // the engine view's send + recv buffers (sized to the largest round)
     DevBuf<u32> lq_v;
     DevBuf<u64> lq_b, lq_e;
@@ -879,6 +880,79 @@ __global__ void wp_filter_write_k(const u32* __restrict__ src, const u32* __rest
     }
 }
 
+
+// ---- per-block degree order (PJ_WP_RELABEL) --------------------------------------
+// delta.hip's relabel (hot distances share lines) restated for the partition: inside
+// every block, vertices by out-degree descending (ties by input id). A vertex keeps its
+// block, so the owner of a new id is the owner of the old one and the block geometry,
+// the exchange and the pulls' byte map are unchanged; every rank derives the same map
+// from the degrees of ALL vertices (each builder sees every entry: the generator's
+// tuples, the parsed file, the full graph) and keeps only its block's inverse. The
+// source is mapped on entry, distances are mapped back on the way out.
+#ifndef PJ_WP_RELABEL
+#define PJ_WP_RELABEL 0
+#endif
+__global__ void wp_deg_key_k(const u32* __restrict__ deg, i64 n, u32 maxdeg, u32* __restrict__ key,
+                             u32* __restrict__ ids) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
+        key[v] = maxdeg - deg[v];
+        ids[v] = (u32)v;
+    }
+}
+__global__ void wp_blk_key_k(const u32* __restrict__ ids, i64 n, i64 block, u32* __restrict__ key) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
+        key[i] = (u32)((i64)ids[i] / block);
+}
+__global__ void wp_inv_k(const u32* __restrict__ order, i64 n, u32* __restrict__ inv) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
+        inv[order[i]] = (u32)i;
+}
+// new local row l = old local row order[lo + l] - lo: its degree, and the old local -> new local map
+__global__ void wp_newdeg_k(const u32* __restrict__ order, const u32* __restrict__ inv, const u64* __restrict__ row,
+                            i64 lo, i64 nl, u32* __restrict__ ndeg, u32* __restrict__ linv) {
+    for (i64 l = (i64)blockIdx.x * blockDim.x + threadIdx.x; l < nl; l += (i64)gridDim.x * blockDim.x) {
+        const i64 o = (i64)order[lo + l] - lo;
+        ndeg[l] = (u32)(row[o + 1] - row[o]);
+        linv[l] = (u32)((i64)inv[lo + l] - lo);
+    }
+}
+// copy the rows in the new order, columns through the global map (a wave per row)
+__global__ __launch_bounds__(256) void wp_copy_rows_k(const u32* __restrict__ order, const u32* __restrict__ inv,
+                                                      const u64* __restrict__ row, const u32* __restrict__ col,
+                                                      const u32* __restrict__ w, const u64* __restrict__ nrow, i64 lo,
+                                                      i64 nl, u32* __restrict__ ncol, u32* __restrict__ nw) {
+    const int lane = lane_id();
+    for (i64 l = ((i64)blockIdx.x * blockDim.x + threadIdx.x) / WAVE; l < nl;
+         l += (i64)gridDim.x * blockDim.x / WAVE) {
+        const i64 o = (i64)order[lo + l] - lo;
+        const u64 b = row[o], e = row[o + 1], nb = nrow[l];
+        for (u64 k = b + (u64)lane; k < e; k += WAVE) {
+            ncol[nb + (k - b)] = inv[col[k]];
+            nw[nb + (k - b)] = w[k];
+        }
+    }
+}
+__global__ void wp_deg_coo_k(const u32* __restrict__ src, i64 m, u32* __restrict__ deg) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x)
+        atomicAdd(&deg[src[i]], 1u);
+}
+__global__ void wp_deg_row_k(const void* row, bool off64, i64 n, u32* __restrict__ deg) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x)
+        deg[v] = off64 ? (u32)(((const u64*)row)[v + 1] - ((const u64*)row)[v])
+                       : ((const u32*)row)[v + 1] - ((const u32*)row)[v];
+}
+__global__ void wp_max_k(const u32* __restrict__ in, i64 n, u32* __restrict__ out) {
+    u32 m = 0;
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) m = max(m, in[i]);
+    m = wave_max(m);
+    if (lane_id() == 0 && m) atomicMax(out, m);
+}
+__global__ void wp_unlabel_k(const int32_t* __restrict__ dist, const u32* __restrict__ linv, i64 nl,
+                             int32_t* __restrict__ out) {
+    for (i64 l = (i64)blockIdx.x * blockDim.x + threadIdx.x; l < nl; l += (i64)gridDim.x * blockDim.x)
+        out[l] = dist[linv[l]];
+}
+
 // Per-block weighted Kronecker build: every rank enumerates the tuples of the
 // generator spec (kron.h, both directions, the tuple's weight on each), keeps the
 // entries whose source lies in its block, in enumeration order (= the single-GPU
@@ -906,6 +980,18 @@ __global__ __launch_bounds__(256) void wp_kron_count_k(int scale, u64 seed, Perm
     if (threadIdx.x == 0) {
         bcnt[blockIdx.x] = c;
         atomicAdd(wsum, ws);
+    }
+}
+__global__ __launch_bounds__(256) void wp_kron_deg_k(int scale, u64 seed, PermKeys pk, u64 M, u32* __restrict__ deg) {
+    const u64 base = (u64)blockIdx.x * 256 * WK_IPT;
+    for (int k = 0; k < WK_IPT; ++k) {
+        const u64 i = base + (u64)k * 256 + threadIdx.x;
+        if (i < M) {
+            u32 pu, pv;
+            kron_tuple(scale, seed, pk, i, pu, pv);
+            atomicAdd(&deg[pu], 1u);
+            atomicAdd(&deg[pv], 1u);
+        }
     }
 }
 __global__ __launch_bounds__(256) void wp_kron_write_k(int scale, u64 seed, PermKeys pk, u64 M, u32 lo, u32 hi,
@@ -943,6 +1029,62 @@ __global__ __launch_bounds__(256) void wp_kron_write_k(int scale, u64 seed, Perm
 
 }  // namespace
 
+namespace {
+// Relabel a built block (rows, col, w in input ids) given the degrees of every vertex.
+void wpart_relabel(WPart& p, DevBuf<u32>& deg) {
+    hipStream_t s = p.ctx->stream;
+    const i64 n = p.n;
+    if (n == 0) return;
+    const unsigned grid = p.grid();
+    DevBuf<u32> mx(1);
+    PJ_HIP(hipMemsetAsync(mx.p, 0, sizeof(u32), s));
+    wp_max_k<<<grid_for(n, 256, grid), 256, 0, s>>>(deg.p, n, mx.p);
+    PJ_LAUNCH_CHECK();
+    u32 maxdeg = 0;
+    PJ_HIP(hipMemcpyAsync(&maxdeg, mx.p, sizeof(u32), hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    DevBuf<u32> key((size_t)n), kalt((size_t)n), ids((size_t)n), valt((size_t)n);
+    wp_deg_key_k<<<grid_for(n, 256, grid), 256, 0, s>>>(deg.p, n, maxdeg, key.p, ids.p);
+    PJ_LAUNCH_CHECK();
+    deg.release();
+    SortWs ws;
+    int bits = 1;
+    while (bits < 32 && ((u64)1 << bits) <= (u64)maxdeg) ++bits;
+    u32 *kr, *vr;
+    radix_sort_pairs<u32>(key.p, kalt.p, ids.p, valt.p, n, bits, ws, s, &kr, &vr);
+    u32* kfree = kr == key.p ? kalt.p : key.p;  // the key buffer not holding the result
+    wp_blk_key_k<<<grid_for(n, 256, grid), 256, 0, s>>>(vr, n, p.block, kr);
+    PJ_LAUNCH_CHECK();
+    int bb = 1;
+    while (bb < 32 && ((u64)1 << bb) <= (u64)p.world) ++bb;
+    u32* valt2 = vr == ids.p ? valt.p : ids.p;
+    u32 *kr2, *order;
+    radix_sort_pairs<u32>(kr, kfree, vr, valt2, n, bb, ws, s, &kr2, &order);
+    u32* inv = order == ids.p ? valt.p : ids.p;  // the free value buffer
+    wp_inv_k<<<grid_for(n, 256, grid), 256, 0, s>>>(order, n, inv);
+    PJ_LAUNCH_CHECK();
+    const i64 nl = p.nl;
+    DevBuf<u32> ndeg((size_t)std::max<i64>(nl, 1));
+    p.rl_inv.alloc((size_t)std::max<i64>(nl, 1));
+    DevBuf<u64> nrow((size_t)nl + 1);
+    if (nl > 0) {
+        wp_newdeg_k<<<grid_for(nl, 256, grid), 256, 0, s>>>(order, inv, p.row.p, p.lo, nl, ndeg.p, p.rl_inv.p);
+        PJ_LAUNCH_CHECK();
+        ScanWs sw;
+        exclusive_scan_u32(ndeg.p, nrow.p, nl, sw, s);
+        DevBuf<u32> ncol((size_t)std::max<i64>(p.nnz_local, 1)), nw((size_t)std::max<i64>(p.nnz_local, 1));
+        wp_copy_rows_k<<<grid_for(nl * WAVE, 256, grid), 256, 0, s>>>(order, inv, p.row.p, p.col.p, p.w.p, nrow.p,
+                                                                      p.lo, nl, ncol.p, nw.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipStreamSynchronize(s));
+        p.row = std::move(nrow);
+        p.col = std::move(ncol);
+        p.w = std::move(nw);
+    }
+    PJ_HIP(hipStreamSynchronize(s));
+}
+}  // namespace
+
 WPart* wpart_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, int rank, int world) {
     hipStream_t s = ctx.stream;
     const u64 M = (u64)edgefactor << scale;
@@ -978,6 +1120,13 @@ WPart* wpart_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, 
     build_graph_from_coo(local, ls, ld, &lw, m, p->nl, false);
     wpart_cut(p.get(), local, 0, M > 0 ? (double)wsum / (double)(2 * M) : 1.0);
     p->symmetric = true;  // both directions of every tuple, same weight
+    if (PJ_WP_RELABEL && nb > 0) {  // every vertex's degree: both entries of every tuple
+        DevBuf<u32> deg((size_t)p->n);
+        PJ_HIP(hipMemsetAsync(deg.p, 0, deg.bytes(), s));
+        wp_kron_deg_k<<<(unsigned)nb, 256, 0, s>>>(scale, seed, pk, M, deg.p);
+        PJ_LAUNCH_CHECK();
+        wpart_relabel(*p, deg);
+    }
     return p.release();
 }
 
@@ -987,6 +1136,12 @@ WPart* wpart_from_graph(Graph& g, int rank, int world) {
     const u64 wsum = weight_sum(g.w.p, g.nnz, p->grid(), g.ctx->stream);
     wpart_cut(p.get(), g, p->lo, g.nnz > 0 ? (double)wsum / (double)g.nnz : 1.0);
     p->symmetric = g.symmetric;
+    if (PJ_WP_RELABEL && g.n > 0) {
+        DevBuf<u32> deg((size_t)g.n);
+        wp_deg_row_k<<<grid_for(g.n, 256, p->grid()), 256, 0, g.ctx->stream>>>(g.row_ptr(), g.off64, g.n, deg.p);
+        PJ_LAUNCH_CHECK();
+        wpart_relabel(*p, deg);
+    }
     return p.release();
 }
 
@@ -1019,6 +1174,15 @@ WPart* wpart_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>&
         PJ_LAUNCH_CHECK();
         PJ_HIP(hipStreamSynchronize(s));
     }
+    DevBuf<u32> deg;
+    if (PJ_WP_RELABEL && n > 0) {  // every vertex's out-degree, from the whole COO
+        deg.alloc((size_t)n);
+        PJ_HIP(hipMemsetAsync(deg.p, 0, deg.bytes(), s));
+        if (nnz > 0) {
+            wp_deg_coo_k<<<grid_for(nnz, 256, p->grid()), 256, 0, s>>>(src.p, nnz, deg.p);
+            PJ_LAUNCH_CHECK();
+        }
+    }
     src.release();
     dst.release();
     w.release();
@@ -1026,6 +1190,7 @@ WPart* wpart_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>&
     local.ctx = &ctx;
     build_graph_from_coo(local, ls, ld, &lw, m, p->nl, false);
     wpart_cut(p.get(), local, 0, nnz > 0 ? (double)wsum / (double)nnz : 1.0);
+    if (deg.p) wpart_relabel(*p, deg);
     return p.release();
 }
 
@@ -1159,7 +1324,14 @@ int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
     if (p.world > 1 && p.n > 0)
         PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.cand.p), INT_INF, (size_t)p.n, s));
     if (source >= 0 && source < p.n) {
-        wp_seed_k<<<1, 1, 0, s>>>(p.args(), source);
+        i64 src = source;
+        if (p.rl_inv.p && source >= p.lo && source < p.hi) {  // relabeled block: the source's new id
+            u32 x = 0;
+            PJ_HIP(hipMemcpyAsync(&x, p.rl_inv.p + (source - p.lo), sizeof(u32), hipMemcpyDeviceToHost, s));
+            PJ_HIP(hipStreamSynchronize(s));
+            src = p.lo + (i64)x;
+        }
+        wp_seed_k<<<1, 1, 0, s>>>(p.args(), src);
         PJ_LAUNCH_CHECK();
     }
     PJ_HIP(hipStreamSynchronize(s));
@@ -1247,7 +1419,16 @@ void wpart_reach(WPart& p, i64* out2) {
 }
 
 void wpart_copy_dist(WPart& p, int32_t* host) {
-    if (p.nl > 0) PJ_HIP(hipMemcpy(host, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToHost));
+    if (p.nl <= 0) return;
+    if (p.rl_inv.p) {  // back to input ids
+        DevBuf<int32_t> o((size_t)p.nl);
+        wp_unlabel_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, p.ctx->stream>>>(p.dist.p, p.rl_inv.p, p.nl, o.p);
+        PJ_LAUNCH_CHECK();
+        PJ_HIP(hipMemcpyAsync(host, o.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToHost, p.ctx->stream));
+        PJ_HIP(hipStreamSynchronize(p.ctx->stream));
+        return;
+    }
+    PJ_HIP(hipMemcpy(host, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToHost));
 }
 
 // ------------------------------------------------------------ engine view ---
@@ -1330,7 +1511,12 @@ void wpart_gather_dist(WPart& p, Comm& comm, int32_t* out) {
     hipStream_t s = p.ctx->stream;
     DevBuf<int32_t> own((size_t)p.block), all((size_t)p.world * (size_t)p.block);
     PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(own.p), INT_INF, (size_t)p.block, s));
-    if (p.nl) PJ_HIP(hipMemcpyAsync(own.p, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToDevice, s));
+    if (p.nl && p.rl_inv.p) {  // relabeled block: back to input ids
+        wp_unlabel_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, s>>>(p.dist.p, p.rl_inv.p, p.nl, own.p);
+        PJ_LAUNCH_CHECK();
+    } else if (p.nl) {
+        PJ_HIP(hipMemcpyAsync(own.p, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToDevice, s));
+    }
     comm.allgather(own.p, all.p, sizeof(int32_t) * (size_t)p.block, s);
     if (out && p.n) PJ_HIP(hipMemcpyAsync(out, all.p, sizeof(int32_t) * (size_t)p.n, hipMemcpyDeviceToHost, s));
     PJ_HIP(hipStreamSynchronize(s));
