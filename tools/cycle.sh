@@ -11,6 +11,7 @@
 #   probe:<cmd>   any python command line under a 240 s limit (e.g. probe:tools/stats_probe.py 26 3)
 #   vtests:<v>:<pytest args>  -m gpu tests under the libpj build variant <v>
 #   ktp:<cmd>     rocprofv3 kernel trace + stats of any python command line -> kt_<name>/
+#   abp:<v1+v2..>:<python args>  interleaved A/B of any probe under build variants -> abp_<v>.<pass>.log
 #   ab:<v1+v2..>  interleaved A/B (AB_PASSES times, default 2) of the k26w bench line under libpj
 #                 build variants (lib/variants/<v>/libpj.so; "default" = the main build)
 # Output under gpurun_out/TAG.
@@ -61,6 +62,17 @@ for st in "${LIST[@]}"; do
       kn=kt_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-30)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$kn" -o run -- python3 -u $arg \
         > "$OUT/$kn.log" 2>&1 || { echo "ktp failed: $arg"; tail "$OUT/$kn.log"; exit 1; } ;;
+    abp)
+      vl=${arg%%:*}; cmd=${arg#*:}
+      IFS='+' read -ra VS <<< "$vl"
+      for pass in $(seq 1 ${AB_PASSES:-2}); do
+        for v in "${VS[@]}"; do
+          if [ "$v" != default ]; then export PJ_LIB_OVERRIDE=$PWD/paralleljohnson_amd/lib/variants/$v/libpj.so; else unset PJ_LIB_OVERRIDE; fi
+          timeout -k 10 240 python3 -u $cmd > "$OUT/abp_$v.$pass.log" 2>&1 || { echo "abp $v failed"; tail -5 "$OUT/abp_$v.$pass.log"; exit 1; }
+          echo "== $v $pass"; grep -v "^Warn\|amdgpu.ids" "$OUT/abp_$v.$pass.log" | tail -4
+        done
+      done
+      unset PJ_LIB_OVERRIDE ;;
     ab)
       IFS='+' read -ra VS <<< "$arg"
       for pass in $(seq 1 ${AB_PASSES:-2}); do
