@@ -14,6 +14,7 @@
 #   abp:<v1+v2..>:<python args>  interleaved A/B of any probe under build variants -> abp_<v>.<pass>.log
 #   ab:<v1+v2..>  interleaved A/B (AB_PASSES times, default 2) of the k26w bench line under libpj
 #                 build variants (lib/variants/<v>/libpj.so; "default" = the main build)
+# Inside a step's arguments "~" stands for a space and "^" for a comma (STEPS is one word).
 # Output under gpurun_out/TAG.
 set -o pipefail
 TAG=${1:?tag}; STEPS=${2:?steps}; shift 2
@@ -22,6 +23,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 IFS=',' read -ra LIST <<< "$STEPS"
 for st in "${LIST[@]}"; do
   name=${st%%:*}; arg=""; [[ "$st" == *:* ]] && arg=${st#*:}
+  arg=${arg//\~/ }; arg=${arg//^/,}
   echo "== $name $arg"
   case $name in
     tests)
