@@ -172,8 +172,15 @@ int pj_sample_roots(const pj_graph* g, uint64_t seed, int n, int64_t* roots, int
  * run delta-stepping. dist_out (host, n int32) may be NULL: the result then
  * stays on the device (pj_copy_dist fetches it). */
 int pj_sssp(pj_graph* g, int64_t source, int32_t* dist_out);
-/* Copy the last result to the host. */
+/* Copy the last result to the host. Pageable memory goes through pinned
+ * staging slots on up to 8 host threads; memory pinned with pj_host_pin is
+ * written by one direct DMA copy. */
 int pj_copy_dist(pj_graph* g, int32_t* dist_out);
+/* Pin (page-lock) host memory for the device -> host copies of pj_copy_dist /
+ * pj_sssp, e.g. from a helper thread while the GPU builds the graph; the pages
+ * stay pinned until pj_host_unpin (or process exit). No reference counterpart. */
+int pj_host_pin(void* p, size_t bytes);
+int pj_host_unpin(void* p);
 /* Device pointer to the last result (int32[n]); valid until the next solve. */
 const int32_t* pj_dist_device(pj_graph* g);
 /* Batched multi-source (Johnson-style all-pairs rows): dist_out is n_src x n

@@ -102,6 +102,8 @@ _SIGS = {
     "pj_sssp": ([_P, _I64, _P], _INT),
     "pj_copy_dist": ([_P, _P], _INT),
     "pj_dist_device": ([_P], _P),
+    "pj_host_pin": ([_P, ctypes.c_size_t], _INT),
+    "pj_host_unpin": ([_P], _INT),
     "pj_sssp_batch": ([_P, _P, _INT, _P], _INT),
     "pj_sssp_batch_write": ([_P, _P, _INT, _P, _INT], _INT),
     "pj_device_count": ([_P], _INT),

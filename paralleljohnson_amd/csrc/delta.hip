@@ -345,11 +345,8 @@ __device__ __forceinline__ u64 v2_slot_edges(const V2Line* sl) {
 // round's push cost, read from lsplit):
 //   PJ_V2_MARK 0: a returning atomicOr, then the lsplit read of a newly marked
 //                 target (two dependent round trips after the distance);
-//   PJ_V2_MARK 1: the lsplit read issued beside the returning atomicOr (one);
-//   PJ_V2_MARK 2: the mark word read (agent scope) beside the distance, a
-//                 returnless atomicOr when the bit is clear, the lsplit read beside
-//                 it: the count may include a target two lanes marked at once
-//                 (a pull-decision estimate; never zero for a non-empty frontier).
+//   PJ_V2_MARK 1: the lsplit read issued beside the returning atomicOr (one).
+// (A returnless atomicOr after a plain read of the mark word ran 5% slower, r4a.)
 #ifndef PJ_V2_MARK
 #define PJ_V2_MARK 0
 #endif
@@ -380,14 +377,9 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
         for (int j = 0; j < N; ++j) ok[j] = ok[j] && !((sw[j] >> (t[j] & 63)) & 1ull);
     }
     int32_t cd[N];
-    u64 fw[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         cd[j] = ok[j] ? dist_now(a.dist + t[j]) : 0;
-        if (LIGHT && PJ_V2_MARK == 2)
-            fw[j] = ok[j] && (int32_t)nd[j] < a.hi
-                        ? __hip_atomic_load(fout + (t[j] >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : ~0ull;
     }
     if (PJ_V2_STATS)
         for (int j = 0; j < N; ++j)
@@ -404,20 +396,7 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
     }
     if (!LIGHT) return 0u;
     u32 newc = 0;
-    if (PJ_V2_MARK == 2) {
-        u32 ls[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            mk[j] = mk[j] && !((fw[j] >> (t[j] & 63)) & 1ull);
-            if (mk[j]) atomicOr(fout + (t[j] >> 6), 1ull << (t[j] & 63));
-            ls[j] = mk[j] ? a.lsplit[t[j]] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            newc += mk[j];
-            fe += ls[j];
-        }
-    } else if (PJ_V2_MARK == 1) {
+    if (PJ_V2_MARK == 1) {
         u64 old[N];
         u32 ls[N];
 #pragma unroll
@@ -489,13 +468,10 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
 #ifndef PJ_V2_HWF
 #define PJ_V2_HWF 0
 #endif
-// light pull rounds: new members' degree sums with a lane per vertex (v2_pull_light_body)
-#ifndef PJ_V2_MBPAR
-#define PJ_V2_MBPAR 0
-#endif
-// light pull candidates filtered by the row's lightest weight (V2Args::w1)
+// light pull candidates filtered by the row's lightest weight (V2Args::w1): k26w 438.8 ->
+// 451.0 / 448.6 GTEPS interleaved (r4a, profiles/r04/ab_r4a.txt)
 #ifndef PJ_V2_LWF
-#define PJ_V2_LWF 0
+#define PJ_V2_LWF 1
 #endif
 constexpr u32 V2_HCH = PJ_V2_HCH > 0 ? PJ_V2_HCH : 256;
 __device__ __forceinline__ void v2_hub_append(const V2Args& a, int hs, bool hub, u32 v, int32_t du, u64 b, u64& e) {
@@ -1152,10 +1128,9 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
     const i64 nsc = (a.nwords + PSC - 1) / PSC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
         const i64 gbase = sc * PSC;
-        // the frontier joins the members; new members add their heavy / light degrees.
-        // PJ_V2_MBPAR 1: lane = vertex of each of the PSC words (the loads of all words
-        // issued together); 0: a lane walks the bits of its word serially (one dependent
-        // round trip per new member: ~35 per word in a band-start pull of the tail)
+        // the frontier joins the members; new members add their heavy / light degrees (a
+        // lane walks the bits of its word; a lane per vertex of the PSC words with the loads
+        // issued together, PJ_V2_MBPAR in round 4, ran the pull rounds 1.5x slower, r4a)
         u64 nmw = 0;
         if (lane < PSC && gbase + lane < a.nwords) {
             const u64 f = fin[gbase + lane];
@@ -1165,38 +1140,13 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                 if (nmw) a.mb[gbase + lane] = old | f;
             }
         }
-        if (PJ_V2_MBPAR) {
-            if (__ballot(nmw != 0)) {
-                constexpr int MB4 = 4;
-#pragma unroll
-                for (int k0 = 0; k0 < PSC; k0 += MB4) {
-                    u64 rb[MB4], re[MB4], ls[MB4];
-                    bool on[MB4];
-#pragma unroll
-                    for (int j = 0; j < MB4; ++j) {
-                        const u64 w = __shfl(nmw, k0 + j, 64);
-                        on[j] = (w >> lane) & 1ull;
-                        const i64 v = (gbase + k0 + j) * 64 + lane;
-                        rb[j] = on[j] ? (u64)row[v] : 0;
-                        re[j] = on[j] ? (u64)row[v + 1] : 0;
-                        ls[j] = on[j] ? a.lsplit[v] : 0;
-                    }
-#pragma unroll
-                    for (int j = 0; j < MB4; ++j) {
-                        mh += re[j] - rb[j] - ls[j];
-                        ml += ls[j];
-                    }
-                }
-            }
-        } else {
-            while (nmw) {
-                const int b = __ffsll((long long)nmw) - 1;
-                nmw &= nmw - 1;
-                const i64 v = (gbase + lane) * 64 + b;
-                const u64 rb = (u64)row[v], ls = a.lsplit[v];
-                mh += (u64)row[v + 1] - rb - ls;
-                ml += ls;
-            }
+        while (nmw) {
+            const int b = __ffsll((long long)nmw) - 1;
+            nmw &= nmw - 1;
+            const i64 v = (gbase + lane) * 64 + b;
+            const u64 rb = (u64)row[v], ls = a.lsplit[v];
+            mh += (u64)row[v + 1] - rb - ls;
+            ml += ls;
         }
         u64 mytodo = 0;
 #pragma unroll

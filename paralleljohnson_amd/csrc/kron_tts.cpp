@@ -12,13 +12,19 @@
 // stdout: one line "phases_s <create> <build> <solve> <d2h> <write> <launch> <teardown>
 // root <source> exit_ns <t>" (the parent times the whole process itself; launch = the
 // parent's PJ_TTS_LAUNCH_NS (CLOCK_MONOTONIC) -> main, teardown = graph + context
-// destruction, exit_ns = CLOCK_MONOTONIC just before main returns, so the parent can
+// destruction (PJ_TTS_TEARDOWN=1, else ~0), exit_ns = CLOCK_MONOTONIC just before main returns, so the parent can
 // report the process exit too).
 //
-// The n-entry host distance buffer is allocated without zero-filling and its pages
-// are faulted in by host threads while the GPU builds the graph (a zero-filled
-// std::vector cost ~0.05 s of page faults on the critical path at s26: 268 MB).
+// The n-entry host distance buffer is allocated without zero-filling, its pages are
+// faulted in by host threads and then pinned (pj_host_pin) while the GPU builds the
+// graph, so the D2H is one DMA copy (a zero-filled std::vector cost ~0.05 s of page
+// faults on the critical path at s26: 268 MB; the staged copy into pageable memory
+// 0.056 s, r4a). After the sol_file is closed and the phases are printed the process
+// ends with _exit: the HIP runtime's teardown at exit cost 0.12 s and the graph and
+// context destruction 0.03 s (r4a) that no result depends on; PJ_TTS_TEARDOWN=1
+// destroys the graph and the context and returns from main instead.
 #include <sys/mman.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cstdio>
@@ -63,7 +69,21 @@ struct HostRows {
         for (auto& x : th) x.join();
         th.clear();
     }
-    ~HostRows() { join(); }  // (the mapping goes with the process)
+    // after pj_create: one thread waits for the faulting threads, then pins the rows
+    std::thread pinner;
+    bool pinned = false;
+    void pin() {
+        if (!p) return;
+        pinner = std::thread([this] {
+            join();
+            pinned = pj_host_pin(p, bytes) == PJ_OK;
+        });
+    }
+    void finish() {
+        if (pinner.joinable()) pinner.join();
+        join();
+    }
+    ~HostRows() { finish(); }  // (the mapping goes with the process)
 };
 
 int main(int argc, char** argv) {
@@ -80,6 +100,7 @@ int main(int argc, char** argv) {
     const double t0 = (double)t0n * 1e-9;
     pj_ctx* ctx = nullptr;
     if (pj_create(0, &ctx) != PJ_OK) return fail("pj_create");
+    rows.pin();
     const double t1 = now_s();
     pj_graph* g = nullptr;
     if (pj_generate_kronecker(ctx, scale, std::atoi(argv[2]), std::strtoull(argv[3], nullptr, 10), std::atoi(argv[4]),
@@ -98,7 +119,7 @@ int main(int argc, char** argv) {
     }
     if (pj_sssp(g, source, nullptr) != PJ_OK) return fail("pj_sssp");
     const double t3 = now_s();
-    rows.join();
+    rows.finish();
     std::vector<int32_t> fallback;
     int32_t* dist = rows.p;
     if (!dist || (size_t)n * sizeof(int32_t) > rows.bytes) {
@@ -109,11 +130,16 @@ int main(int argc, char** argv) {
     const double t4 = now_s();
     if (pj_write_sol(dist, n, argv[6], 1) != PJ_OK) return fail("pj_write_sol");
     const double t5 = now_s();
-    pj_graph_destroy(g);
-    pj_destroy(ctx);
+    const bool teardown = std::getenv("PJ_TTS_TEARDOWN") && std::atoi(std::getenv("PJ_TTS_TEARDOWN"));
+    if (teardown) {
+        if (rows.pinned) pj_host_unpin(rows.p);
+        pj_graph_destroy(g);
+        pj_destroy(ctx);
+    }
     const long long t6n = now_ns();
     std::printf("phases_s %.4f %.4f %.4f %.4f %.4f %.4f %.4f root %lld exit_ns %lld\n", t1 - t0, t2 - t1, t3 - t2,
                 t4 - t3, t5 - t4, launch_s, (double)t6n * 1e-9 - t5, (long long)source, t6n);
     std::fflush(stdout);
+    if (!teardown) _exit(0);
     return 0;
 }
