@@ -130,6 +130,16 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
     return x;
 }
 
+// PJ_MS_FZ 1: a bitmap Z (one bit per vertex, "F[v] is nonzero", written whole by every
+// level, a wave's 64 vertices as one word) beside the masks: the pull probes Z[u] (n / 8
+// bytes, cache-resident) before the 8W-byte F[u] and skips zero rows, the push skips
+// waves whose 64 vertices have no frontier, and a pull level stores only nonzero Fn rows
+// (readers consult Zn first).
+#ifndef PJ_MS_FZ
+#define PJ_MS_FZ 0
+#endif
+__device__ __forceinline__ bool zbit(const u64* __restrict__ Z, u32 u) { return (Z[u >> 6] >> (u & 63)) & 1ull; }
+
 #ifndef PJ_MS_GPC
 #define PJ_MS_GPC 8  // level-kernel workgroups per CU (MS1024: 12.8 -> 12.4 ms with MS_U 4, round 3)
 #endif
@@ -138,7 +148,7 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
 // the end of the pass, measured 0.72 ms: that loop's stores are mostly partial)
 __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __restrict__ F, i64 nw,
                                                 int32_t* __restrict__ dist, i64 nb_dist, MsCtl* ctl,
-                                                int64_t* host_done) {
+                                                int64_t* host_done, u64* __restrict__ Z, i64 nzw) {
     const i64 tid = (i64)blockIdx.x * MB + threadIdx.x, nth = (i64)gridDim.x * MB;
     if (tid == 0) {
         for (int i = 0; i < 3; ++i) {
@@ -152,6 +162,7 @@ __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __rest
         V[i] = 0;
         F[i] = 0;
     }
+    for (i64 i = tid; i < nzw; i += nth) Z[i] = 0;
     int4* d4 = reinterpret_cast<int4*>(dist);
     const i64 n4 = nb_dist / 4;
     for (i64 i = tid; i < n4; i += nth) d4[i] = make_int4(INT_INF, INT_INF, INT_INF, INT_INF);
@@ -161,13 +172,15 @@ __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __rest
 // one thread per source (sources may repeat: atomics on the masks)
 template <typename Off>
 __global__ void ms_sources_k(const int64_t* __restrict__ src, int ns, int W, i64 n, const Off* __restrict__ row,
-                             u64* __restrict__ V, u64* __restrict__ F, int32_t* __restrict__ dist, MsCtl* ctl) {
+                             u64* __restrict__ V, u64* __restrict__ F, int32_t* __restrict__ dist, MsCtl* ctl,
+                             u64* __restrict__ Z) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ns) return;
     const int64_t s = src[i];
     if (s < 0 || s >= n) return;
     atomicOr(&V[s * W + (i >> 6)], 1ull << (i & 63));
     atomicOr(&F[s * W + (i >> 6)], 1ull << (i & 63));
+    atomicOr(&Z[s >> 6], 1ull << (s & 63));
     dist[(i64)i * n + s] = 0;
     ctl->active[2] = 1;  // "level -1" found the sources
     atomicAdd(&ctl->fedges[2][0][0], (u64)(row[s + 1] - row[s]));
@@ -221,14 +234,20 @@ __device__ __forceinline__ void ms_write_dist(const Mask<W>& newb, int32_t* __re
 template <typename Off, int W>
 __global__ __launch_bounds__(MB) void ms_push_k(i64 n, const Off* __restrict__ row, const u32* __restrict__ col,
                                                 const u64* __restrict__ F, u64* __restrict__ Fn, int32_t L,
-                                                u64 push_max, const MsCtl* ctl) {
+                                                u64 push_max, const MsCtl* ctl, const u64* __restrict__ Z) {
     if (!ms_live(ctl, L) || !ms_is_push(ctl, L, push_max)) return;
     const int lane = lane_id();
     const i64 nwaves = (i64)gridDim.x * (MB / WAVE);
     for (i64 base = ((i64)blockIdx.x * (MB / WAVE) + wave_id()) * 64; base < n; base += nwaves * 64) {
         const i64 u = base + lane;
         Mask<W> f{};
-        if (u < n) f = mload<W>(F, u);
+        if (PJ_MS_FZ) {
+            const u64 zw = Z[base >> 6];
+            if (!zw) continue;
+            if ((zw >> lane) & 1ull) f = mload<W>(F, u);
+        } else if (u < n) {
+            f = mload<W>(F, u);
+        }
         const bool act = many<W>(f);
         if (!__ballot(act)) continue;
         Off b = 0, e = 0;
@@ -264,7 +283,7 @@ __global__ __launch_bounds__(MB) void ms_push_k(i64 n, const Off* __restrict__ r
 template <typename Off, int W>
 __global__ __launch_bounds__(MB) void ms_fin_k(i64 n, const Off* __restrict__ row, u64* __restrict__ V,
                                                u64* __restrict__ Fn, int32_t* __restrict__ dist, int32_t L,
-                                               Mask<W> smask, u64 push_max, MsCtl* ctl) {
+                                               Mask<W> smask, u64 push_max, MsCtl* ctl, u64* __restrict__ Zn) {
     if (!ms_live(ctl, L) || !ms_is_push(ctl, L, push_max)) return;
     __shared__ u64 red[MB / WAVE];
     const int lane = lane_id();
@@ -275,7 +294,10 @@ __global__ __launch_bounds__(MB) void ms_fin_k(i64 n, const Off* __restrict__ ro
         Mask<W> fn{};
         if (v < n) fn = mload<W>(Fn, v);
         const bool act = many<W>(fn);
-        if (!__ballot(act)) continue;
+        if (!__ballot(act)) {
+            if (PJ_MS_FZ && lane == 0) Zn[base >> 6] = 0;
+            continue;
+        }
         Mask<W> newb{};
         bool anynew = false;
         if (act) {
@@ -294,6 +316,10 @@ __global__ __launch_bounds__(MB) void ms_fin_k(i64 n, const Off* __restrict__ ro
             }
         }
         found_any |= anynew ? 1ull : 0ull;
+        if (PJ_MS_FZ) {
+            const u64 zb = __ballot(anynew);
+            if (lane == 0) Zn[base >> 6] = zb;
+        }
         ms_write_dist<W>(newb, dist, n, v, L + 1);
     }
     fe = block_sum<MB / WAVE>(fe, red);
@@ -306,7 +332,8 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
                                                  const Off* __restrict__ row, u64* __restrict__ V,
                                                  const u64* __restrict__ F, u64* __restrict__ Fn,
                                                  int32_t* __restrict__ dist, int32_t L, Mask<W> smask,
-                                                 u64 push_max, MsCtl* ctl) {
+                                                 u64 push_max, MsCtl* ctl, const u64* __restrict__ Z,
+                                                 u64* __restrict__ Zn) {
     // level L computes distance L+1 from the frontier of level L-1 (pull form)
     if (!ms_live(ctl, L) || ms_is_push(ctl, L, push_max)) return;
     __shared__ u64 red[MB / WAVE];
@@ -325,7 +352,11 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
         }
         const bool hasneed = many<W>(need);
         if (__ballot(hasneed) == 0) {
-            if (inr) mstore<W>(Fn, v, Mask<W>{});
+            if (PJ_MS_FZ) {
+                if (lane == 0) Zn[base >> 6] = 0;
+            } else if (inr) {
+                mstore<W>(Fn, v, Mask<W>{});
+            }
             continue;
         }
         Off b = 0, e = 0;
@@ -343,10 +374,13 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
                 u32 u[MS_U];
 #pragma unroll
                 for (int q = 0; q < MS_U; ++q) u[q] = (k + (Off)q < lim) ? ccol[k + q] : 0u;
+                bool z[MS_U];
+#pragma unroll
+                for (int q = 0; q < MS_U; ++q) z[q] = (k + (Off)q < lim) && (!PJ_MS_FZ || zbit(Z, u[q]));
                 Mask<W> f[MS_U];
 #pragma unroll
                 for (int q = 0; q < MS_U; ++q) {
-                    if (k + (Off)q < lim) f[q] = mload<W>(F, u[q]);
+                    if (z[q]) f[q] = mload<W>(F, u[q]);
                     else f[q] = Mask<W>{};
                 }
 #pragma unroll
@@ -372,9 +406,10 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
             for (Off kk = kb; kk < ke && mopen<W>(want, got); kk += 2 * WAVE) {
                 const Off k0 = kk + lane, k1 = kk + WAVE + lane;
                 const u32 u0 = k0 < ke ? ccol[k0] : 0u, u1 = k1 < ke ? ccol[k1] : 0u;
+                const bool z0 = k0 < ke && (!PJ_MS_FZ || zbit(Z, u0)), z1 = k1 < ke && (!PJ_MS_FZ || zbit(Z, u1));
                 Mask<W> x{}, y{};
-                if (k0 < ke) x = mload<W>(F, u0);
-                if (k1 < ke) y = mload<W>(F, u1);
+                if (z0) x = mload<W>(F, u0);
+                if (z1) y = mload<W>(F, u1);
 #pragma unroll
                 for (int j = 0; j < W; ++j) got.w[j] |= wave_or(x.w[j] | y.w[j]);
             }
@@ -388,7 +423,7 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
             anynew |= newb.w[j] != 0;
         }
         if (inr) {
-            mstore<W>(Fn, v, newb);
+            if (!PJ_MS_FZ || anynew) mstore<W>(Fn, v, newb);
             if (anynew) {
                 Mask<W> nv;
 #pragma unroll
@@ -397,6 +432,10 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
             }
         }
         found_any |= anynew ? 1ull : 0ull;
+        if (PJ_MS_FZ) {
+            const u64 zb = __ballot(anynew);
+            if (lane == 0) Zn[base >> 6] = zb;
+        }
         if (anynew) fe += (u64)(row[v + 1] - row[v]);
         ms_write_dist<W>(newb, dist, n, v, L + 1);
     }
@@ -413,6 +452,7 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
 // of latency-bound levels, so two of them interleave on the CUs.
 struct MsSlot {
     DevBuf<u64> V, F, Fn;
+    DevBuf<u64> Z, Zn;  // (PJ_MS_FZ) nonzero-row bitmaps of F and Fn
     DevBuf<int32_t> dist;
     DevBuf<int64_t> src;
     DevBuf<MsCtl> ctl;
@@ -459,9 +499,10 @@ static void ms_pass(Graph& g, MsSlot& w, const int64_t* sources, int ns, double*
     const u64 push_max = g.ms_alpha > 0 ? (u64)((double)g.nnz / g.ms_alpha) : 0ull;
     PJ_HIP(hipEventRecord(w.ev0, s));
     ms_init_k<<<grid_for(std::max<i64>(n * W, (i64)ns * n / 4), MB, (unsigned)g.ctx->cu_count * 8u), MB, 0, s>>>(
-        w.V.p, w.F.p, n * W, w.dist.p, (i64)ns * n, w.ctl.p, host_dev);
+        w.V.p, w.F.p, n * W, w.dist.p, (i64)ns * n, w.ctl.p, host_dev, w.Z.p, (n + 63) / 64);
     PJ_LAUNCH_CHECK();
-    ms_sources_k<Off><<<(ns + 255) / 256, 256, 0, s>>>(w.src.p, ns, W, n, row, w.V.p, w.F.p, w.dist.p, w.ctl.p);
+    ms_sources_k<Off><<<(ns + 255) / 256, 256, 0, s>>>(w.src.p, ns, W, n, row, w.V.p, w.F.p, w.dist.p, w.ctl.p,
+                                                    w.Z.p);
     PJ_LAUNCH_CHECK();
     int32_t L = 0;
     // first batch: the previous pass's levels (passes over one graph need about as many);
@@ -470,20 +511,24 @@ static void ms_pass(Graph& g, MsSlot& w, const int64_t* sources, int ns, double*
     int next = 2;
     u64* F = w.F.p;
     u64* Fn = w.Fn.p;
+    u64* Z = w.Z.p;
+    u64* Zn = w.Zn.p;
     for (;;) {
         for (int i = 0; i < batch && L < INT_INF; ++i, ++L) {
             ms_prep_k<W><<<grid, MB, 0, s>>>(n, Fn, L, push_max, w.ctl.p, host_dev);
             PJ_LAUNCH_CHECK();
             ms_level_k<Off, W><<<grid, MB, 0, s>>>(n, crow, ccol, row, w.V.p, F, Fn, w.dist.p, L, smask, push_max,
-                                                   w.ctl.p);
+                                                   w.ctl.p, Z, Zn);
             PJ_LAUNCH_CHECK();
             if (push_max) {
-                ms_push_k<Off, W><<<grid, MB, 0, s>>>(n, row, col, F, Fn, L, push_max, w.ctl.p);
+                ms_push_k<Off, W><<<grid, MB, 0, s>>>(n, row, col, F, Fn, L, push_max, w.ctl.p, Z);
                 PJ_LAUNCH_CHECK();
-                ms_fin_k<Off, W><<<grid, MB, 0, s>>>(n, row, w.V.p, Fn, w.dist.p, L, smask, push_max, w.ctl.p);
+                ms_fin_k<Off, W><<<grid, MB, 0, s>>>(n, row, w.V.p, Fn, w.dist.p, L, smask, push_max, w.ctl.p,
+                                                     Zn);
                 PJ_LAUNCH_CHECK();
             }
             std::swap(F, Fn);
+            std::swap(Z, Zn);
         }
         PJ_HIP(hipStreamSynchronize(s));
         if (*(volatile int64_t*)w.host >= 0 || L >= INT_INF || !any) break;
@@ -523,6 +568,8 @@ static void ms_slot_alloc(Graph& g, MsSlot& sl, int W, bool own_stream) {
     sl.V.alloc(n ? n * W : 1);
     sl.F.alloc(n ? n * W : 1);
     sl.Fn.alloc(n ? n * W : 1);
+    sl.Z.alloc((n + 63) / 64 + 1);
+    sl.Zn.alloc((n + 63) / 64 + 1);
     sl.dist.alloc(n ? 64 * W * n : 1);
     sl.src.alloc(64 * W);
     sl.ctl.alloc(1);

@@ -11,6 +11,7 @@
 #   probe:<cmd>   any python command line under a 240 s limit (e.g. probe:tools/stats_probe.py 26 3)
 #   vtests:<v>:<pytest args>  -m gpu tests under the libpj build variant <v>
 #   ktp:<cmd>     rocprofv3 kernel trace + stats of any python command line -> kt_<name>/
+#   vktp:<v>:<cmd>  the same under the libpj build variant <v> -> kt_<v>_<name>/
 #   abp:<v1+v2..>:<python args>  interleaved A/B of any probe under build variants -> abp_<v>.<pass>.log
 #   ab:<v1+v2..>  interleaved A/B (AB_PASSES times, default 2) of the k26w bench line under libpj
 #                 build variants (lib/variants/<v>/libpj.so; "default" = the main build)
@@ -64,6 +65,11 @@ for st in "${LIST[@]}"; do
       kn=kt_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-30)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$kn" -o run -- python3 -u $arg \
         > "$OUT/$kn.log" 2>&1 || { echo "ktp failed: $arg"; tail "$OUT/$kn.log"; exit 1; } ;;
+    vktp)
+      v=${arg%%:*}; cmd=${arg#*:}; kn=kt_${v}_$(echo "$cmd" | tr -c 'A-Za-z0-9' '_' | cut -c1-30)
+      PJ_LIB_OVERRIDE=$PWD/paralleljohnson_amd/lib/variants/$v/libpj.so timeout -k 10 300 rocprofv3 --kernel-trace \
+        --stats --output-format csv -d "$OUT/$kn" -o run -- python3 -u $cmd > "$OUT/$kn.log" 2>&1 \
+        || { echo "vktp failed: $arg"; tail "$OUT/$kn.log"; exit 1; } ;;
     abp)
       vl=${arg%%:*}; cmd=${arg#*:}
       IFS='+' read -ra VS <<< "$vl"
