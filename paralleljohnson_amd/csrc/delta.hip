@@ -1130,7 +1130,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
         const i64 gbase = sc * PSC;
         // the frontier joins the members; new members add their heavy / light degrees (a
         // lane walks the bits of its word; a lane per vertex of the PSC words with the loads
-        // issued together, PJ_V2_MBPAR in round 4, ran the pull rounds 1.5x slower, r4a)
+        // issued together, PJ_V2_MBPAR in round 4, made the k26w solve 1.5x slower, r4a)
         u64 nmw = 0;
         if (lane < PSC && gbase + lane < a.nwords) {
             const u64 f = fin[gbase + lane];
