@@ -982,8 +982,10 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
             // heavy-head filter: no band member can lower d below lo + (the row's lightest
             // heavy weight); such vertices (and those without heavy edges) are not scanned,
             // but still join the next band / its minimum
+            // (without the filter every vertex >= hi is a candidate: the skipped ones are
+            // accounted below only when a.hw is set)
             const int h = (a.hw && up) ? (int)a.hw[v] : 1;
-            const bool cand = up && h != 0 && (long long)lo + h < (long long)d;
+            const bool cand = up && (!a.hw || (h != 0 && (long long)lo + h < (long long)d));
             const u64 m = __ballot(cand);
             u64 nm = 0;
             if (a.hw) {
