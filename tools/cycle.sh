@@ -12,7 +12,8 @@
 #   vtests:<v>:<pytest args>  -m gpu tests under the libpj build variant <v>
 #   ktp:<cmd>     rocprofv3 kernel trace + stats of any python command line -> kt_<name>/
 #   vktp:<v>:<cmd>  the same under the libpj build variant <v> -> kt_<v>_<name>/
-#   abp:<v1+v2..>:<python args>  interleaved A/B of any probe under build variants -> abp_<v>.<pass>.log
+#   abp:<v1+v2..>:<python args>  interleaved A/B (ABP_PASSES times, default AB_PASSES) of any probe under
+#                 build variants -> abp_<v>.<pass>.log
 #   ab:<v1+v2..>  interleaved A/B (AB_PASSES times, default 2) of the k26w bench line under libpj
 #                 build variants (lib/variants/<v>/libpj.so; "default" = the main build)
 # Inside a step's arguments "~" stands for a space and "^" for a comma (STEPS is one word).
@@ -73,7 +74,7 @@ for st in "${LIST[@]}"; do
     abp)
       vl=${arg%%:*}; cmd=${arg#*:}
       IFS='+' read -ra VS <<< "$vl"
-      for pass in $(seq 1 ${AB_PASSES:-2}); do
+      for pass in $(seq 1 ${ABP_PASSES:-${AB_PASSES:-2}}); do
         for v in "${VS[@]}"; do
           if [ "$v" != default ]; then export PJ_LIB_OVERRIDE=$PWD/paralleljohnson_amd/lib/variants/$v/libpj.so; else unset PJ_LIB_OVERRIDE; fi
           timeout -k 10 240 python3 -u $cmd > "$OUT/abp_$v.$pass.log" 2>&1 || { echo "abp $v failed"; tail -5 "$OUT/abp_$v.$pass.log"; exit 1; }
