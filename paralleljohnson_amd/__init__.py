@@ -231,8 +231,12 @@ class Graph:
         _check(_lib.pj_sssp(self._h, int(source), _ptr(out)))
         return out[: self.n] if copy else None
 
-    def copy_dist(self) -> np.ndarray:
-        out = np.empty(max(self.n, 1), np.int32)
+    def copy_dist(self, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """The last result into `out` (int32, >= n entries, e.g. pinned with host_pin) or a new array."""
+        if out is None:
+            out = np.empty(max(self.n, 1), np.int32)
+        elif out.dtype != np.int32 or out.size < self.n or not out.flags.c_contiguous:
+            raise ValueError("copy_dist: out must be a contiguous int32 array of >= n entries")
         _check(_lib.pj_copy_dist(self._h, _ptr(out)))
         return out[: self.n]
 
@@ -415,6 +419,17 @@ def write_sol(dist, path: str, strict: bool = False):
 def write_parents(parent, path: str):
     p = np.ascontiguousarray(parent, dtype=np.int64)
     _check(_lib.pj_write_parents(_ptr(p), len(p), os.fsencode(path)))
+
+
+def host_pin(a: np.ndarray):
+    """Page-lock a (contiguous) host array for direct device -> host copies (pj_host_pin)."""
+    if not a.flags.c_contiguous or a.nbytes == 0:
+        raise ValueError("host_pin: a contiguous, non-empty array")
+    _check(_lib.pj_host_pin(a.ctypes.data, a.nbytes))
+
+
+def host_unpin(a: np.ndarray):
+    _check(_lib.pj_host_unpin(a.ctypes.data))
 
 
 def device_count() -> int:

@@ -349,6 +349,27 @@ def test_batch_and_empty(ctx, oracle):
     assert e.n == 0 and e.sssp(0).size == 0
 
 
+def test_copy_dist_into_pinned_rows(ctx, pj, oracle):
+    """pj_host_pin'd rows take the direct DMA path of pj_copy_dist (> 1 MiB), pageable rows
+    the staged one: the same distances either way."""
+    g = ctx.generate_kronecker(19, 8, 4)
+    row, col, _ = g.get_csr()
+    r = int(g.sample_roots(2, 1)[0])
+    g.sssp(r, copy=False)
+    staged = g.copy_dist()
+    rows = np.empty(g.n + 17, np.int32)  # (larger than n, and not page-aligned at its end)
+    pj.host_pin(rows)
+    try:
+        pinned = g.copy_dist(rows)
+    finally:
+        pj.host_unpin(rows)
+    assert 4 * g.n > (1 << 20)
+    assert (pinned == staged).all() and (staged == oracle.bfs(row, col.astype(np.uint32), r)).all()
+    with pytest.raises(ValueError):
+        g.copy_dist(np.empty(g.n - 1, np.int32))
+    g.close()
+
+
 def test_cli_end_to_end(pj, oracle, tmp_path):
     rng = np.random.default_rng(3)
     src, dst = random_graph(rng, "hub", 5000)
