@@ -702,6 +702,19 @@ __global__ void wsum_all_k(const u32* __restrict__ w, i64 m, u64* __restrict__ o
 
 }  // namespace
 
+// the stat block's host copy: pinned, so each of a solve's ~40 counter reads is one
+// small DMA instead of a staged pageable copy
+struct PinnedStat {
+    u64* p = nullptr;
+    PinnedStat() { PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(u64) * ST_N, hipHostMallocDefault)); }
+    ~PinnedStat() {
+        if (p) (void)hipHostFree(p);
+    }
+    u64& operator[](size_t i) { return p[i]; }
+    PinnedStat(const PinnedStat&) = delete;
+    PinnedStat& operator=(const PinnedStat&) = delete;
+};
+
 struct WPart {
     Ctx* ctx = nullptr;
     i64 n = 0, lo = 0, hi = 0, nl = 0, block = 64, bw = 1, nnz_local = 0, nnz = 0;
@@ -727,7 +740,7 @@ struct WPart {
     i64 exch_bytes = 0;  // the engine view's send + recv buffers (sized to the largest round)
     DevBuf<u32> lq_v;
     DevBuf<u64> lq_b, lq_e;
-    std::vector<u64> hstat;
+    PinnedStat hstat;
     std::unique_ptr<DeltaSteps> steps;  // engine view with its own exchange buffers (lazy)
     unsigned grid() const { return (unsigned)ctx->cu_count * 8u; }
     WArgs args(int32_t dlo = 0, int32_t dhi = 0) {
@@ -757,7 +770,7 @@ struct WPart {
         return a;
     }
     void read_stat() {
-        PJ_HIP(hipMemcpyAsync(hstat.data(), stat.p, sizeof(u64) * ST_N, hipMemcpyDeviceToHost, ctx->stream));
+        PJ_HIP(hipMemcpyAsync(hstat.p, stat.p, sizeof(u64) * ST_N, hipMemcpyDeviceToHost, ctx->stream));
         PJ_HIP(hipStreamSynchronize(ctx->stream));
     }
     void clear_stat() { PJ_HIP(hipMemsetAsync(stat.p, 0, sizeof(u64) * ST_N, ctx->stream)); }
@@ -842,7 +855,7 @@ void wpart_cut(WPart* p, const Graph& g, i64 first, double mean_w) {
     p->lq_b.alloc(nl1);
     p->lq_e.alloc(nl1);
     p->stat.alloc(ST_N);
-    p->hstat.assign(ST_N, 0);
+    std::fill(p->hstat.p, p->hstat.p + ST_N, 0ull);
     if (p->world > 1) {
         p->cand.alloc((size_t)std::max<i64>(p->n, 1));
         p->touched.alloc((size_t)std::max<i64>((p->n + 63) / 64, 1));
@@ -1370,8 +1383,8 @@ void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* co
     if (p.world > 1) {
         wp_count_k<<<p.grid(), WB, 0, s>>>(a, (p.n + 63) / 64);
         PJ_LAUNCH_CHECK();
+        p.read_stat();  // (world 1 sends nothing: no host wait here)
     }
-    p.read_stat();
     for (int o = 0; o < p.world; ++o) counts[o] = p.world > 1 ? (i64)p.hstat[o] : 0;
     if (send) wpart_pack(p, send);
 }
