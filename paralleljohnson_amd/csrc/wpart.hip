@@ -67,6 +67,7 @@ constexpr int ST_NF = 65;      // vertices marked in the next frontier
 constexpr int ST_MIN = 66;     // min owned dist >= lo (select)
 constexpr int ST_CNT = 67;     // selected frontier size
 constexpr int ST_REACH = 68;   // reached vertices, [69] their out-edges
+constexpr int ST_ACC = 70;     // [70, 72): the per-band counts (heavy / light / unsettled edges)
 constexpr int ST_CUR = 72;     // [72, 72 + 64): pack cursors per owner
 constexpr int ST_N = 72 + WP_MAXW;
 
@@ -773,6 +774,12 @@ struct WPart {
         PJ_HIP(hipMemcpyAsync(hstat.p, stat.p, sizeof(u64) * ST_N, hipMemcpyDeviceToHost, ctx->stream));
         PJ_HIP(hipStreamSynchronize(ctx->stream));
     }
+    void read_acc(u64* out, int k) {  // stat[ST_ACC, ST_ACC + k) through the pinned copy
+        PJ_HIP(hipMemcpyAsync(hstat.p + ST_ACC, stat.p + ST_ACC, sizeof(u64) * (size_t)k, hipMemcpyDeviceToHost,
+                              ctx->stream));
+        PJ_HIP(hipStreamSynchronize(ctx->stream));
+        for (int i = 0; i < k; ++i) out[i] = hstat.p[ST_ACC + i];
+    }
     void clear_stat() { PJ_HIP(hipMemsetAsync(stat.p, 0, sizeof(u64) * ST_N, ctx->stream)); }
 };
 
@@ -1233,12 +1240,11 @@ void wpart_heavy_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
     hipStream_t s = p.ctx->stream;
     u64 h[2] = {0, 0};
     if (p.nl > 0) {
-        DevBuf<u64> acc(2);
-        PJ_HIP(hipMemsetAsync(acc.p, 0, 2 * sizeof(u64), s));
-        wp_heavy_counts_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), hi, acc.p);
+        u64* acc = p.stat.p + ST_ACC;  // (a temporary buffer here cost a hipFree per band)
+        PJ_HIP(hipMemsetAsync(acc, 0, 2 * sizeof(u64), s));
+        wp_heavy_counts_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), hi, acc);
         PJ_LAUNCH_CHECK();
-        PJ_HIP(hipMemcpyAsync(h, acc.p, 2 * sizeof(u64), hipMemcpyDeviceToHost, s));
-        PJ_HIP(hipStreamSynchronize(s));
+        p.read_acc(h, 2);
     }
     out2[0] = (i64)h[0];
     out2[1] = (i64)h[1];
@@ -1248,12 +1254,11 @@ void wpart_light_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
     hipStream_t s = p.ctx->stream;
     u64 h[2] = {0, 0};
     if (p.nl > 0) {
-        DevBuf<u64> acc(2);
-        PJ_HIP(hipMemsetAsync(acc.p, 0, 2 * sizeof(u64), s));
-        wp_light_counts_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), acc.p);
+        u64* acc = p.stat.p + ST_ACC;
+        PJ_HIP(hipMemsetAsync(acc, 0, 2 * sizeof(u64), s));
+        wp_light_counts_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), acc);
         PJ_LAUNCH_CHECK();
-        PJ_HIP(hipMemcpyAsync(h, acc.p, 2 * sizeof(u64), hipMemcpyDeviceToHost, s));
-        PJ_HIP(hipStreamSynchronize(s));
+        p.read_acc(h, 2);
     }
     out2[0] = (i64)h[0];
     out2[1] = (i64)h[1];
@@ -1289,19 +1294,18 @@ void wpart_heavy_pull(WPart& p, int32_t lo, int32_t hi) {
         wp_pull_heavy_k<<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.mmap.p);
         PJ_LAUNCH_CHECK();
     }
-    PJ_HIP(hipStreamSynchronize(s));
+    // (no wait: the band's next host step -- the tail count or the select -- waits on the stream)
 }
 
 i64 wpart_unsettled(WPart& p, int32_t hi) {
     hipStream_t s = p.ctx->stream;
     u64 h = 0;
     if (p.nl > 0) {
-        DevBuf<u64> acc(1);
-        PJ_HIP(hipMemsetAsync(acc.p, 0, sizeof(u64), s));
-        wp_unsettled_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(), hi, acc.p);
+        u64* acc = p.stat.p + ST_ACC;
+        PJ_HIP(hipMemsetAsync(acc, 0, sizeof(u64), s));
+        wp_unsettled_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(), hi, acc);
         PJ_LAUNCH_CHECK();
-        PJ_HIP(hipMemcpyAsync(&h, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
-        PJ_HIP(hipStreamSynchronize(s));
+        p.read_acc(&h, 1);
     }
     return (i64)h;
 }
