@@ -298,6 +298,14 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
                         delta = tdelta;
                         S.set_delta(delta);
                         tail_on = false;
+                        if (S.settled_map()) {  // everything below hi is settled from here on
+                            S.settled_slice((int32_t)hi);
+                            if (S.world > 1) {
+                                const size_t sl = S.settled_bytes();
+                                comm.allgather(static_cast<char*>(S.settled_map()) + (size_t)S.rank * sl,
+                                               S.settled_map(), sl, s);
+                            }
+                        }
                     }
                 }
             }

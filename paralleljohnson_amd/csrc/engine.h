@@ -137,6 +137,13 @@ struct DeltaSteps {
     virtual i64 unsettled_edges(int32_t hi) { (void)hi; return -1; }
     virtual i64 local_edges() { return 0; }
     virtual void set_delta(int32_t delta) { (void)delta; }
+    // Settled filter of the tail (optional): settled_slice(lo) writes this rank's words of
+    // settled_map() (bit v: dist[v] < lo, settled_bytes() bytes at rank x settled_bytes();
+    // 64-aligned blocks), the engine all-gathers it once, at the tail switch; the tail's
+    // relaxations then skip settled targets without reading their distance.
+    virtual void* settled_map() { return nullptr; }
+    virtual size_t settled_bytes() { return 0; }
+    virtual void settled_slice(int32_t lo) { (void)lo; }
     // Heavy pull (optional; symmetric graphs): instead of the members pushing their heavy
     // edges (relax / exchange / apply), every rank's unsettled vertices scan their own heavy
     // rows for members, read from a replicated byte map (dist - lo of a member, 0xFF

@@ -67,9 +67,9 @@ constexpr int ST_NF = 65;      // vertices marked in the next frontier
 constexpr int ST_MIN = 66;     // min owned dist >= lo (select)
 constexpr int ST_CNT = 67;     // selected frontier size
 constexpr int ST_REACH = 68;   // reached vertices, [69] their out-edges
-constexpr int ST_ACC = 70;     // [70, 72): the per-band counts (heavy / light / unsettled edges)
-constexpr int ST_CUR = 72;     // [72, 72 + 64): pack cursors per owner
-constexpr int ST_N = 72 + WP_MAXW;
+constexpr int ST_ACC = 72;     // [72, 75): the per-band counts (heavy / light / unsettled edges)
+constexpr int ST_CUR = 75;     // [75, 75 + 64): pack cursors per owner
+constexpr int ST_N = 75 + WP_MAXW;
 
 struct WArgs {
     i64 n, lo, nl, block, bw;
@@ -89,13 +89,18 @@ struct WArgs {
     u64* lq_b;
     u64* lq_e;
     u64* stat;
+    const u64* sbits;  // the tail's settled filter (global ids; null before the tail switch)
 };
+
+__device__ __forceinline__ bool wp_settled(const WArgs& a, u32 t) {
+    return a.sbits && ((a.sbits[t >> 6] >> (t & 63)) & 1ull);
+}
 
 // one relaxation; returns 1 when it adds t to the next frontier (the callers count
 // these per thread and add the block's sum to ST_NF once: an atomicAdd per marked
 // vertex on that one word serialized the light rounds behind its atomic rate)
 __device__ __forceinline__ u32 wp_edge(const WArgs& a, bool light, u32 t, long long nd) {
-    if (nd >= INT_INF) return 0u;
+    if (nd >= INT_INF || wp_settled(a, t)) return 0u;
     const i64 tl = (i64)t - a.lo;
     if (tl >= 0 && tl < a.nl) {
         if ((int32_t)nd < wp_now(a.dist + tl)) {
@@ -130,6 +135,13 @@ __device__ __forceinline__ u32 wp_edges(const WArgs& a, bool light, u64 k, u64 l
         t[j] = ok[j] ? a.col[k + j] : 0u;
         nd[j] = (long long)du + (ok[j] ? a.w[k + j] : 0u);
         ok[j] = ok[j] && nd[j] < INT_INF;
+    }
+    if (a.sbits) {  // the tail: settled targets are skipped before their distance is read
+        u64 sw[WP_PU];
+#pragma unroll
+        for (int j = 0; j < WP_PU; ++j) sw[j] = ok[j] ? a.sbits[t[j] >> 6] : 0ull;
+#pragma unroll
+        for (int j = 0; j < WP_PU; ++j) ok[j] = ok[j] && !((sw[j] >> (t[j] & 63)) & 1ull);
     }
 #pragma unroll
     for (int j = 0; j < WP_PU; ++j) {
@@ -423,13 +435,6 @@ __global__ __launch_bounds__(WB) void wp_apply_k(WArgs a, const u64* __restrict_
     if (light) wp_flush_nf(a, nf, red);
 }
 
-// fr := frn, frn := 0 (the round's new frontier becomes current)
-__global__ void wp_swap_k(WArgs a) {
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < a.bw; i += (i64)gridDim.x * blockDim.x) {
-        a.fr[i] = a.frn[i];
-        a.frn[i] = 0;
-    }
-}
 
 __global__ void wp_rebase_k(const void* row, bool off64, i64 lo, i64 nl, u64* __restrict__ out) {
     const u64 base = off64 ? ((const u64*)row)[lo] : (u64)((const u32*)row)[lo];
@@ -451,20 +456,48 @@ __global__ void wp_lsplit_k(const u64* __restrict__ row, const u32* __restrict__
     }
 }
 
-// Heavy pull (engine.h DeltaSteps): (members' heavy edges, unsettled vertices' heavy edges)
-__global__ __launch_bounds__(WB) void wp_heavy_counts_k(WArgs a, int32_t hi, u64* __restrict__ out) {
+// Heavy pull (engine.h DeltaSteps): (members' heavy edges, unsettled vertices' heavy edges,
+// and all out-edges of the vertices >= hi: the tail switch's count, which the heavy step
+// does not change -- its offers are >= lo + delta = hi -- so wpart_unsettled reuses it)
+// It also writes this rank's slice of the member map (as wp_member_slice_k) when `own` is
+// set: the heavy pull that may follow then needs no pass of its own.
+__global__ __launch_bounds__(WB) void wp_heavy_counts_k(WArgs a, int32_t hi, u64* __restrict__ out,
+                                                       uint8_t* __restrict__ own) {
     __shared__ u64 red[WB / WAVE];
-    u64 m = 0, u = 0;
-    for (i64 v = (i64)blockIdx.x * WB + threadIdx.x; v < a.nl; v += (i64)gridDim.x * WB) {
-        const u64 hd = a.row[v + 1] - a.row[v] - a.lsplit[v];
-        if ((a.mb[v >> 6] >> (v & 63)) & 1ull) m += hd;
-        else if (a.dist[v] >= hi) u += hd;
+    u64 m = 0, u = 0, ua = 0;
+    for (i64 v = (i64)blockIdx.x * WB + threadIdx.x; v < a.block; v += (i64)gridDim.x * WB) {
+        uint8_t x = 0xFF;
+        if (v < a.nl) {
+            const u64 deg = a.row[v + 1] - a.row[v], hd = deg - a.lsplit[v];
+            const int32_t d = a.dist[v];
+            if ((a.mb[v >> 6] >> (v & 63)) & 1ull) {
+                m += hd;
+                x = (uint8_t)(d - a.dlo);
+            } else if (d >= hi) {
+                u += hd;
+                ua += deg;
+            }
+        }
+        if (own) own[v] = x;
     }
     m = block_sum<WB / WAVE>(m, red);
     u = block_sum<WB / WAVE>(u, red);
+    ua = block_sum<WB / WAVE>(ua, red);
     if (threadIdx.x == 0) {
         if (m) atomicAdd(&out[0], m);
         if (u) atomicAdd(&out[1], u);
+        if (ua) atomicAdd(&out[2], ua);
+    }
+}
+
+// bit v of the rank's words of the settled map: dist[v] < lo (v past nl: 0)
+__global__ void wp_settled_k(WArgs a, int32_t lo, u64* __restrict__ words) {
+    const int lane = lane_id();
+    const i64 nwaves = (i64)gridDim.x * (blockDim.x / WAVE);
+    for (i64 wi = (i64)blockIdx.x * (blockDim.x / WAVE) + wave_id(); wi < a.bw; wi += nwaves) {
+        const i64 v = wi * 64 + lane;
+        const u64 m = __ballot(v < a.nl && a.dist[v] < lo);
+        if (lane == 0) words[wi] = m;
     }
 }
 // this rank's slice of the member map: dist - lo of a band member, 0xFF otherwise
@@ -601,9 +634,12 @@ __global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const uint8_t* __
     u64 marks = 0;
     for (i64 b0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; b0 < a.nl; b0 += nwaves * 64) {
         const i64 v = b0 + lane;
-        if (lane == 0) {
+        if (lane == 0) {  // (cleared as consumed: end_round swaps fr and frn)
             const u64 f = a.fr[b0 >> 6];
-            if (f) a.mb[b0 >> 6] |= f;
+            if (f) {
+                a.mb[b0 >> 6] |= f;
+                a.fr[b0 >> 6] = 0;
+            }
         }
         int32_t d0 = INT_INF, cur = INT_INF;
         u64 k = 0, e = 0;
@@ -738,6 +774,11 @@ struct WPart {
     DevBuf<int32_t> dist, cand;
     DevBuf<u64> touched, fr, frn, mb, stat;
     DevBuf<u32> rl_inv;   // (relabeled blocks) old local id -> new local id; empty: input ids
+    DevBuf<u64> sb;       // the tail's settled map, world x block bits (engine all-gathers the slices)
+    bool sb_on = false;   // sb holds this solve's map (set at the tail switch)
+    int32_t ua_hi = INT_MIN;  // wp_heavy_counts_k's third count is for this hi (this band)
+    i64 ua = 0;
+    int32_t ms_lo = INT_MIN;  // wp_heavy_counts_k wrote the member slice of the band starting here
     i64 exch_bytes = 0;  // the engine view's send + recv buffers (sized to the largest round)
     DevBuf<u32> lq_v;
     DevBuf<u64> lq_b, lq_e;
@@ -768,6 +809,7 @@ struct WPart {
         a.lq_b = lq_b.p;
         a.lq_e = lq_e.p;
         a.stat = stat.p;
+        a.sbits = sb_on ? sb.p : nullptr;
         return a;
     }
     void read_stat() {
@@ -1238,16 +1280,21 @@ void wpart_device_bytes(const WPart& p, i64* out4) {
 
 void wpart_heavy_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
     hipStream_t s = p.ctx->stream;
-    u64 h[2] = {0, 0};
+    u64 h[3] = {0, 0, 0};
     if (p.nl > 0) {
         u64* acc = p.stat.p + ST_ACC;  // (a temporary buffer here cost a hipFree per band)
-        PJ_HIP(hipMemsetAsync(acc, 0, 2 * sizeof(u64), s));
-        wp_heavy_counts_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), hi, acc);
+        PJ_HIP(hipMemsetAsync(acc, 0, 3 * sizeof(u64), s));
+        if (!p.mmap.p) p.mmap.alloc((size_t)p.world * (size_t)p.block);
+        wp_heavy_counts_k<<<grid_for(p.block, WB, p.grid()), WB, 0, s>>>(
+            p.args(lo, hi), hi, acc, hi - lo <= 255 ? p.mmap.p + (size_t)p.rank * (size_t)p.block : nullptr);
         PJ_LAUNCH_CHECK();
-        p.read_acc(h, 2);
+        p.read_acc(h, 3);
     }
     out2[0] = (i64)h[0];
     out2[1] = (i64)h[1];
+    p.ua_hi = hi;  // (wpart_unsettled(hi) of this band)
+    p.ua = (i64)h[2];
+    p.ms_lo = hi - lo <= 255 && p.nl > 0 ? lo : INT_MIN;  // (the member slice of this band is written)
 }
 
 void wpart_light_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
@@ -1282,6 +1329,10 @@ void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
 }
 
 void wpart_member_slice(WPart& p, int32_t lo, int32_t hi) {
+    if (p.ms_lo == lo) {  // written by this band's wp_heavy_counts_k
+        p.ms_lo = INT_MIN;
+        return;
+    }
     if (!p.mmap.p) p.mmap.alloc((size_t)p.world * (size_t)p.block);
     wp_member_slice_k<<<grid_for(p.block, 256, p.grid()), 256, 0, p.ctx->stream>>>(
         p.args(lo, hi), p.mmap.p + (size_t)p.rank * (size_t)p.block);
@@ -1299,6 +1350,10 @@ void wpart_heavy_pull(WPart& p, int32_t lo, int32_t hi) {
 
 i64 wpart_unsettled(WPart& p, int32_t hi) {
     hipStream_t s = p.ctx->stream;
+    if (p.ua_hi == hi) {  // counted by this band's wp_heavy_counts_k
+        p.ua_hi = INT_MIN;
+        return p.ua;
+    }
     u64 h = 0;
     if (p.nl > 0) {
         u64* acc = p.stat.p + ST_ACC;
@@ -1308,6 +1363,18 @@ i64 wpart_unsettled(WPart& p, int32_t hi) {
         p.read_acc(&h, 1);
     }
     return (i64)h;
+}
+
+// the tail's settled map: this rank's words (bit v: dist[v] < lo), enabled for the rest of the solve
+static u64* wpart_settled_map(WPart& p) {
+    if (!p.sb.p) p.sb.alloc((size_t)p.world * (size_t)p.bw);
+    return p.sb.p;
+}
+static void wpart_settled_slice(WPart& p, int32_t lo) {
+    u64* words = wpart_settled_map(p) + (size_t)p.rank * (size_t)p.bw;
+    wp_settled_k<<<grid_for(p.bw * 64, 256, p.grid()), 256, 0, p.ctx->stream>>>(p.args(), lo, words);
+    PJ_LAUNCH_CHECK();
+    p.sb_on = true;
 }
 
 // the light prefixes of light threshold delta in p.lsplit: the current buffer, the other
@@ -1337,6 +1404,9 @@ int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
         delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(3.5 * p.mean_w / std::max(1.0, mean_deg))));
     }
     wpart_use_delta(p, delta);
+    p.sb_on = false;
+    p.ua_hi = INT_MIN;
+    p.ms_lo = INT_MIN;
     if (p.nl > 0) PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.dist.p), INT_INF, (size_t)p.nl, s));
     if (p.world > 1 && p.n > 0)
         PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.cand.p), INT_INF, (size_t)p.n, s));
@@ -1414,11 +1484,9 @@ void wpart_apply(WPart& p, const u64* recv, i64 nr, int light, int32_t lo, int32
 
 // The round's new frontier becomes current; returns its size on this rank (the
 // marks counted by the round's relax and apply: each vertex once, by the
-// atomicOr's old bit).
-static void wpart_end_round_async(WPart& p) {
-    wp_swap_k<<<grid_for(p.bw, 256, p.grid()), 256, 0, p.ctx->stream>>>(p.args());
-    PJ_LAUNCH_CHECK();
-}
+// atomicOr's old bit). The round's kernels cleared fr's words as they consumed them,
+// so the two bitmaps trade places with no kernel (wp_swap_k copied and cleared them).
+static void wpart_end_round_async(WPart& p) { std::swap(p.fr, p.frn); }
 
 i64 wpart_end_round(WPart& p) {
     wpart_end_round_async(p);
@@ -1499,6 +1567,9 @@ struct WPartGpuSteps final : DeltaSteps {
     i64 unsettled_edges(int32_t hi) override { return wpart_unsettled(p, hi); }
     i64 local_edges() override { return p.nnz_local; }
     void set_delta(int32_t delta) override { wpart_set_delta(p, delta); }
+    void* settled_map() override { return wpart_settled_map(p); }
+    size_t settled_bytes() override { return (size_t)p.bw * sizeof(u64); }
+    void settled_slice(int32_t lo) override { wpart_settled_slice(p, lo); }
     double pull_factor() override { return p.symmetric ? p.pull_factor : 0.0; }  // (0: this rank vetoes)
     void heavy_counts(int32_t lo, int32_t hi, i64* out2) override { wpart_heavy_counts(p, lo, hi, out2); }
     void member_slice(int32_t lo, int32_t hi) override { wpart_member_slice(p, lo, hi); }
