@@ -281,8 +281,6 @@ struct V2Args {
     u64* hbeg;   // [3][hcap]
     u64* hoff;   // [3][hcap]
     u64 hcap;
-    uint4* hq;   // PJ_V2_HCH > 0: [3][hqcap] chunk descriptors (row position lo / hi, source dist, edges)
-    u64 hqcap;
     u64* rlog;   // round_log option: [0] = rounds logged, then (kind, frontier, its light edges) per round
 };
 // the light edges of a band round (light CSR, or the light prefixes of cw in the tail)
@@ -342,19 +340,9 @@ __device__ __forceinline__ u64 v2_slot_edges(const V2Line* sl) {
 // whose read distance was above nd has been lowered to <= nd this round, by
 // this lane or another, so it belongs in the next frontier either way. The
 // frontier mark counts the new frontier vertex and its light edges (the next
-// round's push cost, read from lsplit):
-//   PJ_V2_MARK 0: a returning atomicOr, then the lsplit read of a newly marked
-//                 target (two dependent round trips after the distance);
-//   PJ_V2_MARK 1: the lsplit read issued beside the returning atomicOr (one).
-// (A returnless atomicOr after a plain read of the mark word ran 5% slower, r4a.)
-#ifndef PJ_V2_MARK
-#define PJ_V2_MARK 0
-#endif
-// hub queue slots carry the source's distance read by the producing round (PJ_V2_HUBDU 1)
-// instead of its id (0: the hub kernel reads dist[v], one dependent load per slot)
-#ifndef PJ_V2_HUBDU
-#define PJ_V2_HUBDU 0
-#endif
+// round's push cost): a returning atomicOr, then the lsplit read of a newly marked
+// target. (Round 4: the lsplit read issued beside the atomicOr measured equal, a plain
+// read of the mark word plus a returnless atomicOr 5% slower; both removed.)
 template <bool LIGHT, int N>
 __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const u64 (&idx)[N],
                                           const int32_t (&du)[N], const bool (&val)[N], u64* __restrict__ fout,
@@ -396,32 +384,16 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
     }
     if (!LIGHT) return 0u;
     u32 newc = 0;
-    if (PJ_V2_MARK == 1) {
-        u64 old[N];
-        u32 ls[N];
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-            old[j] = mk[j] ? atomicOr(fout + (t[j] >> 6), 1ull << (t[j] & 63)) : ~0ull;
-            ls[j] = mk[j] ? a.lsplit[t[j]] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (!((old[j] >> (t[j] & 63)) & 1ull)) {
+    for (int j = 0; j < N; ++j)
+        if (mk[j]) {
+            if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[4].v, 1ull);
+            if (v2_mark(fout, t[j])) {
+                if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[3].v, 1ull);
                 ++newc;
-                fe += ls[j];
+                fe += a.lsplit[t[j]];
             }
-    } else {
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (mk[j]) {
-                if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[4].v, 1ull);
-                if (v2_mark(fout, t[j])) {
-                    if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[3].v, 1ull);
-                    ++newc;
-                    fe += a.lsplit[t[j]];
-                }
-            }
-    }
+        }
     return newc;
 }
 
@@ -453,56 +425,25 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
 
 // Hub queue appends (whole wave; lanes with hub = true hand their segment [b, e) to the
 // queue of ring slot hs and get e = b back).
-//   PJ_V2_HCH 0: one slot per segment, (source, row position, edge offset) from ONE packed
-//                atomic, relaxed by v2_hub_body in edge-balanced block tiles (an LDS binary
-//                search per edge, the tile's slot offsets and source distances staged in LDS);
-//   PJ_V2_HCH > 0: the segment cut into chunks of HCH edges, one 16-byte descriptor each
-//                (row position, the source's distance, edge count), appended with one atomic
-//                per wave and written by the whole wave; v2_hub_chunks gives a wave one
-//                descriptor at a time: one load, then the chunk's edges in coalesced runs,
-//                no search, no block barrier.
-#ifndef PJ_V2_HCH
-#define PJ_V2_HCH 0
-#endif
-// heavy pull candidates filtered by the row's first heavy weight (V2Args::hw)
+// One slot per segment, (source, row position, edge offset) from ONE packed atomic,
+// relaxed by v2_hub_body in edge-balanced block tiles (an LDS binary search per edge, the
+// tile's slot offsets and source distances staged in LDS). (Round 4: 256- or 128-edge chunk
+// descriptors, one wave each, measured 2-3% slower; a slot carrying the source's distance
+// instead of its id 1% slower; removed.)
+// heavy pull candidates filtered by the row's first heavy weight (V2Args::hw): k26w 447.1 /
+// 451.3 -> 452.3 / 455.3 GTEPS interleaved (r4c, profiles/r04/ab_r4c.txt)
 #ifndef PJ_V2_HWF
-#define PJ_V2_HWF 0
+#define PJ_V2_HWF 1
 #endif
 // light pull candidates filtered by the row's lightest weight (V2Args::w1): k26w 438.8 ->
 // 451.0 / 448.6 GTEPS interleaved (r4a, profiles/r04/ab_r4a.txt)
 #ifndef PJ_V2_LWF
 #define PJ_V2_LWF 1
 #endif
-constexpr u32 V2_HCH = PJ_V2_HCH > 0 ? PJ_V2_HCH : 256;
 __device__ __forceinline__ void v2_hub_append(const V2Args& a, int hs, bool hub, u32 v, int32_t du, u64 b, u64& e) {
     const int lane = lane_id();
     const u64 hm = __ballot(hub);
     if (!hm) return;
-    if (PJ_V2_HCH > 0) {
-        const u32 nc = hub ? (u32)((e - b + V2_HCH - 1) / V2_HCH) : 0u;
-        const u32 inc = wave_incl_scan(nc);
-        const u32 tot = __shfl(inc, 63, 64);
-        u64 base = 0;
-        if (lane == 63) base = atomicAdd(&a.ctl->hub[hs].v, (u64)tot);
-        base = __shfl(base, 63, 64);
-        uint4* q = a.hq + (u64)hs * a.hqcap;
-        u64 m = hm;
-        while (m) {  // the wave writes each hub's descriptors
-            const int l = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            const u32 ncl = __shfl(nc, l, 64);
-            const u64 bl = __shfl(b, l, 64), el = __shfl(e, l, 64);
-            const int32_t dl = __shfl(du, l, 64);
-            const u64 qb = base + __shfl(inc, l, 64) - ncl;
-            for (u32 c = (u32)lane; c < ncl; c += WAVE) {
-                const u64 cb = bl + (u64)c * V2_HCH;
-                const u32 cn = (u32)min((u64)V2_HCH, el - cb);
-                q[qb + c] = make_uint4((u32)cb, (u32)(cb >> 32), (u32)dl, cn);
-            }
-        }
-        if (hub) e = b;
-        return;
-    }
     const u64 mask = (1ull << V2_EB) - 1ull;
     const u64 seg = hub ? e - b : 0;
     const u64 ie = wave_incl_scan(seg);
@@ -514,7 +455,7 @@ __device__ __forceinline__ void v2_hub_append(const V2Args& a, int hs, bool hub,
     if (hub) {
         const u64 slot = (base >> V2_EB) + (u64)__popcll(hm & lanemask_lt());
         const u64 q = (u64)hs * a.hcap + slot;
-        a.hv[q] = PJ_V2_HUBDU ? (u32)du : v;
+        a.hv[q] = v;
         a.hbeg[q] = b;
         a.hoff[q] = (base & mask) + ie - seg;
         e = b;
@@ -835,7 +776,7 @@ __device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ f
         u32 ns;
         lb_tile_load<V2_HTILE>(ho, nq, e0, L.sh, s0, ns);
         for (u32 i = threadIdx.x; i < ns; i += DB) {
-            L.s_du[i] = PJ_V2_HUBDU ? (int32_t)hv[s0 + i] : a.dist[hv[s0 + i]];
+            L.s_du[i] = a.dist[hv[s0 + i]];
             L.s_b[i] = hb[s0 + i];
         }
         __syncthreads();
@@ -858,45 +799,16 @@ __device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ f
 
 // The hub queue hs of one round in its own launch. Zeroes the next ring slot hz for
 // later appends.
-// PJ_V2_HCH > 0: a wave takes one chunk descriptor at a time (grid-stride over the
-// chunks); lane l relaxes edges l, l + 64, ... of the chunk, HCH / 64 per lane with the
-// loads issued together (v2_relax_g).
-template <bool LIGHT>
-__device__ __forceinline__ void v2_hub_chunks(const V2Args& a, u64* __restrict__ fout, int hs, u64 nch, u32& newc,
-                                              u64& fe) {
-    constexpr int NJ = (int)(V2_HCH / WAVE);
-    const int lane = lane_id();
-    const uint4* q = a.hq + (u64)hs * a.hqcap;
-    const ESrc ed = LIGHT ? v2_light_src(a) : v2_cw_src(a);
-    const u64 nwv = (u64)gridDim.x * (DB / WAVE);
-    for (u64 c = (u64)blockIdx.x * (DB / WAVE) + wave_id(); c < nch; c += nwv) {
-        const uint4 d = q[c];
-        const u64 cb = (u64)d.x | ((u64)d.y << 32);
-        u64 idx[NJ];
-        int32_t du[NJ];
-        bool val[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const u32 o = (u32)lane + (u32)j * WAVE;
-            val[j] = o < d.w;
-            idx[j] = cb + o;
-            du[j] = (int32_t)d.z;
-        }
-        newc += v2_relax_g<LIGHT, NJ>(a, ed, idx, du, val, fout, fe);
-    }
-}
-
 template <bool LIGHT>
 __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout, int cin, int hs, int hz) {
     __shared__ V2HubLds L;
     __shared__ u64 red[DB / WAVE];
     const u64 packed = a.ctl->hub[hs].v;
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->hub[hz].v = 0;
-    if (PJ_V2_HCH > 0 ? packed == 0 : (packed >> V2_EB) == 0) return;
+    if ((packed >> V2_EB) == 0) return;
     u32 newc = 0;
     u64 fe = 0;
-    if (PJ_V2_HCH > 0) v2_hub_chunks<LIGHT>(a, fout, hs, packed, newc, fe);
-    else v2_hub_body<LIGHT>(a, fout, hs, packed, newc, fe, L);
+    v2_hub_body<LIGHT>(a, fout, hs, packed, newc, fe, L);
     if (LIGHT) v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
 }
 
@@ -1522,8 +1434,6 @@ struct DeltaSolve {
     DevBuf<u32> hv;
     DevBuf<u64> hbeg, hoff;
     u64 hcap = 0;
-    DevBuf<uint4> hq;          // (PJ_V2_HCH > 0) hub chunk descriptors, [3][hqcap]
-    u64 hqcap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     pj_stats st{};
     ~DeltaSolve() {
@@ -1770,18 +1680,6 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     v.sb.alloc(nw);
     v.ctl.alloc(1);
     v.hcap = (u64)std::max<i64>(1, std::min<i64>(n, g.nnz / (i64)V2_HT + 1));
-    if (PJ_V2_HCH > 0) {
-        // every segment has more than V2_HT edges: at most nnz / V2_HCH + nnz / V2_HT chunks a round
-        v.hqcap = (u64)std::max<i64>(1, g.nnz / (i64)V2_HCH + g.nnz / (i64)V2_HT + 1);
-        v.hq.alloc(3 * v.hqcap);
-        v.hv.alloc(1);
-        v.hbeg.alloc(1);
-        v.hoff.alloc(1);
-    } else {
-        v.hv.alloc(3 * v.hcap);
-        v.hbeg.alloc(3 * v.hcap);
-        v.hoff.alloc(3 * v.hcap);
-    }
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hctl), sizeof(V2Ctl), hipHostMallocMapped));
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&v.hctl_dev), v.hctl, 0));
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hseq), 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -1837,8 +1735,6 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     a.hbeg = v.hbeg.p;
     a.hoff = v.hoff.p;
     a.hcap = v.hcap;
-    a.hq = v.hq.p;
-    a.hqcap = v.hqcap;
     DevBuf<u64> rlog;
     if (g.round_log) {
         rlog.alloc(1 + 3 * 255);

@@ -135,8 +135,9 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
 // bytes, cache-resident) before the 8W-byte F[u] and skips zero rows, the push skips
 // waves whose 64 vertices have no frontier, and a pull level stores only nonzero Fn rows
 // (readers consult Zn first).
+// MS1024: 11.72 / 11.73 -> 11.59 / 11.65 ms per batch interleaved (r4b, profiles/r04/ms_fz_r4b.txt)
 #ifndef PJ_MS_FZ
-#define PJ_MS_FZ 0
+#define PJ_MS_FZ 1
 #endif
 __device__ __forceinline__ bool zbit(const u64* __restrict__ Z, u32 u) { return (Z[u >> 6] >> (u & 63)) & 1ull; }
 

@@ -54,7 +54,7 @@ constexpr int WB = 256;
 constexpr int WSC = 16;        // frontier words a wave screens at once
 constexpr int WP_SERIAL = 8;   // edges a lane relaxes alone
 #ifndef PJ_WP_LONG
-#define PJ_WP_LONG 1024
+#define PJ_WP_LONG 64  // with the per-block degree order (below); 1024 before it (r4c: 64 without it ~6% slower)
 #endif
 constexpr u64 WP_LONG = PJ_WP_LONG;  // longer row segments: the grid-wide queue
 constexpr int WP_MAXW = 64;    // largest world size
@@ -950,9 +950,13 @@ __global__ void wp_filter_write_k(const u32* __restrict__ src, const u32* __rest
 // the exchange and the pulls' byte map are unchanged; every rank derives the same map
 // from the degrees of ALL vertices (each builder sees every entry: the generator's
 // tuples, the parsed file, the full graph) and keeps only its block's inverse. The
-// source is mapped on entry, distances are mapped back on the way out.
+// source is mapped on entry, distances are mapped back on the way out. With it, the rows
+// longer than WP_LONG = 64 edges go to the edge-balanced queue: the order puts the long
+// rows into the first waves of the block, and one wave per 64 of them relaxed 3x slower
+// (r4a, at 1024). s26w 11.1-12.7 -> 8.9-10.5 ms at world 1, 17.1-18.6 -> 13.4-15.6 ms at
+// world 2 (r4c, profiles/r04/wpart_r4c.txt).
 #ifndef PJ_WP_RELABEL
-#define PJ_WP_RELABEL 0
+#define PJ_WP_RELABEL 1
 #endif
 __global__ void wp_deg_key_k(const u32* __restrict__ deg, i64 n, u32 maxdeg, u32* __restrict__ key,
                              u32* __restrict__ ids) {
