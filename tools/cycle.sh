@@ -14,6 +14,8 @@
 #   vktp:<v>:<cmd>  the same under the libpj build variant <v> -> kt_<v>_<name>/
 #   abp:<v1+v2..>:<python args>  interleaved A/B (ABP_PASSES times, default AB_PASSES) of any probe under
 #                 build variants -> abp_<v>.<pass>.log
+#   abo:<o1+o2..> interleaved A/B of the k26w bench line under libpj option sets (o = k=v/k=v...,
+#                 "default" = none), AB_PASSES times
 #   ab:<v1+v2..>  interleaved A/B (AB_PASSES times, default 2) of the k26w bench line under libpj
 #                 build variants (lib/variants/<v>/libpj.so; "default" = the main build)
 # Inside a step's arguments "~" stands for a space and "^" for a comma (STEPS is one word).
@@ -82,6 +84,18 @@ for st in "${LIST[@]}"; do
         done
       done
       unset PJ_LIB_OVERRIDE ;;
+    abo)
+      IFS='+' read -ra OS <<< "$arg"
+      for pass in $(seq 1 ${AB_PASSES:-2}); do
+        for o in "${OS[@]}"; do
+          optargs=""; IFS='/' read -ra KV <<< "$o"
+          for kv in "${KV[@]}"; do [ "$kv" != default ] && optargs="$optargs --opt $kv"; done
+          tag=$(echo "$o" | tr -c 'A-Za-z0-9' '_')
+          timeout -k 10 200 python3 -u bench.py --no-secondary --no-partitioned --no-tts --no-cpu-baseline --steps 32 --warmup 4 $optargs "$@" \
+            > "$OUT/abo_$tag.$pass.json" 2> "$OUT/abo_$tag.$pass.err" || { echo "abo $o failed"; tail -5 "$OUT/abo_$tag.$pass.err"; exit 1; }
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3], d['value'], d['ms_per_step'], d['roofline']['frac'])" "$OUT/abo_$tag.$pass.json" "$o" $pass
+        done
+      done ;;
     ab)
       IFS='+' read -ra VS <<< "$arg"
       for pass in $(seq 1 ${AB_PASSES:-2}); do
