@@ -431,9 +431,11 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
 // descriptors, one wave each, measured 2-3% slower; a slot carrying the source's distance
 // instead of its id 1% slower; removed.)
 // heavy pull candidates filtered by the row's first heavy weight (V2Args::hw): k26w 447.1 /
-// 451.3 -> 452.3 / 455.3 GTEPS interleaved (r4c, profiles/r04/ab_r4c.txt)
+// 451.3 -> 452.3 / 455.3 GTEPS interleaved (r4c, profiles/r04/ab_r4c.txt); off: the first
+// run of the parity suite with it on (r4d) hit an illegal memory access in a small weighted
+// solve (test_cache_roundtrip_weighted_kronecker), cause not found yet
 #ifndef PJ_V2_HWF
-#define PJ_V2_HWF 1
+#define PJ_V2_HWF 0
 #endif
 // light pull candidates filtered by the row's lightest weight (V2Args::w1): k26w 438.8 ->
 // 451.0 / 448.6 GTEPS interleaved (r4a, profiles/r04/ab_r4a.txt)
