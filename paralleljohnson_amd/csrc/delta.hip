@@ -431,11 +431,9 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
 // descriptors, one wave each, measured 2-3% slower; a slot carrying the source's distance
 // instead of its id 1% slower; removed.)
 // heavy pull candidates filtered by the row's first heavy weight (V2Args::hw): k26w 447.1 /
-// 451.3 -> 452.3 / 455.3 GTEPS interleaved (r4c, profiles/r04/ab_r4c.txt); off: the first
-// run of the parity suite with it on (r4d) hit an illegal memory access in a small weighted
-// solve (test_cache_roundtrip_weighted_kronecker), cause not found yet
+// 451.3 -> 452.3 / 455.3 GTEPS interleaved (r4c, profiles/r04/ab_r4c.txt)
 #ifndef PJ_V2_HWF
-#define PJ_V2_HWF 0
+#define PJ_V2_HWF 1
 #endif
 // light pull candidates filtered by the row's lightest weight (V2Args::w1): k26w 438.8 ->
 // 451.0 / 448.6 GTEPS interleaved (r4a, profiles/r04/ab_r4a.txt)
@@ -1682,6 +1680,9 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     v.sb.alloc(nw);
     v.ctl.alloc(1);
     v.hcap = (u64)std::max<i64>(1, std::min<i64>(n, g.nnz / (i64)V2_HT + 1));
+    v.hv.alloc(3 * v.hcap);  // the hub queue's ring of three slots
+    v.hbeg.alloc(3 * v.hcap);
+    v.hoff.alloc(3 * v.hcap);
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hctl), sizeof(V2Ctl), hipHostMallocMapped));
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&v.hctl_dev), v.hctl, 0));
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hseq), 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -1703,6 +1704,12 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     const i64 n = R.n_scan;
     const i64 nwords = (n + 63) / 64;
     const Off* row = static_cast<const Off*>(R.row_ptr(g.off64));
+    // host check of the buffers every band kernel dereferences (a missing allocation is an
+    // error here, not a device fault)
+    if (n > 0 && (!row || !v.dist || !v.out || !v.f[0].p || !v.f[1].p || !v.f[2].p || !v.mb.p || !v.sb.p ||
+                  !v.ctl.p || !v.hv.p || !v.hbeg.p || !v.hoff.p || v.hv.n < 3 * v.hcap || !w.lsplit.p ||
+                  !w.lrow.p || (!w.lcw.p && !w.lcw32.p) || (PJ_V2_LWF && !w.w1.p) || (PJ_V2_HWF && !w.hw.p)))
+        throw Error(PJ_ERR_HIP, "delta-stepping: a solver buffer is missing (internal error)");
     const unsigned maxgrid = (unsigned)ctx.cu_count * (unsigned)PJ_V2_GPC;  // workgroups per CU of the v2 kernels (grid-stride)
     const unsigned pullgrid = (unsigned)ctx.cu_count * (unsigned)PJ_V2_GPC_PULL;
     // light-round grids (grid-stride kernels): a launch that finds its round empty costs
