@@ -54,7 +54,43 @@ struct MsCtl {
     // cost), summed over MS_NSH shards: every workgroup of a level adds its count, and one
     // word taking them all saturates at ~88 atomics per microsecond
     u64 fedges[3][MS_NSH][8];
+    // (PJ_MS_UF) same ring: the sources that reached some vertex at that level (the OR of
+    // the level's new masks, sharded like fedges): only they can extend the next level
+    u64 uf[3][MS_NSH][MS_WMAX];
 };
+
+// PJ_MS_UF 1: a pull level looks only for the sources whose frontier is not empty (the
+// previous level's uf): a vertex that all still-active sources have reached needs no scan,
+// and its scan stops once those are covered (late levels, where few sources' searches are
+// still running, otherwise scan every in-edge of every vertex some source never reaches)
+#ifndef PJ_MS_UF
+#define PJ_MS_UF 0
+#endif
+template <int W>
+__device__ __forceinline__ void ms_uf_read(const MsCtl* c, int slot, u64 (&m)[W]) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) m[j] = 0;
+    for (int i = 0; i < MS_NSH; ++i)
+#pragma unroll
+        for (int j = 0; j < W; ++j) m[j] |= c->uf[slot][i][j];
+}
+// the block's OR of the lanes' masks into shard blockIdx % MS_NSH of slot (block-uniform call)
+template <int W>
+__device__ __forceinline__ void ms_uf_add(MsCtl* c, int slot, const u64 (&m)[W], u64 (*red)[MS_WMAX]) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        u64 x = m[j];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x |= __shfl_xor(x, off, 64);
+        if (lane_id() == 0) red[threadIdx.x / WAVE][j] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)W) {
+        u64 o = 0;
+        for (int w = 0; w < 256 / WAVE; ++w) o |= red[w][threadIdx.x];
+        if (o) atomicOr(&c->uf[slot][blockIdx.x % MS_NSH][threadIdx.x], o);
+    }
+}
 
 __device__ __forceinline__ u64 ms_fedges(const MsCtl* c, int slot) {
     u64 t = 0;
@@ -159,6 +195,7 @@ __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __rest
         ctl->done = 0;
         *host_done = -1;
     }
+    for (i64 i = tid; i < 3 * MS_NSH * MS_WMAX; i += nth) (&ctl->uf[0][0][0])[i] = 0;
     for (i64 i = tid; i < nw; i += nth) {
         V[i] = 0;
         F[i] = 0;
@@ -184,6 +221,7 @@ __global__ void ms_sources_k(const int64_t* __restrict__ src, int ns, int W, i64
     atomicOr(&Z[s >> 6], 1ull << (s & 63));
     dist[(i64)i * n + s] = 0;
     ctl->active[2] = 1;  // "level -1" found the sources
+    atomicOr(&ctl->uf[2][0][i >> 6], 1ull << (i & 63));
     atomicAdd(&ctl->fedges[2][0][0], (u64)(row[s + 1] - row[s]));
 }
 
@@ -203,6 +241,8 @@ __global__ __launch_bounds__(MB) void ms_prep_k(i64 n, u64* __restrict__ Fn, int
         if (threadIdx.x == 0) ctl->active[(L + 1) % 3] = 0;
         ctl->fedges[(L + 1) % 3][threadIdx.x][0] = 0;
     }
+    if (PJ_MS_UF && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < MS_NSH * MS_WMAX; i += MB) (&ctl->uf[(L + 1) % 3][0][0])[i] = 0;
     if (!ms_is_push(ctl, L, push_max)) return;
     ulonglong2* p = reinterpret_cast<ulonglong2*>(Fn);
     const i64 n2 = n * W / 2;
@@ -287,8 +327,10 @@ __global__ __launch_bounds__(MB) void ms_fin_k(i64 n, const Off* __restrict__ ro
                                                Mask<W> smask, u64 push_max, MsCtl* ctl, u64* __restrict__ Zn) {
     if (!ms_live(ctl, L) || !ms_is_push(ctl, L, push_max)) return;
     __shared__ u64 red[MB / WAVE];
+    __shared__ u64 ured[MB / WAVE][MS_WMAX];
     const int lane = lane_id();
     u64 found_any = 0, fe = 0;
+    u64 ufl[W] = {};
     const i64 nwaves = (i64)gridDim.x * (MB / WAVE);
     for (i64 base = ((i64)blockIdx.x * (MB / WAVE) + wave_id()) * 64; base < n; base += nwaves * 64) {
         const i64 v = base + lane;
@@ -321,8 +363,12 @@ __global__ __launch_bounds__(MB) void ms_fin_k(i64 n, const Off* __restrict__ ro
             const u64 zb = __ballot(anynew);
             if (lane == 0) Zn[base >> 6] = zb;
         }
+        if (PJ_MS_UF)
+#pragma unroll
+            for (int j = 0; j < W; ++j) ufl[j] |= newb.w[j];
         ms_write_dist<W>(newb, dist, n, v, L + 1);
     }
+    if (PJ_MS_UF) ms_uf_add<W>(ctl, L % 3, ufl, ured);
     fe = block_sum<MB / WAVE>(fe, red);
     if (threadIdx.x == 0 && fe) ms_add_fedges(ctl, L % 3, fe);
     if (__ballot(found_any != 0) && lane == 0) ctl->active[L % 3] = 1;
@@ -338,8 +384,11 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
     // level L computes distance L+1 from the frontier of level L-1 (pull form)
     if (!ms_live(ctl, L) || ms_is_push(ctl, L, push_max)) return;
     __shared__ u64 red[MB / WAVE];
+    __shared__ u64 ured[MB / WAVE][MS_WMAX];
     const int lane = lane_id();
     u64 found_any = 0, fe = 0;
+    u64 ufl[W] = {}, act[W];
+    if (PJ_MS_UF) ms_uf_read<W>(ctl, (L + 2) % 3, act);
     const i64 nwaves = (i64)gridDim.x * (MB / WAVE);
     for (i64 base = ((i64)blockIdx.x * (MB / WAVE) + wave_id()) * 64; base < n; base += nwaves * 64) {
         const i64 v = base + lane;
@@ -350,6 +399,7 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
         for (int j = 0; j < W; ++j) {
             if (!inr) vv.w[j] = ~0ull;
             need.w[j] = ~vv.w[j] & smask.w[j];  // sources of this batch that have not reached v
+            if (PJ_MS_UF) need.w[j] &= act[j];  // ... and whose search is still running
         }
         const bool hasneed = many<W>(need);
         if (__ballot(hasneed) == 0) {
@@ -437,9 +487,13 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
             const u64 zb = __ballot(anynew);
             if (lane == 0) Zn[base >> 6] = zb;
         }
+        if (PJ_MS_UF)
+#pragma unroll
+            for (int j = 0; j < W; ++j) ufl[j] |= newb.w[j];
         if (anynew) fe += (u64)(row[v + 1] - row[v]);
         ms_write_dist<W>(newb, dist, n, v, L + 1);
     }
+    if (PJ_MS_UF) ms_uf_add<W>(ctl, L % 3, ufl, ured);
     fe = block_sum<MB / WAVE>(fe, red);
     if (threadIdx.x == 0 && fe) ms_add_fedges(ctl, L % 3, fe);
     if (__ballot(found_any != 0) && lane == 0) ctl->active[L % 3] = 1;
