@@ -92,34 +92,15 @@ struct WArgs {
     const u64* sbits;  // the tail's settled filter (global ids; null before the tail switch)
 };
 
-__device__ __forceinline__ bool wp_settled(const WArgs& a, u32 t) {
-    return a.sbits && ((a.sbits[t >> 6] >> (t & 63)) & 1ull);
-}
-
-// one relaxation; returns 1 when it adds t to the next frontier (the callers count
-// these per thread and add the block's sum to ST_NF once: an atomicAdd per marked
-// vertex on that one word serialized the light rounds behind its atomic rate)
-__device__ __forceinline__ u32 wp_edge(const WArgs& a, bool light, u32 t, long long nd) {
-    if (nd >= INT_INF || wp_settled(a, t)) return 0u;
-    const i64 tl = (i64)t - a.lo;
-    if (tl >= 0 && tl < a.nl) {
-        if ((int32_t)nd < wp_now(a.dist + tl)) {
-            atomicMin(a.dist + tl, (int32_t)nd);
-            if (light && (int32_t)nd < a.dhi) {
-                const u64 bit = 1ull << (tl & 63);
-                if (!(atomicOr(a.frn + (tl >> 6), bit) & bit)) return 1u;
-            }
-        }
-    } else if ((int32_t)nd < wp_now(a.cand + t)) {
-        atomicMin(a.cand + t, (int32_t)nd);
-        atomicOr(a.touched + (t >> 6), 1ull << (t & 63));
-    }
-    return 0u;
-}
+// A relaxation: an owned target is lowered with atomicMin and, in a light step below hi,
+// marked in the next frontier (returning 1 when this relaxation set the mark: the callers
+// count the marks per thread and add the block's sum to ST_NF once -- an atomicAdd per
+// marked vertex on that one word serialized the light rounds behind its atomic rate); a
+// remote target's candidate is folded into cand and its touched bit set.
 
 // WP_PU edges of one source in one step: the target reads of all of them issued before
-// any atomic (wp_edge one by one is a dependent chain of read, atomicMin and atomicOr per
-// edge); same rule as wp_edge, returns the number of newly marked frontier vertices
+// any atomic (one edge at a time is a dependent chain of read, atomicMin and atomicOr per
+// edge); returns the number of newly marked frontier vertices
 #ifndef PJ_WP_PU
 #define PJ_WP_PU 2
 #endif
@@ -152,6 +133,48 @@ __device__ __forceinline__ u32 wp_edges(const WArgs& a, bool light, u64 k, u64 l
     u32 nf = 0;
 #pragma unroll
     for (int j = 0; j < WP_PU; ++j) {
+        if (!ok[j] || (int32_t)nd[j] >= cur[j]) continue;
+        if (loc[j]) {
+            const i64 tl = (i64)t[j] - a.lo;
+            atomicMin(a.dist + tl, (int32_t)nd[j]);
+            if (light && (int32_t)nd[j] < a.dhi) {
+                const u64 bit = 1ull << (tl & 63);
+                if (!(atomicOr(a.frn + (tl >> 6), bit) & bit)) ++nf;
+            }
+        } else {
+            atomicMin(a.cand + t[j], (int32_t)nd[j]);
+            atomicOr(a.touched + (t[j] >> 6), 1ull << (t[j] & 63));
+        }
+    }
+    return nf;
+}
+
+// N independent edges (any sources: target t, offer nd, valid ok) relaxed with the loads
+// issued together -- the settled bits, then the target distances / candidates, then the
+// atomics -- instead of one dependent chain per edge (wp_edge); returns the marks
+template <int N>
+__device__ __forceinline__ u32 wp_edges_g(const WArgs& a, bool light, const u32 (&t)[N], const long long (&nd)[N],
+                                          bool (&ok)[N]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) ok[j] = ok[j] && nd[j] < INT_INF;
+    if (a.sbits) {
+        u64 sw[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) sw[j] = ok[j] ? a.sbits[t[j] >> 6] : 0ull;
+#pragma unroll
+        for (int j = 0; j < N; ++j) ok[j] = ok[j] && !((sw[j] >> (t[j] & 63)) & 1ull);
+    }
+    bool loc[N];
+    int32_t cur[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const i64 tl = (i64)t[j] - a.lo;
+        loc[j] = tl >= 0 && tl < a.nl;
+        cur[j] = !ok[j] ? 0 : (loc[j] ? wp_now(a.dist + tl) : wp_now(a.cand + t[j]));
+    }
+    u32 nf = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
         if (!ok[j] || (int32_t)nd[j] >= cur[j]) continue;
         if (loc[j]) {
             const i64 tl = (i64)t[j] - a.lo;
@@ -305,18 +328,26 @@ __global__ __launch_bounds__(WB) void wp_relax_k(WArgs a) {
                 const u64 inc = wave_incl_scan(rem);
                 const u64 exc = inc - rem;
                 const u64 tot = __shfl(inc, 63, 64);
-                for (u64 g0 = 0; g0 < tot; g0 += WAVE) {
-                    const u64 gi = g0 + lane;
-                    int l = 0;
+                constexpr int NJ = 4;  // edges per lane and step, relaxed together (wp_edges_g)
+                for (u64 g0 = 0; g0 < tot; g0 += NJ * WAVE) {
+                    u32 t[NJ];
+                    long long nd[NJ];
+                    bool ok[NJ];
 #pragma unroll
-                    for (int step = 32; step > 0; step >>= 1)
-                        if (__shfl(inc, l + step - 1, 64) <= gi) l += step;
-                    const u64 kl = __shfl(k, l, 64), xl = __shfl(exc, l, 64);
-                    const int32_t dl = __shfl(du, l, 64);
-                    if (gi < tot) {
+                    for (int j = 0; j < NJ; ++j) {
+                        const u64 gi = g0 + (u64)j * WAVE + lane;
+                        int l = 0;
+#pragma unroll
+                        for (int step = 32; step > 0; step >>= 1)
+                            if (__shfl(inc, l + step - 1, 64) <= gi) l += step;
+                        const u64 kl = __shfl(k, l, 64), xl = __shfl(exc, l, 64);
+                        const int32_t dl = __shfl(du, l, 64);
+                        ok[j] = gi < tot;
                         const u64 kk = kl + (gi - xl);
-                        nf += wp_edge(a, LIGHT, a.col[kk], (long long)dl + a.w[kk]);
+                        t[j] = ok[j] ? a.col[kk] : 0u;
+                        nd[j] = (long long)dl + (ok[j] ? a.w[kk] : 0u);
                     }
+                    nf += wp_edges_g<NJ>(a, LIGHT, t, nd, ok);
                 }
             }
         }
@@ -345,15 +376,25 @@ __global__ __launch_bounds__(WB) void wp_long_k(WArgs a) {
             s_b[i] = a.lq_b[s0 + i];
         }
         __syncthreads();
+        constexpr int NJ = WP_TILE / WB;  // the thread's edges, relaxed together (wp_edges_g)
+        u32 t[NJ];
+        long long nd[NJ];
+        bool ok[NJ];
 #pragma unroll
-        for (int j = 0; j < WP_TILE / WB; ++j) {
+        for (int j = 0; j < NJ; ++j) {
             const u64 e = e0 + (u64)j * WB + threadIdx.x;
-            if (e < total) {
+            ok[j] = e < total;
+            u64 k = 0;
+            int32_t du = 0;
+            if (ok[j]) {
                 const u32 sl = lb_find<WP_TILE>(sh, ns, e);
-                const u64 k = s_b[sl] + (e - sh.off[sl]);
-                nf += wp_edge(a, LIGHT, a.col[k], (long long)s_du[sl] + a.w[k]);
+                k = s_b[sl] + (e - sh.off[sl]);
+                du = s_du[sl];
             }
+            t[j] = ok[j] ? a.col[k] : 0u;
+            nd[j] = (long long)du + (ok[j] ? a.w[k] : 0u);
         }
+        nf += wp_edges_g<NJ>(a, LIGHT, t, nd, ok);
         __syncthreads();
     }
     if (LIGHT) wp_flush_nf(a, nf, red);
@@ -428,9 +469,21 @@ __global__ __launch_bounds__(WB) void wp_pack_k(WArgs a, i64 nwords, int world, 
 __global__ __launch_bounds__(WB) void wp_apply_k(WArgs a, const u64* __restrict__ recv, i64 nr, int light) {
     __shared__ u64 red[WB / WAVE];
     u32 nf = 0;
-    for (i64 i = (i64)blockIdx.x * WB + threadIdx.x; i < nr; i += (i64)gridDim.x * WB) {
-        const u64 x = recv[i];
-        nf += wp_edge(a, light != 0, (u32)x, (long long)(int32_t)(u32)(x >> 32));
+    constexpr int NJ = 4;  // received pairs per thread and step, relaxed together
+    const i64 stride = (i64)gridDim.x * WB;
+    for (i64 i0 = (i64)blockIdx.x * WB + threadIdx.x; i0 < nr; i0 += NJ * stride) {
+        u32 t[NJ];
+        long long nd[NJ];
+        bool ok[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const i64 i = i0 + (i64)j * stride;
+            ok[j] = i < nr;
+            const u64 x = ok[j] ? recv[i] : 0ull;
+            t[j] = (u32)x;
+            nd[j] = (long long)(int32_t)(u32)(x >> 32);
+        }
+        nf += wp_edges_g<NJ>(a, light != 0, t, nd, ok);
     }
     if (light) wp_flush_nf(a, nf, red);
 }
