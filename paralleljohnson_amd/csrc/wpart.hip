@@ -569,11 +569,17 @@ constexpr int WP_PSERIAL = 16;
 #define PJ_WP_HPU 1  // 2 and 4 measured no faster at s26w (13.0-13.5 against 12.8-13.2 ms at world 1, r3ai)
 #endif
 constexpr int WP_HPU = PJ_WP_HPU;
-__global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __restrict__ mmap) {
+// It also selects the next band [hi, nhi) as wp_select_k would (frontier words, frn and mb
+// cleared, ST_CNT and ST_MIN): a vertex's distance is final for this step once its lane is
+// done, and the wave owns its word.
+__global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __restrict__ mmap, int32_t nhi) {
+    __shared__ u64 red[WB / WAVE];
     const int lane = lane_id();
     const int32_t lo = a.dlo, hi = a.dhi;
     const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
-    for (i64 b0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; b0 < a.nl; b0 += nwaves * 64) {
+    u64 c = 0;
+    int32_t mn = INT_INF;
+    for (i64 b0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; b0 < a.bw * 64; b0 += nwaves * 64) {
         const i64 v = b0 + lane;
         int32_t d0 = INT_INF, cur = INT_INF;
         u64 k = 0, e = 0;
@@ -647,6 +653,30 @@ __global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __
             if (lane == l) cur = cl;
         }
         if (act && cur < d0) a.dist[v] = cur;  // (the vertex's own rank is its only writer here)
+        const int32_t dn = act ? cur : d0;  // (d0 = INT_INF past nl)
+        const u64 m = __ballot(dn >= hi && dn < nhi);
+        if (dn >= hi && dn < mn) mn = dn;
+        if (lane == 0) {
+            a.fr[b0 >> 6] = m;
+            a.frn[b0 >> 6] = 0;
+            a.mb[b0 >> 6] = 0;
+            c += (u64)__popcll(m);
+        }
+    }
+    c = block_sum<WB / WAVE>(c, red);
+    if (threadIdx.x == 0 && c) atomicAdd(&a.stat[ST_CNT], c);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int32_t y = __shfl_xor(mn, off, 64);
+        mn = y < mn ? y : mn;
+    }
+    __syncthreads();
+    if (lane == 0) red[wave_id()] = (u64)(u32)mn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t m = INT_INF;
+        for (int k = 0; k < WB / WAVE; ++k) m = min(m, (int32_t)(u32)red[k]);
+        if (m < INT_INF) atomicMin(&a.stat[ST_MIN], (u64)m);
     }
 }
 
@@ -832,6 +862,7 @@ struct WPart {
     int32_t ua_hi = INT_MIN;  // wp_heavy_counts_k's third count is for this hi (this band)
     i64 ua = 0;
     int32_t ms_lo = INT_MIN;  // wp_heavy_counts_k wrote the member slice of the band starting here
+    int32_t fs_lo = INT_MIN, fs_hi = INT_MIN;  // wp_pull_heavy_k selected [fs_lo, fs_hi) (stat, fr, frn, mb)
     i64 exch_bytes = 0;  // the engine view's send + recv buffers (sized to the largest round)
     DevBuf<u32> lq_v;
     DevBuf<u64> lq_b, lq_e;
@@ -1399,7 +1430,13 @@ void wpart_member_slice(WPart& p, int32_t lo, int32_t hi) {
 void wpart_heavy_pull(WPart& p, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
     if (p.nl > 0) {
-        wp_pull_heavy_k<<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.mmap.p);
+        // the next band's select rides along (wpart_select_async of [hi, nhi) then reads it)
+        const int32_t nhi = (int32_t)std::min<i64>((i64)hi + p.delta, INT_INF);
+        PJ_HIP(hipMemsetAsync(p.stat.p + ST_MIN, 0xFF, sizeof(u64), s));
+        PJ_HIP(hipMemsetAsync(p.stat.p + ST_CNT, 0, sizeof(u64), s));
+        wp_pull_heavy_k<<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.mmap.p, nhi);
+        p.fs_lo = hi;
+        p.fs_hi = nhi;
         PJ_LAUNCH_CHECK();
     }
     // (no wait: the band's next host step -- the tail count or the select -- waits on the stream)
@@ -1464,6 +1501,7 @@ int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
     p.sb_on = false;
     p.ua_hi = INT_MIN;
     p.ms_lo = INT_MIN;
+    p.fs_lo = p.fs_hi = INT_MIN;
     if (p.nl > 0) PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.dist.p), INT_INF, (size_t)p.nl, s));
     if (p.world > 1 && p.n > 0)
         PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.cand.p), INT_INF, (size_t)p.n, s));
@@ -1484,6 +1522,11 @@ int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
 
 static void wpart_select_async(WPart& p, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
+    if (p.fs_lo == lo && p.fs_hi == hi) {  // selected by the heavy pull that ended the last band
+        p.fs_lo = p.fs_hi = INT_MIN;
+        return;
+    }
+    p.fs_lo = p.fs_hi = INT_MIN;
     p.clear_stat();
     PJ_HIP(hipMemsetAsync(p.stat.p + ST_MIN, 0xFF, sizeof(u64), s));
     wp_select_k<<<grid_for(p.bw * 64, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi));
