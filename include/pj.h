@@ -476,9 +476,9 @@ int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj
  * 0 = always push; default 4) and "light_pull" (a light round whose frontier has more light
  * edges than the vertices above the band start / light_pull runs as a pull through an
  * all-gathered frontier map; symmetric graphs; 0 = push; default 0: since the push rounds
- * count their frontier per workgroup the pull no longer pays, profiles/r03/wpart_light_pull_r3ad.txt).
- * Every rank must use the
- * same values. */
+ * count their frontier per workgroup the pull no longer pays, profiles/r03/wpart_light_pull_r3ad.txt)
+ * and "tail_light_pull" (the same rule in the tail's bands, independent of light_pull, the
+ * frontier map then 16-bit; 0 = push; default 3). Every rank must use the same values. */
 int pj_wpart_set_option(pj_wpart* p, const char* key, double value);
 int pj_wpart_delta_group(int world, pj_wpart* const* parts, pj_comm* const* comms, int64_t source, int32_t delta,
                          pj_part_stats* st);

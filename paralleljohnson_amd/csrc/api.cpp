@@ -1715,6 +1715,7 @@ int pj_wpart_set_option(pj_wpart* p, const char* key, double value) {
     else if (k == "tail_mult" && value >= 1) wpart_tail_params(P)[1] = value;
     else if (k == "pull_factor" && value >= 0) wpart_pull_factor(P) = value;
     else if (k == "light_pull" && value >= 0) wpart_light_pull(P) = value;
+    else if (k == "tail_light_pull" && value >= 0) wpart_tail_light_pull(P) = value;
     else return arg_error("pj_wpart_set_option: unknown key or bad value");
     return PJ_OK;
 }

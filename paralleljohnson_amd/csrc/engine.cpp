@@ -179,10 +179,13 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
         }
         // the pull rules: agreed once per solve (any rank vetoes: a rank whose rows are not
         // its in-edges, or with a pull off), so a vetoed pull costs no per-band collective
-        const double pf = S.pull_factor(), lpf = S.light_pull_factor();
-        i64 allow[2] = {pf > 0.0 ? 1 : 0, lpf > 0.0 ? 1 : 0};
-        comm.allreduce(allow, 2, false, s);
-        const bool heavy_pull_ok = allow[0] == S.world, light_pull_ok = allow[1] == S.world;
+        const double pf = S.pull_factor(), lpf0 = S.light_pull_factor(), tlpf = S.tail_light_pull_factor();
+        i64 allow[3] = {pf > 0.0 ? 1 : 0, lpf0 > 0.0 ? 1 : 0, tlpf > 0.0 ? 1 : 0};
+        comm.allreduce(allow, 3, false, s);
+        const bool heavy_pull_ok = allow[0] == S.world, tail_light_ok = allow[2] == S.world;
+        bool light_pull_ok = allow[1] == S.world;
+        double lpf = lpf0;
+        const i64 map_w = S.pull_map_width();
         std::vector<i64> counts((size_t)S.world), rcounts((size_t)S.world);
         i64 sent = 0, bands = 0, rounds = 0, pulls = 0, lpulls = 0;
         auto exchange_apply = [&](int light, int32_t lo, int32_t hi) {
@@ -239,7 +242,7 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
                 // a big round may pull (the gate keeps the counts off small rounds; every rank
                 // sees the same fsize)
                 bool lpulled = false;
-                if (light_pull_ok && hi - lo <= 255 && fsize * 64 >= S.n) {
+                if (light_pull_ok && hi - lo <= map_w && fsize * 64 >= S.n) {
                     i64 lc[2] = {0, 0};
                     S.light_counts((int32_t)lo, (int32_t)hi, lc);
                     comm.allreduce(lc, 2, false, s);
@@ -298,6 +301,8 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
                         delta = tdelta;
                         S.set_delta(delta);
                         tail_on = false;
+                        light_pull_ok = tail_light_ok;  // the tail's own light-pull rule
+                        lpf = tlpf;
                         if (S.settled_map()) {  // everything below hi is settled from here on
                             S.settled_slice((int32_t)hi);
                             if (S.world > 1) {

@@ -163,6 +163,10 @@ struct DeltaSteps {
     // above lo scan its light row for frontier vertices and marks the improved ones below hi.
     // light_counts(): this rank's (frontier light edges, light edges of vertices above lo).
     virtual double light_pull_factor() { return -1.0; }
+    // the same rule after the tail switch (defaults to light_pull_factor), and the widest band
+    // the frontier map can encode (dist - lo per vertex)
+    virtual double tail_light_pull_factor() { return light_pull_factor(); }
+    virtual int32_t pull_map_width() { return 255; }
     virtual void light_counts(int32_t lo, int32_t hi, i64* out2) { (void)lo, (void)hi, out2[0] = out2[1] = 0; }
     virtual void frontier_slice(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
     virtual void light_pull(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
@@ -190,6 +194,7 @@ const Ctx& wpart_ctx(const WPart& p);
 double* wpart_tail_params(WPart& p);  // [0] tail_frac, [1] tail_mult (pj_wpart_set_option)
 double& wpart_pull_factor(WPart& p);  // heavy pull rule (pj_wpart_set_option "pull_factor")
 double& wpart_light_pull(WPart& p);   // light pull rule (pj_wpart_set_option "light_pull")
+double& wpart_tail_light_pull(WPart& p);  // its tail form ("tail_light_pull")
 // every rank's slice of dist, gathered (n int32 to host; NULL: gather only)
 void part_gather_dist(Part& p, Comm& comm, int32_t* out);
 void wpart_gather_dist(WPart& p, Comm& comm, int32_t* out);

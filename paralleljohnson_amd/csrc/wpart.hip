@@ -696,11 +696,14 @@ __global__ __launch_bounds__(WB) void wp_light_counts_k(WArgs a, u64* __restrict
         if (u) atomicAdd(&out[1], u);
     }
 }
-// this rank's slice of the frontier map: dist - lo of a frontier vertex, 0xFF otherwise
-__global__ void wp_frontier_slice_k(WArgs a, uint8_t* __restrict__ own) {
+// this rank's slice of the frontier map: dist - lo of a frontier vertex, all ones otherwise
+// (MT = u8 for bands up to 255 wide, u16 for the tail's wide bands)
+template <typename MT>
+__global__ void wp_frontier_slice_k(WArgs a, MT* __restrict__ own) {
+    constexpr MT NONE = (MT)~(MT)0;
     for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < a.block; v += (i64)gridDim.x * blockDim.x) {
-        uint8_t x = 0xFF;
-        if (v < a.nl && ((a.fr[v >> 6] >> (v & 63)) & 1ull)) x = (uint8_t)(a.dist[v] - a.dlo);
+        MT x = NONE;
+        if (v < a.nl && ((a.fr[v >> 6] >> (v & 63)) & 1ull)) x = (MT)(a.dist[v] - a.dlo);
         own[v] = x;
     }
 }
@@ -709,7 +712,9 @@ __global__ void wp_frontier_slice_k(WArgs a, uint8_t* __restrict__ own) {
 // once lo + w >= its best value; improved vertices below hi join the next frontier. The
 // wave owns its 64 vertices' words: the frontier word moves into mb (the round consumed
 // it) and the next-frontier word is OR-ed in whole.
-__global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const uint8_t* __restrict__ fmap) {
+template <typename MT>
+__global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const MT* __restrict__ fmap) {
+    constexpr MT NONE = (MT)~(MT)0;
     __shared__ u64 red[WB / WAVE];
     const int lane = lane_id();
     const int32_t lo = a.dlo, hi = a.dhi;
@@ -744,8 +749,8 @@ __global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const uint8_t* __
                 done = true;
                 break;
             }
-            const uint8_t m = fmap[a.col[k]];
-            if (m != 0xFF) cur = min(cur, lo + (int32_t)m + (int32_t)w);
+            const MT m = fmap[a.col[k]];
+            if (m != NONE) cur = min(cur, lo + (int32_t)m + (int32_t)w);
             ++k;
         }
         if (k >= e) done = true;
@@ -762,8 +767,8 @@ __global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const uint8_t* __
                 const bool stop = !valid || (long long)lo + w >= (long long)cl;
                 int32_t cand = INT_INF;
                 if (!stop) {
-                    const uint8_t m = fmap[a.col[k0]];
-                    if (m != 0xFF) cand = lo + (int32_t)m + (int32_t)w;
+                    const MT m = fmap[a.col[k0]];
+                    if (m != NONE) cand = lo + (int32_t)m + (int32_t)w;
                 }
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) {
@@ -844,12 +849,16 @@ struct WPart {
     int32_t delta_alt = 0;         // the light threshold lsplit_alt was computed for (0 = none)
     double tail[2] = {0.1, 64.0};  // tail switch (engine.h DeltaSteps): tail_frac (0 = off), threshold / delta
     double pull_factor = 4.0;      // heavy pull when unsettled heavy edges < pull_factor x members' (0 = push)
+    double tail_light_pull = 3.0;  // the same rule after the tail switch (independent of light_pull; 0 =
+                                   // push), with a 16-bit frontier map for the tail's wide bands
     double light_pull = 0.0;       // light pull round when the frontier's light edges > the light edges
                                    // of the vertices above lo / light_pull (0 = push; 3 was the default
                                    // until the push rounds counted their frontier per workgroup: then
                                    // 0 measured best at s24w / s26w, world 1 and 2, r3ad)
     bool symmetric = false;        // rows are also the in-edges (Kronecker graphs): the heavy pull applies
     DevBuf<uint8_t> mmap;          // replicated member map of the heavy pull (world x block bytes)
+    DevBuf<uint16_t> fmap16;       // replicated frontier map of a light pull in a band wider than 255
+    bool map16 = false;            // the last slice went to fmap16 (member_map() hands it out)
     DevBuf<u64> row;
     DevBuf<u32> col, w, lsplit;
     DevBuf<u32> lsplit_alt;        // the other light threshold's prefixes (delta and the tail's are
@@ -1380,6 +1389,7 @@ void wpart_heavy_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
     }
     out2[0] = (i64)h[0];
     out2[1] = (i64)h[1];
+    p.map16 = false;  // (the member map is the u8 one)
     p.ua_hi = hi;  // (wpart_unsettled(hi) of this band)
     p.ua = (i64)h[2];
     p.ms_lo = hi - lo <= 255 && p.nl > 0 ? lo : INT_MIN;  // (the member slice of this band is written)
@@ -1400,9 +1410,16 @@ void wpart_light_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
 }
 
 void wpart_frontier_slice(WPart& p, int32_t lo, int32_t hi) {
-    if (!p.mmap.p) p.mmap.alloc((size_t)p.world * (size_t)p.block);
-    wp_frontier_slice_k<<<grid_for(p.block, 256, p.grid()), 256, 0, p.ctx->stream>>>(
-        p.args(lo, hi), p.mmap.p + (size_t)p.rank * (size_t)p.block);
+    p.map16 = hi - lo > 255;  // (the tail's bands: 16-bit offsets; member_map() follows)
+    if (p.map16) {
+        if (!p.fmap16.p) p.fmap16.alloc((size_t)p.world * (size_t)p.block);
+        wp_frontier_slice_k<uint16_t><<<grid_for(p.block, 256, p.grid()), 256, 0, p.ctx->stream>>>(
+            p.args(lo, hi), p.fmap16.p + (size_t)p.rank * (size_t)p.block);
+    } else {
+        if (!p.mmap.p) p.mmap.alloc((size_t)p.world * (size_t)p.block);
+        wp_frontier_slice_k<uint8_t><<<grid_for(p.block, 256, p.grid()), 256, 0, p.ctx->stream>>>(
+            p.args(lo, hi), p.mmap.p + (size_t)p.rank * (size_t)p.block);
+    }
     PJ_LAUNCH_CHECK();
 }
 
@@ -1411,12 +1428,14 @@ void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
     p.clear_stat();
     if (p.nl > 0) {
-        wp_pull_light_k<<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.mmap.p);
+        if (p.map16) wp_pull_light_k<uint16_t><<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.fmap16.p);
+        else wp_pull_light_k<uint8_t><<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.mmap.p);
         PJ_LAUNCH_CHECK();
     }
 }
 
 void wpart_member_slice(WPart& p, int32_t lo, int32_t hi) {
+    p.map16 = false;
     if (p.ms_lo == lo) {  // written by this band's wp_heavy_counts_k
         p.ms_lo = INT_MIN;
         return;
@@ -1673,10 +1692,12 @@ struct WPartGpuSteps final : DeltaSteps {
     double pull_factor() override { return p.symmetric ? p.pull_factor : 0.0; }  // (0: this rank vetoes)
     void heavy_counts(int32_t lo, int32_t hi, i64* out2) override { wpart_heavy_counts(p, lo, hi, out2); }
     void member_slice(int32_t lo, int32_t hi) override { wpart_member_slice(p, lo, hi); }
-    void* member_map() override { return p.mmap.p; }
-    size_t member_bytes() override { return (size_t)p.block; }
+    void* member_map() override { return p.map16 ? (void*)p.fmap16.p : (void*)p.mmap.p; }
+    size_t member_bytes() override { return (size_t)p.block * (p.map16 ? 2 : 1); }
     void heavy_pull(int32_t lo, int32_t hi) override { wpart_heavy_pull(p, lo, hi); }
     double light_pull_factor() override { return p.symmetric ? p.light_pull : 0.0; }
+    double tail_light_pull_factor() override { return p.symmetric ? p.tail_light_pull : 0.0; }
+    int32_t pull_map_width() override { return 65534; }
     void light_counts(int32_t lo, int32_t hi, i64* out2) override { wpart_light_counts(p, lo, hi, out2); }
     void frontier_slice(int32_t lo, int32_t hi) override { wpart_frontier_slice(p, lo, hi); }
     void light_pull(int32_t lo, int32_t hi) override { wpart_light_pull(p, lo, hi); }
@@ -1689,6 +1710,7 @@ const Ctx& wpart_ctx(const WPart& p) { return *p.ctx; }
 double* wpart_tail_params(WPart& p) { return p.tail; }
 double& wpart_pull_factor(WPart& p) { return p.pull_factor; }
 double& wpart_light_pull(WPart& p) { return p.light_pull; }
+double& wpart_tail_light_pull(WPart& p) { return p.tail_light_pull; }
 
 DeltaSteps& wpart_steps(WPart& p) {
     if (!p.steps) p.steps.reset(new WPartGpuSteps(p));

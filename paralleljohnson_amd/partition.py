@@ -309,7 +309,8 @@ class DeviceWPart:
         return {"rows": int(out[0]), "state": int(out[1]), "tables": int(out[2]), "exchange": int(out[3])}
 
     def set_option(self, key: str, value: float):
-        """pj_wpart_set_option: "tail_frac", "tail_mult", "pull_factor" or "light_pull".
+        """pj_wpart_set_option: "tail_frac", "tail_mult", "pull_factor", "light_pull" or
+        "tail_light_pull".
 
         Every rank of a group must set the same values (the ranks take the tail switch and
         the pull decisions from all-reduced counts, and agree once per solve whether every
