@@ -1,7 +1,8 @@
 """Weighted partitioned solve (wpart.hip + engine.cpp) on Kronecker s{scale} weights 1..255 at
 world 1 (no transport) and world 2 (both ranks on this GPU, host transport): per-solve time
 with the tail switch, the heavy pull and the light pull rounds at their defaults and off, or under the
-given (tail_frac, pull_factor, light_pull) sets. Usage: python tools/probe_wpart.py [scale=26] ["tf,pf,lp;tf,pf,lp..."]"""
+given (tail_frac, pull_factor, light_pull[, tail_light_pull = 3]) sets.
+Usage: python tools/probe_wpart.py [scale=26] ["tf,pf,lp[,tlp];tf,pf,lp[,tlp]..."]"""
 import os, sys, time
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
 import numpy as np
@@ -20,16 +21,19 @@ for world in (1, 2):
     sets = ((0.1, 4, 0), (0.1, 4, 0))
     if len(sys.argv) > 2:
         sets = [tuple(float(x) for x in t.split(",")) for t in sys.argv[2].split(";")]
-    for tf, pf, lp in sets:
+    for st4 in sets:
+        tf, pf, lp = st4[:3]
+        tlp = st4[3] if len(st4) > 3 else 3.0
         for p in parts:
             p.set_option("tail_frac", tf)
             p.set_option("pull_factor", pf)
             p.set_option("light_pull", lp)
+            p.set_option("tail_light_pull", tlp)
         ms = []
         for r in roots:
             st = delta_group(parts, comms, r)
             ms.append(max(s["solve_ms"] for s in st))
-        print(f"world {world} s{scale}w tail_frac {tf} pull_factor {pf} light_pull {lp}: solve ms "
+        print(f"world {world} s{scale}w tail_frac {tf} pull_factor {pf} light_pull {lp} tail_light_pull {tlp}: solve ms "
               f"{[round(x, 2) for x in ms]} bands {st[0]['bands']} rounds {st[0]['rounds']} heavy pulls "
               f"{st[0]['heavy_pulls']} light pulls {st[0]['bu_levels']} "
               f"sent {[s['sent'] for s in st]}", flush=True)
