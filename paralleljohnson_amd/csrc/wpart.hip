@@ -208,8 +208,9 @@ __global__ __launch_bounds__(WB) void wp_select_k(WArgs a) {
     const int lane = lane_id();
     u64 c = 0;
     int32_t mn = INT_INF;
-    // (4 words per wave step, loads issued together, as delta.hip's v2_select_k)
-    constexpr int SELW = 4;
+    // (8 words per wave step, loads issued together; lane j then stores word j of the step,
+    // so the three bitmaps take one 64-byte store each instead of eight single-lane stores)
+    constexpr int SELW = 8;
     for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * SELW; w0 < a.bw;
          w0 += (i64)gridDim.x * (WB / WAVE) * SELW) {
         int32_t dd[SELW];
@@ -218,19 +219,19 @@ __global__ __launch_bounds__(WB) void wp_select_k(WArgs a) {
             const i64 v = (w0 + j) * 64 + lane;
             dd[j] = v < a.nl ? a.dist[v] : INT_INF;
         }
+        u64 mine = 0;
 #pragma unroll
         for (int j = 0; j < SELW; ++j) {
-            const i64 wi = w0 + j;
-            if (wi >= a.bw) break;
             const int32_t d = dd[j];
             const u64 m = __ballot(d >= a.dlo && d < a.dhi);
             if (d >= a.dlo && d < mn) mn = d;
-            if (lane == 0) {
-                a.fr[wi] = m;
-                a.frn[wi] = 0;
-                a.mb[wi] = 0;
-                c += (u64)__popcll(m);
-            }
+            if (lane == j) mine = m;
+        }
+        if (lane < SELW && w0 + lane < a.bw) {
+            a.fr[w0 + lane] = mine;
+            a.frn[w0 + lane] = 0;
+            a.mb[w0 + lane] = 0;
+            c += (u64)__popcll(mine);
         }
     }
     c = block_sum<WB / WAVE>(c, red);
@@ -518,20 +519,39 @@ __global__ __launch_bounds__(WB) void wp_heavy_counts_k(WArgs a, int32_t hi, u64
                                                        uint8_t* __restrict__ own) {
     __shared__ u64 red[WB / WAVE];
     u64 m = 0, u = 0, ua = 0;
-    for (i64 v = (i64)blockIdx.x * WB + threadIdx.x; v < a.block; v += (i64)gridDim.x * WB) {
-        uint8_t x = 0xFF;
-        if (v < a.nl) {
-            const u64 deg = a.row[v + 1] - a.row[v], hd = deg - a.lsplit[v];
-            const int32_t d = a.dist[v];
-            if ((a.mb[v >> 6] >> (v & 63)) & 1ull) {
-                m += hd;
-                x = (uint8_t)(d - a.dlo);
-            } else if (d >= hi) {
-                u += hd;
-                ua += deg;
-            }
+    constexpr int HU = 4;  // vertices per thread step, their loads issued together
+    const i64 stride = (i64)gridDim.x * WB;
+    for (i64 v0 = (i64)blockIdx.x * WB + threadIdx.x; v0 < a.block; v0 += HU * stride) {
+        u64 rb[HU], re[HU], mw[HU];
+        u32 ls[HU];
+        int32_t d[HU];
+#pragma unroll
+        for (int j = 0; j < HU; ++j) {
+            const i64 v = v0 + (i64)j * stride;
+            const bool in = v < a.nl;
+            rb[j] = in ? a.row[v] : 0;
+            re[j] = in ? a.row[v + 1] : 0;
+            ls[j] = in ? a.lsplit[v] : 0;
+            d[j] = in ? a.dist[v] : 0;
+            mw[j] = in ? a.mb[v >> 6] : 0;
         }
-        if (own) own[v] = x;
+#pragma unroll
+        for (int j = 0; j < HU; ++j) {
+            const i64 v = v0 + (i64)j * stride;
+            if (v >= a.block) break;
+            uint8_t x = 0xFF;
+            if (v < a.nl) {
+                const u64 deg = re[j] - rb[j], hd = deg - ls[j];
+                if ((mw[j] >> (v & 63)) & 1ull) {
+                    m += hd;
+                    x = (uint8_t)(d[j] - a.dlo);
+                } else if (d[j] >= hi) {
+                    u += hd;
+                    ua += deg;
+                }
+            }
+            if (own) own[v] = x;
+        }
     }
     m = block_sum<WB / WAVE>(m, red);
     u = block_sum<WB / WAVE>(u, red);
@@ -545,12 +565,23 @@ __global__ __launch_bounds__(WB) void wp_heavy_counts_k(WArgs a, int32_t hi, u64
 
 // bit v of the rank's words of the settled map: dist[v] < lo (v past nl: 0)
 __global__ void wp_settled_k(WArgs a, int32_t lo, u64* __restrict__ words) {
+    constexpr int SW = 8;  // words per wave step (loads together, one 8-lane store)
     const int lane = lane_id();
     const i64 nwaves = (i64)gridDim.x * (blockDim.x / WAVE);
-    for (i64 wi = (i64)blockIdx.x * (blockDim.x / WAVE) + wave_id(); wi < a.bw; wi += nwaves) {
-        const i64 v = wi * 64 + lane;
-        const u64 m = __ballot(v < a.nl && a.dist[v] < lo);
-        if (lane == 0) words[wi] = m;
+    for (i64 w0 = ((i64)blockIdx.x * (blockDim.x / WAVE) + wave_id()) * SW; w0 < a.bw; w0 += nwaves * SW) {
+        int32_t dd[SW];
+#pragma unroll
+        for (int j = 0; j < SW; ++j) {
+            const i64 v = (w0 + j) * 64 + lane;
+            dd[j] = v < a.nl ? a.dist[v] : INT_INF;
+        }
+        u64 mine = 0;
+#pragma unroll
+        for (int j = 0; j < SW; ++j) {
+            const u64 m = __ballot(dd[j] < lo);
+            if (lane == j) mine = m;
+        }
+        if (lane < SW && w0 + lane < a.bw) words[w0 + lane] = mine;
     }
 }
 // this rank's slice of the member map: dist - lo of a band member, 0xFF otherwise
@@ -684,10 +715,25 @@ __global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __
 __global__ __launch_bounds__(WB) void wp_light_counts_k(WArgs a, u64* __restrict__ out) {
     __shared__ u64 red[WB / WAVE];
     u64 f = 0, u = 0;
-    for (i64 v = (i64)blockIdx.x * WB + threadIdx.x; v < a.nl; v += (i64)gridDim.x * WB) {
-        const u64 ls = a.lsplit[v];
-        if ((a.fr[v >> 6] >> (v & 63)) & 1ull) f += ls;
-        if (a.dist[v] > a.dlo) u += ls;
+    constexpr int LU = 4;  // vertices per thread step, loads issued together
+    const i64 stride = (i64)gridDim.x * WB;
+    for (i64 v0 = (i64)blockIdx.x * WB + threadIdx.x; v0 < a.nl; v0 += LU * stride) {
+        u64 ls[LU], fw[LU];
+        int32_t d[LU];
+#pragma unroll
+        for (int j = 0; j < LU; ++j) {
+            const i64 v = v0 + (i64)j * stride;
+            const bool in = v < a.nl;
+            ls[j] = in ? a.lsplit[v] : 0;
+            fw[j] = in ? a.fr[v >> 6] : 0;
+            d[j] = in ? a.dist[v] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < LU; ++j) {
+            const i64 v = v0 + (i64)j * stride;
+            if ((fw[j] >> (v & 63)) & 1ull) f += ls[j];
+            if (v < a.nl && d[j] > a.dlo) u += ls[j];
+        }
     }
     f = block_sum<WB / WAVE>(f, red);
     u = block_sum<WB / WAVE>(u, red);
