@@ -82,7 +82,6 @@ struct WArgs {
     int32_t* dist;     // nl
     int32_t* cand;     // n (world > 1)
     u64* touched;      // n / 64 words (world > 1)
-    u64* tgroups;      // bit g: touched words [64 g, 64 g + 64) hold a bit (n / 4096 bits; world > 1)
     u64* fr;           // bw
     u64* frn;          // bw
     u64* mb;           // bw
@@ -92,13 +91,6 @@ struct WArgs {
     u64* stat;
     const u64* sbits;  // the tail's settled filter (global ids; null before the tail switch)
 };
-
-// a remote target's touched bit; the first bit of a touched word also sets its group's bit
-// (the count and pack passes then visit only the groups that hold touched words)
-__device__ __forceinline__ void wp_touch(const WArgs& a, u32 t) {
-    const u64 old = atomicOr(a.touched + (t >> 6), 1ull << (t & 63));
-    if (!old) atomicOr(a.tgroups + (t >> 18), 1ull << ((t >> 12) & 63));
-}
 
 // A relaxation: an owned target is lowered with atomicMin and, in a light step below hi,
 // marked in the next frontier (returning 1 when this relaxation set the mark: the callers
@@ -151,7 +143,7 @@ __device__ __forceinline__ u32 wp_edges(const WArgs& a, bool light, u64 k, u64 l
             }
         } else {
             atomicMin(a.cand + t[j], (int32_t)nd[j]);
-            wp_touch(a, t[j]);
+            atomicOr(a.touched + (t[j] >> 6), 1ull << (t[j] & 63));
         }
     }
     return nf;
@@ -193,7 +185,7 @@ __device__ __forceinline__ u32 wp_edges_g(const WArgs& a, bool light, const u32 
             }
         } else {
             atomicMin(a.cand + t[j], (int32_t)nd[j]);
-            wp_touch(a, t[j]);
+            atomicOr(a.touched + (t[j] >> 6), 1ull << (t[j] & 63));
         }
     }
     return nf;
@@ -415,7 +407,6 @@ __global__ __launch_bounds__(WB) void wp_count_k(WArgs a, i64 nwords) {
     const int lane = lane_id();
     const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
     for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; w0 < nwords; w0 += nwaves * 64) {
-        if (!((a.tgroups[w0 >> 12] >> ((w0 >> 6) & 63)) & 1ull)) continue;  // (wave-uniform)
         const i64 wi = w0 + lane;
         const u32 cnt = wi < nwords ? (u32)__popcll(a.touched[wi]) : 0u;
         const int owner = wi < nwords ? (int)((wi * 64) / a.block) : -1;
@@ -438,9 +429,6 @@ __global__ __launch_bounds__(WB) void wp_pack_k(WArgs a, i64 nwords, int world, 
     const int lane = lane_id();
     const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
     for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; w0 < nwords; w0 += nwaves * 64) {
-        const u64 gbit = 1ull << ((w0 >> 6) & 63);
-        if (!(a.tgroups[w0 >> 12] & gbit)) continue;  // (wave-uniform)
-        if (lane_id() == 0) atomicAnd(a.tgroups + (w0 >> 12), ~gbit);  // the group is emptied below
         const i64 wi = w0 + lane;
         u64 bits = 0;
         if (wi < nwords) {
@@ -906,7 +894,6 @@ struct WPart {
                                    // used in turn by every solve: each was recomputed per solve)
     DevBuf<int32_t> dist, cand;
     DevBuf<u64> touched, fr, frn, mb, stat;
-    DevBuf<u64> tgroups;  // (world > 1) groups of 64 touched words that hold a bit
     DevBuf<u32> rl_inv;   // (relabeled blocks) old local id -> new local id; empty: input ids
     DevBuf<u64> sb;       // the tail's settled map, world x block bits (engine all-gathers the slices)
     bool sb_on = false;   // sb holds this solve's map (set at the tail switch)
@@ -937,7 +924,6 @@ struct WPart {
         a.dist = dist.p;
         a.cand = cand.p;
         a.touched = touched.p;
-        a.tgroups = tgroups.p;
         a.fr = fr.p;
         a.frn = frn.p;
         a.mb = mb.p;
@@ -1045,8 +1031,6 @@ void wpart_cut(WPart* p, const Graph& g, i64 first, double mean_w) {
         p->cand.alloc((size_t)std::max<i64>(p->n, 1));
         p->touched.alloc((size_t)std::max<i64>((p->n + 63) / 64, 1));
         PJ_HIP(hipMemsetAsync(p->touched.p, 0, p->touched.bytes(), s));
-        p->tgroups.alloc((size_t)std::max<i64>((p->n + 4095) / 4096 / 64 + 1, 1));
-        PJ_HIP(hipMemsetAsync(p->tgroups.p, 0, p->tgroups.bytes(), s));
     }
     PJ_HIP(hipStreamSynchronize(s));
 }
@@ -1416,7 +1400,7 @@ void wpart_device_bytes(const WPart& p, i64* out4) {
     out4[0] = (i64)(p.row.bytes() + p.col.bytes() + p.w.bytes());
     out4[1] = (i64)(p.lsplit.bytes() + p.lsplit_alt.bytes() + p.dist.bytes() + p.fr.bytes() + p.frn.bytes() +
                     p.mb.bytes() + p.lq_v.bytes() + p.lq_b.bytes() + p.lq_e.bytes() + p.stat.bytes());
-    out4[2] = (i64)(p.cand.bytes() + p.touched.bytes() + p.tgroups.bytes() + p.mmap.bytes() + p.fmap16.bytes());
+    out4[2] = (i64)(p.cand.bytes() + p.touched.bytes() + p.mmap.bytes());
     out4[3] = p.exch_bytes;
 }
 
