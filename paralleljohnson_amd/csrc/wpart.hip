@@ -1400,7 +1400,7 @@ void wpart_device_bytes(const WPart& p, i64* out4) {
     out4[0] = (i64)(p.row.bytes() + p.col.bytes() + p.w.bytes());
     out4[1] = (i64)(p.lsplit.bytes() + p.lsplit_alt.bytes() + p.dist.bytes() + p.fr.bytes() + p.frn.bytes() +
                     p.mb.bytes() + p.lq_v.bytes() + p.lq_b.bytes() + p.lq_e.bytes() + p.stat.bytes());
-    out4[2] = (i64)(p.cand.bytes() + p.touched.bytes() + p.mmap.bytes());
+    out4[2] = (i64)(p.cand.bytes() + p.touched.bytes() + p.mmap.bytes() + p.fmap16.bytes());
     out4[3] = p.exch_bytes;
 }
 
