@@ -178,9 +178,6 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
 #endif
 __device__ __forceinline__ bool zbit(const u64* __restrict__ Z, u32 u) { return (Z[u >> 6] >> (u & 63)) & 1ull; }
 
-#ifndef PJ_MS_PIPE
-#define PJ_MS_PIPE 0
-#endif
 #ifndef PJ_MS_GPC
 #define PJ_MS_GPC 8  // level-kernel workgroups per CU (MS1024: 12.8 -> 12.4 ms with MS_U 4, round 3)
 #endif
@@ -423,28 +420,12 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
         Off k = b;
         const Off lim = (e - b > (Off)MS_SERIAL) ? b + (Off)MS_SERIAL : e;
         bool go = hasneed && k < lim;
-        // PJ_MS_PIPE: the next step's in-edge ids are loaded while this step's probes are in
-        // flight (one dependent load fewer per step)
-        u32 un[MS_U];
-        if (PJ_MS_PIPE) {
-#pragma unroll
-            for (int q = 0; q < MS_U; ++q) un[q] = (go && k + (Off)q < lim) ? ccol[k + q] : 0u;
-        }
         while (__ballot(go)) {
             if (go) {
                 // MS_U in-edges per step: their ids, then their masks, as independent loads
                 u32 u[MS_U];
-                const Off kn = (lim - k > (Off)MS_U) ? k + (Off)MS_U : lim;
-                if (PJ_MS_PIPE) {
 #pragma unroll
-                    for (int q = 0; q < MS_U; ++q) {
-                        u[q] = un[q];
-                        un[q] = (kn + (Off)q < lim) ? ccol[kn + q] : 0u;
-                    }
-                } else {
-#pragma unroll
-                    for (int q = 0; q < MS_U; ++q) u[q] = (k + (Off)q < lim) ? ccol[k + q] : 0u;
-                }
+                for (int q = 0; q < MS_U; ++q) u[q] = (k + (Off)q < lim) ? ccol[k + q] : 0u;
                 bool z[MS_U];
 #pragma unroll
                 for (int q = 0; q < MS_U; ++q) z[q] = (k + (Off)q < lim) && (!PJ_MS_FZ || zbit(Z, u[q]));
@@ -458,7 +439,7 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
                 for (int q = 0; q < MS_U; ++q)
 #pragma unroll
                     for (int j = 0; j < W; ++j) acc.w[j] |= f[q].w[j];
-                k = kn;
+                k = (lim - k > (Off)MS_U) ? k + (Off)MS_U : lim;
                 go = mopen<W>(need, acc) && k < lim;
             }
         }
