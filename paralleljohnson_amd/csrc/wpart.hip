@@ -409,7 +409,7 @@ __global__ __launch_bounds__(WB) void wp_count_k(WArgs a, i64 nwords) {
     for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; w0 < nwords; w0 += nwaves * 64) {
         const i64 wi = w0 + lane;
         const u32 cnt = wi < nwords ? (u32)__popcll(a.touched[wi]) : 0u;
-        const int owner = wi < nwords ? (int)((wi * 64) / a.block) : -1;
+        const int owner = wi < nwords ? (int)((u32)wi / (u32)a.bw) : -1;  // (a block is bw words; wi < 2^26)
         u64 pending = __ballot(cnt != 0);
         while (pending) {
             const int l = __ffsll((long long)pending) - 1;
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(WB) void wp_pack_k(WArgs a, i64 nwords, int world, 
             if (bits) a.touched[wi] = 0;
         }
         const u32 cnt = (u32)__popcll(bits);
-        const int owner = wi < nwords ? (int)((wi * 64) / a.block) : -1;
+        const int owner = wi < nwords ? (int)((u32)wi / (u32)a.bw) : -1;  // (a block is bw words; wi < 2^26)
         u64 pending = __ballot(cnt != 0);
         u64 base = 0;
         while (pending) {  // one atomic per (wave, owner)
