@@ -588,6 +588,7 @@ def test_partitioned_bfs_s28_full_size(ctx, pj):
     # rows and vertex state shrink with the world size; the N-bit bitmaps stay
     assert mem[8]["rows"] < mem[2]["rows"] / 3 and mem[8]["state"] < mem[2]["state"] / 3, mem
     assert mem[8]["exchange"] <= mem[2]["exchange"], mem
+    print("per-rank device bytes by world:", mem)  # (shown with pytest -s)
     total = {w: sum(m.values()) for w, m in mem.items()}
     assert total[8] < total[4] < total[2], mem
     g = ctx.generate_kronecker(28, 16, 1)
