@@ -454,7 +454,9 @@ typedef struct pj_part_stats {
 /* The partitioned BFS of this rank (part.hip + the level loop of engine.cpp,
  * the analogue of :488-594): every rank of comm calls it with the same source.
  * pj_part_set_option keys: "alpha", "beta" (Beamer), "direction" (0 auto,
- * 1 push, 2 pull). */
+ * 1 push, 2 pull), "exchange_cap" (ids per rank and direction the exchange buffers
+ * hold; a push level with more goes out in pieces by word range of the owners' slices;
+ * -1 = block / 16 (default), 0 = no cap). Every rank must use the same values. */
 int pj_part_bfs(pj_part* p, pj_comm* comm, int64_t source, pj_part_stats* st);
 int pj_part_set_option(pj_part* p, const char* key, double value);
 /* All ranks of a one-process group at once (one host thread per rank);

@@ -1674,6 +1674,7 @@ int pj_part_set_option(pj_part* p, const char* key, double value) {
     if (k == "alpha" && value > 0) prm.alpha = value;
     else if (k == "beta" && value > 0) prm.beta = value;
     else if (k == "direction" && (value == 0 || value == 1 || value == 2)) prm.force = (int)value;
+    else if (k == "exchange_cap" && value >= -1) prm.xcap = (i64)value;
     else return arg_error("pj_part_set_option: unknown key or bad value");
     return PJ_OK;
 }

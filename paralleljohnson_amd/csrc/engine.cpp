@@ -113,17 +113,43 @@ void bfs_engine(BfsSteps& S, Comm& comm, i64 source, const BfsParams& prm, bool 
                     S.push(level, counts.data());
                     if (exchanges(comm)) comm.alltoall_counts(counts.data(), rcounts.data(), s);
                 }
+                i64 npieces = 1;
                 if (exchanges(comm)) {
                     i64 ns = 0;
                     for (int q = 0; q < S.world; ++q) {
                         ns += q == S.rank ? 0 : counts[(size_t)q];
                         nr += rcounts[(size_t)q];
                     }
-                    S.exchange_buffers(ns, nr);
-                    comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u32), s);
-                    sent += ns;
+                    const i64 cap = S.exchange_cap();
+                    if (cap > 0) {  // the pieces every rank uses: from the largest side of any rank
+                        i64 need = -std::max(ns, nr);  // (max over ranks as a min of negatives)
+                        comm.allreduce(&need, 1, true, s);
+                        need = -need;
+                        npieces = std::min<i64>((need + cap - 1) / cap, std::max<i64>(1, S.bw));
+                    }
+                    if (npieces <= 1) {
+                        S.exchange_buffers(ns, nr);
+                        comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u32), s);
+                        sent += ns;
+                    }
                 }
-                S.apply(level, nr);
+                if (npieces <= 1) {
+                    S.apply(level, nr);
+                } else {
+                    for (int k = 0; k < (int)npieces; ++k) {
+                        S.piece_counts(k, (int)npieces, counts.data());
+                        comm.alltoall_counts(counts.data(), rcounts.data(), s);
+                        i64 ns = 0, nrk = 0;
+                        for (int q = 0; q < S.world; ++q) {
+                            ns += q == S.rank ? 0 : counts[(size_t)q];
+                            nrk += rcounts[(size_t)q];
+                        }
+                        S.exchange_buffers(ns, nrk);
+                        comm.alltoallv(S.send, counts.data(), S.recv, rcounts.data(), sizeof(u32), s);
+                        sent += ns;
+                        S.apply(level, nrk);
+                    }
+                }
                 ++td;
             } else {
                 S.pull(level);

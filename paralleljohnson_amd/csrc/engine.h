@@ -100,6 +100,12 @@ struct BfsSteps {
     // send must then hold the packed ids (nsend of them) and recv room for nrecv. The
     // default (callback steps) keeps the caller's buffers, packed by push itself.
     virtual void exchange_buffers(i64 nsend, i64 nrecv) { (void)nsend, (void)nrecv; }
+    // Pieces (optional): a level whose ids exceed exchange_cap() (per rank and direction; 0 =
+    // no cap) goes out in K pieces by word range of every owner's slice: piece_counts(k, K)
+    // gives the per-owner counts of piece k (its ids stay marked until packed),
+    // exchange_buffers(nsend, nrecv) then packs that piece, and each piece is applied.
+    virtual i64 exchange_cap() { return 0; }
+    virtual void piece_counts(int k, int npieces, i64* counts) { (void)k, (void)npieces, (void)counts; }
 };
 
 // The pj_wpart_* steps; send / recv hold u64 (id | cand << 32): world * block for
@@ -175,6 +181,7 @@ struct DeltaSteps {
 struct BfsParams {
     double alpha = 14.0, beta = 24.0;
     int force = 0;  // 0 auto, 1 push only, 2 pull from level 1 on
+    i64 xcap = -1;  // exchange buffer cap in ids per rank and direction (-1: block / 16; 0: none)
 };
 
 // The rank-local loops. `iso_ready` says the replicated isolated mask in

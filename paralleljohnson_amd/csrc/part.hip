@@ -355,16 +355,17 @@ __global__ void part_counts_k(PartArgs a) {
 // packed = [owner 0 | owner 1 | ...] (owner offsets from stat[8 ..]); a wave takes 64
 // words of one owner's slice, places its ids with one cursor atomic and clears the
 // words. (Order inside an owner's segment is free: the owner settles ids in any order.)
-__global__ __launch_bounds__(TB) void part_pack_k(PartArgs a, u32* __restrict__ packed) {
+// Only the words [wlo, wlo + span) of each owner's slice (a piece of the level, engine.h).
+__global__ __launch_bounds__(TB) void part_pack_k(PartArgs a, u32* __restrict__ packed, i64 wlo, i64 span) {
     const int lane = lane_id();
-    const i64 cpo = (a.bw + 63) / 64;  // chunks per owner slice
+    const i64 cpo = (span + 63) / 64;  // chunks per owner slice
     const i64 nch = cpo * a.world;
     for (i64 c = (i64)blockIdx.x * NW + wave_id(); c < nch; c += (i64)gridDim.x * NW) {
         const int o = (int)(c / cpo);
         if (o == a.rank) continue;  // (wave-uniform)
-        const i64 wi = (c - (i64)o * cpo) * 64 + lane;
+        const i64 wr = (c - (i64)o * cpo) * 64 + lane, wi = wlo + wr;
         u64 bits = 0;
-        if (wi < a.bw) {
+        if (wr < span && wi < a.bw) {
             bits = a.sent[(i64)o * a.bw + wi];
             if (bits) a.sent[(i64)o * a.bw + wi] = 0;
         }
@@ -383,6 +384,32 @@ __global__ __launch_bounds__(TB) void part_pack_k(PartArgs a, u32* __restrict__ 
             const int b = __ffsll((long long)bits) - 1;
             bits &= bits - 1;
             packed[p++] = (u32)(w0 + (u64)b);
+        }
+    }
+}
+
+// Per-owner claim counts of the words [wlo, wlo + span) of every remote slice (a piece):
+// cnt[o] (zeroed by the caller), one atomic per (wave, owner).
+__global__ __launch_bounds__(TB) void part_piece_counts_k(PartArgs a, i64 wlo, i64 span, u64* __restrict__ cnt) {
+    const int lane = lane_id();
+    const i64 tot = (i64)a.world * span;
+    for (i64 b0 = ((i64)blockIdx.x * NW + wave_id()) * 64; b0 < tot; b0 += (i64)gridDim.x * NW * 64) {
+        const i64 i = b0 + lane;
+        int o = -1;
+        u32 c = 0;
+        if (i < tot) {
+            o = (int)(i / span);
+            const i64 wi = wlo + (i - (i64)o * span);
+            if (o != a.rank && wi < a.bw) c = (u32)__popcll(a.sent[(i64)o * a.bw + wi]);
+        }
+        u64 pending = __ballot(c != 0);
+        while (pending) {
+            const int l = __ffsll((long long)pending) - 1;
+            const int oo = __shfl(o, l, 64);
+            const bool mine = c != 0 && o == oo;
+            pending &= ~__ballot(mine);
+            const u32 t = wave_sum(mine ? c : 0u);
+            if (lane == l) atomicAdd(&cnt[oo], (u64)t);
         }
     }
 }
@@ -523,6 +550,7 @@ struct Part {
     ScanWs scan;
     u64 nq = 0, mq = 0;  // push queue of the current frontier (host copy from end_level)
     i64 exch_bytes = 0;  // the engine view's send + recv buffers (sized to the largest level)
+    i64 pw_lo = 0, pw_span = 0;  // the piece the next part_pack packs (span 0: the whole level)
     int32_t level = 0;
     std::unique_ptr<BfsSteps> steps;  // engine view with its own exchange buffers (lazy)
     const Comm* iso_comm = nullptr;   // transport the replicated isolated mask was gathered over
@@ -788,9 +816,35 @@ void part_begin(Part& p, i64 source, const u64* iso, u64* vis, i64* out3) {
 void part_pack(Part& p, u64* vis, u32* packed) {
     if (p.world < 2) return;
     PartArgs a = part_args(p, vis);
-    const i64 nch = (p.bw + 63) / 64 * p.world;
-    part_pack_k<<<grid_for(nch, NW, (unsigned)p.ctx->cu_count * 8), TB, 0, p.ctx->stream>>>(a, packed);
+    const i64 span = p.pw_span > 0 ? p.pw_span : p.bw;
+    const i64 nch = (span + 63) / 64 * p.world;
+    part_pack_k<<<grid_for(nch, NW, (unsigned)p.ctx->cu_count * 8), TB, 0, p.ctx->stream>>>(a, packed, p.pw_lo,
+                                                                                             span);
     PJ_LAUNCH_CHECK();
+    p.pw_lo = 0;  // (the next pack is a whole level unless a piece is counted first)
+    p.pw_span = 0;
+}
+
+// Piece k of npieces of the level's claims (words [k bw / npieces, (k + 1) bw / npieces) of
+// every remote slice): per-owner counts into counts[] and stat[8 ..], pack cursors cleared;
+// the next part_pack packs this piece.
+void part_piece_counts(Part& p, int k, int npieces, i64* counts) {
+    hipStream_t s = p.ctx->stream;
+    const i64 wlo = p.bw * k / npieces, whi = p.bw * (k + 1) / npieces;
+    PJ_HIP(hipMemsetAsync(p.stat.p + 8, 0, sizeof(u64) * (size_t)p.world, s));
+    PJ_HIP(hipMemsetAsync(p.cur.p, 0, p.cur.bytes(), s));
+    if (whi > wlo && p.world > 1) {
+        PartArgs a = part_args(p, nullptr);
+        const i64 tot = (i64)p.world * (whi - wlo);
+        part_piece_counts_k<<<grid_for((tot + 63) / 64, NW, (unsigned)p.ctx->cu_count * 8), TB, 0, s>>>(
+            a, wlo, whi - wlo, p.stat.p + 8);
+        PJ_LAUNCH_CHECK();
+    }
+    PJ_HIP(hipMemcpyAsync(p.hstat.p + 8, p.stat.p + 8, sizeof(u64) * (size_t)p.world, hipMemcpyDeviceToHost, s));
+    PJ_HIP(hipStreamSynchronize(s));
+    for (int o = 0; o < p.world; ++o) counts[o] = (i64)p.hstat.p[8 + o];
+    p.pw_lo = wlo;
+    p.pw_span = whi - wlo;
 }
 
 namespace {
@@ -906,6 +960,8 @@ struct PartGpuSteps final : BfsSteps {
         part_pack(p, vis_b.p, send_b.p);
     }
     void apply(int level, i64 nr) override { part_apply(p, level, vis_b.p, recv_b.p, nr); }
+    i64 exchange_cap() override { return p.prm.xcap < 0 ? std::max<i64>(p.block / 16, 4096) : p.prm.xcap; }
+    void piece_counts(int k, int npieces, i64* counts) override { part_piece_counts(p, k, npieces, counts); }
     void pull(int level) override { part_pull(p, level, vis_b.p); }
     void end_level(i64* st3) override { part_end_level(p, vis_b.p, st3); }
     const i64* counts_dev() override { return reinterpret_cast<const i64*>(p.stat.p + 8); }

@@ -587,7 +587,9 @@ def test_partitioned_bfs_s28_full_size(ctx, pj):
         torch.cuda.empty_cache()
     # rows and vertex state shrink with the world size; the N-bit bitmaps stay
     assert mem[8]["rows"] < mem[2]["rows"] / 3 and mem[8]["state"] < mem[2]["state"] / 3, mem
-    assert mem[8]["exchange"] <= mem[2]["exchange"], mem
+    # the exchange buffers are capped at block / 16 ids per direction (bigger push levels go
+    # out in pieces): O(N / P) like the rest of the rank's state
+    assert mem[8]["exchange"] <= 0.3 * mem[2]["exchange"], mem
     print("per-rank device bytes by world:", mem)  # (shown with pytest -s)
     total = {w: sum(m.values()) for w, m in mem.items()}
     assert total[8] < total[4] < total[2], mem

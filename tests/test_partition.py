@@ -293,11 +293,12 @@ def test_part_kronecker_matches_single_gpu(ctx, pj, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,force", [(2, 0), (2, 1), (2, 2), (3, 0)])
-def test_part_group_one_gpu(pj, oracle, world, force):
+@pytest.mark.parametrize("world,force,cap", [(2, 0, -1), (2, 1, -1), (2, 2, -1), (3, 0, -1), (2, 1, 50), (3, 0, 200)])
+def test_part_group_one_gpu(pj, oracle, world, force, cap):
     """world ranks of one process sharing the one GPU (host transport: device copies between
     the ranks' buffers, one host thread per rank): libpj kernels + the C++ level loop + the
-    exchange end to end, on random graphs and Kronecker s14."""
+    exchange end to end, on random graphs and Kronecker s14; with a small exchange_cap the
+    big push levels go out in pieces (word ranges of the owners' slices)."""
     from paralleljohnson_amd.partition import bfs_group, gather_group, load_coo, load_kronecker
     ctxs, comms = _group(pj, world)
     assert all(c.kind == "host" for c in comms)
@@ -306,6 +307,7 @@ def test_part_group_one_gpu(pj, oracle, world, force):
         parts = [load_coo(ctxs[r], s, d, n, r, world, symmetric=(kind == "sym")) for r in range(world)]
         for p in parts:
             p.set_option("direction", force)
+            p.set_option("exchange_cap", cap)
         row, _, _ = _csr(oracle, s, d, n)
         for source in (0, n // 3, n - 1, n + 5):
             st = bfs_group(parts, comms, source)
@@ -322,9 +324,15 @@ def test_part_group_one_gpu(pj, oracle, world, force):
     k = oracle.kronecker(14, 16, 7)
     krow, kcol, _ = oracle.coo2csr(k[0], k[1], 1 << 14)
     parts = [load_kronecker(ctxs[r], 14, 16, 7, r, world) for r in range(world)]
+    for p in parts:
+        p.set_option("direction", force)
+        p.set_option("exchange_cap", cap)
     for source in (1, 777, 12345):
         bfs_group(parts, comms, source)
         assert np.array_equal(gather_group(parts, comms), oracle.bfs(krow, kcol, source)), source
+    if cap > 0:  # the buffers stay near the cap (pieces are word ranges: up to ~2x on skew)
+        for p in parts:
+            assert p.device_bytes()["exchange"] <= 2 * 4 * 1.25 * 3 * cap + 64, p.device_bytes()
     for p in parts:
         p.close()
 
