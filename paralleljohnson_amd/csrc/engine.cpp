@@ -125,7 +125,9 @@ void bfs_engine(BfsSteps& S, Comm& comm, i64 source, const BfsParams& prm, bool 
                         i64 need = -std::max(ns, nr);  // (max over ranks as a min of negatives)
                         comm.allreduce(&need, 1, true, s);
                         need = -need;
-                        npieces = std::min<i64>((need + cap - 1) / cap, std::max<i64>(1, S.bw));
+                        // pieces of about cap / 2 (a piece of a skewed level may exceed its share)
+                        const i64 half = std::max<i64>(1, cap / 2);
+                        if (need > cap) npieces = std::min<i64>((need + half - 1) / half, std::max<i64>(1, S.bw));
                     }
                     if (npieces <= 1) {
                         S.exchange_buffers(ns, nr);

@@ -947,13 +947,21 @@ struct PartGpuSteps final : BfsSteps {
     void zmask() override { part_zmask(p, zown_b.p); }
     void begin(i64 source, i64* st3) override { part_begin(p, source, iso_b.p, vis_b.p, st3); }
     void push(int level, i64* counts) override { part_push(p, level, vis_b.p, nullptr, counts); }
+    // growth: x1.25 of the need, but never past the cap unless the need itself is; a piece
+    // (pw_span > 0) takes the cap whole, so every later piece and level fits
+    size_t grow_to(i64 need) {
+        const i64 cap = exchange_cap();
+        i64 t = need + need / 4;
+        if (cap > 0) t = std::max(need, p.pw_span > 0 ? cap : std::min(t, cap));
+        return (size_t)t;
+    }
     void exchange_buffers(i64 nsend, i64 nrecv) override {
         if ((size_t)nsend > send_b.n) {
-            send_b.ensure((size_t)nsend + (size_t)nsend / 4);
+            send_b.ensure(grow_to(nsend));
             send = send_b.p;
         }
         if ((size_t)nrecv > recv_b.n) {
-            recv_b.ensure((size_t)nrecv + (size_t)nrecv / 4);
+            recv_b.ensure(grow_to(nrecv));
             recv = recv_b.p;
         }
         p.exch_bytes = (i64)(send_b.bytes() + recv_b.bytes());
