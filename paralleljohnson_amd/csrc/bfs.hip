@@ -34,8 +34,6 @@
 //   * new frontier entries are staged in LDS and published with one atomic per
 //     block step (per segment), not one per wave.
 #include <chrono>
-#include <cstring>
-#include <vector>
 
 #include "lb.h"
 
@@ -1350,15 +1348,7 @@ struct BfsWorkHolder {
     DevBuf<uint8_t> ctl;  // C[3] + S[2] + nmode[2]
     int64_t* host = nullptr;  // mapped pinned host words (see BfsArgs::host)
     int32_t last_launches = 0;  // level launches the previous solve used: sizes the first batch
-    // (bfs_graph option) the first batch's level launches as one HIP graph, rebuilt when its
-    // launch count, grid or kernel arguments change
-    hipGraphExec_t gexec = nullptr;
-    int g_launches = 0;
-    unsigned g_grid = 0;
-    bool g_sym = false;
-    std::vector<uint8_t> g_key;
     ~BfsWorkHolder() {
-        if (gexec) (void)hipGraphExecDestroy(gexec);
         if (host) (void)hipHostFree(host);
     }
 };
@@ -1460,36 +1450,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
         // of idle ~7 us launches inside the timed region: K22, 14 behind an 8-level solve)
         int next = 2;
         for (;;) {
-            bool graphed = false;
-            if (g.bfs_graph && li == 0 && batch > 0) {
-                // the first batch as one graph launch (its kernels depend only on the state the
-                // init kernel wrote, not on the source): captured once per configuration
-                std::vector<uint8_t> key(sizeof(a) + sizeof(gd));
-                std::memcpy(key.data(), &a, sizeof(a));
-                std::memcpy(key.data() + sizeof(a), &gd, sizeof(gd));
-                if (!w.gexec || w.g_launches != batch || w.g_grid != grid || w.g_sym != g.symmetric || w.g_key != key) {
-                    if (w.gexec) PJ_HIP(hipGraphExecDestroy(w.gexec));
-                    w.gexec = nullptr;
-                    hipGraph_t graph = nullptr;
-                    PJ_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-                    for (int i = 0; i < batch; ++i) {
-                        if (g.symmetric) bfs_level_k<Off, true><<<grid, TB, 0, s>>>(a, gd, i);
-                        else bfs_level_k<Off, false><<<grid, TB, 0, s>>>(a, gd, i);
-                    }
-                    PJ_HIP(hipStreamEndCapture(s, &graph));
-                    const hipError_t e = hipGraphInstantiate(&w.gexec, graph, nullptr, nullptr, 0);
-                    (void)hipGraphDestroy(graph);
-                    PJ_HIP(e);
-                    w.g_launches = batch;
-                    w.g_grid = grid;
-                    w.g_sym = g.symmetric;
-                    w.g_key = key;
-                }
-                PJ_HIP(hipGraphLaunch(w.gexec, s));
-                li += batch;
-                graphed = true;
-            }
-            for (int i = 0; !graphed && i < batch && li < INT_INF; ++i, ++li) {
+            for (int i = 0; i < batch && li < INT_INF; ++i, ++li) {
                 if (g.symmetric) bfs_level_k<Off, true><<<grid, TB, 0, s>>>(a, gd, li);
                 else bfs_level_k<Off, false><<<grid, TB, 0, s>>>(a, gd, li);
                 PJ_LAUNCH_CHECK();
