@@ -88,7 +88,7 @@ __device__ __forceinline__ void ms_uf_add(MsCtl* c, int slot, const u64 (&m)[W],
     __syncthreads();
     if (threadIdx.x < (unsigned)W) {
         u64 o = 0;
-        for (int w = 0; w < 256 / WAVE; ++w) o |= red[w][threadIdx.x];
+        for (int w = 0; w < MB / WAVE; ++w) o |= red[w][threadIdx.x];
         if (o) atomicOr(&c->uf[slot][blockIdx.x % MS_NSH][threadIdx.x], o);
     }
 }
