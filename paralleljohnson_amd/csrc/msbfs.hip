@@ -141,28 +141,6 @@ __device__ __forceinline__ Mask<W> mload(const u64* __restrict__ p, i64 v) {
     }
     return m;
 }
-// PJ_MS_NW 1: the pull loads only the 16-byte pairs of a mask row that hold sources v still
-// needs and has not yet found (per lane in the serial steps, wave-uniform in the wave loop)
-#ifndef PJ_MS_NW
-#define PJ_MS_NW 0
-#endif
-template <int W>
-__device__ __forceinline__ Mask<W> mload_need(const u64* __restrict__ p, i64 v, const Mask<W>& need) {
-    if constexpr (W >= 4 && PJ_MS_NW) {
-        Mask<W> m;
-        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p + v * W);
-#pragma unroll
-        for (int k = 0; k < W / 2; ++k) {
-            ulonglong2 x{0ull, 0ull};
-            if (need.w[2 * k] | need.w[2 * k + 1]) x = q[k];
-            m.w[2 * k] = x.x;
-            m.w[2 * k + 1] = x.y;
-        }
-        return m;
-    } else {
-        return mload<W>(p, v);
-    }
-}
 template <int W>
 __device__ __forceinline__ void mstore(u64* __restrict__ p, i64 v, const Mask<W>& m) {
 #pragma unroll
@@ -451,12 +429,10 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
                 bool z[MS_U];
 #pragma unroll
                 for (int q = 0; q < MS_U; ++q) z[q] = (k + (Off)q < lim) && (!PJ_MS_FZ || zbit(Z, u[q]));
-                Mask<W> f[MS_U], rem;
-#pragma unroll
-                for (int j = 0; j < W; ++j) rem.w[j] = need.w[j] & ~acc.w[j];
+                Mask<W> f[MS_U];
 #pragma unroll
                 for (int q = 0; q < MS_U; ++q) {
-                    if (z[q]) f[q] = mload_need<W>(F, u[q], rem);
+                    if (z[q]) f[q] = mload<W>(F, u[q]);
                     else f[q] = Mask<W>{};
                 }
 #pragma unroll
@@ -483,11 +459,9 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
                 const Off k0 = kk + lane, k1 = kk + WAVE + lane;
                 const u32 u0 = k0 < ke ? ccol[k0] : 0u, u1 = k1 < ke ? ccol[k1] : 0u;
                 const bool z0 = k0 < ke && (!PJ_MS_FZ || zbit(Z, u0)), z1 = k1 < ke && (!PJ_MS_FZ || zbit(Z, u1));
-                Mask<W> x{}, y{}, rem;
-#pragma unroll
-                for (int j = 0; j < W; ++j) rem.w[j] = want.w[j] & ~got.w[j];
-                if (z0) x = mload_need<W>(F, u0, rem);
-                if (z1) y = mload_need<W>(F, u1, rem);
+                Mask<W> x{}, y{};
+                if (z0) x = mload<W>(F, u0);
+                if (z1) y = mload<W>(F, u1);
 #pragma unroll
                 for (int j = 0; j < W; ++j) got.w[j] |= wave_or(x.w[j] | y.w[j]);
             }
