@@ -381,6 +381,46 @@ def run_wpartitioned_host(args, world_h=2, nroots=3, scale=26):
             c.close()
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: N rank processes of this script under torch's
+    launcher on 127.0.0.1 (one per GPU, LOCAL_RANK = its GPU), started as a child process from
+    a parent that never touches the GPU; rank 0's line goes straight to stdout. Returns the
+    launcher's exit status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def launch_check(rank, world, backend):
+    """--launch-check: the rank bookkeeping of a run without the GPU legs -- the process group,
+    the timed-region barriers and the max-over-ranks / sum-over-ranks reductions the line
+    uses -- so that the N-rank launch is testable on the CPU (gloo)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(backend="gloo" if backend != "nccl" else backend)
+    el, m = 0.5 + rank, float(10 * (rank + 1))  # per-rank stand-ins for (elapsed, units processed)
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([el, m], dtype=torch.float64)
+        tm = t[:1].clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        el, m = float(tm[0]), float(t[1])
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "elapsed_max": el, "units_sum": m}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -402,16 +442,30 @@ def main():
     ap.add_argument("--no-part-host", action="store_true", help="skip the world-2 host-transport partitioned leg")
     ap.add_argument("--no-tts", action="store_true", help="skip the time-to-solution process (tuning runs)")
     ap.add_argument("--opt", action="append", default=[], help="libpj graph option key=value (tuning)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test only: start the ranks, rendezvous, barrier and the max/sum reductions of the line, "
+                         "no GPU work (the CPU test of the --gpus launch path)")
     args = ap.parse_args()
 
+    # --gpus N means N ranks, one process per GPU (the reference's `mpirun -np P`, README:9).
+    # Without a launcher (no WORLD_SIZE) this process starts them itself, before anything here
+    # touches torch or the GPU, and only relays rank 0's line and the exit status.
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-
-    import torch
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s); refusing to report a "
+              f"{world}-rank run as {args.gpus} GPU(s)", file=sys.stderr)
+        sys.exit(2)
     # one rank per GPU; PJ_BENCH_BACKEND=gloo rehearses the N>1 bookkeeping with several
     # ranks sharing fewer GPUs (the driver's runs use RCCL, one GPU per rank)
     backend = os.environ.get("PJ_BENCH_BACKEND", "nccl")
+    if args.launch_check:
+        return launch_check(rank, world, backend)
+
+    import torch
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None

@@ -91,10 +91,29 @@ __device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
     return s.e64[k];
 }
 
+// PJ_V2_NOFIN (1: light pulls, 2: light and heavy pulls): a pull takes its candidate from
+// every in-neighbour u with dist[u] < hi, one dist probe, instead of first testing u's bit
+// in the round's frontier (light) or the band's members (heavy) and reading dist[u] only for
+// a set bit. Exact: every u with dist[u] < hi outside that set has already relaxed its
+// edges of this kind at its current distance (a lowered vertex re-enters the frontier), so
+// dist[u] + w >= dist[v] and it never lowers v's running best.
+#ifndef PJ_V2_NOFIN
+#define PJ_V2_NOFIN 0
+#endif
+// the candidate distance u offers through a pulled edge (INT_INF = none): bits == null
+// probes dist[u] alone (PJ_V2_NOFIN), else u's bit first
+__device__ __forceinline__ int32_t pull_src(const u64* __restrict__ bits, const int32_t* __restrict__ dist, u32 u,
+                                            int32_t hi) {
+    if (!bits) {
+        const int32_t d = dist[u];
+        return d < hi ? d : INT_INF;
+    }
+    return ((bits[u >> 6] >> (u & 63)) & 1ull) ? dist[u] : INT_INF;
+}
 template <typename Off, typename E>
 __device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __restrict__ dist,
                                                  const u64* __restrict__ fin, Off& k, Off lim, int32_t lo,
-                                                 int32_t& cur) {
+                                                 int32_t hi, int32_t& cur) {
     u32 w[PU], u[PU];
     bool ok[PU];
 #pragma unroll
@@ -112,12 +131,19 @@ __device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __re
         ok[j] = ok[j] && !stop;
         nv += ok[j];
     }
-    u64 fw[PU];
-#pragma unroll
-    for (int j = 0; j < PU; ++j) fw[j] = ok[j] ? fin[u[j] >> 6] : 0ull;
     int32_t du[PU];
+    if (!fin) {
 #pragma unroll
-    for (int j = 0; j < PU; ++j) du[j] = (ok[j] && ((fw[j] >> (u[j] & 63)) & 1ull)) ? dist[u[j]] : INT_INF;
+        for (int j = 0; j < PU; ++j) du[j] = ok[j] ? dist[u[j]] : INT_INF;
+#pragma unroll
+        for (int j = 0; j < PU; ++j) du[j] = du[j] < hi ? du[j] : INT_INF;
+    } else {
+        u64 fw[PU];
+#pragma unroll
+        for (int j = 0; j < PU; ++j) fw[j] = ok[j] ? fin[u[j] >> 6] : 0ull;
+#pragma unroll
+        for (int j = 0; j < PU; ++j) du[j] = (ok[j] && ((fw[j] >> (u[j] & 63)) & 1ull)) ? dist[u[j]] : INT_INF;
+    }
 #pragma unroll
     for (int j = 0; j < PU; ++j)
         if (du[j] < INT_INF) {
@@ -877,6 +903,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
     __shared__ u64 red[NWV];
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
+    const u64* hmb = PJ_V2_NOFIN >= 2 ? nullptr : a.mb;
     u32* newb = s_new[wave_id()];
     u32 ccount = 0;
     u64 fe = 0;
@@ -949,7 +976,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                 if (go) {
                     // band members are exactly mb's bits: probe the (cache-resident)
                     // bitmap first, read dist only for members
-                    if (pull_step_fin_cw<Off>(v2_cw_src(a), a.dist, a.mb, k, lim, lo, cur)) {
+                    if (pull_step_fin_cw<Off>(v2_cw_src(a), a.dist, hmb, k, lim, lo, hi, cur)) {
                         done = true;
                         go = false;
                     } else {
@@ -988,9 +1015,9 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
                     int32_t cand = INT_INF;
                     if (!stop) {
-                        const u32 u = (u32)x;
-                        if ((a.mb[u >> 6] >> (u & 63)) & 1ull) {
-                            const long long nd = (long long)a.dist[u] + w;
+                        const int32_t du = pull_src(hmb, a.dist, (u32)x, hi);
+                        if (du < INT_INF) {
+                            const long long nd = (long long)du + w;
                             cand = nd < INT_INF ? (int32_t)nd : INT_INF;
                         }
                     }
@@ -1039,6 +1066,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
     constexpr int NWV = DB / WAVE;
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
+    const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
     const i64 nsc = (a.nwords + PSC - 1) / PSC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
         const i64 gbase = sc * PSC;
@@ -1111,7 +1139,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             bool go = act && k < lim, done = !act || k >= e;
             while (__ballot(go)) {
                 if (go) {
-                    if (pull_step_fin_cw<Off>(v2_light_src(a), a.dist, fin, k, lim, lo, cur)) {
+                    if (pull_step_fin_cw<Off>(v2_light_src(a), a.dist, lfin, k, lim, lo, hi, cur)) {
                         done = true;
                         go = false;
                     } else {
@@ -1134,9 +1162,9 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
                     int32_t cand = INT_INF;
                     if (!stop) {
-                        const u32 u = (u32)x;
-                        if ((fin[u >> 6] >> (u & 63)) & 1ull) {
-                            const long long nd = (long long)a.dist[u] + w;
+                        const int32_t du = pull_src(lfin, a.dist, (u32)x, hi);
+                        if (du < INT_INF) {
+                            const long long nd = (long long)du + w;
                             cand = nd < INT_INF ? (int32_t)nd : INT_INF;
                         }
                     }
@@ -1180,6 +1208,7 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
                                                   u32& newc, u64& fe) {
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
+    const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
     for (u64 it = (u64)blockIdx.x * (DB / WAVE) + wave_id(); it < nlc; it += (u64)gridDim.x * (DB / WAVE)) {
         const u32 v = lcv[it];
         const int32_t d0 = dist_now(a.dist + v);
@@ -1198,9 +1227,9 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
             const bool stop = !valid || (long long)lo + w >= (long long)cur;
             int32_t cand = INT_INF;
             if (!stop) {
-                const u32 u = (u32)x;
-                if ((fin[u >> 6] >> (u & 63)) & 1ull) {
-                    const long long nd = (long long)a.dist[u] + w;
+                const int32_t du = pull_src(lfin, a.dist, (u32)x, hi);
+                if (du < INT_INF) {
+                    const long long nd = (long long)du + w;
                     cand = nd < INT_INF ? (int32_t)nd : INT_INF;
                 }
             }

@@ -1,0 +1,52 @@
+"""bench.py's rank launch (`--gpus N` = N rank processes, the reference's `mpirun -np P`,
+README:9), on the CPU: `--launch-check` runs the process group, barrier and max/sum
+reductions of the bench line over gloo without any GPU leg."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                              "MASTER_PORT")}
+    env["PJ_BENCH_BACKEND"] = "gloo"
+    env["MASTER_ADDR"] = "127.0.0.1"
+    return env
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_gpus_flag_starts_that_many_ranks():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"], capture_output=True, text=True,
+                       timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 alone prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert d["elapsed_max"] == 1.5  # max over ranks of 0.5 + rank
+    assert d["units_sum"] == 30.0   # sum over ranks of 10 * (rank + 1)
+
+
+def test_gpus_one_runs_in_process():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--launch-check"], capture_output=True, text=True,
+                       timeout=120, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+
+
+def test_gpus_mismatching_the_launcher_fails():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", BENCH, "--gpus", "3", "--launch-check"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode != 0
+    assert "--gpus 3 but the launcher started 2" in r.stderr
