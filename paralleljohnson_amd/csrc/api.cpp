@@ -891,7 +891,6 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "grid_per_cu" && value >= 0 && value <= 16) g.grid_per_cu = (int)value;
     else if (k == "max_levels" && value >= 0) g.max_levels = (int)value;
     else if (k == "bfs_small" && (value == 0 || value == 1)) g.bfs_small = (int)value;
-    else if (k == "bfs_mid" && (value == 0 || value == 1)) g.bfs_mid = (int)value;
     else if (k == "bfs_spare" && value >= 0 && value <= 16) g.bfs_spare = (int)value;
     else if (k == "ms_width" && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16))
         g.ms_width = (int)value;

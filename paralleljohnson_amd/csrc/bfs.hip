@@ -70,41 +70,12 @@ constexpr int RPI = PJ_RPI;   // pull levels: rounds of 64 candidates in flight 
 constexpr u32 SMALL_N = TB;   // one-workgroup levels: frontier vertices (one per thread)
 constexpr u32 SEPT = 8;       // one-workgroup levels: frontier edges per thread
 constexpr u32 SMALL_M = SEPT * TB;
-// mid-size push levels on MID_NB workgroups (mid_levels): blocks 0, 8, 16, ... of the launch,
-// one XCD under the observed round-robin placement (speed only: the protocol is placement-free)
-#ifndef PJ_MID_NB
-#define PJ_MID_NB 32
-#endif
-#ifndef PJ_MID_N
-#define PJ_MID_N 32768
-#endif
-#ifndef PJ_MID_M
-#define PJ_MID_M 262144
-#endif
-constexpr u32 MID_NB = PJ_MID_NB;
-constexpr u64 MID_N = PJ_MID_N;    // most frontier vertices of a mid level
-constexpr u64 MID_M = PJ_MID_M;    // most frontier edges of a mid level
-constexpr int MID_TILE = 1024;     // edges per workgroup step
-constexpr int MID_EB = 40;         // packed frontier counter: (entries << MID_EB) | edges
-
 struct alignas(64) Line {
     u64 v;
     u64 pad[7];
 };
 
-struct alignas(64) MidLvl {  // one level of a mid loop (ring of 3)
-    u64 packed;  // the frontier it holds: (entries << MID_EB) | their out-edges
-    u64 found;   // vertices the level before it claimed
-    u64 in;      // their in-degree sum
-    u64 pad[5];
-};
-struct MidCtl {
-    Line bar;      // barrier arrivals of the launch's mid loop (monotonic)
-    MidLvl lv[3];
-};
-
 struct LevelCnt {
-    MidCtl mid;        // the mid loop of the launch that accumulates into this slot
     Line n_norm[NQS];  // normal-queue entries appended, per segment
     Line hub_packed;   // (hub count << eb) | hub edges
     u64 m_next[NSH];   // out-degree sum of the new frontier (edges of the next push level)
@@ -129,7 +100,6 @@ struct BfsArgs {
     double alpha, beta;
     int force;  // 0 auto, 1 push only, 2 pull whenever possible
     int small;  // one-workgroup levels for small push frontiers
-    int mid;    // MID_NB-workgroup levels for mid-size push frontiers
     int32_t max_levels;  // debug: stop after this many levels
     int32_t* dist;
     u64* vis[2];
@@ -141,12 +111,7 @@ struct BfsArgs {
     LevelCnt* C;    // [3]
     LevelState* S;  // [2]
     u64* nmode;     // [2] push / pull levels run (device)
-    int64_t* host;  // mapped host words: [0] levels run (-1 while running), [1] push, [2] pull, [3] launches,
-                    // [4] a mid loop's barrier timed out (nonzero: the solve is void)
-    u32* mv[2];     // mid loops: frontier vertex, out-degree, row begin, edge offset (capacity n each)
-    u32* mdeg[2];
-    u64* mbeg[2];
-    u64* moff[2];
+    int64_t* host;  // mapped host words: [0] levels run (-1 while running), [1] push, [2] pull, [3] launches
     u64* stamps;    // PJ_BFS_STAMPS builds: [launch * 64 + slot] 100 MHz timestamps of block 0
 };
 
@@ -620,268 +585,11 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
 }
 
 
-// ---- mid_levels: mid-size push levels on MID_NB workgroups -----------------------
-// The BFS of a web graph spends most of its launches on push levels of a few thousand
-// vertices: every one a grid launch whose blocks re-derive the decision from counters
-// another XCD wrote (2-2.8 us), then ~7 dependent global round trips in block 0, then a
-// kernel boundary (4-6 us) -- profiles/r03/wg_level_stamps.txt. Here MID_NB workgroups
-// (blocks 0, 8, 16, ...: one XCD under round-robin placement) run such levels in one
-// launch: the frontier is a list (vertex, degree, row begin, edge offset) whose offsets
-// come from ONE packed atomic per wave, edges are relaxed in 1024-edge tiles (slot found
-// in LDS, lb.h), claims are device-scope atomicOr on the visited bitmap, and the level
-// ends at a counter barrier (release fence -> arrive -> poll -> acquire fence; MI355X
-// guide, workgroup dispatch). Every block then takes the same decision from the same
-// counters: continue while the next level is push (Beamer) and mid-size, else hand the
-// frontier to the grid (queues, counters and state exactly as a grid level leaves them,
-// as small_levels does) or end the BFS. Non-participating blocks exit at once, so the
-// participants (at most 2 per CU of their XCD) are always co-resident.
-__device__ __forceinline__ bool mid_bar(u64* bar, u64 target, int64_t* err) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    __shared__ int ok_s;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int ok = 1;
-        for (u64 spin = 0; __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
-            __builtin_amdgcn_s_sleep(2);
-            if (spin > (1ull << 26)) {  // (never expected: the participants are co-resident)
-                __hip_atomic_store(err, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                ok = 0;
-                break;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        ok_s = ok;
-    }
-    __syncthreads();
-    return ok_s != 0;
-}
-
-// append the lanes with app = true to the mid frontier list of parity par (ring slot lv)
-__device__ __forceinline__ void mid_append(const BfsArgs& a, MidLvl* lv, int par, bool app, u32 v, u32 deg, u64 beg) {
-    const u64 m = __ballot(app);
-    if (!m) return;
-    const u64 d = app ? (u64)deg : 0ull;
-    const u64 inc = wave_incl_scan(d);
-    const u64 tot = __shfl(inc, 63, 64);
-    const int leader = __ffsll((long long)m) - 1;
-    u64 old = 0;
-    if (lane_id() == leader)
-        old = __hip_atomic_fetch_add(&lv->packed, ((u64)__popcll(m) << MID_EB) + tot, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-    old = __shfl(old, leader, 64);
-    if (app) {
-        const u64 slot = (old >> MID_EB) + (u64)__popcll(m & lanemask_lt());
-        a.mv[par][slot] = v;
-        a.mdeg[par][slot] = deg;
-        a.mbeg[par][slot] = beg;
-        a.moff[par][slot] = (old & ((1ull << MID_EB) - 1ull)) + inc - d;
-    }
-}
-
-struct MidShared {
-    LbShared<MID_TILE> sh;
-};
-
-template <typename Off, bool SYM>
-__device__ void mid_levels(const BfsArgs& a, const Graph_d<Off>& g, const Decision& d, int32_t li, MidShared& ms,
-                           u64* red) {
-    const u32 t = threadIdx.x;
-    const u32 nb = min(MID_NB, (u32)gridDim.x / 8u);
-    const u32 p = blockIdx.x / 8u;  // participant index
-    MidCtl* mc = &a.C[li % 3].mid;
-    int64_t* err = a.host + 4;
-    u64 bars = 0;
-    // phase 0: level d.L's frontier from the queues (normal segments, hub queue) into list 0
-    {
-        u64 nn = 0;
-#pragma unroll
-        for (int k = 0; k < NQS; ++k) nn += d.nseg[k];
-        const u64 F = nn + d.nh;
-        const int cp = d.L & 1;
-        for (u64 i0 = (u64)p * TB; i0 < F; i0 += (u64)nb * TB) {
-            const u64 i = i0 + t;
-            bool ok = i < F;
-            u32 v = 0;
-            if (ok) {
-                if (i < nn) {
-                    u64 r = 0, pre = 0;
-                    int k = 0;
-#pragma unroll
-                    for (int j = 0; j < NQS; ++j) {
-                        if (i >= pre && i < pre + d.nseg[j]) {
-                            k = j;
-                            r = i - pre;
-                        }
-                        pre += d.nseg[j];
-                    }
-                    v = a.qv[cp][(u64)k * (u64)a.n + r];
-                } else {
-                    v = a.hv[cp][i - nn];
-                }
-            }
-            Off b = 0, e = 0;
-            if (ok) {
-                b = g.row[v];
-                e = g.row[v + 1];
-            }
-            mid_append(a, &mc->lv[0], 0, ok && e > b, v, (u32)(e - b), (u64)b);
-        }
-        bars += nb;
-        if (!mid_bar(&mc->bar.v, bars, err)) return;
-    }
-    u64* vis = a.vis[d.vsel];
-    int32_t L = d.L;
-    double m_u = d.m_u;
-    u64 fprev = d.found, nlev = 0;
-    for (int k = 0;; ++k) {
-        const int cur = k % 3, nxt = (k + 1) % 3, par = k & 1;
-        if (p == 0 && t == 0) {  // the slot level k + 1 will fill (read last before level k - 1's barrier)
-            MidLvl* z = &mc->lv[(k + 2) % 3];
-            __hip_atomic_store(&z->packed, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&z->found, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&z->in, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const u64 pk = mc->lv[cur].packed;
-        const u64 F = pk >> MID_EB, E = pk & ((1ull << MID_EB) - 1ull);
-        const int32_t nl = L + 1;
-        u64 f = 0, in = 0;
-        for (u64 e0 = (u64)p * MID_TILE; e0 < E; e0 += (u64)nb * MID_TILE) {
-            u64 s0;
-            u32 ns;
-            lb_tile_load<MID_TILE>(a.moff[par], F, e0, ms.sh, s0, ns);
-            u32 vv[MID_TILE / TB];
-            bool ok[MID_TILE / TB], c[MID_TILE / TB];
-#pragma unroll
-            for (int j = 0; j < MID_TILE / TB; ++j) {
-                const u64 e = e0 + (u64)j * TB + t;
-                ok[j] = e < E;
-                vv[j] = 0;
-                if (ok[j]) {
-                    const u32 sl = lb_find<MID_TILE>(ms.sh, ns, e);
-                    vv[j] = g.col[a.mbeg[par][s0 + sl] + (e - ms.sh.off[sl])];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < MID_TILE / TB; ++j) {
-                c[j] = false;
-                if (ok[j]) {
-                    const u64 bit = 1ull << (vv[j] & 63);
-                    c[j] = !(atomicOr(vis + (vv[j] >> 6), bit) & bit);
-                }
-            }
-            Off rb[MID_TILE / TB], re[MID_TILE / TB];
-            u64 ind[MID_TILE / TB];
-#pragma unroll
-            for (int j = 0; j < MID_TILE / TB; ++j) {  // issued beside the claims, used by the winners
-                rb[j] = re[j] = 0;
-                ind[j] = 0;
-                if (ok[j]) {
-                    rb[j] = g.row[vv[j]];
-                    re[j] = g.row[vv[j] + 1];
-                    if (!SYM) ind[j] = (u64)(g.crow[vv[j] + 1] - g.crow[vv[j]]);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < MID_TILE / TB; ++j) {
-                const u32 dg = c[j] ? (u32)(re[j] - rb[j]) : 0u;
-                if (c[j]) {
-                    a.dist[vv[j]] = nl;
-                    f += 1;
-                    in += SYM ? (u64)dg : ind[j];
-                }
-                mid_append(a, &mc->lv[nxt], par ^ 1, c[j] && dg > 0, vv[j], dg, (u64)rb[j]);
-            }
-            __syncthreads();  // (ms.sh is reloaded by the next tile)
-        }
-        f = block_sum<NW>(f, red);
-        in = block_sum<NW>(in, red);
-        if (t == 0) {
-            if (f) __hip_atomic_fetch_add(&mc->lv[nxt].found, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (in) __hip_atomic_fetch_add(&mc->lv[nxt].in, in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        ++nlev;
-        bars += nb;
-        if (!mid_bar(&mc->bar.v, bars, err)) return;
-        // decide() for level L + 1, from what level L found (identical in every block)
-        const u64 pk2 = mc->lv[nxt].packed;
-        const u64 fz = pk2 >> MID_EB, mq = pk2 & ((1ull << MID_EB) - 1ull);
-        const u64 fl = mc->lv[nxt].found, inl = mc->lv[nxt].in;
-        const int32_t L2 = L + 1;
-        const double m_u2 = m_u - (double)inl;
-        const bool end = fz == 0 || L2 + 1 >= INT_INF || L2 >= a.max_levels;
-        if (end) {
-            if (p == 0 && t == 0) {  // what the grid kernel publishes when decide() ends the BFS at L2
-                a.nmode[0] += nlev;
-                LevelState& st = a.S[li & 1];
-                st.mode = 0;
-                st.done = 1;
-                st.vsel = d.vsel;
-                st.level = L2;
-                st.m_u = m_u2;
-                st.prev_found = fl;
-                a.host[1] = (int64_t)a.nmode[0];
-                a.host[2] = (int64_t)a.nmode[1];
-                a.host[3] = (int64_t)li + 1;
-                __atomic_store_n(&a.host[0], (int64_t)L2, __ATOMIC_RELEASE);
-            }
-            return;
-        }
-        bool pull = a.force == 2 ? true : (a.force == 1 ? false : (double)mq > m_u2 / a.alpha);
-        if (pull && a.small && a.force == 0 && fz <= SMALL_N && mq <= SMALL_M) pull = false;
-        if (!pull && fz <= MID_N && mq <= MID_M) {
-            L = L2;
-            m_u = m_u2;
-            fprev = fl;
-            continue;
-        }
-        // hand level L2 to the grid: list (parity par ^ 1) -> normal segment 0 and the hub
-        // queue of parity L2 & 1; level L's counters into C[li % 3], its state into S[li % 2]
-        const int np = L2 & 1, lp = par ^ 1;
-        LevelCnt* cacc = a.C + li % 3;
-        for (u64 i0 = (u64)p * TB; i0 < fz; i0 += (u64)nb * TB) {
-            const u64 i = i0 + t;
-            const bool ok = i < fz;
-            const u32 v = ok ? a.mv[lp][i] : 0u;
-            const u32 dg = ok ? a.mdeg[lp][i] : 0u;
-            const bool isn = ok && dg <= HUBT, ish = ok && dg > HUBT;
-            const u64 m = __ballot(isn);
-            if (m) {
-                const int leader = __ffsll((long long)m) - 1;
-                u64 pos = 0;
-                if (lane_id() == leader) pos = atomicAdd(&cacc->n_norm[0].v, (u64)__popcll(m));
-                pos = __shfl(pos, leader, 64) + (u64)__popcll(m & lanemask_lt());
-                if (isn) a.qv[np][pos] = v;
-            }
-            hub_direct(a, cacc, L, ish, v, dg, ok ? a.mbeg[lp][i] : 0ull);
-        }
-        if (p == 0 && t == 0) {
-            a.nmode[0] += nlev;
-            cacc->m_next[0] = mq;
-            cacc->found[0] = fl;
-            cacc->in_next[0] = inl;
-            cacc->fnz[0] = fz;
-            LevelState& st = a.S[li & 1];
-            st.mode = 0;
-            st.done = 0;
-            st.vsel = d.vsel;
-            st.level = L;
-            st.m_u = m_u;
-            st.prev_found = fprev;
-        }
-        return;
-    }
-}
-
 template <typename Off, bool SYM>
 __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int32_t li) {
     __shared__ union {
         LevelShared lv;
         SmallShared sm;
-        MidShared md;
     } U;
     __shared__ u64 red[NW];
     Decision d;
@@ -897,12 +605,10 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
     // every block reaches the same verdict: the inputs are not written by this launch
     const bool queued = d.prev_mode == 0;  // the frontier is in the queues (else in fnew)
     const bool small = go && a.small && d.mode == 0 && queued && nfr <= SMALL_N && d.mq <= SMALL_M;
-    const bool mid = go && !small && a.mid && d.mode == 0 && queued && nfr <= MID_N && d.mq <= MID_M &&
-                     gridDim.x >= 16;
     if (blockIdx.x == 0) {
         u64* zp = reinterpret_cast<u64*>(a.C + (li + 1) % 3);
         for (u32 i = t; i < sizeof(LevelCnt) / 8; i += TB) zp[i] = 0;
-        if (t == 0 && !small && !mid) {
+        if (t == 0 && !small) {
             LevelState& s = a.S[li & 1];
             s.mode = d.mode;
             s.done = go ? 0 : 1;
@@ -921,10 +627,6 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
     }
     if (small) {
         if (blockIdx.x == 0) small_levels<Off, SYM>(a, g, d, li, U.sm, red);
-        return;
-    }
-    if (mid) {
-        if (blockIdx.x % 8 == 0 && blockIdx.x / 8 < min(MID_NB, gridDim.x / 8u)) mid_levels<Off, SYM>(a, g, d, li, U.md, red);
         return;
     }
     if (!go) return;
@@ -1288,7 +990,6 @@ __global__ __launch_bounds__(TB) void bfs_init_k(BfsArgs a, Graph_d<Off> g, cons
         a.nmode[0] = a.nmode[1] = 0;
         a.host[0] = -1;
         a.host[3] = 0;
-        a.host[4] = 0;
     }
 }
 
@@ -1338,8 +1039,6 @@ int edge_bits(i64 nnz) {
 
 struct BfsWorkHolder {
     DevBuf<u32> qv[2];  // NQS segments of n entries
-    DevBuf<u32> mv[2], mdeg[2];  // mid-loop frontier lists (MID_M + 1 entries: a mid level's claims
-    DevBuf<u64> mbeg[2], moff[2];  // are at most its edges)
     DevBuf<u32> hv[2];
     DevBuf<u64> hbeg[2], hoff[2];
     DevBuf<u64> vis2;   // second visited buffer
@@ -1392,17 +1091,12 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     a.beta = g.beta;
     a.force = g.force_mode;
     a.small = g.bfs_small;
-    a.mid = g.bfs_mid;
     a.max_levels = g.max_levels > 0 ? g.max_levels : INT_INF;
     a.dist = g.dist.p;
     a.vis[0] = g.visited.p;
     a.vis[1] = w.vis2.p;
     a.fnew = w.fnew.p;
     for (int i = 0; i < 2; ++i) {
-        a.mv[i] = w.mv[i].p;
-        a.mdeg[i] = w.mdeg[i].p;
-        a.mbeg[i] = w.mbeg[i].p;
-        a.moff[i] = w.moff[i].p;
         a.qv[i] = w.qv[i].p;
         a.hv[i] = w.hv[i].p;
         a.hbeg[i] = w.hbeg[i].p;
@@ -1465,8 +1159,6 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
         }
         st.levels = *(volatile int64_t*)w.host;
         w.last_launches = (int32_t)((volatile int64_t*)w.host)[3];
-        if (((volatile int64_t*)w.host)[4])
-            throw Error(PJ_ERR_HIP, "BFS mid-level loop: a workgroup barrier timed out (solve void)");
     }
     if (!valid) PJ_HIP(hipEventRecord(g.ev1, s));
     spin_wait(s, g.ev1, nullptr);
@@ -1509,11 +1201,6 @@ void bfs_workspace(Graph& g) {
         w.hv[i].alloc(n ? n : 1);
         w.hbeg[i].alloc(n ? n : 1);
         w.hoff[i].alloc(n ? n : 1);
-        const size_t mc = (size_t)std::min<u64>(MID_M, (u64)std::max<size_t>(n, 1)) + 1;
-        w.mv[i].alloc(mc);
-        w.mdeg[i].alloc(mc);
-        w.mbeg[i].alloc(mc);
-        w.moff[i].alloc(mc);
     }
     w.vis2.alloc(nwords ? nwords : 1);
     w.zmask.alloc(nwords ? nwords : 1);

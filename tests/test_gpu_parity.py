@@ -77,12 +77,11 @@ def test_parse_weird_lines(ctx, oracle):
             ctx.load_snap_buffer(bad)
 
 
-@pytest.mark.parametrize("small,mid", [(0, 0), (1, 0), (1, 1), (0, 1)])
+@pytest.mark.parametrize("small", [0, 1])
 @pytest.mark.parametrize("kind", ["uniform", "hub", "chain"])
 @pytest.mark.parametrize("direction", [0, 1, 2])
-def test_bfs_random_graphs(ctx, oracle, kind, direction, small, mid):
-    """small = 1: levels with small push frontiers run on one workgroup (bfs.hip small_levels);
-    mid = 1: mid-size push levels run on 32 workgroups of one launch (bfs.hip mid_levels)."""
+def test_bfs_random_graphs(ctx, oracle, kind, direction, small):
+    """small = 1: levels with small push frontiers run on one workgroup (bfs.hip small_levels)."""
     rng = np.random.default_rng(100 + 7 * direction + len(kind))
     for trial in range(4):
         n = int(rng.integers(2, 60000))
@@ -90,7 +89,6 @@ def test_bfs_random_graphs(ctx, oracle, kind, direction, small, mid):
         g = ctx.load_coo(src, dst, n=n)
         g.set_option("direction", direction)
         g.set_option("bfs_small", small)
-        g.set_option("bfs_mid", mid)
         row, col, _ = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n)
         roots = [int(src[0]) if len(src) else 0, int(rng.integers(0, n)), n, -5]
         for r in roots:
@@ -157,10 +155,9 @@ def test_bfs_kronecker(ctx, oracle, scale):
         d = g.sssp(int(r))
         exp = oracle.bfs(row, col, int(r))
         assert (d == exp).all()
-        for mid, direction in ((1, 0), (1, 1), (0, 0)):  # mid-size levels on 32 workgroups (bfs_mid)
-            g.set_option("bfs_mid", mid)
+        for direction in (1, 2, 0):  # push only, pull whenever possible, automatic
             g.set_option("direction", direction)
-            assert (g.sssp(int(r)) == exp).all(), (mid, direction)
+            assert (g.sssp(int(r)) == exp).all(), direction
         st = g.reach_stats()
         reached = exp < INF
         assert st["reached"] == reached.sum()
@@ -495,12 +492,12 @@ def test_webgraph_cli_config0(ctx, pj, oracle, tmp_path):
     assert (ref4 == exp).all()
     assert out.read_bytes() == oracle.format_sol(exp)
     assert (exp < INF).sum() > 100000  # source 0 reaches a large part of the graph
-    # the in-process solver with and without the mid-size level loop, several sources
-    for mid in (1, 0, 1):
-        g.set_option("bfs_mid", mid)
-        assert (g.sssp(0) == exp).all(), mid
+    # the in-process solver with and without the one-workgroup small levels, several sources
+    for small in (0, 1):
+        g.set_option("bfs_small", small)
+        assert (g.sssp(0) == exp).all(), small
         for s in (1, 77, 5000):
-            assert (g.sssp(s) == oracle.bfs(row, col, s)).all(), (mid, s)
+            assert (g.sssp(s) == oracle.bfs(row, col, s)).all(), (small, s)
     g.close()
 
 
