@@ -190,7 +190,13 @@ const int32_t* pj_dist_device(pj_graph* g);
  * graphs run delta-stepping solves with `batch_streams` (default 2, 1-8) of
  * them in flight at once, each on its own stream and host thread with its own
  * frontiers and counters, the graph shared (delta.hip delta_batch; rows in
- * source order whatever finishes first). Either way pj_last_stats
+ * source order whatever finishes first). Device memory per slot in flight:
+ * unit weights ~n x (256 W + 24 W) bytes (a 64 W x n int32 distance block and
+ * three W-word masks per vertex; ms_streams slots, default 2, all slots within
+ * 16 GB); weights ~8 n bytes of rows plus ~60 x nnz / 64 bytes of hub queues per
+ * extra slot. A slot beyond the first is added only while it takes at most half
+ * the free device memory, and a failed allocation leaves the batch on the
+ * slots it has (no error). Either way pj_last_stats
  * then describes the whole batch (kernel_ms and levels summed over passes or
  * solves) and pj_copy_dist / pj_reach_stats fail with PJ_ERR_STATE until the
  * next pj_sssp. No reference counterpart: the reference answers one source

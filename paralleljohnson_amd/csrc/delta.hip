@@ -2092,17 +2092,31 @@ void delta_batch(Graph& g, const i64* sources, int n_src, int slots,
     DeltaWork& w = *g.delta_work;
     slots = std::max(1, std::min(slots, n_src));
     const i64 n_scan = g.rl->n_scan;
+    // A slot beyond the main one holds its own rows (relabeled and input-id distances), five
+    // n-bit bitmaps and the hub queue ring (3 x hcap x 20 bytes, hcap ~ nnz / 64: ~2 GB at
+    // s26). One is added only while it takes at most half the free device memory, and if its
+    // allocation still fails the batch runs on the slots it has.
+    const double slot_bytes = 4.0 * (double)(n_scan + g.n) + 5.0 * 8.0 * (double)((n_scan + 63) / 64) +
+                              60.0 * (double)std::max<i64>(1, std::min<i64>(n_scan, g.nnz / (i64)V2_HT + 1));
     while ((int)w.extra.size() < slots - 1) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess || slot_bytes > 0.5 * (double)fr) break;
         std::unique_ptr<DeltaSolve> v(new DeltaSolve());
-        PJ_HIP(hipStreamCreateWithFlags(&v->s, hipStreamNonBlocking));
-        v->own_stream = true;
-        v->dist_own.alloc((size_t)std::max<i64>(n_scan, 1));
-        v->out_own.alloc((size_t)std::max<i64>(g.n, 1));
-        v->dist = v->dist_own.p;
-        v->out = v->out_own.p;
-        ensure_solve(g, *v);
+        try {
+            PJ_HIP(hipStreamCreateWithFlags(&v->s, hipStreamNonBlocking));
+            v->own_stream = true;
+            v->dist_own.alloc((size_t)std::max<i64>(n_scan, 1));
+            v->out_own.alloc((size_t)std::max<i64>(g.n, 1));
+            v->dist = v->dist_own.p;
+            v->out = v->out_own.p;
+            ensure_solve(g, *v);
+        } catch (const Error&) {
+            (void)hipGetLastError();
+            break;
+        }
         w.extra.push_back(std::move(v));
     }
+    slots = std::min(slots, (int)w.extra.size() + 1);
     std::vector<DeltaSolve*> slot{&w.main};
     for (int k = 0; k + 1 < slots; ++k) slot.push_back(w.extra[(size_t)k].get());
     PJ_HIP(hipDeviceSynchronize());  // (the preparation ran on the ctx stream)

@@ -610,12 +610,18 @@ static void ms_pass_w(int W, Graph& g, MsSlot& w, const int64_t* sources, int ns
     else ms_pass<Off, 1>(g, w, sources, ns, kernel_ms, levels);
 }
 
+// Device bytes of one pass slot: the distance block (64 W x n int32), the masks V, F,
+// Fn (W words per vertex each) and the two nonzero-row bitmaps.
+static double ms_slot_bytes(i64 n, int W) {
+    return (double)n * (64.0 * W * 4.0 + 3.0 * W * 8.0) + 2.0 * ((double)n / 8.0 + 16.0);
+}
+constexpr double MS_BUDGET = 16e9;  // device bytes all slots of a batch may hold
 // Pass width: the fewest words that hold the batch, at most MS_WMAX (g.ms_width
-// caps it), and the pass's distance block (64 W x n int32) kept under 16 GB.
+// caps it), with one slot's buffers within the budget.
 static int ms_words(const Graph& g, int n_src) {
     int W = 1;
     const int cap = g.ms_width > 0 ? std::min(g.ms_width, MS_WMAX) : MS_WDEF;
-    while (W < cap && 64 * W < n_src && (double)(128 * W) * 4.0 * (double)g.n <= 16e9) W *= 2;
+    while (W < cap && 64 * W < n_src && ms_slot_bytes(g.n, 2 * W) <= MS_BUDGET) W *= 2;
     return W;
 }
 
@@ -642,17 +648,36 @@ void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_
     const int W = ms_words(g, n_src);
     const int per = 64 * W;
     const int npass = (n_src + per - 1) / per;
-    const int nslots = std::max(1, std::min(g.ms_streams, npass));
+    int nslots = std::max(1, std::min(g.ms_streams, npass));
     if (!g.ms_work || g.ms_work->W < W) {
         g.ms_work.reset(new MsWork());
         g.ms_work->W = W;
     }
     MsWork& mw = *g.ms_work;
-    while ((int)mw.slots.size() < nslots) {
+    // Every slot holds a whole pass (ms_slot_bytes: ~1.9 GB at n = 916K, W = 8): the slots
+    // in flight stay within MS_BUDGET, and a slot beyond the first is only added while it
+    // takes at most half the free device memory; if its allocation still fails, the batch
+    // runs on the slots it has.
+    const double sb = ms_slot_bytes(g.n, mw.W);
+    while (nslots > 1 && (double)nslots * sb > MS_BUDGET) --nslots;
+    if (mw.slots.empty()) {
         std::unique_ptr<MsSlot> sl(new MsSlot());
-        ms_slot_alloc(g, *sl, mw.W, !mw.slots.empty());
+        ms_slot_alloc(g, *sl, mw.W, false);
         mw.slots.push_back(std::move(sl));
     }
+    while ((int)mw.slots.size() < nslots) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess || sb > 0.5 * (double)fr) break;
+        std::unique_ptr<MsSlot> sl(new MsSlot());
+        try {
+            ms_slot_alloc(g, *sl, mw.W, true);
+        } catch (const Error&) {
+            (void)hipGetLastError();
+            break;
+        }
+        mw.slots.push_back(std::move(sl));
+    }
+    nslots = std::min(nslots, (int)mw.slots.size());
     mw.slots[0]->s = g.ctx->stream;  // (pj_set_stream may change it)
     auto t0 = std::chrono::steady_clock::now();
     pj_stats st{};
