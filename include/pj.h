@@ -390,7 +390,11 @@ int pj_wpart_begin(pj_wpart* p, int64_t source, int32_t delta, int32_t* delta_ou
 int pj_wpart_select(pj_wpart* p, int32_t lo, int32_t hi, int64_t* out);
 /* light != 0: the frontier relaxes its light edges (w < delta) and joins the
  * band's members; light == 0: the members relax their heavy edges. Remote
- * candidates are written to send owner-major, counts[world] per owner. */
+ * candidates are written to send owner-major, counts[world] per owner; send
+ * may be NULL only at world 1 (PJ_ERR_ARG otherwise). The ids in send are the
+ * partition's internal ids (with the per-block degree order, PJ_WP_RELABEL, a
+ * block's relabeled ids): only their owner, id / block, is meaningful outside,
+ * and pj_wpart_apply on that owner takes them back unchanged. */
 int pj_wpart_relax(pj_wpart* p, int light, int32_t lo, int32_t hi, uint64_t* send, int64_t* counts);
 /* Fold the received candidates into the owned distances (light: those below hi
  * join the next frontier). */
@@ -461,8 +465,10 @@ typedef struct pj_part_stats {
  * the analogue of :488-594): every rank of comm calls it with the same source.
  * pj_part_set_option keys: "alpha", "beta" (Beamer), "direction" (0 auto,
  * 1 push, 2 pull), "exchange_cap" (ids per rank and direction the exchange buffers
- * hold; a push level with more goes out in pieces by word range of the owners' slices;
- * -1 = block / 16 (default), 0 = no cap). Every rank must use the same values. */
+ * hold; a push level with more goes out in pieces by word range of the owners' slices,
+ * each piece its own count exchange, alltoallv and host wait; -1 = max(block / 16,
+ * 4096) ids (default), 0 = no cap, else at least 64 ids: smaller caps are
+ * PJ_ERR_ARG). Every rank must use the same values. */
 int pj_part_bfs(pj_part* p, pj_comm* comm, int64_t source, pj_part_stats* st);
 int pj_part_set_option(pj_part* p, const char* key, double value);
 /* All ranks of a one-process group at once (one host thread per rank);

@@ -421,15 +421,55 @@ def write_parents(parent, path: str):
     _check(_lib.pj_write_parents(_ptr(p), len(p), os.fsencode(path)))
 
 
-def host_pin(a: np.ndarray):
-    """Page-lock a (contiguous) host array for direct device -> host copies (pj_host_pin)."""
+class Pinned:
+    """A host array page-locked by host_pin. Holds the array, so its pages cannot be freed
+    (and the address reused by another array) while the registration stands; unpins on
+    close(), at the end of a `with` block, or when the handle is garbage-collected."""
+
+    def __init__(self, a: np.ndarray):
+        self.array = a
+        self.addr = a.ctypes.data
+        _check(_lib.pj_host_pin(self.addr, a.nbytes))
+        _PINNED[self.addr] = self
+
+    def close(self):
+        if self.array is not None:
+            _PINNED.pop(self.addr, None)
+            self.array = None
+            _check(_lib.pj_host_unpin(self.addr))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            if self.array is not None and _lib is not None:
+                _lib.pj_host_unpin(self.addr)
+        except Exception:  # noqa: BLE001 (interpreter shutdown)
+            pass
+
+
+_PINNED = {}  # address -> Pinned (keeps the array alive while registered)
+
+
+def host_pin(a: np.ndarray) -> Pinned:
+    """Page-lock a (contiguous) host array for direct device -> host copies (pj_host_pin).
+    Returns a Pinned handle (also a context manager); host_unpin(a) or handle.close() undoes it."""
     if not a.flags.c_contiguous or a.nbytes == 0:
         raise ValueError("host_pin: a contiguous, non-empty array")
-    _check(_lib.pj_host_pin(a.ctypes.data, a.nbytes))
+    if a.ctypes.data in _PINNED:
+        raise ValueError("host_pin: this address is already pinned")
+    return Pinned(a)
 
 
 def host_unpin(a: np.ndarray):
-    _check(_lib.pj_host_unpin(a.ctypes.data))
+    h = _PINNED.get(a.ctypes.data)
+    if h is None:
+        raise ValueError("host_unpin: not pinned through host_pin")
+    h.close()
 
 
 def device_count() -> int:

@@ -1259,6 +1259,9 @@ int pj_wpart_relax(pj_wpart* p, int light, int32_t lo, int32_t hi, uint64_t* sen
     if (!p || !counts || lo < 0 || hi < lo) return arg_error("pj_wpart_relax: bad argument");
     return guarded([&] {
         bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
+        if (!send && wpart_world(*reinterpret_cast<WPart*>(p)) > 1)
+            throw Error(PJ_ERR_ARG, "pj_wpart_relax: world > 1 needs the send buffer (the remote pairs are packed "
+                                    "into it)");
         wpart_relax(*reinterpret_cast<WPart*>(p), light, lo, hi, (u64*)send, counts);
         return (int)PJ_OK;
     });
@@ -1673,7 +1676,7 @@ int pj_part_set_option(pj_part* p, const char* key, double value) {
     if (k == "alpha" && value > 0) prm.alpha = value;
     else if (k == "beta" && value > 0) prm.beta = value;
     else if (k == "direction" && (value == 0 || value == 1 || value == 2)) prm.force = (int)value;
-    else if (k == "exchange_cap" && value >= -1) prm.xcap = (i64)value;
+    else if (k == "exchange_cap" && (value == -1 || value == 0 || value >= 64)) prm.xcap = (i64)value;
     else return arg_error("pj_part_set_option: unknown key or bad value");
     return PJ_OK;
 }

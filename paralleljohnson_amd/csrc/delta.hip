@@ -97,8 +97,9 @@ __device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
 // a set bit. Exact: every u with dist[u] < hi outside that set has already relaxed its
 // edges of this kind at its current distance (a lowered vertex re-enters the frontier), so
 // dist[u] + w >= dist[v] and it never lowers v's running best.
+// k26w 450.6 / 450.6 -> 472.8 / 471.3 (1) -> 487.0 / 486.9 GTEPS (2) interleaved (r5a)
 #ifndef PJ_V2_NOFIN
-#define PJ_V2_NOFIN 0
+#define PJ_V2_NOFIN 2
 #endif
 // the candidate distance u offers through a pulled edge (INT_INF = none): bits == null
 // probes dist[u] alone (PJ_V2_NOFIN), else u's bit first

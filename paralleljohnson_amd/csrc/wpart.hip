@@ -1735,6 +1735,7 @@ struct WPartGpuSteps final : DeltaSteps {
 }  // namespace
 
 const Ctx& wpart_ctx(const WPart& p) { return *p.ctx; }
+int wpart_world(const WPart& p) { return p.world; }
 
 double* wpart_tail_params(WPart& p) { return p.tail; }
 double& wpart_pull_factor(WPart& p) { return p.pull_factor; }

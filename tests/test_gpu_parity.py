@@ -362,6 +362,13 @@ def test_copy_dist_into_pinned_rows(ctx, pj, oracle):
         pj.host_unpin(rows)
     assert 4 * g.n > (1 << 20)
     assert (pinned == staged).all() and (staged == oracle.bfs(row, col.astype(np.uint32), r)).all()
+    rows2 = np.empty(g.n, np.int32)
+    with pj.host_pin(rows2):  # the handle form: unpinned at the end of the block
+        with pytest.raises(ValueError):
+            pj.host_pin(rows2)  # (already registered)
+        assert (g.copy_dist(rows2) == staged).all()
+    with pytest.raises(ValueError):
+        pj.host_unpin(rows2)  # (no longer registered)
     with pytest.raises(ValueError):
         g.copy_dist(np.empty(g.n - 1, np.int32))
     g.close()

@@ -293,7 +293,7 @@ def test_part_kronecker_matches_single_gpu(ctx, pj, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,force,cap", [(2, 0, -1), (2, 1, -1), (2, 2, -1), (3, 0, -1), (2, 1, 50), (3, 0, 200)])
+@pytest.mark.parametrize("world,force,cap", [(2, 0, -1), (2, 1, -1), (2, 2, -1), (3, 0, -1), (2, 1, 64), (3, 0, 200)])
 def test_part_group_one_gpu(pj, oracle, world, force, cap):
     """world ranks of one process sharing the one GPU (host transport: device copies between
     the ranks' buffers, one host thread per rank): libpj kernels + the C++ level loop + the
