@@ -208,7 +208,7 @@ def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
                   for _, st in roots))
     st0 = roots[0][1]
     res = dict(elapsed=elapsed, m=m, b=b, n=ops.n, nnz_local=ops.nnz_local, build_s=build_s, roots=len(roots),
-               st0=st0, transport=comm.kind)
+               st0=st0, transport=comm.kind, build_phases=ops.build_phases())
     ops.close()
     comm.close()
     return res
@@ -224,7 +224,11 @@ def run_partitioned_host(args, world_h=2, nroots=4):
     ctxs = [pj.Context(0) for _ in range(world_h)]
     comms = Comm.group(ctxs, "host")
     t0 = time.perf_counter()
-    parts = [load_kronecker(ctxs[r], args.part_scale, args.edgefactor, args.seed, r, world_h) for r in range(world_h)]
+    parts, build_rank_s = [], []
+    for r in range(world_h):  # (the ranks build one after the other, each with the whole GPU)
+        t1 = time.perf_counter()
+        parts.append(load_kronecker(ctxs[r], args.part_scale, args.edgefactor, args.seed, r, world_h))
+        build_rank_s.append(round(time.perf_counter() - t1, 3))
     build_s = time.perf_counter() - t0
     try:
         rng = np.random.default_rng(args.seed + 7)  # run_partitioned's candidates
@@ -251,7 +255,8 @@ def run_partitioned_host(args, world_h=2, nroots=4):
             "ids_sent_per_bfs_by_rank": [x["sent"] for x in st0],
             "nnz_local_by_rank": [p.nnz_local for p in parts],
             "device_bytes_by_rank": [p.device_bytes() for p in parts],
-            "build_s": round(build_s, 2),
+            "build_s": round(build_s, 2), "build_s_by_rank": build_rank_s,
+            "build_phases_by_rank": [p.build_phases() for p in parts],
         }
     finally:
         for p in parts:
@@ -633,7 +638,8 @@ def main():
             "gteps": round(pr["m"] / el / 1e9, 3), "gteps_graph500": round(pr["m"] / el / 2e9, 3),
             "hbm_frac_algorithmic": round(pr["b"] / el / 1e9 / (HBM_PEAK_GBS * world), 4),
             "levels_td_bu": [pr["st0"]["td_levels"], pr["st0"]["bu_levels"]],
-            "build_s": round(pr["build_s"], 2), "scaling": "strong (one graph, all ranks)",
+            "build_s": round(pr["build_s"], 2), "build_phases_rank0": pr["build_phases"],
+            "scaling": "strong (one graph, all ranks)",
         }
 
     emit()

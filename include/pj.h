@@ -292,6 +292,12 @@ typedef struct pj_part_info {
      * and the engine's replicated visited / isolated masks once pj_part_bfs ran) and
      * the exchange buffers (sized to the largest level's ids sent / received) */
     int64_t bytes_rows, bytes_state, bytes_bitmaps, bytes_exchange;
+    /* how the block was built (host wall microseconds, each phase ending at a stream
+     * sync): [0] tuple enumeration + owned-entry count, [1] enumeration + write of the
+     * owned entries, [2] radix sort of the local COO, [3] CSR bounds, [4] device
+     * allocations, [5] per-solve state, [6] total, [7] device frees, [8] the slowest
+     * single allocation, [9] its size in MB (not microseconds) */
+    int64_t build_us[10];
 } pj_part_info;
 
 /* The rank's share of pj_generate_kronecker(scale, edgefactor, seed, unit
@@ -349,14 +355,18 @@ const int32_t* pj_part_dist_device(pj_part* p);
  *         all_reduce sum(count), min(min): count 0 -> jump lo to the band of
  *         min, or stop when min = INF (the termination test :579-593)
  *         light rounds until all_reduce sum(new frontier) = 0:
- *           pj_wpart_relax(light = 1) -> send (u64 id | cand << 32, owner-major),
- *           counts[world]; all_to_all_single; pj_wpart_apply(received);
+ *           pj_wpart_relax(light = 1) -> counts[world] of the queued pairs
+ *           (u64 id | cand << 32); all_to_all counts; pj_wpart_pack into a send
+ *           buffer of their sum (owner-major); all_to_all_v; pj_wpart_apply(received);
  *           pj_wpart_end_round -> new frontier size on this rank
  *         heavy step: pj_wpart_relax(light = 0); exchange; pj_wpart_apply
  *         lo += delta
  *
- * send and recv are device buffers of capacity world * block u64. Distances
- * follow the R9 contract with the graph's integer weights. */
+ * send and recv are caller-owned device buffers sized to the counts. A relax
+ * queues its remote pairs itself (a claim queue that grows with the traffic) and
+ * skips the pairs a cache of the pairs already sent shows as useless, so the
+ * owner may receive the same id twice in a round (its apply takes the minimum).
+ * Distances follow the R9 contract with the graph's integer weights. */
 typedef struct pj_wpart pj_wpart;
 /* The rank's block of a weighted graph (pj_load_coo / pj_load_snap(weighted) /
  * pj_generate_kronecker(weighted)); the graph may be destroyed afterwards.
@@ -377,10 +387,15 @@ int pj_wpart_generate_kronecker(pj_ctx* ctx, int scale, int edgefactor, uint64_t
 int pj_wpart_destroy(pj_wpart* p);
 /* out[8] = (n, lo, hi, block, nnz_local, world, rank, nnz of the whole graph) */
 int pj_wpart_info(const pj_wpart* p, int64_t* out);
-/* out[4] = this rank's device bytes: its rows; the O(block) vertex state; the
- * N-sized tables (remote candidates, int32 per vertex, with their touched bitmap,
- * and the pull rounds' replicated byte map); the exchange buffers, sized to the
- * largest round's (id, candidate) traffic once pj_wpart_delta ran. */
+/* out[4] = this rank's device bytes: its rows; the O(block) vertex state (with the
+ * sent-pair cache, 2 x block entries); the replicated maps the pulls and the tail
+ * all-gather (N bytes, 2N for the tail's 16-bit frontier map, N bits for the
+ * settled map: the analogue of the BFS pull's visited bitmap); the claim queue and
+ * the exchange buffers, sized to the largest round's pairs. Building a block with
+ * the per-block degree order (pj_wpart_generate_kronecker, pj_wpart_from_graph,
+ * pj_wpart_load_snap) also holds ~20 bytes per vertex of the WHOLE graph for a
+ * moment (every vertex's degree, the sort keys and the relabel table, which all
+ * ranks must agree on); none of it stays. */
 int pj_wpart_device_bytes(const pj_wpart* p, int64_t* out);
 /* Start a solve from `source` (dist := INF, then the source); delta <= 0 picks
  * the single-GPU default (3.5 x mean weight / mean degree). *delta_out = delta. */
@@ -389,13 +404,18 @@ int pj_wpart_begin(pj_wpart* p, int64_t source, int32_t delta, int32_t* delta_ou
  * (its size, min owned dist >= lo or PJ_INT_INF). */
 int pj_wpart_select(pj_wpart* p, int32_t lo, int32_t hi, int64_t* out);
 /* light != 0: the frontier relaxes its light edges (w < delta) and joins the
- * band's members; light == 0: the members relax their heavy edges. Remote
- * candidates are written to send owner-major, counts[world] per owner; send
- * may be NULL only at world 1 (PJ_ERR_ARG otherwise). The ids in send are the
- * partition's internal ids (with the per-block degree order, PJ_WP_RELABEL, a
- * block's relabeled ids): only their owner, id / block, is meaningful outside,
- * and pj_wpart_apply on that owner takes them back unchanged. */
+ * band's members; light == 0: the members relax their heavy edges. counts[o] =
+ * the pairs queued for owner o. With send != NULL (room for their sum) the
+ * pairs are also packed into it owner-major; with send == NULL the caller
+ * sizes its buffer and calls pj_wpart_pack before any other step of p
+ * (PJ_ERR_STATE otherwise: the cache already counts the pairs as sent). The ids
+ * are the partition's internal ids (with the per-block degree order,
+ * PJ_WP_RELABEL, a block's relabeled ids): only their owner, id / block, is
+ * meaningful outside, and pj_wpart_apply on that owner takes them back unchanged. */
 int pj_wpart_relax(pj_wpart* p, int light, int32_t lo, int32_t hi, uint64_t* send, int64_t* counts);
+/* The pairs of the last pj_wpart_relax (send == NULL), owner-major, into send
+ * (room for the sum of its counts). */
+int pj_wpart_pack(pj_wpart* p, uint64_t* send);
 /* Fold the received candidates into the owned distances (light: those below hi
  * join the next frontier). */
 int pj_wpart_apply(pj_wpart* p, const uint64_t* recv, int64_t n_recv, int light, int32_t lo, int32_t hi);
@@ -492,7 +512,10 @@ int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj
  * all-gathered frontier map; symmetric graphs; 0 = push; default 0: since the push rounds
  * count their frontier per workgroup the pull no longer pays, profiles/r03/wpart_light_pull_r3ad.txt)
  * and "tail_light_pull" (the same rule in the tail's bands, independent of light_pull, the
- * frontier map then 16-bit; 0 = push; default 3). Every rank must use the same values. */
+ * frontier map then 16-bit; 0 = push; default 3). Every rank must use the same values.
+ * "queue_shard" (this rank only, any time between steps): the claim queue's shard
+ * capacity in pairs from now on, >= 1 (64 shards; it still grows when a round
+ * overflows it: tests use small values to run that path). */
 int pj_wpart_set_option(pj_wpart* p, const char* key, double value);
 int pj_wpart_delta_group(int world, pj_wpart* const* parts, pj_comm* const* comms, int64_t source, int32_t delta,
                          pj_part_stats* st);
@@ -569,9 +592,15 @@ int pj_multi_load_snap(pj_multi* m, const char* path, int weighted, int layout);
 /* CSR cache for later replicated loads (pj_load_snap_cached; rank 0 writes it);
  * NULL or "" turns it off. Partitioned loads always parse. */
 int pj_multi_set_csr_cache(pj_multi* m, const char* cache_path);
-/* pj_generate_kronecker on every rank (partitioned + weighted: the whole graph
- * is resident on each GPU while its block is cut, as pj_wpart_from_graph). */
+/* pj_generate_kronecker on every rank; partitioned: every rank enumerates the
+ * tuples on its GPU and keeps only its block's rows (pj_part_generate_kronecker /
+ * pj_wpart_generate_kronecker), so no GPU ever holds the whole graph. */
 int pj_multi_generate_kronecker(pj_multi* m, int scale, int edgefactor, uint64_t seed, int weighted, int layout);
+/* Rank `rank`'s device bytes of the loaded graph, out[4] = (rows, O(block) vertex
+ * state, replicated maps / N-bit bitmaps, exchange buffers): pj_part_info_get's or
+ * pj_wpart_device_bytes' four numbers for a partitioned graph; (graph bytes, 0, 0, 0)
+ * for a replicated one. */
+int pj_multi_device_bytes(const pj_multi* m, int rank, int64_t* out);
 int pj_multi_info(const pj_multi* m, pj_multi_info_t* out);
 /* One source: dist_out (n int32, host) may be NULL. st (may be NULL): rank 0's
  * counts with solve_ms = the max over ranks (the reference's Time:, :597-605). */

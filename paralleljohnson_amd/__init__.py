@@ -140,6 +140,7 @@ _SIGS = {
     "pj_wpart_select": ([_P, ctypes.c_int32, ctypes.c_int32, _P], _INT),
     "pj_wpart_relax": ([_P, _INT, ctypes.c_int32, ctypes.c_int32, _P, _P], _INT),
     "pj_wpart_apply": ([_P, _P, _I64, _INT, ctypes.c_int32, ctypes.c_int32], _INT),
+    "pj_wpart_pack": ([_P, _P], _INT),
     "pj_wpart_end_round": ([_P, _P], _INT),
     "pj_wpart_reach": ([_P, _P], _INT),
     "pj_wpart_copy_dist": ([_P, _P], _INT),
@@ -168,6 +169,7 @@ _SIGS = {
     "pj_multi_load_snap": ([_P, ctypes.c_char_p, _INT, _INT], _INT),
     "pj_multi_generate_kronecker": ([_P, _INT, _INT, ctypes.c_uint64, _INT, _INT], _INT),
     "pj_multi_info": ([_P, _P], _INT),
+    "pj_multi_device_bytes": ([_P, _INT, _P], _INT),
     "pj_multi_sssp": ([_P, _I64, _P, _P], _INT),
     "pj_multi_sssp_batch": ([_P, _P, _INT, _P], _INT),
     "pj_multi_sssp_batch_write": ([_P, _P, _INT, _P, _INT, _P], _INT),

@@ -1259,10 +1259,19 @@ int pj_wpart_relax(pj_wpart* p, int light, int32_t lo, int32_t hi, uint64_t* sen
     if (!p || !counts || lo < 0 || hi < lo) return arg_error("pj_wpart_relax: bad argument");
     return guarded([&] {
         bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
-        if (!send && wpart_world(*reinterpret_cast<WPart*>(p)) > 1)
-            throw Error(PJ_ERR_ARG, "pj_wpart_relax: world > 1 needs the send buffer (the remote pairs are packed "
-                                    "into it)");
         wpart_relax(*reinterpret_cast<WPart*>(p), light, lo, hi, (u64*)send, counts);
+        return (int)PJ_OK;
+    });
+}
+
+int pj_wpart_pack(pj_wpart* p, uint64_t* send) {
+    if (!p) return arg_error("pj_wpart_pack: bad argument");
+    return guarded([&] {
+        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
+        WPart& P = *reinterpret_cast<WPart*>(p);
+        if (!wpart_pending(P)) throw Error(PJ_ERR_STATE, "pj_wpart_pack: no relax is waiting to be packed");
+        if (!send) throw Error(PJ_ERR_ARG, "pj_wpart_pack: send is NULL");
+        wpart_pack(P, (u64*)send);
         return (int)PJ_OK;
     });
 }
@@ -1395,7 +1404,7 @@ int pj_part_destroy(pj_part* p) {
 
 int pj_part_info_get(const pj_part* p, pj_part_info* out) {
     if (!p || !out) return arg_error("pj_part_info_get: bad argument");
-    i64 v[15];
+    i64 v[25];
     part_info(*reinterpret_cast<const Part*>(p), v);
     out->n = v[0];
     out->lo = v[1];
@@ -1412,6 +1421,7 @@ int pj_part_info_get(const pj_part* p, pj_part_info* out) {
     out->bytes_state = v[12];
     out->bytes_bitmaps = v[13];
     out->bytes_exchange = v[14];
+    for (int k = 0; k < 10; ++k) out->build_us[k] = v[15 + k];
     return PJ_OK;
 }
 
@@ -1439,7 +1449,7 @@ int pj_part_push(pj_part* p, int level, uint64_t* vis, uint32_t* send, int64_t* 
     return guarded([&] {
         bind(part_ctx(*reinterpret_cast<Part*>(p)));
         Part& P = *reinterpret_cast<Part*>(p);
-        i64 info[15];
+        i64 info[25];
         part_info(P, info);
         if (info[9] > 1 && !send) throw Error(PJ_ERR_ARG, "pj_part_push: send is NULL");
         part_push(P, level, reinterpret_cast<u64*>(vis), send, counts);
@@ -1719,6 +1729,12 @@ int pj_wpart_set_option(pj_wpart* p, const char* key, double value) {
     else if (k == "pull_factor" && value >= 0) wpart_pull_factor(P) = value;
     else if (k == "light_pull" && value >= 0) wpart_light_pull(P) = value;
     else if (k == "tail_light_pull" && value >= 0) wpart_tail_light_pull(P) = value;
+    else if (k == "queue_shard" && value >= 1 && value <= 1e9)
+        return guarded([&] {
+            bind(wpart_ctx(P));
+            wpart_set_queue_shard(P, (i64)value);
+            return (int)PJ_OK;
+        });
     else return arg_error("pj_wpart_set_option: unknown key or bad value");
     return PJ_OK;
 }

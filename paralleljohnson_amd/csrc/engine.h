@@ -199,6 +199,8 @@ BfsParams& part_params(Part& p);
 const Ctx& part_ctx(const Part& p);
 const Ctx& wpart_ctx(const WPart& p);
 int wpart_world(const WPart& p);
+bool wpart_pending(const WPart& p);
+void wpart_set_queue_shard(WPart& p, i64 pairs);
 double* wpart_tail_params(WPart& p);  // [0] tail_frac, [1] tail_mult (pj_wpart_set_option)
 double& wpart_pull_factor(WPart& p);  // heavy pull rule (pj_wpart_set_option "pull_factor")
 double& wpart_light_pull(WPart& p);   // light pull rule (pj_wpart_set_option "light_pull")

@@ -229,16 +229,11 @@ int pj_multi_generate_kronecker(pj_multi* m, int scale, int edgefactor, uint64_t
         if (rc == PJ_OK) {
             m->parts.assign((size_t)P, nullptr);
             m->wparts.assign((size_t)P, nullptr);
-            rc = per_rank(P, [&](int r) {
-                if (!weighted)
-                    return pj_part_generate_kronecker(m->ctxs[(size_t)r], scale, edgefactor, seed, r, P,
-                                                      &m->parts[(size_t)r]);
-                // weighted: the whole graph on the rank's GPU while its block is cut (pj_wpart_from_graph)
-                pj_graph* g = nullptr;
-                int e = pj_generate_kronecker(m->ctxs[(size_t)r], scale, edgefactor, seed, 1, &g);
-                if (e == PJ_OK) e = pj_wpart_from_graph(g, r, P, &m->wparts[(size_t)r]);
-                pj_graph_destroy(g);
-                return e;
+            rc = per_rank(P, [&](int r) {  // every rank enumerates the tuples and keeps its block's rows
+                return weighted ? pj_wpart_generate_kronecker(m->ctxs[(size_t)r], scale, edgefactor, seed, r, P,
+                                                              &m->wparts[(size_t)r])
+                                : pj_part_generate_kronecker(m->ctxs[(size_t)r], scale, edgefactor, seed, r, P,
+                                                             &m->parts[(size_t)r]);
             });
         }
     }
@@ -249,6 +244,28 @@ int pj_multi_generate_kronecker(pj_multi* m, int scale, int edgefactor, uint64_t
         return rc;
     }
     return finish_load(m, layout, weighted);
+}
+
+int pj_multi_device_bytes(const pj_multi* m, int rank, int64_t* out) {
+    if (!m || !out || rank < 0 || rank >= m->world) return arg_error("pj_multi_device_bytes: bad argument");
+    const int rc = check_loaded(m, "pj_multi_device_bytes");
+    if (rc != PJ_OK) return rc;
+    for (int k = 0; k < 4; ++k) out[k] = 0;
+    if (m->layout == PJ_LAYOUT_REPLICATED) {
+        int64_t n = 0, nnz = 0;
+        int32_t w = 0, sym = 0;
+        pj_graph_info(m->graphs[(size_t)rank], &n, &nnz, &w, &sym);
+        out[0] = 4 * (n + 1) + (4 + (w ? 4 : 0)) * nnz;  // (row offsets, columns, weights)
+        return PJ_OK;
+    }
+    if (m->weighted) return pj_wpart_device_bytes(m->wparts[(size_t)rank], out);
+    pj_part_info pi{};
+    const int e = pj_part_info_get(m->parts[(size_t)rank], &pi);
+    out[0] = pi.bytes_rows;
+    out[1] = pi.bytes_state;
+    out[2] = pi.bytes_bitmaps;
+    out[3] = pi.bytes_exchange;
+    return e;
 }
 
 int pj_multi_info(const pj_multi* m, pj_multi_info_t* out) {

@@ -41,6 +41,9 @@
 //          m_f); the driver sums them over ranks (the analogue of the
 //          MPI_Allreduce termination test at :589-590) and all-gathers the vis
 //          slices before pull levels.
+#include <chrono>
+#include <cmath>
+
 #include "kron.h"
 #include "lb.h"
 #include "engine.h"
@@ -556,9 +559,45 @@ struct Part {
     const Comm* iso_comm = nullptr;   // transport the replicated isolated mask was gathered over
     bool iso_ok = false;
     BfsParams prm;
+    // build phases (host wall seconds, each ending at a stream sync): [0] enumerate + count
+    // (filter_count_k: every tuple generated, the owned ones counted), [1] enumerate + write
+    // (filter_write_k), [2] radix sort of the local COO, [3] CSR bounds, [4] device
+    // allocations, [5] per-solve state, [6] total, [7] device frees; [8] the slowest single
+    // allocation and [9] its GB
+    double bt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 void delete_part(Part* p) { delete p; }
+
+namespace {
+// host wall clock since the last call, added to acc (the build phases of Part::bt)
+struct PhaseClock {
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(double& acc) {
+        const auto u = std::chrono::steady_clock::now();
+        acc += std::chrono::duration<double>(u - t).count();
+        t = u;
+    }
+};
+// one timed device allocation (bt[4]; the slowest one in bt[8], its GB in bt[9]) and
+// one timed free (bt[7]); the caller laps whatever ran before into its own phase
+template <typename T>
+void timed_alloc(double* bt, PhaseClock& pc, DevBuf<T>& b, size_t count) {
+    const auto t0 = std::chrono::steady_clock::now();
+    b.alloc(count);
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (dt > bt[8]) {
+        bt[8] = dt;
+        bt[9] = (double)(count * sizeof(T)) / 1e9;
+    }
+    pc.lap(bt[4]);
+}
+template <typename T>
+void timed_free(double* bt, PhaseClock& pc, DevBuf<T>& b) {
+    b.release();
+    pc.lap(bt[7]);
+}
+}  // namespace
 
 namespace {
 
@@ -601,9 +640,9 @@ PartArgs part_args(Part& p, u64* vis) {
 }
 
 template <class S>
-i64 filter_into(Ctx& ctx, const S& src, i64 items, bool by_dst, i64 lo, i64 hi, DevBuf<u32>& key,
-                DevBuf<u32>& val) {
-    hipStream_t s = ctx.stream;
+i64 filter_into(Part& p, const S& src, i64 items, bool by_dst, i64 lo, i64 hi, DevBuf<u32>& key,
+                DevBuf<u32>& val, PhaseClock& pc) {
+    hipStream_t s = p.ctx->stream;
     const i64 per = (i64)TB * IPT;
     const i64 nb = (items + per - 1) / per;
     if (nb == 0) {
@@ -611,61 +650,80 @@ i64 filter_into(Ctx& ctx, const S& src, i64 items, bool by_dst, i64 lo, i64 hi, 
         val.alloc(0);
         return 0;
     }
-    DevBuf<u32> bcnt((size_t)nb);
-    DevBuf<u64> boff((size_t)nb + 1);
+    DevBuf<u32> bcnt;
+    DevBuf<u64> boff;
     ScanWs ws;
+    pc.lap(p.bt[0]);
+    timed_alloc(p.bt, pc, bcnt, (size_t)nb);
+    timed_alloc(p.bt, pc, boff, (size_t)nb + 1);
     filter_count_k<S><<<(unsigned)nb, TB, 0, s>>>(src, by_dst, (u64)lo, (u64)hi, bcnt.p);
     PJ_LAUNCH_CHECK();
     exclusive_scan_u32(bcnt.p, boff.p, nb, ws, s);
     u64 total = 0;
     PJ_HIP(hipMemcpyAsync(&total, boff.p + nb, sizeof(u64), hipMemcpyDeviceToHost, s));
     PJ_HIP(hipStreamSynchronize(s));
-    key.alloc((size_t)total);
-    val.alloc((size_t)total);
+    pc.lap(p.bt[0]);
+    timed_alloc(p.bt, pc, key, (size_t)total);
+    timed_alloc(p.bt, pc, val, (size_t)total);
     if (total) {
         filter_write_k<S><<<(unsigned)nb, TB, 0, s>>>(src, by_dst, (u64)lo, (u64)hi, boff.p, key.p, val.p);
         PJ_LAUNCH_CHECK();
     }
     PJ_HIP(hipStreamSynchronize(s));
+    pc.lap(p.bt[1]);
+    timed_free(p.bt, pc, bcnt);
+    timed_free(p.bt, pc, boff);
     return (i64)total;
 }
 
 // sort the local COO by key and turn it into rows [nl+1] (Off) + vals
 void rows_from_local(Part& p, DevBuf<u32>& key, DevBuf<u32>& val, i64 m, DevBuf<u32>& r32, DevBuf<u64>& r64,
-                     DevBuf<u32>& out) {
+                     DevBuf<u32>& out, PhaseClock& pc) {
     hipStream_t s = p.ctx->stream;
     int bits = 0;
     while (bits < 32 && ((u64)1 << bits) < (u64)p.nl) ++bits;
     SortWs ws;
-    DevBuf<u32> kalt((size_t)m), valt((size_t)m);
+    DevBuf<u32> kalt, valt;
+    timed_alloc(p.bt, pc, kalt, (size_t)m);
+    timed_alloc(p.bt, pc, valt, (size_t)m);
     u32 *kr, *vr;
     radix_sort_pairs<u32>(key.p, kalt.p, val.p, valt.p, m, bits, ws, s, &kr, &vr);
+    PJ_HIP(hipStreamSynchronize(s));
+    pc.lap(p.bt[2]);
     if (p.off64) {
-        r64.alloc((size_t)p.nl + 1);
+        timed_alloc(p.bt, pc, r64, (size_t)p.nl + 1);
         csr_bounds<u64>(kr, m, p.nl, r64.p, s);
     } else {
-        r32.alloc((size_t)p.nl + 1);
+        timed_alloc(p.bt, pc, r32, (size_t)p.nl + 1);
         csr_bounds<u32>(kr, m, p.nl, r32.p, s);
     }
     PJ_HIP(hipStreamSynchronize(s));
+    pc.lap(p.bt[3]);
     out = std::move(vr == val.p ? val : valt);
+    timed_free(p.bt, pc, key);
+    timed_free(p.bt, pc, val);
+    timed_free(p.bt, pc, kalt);
+    timed_free(p.bt, pc, valt);
+    ws = SortWs();
+    pc.lap(p.bt[7]);
 }
 
 template <class S>
 void build_part(Part& p, const S& src, i64 items, bool symmetric) {
     hipStream_t s = p.ctx->stream;
     p.symmetric = symmetric;
+    const auto t0 = std::chrono::steady_clock::now();
+    PhaseClock pc;
     DevBuf<u32> key, val;
-    const i64 m = filter_into(*p.ctx, src, items, false, p.lo, p.hi, key, val);
+    const i64 m = filter_into(p, src, items, false, p.lo, p.hi, key, val, pc);
     p.nnz_local = m;
     i64 mi = m;
     DevBuf<u32> ikey, ival;
-    if (!symmetric) mi = filter_into(*p.ctx, src, items, true, p.lo, p.hi, ikey, ival);
+    if (!symmetric) mi = filter_into(p, src, items, true, p.lo, p.hi, ikey, ival, pc);
     p.nnz_in_local = mi;
     p.off64 = (u64)std::max(m, mi) > 0xFFFFFFFFull;
-    rows_from_local(p, key, val, m, p.row32, p.row64, p.col);
-    key.release();
-    if (!symmetric) rows_from_local(p, ikey, ival, mi, p.crow32, p.crow64, p.ccol);
+    rows_from_local(p, key, val, m, p.row32, p.row64, p.col, pc);
+    if (!symmetric) rows_from_local(p, ikey, ival, mi, p.crow32, p.crow64, p.ccol, pc);
     // per-solve state
     p.dist.alloc((size_t)std::max<i64>(p.nl, 1));
     p.zmask.alloc((size_t)p.bw);
@@ -689,6 +747,8 @@ void build_part(Part& p, const S& src, i64 items, bool symmetric) {
     else part_zmask_k<u32><<<grid_for(p.bw, 256, 4096), 256, 0, s>>>(part_d<u32>(p), p.nl, p.bw, p.zmask.p);
     PJ_LAUNCH_CHECK();
     PJ_HIP(hipStreamSynchronize(s));
+    pc.lap(p.bt[5]);
+    p.bt[6] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 void part_geometry(Part& p, i64 n, int rank, int world) {
@@ -761,6 +821,8 @@ void part_info(const Part& p, i64* out) {
                     p.qoff.bytes() + p.ctr.bytes() + p.cur.bytes() + p.stat.bytes());
     out[13] = (i64)p.sent.bytes() + (p.steps ? 2 * (i64)p.world * p.bw * 8 + p.bw * 8 : 0);
     out[14] = p.exch_bytes;
+    for (int k = 0; k < 10; ++k)  // build phases: microseconds ([9]: the slowest allocation's MB)
+        out[15 + k] = (i64)std::llround(p.bt[k] * (k == 9 ? 1e3 : 1e6));
 }
 
 void part_zmask(Part& p, u64* out_dev) {

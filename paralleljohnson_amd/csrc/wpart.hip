@@ -15,22 +15,25 @@
 //   light rounds       : relax the frontier's light edges (w < delta). An owned
 //                        target is lowered with atomicMin and joins the next
 //                        frontier when it lands below hi; a remote target's
-//                        candidate is folded into a full-size `cand` array
-//                        (atomicMin) and its `touched` bit set. count: touched
-//                        remote targets per owner; pack (into a send buffer sized
-//                        to that count): every touched remote target once, as
-//                        (id, cand) owner-major —
+//                        (id, candidate) pair is appended by the relax itself to
+//                        the rank's claim queue (64 shards, one counter each).
+//                        count: the queued pairs per owner; pack (into a send
+//                        buffer sized to that count): the pairs owner-major —
 //                        the per-owner send buffers of :537-542 — exchanged with
 //                        all_to_all_single (:522-554); apply: the owner folds the
-//                        received candidates in the same way. A round ends with
-//                        all_reduce(sum) of the new frontier sizes.
+//                        received candidates in the same way (duplicates fold
+//                        into the same atomicMin: the dedup is the owner's).
+//                        A round ends with all_reduce(sum) of the new frontier sizes.
 //   heavy step         : the band's members relax their heavy edges once (same
 //                        relax / pack / exchange / apply).
 //
-// `cand` keeps the best value sent for each remote id during a solve, so a
-// target is re-sent only when this rank improves on it: the send volume of a
-// round is bounded by the distinct remote targets improved (<= block per
-// owner), unlike the reference's unbounded buffers.
+// A direct-mapped cache of the (id, best value) pairs this rank has sent during the
+// solve (2 x block entries: O(block) like the rest of the rank's vertex state) drops a
+// remote relaxation that cannot beat what was already sent for that id. It may forget
+// (a colliding id evicts the entry), which costs only a redundant pair, never a lost
+// one. A round whose pairs overflow a queue shard is run again after the queue grows
+// (the band's members as its frontier, the cache cleared: see wpart_relax); the queue
+// keeps its size for the later rounds and solves.
 // Row segments longer than WP_LONG edges go to a queue relaxed edge-balanced
 // over the whole grid (1024-edge tiles, lb.h).
 #include <algorithm>
@@ -69,7 +72,9 @@ constexpr int ST_CNT = 67;     // selected frontier size
 constexpr int ST_REACH = 68;   // reached vertices, [69] their out-edges
 constexpr int ST_ACC = 72;     // [72, 75): the per-band counts (heavy / light / unsettled edges)
 constexpr int ST_CUR = 75;     // [75, 75 + 64): pack cursors per owner
-constexpr int ST_N = 75 + WP_MAXW;
+constexpr int ST_QMAX = 75 + WP_MAXW;  // the largest claim-queue shard count of the round (> capacity: overflow)
+constexpr int ST_N = ST_QMAX + 1;
+constexpr int WQ_S = 64;       // claim-queue shards (blockIdx % WQ_S), each counter on its own 64-byte line
 
 struct WArgs {
     i64 n, lo, nl, block, bw;
@@ -80,8 +85,11 @@ struct WArgs {
     const u32* w;
     const u32* lsplit;
     int32_t* dist;     // nl
-    int32_t* cand;     // n (world > 1)
-    u64* touched;      // n / 64 words (world > 1)
+    u64* rc;           // (world > 1) sent-pair cache: (id << 32 | best), 2^rcb entries, ~0 = empty
+    u32 rcb;
+    u64* q;            // (world > 1) claim queue: WQ_S shards of qsh pairs (id | cand << 32)
+    u64 qsh;
+    u64* qctr;         // WQ_S counters, 8 words apart
     u64* fr;           // bw
     u64* frn;          // bw
     u64* mb;           // bw
@@ -96,7 +104,51 @@ struct WArgs {
 // marked in the next frontier (returning 1 when this relaxation set the mark: the callers
 // count the marks per thread and add the block's sum to ST_NF once -- an atomicAdd per
 // marked vertex on that one word serialized the light rounds behind its atomic rate); a
-// remote target's candidate is folded into cand and its touched bit set.
+// remote target's (id, candidate) goes to the claim queue unless the sent-pair cache
+// shows a value at least as good already sent for that id.
+
+// the cache slot of id t (multiplicative hash) and its entry (id << 32 | value)
+__device__ __forceinline__ u64* wp_rc_slot(const WArgs& a, u32 t) {
+    return a.rc + (((u32)(t * 0x9E3779B1u)) >> (32 - a.rcb));
+}
+// the best value the cache shows as sent for t (INT_INF: none). Agent-scope accesses: the
+// entries written during the round by other XCDs' lanes are seen (a stale hit is still a
+// value that was sent, so no pair is ever lost; a miss costs one redundant pair).
+__device__ __forceinline__ int32_t wp_rc_get(const WArgs& a, u32 t) {
+    const u64 c = __hip_atomic_load(wp_rc_slot(a, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (u32)(c >> 32) == t ? (int32_t)(u32)c : INT_INF;
+}
+__device__ __forceinline__ void wp_rc_put(const WArgs& a, u32 t, int32_t v) {
+    __hip_atomic_store(wp_rc_slot(a, t), ((u64)t << 32) | (u32)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Appends the pairs (t[j], nd[j]) with app[j] set to the claim queue: one atomic per call
+// for all active lanes (positions from the ballots), in shard blockIdx % WQ_S. A pair past
+// the shard's capacity is not written; the shard counter still counts it, which is how the
+// host sees the overflow (ST_QMAX) and the size the queue needs.
+template <int N>
+__device__ __forceinline__ void wp_append(const WArgs& a, const bool (&app)[N], const u32 (&t)[N],
+                                          const long long (&nd)[N]) {
+    u32 off[N], tot = 0;
+    const u64 lt = lanemask_lt();
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const u64 m = __ballot(app[j]);
+        off[j] = tot + (u32)__popcll(m & lt);
+        tot += (u32)__popcll(m);
+    }
+    if (tot == 0) return;
+    const int leader = __ffsll((long long)__ballot(true)) - 1;
+    u64* ctr = a.qctr + (size_t)(blockIdx.x % WQ_S) * 8;
+    u64 base = 0;
+    if (lane_id() == leader) base = atomicAdd(ctr, (u64)tot);
+    base = __shfl(base, leader, 64);
+    u64* qs = a.q + (size_t)(blockIdx.x % WQ_S) * a.qsh;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const u64 pos = base + off[j];
+        if (app[j] && pos < a.qsh) qs[pos] = (u64)t[j] | ((u64)(u32)(int32_t)nd[j] << 32);
+    }
+}
 
 // WP_PU edges of one source in one step: the target reads of all of them issued before
 // any atomic (one edge at a time is a dependent chain of read, atomicMin and atomicOr per
@@ -128,11 +180,13 @@ __device__ __forceinline__ u32 wp_edges(const WArgs& a, bool light, u64 k, u64 l
     for (int j = 0; j < WP_PU; ++j) {
         const i64 tl = (i64)t[j] - a.lo;
         loc[j] = tl >= 0 && tl < a.nl;
-        cur[j] = !ok[j] ? 0 : (loc[j] ? wp_now(a.dist + tl) : wp_now(a.cand + t[j]));
+        cur[j] = !ok[j] ? 0 : (loc[j] ? wp_now(a.dist + tl) : wp_rc_get(a, t[j]));
     }
     u32 nf = 0;
+    bool app[WP_PU];
 #pragma unroll
     for (int j = 0; j < WP_PU; ++j) {
+        app[j] = false;
         if (!ok[j] || (int32_t)nd[j] >= cur[j]) continue;
         if (loc[j]) {
             const i64 tl = (i64)t[j] - a.lo;
@@ -142,10 +196,11 @@ __device__ __forceinline__ u32 wp_edges(const WArgs& a, bool light, u64 k, u64 l
                 if (!(atomicOr(a.frn + (tl >> 6), bit) & bit)) ++nf;
             }
         } else {
-            atomicMin(a.cand + t[j], (int32_t)nd[j]);
-            atomicOr(a.touched + (t[j] >> 6), 1ull << (t[j] & 63));
+            wp_rc_put(a, t[j], (int32_t)nd[j]);
+            app[j] = true;
         }
     }
+    if (a.q) wp_append<WP_PU>(a, app, t, nd);
     return nf;
 }
 
@@ -170,11 +225,13 @@ __device__ __forceinline__ u32 wp_edges_g(const WArgs& a, bool light, const u32 
     for (int j = 0; j < N; ++j) {
         const i64 tl = (i64)t[j] - a.lo;
         loc[j] = tl >= 0 && tl < a.nl;
-        cur[j] = !ok[j] ? 0 : (loc[j] ? wp_now(a.dist + tl) : wp_now(a.cand + t[j]));
+        cur[j] = !ok[j] ? 0 : (loc[j] ? wp_now(a.dist + tl) : wp_rc_get(a, t[j]));
     }
     u32 nf = 0;
+    bool app[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
+        app[j] = false;
         if (!ok[j] || (int32_t)nd[j] >= cur[j]) continue;
         if (loc[j]) {
             const i64 tl = (i64)t[j] - a.lo;
@@ -184,10 +241,11 @@ __device__ __forceinline__ u32 wp_edges_g(const WArgs& a, bool light, const u32 
                 if (!(atomicOr(a.frn + (tl >> 6), bit) & bit)) ++nf;
             }
         } else {
-            atomicMin(a.cand + t[j], (int32_t)nd[j]);
-            atomicOr(a.touched + (t[j] >> 6), 1ull << (t[j] & 63));
+            wp_rc_put(a, t[j], (int32_t)nd[j]);
+            app[j] = true;
         }
     }
+    if (a.q) wp_append<N>(a, app, t, nd);
     return nf;
 }
 
@@ -401,68 +459,74 @@ __global__ __launch_bounds__(WB) void wp_long_k(WArgs a) {
     if (LIGHT) wp_flush_nf(a, nf, red);
 }
 
-// Touched remote targets per owner -> stat[o] (wave-aggregated: one atomic per
-// (wave, owner)). A lane owns one touched word (64 ids of one owner).
-__global__ __launch_bounds__(WB) void wp_count_k(WArgs a, i64 nwords) {
+// The claim queue's pairs per owner -> stat[o], and the largest shard count -> ST_QMAX
+// (above the shard capacity: the round overflowed). Block b reads shard b % WQ_S, the
+// blocks of a shard stride over its pairs; per wave one LDS add per owner present.
+__device__ __forceinline__ void wp_owner_rank(u32 o, bool ok, u32* cnt, u32* rank_out) {
+    // (wave) lanes with ok grouped by owner o: cnt[o] += group size (LDS), *rank_out = the
+    // lane's rank in its group plus the LDS count before the group's add
+    u64 pending = __ballot(ok);
     const int lane = lane_id();
-    const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
-    for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; w0 < nwords; w0 += nwaves * 64) {
-        const i64 wi = w0 + lane;
-        const u32 cnt = wi < nwords ? (u32)__popcll(a.touched[wi]) : 0u;
-        const int owner = wi < nwords ? (int)((u32)wi / (u32)a.bw) : -1;  // (a block is bw words; wi < 2^26)
-        u64 pending = __ballot(cnt != 0);
-        while (pending) {
-            const int l = __ffsll((long long)pending) - 1;
-            const int o = __shfl(owner, l, 64);
-            const bool mine = cnt != 0 && owner == o;
-            pending &= ~__ballot(mine);
-            const u32 tot = wave_sum(mine ? cnt : 0u);
-            if (lane == l) atomicAdd(&a.stat[o], (u64)tot);
-        }
+    while (pending) {
+        const int l = __ffsll((long long)pending) - 1;
+        const u32 ol = __shfl(o, l, 64);
+        const u64 grp = __ballot(ok && o == ol);
+        pending &= ~grp;
+        u32 b = 0;
+        if (lane == l) b = atomicAdd(&cnt[ol], (u32)__popcll(grp));
+        b = __shfl(b, l, 64);
+        if (ok && o == ol && rank_out) *rank_out = b + (u32)__popcll(grp & lanemask_lt());
     }
 }
+__global__ __launch_bounds__(WB) void wp_qcount_k(WArgs a, int world) {
+    __shared__ u32 h[WP_MAXW];
+    for (int o = threadIdx.x; o < world; o += WB) h[o] = 0;
+    __syncthreads();
+    const u32 sh = blockIdx.x % WQ_S, per = gridDim.x / WQ_S, c = blockIdx.x / WQ_S;
+    const u64 att = a.qctr[(size_t)sh * 8], cnt = min(att, a.qsh);
+    const u64* qs = a.q + (size_t)sh * a.qsh;
+    for (u64 i0 = (u64)c * WB; i0 < cnt; i0 += (u64)per * WB) {
+        const u64 i = i0 + threadIdx.x;
+        const bool ok = i < cnt;
+        const u32 o = ok ? (u32)((u64)(u32)qs[i] / (u64)a.block) : 0u;
+        wp_owner_rank(o, ok, h, nullptr);
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < world; o += WB)
+        if (h[o]) atomicAdd(&a.stat[o], (u64)h[o]);
+    if (c == 0 && threadIdx.x == 0 && att) atomicMax(&a.stat[ST_QMAX], att);
+}
 
-// Pack: touched remote targets -> (id | cand << 32) at their owner's segment of send
-// (segments owner-major, sizes stat[o] from wp_count_k; a cursor per owner). Bits are
-// cleared as read.
-__global__ __launch_bounds__(WB) void wp_pack_k(WArgs a, i64 nwords, int world, u64* __restrict__ send) {
-    const int lane = lane_id();
-    const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
-    for (i64 w0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; w0 < nwords; w0 += nwaves * 64) {
-        const i64 wi = w0 + lane;
-        u64 bits = 0;
-        if (wi < nwords) {
-            bits = a.touched[wi];
-            if (bits) a.touched[wi] = 0;
-        }
-        const u32 cnt = (u32)__popcll(bits);
-        const int owner = wi < nwords ? (int)((u32)wi / (u32)a.bw) : -1;  // (a block is bw words; wi < 2^26)
-        u64 pending = __ballot(cnt != 0);
-        u64 base = 0;
-        while (pending) {  // one atomic per (wave, owner)
-            const int l = __ffsll((long long)pending) - 1;
-            const int o = __shfl(owner, l, 64);
-            const bool mine = cnt != 0 && owner == o;
-            const u64 grp = __ballot(mine);
-            pending &= ~grp;
-            const u32 x = mine ? cnt : 0u;
-            const u32 inc = wave_incl_scan(x);
-            const u32 tot = __shfl(inc, 63, 64);
-            u64 ob = 0;
-            if (lane == l) {
-                ob = atomicAdd(&a.stat[ST_CUR + o], (u64)tot);
-                for (int q = 0; q < o && q < world; ++q) ob += a.stat[q];
+// Pack: the queued pairs at their owner's segment of send (segments owner-major, sizes
+// stat[o] from wp_qcount_k; a cursor per owner, one atomic per block tile and owner).
+// Order inside a segment is free: the owner folds the pairs with atomicMin.
+__global__ __launch_bounds__(WB) void wp_qpack_k(WArgs a, int world, u64* __restrict__ send) {
+    __shared__ u32 h[WP_MAXW];
+    __shared__ u64 base[WP_MAXW];
+    const u32 sh = blockIdx.x % WQ_S, per = gridDim.x / WQ_S, c = blockIdx.x / WQ_S;
+    const u64 cnt = min(a.qctr[(size_t)sh * 8], a.qsh);
+    const u64* qs = a.q + (size_t)sh * a.qsh;
+    for (u64 i0 = (u64)c * WB; i0 < cnt; i0 += (u64)per * WB) {  // (block-uniform)
+        for (int o = threadIdx.x; o < world; o += WB) h[o] = 0;
+        __syncthreads();
+        const u64 i = i0 + threadIdx.x;
+        const bool ok = i < cnt;
+        const u64 x = ok ? qs[i] : 0ull;
+        const u32 o = ok ? (u32)((u64)(u32)x / (u64)a.block) : 0u;
+        u32 r = 0;
+        wp_owner_rank(o, ok, h, &r);
+        __syncthreads();
+        for (int q = threadIdx.x; q < world; q += WB) {
+            u64 b = 0;
+            if (h[q]) {
+                b = atomicAdd(&a.stat[ST_CUR + q], (u64)h[q]);
+                for (int k = 0; k < q; ++k) b += a.stat[k];  // the segment's start
             }
-            ob = __shfl(ob, l, 64);
-            if (mine) base = ob + (inc - x);
+            base[q] = b;
         }
-        u64* out = cnt ? send + base : nullptr;
-        while (bits) {
-            const int bb = __ffsll((long long)bits) - 1;
-            bits &= bits - 1;
-            const u32 t = (u32)(wi * 64 + bb);
-            *out++ = (u64)t | ((u64)(u32)a.cand[t] << 32);
-        }
+        __syncthreads();
+        if (ok) send[base[o] + r] = x;
+        __syncthreads();
     }
 }
 
@@ -892,8 +956,14 @@ struct WPart {
     DevBuf<u32> col, w, lsplit;
     DevBuf<u32> lsplit_alt;        // the other light threshold's prefixes (delta and the tail's are
                                    // used in turn by every solve: each was recomputed per solve)
-    DevBuf<int32_t> dist, cand;
-    DevBuf<u64> touched, fr, frn, mb, stat;
+    DevBuf<int32_t> dist;
+    DevBuf<u64> fr, frn, mb, stat;
+    DevBuf<u64> rc;                // (world > 1) sent-pair cache, 2^rcb entries (>= 2 x block)
+    u32 rcb = 1;
+    DevBuf<u64> q, qctr;           // (world > 1) claim queue, WQ_S shards of qsh pairs, and its counters
+    u64 qsh = 0;
+    i64 qsh_min = -1;              // option "queue_shard": smallest shard capacity (-1 = automatic)
+    bool pending_pack = false;     // the last relax's pairs are queued and not packed yet
     DevBuf<u32> rl_inv;   // (relabeled blocks) old local id -> new local id; empty: input ids
     DevBuf<u64> sb;       // the tail's settled map, world x block bits (engine all-gathers the slices)
     bool sb_on = false;   // sb holds this solve's map (set at the tail switch)
@@ -907,6 +977,7 @@ struct WPart {
     PinnedStat hstat;
     std::unique_ptr<DeltaSteps> steps;  // engine view with its own exchange buffers (lazy)
     unsigned grid() const { return (unsigned)ctx->cu_count * 8u; }
+    unsigned qgrid() const { return (unsigned)WQ_S * std::max(1u, grid() / (unsigned)WQ_S); }  // (shard-major)
     WArgs args(int32_t dlo = 0, int32_t dhi = 0) {
         WArgs a{};
         a.n = n;
@@ -922,8 +993,11 @@ struct WPart {
         a.w = w.p;
         a.lsplit = lsplit.p;
         a.dist = dist.p;
-        a.cand = cand.p;
-        a.touched = touched.p;
+        a.rc = rc.p;
+        a.rcb = rcb;
+        a.q = world > 1 ? q.p : nullptr;
+        a.qsh = qsh;
+        a.qctr = qctr.p;
         a.fr = fr.p;
         a.frn = frn.p;
         a.mb = mb.p;
@@ -950,6 +1024,13 @@ struct WPart {
 void delete_wpart(WPart* p) { delete p; }
 
 namespace {
+
+// the claim queue at shard capacity qsh (pairs), counters cleared
+void wpart_queue(WPart& p, u64 qsh) {
+    p.qsh = std::max<u64>(qsh, 1ull);
+    p.q.alloc((size_t)WQ_S * (size_t)p.qsh);
+    PJ_HIP(hipMemsetAsync(p.qctr.p, 0, p.qctr.bytes(), p.ctx->stream));
+}
 
 u64 weight_sum(const u32* w, i64 m, unsigned grid, hipStream_t s) {
     u64 wsum = 0;
@@ -1028,9 +1109,10 @@ void wpart_cut(WPart* p, const Graph& g, i64 first, double mean_w) {
     p->stat.alloc(ST_N);
     std::fill(p->hstat.p, p->hstat.p + ST_N, 0ull);
     if (p->world > 1) {
-        p->cand.alloc((size_t)std::max<i64>(p->n, 1));
-        p->touched.alloc((size_t)std::max<i64>((p->n + 63) / 64, 1));
-        PJ_HIP(hipMemsetAsync(p->touched.p, 0, p->touched.bytes(), s));
+        while (p->rcb < 31 && ((i64)1 << p->rcb) < std::max<i64>(2 * p->block, 4096)) ++p->rcb;
+        p->rc.alloc((size_t)1 << p->rcb);
+        p->qctr.alloc((size_t)WQ_S * 8);
+        wpart_queue(*p, (u64)std::max<i64>(16, p->block / 1024));  // (grows with the rounds' pairs)
     }
     PJ_HIP(hipStreamSynchronize(s));
 }
@@ -1393,15 +1475,18 @@ void wpart_info(const WPart& p, i64* out) {
     out[7] = p.nnz;
 }
 
-// device bytes of this rank: rows, O(block) vertex state, the N-sized tables (the remote
-// candidates `cand` (int32 per vertex) with their touched bitmap, and the pull rounds'
-// replicated byte map), the exchange buffers (sized to the largest round's traffic)
+// device bytes of this rank: [0] rows; [1] O(block) vertex state, the sent-pair cache
+// (2 x block entries) included; [2] the replicated maps the pulls and the tail all-gather
+// (member / frontier byte maps: N bytes, 2N for the tail's 16-bit map; the settled map:
+// N bits -- the analogue of the BFS pull's replicated visited bitmap); [3] the claim queue
+// and the exchange buffers (sized to the largest round's pairs)
 void wpart_device_bytes(const WPart& p, i64* out4) {
     out4[0] = (i64)(p.row.bytes() + p.col.bytes() + p.w.bytes());
     out4[1] = (i64)(p.lsplit.bytes() + p.lsplit_alt.bytes() + p.dist.bytes() + p.fr.bytes() + p.frn.bytes() +
-                    p.mb.bytes() + p.lq_v.bytes() + p.lq_b.bytes() + p.lq_e.bytes() + p.stat.bytes());
-    out4[2] = (i64)(p.cand.bytes() + p.touched.bytes() + p.mmap.bytes() + p.fmap16.bytes());
-    out4[3] = p.exch_bytes;
+                    p.mb.bytes() + p.lq_v.bytes() + p.lq_b.bytes() + p.lq_e.bytes() + p.stat.bytes() +
+                    p.rc.bytes() + p.qctr.bytes() + p.rl_inv.bytes());
+    out4[2] = (i64)(p.mmap.bytes() + p.fmap16.bytes() + p.sb.bytes());
+    out4[3] = p.exch_bytes + (i64)p.q.bytes();
 }
 
 void wpart_heavy_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
@@ -1551,8 +1636,8 @@ int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
     p.ms_lo = INT_MIN;
     p.fs_lo = p.fs_hi = INT_MIN;
     if (p.nl > 0) PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.dist.p), INT_INF, (size_t)p.nl, s));
-    if (p.world > 1 && p.n > 0)
-        PJ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.cand.p), INT_INF, (size_t)p.n, s));
+    if (p.world > 1) PJ_HIP(hipMemsetAsync(p.rc.p, 0xFF, p.rc.bytes(), s));  // (the sent-pair cache: empty)
+    p.pending_pack = false;
     if (source >= 0 && source < p.n) {
         i64 src = source;
         if (p.rl_inv.p && source >= p.lo && source < p.hi) {  // relabeled block: the source's new id
@@ -1570,6 +1655,7 @@ int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
 
 static void wpart_select_async(WPart& p, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
+    if (p.pending_pack) throw Error(PJ_ERR_STATE, "wpart select: the last relax's pairs were not packed");
     if (p.fs_lo == lo && p.fs_hi == hi) {  // selected by the heavy pull that ended the last band
         p.fs_lo = p.fs_hi = INT_MIN;
         return;
@@ -1588,40 +1674,64 @@ void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2) {
     out2[1] = p.hstat[ST_MIN] >= (u64)INT_INF ? (i64)INT_INF : (i64)p.hstat[ST_MIN];
 }
 
-// Relax the frontier's light (or the members' heavy) edges; counts[o] = the distinct
-// remote targets improved for owner o. send != NULL (room for their sum; world x block
-// always suffices) also packs them (wpart_pack); else the caller packs once it has
-// sized its buffer.
+// Relax the frontier's light (or the members' heavy) edges; counts[o] = the pairs queued
+// for owner o. send != NULL (room for their sum) also packs them (wpart_pack); else the
+// caller packs once it has sized its buffer, before the next step.
+//
+// Overflow: a round whose pairs exceed a queue shard is run again with the queue grown to
+// twice the largest shard count seen. Everything the first run did stays valid (owned
+// targets lowered and marked, ST_NF counting each new mark once); its lost pairs are
+// recovered by relaxing again all of the band's members (light) or again the members'
+// heavy edges, with the sent-pair cache cleared so that no pair is skipped for having
+// been "sent" by the run whose queue was dropped. Redundant work, but only until the
+// queue has grown: it keeps its size.
 void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts) {
     hipStream_t s = p.ctx->stream;
+    if (p.pending_pack) throw Error(PJ_ERR_STATE, "wpart relax: the last relax's pairs were not packed");
     p.clear_stat();
-    const WArgs a = p.args(lo, hi);
-    if (light) wp_relax_k<true><<<p.grid(), WB, 0, s>>>(a);
-    else wp_relax_k<false><<<p.grid(), WB, 0, s>>>(a);
-    PJ_LAUNCH_CHECK();
-    if (light) wp_long_k<true><<<p.grid(), WB, 0, s>>>(a);
-    else wp_long_k<false><<<p.grid(), WB, 0, s>>>(a);
-    PJ_LAUNCH_CHECK();
-    if (p.world > 1) {
-        wp_count_k<<<p.grid(), WB, 0, s>>>(a, (p.n + 63) / 64);
+    for (int attempt = 0;; ++attempt) {
+        if (p.world > 1) PJ_HIP(hipMemsetAsync(p.qctr.p, 0, p.qctr.bytes(), s));
+        const WArgs a = p.args(lo, hi);
+        if (light) wp_relax_k<true><<<p.grid(), WB, 0, s>>>(a);
+        else wp_relax_k<false><<<p.grid(), WB, 0, s>>>(a);
         PJ_LAUNCH_CHECK();
-        p.read_stat();  // (world 1 sends nothing: no host wait here)
+        if (light) wp_long_k<true><<<p.grid(), WB, 0, s>>>(a);
+        else wp_long_k<false><<<p.grid(), WB, 0, s>>>(a);
+        PJ_LAUNCH_CHECK();
+        if (p.world < 2) break;  // (world 1 sends nothing: no host wait here)
+        wp_qcount_k<<<p.qgrid(), WB, 0, s>>>(a, p.world);
+        PJ_LAUNCH_CHECK();
+        p.read_stat();
+        const u64 need = p.hstat[ST_QMAX];
+        if (need <= p.qsh) break;
+        if (attempt > 8) throw Error(PJ_ERR_HIP, "wpart relax: the claim queue keeps overflowing (internal error)");
+        wpart_queue(p, 2 * need);
+        PJ_HIP(hipMemsetAsync(p.rc.p, 0xFF, p.rc.bytes(), s));
+        if (light)  // (the run consumed the frontier into the members: relax all of them again)
+            PJ_HIP(hipMemcpyAsync(p.fr.p, p.mb.p, p.fr.bytes(), hipMemcpyDeviceToDevice, s));
+        // every counter but the marks of the first run (ST_NF)
+        PJ_HIP(hipMemsetAsync(p.stat.p, 0, sizeof(u64) * ST_NF, s));
+        PJ_HIP(hipMemsetAsync(p.stat.p + ST_NF + 1, 0, sizeof(u64) * (ST_N - ST_NF - 1), s));
     }
     for (int o = 0; o < p.world; ++o) counts[o] = p.world > 1 ? (i64)p.hstat[o] : 0;
+    p.pending_pack = p.world > 1;
     if (send) wpart_pack(p, send);
 }
 
-// The touched remote targets as (id | cand << 32), owner-major, into send.
+// The queued pairs (id | cand << 32), owner-major, into send (room for the sum of the
+// last relax's counts).
 void wpart_pack(WPart& p, u64* send) {
     if (p.world < 2) return;
     hipStream_t s = p.ctx->stream;
-    wp_pack_k<<<p.grid(), WB, 0, s>>>(p.args(), (p.n + 63) / 64, p.world, send);
+    wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(p.args(), p.world, send);
     PJ_LAUNCH_CHECK();
     PJ_HIP(hipStreamSynchronize(s));
+    p.pending_pack = false;
 }
 
 void wpart_apply(WPart& p, const u64* recv, i64 nr, int light, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
+    if (p.pending_pack) throw Error(PJ_ERR_STATE, "wpart apply: the last relax's pairs were not packed");
     if (nr > 0) {
         wp_apply_k<<<grid_for(nr, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), recv, nr, light);
         PJ_LAUNCH_CHECK();
@@ -1634,7 +1744,10 @@ void wpart_apply(WPart& p, const u64* recv, i64 nr, int light, int32_t lo, int32
 // marks counted by the round's relax and apply: each vertex once, by the
 // atomicOr's old bit). The round's kernels cleared fr's words as they consumed them,
 // so the two bitmaps trade places with no kernel (wp_swap_k copied and cleared them).
-static void wpart_end_round_async(WPart& p) { std::swap(p.fr, p.frn); }
+static void wpart_end_round_async(WPart& p) {
+    if (p.pending_pack) throw Error(PJ_ERR_STATE, "wpart end_round: the last relax's pairs were not packed");
+    std::swap(p.fr, p.frn);
+}
 
 i64 wpart_end_round(WPart& p) {
     wpart_end_round_async(p);
@@ -1736,6 +1849,17 @@ struct WPartGpuSteps final : DeltaSteps {
 
 const Ctx& wpart_ctx(const WPart& p) { return *p.ctx; }
 int wpart_world(const WPart& p) { return p.world; }
+bool wpart_pending(const WPart& p) { return p.pending_pack; }
+// option "queue_shard": the claim queue's shard capacity in pairs from now on (it grows again
+// when a round overflows it; tests use small values to run the overflow path)
+void wpart_set_queue_shard(WPart& p, i64 pairs) {
+    p.qsh_min = pairs;
+    if (p.world > 1) {
+        p.qsh = 0;
+        wpart_queue(p, (u64)pairs);
+        PJ_HIP(hipStreamSynchronize(p.ctx->stream));
+    }
+}
 
 double* wpart_tail_params(WPart& p) { return p.tail; }
 double& wpart_pull_factor(WPart& p) { return p.pull_factor; }

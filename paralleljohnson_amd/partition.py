@@ -42,7 +42,11 @@ class PartInfo(ctypes.Structure):
     _fields_ = [("n", _I64), ("lo", _I64), ("hi", _I64), ("block", _I64), ("words_per_rank", _I64),
                 ("nnz_local", _I64), ("nnz_in_local", _I64), ("rank", _I32),
                 ("world", _I32), ("symmetric", _I32), ("off64", _I32), ("bytes_rows", _I64),
-                ("bytes_state", _I64), ("bytes_bitmaps", _I64), ("bytes_exchange", _I64)]
+                ("bytes_state", _I64), ("bytes_bitmaps", _I64), ("bytes_exchange", _I64),
+                ("build_us", _I64 * 10)]
+
+BUILD_PHASES = ("enumerate_count_s", "enumerate_write_s", "sort_s", "csr_s", "alloc_s", "state_s", "total_s", "free_s",
+                "slowest_alloc_s", "slowest_alloc_gb")
 
 
 class PartStats(ctypes.Structure):
@@ -225,6 +229,13 @@ class DevicePart:
         return {"rows": info.bytes_rows, "state": info.bytes_state, "bitmaps": info.bytes_bitmaps,
                 "exchange": info.bytes_exchange}
 
+    def build_phases(self) -> dict:
+        """pj_part_info_get's build phases in seconds (BUILD_PHASES)."""
+        info = PartInfo()
+        _check(_lib.pj_part_info_get(self._h, ctypes.byref(info)))
+        return {k: round(info.build_us[i] * (1e-3 if k.endswith("_gb") else 1e-6), 4)  # ([9] is in MB)
+                for i, k in enumerate(BUILD_PHASES)}
+
     def set_option(self, key: str, value: float):
         _check(_lib.pj_part_set_option(self._h, key.encode(), float(value)))
 
@@ -303,14 +314,14 @@ class DeviceWPart:
         self.nl = self.hi - self.lo
 
     def device_bytes(self) -> dict:
-        """pj_wpart_device_bytes: rows, vertex state, N-sized tables, exchange buffers."""
+        """pj_wpart_device_bytes: rows, O(block) vertex state, replicated maps, queue + exchange buffers."""
         out = np.zeros(4, np.int64)
         _check(_lib.pj_wpart_device_bytes(self._h, _ptr(out)))
-        return {"rows": int(out[0]), "state": int(out[1]), "tables": int(out[2]), "exchange": int(out[3])}
+        return {"rows": int(out[0]), "state": int(out[1]), "maps": int(out[2]), "exchange": int(out[3])}
 
     def set_option(self, key: str, value: float):
-        """pj_wpart_set_option: "tail_frac", "tail_mult", "pull_factor", "light_pull" or
-        "tail_light_pull".
+        """pj_wpart_set_option: "tail_frac", "tail_mult", "pull_factor", "light_pull",
+        "tail_light_pull" or "queue_shard" (the claim queue's shard capacity, this rank).
 
         Every rank of a group must set the same values (the ranks take the tail switch and
         the pull decisions from all-reduced counts, and agree once per solve whether every
@@ -532,6 +543,12 @@ class Multi:
         _check(_lib.pj_multi_info(self._h, ctypes.byref(i)))
         return {"n": i.n, "world": i.world, "layout": i.layout, "weighted": bool(i.weighted),
                 "transport": (i.transport or b"").decode()}
+
+    def device_bytes(self, rank: int) -> dict:
+        """pj_multi_device_bytes: rank's rows, O(block) vertex state, replicated maps, exchange."""
+        out = np.zeros(4, np.int64)
+        _check(_lib.pj_multi_device_bytes(self._h, int(rank), _ptr(out)))
+        return {"rows": int(out[0]), "state": int(out[1]), "maps": int(out[2]), "exchange": int(out[3])}
 
     def set_csr_cache(self, path: Optional[str]):
         _check(_lib.pj_multi_set_csr_cache(self._h, None if path is None else os.fsencode(path)))

@@ -412,6 +412,64 @@ def test_wpart_generate_kronecker_blocks(pj, oracle, world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_wpart_claim_queue_overflow(pj, oracle, world):
+    """A light or heavy step whose remote pairs overflow a claim-queue shard runs again on a
+    grown queue (all the band's members as the frontier, the sent-pair cache cleared): with
+    the shard capacity cut to a few pairs before every solve, the gathered distances still
+    equal the oracle Dijkstra, and the queue has grown past what was set."""
+    from paralleljohnson_amd.partition import delta_group, gather_group, load_weighted_kronecker
+    ctxs, comms = _group(pj, world, "host")
+    g0 = ctxs[0].generate_kronecker(12, 16, 9, weighted=True)
+    row, col, wc = g0.get_csr()
+    col = col.view(np.uint32)
+    n = g0.n
+    g0.close()
+    parts = [load_weighted_kronecker(ctxs[r], 12, 16, 9, r, world) for r in range(world)]
+    for cap in (1, 3, 40):
+        for source in (0, n // 3, n - 1):
+            for p in parts:
+                p.set_option("queue_shard", cap)
+            delta_group(parts, comms, source)
+            exp = oracle.dijkstra(row, col, wc, source)
+            assert np.array_equal(gather_group(parts, comms), exp), (cap, world, source)
+        assert max(p.device_bytes()["exchange"] for p in parts) > 64 * 8 * cap
+    with pytest.raises(pj.PJError):
+        parts[0].set_option("queue_shard", 0)
+    for p in parts:
+        p.close()
+
+
+@pytest.mark.gpu
+def test_multi_weighted_partition_state_shrinks(pj, oracle):
+    """pj_multi with a weighted partitioned Kronecker s24 (every rank enumerates the tuples
+    and keeps its block's rows: pj_wpart_generate_kronecker) at world 2, 4 and 8 (ranks
+    sharing the one GPU over the host transport): the per-rank O(block) vertex state --
+    distances, frontier bitmaps, light prefixes, long-row queue, sent-pair cache -- at world
+    8 is at most a third of world 2's, the rows shrink with the world, and the distances
+    equal the single-GPU solver's on the same graph."""
+    from paralleljohnson_amd.partition import Multi
+    ctx = pj.Context(0)
+    g = ctx.generate_kronecker(24, 16, 1, weighted=True)
+    root = int(g.sample_roots(2, 1)[0])
+    exp = g.sssp(root)
+    g.close()
+    ctx.close()
+    state, rows = {}, {}
+    for world in (2, 4, 8):
+        with Multi(world, "host") as m:
+            m.generate_kronecker(24, 16, 1, weighted=True)
+            got, st = m.sssp(root)
+            assert np.array_equal(got, exp), world
+            b = [m.device_bytes(r) for r in range(world)]
+            state[world] = max(x["state"] for x in b)
+            rows[world] = max(x["rows"] for x in b)
+            print(f"world {world}: per-rank bytes {b[0]}")
+    assert state[8] * 3 <= state[2], state
+    assert rows[8] * 3 <= rows[2], rows
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("weighted", [False, True])
 def test_cli_processes_byte_identical(pj, oracle, tmp_path, weighted):
     """`parallel_johnson` at P = 1 (single-GPU solver), P = 2 and 3 (PJ_GPUS: the 1D partition
