@@ -313,6 +313,11 @@ int pj_part_load_coo(pj_ctx* ctx, const int64_t* src, const int64_t* dst, int64_
  * weights; N = max id + 1 as :319). Every rank parses the file on its GPU and
  * keeps its rows, so no rank has to scatter (the reference's :344-410). */
 int pj_part_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_part** out);
+/* All ranks of a one-process group at once (ctxs[world], rank r on ctxs[r]; out[world]):
+ * the file is parsed ONCE, on ctxs[0]'s GPU, and every rank gets only its block's
+ * entries from there (peer copies), then builds its rows -- the reference's rank-0
+ * read and scatter (:313-338, :344-410) with the scatter on the device. */
+int pj_part_load_snap_group(int world, pj_ctx* const* ctxs, const char* path, pj_part** out);
 int pj_part_destroy(pj_part* p);
 int pj_part_info_get(const pj_part* p, pj_part_info* out);
 /* Copy the rank's isolated-vertex mask (words_per_rank u64, device) to
@@ -377,6 +382,9 @@ int pj_wpart_from_graph(pj_graph* g, int rank, int world, pj_wpart** out);
  * pj_load_snap grammar): every rank parses the file on its GPU and keeps only
  * its block's rows, weight-sorted (no whole-graph CSR on any GPU). */
 int pj_wpart_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_wpart** out);
+/* The weighted form of pj_part_load_snap_group: one parse on ctxs[0], each rank's
+ * entries (and the degree keys of the per-block order) copied to its GPU. */
+int pj_wpart_load_snap_group(int world, pj_ctx* const* ctxs, const char* path, pj_wpart** out);
 /* The rank's block of pj_generate_kronecker(scale, edgefactor, seed, weighted = 1):
  * every rank enumerates the generator's tuples on its GPU and keeps only its block's
  * rows (weight-sorted, the same rows as the single-GPU graph's), so the weighted

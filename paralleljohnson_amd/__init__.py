@@ -141,6 +141,8 @@ _SIGS = {
     "pj_wpart_relax": ([_P, _INT, ctypes.c_int32, ctypes.c_int32, _P, _P], _INT),
     "pj_wpart_apply": ([_P, _P, _I64, _INT, ctypes.c_int32, ctypes.c_int32], _INT),
     "pj_wpart_pack": ([_P, _P], _INT),
+    "pj_part_load_snap_group": ([_INT, _P, ctypes.c_char_p, _P], _INT),
+    "pj_wpart_load_snap_group": ([_INT, _P, ctypes.c_char_p, _P], _INT),
     "pj_wpart_end_round": ([_P, _P], _INT),
     "pj_wpart_reach": ([_P, _P], _INT),
     "pj_wpart_copy_dist": ([_P, _P], _INT),

@@ -1215,6 +1215,32 @@ int pj_wpart_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_wp
     });
 }
 
+int pj_wpart_load_snap_group(int world, pj_ctx* const* ctxs, const char* path, pj_wpart** out) {
+    if (!ctxs || !path || !out || world < 1 || world > 64) return arg_error("pj_wpart_load_snap_group: bad argument");
+    for (int r = 0; r < world; ++r) {
+        if (!ctxs[r]) return arg_error("pj_wpart_load_snap_group: a context is NULL");
+        out[r] = nullptr;
+    }
+    return guarded([&] {
+        bind(ctxs[0]->c);
+        DevBuf<uint8_t> text;  // missing file: empty graph, as pj_load_snap (:67)
+        const i64 len = read_file_to_device(ctxs[0]->c, path, text);
+        DevBuf<u32> src, dst, w;
+        ParseResult r = parse_device_text(ctxs[0]->c, text.p, len, true, src, dst, w);
+        text.release();
+        if (r.bad_line) {
+            parse_error(r);
+            return (int)PJ_ERR_PARSE;
+        }
+        std::vector<Ctx*> cs;
+        for (int k = 0; k < world; ++k) cs.push_back(&ctxs[k]->c);
+        std::vector<WPart*> ps = wparts_from_coo_group(cs, src, dst, w, r.nnz, r.max_id + 1);
+        for (int k = 0; k < world; ++k) out[k] = reinterpret_cast<pj_wpart*>(ps[(size_t)k]);
+        bind(ctxs[0]->c);
+        return (int)PJ_OK;
+    });
+}
+
 int pj_wpart_destroy(pj_wpart* p) {
     if (!p) return PJ_OK;
     return guarded([&] {
@@ -1389,6 +1415,32 @@ int pj_part_load_snap(pj_ctx* ctx, const char* path, int rank, int world, pj_par
             return (int)PJ_ERR_PARSE;
         }
         *out = reinterpret_cast<pj_part*>(part_from_coo(ctx->c, src, dst, r.nnz, r.max_id + 1, rank, world, false));
+        return (int)PJ_OK;
+    });
+}
+
+int pj_part_load_snap_group(int world, pj_ctx* const* ctxs, const char* path, pj_part** out) {
+    if (!ctxs || !path || !out || world < 1 || world > 64) return arg_error("pj_part_load_snap_group: bad argument");
+    for (int r = 0; r < world; ++r) {
+        if (!ctxs[r]) return arg_error("pj_part_load_snap_group: a context is NULL");
+        out[r] = nullptr;
+    }
+    return guarded([&] {
+        bind(ctxs[0]->c);
+        DevBuf<uint8_t> text;  // missing file: empty graph, as pj_load_snap (:67)
+        const i64 len = read_file_to_device(ctxs[0]->c, path, text);
+        DevBuf<u32> src, dst, w;
+        ParseResult r = parse_device_text(ctxs[0]->c, text.p, len, false, src, dst, w);
+        text.release();
+        if (r.bad_line) {
+            parse_error(r);
+            return (int)PJ_ERR_PARSE;
+        }
+        std::vector<Ctx*> cs;
+        for (int k = 0; k < world; ++k) cs.push_back(&ctxs[k]->c);
+        std::vector<Part*> ps = parts_from_coo_group(cs, src, dst, r.nnz, r.max_id + 1, false);
+        for (int k = 0; k < world; ++k) out[k] = reinterpret_cast<pj_part*>(ps[(size_t)k]);
+        bind(ctxs[0]->c);
         return (int)PJ_OK;
     });
 }

@@ -199,7 +199,7 @@ int run_multi_source(const char* webfile, const std::vector<int64_t>& sources, c
 int run_partitioned(const char* webfile, int source, const char* out, int P, int weighted) {
     Phases ph;
     pj_multi* m = make_multi(P);
-    // every rank builds its own rows on its GPU: no scatter (:344-410)
+    // rank 0's GPU parses the file once, every rank gets its block's entries (:313-338, :344-410)
     int rc = pj_multi_load_snap(m, webfile, weighted, PJ_LAYOUT_PARTITIONED);
     if (rc != PJ_OK) fail("load", rc);
     pj_multi_info_t mi{};

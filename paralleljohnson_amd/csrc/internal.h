@@ -306,6 +306,8 @@ WPart* wpart_from_graph(Graph& g, int rank, int world);
 WPart* wpart_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, int rank, int world);
 WPart* wpart_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w, i64 nnz, i64 n, int rank,
                       int world);
+std::vector<WPart*> wparts_from_coo_group(const std::vector<Ctx*>& ctxs, DevBuf<u32>& src, DevBuf<u32>& dst,
+                                          DevBuf<u32>& w, i64 nnz, i64 n);
 void wpart_info(const WPart& p, i64* out8);
 int32_t wpart_begin(WPart& p, i64 source, int32_t delta);
 void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2);
@@ -322,6 +324,8 @@ void delete_part(Part* p);
 Part* part_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, int rank, int world);
 Part* part_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, i64 nnz, i64 n, int rank, int world,
                     bool symmetric);
+std::vector<Part*> parts_from_coo_group(const std::vector<Ctx*>& ctxs, DevBuf<u32>& src, DevBuf<u32>& dst, i64 nnz,
+                                        i64 n, bool symmetric);
 void part_info(const Part& p, i64* out);  // n lo hi block bw nnz_local sym off64 rank world nnz_in_local, bytes x4
 void part_zmask(Part& p, u64* out_dev);
 void part_begin(Part& p, i64 source, const u64* iso, u64* vis, i64* out3);

@@ -198,10 +198,9 @@ int pj_multi_load_snap(pj_multi* m, const char* path, int weighted, int layout) 
         if (rc == PJ_OK) {
             m->parts.assign((size_t)P, nullptr);
             m->wparts.assign((size_t)P, nullptr);
-            rc = per_rank(P, [&](int r) {  // every rank builds its own rows: no scatter (:344-410)
-                return weighted ? pj_wpart_load_snap(m->ctxs[(size_t)r], path, r, P, &m->wparts[(size_t)r])
-                                : pj_part_load_snap(m->ctxs[(size_t)r], path, r, P, &m->parts[(size_t)r]);
-            });
+            // one parse on rank 0's GPU, each rank's entries scattered to it (:313-338, :344-410)
+            rc = weighted ? pj_wpart_load_snap_group(P, m->ctxs.data(), path, m->wparts.data())
+                          : pj_part_load_snap_group(P, m->ctxs.data(), path, m->parts.data());
         }
     }
     if (rc != PJ_OK) {

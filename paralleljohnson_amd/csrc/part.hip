@@ -43,6 +43,7 @@
 //          slices before pull levels.
 #include <chrono>
 #include <cmath>
+#include <thread>
 
 #include "kron.h"
 #include "lb.h"
@@ -639,10 +640,11 @@ PartArgs part_args(Part& p, u64* vis) {
     return a;
 }
 
+// (on fctx's stream: the rank's own, or the context that parsed a file for every rank)
 template <class S>
-i64 filter_into(Part& p, const S& src, i64 items, bool by_dst, i64 lo, i64 hi, DevBuf<u32>& key,
+i64 filter_into(Part& p, Ctx& fctx, const S& src, i64 items, bool by_dst, i64 lo, i64 hi, DevBuf<u32>& key,
                 DevBuf<u32>& val, PhaseClock& pc) {
-    hipStream_t s = p.ctx->stream;
+    hipStream_t s = fctx.stream;
     const i64 per = (i64)TB * IPT;
     const i64 nb = (items + per - 1) / per;
     if (nb == 0) {
@@ -708,18 +710,28 @@ void rows_from_local(Part& p, DevBuf<u32>& key, DevBuf<u32>& val, i64 m, DevBuf<
     pc.lap(p.bt[7]);
 }
 
+// The rank's rows from its local COO (key = owned id - lo, in file order): out-rows from
+// (key, val), and for a graph not known symmetric the in-rows from (ikey, ival).
+void build_part_local(Part& p, DevBuf<u32>& key, DevBuf<u32>& val, i64 m, DevBuf<u32>& ikey, DevBuf<u32>& ival,
+                      i64 mi, bool symmetric, PhaseClock& pc, std::chrono::steady_clock::time_point t0);
+
 template <class S>
 void build_part(Part& p, const S& src, i64 items, bool symmetric) {
-    hipStream_t s = p.ctx->stream;
-    p.symmetric = symmetric;
     const auto t0 = std::chrono::steady_clock::now();
     PhaseClock pc;
     DevBuf<u32> key, val;
-    const i64 m = filter_into(p, src, items, false, p.lo, p.hi, key, val, pc);
-    p.nnz_local = m;
+    const i64 m = filter_into(p, *p.ctx, src, items, false, p.lo, p.hi, key, val, pc);
     i64 mi = m;
     DevBuf<u32> ikey, ival;
-    if (!symmetric) mi = filter_into(p, src, items, true, p.lo, p.hi, ikey, ival, pc);
+    if (!symmetric) mi = filter_into(p, *p.ctx, src, items, true, p.lo, p.hi, ikey, ival, pc);
+    build_part_local(p, key, val, m, ikey, ival, mi, symmetric, pc, t0);
+}
+
+void build_part_local(Part& p, DevBuf<u32>& key, DevBuf<u32>& val, i64 m, DevBuf<u32>& ikey, DevBuf<u32>& ival,
+                      i64 mi, bool symmetric, PhaseClock& pc, std::chrono::steady_clock::time_point t0) {
+    hipStream_t s = p.ctx->stream;
+    p.symmetric = symmetric;
+    p.nnz_local = m;
     p.nnz_in_local = mi;
     p.off64 = (u64)std::max(m, mi) > 0xFFFFFFFFull;
     rows_from_local(p, key, val, m, p.row32, p.row64, p.col, pc);
@@ -786,6 +798,88 @@ Part* part_from_kronecker(Ctx& ctx, int scale, int edgefactor, uint64_t seed, in
     ks.pk = make_perm_keys(scale, seed);
     build_part(*p, ks, (i64)ks.M, true);
     return p.release();
+}
+
+// Parse once, scatter (the reference's rank 0 reads the file and scatters row blocks,
+// :313-338, :344-410): the device COO on ctxs[0] is filtered into every rank's piece there
+// (entries whose source, and for the in-rows whose target, the rank owns; file order kept),
+// each piece is copied to its rank's GPU (peer copy, or a device copy on a shared GPU), and
+// every rank builds its rows from its piece alone, the ranks in parallel (one host thread
+// each). The COO is consumed.
+std::vector<Part*> parts_from_coo_group(const std::vector<Ctx*>& ctxs, DevBuf<u32>& src, DevBuf<u32>& dst, i64 nnz,
+                                        i64 n, bool symmetric) {
+    const int world = (int)ctxs.size();
+    Ctx& c0 = *ctxs[0];
+    std::vector<std::unique_ptr<Part>> parts((size_t)world);
+    struct Piece {
+        DevBuf<u32> key, val, ikey, ival;
+        i64 m = 0, mi = 0;
+    };
+    std::vector<Piece> pc_((size_t)world);
+    std::vector<std::chrono::steady_clock::time_point> t0((size_t)world);
+    CooSrc cs;
+    cs.src = src.p;
+    cs.dst = dst.p;
+    cs.n = nnz;
+    for (int r = 0; r < world; ++r) {
+        parts[(size_t)r].reset(new Part());
+        Part& p = *parts[(size_t)r];
+        p.ctx = ctxs[(size_t)r];
+        part_geometry(p, n, r, world);
+        t0[(size_t)r] = std::chrono::steady_clock::now();
+        PhaseClock pc;
+        Piece& q = pc_[(size_t)r];
+        DevBuf<u32> k0, v0, ik0, iv0;
+        PJ_HIP(hipSetDevice(c0.device));
+        q.m = filter_into(p, c0, cs, nnz, false, p.lo, p.hi, k0, v0, pc);
+        q.mi = q.m;
+        if (!symmetric) q.mi = filter_into(p, c0, cs, nnz, true, p.lo, p.hi, ik0, iv0, pc);
+        if (p.ctx == &c0) {
+            q.key = std::move(k0);
+            q.val = std::move(v0);
+            q.ikey = std::move(ik0);
+            q.ival = std::move(iv0);
+            continue;
+        }
+        PJ_HIP(hipSetDevice(p.ctx->device));
+        auto ship = [&](DevBuf<u32>& from, DevBuf<u32>& to, i64 cnt) {
+            to.alloc((size_t)cnt);
+            if (cnt)
+                PJ_HIP(hipMemcpyPeerAsync(to.p, p.ctx->device, from.p, c0.device, sizeof(u32) * (size_t)cnt,
+                                          c0.stream));
+        };
+        ship(k0, q.key, q.m);
+        ship(v0, q.val, q.m);
+        if (!symmetric) {
+            ship(ik0, q.ikey, q.mi);
+            ship(iv0, q.ival, q.mi);
+        }
+        PJ_HIP(hipSetDevice(c0.device));
+        PJ_HIP(hipStreamSynchronize(c0.stream));
+        pc.lap(p.bt[1]);
+    }
+    src.release();
+    dst.release();
+    std::vector<std::exception_ptr> errs((size_t)world);
+    std::vector<std::thread> th;
+    for (int r = 0; r < world; ++r)
+        th.emplace_back([&, r] {
+            try {
+                Part& p = *parts[(size_t)r];
+                PJ_HIP(hipSetDevice(p.ctx->device));
+                Piece& q = pc_[(size_t)r];
+                PhaseClock pc;
+                build_part_local(p, q.key, q.val, q.m, q.ikey, q.ival, q.mi, symmetric, pc, t0[(size_t)r]);
+            } catch (...) {
+                errs[(size_t)r] = std::current_exception();
+            }
+        });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
+    std::vector<Part*> out;
+    for (auto& p : parts) out.push_back(p.release());
+    return out;
 }
 
 Part* part_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, i64 nnz, i64 n, int rank, int world,

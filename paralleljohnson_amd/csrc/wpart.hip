@@ -38,6 +38,7 @@
 // over the whole grid (1024-edge tiles, lb.h).
 #include <algorithm>
 #include <cmath>
+#include <thread>
 
 #include "kron.h"
 #include "lb.h"
@@ -1415,21 +1416,19 @@ WPart* wpart_from_graph(Graph& g, int rank, int world) {
     return p.release();
 }
 
-// The rank's block from device COO (consumed): only the block's rows are sorted and
-// kept, so a rank holds its share of the graph plus the parsed COO while building.
-WPart* wpart_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w, i64 nnz, i64 n, int rank,
-                      int world) {
+namespace {
+// The COO entries whose source lies in [lo, hi), as (source - lo, target, weight) in file
+// order, on ctx's stream; returns their count.
+i64 wp_filter(Ctx& ctx, const DevBuf<u32>& src, const DevBuf<u32>& dst, const DevBuf<u32>& w, i64 nnz, i64 lo,
+              i64 hi, DevBuf<u32>& ls, DevBuf<u32>& ld, DevBuf<u32>& lw) {
     hipStream_t s = ctx.stream;
-    std::unique_ptr<WPart> p = wpart_geometry(&ctx, n, nnz, rank, world);
-    const u64 wsum = weight_sum(w.p, nnz, p->grid(), s);
     const i64 nb = (nnz + 4095) / 4096;
     i64 m = 0;
-    DevBuf<u32> ls, ld, lw;
     if (nb > 0) {
         DevBuf<u32> bcnt((size_t)nb);
         DevBuf<u64> boff((size_t)nb + 1);
         ScanWs ws;
-        wp_filter_count_k<<<(unsigned)nb, 256, 0, s>>>(src.p, nnz, (u32)p->lo, (u32)p->hi, bcnt.p);
+        wp_filter_count_k<<<(unsigned)nb, 256, 0, s>>>(src.p, nnz, (u32)lo, (u32)hi, bcnt.p);
         PJ_LAUNCH_CHECK();
         exclusive_scan_u32(bcnt.p, boff.p, nb, ws, s);
         u64 tot = 0;
@@ -1439,29 +1438,124 @@ WPart* wpart_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>&
         ls.alloc((size_t)std::max<i64>(m, 1));
         ld.alloc((size_t)std::max<i64>(m, 1));
         lw.alloc((size_t)std::max<i64>(m, 1));
-        wp_filter_write_k<<<(unsigned)nb, 256, 0, s>>>(src.p, dst.p, w.p, nnz, (u32)p->lo, (u32)p->hi, boff.p, ls.p,
-                                                       ld.p, lw.p);
+        wp_filter_write_k<<<(unsigned)nb, 256, 0, s>>>(src.p, dst.p, w.p, nnz, (u32)lo, (u32)hi, boff.p, ls.p, ld.p,
+                                                       lw.p);
         PJ_LAUNCH_CHECK();
         PJ_HIP(hipStreamSynchronize(s));
     }
+    return m;
+}
+
+// every vertex's out-degree from the whole COO (the per-block degree order's keys)
+DevBuf<u32> wp_coo_degrees(Ctx& ctx, const DevBuf<u32>& src, i64 nnz, i64 n, unsigned grid) {
     DevBuf<u32> deg;
-    if (PJ_WP_RELABEL && n > 0) {  // every vertex's out-degree, from the whole COO
+    if (PJ_WP_RELABEL && n > 0) {
         deg.alloc((size_t)n);
-        PJ_HIP(hipMemsetAsync(deg.p, 0, deg.bytes(), s));
+        PJ_HIP(hipMemsetAsync(deg.p, 0, deg.bytes(), ctx.stream));
         if (nnz > 0) {
-            wp_deg_coo_k<<<grid_for(nnz, 256, p->grid()), 256, 0, s>>>(src.p, nnz, deg.p);
+            wp_deg_coo_k<<<grid_for(nnz, 256, grid), 256, 0, ctx.stream>>>(src.p, nnz, deg.p);
             PJ_LAUNCH_CHECK();
         }
     }
+    return deg;
+}
+
+// the block's rows from its filtered COO (consumed), then the relabel
+void wp_build_block(WPart& p, DevBuf<u32>& ls, DevBuf<u32>& ld, DevBuf<u32>& lw, i64 m, double mean_w,
+                    DevBuf<u32>& deg) {
+    Graph local;  // the block's rows, local ids, global columns, weight-sorted
+    local.ctx = p.ctx;
+    build_graph_from_coo(local, ls, ld, &lw, m, p.nl, false);
+    wpart_cut(&p, local, 0, mean_w);
+    if (deg.p) wpart_relabel(p, deg);
+}
+}  // namespace
+
+// The rank's block from device COO (consumed): only the block's rows are sorted and
+// kept, so a rank holds its share of the graph plus the parsed COO while building.
+WPart* wpart_from_coo(Ctx& ctx, DevBuf<u32>& src, DevBuf<u32>& dst, DevBuf<u32>& w, i64 nnz, i64 n, int rank,
+                      int world) {
+    hipStream_t s = ctx.stream;
+    std::unique_ptr<WPart> p = wpart_geometry(&ctx, n, nnz, rank, world);
+    const u64 wsum = weight_sum(w.p, nnz, p->grid(), s);
+    DevBuf<u32> ls, ld, lw;
+    const i64 m = wp_filter(ctx, src, dst, w, nnz, p->lo, p->hi, ls, ld, lw);
+    DevBuf<u32> deg = wp_coo_degrees(ctx, src, nnz, n, p->grid());
     src.release();
     dst.release();
     w.release();
-    Graph local;  // the block's rows, local ids, global columns, weight-sorted
-    local.ctx = &ctx;
-    build_graph_from_coo(local, ls, ld, &lw, m, p->nl, false);
-    wpart_cut(p.get(), local, 0, nnz > 0 ? (double)wsum / (double)nnz : 1.0);
-    if (deg.p) wpart_relabel(*p, deg);
+    wp_build_block(*p, ls, ld, lw, m, nnz > 0 ? (double)wsum / (double)nnz : 1.0, deg);
     return p.release();
+}
+
+// Parse once, scatter (the reference's rank 0 reads and scatters, :313-338, :344-410): the
+// device COO on ctxs[0] (consumed) is filtered into every rank's piece there, the pieces and
+// the degree keys of the per-block order are copied to the ranks' GPUs, and every rank builds
+// its block from its piece alone, the ranks in parallel (one host thread each).
+std::vector<WPart*> wparts_from_coo_group(const std::vector<Ctx*>& ctxs, DevBuf<u32>& src, DevBuf<u32>& dst,
+                                          DevBuf<u32>& w, i64 nnz, i64 n) {
+    const int world = (int)ctxs.size();
+    Ctx& c0 = *ctxs[0];
+    PJ_HIP(hipSetDevice(c0.device));
+    std::vector<std::unique_ptr<WPart>> parts((size_t)world);
+    for (int r = 0; r < world; ++r) parts[(size_t)r] = wpart_geometry(ctxs[(size_t)r], n, nnz, r, world);
+    const u64 wsum = weight_sum(w.p, nnz, parts[0]->grid(), c0.stream);
+    const double mean_w = nnz > 0 ? (double)wsum / (double)nnz : 1.0;
+    struct Piece {
+        DevBuf<u32> ls, ld, lw, deg;
+        i64 m = 0;
+    };
+    std::vector<Piece> pc((size_t)world);
+    DevBuf<u32> deg0 = wp_coo_degrees(c0, src, nnz, n, parts[0]->grid());
+    for (int r = 0; r < world; ++r) {
+        WPart& p = *parts[(size_t)r];
+        Piece& q = pc[(size_t)r];
+        PJ_HIP(hipSetDevice(c0.device));
+        DevBuf<u32> ls, ld, lw;
+        q.m = wp_filter(c0, src, dst, w, nnz, p.lo, p.hi, ls, ld, lw);
+        if (p.ctx == &c0) {
+            q.ls = std::move(ls);
+            q.ld = std::move(ld);
+            q.lw = std::move(lw);
+            continue;
+        }
+        PJ_HIP(hipSetDevice(p.ctx->device));
+        auto ship = [&](const DevBuf<u32>& from, DevBuf<u32>& to, i64 cnt) {
+            to.alloc((size_t)std::max<i64>(cnt, 1));
+            if (cnt)
+                PJ_HIP(hipMemcpyPeerAsync(to.p, p.ctx->device, from.p, c0.device, sizeof(u32) * (size_t)cnt,
+                                          c0.stream));
+        };
+        ship(ls, q.ls, q.m);
+        ship(ld, q.ld, q.m);
+        ship(lw, q.lw, q.m);
+        if (deg0.p) ship(deg0, q.deg, n);
+        PJ_HIP(hipSetDevice(c0.device));
+        PJ_HIP(hipStreamSynchronize(c0.stream));
+    }
+    if (deg0.p) pc[0].deg = std::move(deg0);  // (rank 0's context keeps the original)
+    src.release();
+    dst.release();
+    w.release();
+    std::vector<std::exception_ptr> errs((size_t)world);
+    std::vector<std::thread> th;
+    for (int r = 0; r < world; ++r)
+        th.emplace_back([&, r] {
+            try {
+                WPart& p = *parts[(size_t)r];
+                PJ_HIP(hipSetDevice(p.ctx->device));
+                Piece& q = pc[(size_t)r];
+                wp_build_block(p, q.ls, q.ld, q.lw, q.m, mean_w, q.deg);
+            } catch (...) {
+                errs[(size_t)r] = std::current_exception();
+            }
+        });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
+    std::vector<WPart*> out;
+    for (auto& p : parts) out.push_back(p.release());
+    return out;
 }
 
 void wpart_info(const WPart& p, i64* out) {
