@@ -1276,11 +1276,11 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     v2_zero_slot(a, (cin + 2) & 3);
     v2_clear_words(fclr, a.nwords);
     const u64 fcount = v2_slot_sum(a.ctl->cnt[cin]);
-    if (a.rlog && blockIdx.x == 0 && threadIdx.x == 0 && fcount) {  // (debug: round_log)
+    if (a.rlog && blockIdx.x == 0 && threadIdx.x == 0) {  // (debug: round_log; one entry per launch)
         const u64 fe0 = v2_slot_edges(a.ctl->cnt[cin]);
         const u64 i = atomicAdd(a.rlog, 1ull);
         if (i < 255) {
-            a.rlog[1 + 3 * i] = fe0 > pull_thresh ? 2ull : (fcount > dense_min ? 1ull : 0ull);
+            a.rlog[1 + 3 * i] = !fcount ? 3ull : fe0 > pull_thresh ? 2ull : (fcount > dense_min ? 1ull : 0ull);
             a.rlog[2 + 3 * i] = fcount;
             a.rlog[3 + 3 * i] = fe0 | ((u64)a.lo << 40);
         }
@@ -2015,10 +2015,10 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     if (g.round_log) {  // debug: one stderr line per non-empty light round
         std::vector<u64> h(1 + 3 * 255);
         PJ_HIP(hipMemcpy(h.data(), rlog.p, sizeof(u64) * h.size(), hipMemcpyDeviceToHost));
-        static const char* kind[3] = {"push", "dense", "pull"};
+        static const char* kind[4] = {"push", "dense", "pull", "empty"};
         for (u64 i = 0; i < std::min<u64>(h[0], 255); ++i)
             fprintf(stderr, "round %llu lo %llu %s frontier %llu light_edges %llu\n", (unsigned long long)i,
-                    (unsigned long long)(h[3 + 3 * i] >> 40), kind[h[1 + 3 * i] % 3], (unsigned long long)h[2 + 3 * i],
+                    (unsigned long long)(h[3 + 3 * i] >> 40), kind[h[1 + 3 * i] % 4], (unsigned long long)h[2 + 3 * i],
                     (unsigned long long)(h[3 + 3 * i] & ((1ull << 40) - 1)));
     }
 }
