@@ -1779,7 +1779,15 @@ void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2) {
 // heavy edges, with the sent-pair cache cleared so that no pair is skipped for having
 // been "sent" by the run whose queue was dropped. Redundant work, but only until the
 // queue has grown: it keeps its size.
+static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts,
+                             DevBuf<u64>* pre);
 void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts) {
+    wpart_relax_impl(p, light, lo, hi, send, counts, nullptr);
+}
+// pre != NULL (the engine's send buffer): grown to the queue's capacity and packed right
+// behind the count kernel, before the one host wait of the step (no second wait to pack)
+static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts,
+                             DevBuf<u64>* pre) {
     hipStream_t s = p.ctx->stream;
     if (p.pending_pack) throw Error(PJ_ERR_STATE, "wpart relax: the last relax's pairs were not packed");
     p.clear_stat();
@@ -1795,6 +1803,11 @@ void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* co
         if (p.world < 2) break;  // (world 1 sends nothing: no host wait here)
         wp_qcount_k<<<p.qgrid(), WB, 0, s>>>(a, p.world);
         PJ_LAUNCH_CHECK();
+        if (pre) {  // (pairs past a shard's capacity are not packed: an overflow reruns anyway)
+            pre->ensure((size_t)WQ_S * (size_t)p.qsh);
+            wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(a, p.world, pre->p);
+            PJ_LAUNCH_CHECK();
+        }
         p.read_stat();
         const u64 need = p.hstat[ST_QMAX];
         if (need <= p.qsh) break;
@@ -1808,7 +1821,7 @@ void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* co
         PJ_HIP(hipMemsetAsync(p.stat.p + ST_NF + 1, 0, sizeof(u64) * (ST_N - ST_NF - 1), s));
     }
     for (int o = 0; o < p.world; ++o) counts[o] = p.world > 1 ? (i64)p.hstat[o] : 0;
-    p.pending_pack = p.world > 1;
+    p.pending_pack = p.world > 1 && !pre;
     if (send) wpart_pack(p, send);
 }
 
@@ -1890,22 +1903,19 @@ struct WPartGpuSteps final : DeltaSteps {
         recv = recv_b.p;
     }
     void exchange_buffers(i64 nsend, i64 nrecv) override {
-        if ((size_t)nsend > send_b.n) {
-            send_b.ensure((size_t)nsend + (size_t)nsend / 4);
-            send = send_b.p;
-        }
+        (void)nsend;  // (relax packed the pairs into send_b already)
         if ((size_t)nrecv > recv_b.n) {
             recv_b.ensure((size_t)nrecv + (size_t)nrecv / 4);
             recv = recv_b.p;
         }
         p.exch_bytes = (i64)(send_b.bytes() + recv_b.bytes());
-        wpart_pack(p, send_b.p);
     }
     hipStream_t stream() override { return p.ctx->stream; }
     int32_t begin(i64 source, int32_t delta) override { return wpart_begin(p, source, delta); }
     void select(int32_t lo, int32_t hi, i64* out2) override { wpart_select(p, lo, hi, out2); }
     void relax(int light, int32_t lo, int32_t hi, i64* counts) override {
-        wpart_relax(p, light, lo, hi, nullptr, counts);
+        wpart_relax_impl(p, light, lo, hi, nullptr, counts, p.world > 1 ? &send_b : nullptr);
+        send = send_b.p;
     }
     void apply(i64 nr, int light, int32_t lo, int32_t hi) override { wpart_apply(p, recv_b.p, nr, light, lo, hi); }
     i64 end_round() override { return wpart_end_round(p); }

@@ -409,9 +409,10 @@ def test_wpart_generate_kronecker_blocks(pj, oracle, world):
             sent = [max(a, x["sent"]) for a, x in zip(sent, st)]
         for p in parts:
             b = p.device_bytes()
-            # send / recv buffers of at most 2n pairs, and the claim queue: 64 shards of at most
-            # twice the largest shard count of a round (<= the pairs the rank sent in a solve)
-            assert b["rows"] > 0 and b["exchange"] <= 8 * (2 * n + 64 * max(16, 2 * sent[p.rank])), (b, sent)
+            # the receive buffer (at most 2n pairs), the claim queue (64 shards of at most twice the
+            # largest shard count of a round, <= the pairs the rank sent in a solve) and the send
+            # buffer the engine packs into (the queue's capacity)
+            assert b["rows"] > 0 and b["exchange"] <= 8 * (2 * n + 2 * 64 * max(16, 2 * sent[p.rank])), (b, sent)
             p.close()
 
 

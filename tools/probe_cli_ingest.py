@@ -5,6 +5,7 @@ partitioned load parses the file once on rank 0's GPU and scatters each rank its
 (pj_part_load_snap_group); before, every rank parsed the whole file.
 Usage: python tools/probe_cli_ingest.py [scale=22] [reps=2]"""
 import os
+import re
 import subprocess
 import sys
 import tempfile
@@ -30,8 +31,8 @@ with tempfile.TemporaryDirectory() as td:
             wall = time.perf_counter() - t
             if r.returncode != 0:
                 raise SystemExit(f"P={P} failed: {r.stderr[-800:]}")
-            ph = {ln.split()[1].rstrip(":"): float(ln.split()[2]) for ln in r.stderr.splitlines()
-                  if ln.startswith("phase ")}
+            ph = {m.group(1): float(m.group(2)) for m in (re.match(r"phase (.+): ([0-9.e+-]+) s", ln)
+                                                          for ln in r.stderr.splitlines()) if m}
             print(f"rep {rep} P={P}: wall {wall:.3f} s, phases {ph}, {r.stdout.strip()}", flush=True)
         same = [open(os.path.join(td, f"sol{P}.txt"), "rb").read() for P in (1, 2, 3)]
         print(f"rep {rep}: sol_files identical across P: {same[0] == same[1] == same[2]}", flush=True)
