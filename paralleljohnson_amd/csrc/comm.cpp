@@ -15,6 +15,9 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <chrono>
 #include <thread>
 
@@ -56,38 +59,53 @@ struct ThreadGroup {
     int world;
     std::mutex mu;
     std::condition_variable cv;
-    int arrived = 0;
-    u64 gen = 0;
-    bool failed = false;
+    std::atomic<int> arrived{0};
+    std::atomic<u64> gen{0};
+    std::atomic<bool> failed{false};
     std::vector<i64> red;                 // world x k allreduce slots
     std::vector<const void*> ptr;         // per rank: published buffer
     std::vector<const i64*> cnt;          // per rank: published host counts
     std::vector<int> dev;                 // per rank: device
     explicit ThreadGroup(int w) : world(w), ptr((size_t)w), cnt((size_t)w), dev((size_t)w, -1) {}
 
+    // Spins for up to ~200 us before it sleeps on the condition variable: a collective step
+    // of the band loop waits for its peer for tens of microseconds, and a futex wake-up costs
+    // about as much again per barrier (round 5: 7 barriers per light round over the host
+    // transport). The ranks are threads of one process on a CPU share of >= 16 cores.
     void barrier() {
-        std::unique_lock<std::mutex> lk(mu);
-        if (failed) throw Error(PJ_ERR_COMM, "a peer rank of the thread group failed");
-        const u64 g = gen;
-        if (++arrived == world) {
-            arrived = 0;
-            ++gen;
+        if (failed.load(std::memory_order_acquire))
+            throw Error(PJ_ERR_COMM, "a peer rank of the thread group failed");
+        const u64 g = gen.load(std::memory_order_acquire);
+        if (arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == world) {
+            arrived.store(0, std::memory_order_relaxed);
+            gen.store(g + 1, std::memory_order_release);
+            { std::lock_guard<std::mutex> lk(mu); }  // (a sleeper sees the new generation or is notified)
             cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return gen != g || failed; });
-            if (failed) throw Error(PJ_ERR_COMM, "a peer rank of the thread group failed");
+            return;
         }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int spin = 0; gen.load(std::memory_order_acquire) == g; ++spin) {
+            if (failed.load(std::memory_order_acquire))
+                throw Error(PJ_ERR_COMM, "a peer rank of the thread group failed");
+            if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != g || failed.load(); });
+                break;
+            }
+        }
+        if (gen.load(std::memory_order_acquire) == g && failed.load())
+            throw Error(PJ_ERR_COMM, "a peer rank of the thread group failed");
     }
     void abort() {
-        std::lock_guard<std::mutex> lk(mu);
-        failed = true;
+        failed.store(true, std::memory_order_release);
+        { std::lock_guard<std::mutex> lk(mu); }
         cv.notify_all();
     }
     // after every rank has left the failed collective (the caller joined the rank threads)
     void reset() {
         std::lock_guard<std::mutex> lk(mu);
-        failed = false;
-        arrived = 0;
+        failed.store(false);
+        arrived.store(0);
     }
 };
 
