@@ -73,8 +73,9 @@ constexpr int ST_CNT = 67;     // selected frontier size
 constexpr int ST_REACH = 68;   // reached vertices, [69] their out-edges
 constexpr int ST_ACC = 72;     // [72, 75): the per-band counts (heavy / light / unsettled edges)
 constexpr int ST_CUR = 75;     // [75, 75 + 64): pack cursors per owner
-constexpr int ST_QMAX = 75 + WP_MAXW;  // the largest claim-queue shard count of the round (> capacity: overflow)
-constexpr int ST_N = ST_QMAX + 1;
+constexpr int ST_QTOT = 75 + WP_MAXW;  // pairs the round tried to queue (all shards)
+constexpr int ST_QSP = ST_QTOT + 1;     // of them, pairs that went to the spill region (> its capacity: overflow)
+constexpr int ST_N = ST_QSP + 1;
 constexpr int WQ_S = 64;       // claim-queue shards (blockIdx % WQ_S), each counter on its own 64-byte line
 
 struct WArgs {
@@ -88,9 +89,9 @@ struct WArgs {
     int32_t* dist;     // nl
     u64* rc;           // (world > 1) sent-pair cache: (id << 32 | best), 2^rcb entries, ~0 = empty
     u32 rcb;
-    u64* q;            // (world > 1) claim queue: WQ_S shards of qsh pairs (id | cand << 32)
-    u64 qsh;
-    u64* qctr;         // WQ_S counters, 8 words apart
+    u64* q;            // (world > 1) claim queue: WQ_S shards of qsh pairs (id | cand << 32), then
+    u64 qsh, qsp;      // the spill region of qsp pairs
+    u64* qctr;         // WQ_S + 1 counters (the shards', the spill's), 8 words apart
     u64* fr;           // bw
     u64* frn;          // bw
     u64* mb;           // bw
@@ -123,9 +124,11 @@ __device__ __forceinline__ void wp_rc_put(const WArgs& a, u32 t, int32_t v) {
     __hip_atomic_store(wp_rc_slot(a, t), ((u64)t << 32) | (u32)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Appends the pairs (t[j], nd[j]) with app[j] set to the claim queue: one atomic per call
-// for all active lanes (positions from the ballots), in shard blockIdx % WQ_S. A pair past
-// the shard's capacity is not written; the shard counter still counts it, which is how the
-// host sees the overflow (ST_QMAX) and the size the queue needs.
+// for all active lanes (positions from the ballots), in shard blockIdx % WQ_S. Pairs past
+// the shard's capacity go to the spill region (a second atomic, only then), so the queue is
+// sized by the round's total pairs, not by its fullest shard. A pair past the spill's
+// capacity is not written; the spill counter still counts it, which is how the host sees the
+// overflow (ST_QSP > qsp).
 template <int N>
 __device__ __forceinline__ void wp_append(const WArgs& a, const bool (&app)[N], const u32 (&t)[N],
                                           const long long (&nd)[N]) {
@@ -144,11 +147,38 @@ __device__ __forceinline__ void wp_append(const WArgs& a, const bool (&app)[N], 
     if (lane_id() == leader) base = atomicAdd(ctr, (u64)tot);
     base = __shfl(base, leader, 64);
     u64* qs = a.q + (size_t)(blockIdx.x % WQ_S) * a.qsh;
+    if (base + tot <= a.qsh) {  // (wave-uniform: the usual case)
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (app[j]) qs[base + off[j]] = (u64)t[j] | ((u64)(u32)(int32_t)nd[j] << 32);
+        return;
+    }
+    u32 soff[N], stot = 0;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        const u64 pos = base + off[j];
-        if (app[j] && pos < a.qsh) qs[pos] = (u64)t[j] | ((u64)(u32)(int32_t)nd[j] << 32);
+        const bool sp = app[j] && base + off[j] >= a.qsh;
+        const u64 m = __ballot(sp);
+        soff[j] = stot + (u32)__popcll(m & lt);
+        stot += (u32)__popcll(m);
     }
+    u64 sbase = 0;
+    if (stot && lane_id() == leader) sbase = atomicAdd(a.qctr + (size_t)WQ_S * 8, (u64)stot);
+    sbase = __shfl(sbase, leader, 64);
+    u64* qp = a.q + (size_t)WQ_S * a.qsh;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        if (!app[j]) continue;
+        const u64 x = (u64)t[j] | ((u64)(u32)(int32_t)nd[j] << 32);
+        const u64 pos = base + off[j];
+        if (pos < a.qsh) qs[pos] = x;
+        else if (sbase + soff[j] < a.qsp) qp[sbase + soff[j]] = x;
+    }
+}
+// region r of the claim queue (r < WQ_S: a shard, r == WQ_S: the spill): its pairs and count
+__device__ __forceinline__ const u64* wp_qregion(const WArgs& a, u32 r, u64& cnt) {
+    const u64 c = a.qctr[(size_t)r * 8];
+    cnt = r < (u32)WQ_S ? min(c, a.qsh) : min(c, a.qsp);
+    return a.q + (size_t)r * a.qsh;
 }
 
 // WP_PU edges of one source in one step: the target reads of all of them issued before
@@ -460,9 +490,10 @@ __global__ __launch_bounds__(WB) void wp_long_k(WArgs a) {
     if (LIGHT) wp_flush_nf(a, nf, red);
 }
 
-// The claim queue's pairs per owner -> stat[o], and the largest shard count -> ST_QMAX
-// (above the shard capacity: the round overflowed). Block b reads shard b % WQ_S, the
-// blocks of a shard stride over its pairs; per wave one LDS add per owner present.
+// The claim queue's pairs per owner -> stat[o]; the pairs tried (ST_QTOT) and spilled
+// (ST_QSP, above the spill's capacity: the round overflowed). Block b reads region
+// b % (WQ_S + 1) (the shards, then the spill), the blocks of a region stride over its pairs;
+// per wave one LDS add per owner present.
 __device__ __forceinline__ void wp_owner_rank(u32 o, bool ok, u32* cnt, u32* rank_out) {
     // (wave) lanes with ok grouped by owner o: cnt[o] += group size (LDS), *rank_out = the
     // lane's rank in its group plus the LDS count before the group's add
@@ -483,9 +514,10 @@ __global__ __launch_bounds__(WB) void wp_qcount_k(WArgs a, int world) {
     __shared__ u32 h[WP_MAXW];
     for (int o = threadIdx.x; o < world; o += WB) h[o] = 0;
     __syncthreads();
-    const u32 sh = blockIdx.x % WQ_S, per = gridDim.x / WQ_S, c = blockIdx.x / WQ_S;
-    const u64 att = a.qctr[(size_t)sh * 8], cnt = min(att, a.qsh);
-    const u64* qs = a.q + (size_t)sh * a.qsh;
+    const u32 sh = blockIdx.x % (WQ_S + 1), per = gridDim.x / (WQ_S + 1), c = blockIdx.x / (WQ_S + 1);
+    const u64 att = a.qctr[(size_t)sh * 8];
+    u64 cnt;
+    const u64* qs = wp_qregion(a, sh, cnt);
     for (u64 i0 = (u64)c * WB; i0 < cnt; i0 += (u64)per * WB) {
         const u64 i = i0 + threadIdx.x;
         const bool ok = i < cnt;
@@ -495,7 +527,7 @@ __global__ __launch_bounds__(WB) void wp_qcount_k(WArgs a, int world) {
     __syncthreads();
     for (int o = threadIdx.x; o < world; o += WB)
         if (h[o]) atomicAdd(&a.stat[o], (u64)h[o]);
-    if (c == 0 && threadIdx.x == 0 && att) atomicMax(&a.stat[ST_QMAX], att);
+    if (c == 0 && threadIdx.x == 0 && att) atomicAdd(&a.stat[sh < (u32)WQ_S ? ST_QTOT : ST_QSP], att);
 }
 
 // Pack: the queued pairs at their owner's segment of send (segments owner-major, sizes
@@ -504,9 +536,9 @@ __global__ __launch_bounds__(WB) void wp_qcount_k(WArgs a, int world) {
 __global__ __launch_bounds__(WB) void wp_qpack_k(WArgs a, int world, u64* __restrict__ send) {
     __shared__ u32 h[WP_MAXW];
     __shared__ u64 base[WP_MAXW];
-    const u32 sh = blockIdx.x % WQ_S, per = gridDim.x / WQ_S, c = blockIdx.x / WQ_S;
-    const u64 cnt = min(a.qctr[(size_t)sh * 8], a.qsh);
-    const u64* qs = a.q + (size_t)sh * a.qsh;
+    const u32 sh = blockIdx.x % (WQ_S + 1), per = gridDim.x / (WQ_S + 1), c = blockIdx.x / (WQ_S + 1);
+    u64 cnt;
+    const u64* qs = wp_qregion(a, sh, cnt);
     for (u64 i0 = (u64)c * WB; i0 < cnt; i0 += (u64)per * WB) {  // (block-uniform)
         for (int o = threadIdx.x; o < world; o += WB) h[o] = 0;
         __syncthreads();
@@ -961,8 +993,8 @@ struct WPart {
     DevBuf<u64> fr, frn, mb, stat;
     DevBuf<u64> rc;                // (world > 1) sent-pair cache, 2^rcb entries (>= 2 x block)
     u32 rcb = 1;
-    DevBuf<u64> q, qctr;           // (world > 1) claim queue, WQ_S shards of qsh pairs, and its counters
-    u64 qsh = 0;
+    DevBuf<u64> q, qctr;           // (world > 1) claim queue: WQ_S shards of qsh pairs + a spill of qsp, and
+    u64 qsh = 0, qsp = 0;          // the counters
     i64 qsh_min = -1;              // option "queue_shard": smallest shard capacity (-1 = automatic)
     bool pending_pack = false;     // the last relax's pairs are queued and not packed yet
     DevBuf<u32> rl_inv;   // (relabeled blocks) old local id -> new local id; empty: input ids
@@ -978,7 +1010,10 @@ struct WPart {
     PinnedStat hstat;
     std::unique_ptr<DeltaSteps> steps;  // engine view with its own exchange buffers (lazy)
     unsigned grid() const { return (unsigned)ctx->cu_count * 8u; }
-    unsigned qgrid() const { return (unsigned)WQ_S * std::max(1u, grid() / (unsigned)WQ_S); }  // (shard-major)
+    unsigned qgrid() const {  // (region-major: the shards and the spill)
+        return (unsigned)(WQ_S + 1) * std::max(1u, grid() / (unsigned)(WQ_S + 1));
+    }
+    u64 qcap() const { return (u64)WQ_S * qsh + qsp; }
     WArgs args(int32_t dlo = 0, int32_t dhi = 0) {
         WArgs a{};
         a.n = n;
@@ -998,6 +1033,7 @@ struct WPart {
         a.rcb = rcb;
         a.q = world > 1 ? q.p : nullptr;
         a.qsh = qsh;
+        a.qsp = qsp;
         a.qctr = qctr.p;
         a.fr = fr.p;
         a.frn = frn.p;
@@ -1026,10 +1062,11 @@ void delete_wpart(WPart* p) { delete p; }
 
 namespace {
 
-// the claim queue at shard capacity qsh (pairs), counters cleared
-void wpart_queue(WPart& p, u64 qsh) {
+// the claim queue at shard capacity qsh and spill capacity qsp (pairs), counters cleared
+void wpart_queue(WPart& p, u64 qsh, u64 qsp) {
     p.qsh = std::max<u64>(qsh, 1ull);
-    p.q.alloc((size_t)WQ_S * (size_t)p.qsh);
+    p.qsp = std::max<u64>(qsp, 1ull);
+    p.q.alloc((size_t)p.qcap());
     PJ_HIP(hipMemsetAsync(p.qctr.p, 0, p.qctr.bytes(), p.ctx->stream));
 }
 
@@ -1112,8 +1149,9 @@ void wpart_cut(WPart* p, const Graph& g, i64 first, double mean_w) {
     if (p->world > 1) {
         while (p->rcb < 31 && ((i64)1 << p->rcb) < std::max<i64>(2 * p->block, 4096)) ++p->rcb;
         p->rc.alloc((size_t)1 << p->rcb);
-        p->qctr.alloc((size_t)WQ_S * 8);
-        wpart_queue(*p, (u64)std::max<i64>(16, p->block / 1024));  // (grows with the rounds' pairs)
+        p->qctr.alloc((size_t)(WQ_S + 1) * 8);
+        const u64 q0 = (u64)std::max<i64>(16, p->block / 1024);  // (grows with the rounds' pairs)
+        wpart_queue(*p, q0, WQ_S * q0 / 2);
     }
     PJ_HIP(hipStreamSynchronize(s));
 }
@@ -1804,15 +1842,17 @@ static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* s
         wp_qcount_k<<<p.qgrid(), WB, 0, s>>>(a, p.world);
         PJ_LAUNCH_CHECK();
         if (pre) {  // (pairs past a shard's capacity are not packed: an overflow reruns anyway)
-            pre->ensure((size_t)WQ_S * (size_t)p.qsh);
+            pre->ensure((size_t)p.qcap());
             wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(a, p.world, pre->p);
             PJ_LAUNCH_CHECK();
         }
         p.read_stat();
-        const u64 need = p.hstat[ST_QMAX];
-        if (need <= p.qsh) break;
+        if (p.hstat[ST_QSP] <= p.qsp) break;
         if (attempt > 8) throw Error(PJ_ERR_HIP, "wpart relax: the claim queue keeps overflowing (internal error)");
-        wpart_queue(p, 2 * need);
+        // shards at 1.25 x the round's average, the spill at half the round's pairs (a rerun
+        // tries more pairs than the run it repeats: it may overflow once more)
+        const u64 tot = p.hstat[ST_QTOT];
+        wpart_queue(p, std::max<u64>(p.qsh, (tot / WQ_S) * 5 / 4 + 16), std::max<u64>(p.qsp, tot / 2 + 4096));
         PJ_HIP(hipMemsetAsync(p.rc.p, 0xFF, p.rc.bytes(), s));
         if (light)  // (the run consumed the frontier into the members: relax all of them again)
             PJ_HIP(hipMemcpyAsync(p.fr.p, p.mb.p, p.fr.bytes(), hipMemcpyDeviceToDevice, s));
@@ -1959,8 +1999,8 @@ bool wpart_pending(const WPart& p) { return p.pending_pack; }
 void wpart_set_queue_shard(WPart& p, i64 pairs) {
     p.qsh_min = pairs;
     if (p.world > 1) {
-        p.qsh = 0;
-        wpart_queue(p, (u64)pairs);
+        p.qsh = p.qsp = 0;
+        wpart_queue(p, (u64)pairs, (u64)pairs);
         PJ_HIP(hipStreamSynchronize(p.ctx->stream));
     }
 }
