@@ -396,7 +396,7 @@ int pj_wpart_destroy(pj_wpart* p);
 /* out[8] = (n, lo, hi, block, nnz_local, world, rank, nnz of the whole graph) */
 int pj_wpart_info(const pj_wpart* p, int64_t* out);
 /* out[4] = this rank's device bytes: its rows; the O(block) vertex state (with the
- * sent-pair cache, 2 x block entries); the replicated maps the pulls and the tail
+ * sent-pair cache, block entries); the replicated maps the pulls and the tail
  * all-gather (N bytes, 2N for the tail's 16-bit frontier map, N bits for the
  * settled map: the analogue of the BFS pull's visited bitmap); the claim queue and
  * the exchange buffers, sized to the largest round's pairs. Building a block with

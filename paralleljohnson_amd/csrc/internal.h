@@ -40,6 +40,13 @@ void set_error(const std::string& msg);
 #define PJ_LAUNCH_CHECK() PJ_HIP(hipGetLastError())
 
 // ------------------------------------------------------------ device memory --
+// Device allocations of DevBuf. Blocks of 1 GiB and more are kept by a process-wide cache
+// when freed and handed out again (devmem.cpp): the partitioned builds allocate and free
+// tens of GB of sort temporaries, and a hipMalloc that has to take fresh device memory
+// from the driver took seconds for one 17-34 GB block (round 5, the bench's partition legs).
+void* dev_alloc(size_t bytes);
+void dev_free(void* p, size_t bytes);
+
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
@@ -57,11 +64,11 @@ struct DevBuf {
     void alloc(size_t count) {
         release();
         n = count;
-        if (count) PJ_HIP(hipMalloc(&p, count * sizeof(T)));
+        if (count) p = static_cast<T*>(dev_alloc(count * sizeof(T)));
     }
     void ensure(size_t count) { if (count > n) alloc(count); }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) dev_free(p, n * sizeof(T));
         p = nullptr;
         n = 0;
     }

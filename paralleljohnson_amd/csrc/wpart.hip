@@ -28,7 +28,7 @@
 //                        relax / pack / exchange / apply).
 //
 // A direct-mapped cache of the (id, best value) pairs this rank has sent during the
-// solve (2 x block entries: O(block) like the rest of the rank's vertex state) drops a
+// solve (block entries: O(block) like the rest of the rank's vertex state) drops a
 // remote relaxation that cannot beat what was already sent for that id. It may forget
 // (a colliding id evicts the entry), which costs only a redundant pair, never a lost
 // one. A round whose pairs overflow a queue shard is run again after the queue grows
@@ -991,7 +991,7 @@ struct WPart {
                                    // used in turn by every solve: each was recomputed per solve)
     DevBuf<int32_t> dist;
     DevBuf<u64> fr, frn, mb, stat;
-    DevBuf<u64> rc;                // (world > 1) sent-pair cache, 2^rcb entries (>= 2 x block)
+    DevBuf<u64> rc;                // (world > 1) sent-pair cache, 2^rcb entries (>= block)
     u32 rcb = 1;
     DevBuf<u64> q, qctr;           // (world > 1) claim queue: WQ_S shards of qsh pairs + a spill of qsp, and
     u64 qsh = 0, qsp = 0;          // the counters
@@ -1147,10 +1147,11 @@ void wpart_cut(WPart* p, const Graph& g, i64 first, double mean_w) {
     p->stat.alloc(ST_N);
     std::fill(p->hstat.p, p->hstat.p + ST_N, 0ull);
     if (p->world > 1) {
-        while (p->rcb < 31 && ((i64)1 << p->rcb) < std::max<i64>(2 * p->block, 4096)) ++p->rcb;
+        while (p->rcb < 31 && ((i64)1 << p->rcb) < std::max<i64>(p->block, 4096)) ++p->rcb;
         p->rc.alloc((size_t)1 << p->rcb);
         p->qctr.alloc((size_t)(WQ_S + 1) * 8);
-        const u64 q0 = (u64)std::max<i64>(16, p->block / 1024);  // (grows with the rounds' pairs)
+        // (grows with the rounds' pairs; a rerun costs a round, so start at a block / 8 pairs)
+        const u64 q0 = (u64)std::max<i64>(16, p->block / 512);
         wpart_queue(*p, q0, WQ_S * q0 / 2);
     }
     PJ_HIP(hipStreamSynchronize(s));
@@ -1849,10 +1850,10 @@ static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* s
         p.read_stat();
         if (p.hstat[ST_QSP] <= p.qsp) break;
         if (attempt > 8) throw Error(PJ_ERR_HIP, "wpart relax: the claim queue keeps overflowing (internal error)");
-        // shards at 1.25 x the round's average, the spill at half the round's pairs (a rerun
-        // tries more pairs than the run it repeats: it may overflow once more)
+        // shards at twice the round's average, the spill at the round's pairs (a rerun tries more
+        // pairs than the run it repeats: it may overflow once more)
         const u64 tot = p.hstat[ST_QTOT];
-        wpart_queue(p, std::max<u64>(p.qsh, (tot / WQ_S) * 5 / 4 + 16), std::max<u64>(p.qsp, tot / 2 + 4096));
+        wpart_queue(p, std::max<u64>(p.qsh, 2 * (tot / WQ_S) + 16), std::max<u64>(p.qsp, tot + 4096));
         PJ_HIP(hipMemsetAsync(p.rc.p, 0xFF, p.rc.bytes(), s));
         if (light)  // (the run consumed the frontier into the members: relax all of them again)
             PJ_HIP(hipMemcpyAsync(p.fr.p, p.mb.p, p.fr.bytes(), hipMemcpyDeviceToDevice, s));

@@ -409,11 +409,11 @@ def test_wpart_generate_kronecker_blocks(pj, oracle, world):
             sent = [max(a, x["sent"]) for a, x in zip(sent, st)]
         for p in parts:
             b = p.device_bytes()
-            # the receive buffer (at most 2n pairs), the claim queue (shards at 1.25 x a round's
-            # average, a spill of half its pairs, <= the pairs the rank sent in a solve, beyond the
+            # the receive buffer (at most 2n pairs), the claim queue (shards at twice a round's
+            # average, a spill of its pairs, <= the pairs the rank sent in a solve, beyond the
             # initial 96 x 16 + 4096) and the send buffer the engine packs into (the queue's capacity)
             q0 = 96 * 16 + 4096 + 16 * 64
-            assert b["rows"] > 0 and b["exchange"] <= 8 * (2 * n + 2 * (1.75 * sent[p.rank] + q0)), (b, sent)
+            assert b["rows"] > 0 and b["exchange"] <= 8 * (2 * n + 2 * (3 * sent[p.rank] + q0)), (b, sent)
             p.close()
 
 
