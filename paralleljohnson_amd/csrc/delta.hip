@@ -91,12 +91,6 @@ __device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
     return s.e64[k];
 }
 
-// PJ_V2_LAZY: the light relaxations mark the next frontier with returnless atomicOr and
-// count nothing; a count kernel after the round's hub launch sums the frontier bitmap
-// (vertices and their light edges, exactly what the marks counted) into the ring slot.
-#ifndef PJ_V2_LAZY
-#define PJ_V2_LAZY 0
-#endif
 // PJ_V2_NOFIN (1: light pulls, 2: light and heavy pulls): a pull takes its candidate from
 // every in-neighbour u with dist[u] < hi, one dist probe, instead of first testing u's bit
 // in the round's frontier (light) or the band's members (heavy) and reading dist[u] only for
@@ -437,12 +431,6 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
         mk[j] = LIGHT && imp && (int32_t)nd[j] < a.hi;
     }
     if (!LIGHT) return 0u;
-    if (PJ_V2_LAZY) {  // returnless marks; v2_count_k counts the round's frontier afterwards
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (mk[j]) atomicOr(fout + (t[j] >> 6), 1ull << (t[j] & 63));
-        return 0u;
-    }
     u32 newc = 0;
 #pragma unroll
     for (int j = 0; j < N; ++j)
@@ -1279,9 +1267,7 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
             const int32_t old = atomicMin(a.dist + v, cur);
             if (cur < old && cur < hi) {
                 const u64 bit = 1ull << (v & 63);
-                if (PJ_V2_LAZY) {
-                    atomicOr(fout + (v >> 6), bit);
-                } else if (!(atomicOr(fout + (v >> 6), bit) & bit)) {
+                if (!(atomicOr(fout + (v >> 6), bit) & bit)) {
                     ++newc;
                     fe += ls;
                 }
@@ -1337,31 +1323,8 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     u64 fe = 0, mh = 0, ml = 0;
     if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe);
     v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml);
-    if (!PJ_V2_LAZY) v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+    v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
     v2_flush2(mh, ml, a.ctl->mh, red);
-}
-
-// (PJ_V2_LAZY) the round's new frontier (fout after the round and hub launches): its
-// vertices and their light edges into count slot cout. A wave screens 64 words, then reads
-// the light-prefix lengths of each nonzero word's 64 vertices with one coalesced load.
-__global__ __launch_bounds__(DB) void v2_count_k(V2Args a, const u64* __restrict__ fout, int cout) {
-    __shared__ u64 red[DB / WAVE];
-    const int lane = lane_id();
-    u64 c = 0, e = 0;
-    for (i64 w0 = ((i64)blockIdx.x * (DB / WAVE) + wave_id()) * 64; w0 < a.nwords;
-         w0 += (i64)gridDim.x * (DB / WAVE) * 64) {
-        const u64 wd = w0 + lane < a.nwords ? fout[w0 + lane] : 0ull;
-        c += (u64)__popcll(wd);
-        u64 nz = __ballot(wd != 0);
-        while (nz) {
-            const int l = __ffsll((long long)nz) - 1;
-            nz &= nz - 1;
-            const u64 x = __shfl(wd, l, 64);
-            const i64 v = (w0 + l) * 64 + lane;
-            if ((x >> lane) & 1ull) e += a.lsplit[v];
-        }
-    }
-    v2_flush2(c, e, a.ctl->cnt[cout], red);
 }
 
 // (PJ_V2_FMAP) before light round r: undoes the frontier byte map round r - 1 built (its
@@ -1961,10 +1924,6 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                     PJ_LAUNCH_CHECK();
                     v2_hub_k<true><<<hubgrid, DB, 0, s>>>(a, fout, cs, hr, (hr + 1) % 3);
                     PJ_LAUNCH_CHECK();
-                    if (PJ_V2_LAZY) {
-                        v2_count_k<<<roundgrid, DB, 0, s>>>(a, fout, (cs + 1) & 3);
-                        PJ_LAUNCH_CHECK();
-                    }
                     fi = (fi + 1) % 3;
                     cs = (cs + 1) & 3;
                     hr = (hr + 1) % 3;
