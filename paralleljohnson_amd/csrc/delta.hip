@@ -101,23 +101,24 @@ __device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
 #ifndef PJ_V2_NOFIN
 #define PJ_V2_NOFIN 2
 #endif
-// PJ_V2_FMAP: the light pull rounds probe a byte map of the round's frontier (dist - lo of
-// a frontier vertex at the round's start, 0xFF otherwise; n bytes instead of the 4n of
-// dist, so 4x the entries per cache line and L2), built by v2_fmap_k before the round and
-// undone by the next round's v2_fmap_k. Round-start values are exact enough: a frontier
-// vertex lowered during the round is marked into the next frontier and relaxes again.
-#ifndef PJ_V2_FMAP
-#define PJ_V2_FMAP 0
+// PJ_V2_FBDEN > 0: a light pull round whose frontier holds fewer than n / PJ_V2_FBDEN
+// vertices probes the frontier bitmap first after all (n / 8 bytes, cache-resident, and
+// mostly clear bits then: one probe of it instead of the dist line for most in-edges)
+#ifndef PJ_V2_FBDEN
+#define PJ_V2_FBDEN 0
 #endif
-// the candidate distance u offers through a pulled edge (INT_INF = none): fm != null probes
-// the frontier byte map (PJ_V2_FMAP), bits == null dist[u] alone (PJ_V2_NOFIN), else u's bit
-// first
+// PJ_V2_HBDEN > 0: the same for a heavy pull whose band members hold fewer than
+// nnz / PJ_V2_HBDEN edges (their member bitmap is probed first)
+#ifndef PJ_V2_HBDEN
+#define PJ_V2_HBDEN 0
+#endif
+// the candidate distance u offers through a pulled edge (INT_INF = none): bits == null
+// probes dist[u] alone (PJ_V2_NOFIN), else u's bit first. (Round 5: a per-round byte map of
+// the frontier's distances, dist - lo, probed instead of dist -- the map 4x denser in the
+// caches, built and undone by a kernel per round -- measured 7% slower: the pull rounds
+// gained 5% and the build launches cost more; removed, profiles/r05/ab_fmap_r5h.txt.)
 __device__ __forceinline__ int32_t pull_src(const u64* __restrict__ bits, const int32_t* __restrict__ dist, u32 u,
-                                            int32_t hi, const uint8_t* __restrict__ fm = nullptr, int32_t lo = 0) {
-    if (fm) {
-        const uint8_t m = fm[u];
-        return m != 0xFF ? lo + (int32_t)m : INT_INF;
-    }
+                                            int32_t hi) {
     if (!bits) {
         const int32_t d = dist[u];
         return d < hi ? d : INT_INF;
@@ -127,7 +128,7 @@ __device__ __forceinline__ int32_t pull_src(const u64* __restrict__ bits, const 
 template <typename Off, typename E>
 __device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __restrict__ dist,
                                                  const u64* __restrict__ fin, Off& k, Off lim, int32_t lo,
-                                                 int32_t hi, int32_t& cur, const uint8_t* __restrict__ fm = nullptr) {
+                                                 int32_t hi, int32_t& cur) {
     u32 w[PU], u[PU];
     bool ok[PU];
 #pragma unroll
@@ -146,13 +147,7 @@ __device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __re
         nv += ok[j];
     }
     int32_t du[PU];
-    if (fm) {
-        uint8_t m[PU];
-#pragma unroll
-        for (int j = 0; j < PU; ++j) m[j] = ok[j] ? fm[u[j]] : (uint8_t)0xFF;
-#pragma unroll
-        for (int j = 0; j < PU; ++j) du[j] = m[j] != 0xFF ? lo + (int32_t)m[j] : INT_INF;
-    } else if (!fin) {
+    if (!fin) {
 #pragma unroll
         for (int j = 0; j < PU; ++j) du[j] = ok[j] ? dist[u[j]] : INT_INF;
 #pragma unroll
@@ -291,7 +286,6 @@ struct V2Ctl {
     V2Line mh[V2_NSH];      // heavy edges of this band's members
     V2Line minv[V2_NSH];    // min dist >= lo of the last select / pull (next band search), per shard
     V2Line dbg[8];          // PJ_V2_STATS builds: vertices, edges, atomics, marks, hub edges
-    V2Line fmb[2];          // (PJ_V2_FMAP) round r's v2_fmap_k built the frontier byte map: fmb[r & 1]
 };
 #ifndef PJ_V2_PSTATS
 #define PJ_V2_PSTATS 0  // debug build: heavy-pull scan-length counters (printed per solve)
@@ -329,7 +323,6 @@ struct V2Args {
     u64* hoff;   // [3][hcap]
     u64 hcap;
     u64* rlog;   // round_log option: [0] = rounds logged, then (kind, frontier, its light edges) per round
-    const uint8_t* fm;  // (PJ_V2_FMAP) the light pull rounds' frontier byte map, or null
 };
 // the light edges of a band round (light CSR, or the light prefixes of cw in the tail)
 __device__ __forceinline__ ESrc v2_cw_src(const V2Args& a) {
@@ -919,13 +912,13 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fo
 // them), counts them into slot cout and folds min{new dist >= hi} into minv.
 template <typename Off>
 __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fout,
-                                                int32_t nhi, int cout) {
+                                                int32_t nhi, int cout, bool hbits) {
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
     __shared__ u64 red[NWV];
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    const u64* hmb = PJ_V2_NOFIN >= 2 ? nullptr : a.mb;
+    const u64* hmb = (PJ_V2_NOFIN >= 2 && !hbits) ? nullptr : a.mb;
     u32* newb = s_new[wave_id()];
     u32 ccount = 0;
     u64 fe = 0;
@@ -1084,11 +1077,11 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
 template <typename Off>
 __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* __restrict__ row,
                                                    const u64* __restrict__ fin, u64* __restrict__ fout, u32* newb,
-                                                   u32& newc, u64& fe, u64& mh, u64& ml) {
+                                                   u32& newc, u64& fe, u64& mh, u64& ml, bool fbits) {
     constexpr int NWV = DB / WAVE;
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
+    const u64* lfin = (PJ_V2_NOFIN && !fbits) ? nullptr : fin;
     const i64 nsc = (a.nwords + PSC - 1) / PSC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
         const i64 gbase = sc * PSC;
@@ -1161,7 +1154,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             bool go = act && k < lim, done = !act || k >= e;
             while (__ballot(go)) {
                 if (go) {
-                    if (pull_step_fin_cw<Off>(v2_light_src(a), a.dist, lfin, k, lim, lo, hi, cur, a.fm)) {
+                    if (pull_step_fin_cw<Off>(v2_light_src(a), a.dist, lfin, k, lim, lo, hi, cur)) {
                         done = true;
                         go = false;
                     } else {
@@ -1184,7 +1177,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
                     int32_t cand = INT_INF;
                     if (!stop) {
-                        const int32_t du = pull_src(lfin, a.dist, (u32)x, hi, a.fm, lo);
+                        const int32_t du = pull_src(lfin, a.dist, (u32)x, hi);
                         if (du < INT_INF) {
                             const long long nd = (long long)du + w;
                             cand = nd < INT_INF ? (int32_t)nd : INT_INF;
@@ -1227,10 +1220,10 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
 // atomicMin (the vertex's chunks run in different waves).
 __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __restrict__ fin, u64* __restrict__ fout,
                                                   const u32* __restrict__ lcv, const u32* __restrict__ lcc, u64 nlc,
-                                                  u32& newc, u64& fe) {
+                                                  u32& newc, u64& fe, bool fbits) {
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
+    const u64* lfin = (PJ_V2_NOFIN && !fbits) ? nullptr : fin;
     for (u64 it = (u64)blockIdx.x * (DB / WAVE) + wave_id(); it < nlc; it += (u64)gridDim.x * (DB / WAVE)) {
         const u32 v = lcv[it];
         const int32_t d0 = dist_now(a.dist + v);
@@ -1249,7 +1242,7 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
             const bool stop = !valid || (long long)lo + w >= (long long)cur;
             int32_t cand = INT_INF;
             if (!stop) {
-                const int32_t du = pull_src(lfin, a.dist, (u32)x, hi, a.fm, lo);
+                const int32_t du = pull_src(lfin, a.dist, (u32)x, hi);
                 if (du < INT_INF) {
                     const long long nd = (long long)du + w;
                     cand = nd < INT_INF ? (int32_t)nd : INT_INF;
@@ -1321,39 +1314,11 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     }
     u32 newc = 0;
     u64 fe = 0, mh = 0, ml = 0;
-    if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe);
-    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml);
+    const bool fbits = PJ_V2_FBDEN > 0 && fcount * (u64)PJ_V2_FBDEN < (u64)a.n;
+    if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe, fbits);
+    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml, fbits);
     v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
     v2_flush2(mh, ml, a.ctl->mh, red);
-}
-
-// (PJ_V2_FMAP) before light round r: undoes the frontier byte map round r - 1 built (its
-// input bitmap fprev is still intact: round r's kernel clears it) and, when round r will
-// pull (the round kernel's own rule on the same counters), builds it from fin: fm[v] = dist[v]
-// - lo for the frontier, 0xFF elsewhere. A vertex in both keeps its new value.
-__global__ __launch_bounds__(DB) void v2_fmap_k(V2Args a, const u64* __restrict__ fin, const u64* __restrict__ fprev,
-                                                int cin, u64 pull_thresh, int rpar, uint8_t* __restrict__ fm) {
-    const u64 fcount = v2_slot_sum(a.ctl->cnt[cin]);
-    const bool build = fcount && v2_slot_edges(a.ctl->cnt[cin]) > pull_thresh;
-    const bool undo = a.ctl->fmb[rpar ^ 1].v != 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->fmb[rpar].v = build ? 1ull : 0ull;
-    if (!build && !undo) return;
-    const int lane = lane_id();
-    for (i64 w0 = ((i64)blockIdx.x * (DB / WAVE) + wave_id()) * 64; w0 < a.nwords;
-         w0 += (i64)gridDim.x * (DB / WAVE) * 64) {
-        const bool in = w0 + lane < a.nwords;
-        const u64 cw = (build && in) ? fin[w0 + lane] : 0ull;
-        const u64 pw = (undo && in) ? fprev[w0 + lane] : 0ull;
-        u64 nz = __ballot((cw | pw) != 0);
-        while (nz) {
-            const int l = __ffsll((long long)nz) - 1;
-            nz &= nz - 1;
-            const u64 c = __shfl(cw, l, 64), q = __shfl(pw, l, 64);
-            const i64 v = (w0 + l) * 64 + lane;
-            if ((c >> lane) & 1ull) fm[v] = (uint8_t)(a.dist[v] - a.lo);
-            else if ((q >> lane) & 1ull) fm[v] = 0xFF;
-        }
-    }
 }
 
 // static chunk list of the long light rows: count, then append (order is irrelevant)
@@ -1505,7 +1470,6 @@ struct DeltaSolve {
     DevBuf<int32_t> out_own;
     DevBuf<u64> f[3], mb;      // light-round frontier ring (v2_clear_words), band members
     DevBuf<u64> sb;            // settled-before-the-tail bitmap
-    DevBuf<uint8_t> fm;        // (PJ_V2_FMAP) the light pull rounds' frontier byte map
     DevBuf<V2Ctl> ctl;
     V2Ctl* hctl = nullptr;     // mapped pinned host copy, written by v2_publish_k
     V2Ctl* hctl_dev = nullptr;
@@ -1759,7 +1723,6 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     v.f[2].alloc(nw);
     v.mb.alloc(nw);
     v.sb.alloc(nw);
-    if (PJ_V2_FMAP) v.fm.alloc(n ? (size_t)n : 1);
     v.ctl.alloc(1);
     v.hcap = (u64)std::max<i64>(1, std::min<i64>(n, g.nnz / (i64)V2_HT + 1));
     v.hv.alloc(3 * v.hcap);  // the hub queue's ring of three slots
@@ -1873,7 +1836,6 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
         v2_init_k<<<grid_for(n, 256, maxgrid), 256, 0, s>>>(v.dist, n, nwords, (valid && ls < n) ? ls : -1,
                                                             v.f[0].p, v.f[1].p, v.mb.p, v.ctl.p);
         PJ_LAUNCH_CHECK();
-        if (PJ_V2_FMAP) PJ_HIP(hipMemsetAsync(v.fm.p, 0xFF, (size_t)n, s));
     }
     if (valid && ls < n) {
         int cs = 0, hr = 0, fi = 0;
@@ -1911,13 +1873,6 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                     u64* fin = v.f[fi].p;
                     u64* fout = v.f[(fi + 1) % 3].p;
                     u64* fclr = v.f[(fi + 2) % 3].p;
-                    if (PJ_V2_FMAP) {  // (the byte map only for bands up to 255 wide, not in the tail)
-                        const bool fm_ok = !tail && bw <= 255;
-                        a.fm = fm_ok ? v.fm.p : nullptr;
-                        v2_fmap_k<<<roundgrid, DB, 0, s>>>(a, fin, fclr, cs, fm_ok ? pull_thresh : ~0ull,
-                                                           (int)(st.relax_rounds & 1), v.fm.p);
-                        PJ_LAUNCH_CHECK();
-                    }
                     // one launch decides pull / tile-dense push / sparse push on the device
                     v2_pull_round_k<Off><<<roundgrid, DB, 0, s>>>(a, row, fin, fout, cs, pull_thresh, w.lcv.p,
                                                                  w.lcc.p, w.nlc, hr, dense_min, fclr);
@@ -1984,7 +1939,8 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             }
             const bool pull_now = can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh;
             if (pull_now) {
-                v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi_t, cs);
+                const bool hbits = PJ_V2_HBDEN > 0 && (double)(mh + ml) * PJ_V2_HBDEN < (double)g.nnz;
+                v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi_t, cs, hbits);
                 PJ_LAUNCH_CHECK();
                 PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 st.bu_levels++;

@@ -1,9 +1,9 @@
 // devmem.cpp — DevBuf's device allocations, with a process-wide cache of big blocks.
 //
 // A block of 1 GiB or more that is freed is kept (up to a third of the device's memory)
-// and handed out again to a later request of at most its size and at least half of it, on
-// the same device. Reason (round 5, bench.py's partition legs): the partitioned builds
-// allocate and free tens of GB of sort temporaries per rank, and the one hipMalloc per
+// and handed out again to a later request of at most its size and at least 4/9 of it, on
+// the same device (a world-2 build's blocks fit in a world-1 build's, about twice their
+// size). Reason (round 5, bench.py's partition legs): the partitioned builds allocate and free tens of GB of sort temporaries per rank, and the one hipMalloc per
 // build that had to take fresh memory from the driver took 2.7-5.2 s for a 17-34 GB block
 // (profiles/r05: the build phases' slowest allocation); from the cache it is free. A
 // request that fails with the cache holding blocks empties the cache and tries again, so
@@ -63,7 +63,7 @@ void* dev_alloc(size_t bytes) {
     size_t best = (size_t)-1;
     for (size_t i = 0; i < c.free_blocks.size(); ++i) {
         const auto& b = c.free_blocks[i];
-        if (b.dev == dev && b.bytes >= bytes && b.bytes / 2 <= bytes &&
+        if (b.dev == dev && b.bytes >= bytes && b.bytes <= bytes / 4 * 9 &&
             (best == (size_t)-1 || b.bytes < c.free_blocks[best].bytes))
             best = i;
     }

@@ -1150,8 +1150,9 @@ void wpart_cut(WPart* p, const Graph& g, i64 first, double mean_w) {
         while (p->rcb < 31 && ((i64)1 << p->rcb) < std::max<i64>(p->block, 4096)) ++p->rcb;
         p->rc.alloc((size_t)1 << p->rcb);
         p->qctr.alloc((size_t)(WQ_S + 1) * 8);
-        // (grows with the rounds' pairs; a rerun costs a round, so start at a block / 8 pairs)
-        const u64 q0 = (u64)std::max<i64>(16, p->block / 512);
+        // (grows with the rounds' pairs; a rerun costs a round, so start at block / 4 pairs over
+        // the shards and block / 8 as spill)
+        const u64 q0 = (u64)std::max<i64>(16, p->block / 256);
         wpart_queue(*p, q0, WQ_S * q0 / 2);
     }
     PJ_HIP(hipStreamSynchronize(s));

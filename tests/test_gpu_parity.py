@@ -637,10 +637,10 @@ def test_partitioned_weighted_s22_world2(ctx, pj):
     # the (id, candidate) exchange follows the traffic, not world x block regions (round 3: 24 N
     # bytes per rank): the claim queue and the send buffer packed from it (each at most twice a
     # round's pairs over the shards plus once as spill, <= the solve's pairs, beyond their initial
-    # 96 x block / 512 pairs) and the receive buffer (x1.25 growth slack)
+    # 96 x block / 256 pairs) and the receive buffer (x1.25 growth slack)
     for p in parts:
         b = p.device_bytes()
-        q0 = 96 * max(16, p.block // 512) + 4096 + 16 * 64
+        q0 = 96 * max(16, p.block // 256) + 4096 + 16 * 64
         assert 0 < b["exchange"] <= 8 * (2 * (3 * sent + q0) + 1.25 * sent * world), (b, sent)
         assert b["exchange"] < 24 * (1 << 22) / 4, b
     row, col, w = gs[0].get_csr()
