@@ -71,6 +71,12 @@ int pj_destroy(pj_ctx* ctx);
 void* pj_stream(pj_ctx* ctx);
 const char* pj_last_error(void);
 const char* pj_version(void);
+/* Device blocks of 1 GiB or more that libpj freed stay cached in the process (up to half
+ * of the device's memory) and serve later big allocations whole or in slices: a fresh
+ * allocation of memory just returned to the driver waits for it to be cleared (seconds
+ * for tens of GB). This returns every wholly free cached block to the driver, e.g.
+ * before the caller allocates large buffers of its own; *released (may be NULL) = bytes. */
+int pj_trim_device_cache(int64_t* released);
 
 /* ---- graph ingestion (replaces read_webgraph :66-105 + coord2csr :117-159) */
 

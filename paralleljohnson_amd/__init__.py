@@ -84,6 +84,7 @@ _SIGS = {
     "pj_stream": ([_P], _P),
     "pj_last_error": ([], ctypes.c_char_p),
     "pj_version": ([], ctypes.c_char_p),
+    "pj_trim_device_cache": ([_P], _INT),
     "pj_load_snap": ([_P, ctypes.c_char_p, _INT, _PP], _INT),
     "pj_load_snap_buffer": ([_P, ctypes.c_char_p, _I64, _INT, _PP], _INT),
     "pj_load_coo": ([_P, _P, _P, _P, _I64, _I64, _PP], _INT),
@@ -195,6 +196,14 @@ def _ptr(a: Optional[np.ndarray]):
 
 def version() -> str:
     return _lib.pj_version().decode()
+
+
+def trim_device_cache() -> int:
+    """Return libpj's cached free device blocks (>= 1 GiB each) to the driver; bytes
+    released (pj_trim_device_cache)."""
+    r = ctypes.c_int64(0)
+    _check(_lib.pj_trim_device_cache(ctypes.byref(r)))
+    return int(r.value)
 
 
 def cli_path() -> str:

@@ -351,6 +351,14 @@ const char* pj_last_error(void) { return g_err.c_str(); }
 
 const char* pj_version(void) { return "libpj 0.1 (gfx950)"; }
 
+int pj_trim_device_cache(int64_t* released) {
+    return guarded([&] {
+        const size_t r = dev_trim();
+        if (released) *released = (int64_t)r;
+        return PJ_OK;
+    });
+}
+
 int pj_device_count(int* out) {
     if (!out) return arg_error("pj_device_count: out is NULL");
     int count = 0;

@@ -62,16 +62,24 @@ struct ThreadGroup {
     std::atomic<int> arrived{0};
     std::atomic<u64> gen{0};
     std::atomic<bool> failed{false};
-    std::vector<i64> red;                 // world x k allreduce slots
+    std::vector<i64> red;                 // world x k allreduce slots (k > kslot)
     std::vector<const void*> ptr;         // per rank: published buffer
     std::vector<const i64*> cnt;          // per rank: published host counts
     std::vector<int> dev;                 // per rank: device
-    explicit ThreadGroup(int w) : world(w), ptr((size_t)w), cnt((size_t)w), dev((size_t)w, -1) {}
+    // two banks of world x kslot slots for the one-barrier allreduce / count exchange: the
+    // collectives alternate banks, and a bank is written again only after every rank has
+    // passed the barrier of the collective in between, so after it has read the bank
+    int kslot;
+    std::vector<i64> bank[2];
+    explicit ThreadGroup(int w) : world(w), ptr((size_t)w), cnt((size_t)w), dev((size_t)w, -1), kslot(std::max(8, w)) {
+        bank[0].assign((size_t)w * (size_t)kslot, 0);
+        bank[1].assign((size_t)w * (size_t)kslot, 0);
+    }
 
     // Spins for up to ~200 us before it sleeps on the condition variable: a collective step
     // of the band loop waits for its peer for tens of microseconds, and a futex wake-up costs
     // about as much again per barrier (round 5: 7 barriers per light round over the host
-    // transport). The ranks are threads of one process on a CPU share of >= 16 cores.
+    // transport, 4 since the one-barrier allreduce and count exchange). The ranks are threads of one process on a CPU share of >= 16 cores.
     void barrier() {
         if (failed.load(std::memory_order_acquire))
             throw Error(PJ_ERR_COMM, "a peer rank of the thread group failed");
@@ -112,9 +120,25 @@ struct ThreadGroup {
 struct ThreadComm final : Comm {
     std::shared_ptr<ThreadGroup> g;
     int device = -1;
+    u64 seq = 0;  // slot collectives so far (the same on every rank): the bank of the next one
     const char* kind() const override { return "host"; }
 
     void allreduce(i64* v, int k, bool is_min, hipStream_t) override {
+        if (k <= g->kslot) {  // one barrier: publish into this collective's bank, then reduce
+            i64* b = g->bank[seq++ & 1].data();
+            const size_t K = (size_t)g->kslot;
+            std::copy(v, v + k, b + (size_t)rank * K);
+            g->barrier();
+            for (int j = 0; j < k; ++j) {
+                i64 a = b[(size_t)j];
+                for (int q = 1; q < world; ++q) {
+                    const i64 x = b[(size_t)q * K + (size_t)j];
+                    a = is_min ? std::min(a, x) : a + x;
+                }
+                v[j] = a;
+            }
+            return;
+        }
         {
             std::lock_guard<std::mutex> lk(g->mu);
             if (g->red.size() < (size_t)world * (size_t)k) g->red.resize((size_t)world * (size_t)k);
@@ -134,10 +158,11 @@ struct ThreadComm final : Comm {
     }
 
     void alltoall_counts(const i64* send, i64* recv, hipStream_t) override {
-        g->cnt[(size_t)rank] = send;
+        i64* b = g->bank[seq++ & 1].data();  // (kslot >= world)
+        const size_t K = (size_t)g->kslot;
+        std::copy(send, send + world, b + (size_t)rank * K);
         g->barrier();
-        for (int q = 0; q < world; ++q) recv[q] = g->cnt[(size_t)q][rank];
-        g->barrier();
+        for (int q = 0; q < world; ++q) recv[q] = b[(size_t)q * K + (size_t)rank];
     }
 
     void alltoallv(const void* send, const i64* scount, void* recv, const i64* rcount, size_t elem,
@@ -175,7 +200,10 @@ struct ThreadComm final : Comm {
     }
 
     void abort() override { g->abort(); }
-    void reset() override { g->reset(); }
+    void reset() override {
+        g->reset();
+        seq = 0;
+    }
 };
 
 }  // namespace

@@ -101,17 +101,9 @@ __device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
 #ifndef PJ_V2_NOFIN
 #define PJ_V2_NOFIN 2
 #endif
-// PJ_V2_FBDEN > 0: a light pull round whose frontier holds fewer than n / PJ_V2_FBDEN
-// vertices probes the frontier bitmap first after all (n / 8 bytes, cache-resident, and
-// mostly clear bits then: one probe of it instead of the dist line for most in-edges)
-#ifndef PJ_V2_FBDEN
-#define PJ_V2_FBDEN 0
-#endif
-// PJ_V2_HBDEN > 0: the same for a heavy pull whose band members hold fewer than
-// nnz / PJ_V2_HBDEN edges (their member bitmap is probed first)
-#ifndef PJ_V2_HBDEN
-#define PJ_V2_HBDEN 0
-#endif
+// (Round 5: the bits probed first again on sparse rounds only -- light pull rounds whose
+// frontier is below n / 16 or n / 64, heavy pulls whose members hold below nnz / 16 edges --
+// measured 1-2% slower or equal, profiles/r05/ab_fbits_r5i.txt: dist alone everywhere.)
 // the candidate distance u offers through a pulled edge (INT_INF = none): bits == null
 // probes dist[u] alone (PJ_V2_NOFIN), else u's bit first. (Round 5: a per-round byte map of
 // the frontier's distances, dist - lo, probed instead of dist -- the map 4x denser in the
@@ -912,13 +904,13 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fo
 // them), counts them into slot cout and folds min{new dist >= hi} into minv.
 template <typename Off>
 __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fout,
-                                                int32_t nhi, int cout, bool hbits) {
+                                                int32_t nhi, int cout) {
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
     __shared__ u64 red[NWV];
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    const u64* hmb = (PJ_V2_NOFIN >= 2 && !hbits) ? nullptr : a.mb;
+    const u64* hmb = PJ_V2_NOFIN >= 2 ? nullptr : a.mb;
     u32* newb = s_new[wave_id()];
     u32 ccount = 0;
     u64 fe = 0;
@@ -1077,11 +1069,11 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
 template <typename Off>
 __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* __restrict__ row,
                                                    const u64* __restrict__ fin, u64* __restrict__ fout, u32* newb,
-                                                   u32& newc, u64& fe, u64& mh, u64& ml, bool fbits) {
+                                                   u32& newc, u64& fe, u64& mh, u64& ml) {
     constexpr int NWV = DB / WAVE;
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    const u64* lfin = (PJ_V2_NOFIN && !fbits) ? nullptr : fin;
+    const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
     const i64 nsc = (a.nwords + PSC - 1) / PSC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
         const i64 gbase = sc * PSC;
@@ -1220,10 +1212,10 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
 // atomicMin (the vertex's chunks run in different waves).
 __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __restrict__ fin, u64* __restrict__ fout,
                                                   const u32* __restrict__ lcv, const u32* __restrict__ lcc, u64 nlc,
-                                                  u32& newc, u64& fe, bool fbits) {
+                                                  u32& newc, u64& fe) {
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    const u64* lfin = (PJ_V2_NOFIN && !fbits) ? nullptr : fin;
+    const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
     for (u64 it = (u64)blockIdx.x * (DB / WAVE) + wave_id(); it < nlc; it += (u64)gridDim.x * (DB / WAVE)) {
         const u32 v = lcv[it];
         const int32_t d0 = dist_now(a.dist + v);
@@ -1314,9 +1306,8 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
     }
     u32 newc = 0;
     u64 fe = 0, mh = 0, ml = 0;
-    const bool fbits = PJ_V2_FBDEN > 0 && fcount * (u64)PJ_V2_FBDEN < (u64)a.n;
-    if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe, fbits);
-    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml, fbits);
+    if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe);
+    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml);
     v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
     v2_flush2(mh, ml, a.ctl->mh, red);
 }
@@ -1939,8 +1930,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             }
             const bool pull_now = can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh;
             if (pull_now) {
-                const bool hbits = PJ_V2_HBDEN > 0 && (double)(mh + ml) * PJ_V2_HBDEN < (double)g.nnz;
-                v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi_t, cs, hbits);
+                v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi_t, cs);
                 PJ_LAUNCH_CHECK();
                 PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 st.bu_levels++;

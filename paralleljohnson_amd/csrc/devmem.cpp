@@ -1,13 +1,22 @@
 // devmem.cpp — DevBuf's device allocations, with a process-wide cache of big blocks.
 //
-// A block of 1 GiB or more that is freed is kept (up to a third of the device's memory)
-// and handed out again to a later request of at most its size and at least 4/9 of it, on
-// the same device (a world-2 build's blocks fit in a world-1 build's, about twice their
-// size). Reason (round 5, bench.py's partition legs): the partitioned builds allocate and free tens of GB of sort temporaries per rank, and the one hipMalloc per
-// build that had to take fresh memory from the driver took 2.7-5.2 s for a 17-34 GB block
-// (profiles/r05: the build phases' slowest allocation); from the cache it is free. A
-// request that fails with the cache holding blocks empties the cache and tries again, so
-// the cache never costs an allocation that would otherwise succeed.
+// Reason (round 5, bench.py's partition legs): the partitioned builds allocate and free
+// tens of GB of sort temporaries per rank, and a hipMalloc that takes memory the driver
+// has just had back from a hipFree waits for that memory to be cleared (2.7-5.2 s for a
+// 17-34 GB block, ~6 GB/s; profiles/r05: the build phases' slowest allocation). Memory
+// that stays allocated in the process skips that.
+//
+// So a block of 1 GiB or more is not returned to the driver when DevBuf frees it: it stays
+// cached (up to half of the device's memory) and is handed out again, whole or in slices,
+// to later requests on the same device. A request takes the smallest free range that holds
+// it and leaves the rest of the range free (a world-2 build's two ranks take the two halves
+// of a block a world-1 build freed); a freed slice merges with its free neighbours. A
+// request that fails while the cache holds blocks returns every wholly free block to the
+// driver and tries again, so the cache never costs an allocation that would otherwise
+// succeed.
+#include <algorithm>
+#include <iterator>
+#include <map>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -19,27 +28,52 @@ namespace pj {
 namespace {
 
 constexpr size_t BIG = size_t(1) << 30;
+constexpr size_t ALIGN = 4096;  // slice boundaries
+
+struct Blk {  // one hipMalloc'ed block: its free ranges (offset -> bytes) and live slices
+    int dev;
+    char* base;
+    size_t bytes;
+    std::map<size_t, size_t> free_ranges;
+    int live;
+};
 
 struct BigCache {
     std::mutex mu;
-    struct Blk {
-        int dev;
-        void* p;
-        size_t bytes;
-    };
-    std::vector<Blk> free_blocks;                // cached, not in use
-    std::unordered_map<void*, Blk> live;         // big blocks in use (their real size)
-    size_t cached = 0;
-    size_t cap(int dev) {
+    std::vector<Blk*> blocks;
+    std::unordered_map<void*, std::pair<Blk*, size_t>> live;  // slice -> (its block, its bytes)
+    size_t held = 0;                                           // bytes of all blocks
+
+    static size_t cap() {
         size_t fr = 0, tot = 0;
-        (void)dev;
         if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
-        return tot / 3;
+        return tot / 2;
     }
-    void flush() {  // (mu held)
-        for (auto& b : free_blocks) (void)hipFree(b.p);
-        free_blocks.clear();
-        cached = 0;
+    void release(Blk* b) {  // (mu held; b has no live slice)
+        (void)hipFree(b->base);
+        held -= b->bytes;
+        blocks.erase(std::find(blocks.begin(), blocks.end(), b));
+        delete b;
+    }
+    void flush() {  // every wholly free block back to the driver (mu held)
+        std::vector<Blk*> idle;
+        for (Blk* b : blocks)
+            if (b->live == 0) idle.push_back(b);
+        for (Blk* b : idle) release(b);
+    }
+    void* take(Blk* b, std::map<size_t, size_t>::iterator it, size_t bytes) {
+        const size_t off = it->first, len = it->second;
+        b->free_ranges.erase(it);
+        const size_t want = (bytes + ALIGN - 1) / ALIGN * ALIGN;
+        size_t taken = len;
+        if (len > want && len - want >= ALIGN) {  // the rest of the range stays free
+            b->free_ranges[off + want] = len - want;
+            taken = want;
+        }
+        b->live++;
+        char* p = b->base + off;
+        live[p] = {b, taken};
+        return p;
     }
 };
 
@@ -60,28 +94,28 @@ void* dev_alloc(size_t bytes) {
     PJ_HIP(hipGetDevice(&dev));
     BigCache& c = cache();
     std::lock_guard<std::mutex> lk(c.mu);
-    size_t best = (size_t)-1;
-    for (size_t i = 0; i < c.free_blocks.size(); ++i) {
-        const auto& b = c.free_blocks[i];
-        if (b.dev == dev && b.bytes >= bytes && b.bytes <= bytes / 4 * 9 &&
-            (best == (size_t)-1 || b.bytes < c.free_blocks[best].bytes))
-            best = i;
+    Blk* bb = nullptr;  // best fit: the smallest free range that holds the request
+    std::map<size_t, size_t>::iterator bi;
+    for (Blk* b : c.blocks) {
+        if (b->dev != dev) continue;
+        for (auto it = b->free_ranges.begin(); it != b->free_ranges.end(); ++it)
+            if (it->second >= bytes && (!bb || it->second < bi->second)) {
+                bb = b;
+                bi = it;
+            }
     }
-    if (best != (size_t)-1) {
-        const BigCache::Blk b = c.free_blocks[best];
-        c.free_blocks.erase(c.free_blocks.begin() + (std::ptrdiff_t)best);
-        c.cached -= b.bytes;
-        c.live[b.p] = b;
-        return b.p;
-    }
+    if (bb) return c.take(bb, bi, bytes);
     hipError_t e = hipMalloc(&p, bytes);
-    if (e != hipSuccess && !c.free_blocks.empty()) {
+    if (e != hipSuccess && c.held > 0) {
         (void)hipGetLastError();
         c.flush();
         e = hipMalloc(&p, bytes);
     }
     PJ_HIP(e);
-    c.live[p] = BigCache::Blk{dev, p, bytes};
+    Blk* b = new Blk{dev, static_cast<char*>(p), bytes, {}, 1};
+    c.blocks.push_back(b);
+    c.held += bytes;
+    c.live[p] = {b, bytes};
     return p;
 }
 
@@ -92,20 +126,39 @@ void dev_free(void* p, size_t bytes) {
         return;
     }
     BigCache& c = cache();
-    {
-        std::lock_guard<std::mutex> lk(c.mu);
-        auto it = c.live.find(p);
-        if (it != c.live.end()) {
-            const BigCache::Blk b = it->second;
-            c.live.erase(it);
-            if (c.cached + b.bytes <= c.cap(b.dev)) {
-                c.free_blocks.push_back(b);
-                c.cached += b.bytes;
-                return;
-            }
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) {  // (not from dev_alloc's big path; DevBuf never does this)
+        (void)hipFree(p);
+        return;
+    }
+    Blk* b = it->second.first;
+    size_t off = (size_t)(static_cast<char*>(p) - b->base), len = it->second.second;
+    c.live.erase(it);
+    b->live--;
+    auto nx = b->free_ranges.lower_bound(off);  // merge with the free neighbours
+    if (nx != b->free_ranges.end() && nx->first == off + len) {
+        len += nx->second;
+        nx = b->free_ranges.erase(nx);
+    }
+    if (nx != b->free_ranges.begin()) {
+        auto pv = std::prev(nx);
+        if (pv->first + pv->second == off) {
+            off = pv->first;
+            len += pv->second;
+            b->free_ranges.erase(pv);
         }
     }
-    (void)hipFree(p);
+    b->free_ranges[off] = len;
+    if (b->live == 0 && c.held > BigCache::cap()) c.release(b);  // over the cap: back to the driver
+}
+
+size_t dev_trim() {
+    BigCache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    const size_t before = c.held;
+    c.flush();
+    return before - c.held;
 }
 
 }  // namespace pj

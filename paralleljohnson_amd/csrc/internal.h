@@ -46,6 +46,7 @@ void set_error(const std::string& msg);
 // from the driver took seconds for one 17-34 GB block (round 5, the bench's partition legs).
 void* dev_alloc(size_t bytes);
 void dev_free(void* p, size_t bytes);
+size_t dev_trim();  // cached big blocks without a live slice back to the driver; bytes released
 
 template <typename T>
 struct DevBuf {

@@ -178,6 +178,11 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
 #endif
 __device__ __forceinline__ bool zbit(const u64* __restrict__ Z, u32 u) { return (Z[u >> 6] >> (u & 63)) & 1ull; }
 
+// (PJ_MS_NODIST: measurement builds only, wrong distances -- 1 skips the per-level distance stores, 2 also
+// the fill of the distance block)
+#ifndef PJ_MS_NODIST
+#define PJ_MS_NODIST 0
+#endif
 #ifndef PJ_MS_GPC
 #define PJ_MS_GPC 8  // level-kernel workgroups per CU (MS1024: 12.8 -> 12.4 ms with MS_U 4, round 3)
 #endif
@@ -202,6 +207,7 @@ __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __rest
         F[i] = 0;
     }
     for (i64 i = tid; i < nzw; i += nth) Z[i] = 0;
+    if (PJ_MS_NODIST >= 2) return;
     int4* d4 = reinterpret_cast<int4*>(dist);
     const i64 n4 = nb_dist / 4;
     for (i64 i = tid; i < n4; i += nth) d4[i] = make_int4(INT_INF, INT_INF, INT_INF, INT_INF);
@@ -259,6 +265,7 @@ __global__ __launch_bounds__(MB) void ms_prep_k(i64 n, u64* __restrict__ Fn, int
 template <int W>
 __device__ __forceinline__ void ms_write_dist(const Mask<W>& newb, int32_t* __restrict__ dist, i64 n, i64 v,
                                               int32_t val) {
+    if (PJ_MS_NODIST) return;
 #pragma unroll
     for (int j = 0; j < W; ++j) {
         u64 un = wave_or(newb.w[j]);

@@ -186,6 +186,32 @@ def test_bfs_kronecker_s22_full_size(ctx, oracle):
     g.close()
 
 
+def test_device_cache_slices_and_trim(ctx, pj):
+    """devmem.cpp: freed device blocks >= 1 GiB stay cached and serve later big allocations
+    whole or in slices (two live s23 graphs inside one s24 build's freed blocks); a graph built
+    from cached memory answers as one built from fresh memory; trim returns the free blocks."""
+    pj.trim_device_cache()
+    g = ctx.generate_kronecker(24, 16, 1, weighted=True)
+    r = int(g.sample_roots(1, 7)[0])
+    d24 = g.sssp(r)
+    g.close()
+    assert pj.trim_device_cache() >= 2**30  # the build's temporaries and the graph's arrays
+    g = ctx.generate_kronecker(23, 16, 1, weighted=True)  # (fresh memory)
+    r = int(g.sample_roots(1, 7)[0])
+    exp = g.sssp(r)
+    g.close()
+    a = ctx.generate_kronecker(24, 16, 1, weighted=True)  # caches s24-sized blocks again
+    assert (a.sssp(int(a.sample_roots(1, 7)[0])) == d24).all()
+    a.close()
+    g1 = ctx.generate_kronecker(23, 16, 1, weighted=True)  # slices of the cached blocks
+    g2 = ctx.generate_kronecker(23, 16, 1, weighted=True)
+    assert (g1.sssp(r) == exp).all() and (g2.sssp(r) == exp).all()
+    g1.close()
+    assert (g2.sssp(r) == exp).all()
+    g2.close()
+    assert pj.trim_device_cache() >= 2**30
+
+
 def test_weighted_delta_stepping(ctx, oracle):
     rng = np.random.default_rng(21)
     for trial in range(6):
