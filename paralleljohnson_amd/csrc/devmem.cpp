@@ -7,7 +7,8 @@
 // that stays allocated in the process skips that.
 //
 // So a block of 1 GiB or more is not returned to the driver when DevBuf frees it: it stays
-// cached (up to half of the device's memory) and is handed out again, whole or in slices,
+// cached (up to half of the device's memory; past that the least recently freed wholly
+// free blocks go back first) and is handed out again, whole or in slices,
 // to later requests on the same device. A request takes the smallest free range that holds
 // it and leaves the rest of the range free (a world-2 build's two ranks take the two halves
 // of a block a world-1 build freed); a freed slice merges with its free neighbours. A
@@ -28,7 +29,9 @@ namespace pj {
 namespace {
 
 constexpr size_t BIG = size_t(1) << 30;
-constexpr size_t ALIGN = 4096;  // slice boundaries
+constexpr size_t ALIGN = 4096;            // slice boundaries
+constexpr size_t SLACK = size_t(2) << 20;  // a fresh block's extra bytes: two slices whose sizes
+                                           // add up to its request still fit after rounding
 
 struct Blk {  // one hipMalloc'ed block: its free ranges (offset -> bytes) and live slices
     int dev;
@@ -36,6 +39,7 @@ struct Blk {  // one hipMalloc'ed block: its free ranges (offset -> bytes) and l
     size_t bytes;
     std::map<size_t, size_t> free_ranges;
     int live;
+    unsigned long long stamp;  // when a slice of it was last freed
 };
 
 struct BigCache {
@@ -43,6 +47,7 @@ struct BigCache {
     std::vector<Blk*> blocks;
     std::unordered_map<void*, std::pair<Blk*, size_t>> live;  // slice -> (its block, its bytes)
     size_t held = 0;                                           // bytes of all blocks
+    unsigned long long clock = 0;
 
     static size_t cap() {
         size_t fr = 0, tot = 0;
@@ -105,17 +110,18 @@ void* dev_alloc(size_t bytes) {
             }
     }
     if (bb) return c.take(bb, bi, bytes);
-    hipError_t e = hipMalloc(&p, bytes);
+    const size_t bb_bytes = (bytes + SLACK - 1) / SLACK * SLACK + SLACK;
+    hipError_t e = hipMalloc(&p, bb_bytes);
     if (e != hipSuccess && c.held > 0) {
         (void)hipGetLastError();
         c.flush();
-        e = hipMalloc(&p, bytes);
+        e = hipMalloc(&p, bb_bytes);
     }
     PJ_HIP(e);
-    Blk* b = new Blk{dev, static_cast<char*>(p), bytes, {}, 1};
+    Blk* b = new Blk{dev, static_cast<char*>(p), bb_bytes, {}, 1, 0};
     c.blocks.push_back(b);
-    c.held += bytes;
-    c.live[p] = {b, bytes};
+    c.held += bb_bytes;
+    c.live[p] = {b, bb_bytes};
     return p;
 }
 
@@ -150,7 +156,18 @@ void dev_free(void* p, size_t bytes) {
         }
     }
     b->free_ranges[off] = len;
-    if (b->live == 0 && c.held > BigCache::cap()) c.release(b);  // over the cap: back to the driver
+    b->stamp = ++c.clock;
+    const size_t cap = BigCache::cap();
+    if (c.held > cap) {  // over the cap: wholly free blocks back to the driver, least recent first
+        std::vector<Blk*> idle;
+        for (Blk* x : c.blocks)
+            if (x->live == 0) idle.push_back(x);
+        std::sort(idle.begin(), idle.end(), [](const Blk* x, const Blk* y) { return x->stamp < y->stamp; });
+        for (Blk* x : idle) {
+            if (c.held <= cap) break;
+            c.release(x);
+        }
+    }
 }
 
 size_t dev_trim() {

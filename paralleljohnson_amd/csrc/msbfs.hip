@@ -12,6 +12,16 @@
 // with the scan stopping as soon as every source still missing at v is covered.
 // Distances follow the R9 contract per source: the level number, capped at INT_INF.
 //
+// Distance output (round 5): the levels do not store distances. Each level's new masks go
+// to a level archive (entry L+1 for level L, entry 0 = the sources; a level writes only
+// the rows with new bits, and a row bitmap Z per entry says which), and one expansion
+// kernel at the end of the pass writes the whole 64 W x n distance block with full-line
+// stores: every (source, vertex) bit is set in exactly one entry, the arrival level. Per
+// level stores of the new pairs' distances into the source-major block were masked
+// partial-line writes, 64 W of them per wave and level: 8 of the 11.5 ms of an MS1024
+// batch (profiles/r05/ms_dist_r5k.txt). A pass deeper than the archive expands it when it
+// fills and stores the later levels' distances directly, as before.
+//
 // Work mapping: one wave per 64 consecutive vertices; each lane walks its first
 // MS_SERIAL in-edges in a wave-uniform loop (predicated body), then the whole wave
 // scans the rest of long rows (web-graph in-hubs) 64 edges at a time. The masks
@@ -178,11 +188,6 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
 #endif
 __device__ __forceinline__ bool zbit(const u64* __restrict__ Z, u32 u) { return (Z[u >> 6] >> (u & 63)) & 1ull; }
 
-// (PJ_MS_NODIST: measurement builds only, wrong distances -- 1 skips the per-level distance stores, 2 also
-// the fill of the distance block)
-#ifndef PJ_MS_NODIST
-#define PJ_MS_NODIST 0
-#endif
 #ifndef PJ_MS_GPC
 #define PJ_MS_GPC 8  // level-kernel workgroups per CU (MS1024: 12.8 -> 12.4 ms with MS_U 4, round 3)
 #endif
@@ -207,7 +212,7 @@ __global__ __launch_bounds__(MB) void ms_init_k(u64* __restrict__ V, u64* __rest
         F[i] = 0;
     }
     for (i64 i = tid; i < nzw; i += nth) Z[i] = 0;
-    if (PJ_MS_NODIST >= 2) return;
+    if (!dist) return;  // (the archive's expansion writes every distance)
     int4* d4 = reinterpret_cast<int4*>(dist);
     const i64 n4 = nb_dist / 4;
     for (i64 i = tid; i < n4; i += nth) d4[i] = make_int4(INT_INF, INT_INF, INT_INF, INT_INF);
@@ -226,7 +231,7 @@ __global__ void ms_sources_k(const int64_t* __restrict__ src, int ns, int W, i64
     atomicOr(&V[s * W + (i >> 6)], 1ull << (i & 63));
     atomicOr(&F[s * W + (i >> 6)], 1ull << (i & 63));
     atomicOr(&Z[s >> 6], 1ull << (s & 63));
-    dist[(i64)i * n + s] = 0;
+    if (dist) dist[(i64)i * n + s] = 0;
     ctl->active[2] = 1;  // "level -1" found the sources
     atomicOr(&ctl->uf[2][0][i >> 6], 1ull << (i & 63));
     atomicAdd(&ctl->fedges[2][0][0], (u64)(row[s + 1] - row[s]));
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(MB) void ms_prep_k(i64 n, u64* __restrict__ Fn, int
 template <int W>
 __device__ __forceinline__ void ms_write_dist(const Mask<W>& newb, int32_t* __restrict__ dist, i64 n, i64 v,
                                               int32_t val) {
-    if (PJ_MS_NODIST) return;
+    if (!dist) return;  // (archive mode: ms_expand_k writes them)
 #pragma unroll
     for (int j = 0; j < W; ++j) {
         u64 un = wave_or(newb.w[j]);
@@ -509,13 +514,57 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
 
 }  // namespace
 
+// The distance block from the level archive: entries [0, nlev), entry a holding at row v
+// the sources that reached v at level a (valid where bit v of its row bitmap is set). A
+// wave takes 64 consecutive vertices; per mask word it ORs each lane's entries into the
+// five bit planes of the level number (MS_LCAP <= 32), then stores source by source 64
+// consecutive distances (INT_INF where no entry holds the bit).
+constexpr int MS_LCAP = 32;  // archive entries at most (the level number in 5 bit planes)
+template <int W>
+__global__ __launch_bounds__(MB) void ms_expand_k(i64 n, const u64* __restrict__ arch, const u64* __restrict__ zarch,
+                                                  i64 nzw, int nlev, int ns, int32_t* __restrict__ dist) {
+    const int lane = lane_id();
+    const i64 nwaves = (i64)gridDim.x * (MB / WAVE);
+    for (i64 base = ((i64)blockIdx.x * (MB / WAVE) + wave_id()) * 64; base < n; base += nwaves * 64) {
+        const i64 v = base + lane;
+        const bool inr = v < n;
+        u32 zm = 0;  // the entries holding a row for v
+        for (int a = 0; a < nlev; ++a)
+            if ((zarch[(i64)a * nzw + (base >> 6)] >> lane) & 1ull) zm |= 1u << a;
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            if (64 * j >= ns) break;
+            u64 any = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0;
+            for (u32 m = zm; m; m &= m - 1) {
+                const int a = __ffs((int)m) - 1;
+                const u64 x = arch[((i64)a * n + v) * W + j];
+                any |= x;
+                if (a & 1) p0 |= x;
+                if (a & 2) p1 |= x;
+                if (a & 4) p2 |= x;
+                if (a & 8) p3 |= x;
+                if (a & 16) p4 |= x;
+            }
+            const int nb = min(64, ns - 64 * j);
+            for (int b = 0; b < nb; ++b) {
+                const int32_t lv = (int32_t)(((p0 >> b) & 1ull) | (((p1 >> b) & 1ull) << 1) | (((p2 >> b) & 1ull) << 2) |
+                                             (((p3 >> b) & 1ull) << 3) | (((p4 >> b) & 1ull) << 4));
+                if (inr) dist[(i64)(64 * j + b) * n + v] = ((any >> b) & 1ull) ? lv : INT_INF;
+            }
+        }
+    }
+}
+
 // One pass in flight: its masks, distance block, control block, stream and events.
 // Slot 0 runs on the ctx stream; further slots (option ms_streams) own a stream, and
 // passes of one batch run on the slots at once, one host thread each: a pass is a chain
 // of latency-bound levels, so two of them interleave on the CUs.
 struct MsSlot {
-    DevBuf<u64> V, F, Fn;
-    DevBuf<u64> Z, Zn;  // (PJ_MS_FZ) nonzero-row bitmaps of F and Fn
+    DevBuf<u64> V;
+    DevBuf<u64> arch;   // level archive: lcap entries of n x W words (the frontier masks F, Fn of
+                        // each level are two of its entries)
+    DevBuf<u64> zarch;  // (PJ_MS_FZ) each entry's nonzero-row bitmap, nzw words
+    int lcap = 0;
     DevBuf<int32_t> dist;
     DevBuf<int64_t> src;
     DevBuf<MsCtl> ctl;
@@ -560,41 +609,68 @@ static void ms_pass(Graph& g, MsSlot& w, const int64_t* sources, int ns, double*
     const u32* col = g.col.p;
     // push while the frontier's out-edges are below nnz / ms_alpha (0: never)
     const u64 push_max = g.ms_alpha > 0 ? (u64)((double)g.nnz / g.ms_alpha) : 0ull;
+    const i64 nzw = (n + 63) / 64 + 1;
+    auto entry = [&](int a) { return w.arch.p + (size_t)a * (size_t)n * W; };
+    auto zentry = [&](int a) { return w.zarch.p + (size_t)a * (size_t)nzw; };
+    // archive mode while level L's output entry L + 1 exists; then (a pass deeper than the
+    // archive, or no archive) the levels store their distances and F / Fn alternate between
+    // the last two entries
+    bool archive = PJ_MS_FZ && w.lcap > 2;
     PJ_HIP(hipEventRecord(w.ev0, s));
-    ms_init_k<<<grid_for(std::max<i64>(n * W, (i64)ns * n / 4), MB, (unsigned)g.ctx->cu_count * 8u), MB, 0, s>>>(
-        w.V.p, w.F.p, n * W, w.dist.p, (i64)ns * n, w.ctl.p, host_dev, w.Z.p, (n + 63) / 64);
+    ms_init_k<<<grid_for(std::max<i64>(n * W, archive ? 0 : (i64)ns * n / 4), MB, (unsigned)g.ctx->cu_count * 8u), MB,
+                0, s>>>(w.V.p, entry(0), n * W, archive ? nullptr : w.dist.p, (i64)ns * n, w.ctl.p, host_dev, zentry(0),
+                        (n + 63) / 64);
     PJ_LAUNCH_CHECK();
-    ms_sources_k<Off><<<(ns + 255) / 256, 256, 0, s>>>(w.src.p, ns, W, n, row, w.V.p, w.F.p, w.dist.p, w.ctl.p,
-                                                    w.Z.p);
+    ms_sources_k<Off><<<(ns + 255) / 256, 256, 0, s>>>(w.src.p, ns, W, n, row, w.V.p, entry(0),
+                                                    archive ? nullptr : w.dist.p, w.ctl.p, zentry(0));
     PJ_LAUNCH_CHECK();
     int32_t L = 0;
     // first batch: the previous pass's levels (passes over one graph need about as many);
     // then 2, 4, 8, ... (each idle level costs its 2-4 launches inside the timed region)
     int batch = w.last_levels > 0 ? w.last_levels : 16;
     int next = 2;
-    u64* F = w.F.p;
-    u64* Fn = w.Fn.p;
-    u64* Z = w.Z.p;
-    u64* Zn = w.Zn.p;
+    int fa = 0, fb = 1;  // entries of F and Fn (direct mode: alternating)
     for (;;) {
         for (int i = 0; i < batch && L < INT_INF; ++i, ++L) {
+            if (archive) {
+                if (L + 1 >= w.lcap) break;  // (the archive is full: the host decides below)
+                fa = L;
+                fb = L + 1;
+            }
+            u64 *F = entry(fa), *Fn = entry(fb), *Z = zentry(fa), *Zn = zentry(fb);
+            int32_t* dst = archive ? nullptr : w.dist.p;
             ms_prep_k<W><<<grid, MB, 0, s>>>(n, Fn, L, push_max, w.ctl.p, host_dev);
             PJ_LAUNCH_CHECK();
-            ms_level_k<Off, W><<<grid, MB, 0, s>>>(n, crow, ccol, row, w.V.p, F, Fn, w.dist.p, L, smask, push_max,
+            ms_level_k<Off, W><<<grid, MB, 0, s>>>(n, crow, ccol, row, w.V.p, F, Fn, dst, L, smask, push_max,
                                                    w.ctl.p, Z, Zn);
             PJ_LAUNCH_CHECK();
             if (push_max) {
                 ms_push_k<Off, W><<<grid, MB, 0, s>>>(n, row, col, F, Fn, L, push_max, w.ctl.p, Z);
                 PJ_LAUNCH_CHECK();
-                ms_fin_k<Off, W><<<grid, MB, 0, s>>>(n, row, w.V.p, Fn, w.dist.p, L, smask, push_max, w.ctl.p,
-                                                     Zn);
+                ms_fin_k<Off, W><<<grid, MB, 0, s>>>(n, row, w.V.p, Fn, dst, L, smask, push_max, w.ctl.p, Zn);
                 PJ_LAUNCH_CHECK();
             }
-            std::swap(F, Fn);
-            std::swap(Z, Zn);
+            if (!archive) std::swap(fa, fb);
         }
         PJ_HIP(hipStreamSynchronize(s));
-        if (*(volatile int64_t*)w.host >= 0 || L >= INT_INF || !any) break;
+        const int64_t done = *(volatile int64_t*)w.host;
+        if (archive && (done >= 0 || !any)) {
+            // level done - 1 found nothing: entries [0, done] hold every arrival
+            const int nlev = any ? (int)done + 1 : 1;
+            ms_expand_k<W><<<grid, MB, 0, s>>>(n, w.arch.p, w.zarch.p, nzw, nlev, ns, w.dist.p);
+            PJ_LAUNCH_CHECK();
+            break;
+        }
+        if (done >= 0 || L >= INT_INF || !any) break;
+        if (archive && L + 1 >= w.lcap) {
+            // the archive is full and the pass goes on: expand it (every distance, INT_INF for
+            // the pairs not reached yet), then store the later levels' distances directly
+            ms_expand_k<W><<<grid, MB, 0, s>>>(n, w.arch.p, w.zarch.p, nzw, w.lcap, ns, w.dist.p);
+            PJ_LAUNCH_CHECK();
+            archive = false;
+            fa = L;      // level L reads entry L (= lcap - 1) ...
+            fb = L - 1;  // ... and writes over entry L - 1, already expanded
+        }
         batch = next;
         next = next < 1024 ? next * 2 : next;
     }
@@ -617,28 +693,36 @@ static void ms_pass_w(int W, Graph& g, MsSlot& w, const int64_t* sources, int ns
     else ms_pass<Off, 1>(g, w, sources, ns, kernel_ms, levels);
 }
 
-// Device bytes of one pass slot: the distance block (64 W x n int32), the masks V, F,
-// Fn (W words per vertex each) and the two nonzero-row bitmaps.
-static double ms_slot_bytes(i64 n, int W) {
-    return (double)n * (64.0 * W * 4.0 + 3.0 * W * 8.0) + 2.0 * ((double)n / 8.0 + 16.0);
+// Device bytes of one pass slot: the distance block (64 W x n int32), the masks V (W words
+// per vertex) and the level archive (lcap entries of W words per vertex and a row bitmap).
+static double ms_slot_bytes(i64 n, int W, int lcap) {
+    return (double)n * (64.0 * W * 4.0 + (1.0 + lcap) * W * 8.0) + lcap * ((double)n / 8.0 + 16.0);
 }
+// Archive entries of a slot: MS_LCAP, fewer when the slot would exceed MS_BUDGET / 2 (the
+// later levels of a deeper pass store their distances directly); 2 = no archive.
+static int ms_lcap(i64 n, int W);
 constexpr double MS_BUDGET = 16e9;  // device bytes all slots of a batch may hold
 // Pass width: the fewest words that hold the batch, at most MS_WMAX (g.ms_width
 // caps it), with one slot's buffers within the budget.
 static int ms_words(const Graph& g, int n_src) {
     int W = 1;
     const int cap = g.ms_width > 0 ? std::min(g.ms_width, MS_WMAX) : MS_WDEF;
-    while (W < cap && 64 * W < n_src && ms_slot_bytes(g.n, 2 * W) <= MS_BUDGET) W *= 2;
+    while (W < cap && 64 * W < n_src && ms_slot_bytes(g.n, 2 * W, 2) <= MS_BUDGET) W *= 2;
     return W;
 }
+static int ms_lcap(i64 n, int W) {
+    if (!PJ_MS_FZ) return 2;  // (the archive needs the row bitmaps)
+    int lc = MS_LCAP;
+    while (lc > 2 && ms_slot_bytes(n, W, lc) > MS_BUDGET / 2) --lc;
+    return lc;
+}
 
-static void ms_slot_alloc(Graph& g, MsSlot& sl, int W, bool own_stream) {
+static void ms_slot_alloc(Graph& g, MsSlot& sl, int W, int lcap, bool own_stream) {
     const size_t n = (size_t)g.n;
     sl.V.alloc(n ? n * W : 1);
-    sl.F.alloc(n ? n * W : 1);
-    sl.Fn.alloc(n ? n * W : 1);
-    sl.Z.alloc((n + 63) / 64 + 1);
-    sl.Zn.alloc((n + 63) / 64 + 1);
+    sl.lcap = lcap;
+    sl.arch.alloc(n ? (size_t)lcap * n * W : 1);
+    sl.zarch.alloc((size_t)lcap * ((n + 63) / 64 + 1));
     sl.dist.alloc(n ? 64 * W * n : 1);
     sl.src.alloc(64 * W);
     sl.ctl.alloc(1);
@@ -661,15 +745,16 @@ void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_
         g.ms_work->W = W;
     }
     MsWork& mw = *g.ms_work;
-    // Every slot holds a whole pass (ms_slot_bytes: ~1.9 GB at n = 916K, W = 8): the slots
-    // in flight stay within MS_BUDGET, and a slot beyond the first is only added while it
-    // takes at most half the free device memory; if its allocation still fails, the batch
-    // runs on the slots it has.
-    const double sb = ms_slot_bytes(g.n, mw.W);
+    // Every slot holds a whole pass (ms_slot_bytes: ~3.8 GB at n = 916K, W = 8, with a
+    // 32-entry archive): the slots in flight stay within MS_BUDGET, and a slot beyond the
+    // first is only added while it takes at most half the free device memory; if its
+    // allocation still fails, the batch runs on the slots it has.
+    const int lcap = ms_lcap(g.n, mw.W);
+    const double sb = ms_slot_bytes(g.n, mw.W, lcap);
     while (nslots > 1 && (double)nslots * sb > MS_BUDGET) --nslots;
     if (mw.slots.empty()) {
         std::unique_ptr<MsSlot> sl(new MsSlot());
-        ms_slot_alloc(g, *sl, mw.W, false);
+        ms_slot_alloc(g, *sl, mw.W, lcap, false);
         mw.slots.push_back(std::move(sl));
     }
     while ((int)mw.slots.size() < nslots) {
@@ -677,7 +762,7 @@ void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_
         if (hipMemGetInfo(&fr, &tot) != hipSuccess || sb > 0.5 * (double)fr) break;
         std::unique_ptr<MsSlot> sl(new MsSlot());
         try {
-            ms_slot_alloc(g, *sl, mw.W, true);
+            ms_slot_alloc(g, *sl, mw.W, lcap, true);
         } catch (const Error&) {
             (void)hipGetLastError();
             break;

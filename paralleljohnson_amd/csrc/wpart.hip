@@ -833,13 +833,90 @@ __global__ void wp_frontier_slice_k(WArgs a, MT* __restrict__ own) {
         own[v] = x;
     }
 }
+// Light rows longer than WP_PLMAX (the hubs, at the lowest ids of the degree order) are
+// pulled by wp_pull_long_k from a static list of (vertex, chunk of WP_PCH light edges),
+// built once per light threshold: scanned inside wp_pull_light_k, one wave walked a hub's
+// whole light row alone while the rest of the grid idled (an s26w solve whose hubs were
+// unsettled at a light pull took 20-25 ms instead of 10, profiles/r05/wpart_sweep_r5k.txt).
+constexpr u32 WP_PLMAX = 64;
+constexpr u32 WP_PCH = 256;
+__global__ void wp_plong_count_k(const u32* __restrict__ lsplit, i64 nl, u64* __restrict__ cnt) {
+    u64 c = 0;
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < nl; v += (i64)gridDim.x * blockDim.x)
+        if (lsplit[v] > WP_PLMAX) c += (lsplit[v] + WP_PCH - 1) / WP_PCH;
+    c = wave_sum(c);
+    if (lane_id() == 0 && c) atomicAdd(cnt, c);
+}
+__global__ void wp_plong_fill_k(const u32* __restrict__ lsplit, i64 nl, u64* __restrict__ cnt, u32* __restrict__ lv,
+                                u32* __restrict__ lc) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < nl; v += (i64)gridDim.x * blockDim.x)
+        if (lsplit[v] > WP_PLMAX) {
+            const u32 nc = (lsplit[v] + WP_PCH - 1) / WP_PCH;
+            const u64 b = atomicAdd(cnt, (u64)nc);
+            for (u32 c = 0; c < nc; ++c) {
+                lv[b + c] = (u32)v;
+                lc[b + c] = c;
+            }
+        }
+}
+// a wave per chunk: skipped when even its lightest edge cannot help, else scanned with the
+// early stop; the result goes in with atomicMin (a vertex's chunks run in different waves)
+// and the vertex's next-frontier bit with a returning atomicOr (counted once)
+template <typename MT>
+__global__ __launch_bounds__(WB) void wp_pull_long_k(WArgs a, const MT* __restrict__ fmap, const u32* __restrict__ lv,
+                                                     const u32* __restrict__ lc, u64 nlc) {
+    constexpr MT NONE = (MT)~(MT)0;
+    __shared__ u64 red[WB / WAVE];
+    const int lane = lane_id();
+    const int32_t lo = a.dlo, hi = a.dhi;
+    u64 marks = 0;
+    for (u64 it = (u64)blockIdx.x * (WB / WAVE) + wave_id(); it < nlc; it += (u64)gridDim.x * (WB / WAVE)) {
+        const u32 v = lv[it];
+        const int32_t d0 = __hip_atomic_load(a.dist + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d0 <= lo) continue;
+        const u64 rb = a.row[v];
+        const u64 kb = rb + (u64)lc[it] * WP_PCH;
+        const u64 ke = min(rb + (u64)a.lsplit[v], kb + WP_PCH);
+        if ((long long)lo + a.w[kb] >= (long long)d0) continue;
+        int32_t cur = d0;
+        for (u64 kk = kb; kk < ke; kk += WAVE) {
+            const u64 k0 = kk + lane;
+            const bool valid = k0 < ke;
+            const u32 w = valid ? a.w[k0] : 0u;
+            const bool stop = !valid || (long long)lo + w >= (long long)cur;
+            int32_t cand = INT_INF;
+            if (!stop) {
+                const MT m = fmap[a.col[k0]];
+                if (m != NONE) cand = lo + (int32_t)m + (int32_t)w;
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const int32_t y = __shfl_xor(cand, off, 64);
+                cand = y < cand ? y : cand;
+            }
+            cur = cand < cur ? cand : cur;
+            if (__ballot(stop)) break;
+        }
+        if (lane == 0 && cur < d0) {
+            const int32_t old = atomicMin(a.dist + v, cur);
+            if (cur < old && cur < hi) {
+                const u64 bit = 1ull << (v & 63);
+                if (!(atomicOr(a.frn + (v >> 6), bit) & bit)) ++marks;
+            }
+        }
+    }
+    marks = block_sum<WB / WAVE>(marks, red);
+    if (threadIdx.x == 0 && marks) atomicAdd(&a.stat[ST_NF], marks);
+}
+
 // every owned vertex above lo scans its light row (ascending weight) for frontier vertices
 // (any rank's, through the map; frozen at the slice: a label-correcting round) and stops
 // once lo + w >= its best value; improved vertices below hi join the next frontier. The
 // wave owns its 64 vertices' words: the frontier word moves into mb (the round consumed
-// it) and the next-frontier word is OR-ed in whole.
+// it) and the next-frontier word is OR-ed in (wp_pull_long_k, launched before, may have
+// set bits of it). Rows longer than plmax are wp_pull_long_k's.
 template <typename MT>
-__global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const MT* __restrict__ fmap) {
+__global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const MT* __restrict__ fmap, u32 plmax) {
     constexpr MT NONE = (MT)~(MT)0;
     __shared__ u64 red[WB / WAVE];
     const int lane = lane_id();
@@ -864,7 +941,8 @@ __global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const MT* __restr
             if (act) {
                 cur = d0;
                 k = a.row[v];
-                e = k + a.lsplit[v];
+                const u32 ls = a.lsplit[v];
+                e = ls > plmax ? k : k + ls;
             }
         }
         const u64 lim = e - k > (u64)WP_PSERIAL ? k + WP_PSERIAL : e;
@@ -951,17 +1029,57 @@ __global__ void wsum_all_k(const u32* __restrict__ w, i64 m, u64* __restrict__ o
     if (lane_id() == 0 && s) atomicAdd(out, s);
 }
 
+// stat[k0, k1) into the host copy, then the sequence word the host spins on (as
+// delta.hip's v2_publish_k)
+__global__ __launch_bounds__(256) void wp_publish_k(const u64* __restrict__ stat, u64* __restrict__ host, int k0,
+                                                    int k1, u64* seqp, u64 seq) {
+    for (int i = k0 + (int)threadIdx.x; i < k1; i += 256) host[i] = stat[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(seqp, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 }  // namespace
 
-// the stat block's host copy: pinned, so each of a solve's ~40 counter reads is one
-// small DMA instead of a staged pageable copy
+// The stat block's host copy: mapped pinned memory written by wp_publish_k, with a sequence
+// word the host spins on. (A D2H hipMemcpyAsync of the block ran as a ~12 us blit per read
+// plus the stream synchronization's wake-up, ~100 reads per world-2 s26w solve,
+// profiles/r05/wpart_timeline_r5i.txt.)
 struct PinnedStat {
     u64* p = nullptr;
-    PinnedStat() { PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(u64) * ST_N, hipHostMallocDefault)); }
+    u64* dev = nullptr;
+    u64* seqw = nullptr;
+    u64* seq_dev = nullptr;
+    u64 seq = 0;
+    PinnedStat() {
+        PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(u64) * ST_N, hipHostMallocMapped));
+        PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), p, 0));
+        PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&seqw), 64, hipHostMallocMapped | hipHostMallocCoherent));
+        PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&seq_dev), seqw, 0));
+        __atomic_store_n(seqw, 0ull, __ATOMIC_RELEASE);
+    }
     ~PinnedStat() {
         if (p) (void)hipHostFree(p);
+        if (seqw) (void)hipHostFree(seqw);
     }
     u64& operator[](size_t i) { return p[i]; }
+    // stat[k0, k1) of the device block once the stream's earlier work is done: the host
+    // spins on the sequence word (after 0.2 s it synchronizes the stream instead, which
+    // surfaces a failed kernel rather than spinning forever)
+    void read(const u64* stat, int k0, int k1, hipStream_t s) {
+        const u64 q = ++seq;
+        wp_publish_k<<<1, 256, 0, s>>>(stat, dev, k0, k1, seq_dev, q);
+        PJ_LAUNCH_CHECK();
+        const auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(seqw, __ATOMIC_ACQUIRE) != q) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                PJ_HIP(hipStreamSynchronize(s));
+                break;
+            }
+        }
+    }
     PinnedStat(const PinnedStat&) = delete;
     PinnedStat& operator=(const PinnedStat&) = delete;
 };
@@ -987,6 +1105,11 @@ struct WPart {
     bool map16 = false;            // the last slice went to fmap16 (member_map() hands it out)
     DevBuf<u64> row;
     DevBuf<u32> col, w, lsplit;
+    struct PullLong {              // the light pull's long-row chunk list of one light threshold
+        DevBuf<u32> v, c;
+        u64 n = 0;
+        bool built = false;
+    } pl, pl_alt;                  // (of delta and delta_alt)
     DevBuf<u32> lsplit_alt;        // the other light threshold's prefixes (delta and the tail's are
                                    // used in turn by every solve: each was recomputed per solve)
     DevBuf<int32_t> dist;
@@ -1045,14 +1168,9 @@ struct WPart {
         a.sbits = sb_on ? sb.p : nullptr;
         return a;
     }
-    void read_stat() {
-        PJ_HIP(hipMemcpyAsync(hstat.p, stat.p, sizeof(u64) * ST_N, hipMemcpyDeviceToHost, ctx->stream));
-        PJ_HIP(hipStreamSynchronize(ctx->stream));
-    }
-    void read_acc(u64* out, int k) {  // stat[ST_ACC, ST_ACC + k) through the pinned copy
-        PJ_HIP(hipMemcpyAsync(hstat.p + ST_ACC, stat.p + ST_ACC, sizeof(u64) * (size_t)k, hipMemcpyDeviceToHost,
-                              ctx->stream));
-        PJ_HIP(hipStreamSynchronize(ctx->stream));
+    void read_stat() { hstat.read(stat.p, 0, ST_N, ctx->stream); }
+    void read_acc(u64* out, int k) {  // stat[ST_ACC, ST_ACC + k) through the host copy
+        hstat.read(stat.p, ST_ACC, ST_ACC + k, ctx->stream);
         for (int i = 0; i < k; ++i) out[i] = hstat.p[ST_ACC + i];
     }
     void clear_stat() { PJ_HIP(hipMemsetAsync(stat.p, 0, sizeof(u64) * ST_N, ctx->stream)); }
@@ -1618,7 +1736,8 @@ void wpart_device_bytes(const WPart& p, i64* out4) {
     out4[0] = (i64)(p.row.bytes() + p.col.bytes() + p.w.bytes());
     out4[1] = (i64)(p.lsplit.bytes() + p.lsplit_alt.bytes() + p.dist.bytes() + p.fr.bytes() + p.frn.bytes() +
                     p.mb.bytes() + p.lq_v.bytes() + p.lq_b.bytes() + p.lq_e.bytes() + p.stat.bytes() +
-                    p.rc.bytes() + p.qctr.bytes() + p.rl_inv.bytes());
+                    p.rc.bytes() + p.qctr.bytes() + p.rl_inv.bytes() + p.pl.v.bytes() + p.pl.c.bytes() +
+                    p.pl_alt.v.bytes() + p.pl_alt.c.bytes());
     out4[2] = (i64)(p.mmap.bytes() + p.fmap16.bytes() + p.sb.bytes());
     out4[3] = p.exch_bytes + (i64)p.q.bytes();
 }
@@ -1676,8 +1795,33 @@ void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
     p.clear_stat();
     if (p.nl > 0) {
-        if (p.map16) wp_pull_light_k<uint16_t><<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.fmap16.p);
-        else wp_pull_light_k<uint8_t><<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.mmap.p);
+        WPart::PullLong& L = p.pl;
+        if (!L.built) {  // the long-row chunk list of this light threshold: count, then fill
+            u64* acc = p.stat.p + ST_ACC;
+            PJ_HIP(hipMemsetAsync(acc, 0, sizeof(u64), s));
+            wp_plong_count_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, s>>>(p.lsplit.p, p.nl, acc);
+            PJ_LAUNCH_CHECK();
+            u64 nc = 0;
+            p.read_acc(&nc, 1);
+            L.v.alloc((size_t)std::max<u64>(nc, 1));
+            L.c.alloc((size_t)std::max<u64>(nc, 1));
+            PJ_HIP(hipMemsetAsync(acc, 0, sizeof(u64), s));
+            if (nc) {
+                wp_plong_fill_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, s>>>(p.lsplit.p, p.nl, acc, L.v.p, L.c.p);
+                PJ_LAUNCH_CHECK();
+            }
+            PJ_HIP(hipMemsetAsync(acc, 0, sizeof(u64), s));
+            L.n = nc;
+            L.built = true;
+        }
+        const WArgs a = p.args(lo, hi);
+        if (L.n) {
+            if (p.map16) wp_pull_long_k<uint16_t><<<p.grid(), WB, 0, s>>>(a, p.fmap16.p, L.v.p, L.c.p, L.n);
+            else wp_pull_long_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, L.v.p, L.c.p, L.n);
+            PJ_LAUNCH_CHECK();
+        }
+        if (p.map16) wp_pull_light_k<uint16_t><<<p.grid(), WB, 0, s>>>(a, p.fmap16.p, WP_PLMAX);
+        else wp_pull_light_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, WP_PLMAX);
         PJ_LAUNCH_CHECK();
     }
 }
@@ -1746,12 +1890,14 @@ void wpart_use_delta(WPart& p, int32_t delta) {
         return;
     }
     std::swap(p.lsplit, p.lsplit_alt);
+    std::swap(p.pl, p.pl_alt);
     std::swap(p.delta, p.delta_alt);
     if (delta == p.delta) return;
     if (!p.lsplit.p) p.lsplit.alloc((size_t)p.nl);
     wp_lsplit_k<<<grid_for(p.nl, 256, p.grid()), 256, 0, p.ctx->stream>>>(p.row.p, p.w.p, p.nl, (u32)delta,
                                                                           p.lsplit.p);
     PJ_LAUNCH_CHECK();
+    p.pl.built = false;
     p.delta = delta;
 }
 

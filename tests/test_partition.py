@@ -363,8 +363,9 @@ def test_wpart_group(pj, oracle, world, transport):
             if r:
                 gr.close()
         g0.close()
+        # (delta 60, light pull always: light rows of hundreds of edges, the long-row chunk list)
         for delta, tf, tm, pf, lp in ((0, 0.1, 64, 4, 3), (7, 2.0, 3, 1e9, 1e9), (60, 0.0, 64, 0, 0),
-                                      (7, 0.1, 64, 1e9, 3), (0, 0.0, 64, 4, 1e9)):
+                                      (7, 0.1, 64, 1e9, 3), (0, 0.0, 64, 4, 1e9), (60, 0.1, 64, 4, 1e9)):
             for p in parts:
                 p.set_option("tail_frac", tf)
                 p.set_option("tail_mult", tm)

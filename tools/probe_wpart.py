@@ -2,7 +2,7 @@
 world 1 (no transport) and world 2 (both ranks on this GPU, host transport): per-solve time
 with the tail switch, the heavy pull and the light pull rounds at their defaults and off, or under the
 given (tail_frac, pull_factor, light_pull[, tail_light_pull = 3]) sets.
-Usage: python tools/probe_wpart.py [scale=26] ["tf,pf,lp[,tlp];tf,pf,lp[,tlp]..."]"""
+Usage: python tools/probe_wpart.py [scale=26] ["tf,pf,lp[,tlp];tf,pf,lp[,tlp]..."] (";" or "/")"""
 import os, sys, time
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
 import numpy as np
@@ -20,7 +20,7 @@ for world in (1, 2):
     parts = [load_weighted_kronecker(ctxs[r], scale, 16, 1, r, world) for r in range(world)]
     sets = ((0.1, 4, 0), (0.1, 4, 0))
     if len(sys.argv) > 2:
-        sets = [tuple(float(x) for x in t.split(",")) for t in sys.argv[2].split(";")]
+        sets = [tuple(float(x) for x in t.split(",")) for t in sys.argv[2].replace("/", ";").split(";")]
     for st4 in sets:
         tf, pf, lp = st4[:3]
         tlp = st4[3] if len(st4) > 3 else 3.0
