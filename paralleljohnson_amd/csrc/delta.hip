@@ -1114,9 +1114,9 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
         const u32 incl = wave_incl_scan(cnt);
         const u32 myex = incl - cnt;
         const u32 T = __shfl(incl, 63, 64);
-        for (u32 r0 = 0; r0 < T; r0 += WAVE) {
-            const u32 c = r0 + lane;
-            const bool act = c < T;
+        // candidate c of the wave's list: its vertex, dist and light-row bounds
+        auto fetch = [&](u32 c, bool& act, i64& v, int32_t& d0, Off& k, u32& ls) {
+            act = c < T;
             u32 jw = 0;
 #pragma unroll
             for (u32 step = PSC / 2; step > 0; step >>= 1) {
@@ -1125,23 +1125,33 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             }
             const u32 ex = __shfl(myex, jw, 64);
             const u64 tw = __shfl(mytodo, jw, 64);
-            const i64 v = act ? (gbase + jw) * 64 + select_bit(tw, c - ex) : 0;
-            int32_t d0 = INT_INF, cur = INT_INF;
-            Off k = 0, e = 0;
-            u32 ls = 0;
+            v = act ? (gbase + jw) * 64 + select_bit(tw, c - ex) : 0;
+            d0 = INT_INF;
+            k = 0;
+            ls = 0;
             if (act) {
                 d0 = a.dist[v];
-                cur = d0;
                 if (a.ltail) {  // the tail: the light prefix of the row in the whole CSR, no long-row list
                     k = row[v];
                     ls = a.lsplit[v];
-                    e = k + (Off)ls;
                 } else {
                     k = (Off)a.lrow[v];
                     ls = (u32)(a.lrow[v + 1] - a.lrow[v]);
-                    e = ls > V2_PLMAX ? k : k + (Off)ls;  // long rows: v2_pull_long_body
                 }
             }
+        };
+        // (round 5: issuing the next 64 candidates' loads before this batch's scan measured
+        // 0.5% slower, profiles/r05/ab_pfx_r5n.txt)
+        for (u32 r0 = 0; r0 < T; r0 += WAVE) {
+            bool act;
+            i64 v;
+            int32_t d0;
+            Off k;
+            u32 ls;
+            fetch(r0 + lane, act, v, d0, k, ls);
+            int32_t cur = d0;
+            Off e = k;
+            if (act) e = (a.ltail || ls <= V2_PLMAX) ? k + (Off)ls : k;  // long rows: v2_pull_long_body
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
             bool go = act && k < lim, done = !act || k >= e;
             while (__ballot(go)) {

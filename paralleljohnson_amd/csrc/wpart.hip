@@ -835,7 +835,9 @@ __global__ void wp_frontier_slice_k(WArgs a, MT* __restrict__ own) {
 }
 // Light rows longer than WP_PLMAX (the hubs, at the lowest ids of the degree order) are
 // pulled by wp_pull_long_k from a static list of (vertex, chunk of WP_PCH light edges),
-// built once per light threshold: scanned inside wp_pull_light_k, one wave walked a hub's
+// built once per light threshold, in the bands before the tail (in the tail the hubs are
+// settled and such a list, of most of the graph's rows at the tail's threshold, cost
+// ~1 ms per solve in skipped chunks): scanned inside wp_pull_light_k, one wave walked a hub's
 // whole light row alone while the rest of the grid idled (an s26w solve whose hubs were
 // unsettled at a light pull took 20-25 ms instead of 10, profiles/r05/wpart_sweep_r5k.txt).
 constexpr u32 WP_PLMAX = 64;
@@ -1794,7 +1796,10 @@ void wpart_frontier_slice(WPart& p, int32_t lo, int32_t hi) {
 void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
     p.clear_stat();
-    if (p.nl > 0) {
+    if (p.nl > 0 && p.map16) {  // the tail's bands (hubs settled; a list would mostly hold settled rows)
+        wp_pull_light_k<uint16_t><<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.fmap16.p, ~0u);
+        PJ_LAUNCH_CHECK();
+    } else if (p.nl > 0) {
         WPart::PullLong& L = p.pl;
         if (!L.built) {  // the long-row chunk list of this light threshold: count, then fill
             u64* acc = p.stat.p + ST_ACC;
@@ -1816,12 +1821,10 @@ void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
         }
         const WArgs a = p.args(lo, hi);
         if (L.n) {
-            if (p.map16) wp_pull_long_k<uint16_t><<<p.grid(), WB, 0, s>>>(a, p.fmap16.p, L.v.p, L.c.p, L.n);
-            else wp_pull_long_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, L.v.p, L.c.p, L.n);
+            wp_pull_long_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, L.v.p, L.c.p, L.n);
             PJ_LAUNCH_CHECK();
         }
-        if (p.map16) wp_pull_light_k<uint16_t><<<p.grid(), WB, 0, s>>>(a, p.fmap16.p, WP_PLMAX);
-        else wp_pull_light_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, WP_PLMAX);
+        wp_pull_light_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, WP_PLMAX);
         PJ_LAUNCH_CHECK();
     }
 }
