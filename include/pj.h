@@ -518,7 +518,8 @@ int pj_part_gather_dist(pj_part* p, pj_comm* comm, int32_t* dist_out);
 int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st);
 /* pj_wpart_set_option keys: "tail_frac" (switch to the tail threshold once the edges of
  * the vertices not settled yet, over all ranks, drop below tail_frac x all edges; 0 = off;
- * default 0.1) and "tail_mult" (tail threshold and band width = tail_mult x delta,
+ * default 0.3 since round 5, profiles/r05/wpart_sweep_r5o.txt) and "tail_mult" (tail
+ * threshold and band width = tail_mult x delta,
  * default 64) and "pull_factor" (heavy steps by pull -- the unsettled vertices scan their
  * heavy rows for band members through an all-gathered byte map -- when the unsettled
  * vertices' heavy edges are fewer than pull_factor x the members'; symmetric graphs only;

@@ -164,7 +164,10 @@ __device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __re
 // Pull screening (v2_pull_k, v2_pull_light_body): a wave reads the dists of PSC
 // groups of 64 vertices, compacts the candidates into lanes, probes PSERIAL edges
 // per lane (wave-uniform loop), then scans the long rows with the whole wave.
-constexpr int PSC = 16;
+#ifndef PJ_PSC
+#define PJ_PSC 16
+#endif
+constexpr int PSC = PJ_PSC;
 #ifndef PJ_PSERIAL
 #define PJ_PSERIAL 32
 #endif

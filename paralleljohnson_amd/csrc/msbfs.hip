@@ -516,10 +516,16 @@ __global__ __launch_bounds__(MB) void ms_level_k(i64 n, const Off* __restrict__ 
 
 // The distance block from the level archive: entries [0, nlev), entry a holding at row v
 // the sources that reached v at level a (valid where bit v of its row bitmap is set). A
-// wave takes 64 consecutive vertices; per mask word it ORs each lane's entries into the
-// five bit planes of the level number (MS_LCAP <= 32), then stores source by source 64
-// consecutive distances (INT_INF where no entry holds the bit).
+// wave takes 64 consecutive vertices; per chunk of up to 8 mask words (one 64-byte line of
+// a row) it ORs each lane's entries into the five bit planes of the level number
+// (MS_LCAP <= 32), then stores source by source 64 consecutive distances (INT_INF where no
+// entry holds the bit), streaming (nontemporal) stores. (A word at a time re-fetched a
+// row's line for every word once the distance stores had pushed it out of L2: 5.4 GB of
+// traffic per 512-source pass against ~2.3 GB of rows and distances, profiles/r05/ms1024_pmc_w8_r5q.txt.)
 constexpr int MS_LCAP = 32;  // archive entries at most (the level number in 5 bit planes)
+#ifndef PJ_MS_JC
+#define PJ_MS_JC 8  // mask words per expansion chunk
+#endif
 template <int W>
 __global__ __launch_bounds__(MB) void ms_expand_k(i64 n, const u64* __restrict__ arch, const u64* __restrict__ zarch,
                                                   i64 nzw, int nlev, int ns, int32_t* __restrict__ dist) {
@@ -531,25 +537,39 @@ __global__ __launch_bounds__(MB) void ms_expand_k(i64 n, const u64* __restrict__
         u32 zm = 0;  // the entries holding a row for v
         for (int a = 0; a < nlev; ++a)
             if ((zarch[(i64)a * nzw + (base >> 6)] >> lane) & 1ull) zm |= 1u << a;
+        constexpr int JC = W < PJ_MS_JC ? W : PJ_MS_JC;
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
-            if (64 * j >= ns) break;
-            u64 any = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0;
+        for (int j0 = 0; j0 < W; j0 += JC) {
+            if (64 * j0 >= ns) break;
+            u64 any[JC], p0[JC], p1[JC], p2[JC], p3[JC], p4[JC];
+#pragma unroll
+            for (int j = 0; j < JC; ++j) any[j] = p0[j] = p1[j] = p2[j] = p3[j] = p4[j] = 0;
             for (u32 m = zm; m; m &= m - 1) {
                 const int a = __ffs((int)m) - 1;
-                const u64 x = arch[((i64)a * n + v) * W + j];
-                any |= x;
-                if (a & 1) p0 |= x;
-                if (a & 2) p1 |= x;
-                if (a & 4) p2 |= x;
-                if (a & 8) p3 |= x;
-                if (a & 16) p4 |= x;
+                u64 x[JC];
+#pragma unroll
+                for (int j = 0; j < JC; ++j) x[j] = arch[((i64)a * n + v) * W + j0 + j];
+#pragma unroll
+                for (int j = 0; j < JC; ++j) {
+                    any[j] |= x[j];
+                    if (a & 1) p0[j] |= x[j];
+                    if (a & 2) p1[j] |= x[j];
+                    if (a & 4) p2[j] |= x[j];
+                    if (a & 8) p3[j] |= x[j];
+                    if (a & 16) p4[j] |= x[j];
+                }
             }
-            const int nb = min(64, ns - 64 * j);
-            for (int b = 0; b < nb; ++b) {
-                const int32_t lv = (int32_t)(((p0 >> b) & 1ull) | (((p1 >> b) & 1ull) << 1) | (((p2 >> b) & 1ull) << 2) |
-                                             (((p3 >> b) & 1ull) << 3) | (((p4 >> b) & 1ull) << 4));
-                if (inr) dist[(i64)(64 * j + b) * n + v] = ((any >> b) & 1ull) ? lv : INT_INF;
+#pragma unroll
+            for (int j = 0; j < JC; ++j) {
+                const int nb = min(64, ns - 64 * (j0 + j));
+                for (int b = 0; b < nb; ++b) {
+                    const int32_t lv =
+                        (int32_t)(((p0[j] >> b) & 1ull) | (((p1[j] >> b) & 1ull) << 1) | (((p2[j] >> b) & 1ull) << 2) |
+                                  (((p3[j] >> b) & 1ull) << 3) | (((p4[j] >> b) & 1ull) << 4));
+                    if (inr)
+                        __builtin_nontemporal_store(((any[j] >> b) & 1ull) ? lv : INT_INF,
+                                                    dist + (i64)(64 * (j0 + j) + b) * n + v);
+                }
             }
         }
     }

@@ -563,6 +563,47 @@ __global__ __launch_bounds__(WB) void wp_qpack_k(WArgs a, int world, u64* __rest
     }
 }
 
+// World 2: every queued pair is the one peer's, so the counts are the regions' fills (one
+// wave: no pass over the pairs) and the pack is a copy of each region's pairs behind the
+// fills of the regions before it (no owner ranking). (round 5: the two general passes took
+// ~0.6 ms per s26w solve and rank, profiles/r05/wpart_timeline_r5m.txt)
+__global__ void wp_qsum2_k(WArgs a, int peer) {
+    const int lane = lane_id();
+    u64 fill = 0, att_sh = 0, att_sp = 0;
+    for (int r = lane; r <= WQ_S; r += WAVE) {
+        const u64 att = a.qctr[(size_t)r * 8];
+        fill += r < WQ_S ? min(att, a.qsh) : min(att, a.qsp);
+        if (r < WQ_S) att_sh += att;
+        else att_sp += att;
+    }
+    fill = wave_sum(fill);
+    att_sh = wave_sum(att_sh);
+    att_sp = wave_sum(att_sp);
+    if (lane == 0) {
+        a.stat[peer] = fill;
+        a.stat[ST_QTOT] = att_sh;
+        a.stat[ST_QSP] = att_sp;
+    }
+}
+__global__ __launch_bounds__(WB) void wp_qcopy2_k(WArgs a, u64* __restrict__ send) {
+    __shared__ u64 s_off;
+    const u32 sh = blockIdx.x % (WQ_S + 1), per = gridDim.x / (WQ_S + 1), c = blockIdx.x / (WQ_S + 1);
+    if (threadIdx.x < WAVE) {  // the fills of the regions before this one
+        u64 f = 0;
+        for (u32 r = threadIdx.x; r < sh; r += WAVE) {
+            const u64 att = a.qctr[(size_t)r * 8];
+            f += r < (u32)WQ_S ? min(att, a.qsh) : min(att, a.qsp);
+        }
+        f = wave_sum(f);
+        if (threadIdx.x == 0) s_off = f;
+    }
+    __syncthreads();
+    u64 cnt;
+    const u64* qs = wp_qregion(a, sh, cnt);
+    u64* dst = send + s_off;
+    for (u64 i = (u64)c * WB + threadIdx.x; i < cnt; i += (u64)per * WB) dst[i] = qs[i];
+}
+
 // received (id | cand << 32) for this rank
 __global__ __launch_bounds__(WB) void wp_apply_k(WArgs a, const u64* __restrict__ recv, i64 nr, int light) {
     __shared__ u64 red[WB / WAVE];
@@ -1031,11 +1072,12 @@ __global__ void wsum_all_k(const u32* __restrict__ w, i64 m, u64* __restrict__ o
     if (lane_id() == 0 && s) atomicAdd(out, s);
 }
 
-// stat[k0, k1) into the host copy, then the sequence word the host spins on (as
-// delta.hip's v2_publish_k)
+// stat[k0, k1) and [k2, k3) into the host copy, then the sequence word the host spins on
+// (as delta.hip's v2_publish_k)
 __global__ __launch_bounds__(256) void wp_publish_k(const u64* __restrict__ stat, u64* __restrict__ host, int k0,
-                                                    int k1, u64* seqp, u64 seq) {
+                                                    int k1, int k2, int k3, u64* seqp, u64 seq) {
     for (int i = k0 + (int)threadIdx.x; i < k1; i += 256) host[i] = stat[i];
+    for (int i = k2 + (int)threadIdx.x; i < k3; i += 256) host[i] = stat[i];
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence_system();
@@ -1070,9 +1112,9 @@ struct PinnedStat {
     // stat[k0, k1) of the device block once the stream's earlier work is done: the host
     // spins on the sequence word (after 0.2 s it synchronizes the stream instead, which
     // surfaces a failed kernel rather than spinning forever)
-    void read(const u64* stat, int k0, int k1, hipStream_t s) {
+    void read(const u64* stat, int k0, int k1, hipStream_t s, int k2 = 0, int k3 = 0) {
         const u64 q = ++seq;
-        wp_publish_k<<<1, 256, 0, s>>>(stat, dev, k0, k1, seq_dev, q);
+        wp_publish_k<<<1, 256, 0, s>>>(stat, dev, k0, k1, k2, k3, seq_dev, q);
         PJ_LAUNCH_CHECK();
         const auto t0 = std::chrono::steady_clock::now();
         while (__atomic_load_n(seqw, __ATOMIC_ACQUIRE) != q) {
@@ -1093,7 +1135,9 @@ struct WPart {
     double mean_w = 1.0;
     int32_t delta = 0;
     int32_t delta_alt = 0;         // the light threshold lsplit_alt was computed for (0 = none)
-    double tail[2] = {0.1, 64.0};  // tail switch (engine.h DeltaSteps): tail_frac (0 = off), threshold / delta
+    double tail[2] = {0.3, 64.0};  // tail switch (engine.h DeltaSteps): tail_frac (0 = off), threshold / delta
+                                   // (tail_frac 0.1 until round 5: 0.3 measured best at s24w / s26w,
+                                   // worlds 1 and 2, profiles/r05/wpart_sweep_r5o.txt)
     double pull_factor = 4.0;      // heavy pull when unsettled heavy edges < pull_factor x members' (0 = push)
     double tail_light_pull = 3.0;  // the same rule after the tail switch (independent of light_pull; 0 =
                                    // push), with a 16-bit frontier map for the tail's wide bands
@@ -1170,7 +1214,8 @@ struct WPart {
         a.sbits = sb_on ? sb.p : nullptr;
         return a;
     }
-    void read_stat() { hstat.read(stat.p, 0, ST_N, ctx->stream); }
+    // (the pack cursors ST_CUR.. are the device's own: every other word)
+    void read_stat() { hstat.read(stat.p, 0, ST_CUR, ctx->stream, ST_QTOT, ST_N); }
     void read_acc(u64* out, int k) {  // stat[ST_ACC, ST_ACC + k) through the host copy
         hstat.read(stat.p, ST_ACC, ST_ACC + k, ctx->stream);
         for (int i = 0; i < k; ++i) out[i] = hstat.p[ST_ACC + i];
@@ -1990,11 +2035,13 @@ static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* s
         else wp_long_k<false><<<p.grid(), WB, 0, s>>>(a);
         PJ_LAUNCH_CHECK();
         if (p.world < 2) break;  // (world 1 sends nothing: no host wait here)
-        wp_qcount_k<<<p.qgrid(), WB, 0, s>>>(a, p.world);
+        if (p.world == 2) wp_qsum2_k<<<1, WAVE, 0, s>>>(a, 1 - p.rank);
+        else wp_qcount_k<<<p.qgrid(), WB, 0, s>>>(a, p.world);
         PJ_LAUNCH_CHECK();
         if (pre) {  // (pairs past a shard's capacity are not packed: an overflow reruns anyway)
             pre->ensure((size_t)p.qcap());
-            wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(a, p.world, pre->p);
+            if (p.world == 2) wp_qcopy2_k<<<p.qgrid(), WB, 0, s>>>(a, pre->p);
+            else wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(a, p.world, pre->p);
             PJ_LAUNCH_CHECK();
         }
         p.read_stat();
@@ -2021,7 +2068,8 @@ static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* s
 void wpart_pack(WPart& p, u64* send) {
     if (p.world < 2) return;
     hipStream_t s = p.ctx->stream;
-    wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(p.args(), p.world, send);
+    if (p.world == 2) wp_qcopy2_k<<<p.qgrid(), WB, 0, s>>>(p.args(), send);
+    else wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(p.args(), p.world, send);
     PJ_LAUNCH_CHECK();
     PJ_HIP(hipStreamSynchronize(s));
     p.pending_pack = false;
