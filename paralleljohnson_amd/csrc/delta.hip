@@ -1117,6 +1117,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
         const u32 incl = wave_incl_scan(cnt);
         const u32 myex = incl - cnt;
         const u32 T = __shfl(incl, 63, 64);
+        if (PJ_V2_STATS && lane == 0 && T) atomicAdd(&a.ctl->dbg[5].v, (u64)T);  // (pull candidates)
         // candidate c of the wave's list: its vertex, dist and light-row bounds
         auto fetch = [&](u32 c, bool& act, i64& v, int32_t& d0, Off& k, u32& ls) {
             act = c < T;
@@ -1157,6 +1158,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             if (act) e = (a.ltail || ls <= V2_PLMAX) ? k + (Off)ls : k;  // long rows: v2_pull_long_body
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
             bool go = act && k < lim, done = !act || k >= e;
+            const Off kst = k;  // (PJ_V2_STATS: edges scanned)
             while (__ballot(go)) {
                 if (go) {
                     if (pull_step_fin_cw<Off>(v2_light_src(a), a.dist, lfin, k, lim, lo, hi, cur)) {
@@ -1168,6 +1170,10 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                     }
                 }
             }
+            if (PJ_V2_STATS) {
+                const u64 sc = wave_sum(act ? (u64)(k - kst) : 0ull);
+                if (lane == 0 && sc) atomicAdd(&a.ctl->dbg[6].v, sc);
+            }
             u64 open = __ballot(!done);
             while (open) {
                 const int l = __ffsll((long long)open) - 1;
@@ -1175,6 +1181,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                 const Off kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
                 int32_t cl = __shfl(cur, l, 64);
                 for (Off kk = kb; kk < ke; kk += WAVE) {
+                    if (PJ_V2_STATS && lane == 0) atomicAdd(&a.ctl->dbg[6].v, (u64)min((Off)WAVE, ke - kk));
                     const Off k0 = kk + lane;
                     const bool valid = k0 < ke;
                     const u64 x = valid ? eat(v2_light_src(a), (u64)k0) : 0ull;
@@ -1240,6 +1247,7 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
         if ((long long)lo + (eat(v2_light_src(a), kb) >> 32) >= (long long)d0) continue;
         int32_t cur = d0;
         for (u64 kk = kb; kk < ke; kk += WAVE) {
+            if (PJ_V2_STATS && lane == 0) atomicAdd(&a.ctl->dbg[7].v, min((u64)WAVE, ke - kk));
             const u64 k0 = kk + lane;
             const bool valid = k0 < ke;
             const u64 x = valid ? eat(v2_light_src(a), k0) : 0ull;
@@ -1912,9 +1920,11 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                     ml += v.hctl->mh[i].pad[0];
                 }
                 if (PJ_V2_STATS) {
-                    fprintf(stderr, "band %d lo %lld rounds %d: frontier %llu edges %llu atomicmin %llu atomicor %llu marks %llu next %llu\n",
+                    fprintf(stderr, "band %d lo %lld rounds %d: frontier %llu edges %llu atomicmin %llu atomicor %llu marks %llu next %llu"
+                            " | pull candidates %llu short-row edges %llu long-chunk edges %llu\n",
                             (int)st.levels, lo, K, v.hctl->dbg[0].v, v.hctl->dbg[1].v, v.hctl->dbg[2].v,
-                            v.hctl->dbg[4].v, v.hctl->dbg[3].v, slot(cs));
+                            v.hctl->dbg[4].v, v.hctl->dbg[3].v, slot(cs), v.hctl->dbg[5].v, v.hctl->dbg[6].v,
+                            v.hctl->dbg[7].v);
                     PJ_HIP(hipMemsetAsync(v.ctl.p->dbg, 0, sizeof(v.ctl.p->dbg), s));
                 }
                 if (slot(cs) == 0) break;
