@@ -101,6 +101,7 @@ __device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
 #ifndef PJ_V2_NOFIN
 #define PJ_V2_NOFIN 2
 #endif
+
 // (Round 5: the bits probed first again on sparse rounds only -- light pull rounds whose
 // frontier is below n / 16 or n / 64, heavy pulls whose members hold below nnz / 16 edges --
 // measured 1-2% slower or equal, profiles/r05/ab_fbits_r5i.txt: dist alone everywhere.)
@@ -1225,7 +1226,9 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
 }
 
 // Long light rows (lsplit > V2_PLMAX, the high-degree vertices) are left out of
-// v2_pull_light_body: one lane scanning tens of thousands of edges would hold up
+// v2_pull_light_body (round 5: chunks that published an improvement at once and re-read
+// the row's distance every 64 edges scanned as many edges -- the hubs' rows hold their
+// first frontier neighbour late -- and measured 0.5% slower, profiles/r05/ab_lpub_r5t.txt): one lane scanning tens of thousands of edges would hold up
 // its wave. Their pull runs here instead, over a static list of (vertex, chunk
 // of V2_PCH light edges) built once per delta; a wave takes a chunk, skips it
 // when even its lightest edge cannot help, and folds the result in with
