@@ -408,9 +408,10 @@ int pj_wpart_info(const pj_wpart* p, int64_t* out);
  * settled map: the analogue of the BFS pull's visited bitmap); the claim queue and
  * the exchange buffers, sized to the largest round's pairs. Building a block with
  * the per-block degree order (pj_wpart_generate_kronecker, pj_wpart_from_graph,
- * pj_wpart_load_snap) also holds ~20 bytes per vertex of the WHOLE graph for a
- * moment (every vertex's degree, the sort keys and the relabel table, which all
- * ranks must agree on); none of it stays. */
+ * pj_wpart_load_snap) also holds 8 bytes per vertex of the WHOLE graph for a moment
+ * (every vertex's degree and the relabel table of all blocks, which the rank's column
+ * ids go through; 20 bytes until round 5), plus 16 bytes per vertex of one block for
+ * the block-by-block sort; none of it stays. */
 int pj_wpart_device_bytes(const pj_wpart* p, int64_t* out);
 /* Start a solve from `source` (dist := INF, then the source); delta <= 0 picks
  * the single-GPU default (3.5 x mean weight / mean degree). *delta_out = delta. */

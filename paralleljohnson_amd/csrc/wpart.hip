@@ -1375,19 +1375,16 @@ __global__ void wp_deg_key_k(const u32* __restrict__ deg, i64 n, u32 maxdeg, u32
         ids[v] = (u32)v;
     }
 }
-__global__ void wp_blk_key_k(const u32* __restrict__ ids, i64 n, i64 block, u32* __restrict__ key) {
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
-        key[i] = (u32)((i64)ids[i] / block);
+// block q's part of the global map: its vertex lo_q + order[i] becomes lo_q + i
+__global__ void wp_inv_blk_k(const u32* __restrict__ order, i64 nq, i64 lo_q, u32* __restrict__ inv) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += (i64)gridDim.x * blockDim.x)
+        inv[lo_q + order[i]] = (u32)(lo_q + i);
 }
-__global__ void wp_inv_k(const u32* __restrict__ order, i64 n, u32* __restrict__ inv) {
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
-        inv[order[i]] = (u32)i;
-}
-// new local row l = old local row order[lo + l] - lo: its degree, and the old local -> new local map
+// new local row l = old local row order[l]: its degree, and the old local -> new local map
 __global__ void wp_newdeg_k(const u32* __restrict__ order, const u32* __restrict__ inv, const u64* __restrict__ row,
                             i64 lo, i64 nl, u32* __restrict__ ndeg, u32* __restrict__ linv) {
     for (i64 l = (i64)blockIdx.x * blockDim.x + threadIdx.x; l < nl; l += (i64)gridDim.x * blockDim.x) {
-        const i64 o = (i64)order[lo + l] - lo;
+        const i64 o = (i64)order[l];
         ndeg[l] = (u32)(row[o + 1] - row[o]);
         linv[l] = (u32)((i64)inv[lo + l] - lo);
     }
@@ -1400,7 +1397,7 @@ __global__ __launch_bounds__(256) void wp_copy_rows_k(const u32* __restrict__ or
     const int lane = lane_id();
     for (i64 l = ((i64)blockIdx.x * blockDim.x + threadIdx.x) / WAVE; l < nl;
          l += (i64)gridDim.x * blockDim.x / WAVE) {
-        const i64 o = (i64)order[lo + l] - lo;
+        const i64 o = (i64)order[l];
         const u64 b = row[o], e = row[o + 1], nb = nrow[l];
         for (u64 k = b + (u64)lane; k < e; k += WAVE) {
             ncol[nb + (k - b)] = inv[col[k]];
@@ -1506,7 +1503,12 @@ __global__ __launch_bounds__(256) void wp_kron_write_k(int scale, u64 seed, Perm
 }  // namespace
 
 namespace {
-// Relabel a built block (rows, col, w in input ids) given the degrees of every vertex.
+// Relabel a built block (rows, col, w in input ids) given the degrees of every vertex:
+// within every block the vertices in descending degree (ties by id), so the new ids stay in
+// their block. The blocks are ordered one at a time (block-sized sort buffers), so the
+// transient device memory is the degrees and the global map, 8 N bytes, plus 16 x block
+// (round 4 sorted all N vertices at once: 20 N bytes); the graph's col ids go through the
+// map, which is why it is global.
 void wpart_relabel(WPart& p, DevBuf<u32>& deg) {
     hipStream_t s = p.ctx->stream;
     const i64 n = p.n;
@@ -1519,37 +1521,40 @@ void wpart_relabel(WPart& p, DevBuf<u32>& deg) {
     u32 maxdeg = 0;
     PJ_HIP(hipMemcpyAsync(&maxdeg, mx.p, sizeof(u32), hipMemcpyDeviceToHost, s));
     PJ_HIP(hipStreamSynchronize(s));
-    DevBuf<u32> key((size_t)n), kalt((size_t)n), ids((size_t)n), valt((size_t)n);
-    wp_deg_key_k<<<grid_for(n, 256, grid), 256, 0, s>>>(deg.p, n, maxdeg, key.p, ids.p);
-    PJ_LAUNCH_CHECK();
-    deg.release();
-    SortWs ws;
-    int bits = 1;
-    while (bits < 32 && ((u64)1 << bits) <= (u64)maxdeg) ++bits;
-    u32 *kr, *vr;
-    radix_sort_pairs<u32>(key.p, kalt.p, ids.p, valt.p, n, bits, ws, s, &kr, &vr);
-    u32* kfree = kr == key.p ? kalt.p : key.p;  // the key buffer not holding the result
-    wp_blk_key_k<<<grid_for(n, 256, grid), 256, 0, s>>>(vr, n, p.block, kr);
-    PJ_LAUNCH_CHECK();
-    int bb = 1;
-    while (bb < 32 && ((u64)1 << bb) <= (u64)p.world) ++bb;
-    u32* valt2 = vr == ids.p ? valt.p : ids.p;
-    u32 *kr2, *order;
-    radix_sort_pairs<u32>(kr, kfree, vr, valt2, n, bb, ws, s, &kr2, &order);
-    u32* inv = order == ids.p ? valt.p : ids.p;  // the free value buffer
-    wp_inv_k<<<grid_for(n, 256, grid), 256, 0, s>>>(order, n, inv);
-    PJ_LAUNCH_CHECK();
     const i64 nl = p.nl;
+    const size_t bsz = (size_t)std::max<i64>(1, std::min<i64>(p.block, n));
+    DevBuf<u32> inv((size_t)n), own((size_t)std::max<i64>(nl, 1));  // the global map, this block's order
+    {
+        DevBuf<u32> key(bsz), kalt(bsz), ids(bsz), valt(bsz);
+        SortWs ws;
+        int bits = 1;
+        while (bits < 32 && ((u64)1 << bits) <= (u64)maxdeg) ++bits;
+        for (int q = 0; q < p.world; ++q) {
+            const i64 lo_q = (i64)q * p.block, nq = std::min<i64>(p.block, n - lo_q);
+            if (nq <= 0) break;
+            wp_deg_key_k<<<grid_for(nq, 256, grid), 256, 0, s>>>(deg.p + lo_q, nq, maxdeg, key.p, ids.p);
+            PJ_LAUNCH_CHECK();
+            u32 *kr, *vr;  // (stable: ties keep ascending ids)
+            radix_sort_pairs<u32>(key.p, kalt.p, ids.p, valt.p, nq, bits, ws, s, &kr, &vr);
+            wp_inv_blk_k<<<grid_for(nq, 256, grid), 256, 0, s>>>(vr, nq, lo_q, inv.p);
+            PJ_LAUNCH_CHECK();
+            if (q == p.rank && nl > 0)
+                PJ_HIP(hipMemcpyAsync(own.p, vr, sizeof(u32) * (size_t)nl, hipMemcpyDeviceToDevice, s));
+        }
+        PJ_HIP(hipStreamSynchronize(s));
+    }
+    deg.release();
+    const u32* order = own.p;
     DevBuf<u32> ndeg((size_t)std::max<i64>(nl, 1));
     p.rl_inv.alloc((size_t)std::max<i64>(nl, 1));
     DevBuf<u64> nrow((size_t)nl + 1);
     if (nl > 0) {
-        wp_newdeg_k<<<grid_for(nl, 256, grid), 256, 0, s>>>(order, inv, p.row.p, p.lo, nl, ndeg.p, p.rl_inv.p);
+        wp_newdeg_k<<<grid_for(nl, 256, grid), 256, 0, s>>>(order, inv.p, p.row.p, p.lo, nl, ndeg.p, p.rl_inv.p);
         PJ_LAUNCH_CHECK();
         ScanWs sw;
         exclusive_scan_u32(ndeg.p, nrow.p, nl, sw, s);
         DevBuf<u32> ncol((size_t)std::max<i64>(p.nnz_local, 1)), nw((size_t)std::max<i64>(p.nnz_local, 1));
-        wp_copy_rows_k<<<grid_for(nl * WAVE, 256, grid), 256, 0, s>>>(order, inv, p.row.p, p.col.p, p.w.p, nrow.p,
+        wp_copy_rows_k<<<grid_for(nl * WAVE, 256, grid), 256, 0, s>>>(order, inv.p, p.row.p, p.col.p, p.w.p, nrow.p,
                                                                       p.lo, nl, ncol.p, nw.p);
         PJ_LAUNCH_CHECK();
         PJ_HIP(hipStreamSynchronize(s));
