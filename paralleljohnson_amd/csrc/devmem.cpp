@@ -14,7 +14,9 @@
 // of a block a world-1 build freed); a freed slice merges with its free neighbours. A
 // request that fails while the cache holds blocks returns every wholly free block to the
 // driver and tries again, so the cache never costs an allocation that would otherwise
-// succeed.
+// succeed. A big free synchronizes the block's device first, as hipFree does: work still
+// in flight on any stream may use the memory, and the next owner of a slice may be another
+// stream (another rank's, or another batch slot's).
 #include <algorithm>
 #include <iterator>
 #include <map>
@@ -132,12 +134,25 @@ void dev_free(void* p, size_t bytes) {
         return;
     }
     BigCache& c = cache();
+    int bdev = -1;
+    {
+        std::lock_guard<std::mutex> lk(c.mu);
+        auto it = c.live.find(p);
+        if (it == c.live.end()) {  // (not from dev_alloc's big path; DevBuf never does this)
+            (void)hipFree(p);
+            return;
+        }
+        bdev = it->second.first->dev;
+    }
+    {  // (hipFree's implicit synchronization, on the block's device)
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != bdev) (void)hipSetDevice(bdev);
+        (void)hipDeviceSynchronize();
+        if (cur != bdev && cur >= 0) (void)hipSetDevice(cur);
+    }
     std::lock_guard<std::mutex> lk(c.mu);
     auto it = c.live.find(p);
-    if (it == c.live.end()) {  // (not from dev_alloc's big path; DevBuf never does this)
-        (void)hipFree(p);
-        return;
-    }
     Blk* b = it->second.first;
     size_t off = (size_t)(static_cast<char*>(p) - b->base), len = it->second.second;
     c.live.erase(it);
