@@ -585,9 +585,36 @@ __global__ void wp_qsum2_k(WArgs a, int peer) {
         a.stat[ST_QSP] = att_sp;
     }
 }
-__global__ __launch_bounds__(WB) void wp_qcopy2_k(WArgs a, u64* __restrict__ send) {
+// (host != null: block 0 also publishes the counts -- the peer's fill and the overflow
+// counters -- into the host copy of the stat block and bumps its sequence word, so the
+// relax step needs no publish launch: the pack's own consumers are stream-ordered)
+__global__ __launch_bounds__(WB) void wp_qcopy2_k(WArgs a, u64* __restrict__ send, int rank, u64* __restrict__ host,
+                                                  u64* seqp, u64 seq) {
     __shared__ u64 s_off;
     const u32 sh = blockIdx.x % (WQ_S + 1), per = gridDim.x / (WQ_S + 1), c = blockIdx.x / (WQ_S + 1);
+    if (host && blockIdx.x == 0 && threadIdx.x < WAVE) {
+        u64 fill = 0, att_sh = 0, att_sp = 0;
+        for (int r = (int)threadIdx.x; r <= WQ_S; r += WAVE) {
+            const u64 att = a.qctr[(size_t)r * 8];
+            fill += r < WQ_S ? min(att, a.qsh) : min(att, a.qsp);
+            if (r < WQ_S) att_sh += att;
+            else att_sp += att;
+        }
+        fill = wave_sum(fill);
+        att_sh = wave_sum(att_sh);
+        att_sp = wave_sum(att_sp);
+        if (threadIdx.x == 0) {
+            a.stat[1 - rank] = fill;
+            a.stat[ST_QTOT] = att_sh;
+            a.stat[ST_QSP] = att_sp;
+            host[rank] = 0;
+            host[1 - rank] = fill;
+            host[ST_QTOT] = att_sh;
+            host[ST_QSP] = att_sp;
+            __threadfence_system();
+            __hip_atomic_store(seqp, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     if (threadIdx.x < WAVE) {  // the fills of the regions before this one
         u64 f = 0;
         for (u32 r = threadIdx.x; r < sh; r += WAVE) {
@@ -1113,9 +1140,13 @@ struct PinnedStat {
     // spins on the sequence word (after 0.2 s it synchronizes the stream instead, which
     // surfaces a failed kernel rather than spinning forever)
     void read(const u64* stat, int k0, int k1, hipStream_t s, int k2 = 0, int k3 = 0) {
-        const u64 q = ++seq;
+        const u64 q = next();
         wp_publish_k<<<1, 256, 0, s>>>(stat, dev, k0, k1, k2, k3, seq_dev, q);
         PJ_LAUNCH_CHECK();
+        wait(q, s);
+    }
+    u64 next() { return ++seq; }  // the sequence value the next publication writes
+    void wait(u64 q, hipStream_t s) {
         const auto t0 = std::chrono::steady_clock::now();
         while (__atomic_load_n(seqw, __ATOMIC_ACQUIRE) != q) {
             if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
@@ -2040,16 +2071,23 @@ static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* s
         else wp_long_k<false><<<p.grid(), WB, 0, s>>>(a);
         PJ_LAUNCH_CHECK();
         if (p.world < 2) break;  // (world 1 sends nothing: no host wait here)
-        if (p.world == 2) wp_qsum2_k<<<1, WAVE, 0, s>>>(a, 1 - p.rank);
-        else wp_qcount_k<<<p.qgrid(), WB, 0, s>>>(a, p.world);
-        PJ_LAUNCH_CHECK();
-        if (pre) {  // (pairs past a shard's capacity are not packed: an overflow reruns anyway)
+        if (p.world == 2 && pre) {  // count, pack and publish in one launch
             pre->ensure((size_t)p.qcap());
-            if (p.world == 2) wp_qcopy2_k<<<p.qgrid(), WB, 0, s>>>(a, pre->p);
-            else wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(a, p.world, pre->p);
+            const u64 q = p.hstat.next();
+            wp_qcopy2_k<<<p.qgrid(), WB, 0, s>>>(a, pre->p, p.rank, p.hstat.dev, p.hstat.seq_dev, q);
             PJ_LAUNCH_CHECK();
+            p.hstat.wait(q, s);
+        } else {
+            if (p.world == 2) wp_qsum2_k<<<1, WAVE, 0, s>>>(a, 1 - p.rank);
+            else wp_qcount_k<<<p.qgrid(), WB, 0, s>>>(a, p.world);
+            PJ_LAUNCH_CHECK();
+            if (pre) {  // (pairs past a shard's capacity are not packed: an overflow reruns anyway)
+                pre->ensure((size_t)p.qcap());
+                wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(a, p.world, pre->p);
+                PJ_LAUNCH_CHECK();
+            }
+            p.read_stat();
         }
-        p.read_stat();
         if (p.hstat[ST_QSP] <= p.qsp) break;
         if (attempt > 8) throw Error(PJ_ERR_HIP, "wpart relax: the claim queue keeps overflowing (internal error)");
         // shards at twice the round's average, the spill at the round's pairs (a rerun tries more
@@ -2073,7 +2111,7 @@ static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* s
 void wpart_pack(WPart& p, u64* send) {
     if (p.world < 2) return;
     hipStream_t s = p.ctx->stream;
-    if (p.world == 2) wp_qcopy2_k<<<p.qgrid(), WB, 0, s>>>(p.args(), send);
+    if (p.world == 2) wp_qcopy2_k<<<p.qgrid(), WB, 0, s>>>(p.args(), send, p.rank, nullptr, nullptr, 0);
     else wp_qpack_k<<<p.qgrid(), WB, 0, s>>>(p.args(), p.world, send);
     PJ_LAUNCH_CHECK();
     PJ_HIP(hipStreamSynchronize(s));
