@@ -219,7 +219,8 @@ int pj_sssp_batch_write(pj_graph* g, const int64_t* sources, int n_src, const ch
 int pj_last_stats(const pj_graph* g, pj_stats* out);
 int pj_reach_stats(pj_graph* g, pj_stats* out);
 /* Tuning knobs: alpha/beta of the direction switch (Beamer), delta for
- * delta-stepping (0 = automatic), direction (0 auto, 1 push, 2 pull),
+ * delta-stepping (0 = automatic: c(n) x mean weight / mean out-degree, c(n) =
+ * 0.1875 log2(n) - 1.875 within [2, 3.5], swept on Kronecker s22-s26), direction (0 auto, 1 push, 2 pull),
  * bfs_small (one-workgroup levels for small frontiers, 0/1), batch_streams
  * (weighted batches: solves in flight, 1-8) and the batch / grid knobs
  * documented in DESIGN.md. Returns PJ_ERR_ARG on bad values. */
@@ -414,7 +415,8 @@ int pj_wpart_info(const pj_wpart* p, int64_t* out);
  * the block-by-block sort; none of it stays. */
 int pj_wpart_device_bytes(const pj_wpart* p, int64_t* out);
 /* Start a solve from `source` (dist := INF, then the source); delta <= 0 picks
- * the single-GPU default (3.5 x mean weight / mean degree). *delta_out = delta. */
+ * the single-GPU default (c(n) x mean weight / mean degree, c(n) = 0.1875 log2(n) -
+ * 1.875 within [2, 3.5]: 12 on Kronecker s26 with weights 1..255). *delta_out = delta. */
 int pj_wpart_begin(pj_wpart* p, int64_t source, int32_t delta, int32_t* delta_out);
 /* Band [lo, hi): frontier := owned vertices with dist in [lo, hi). out[2] =
  * (its size, min owned dist >= lo or PJ_INT_INF). */

@@ -1578,11 +1578,9 @@ void light_csr_tiled(const Relabeled& R, const Off* row, const DeltaWork& w, u64
                                                                   ltrow, out, cb);
 }
 
-// delta (explicit option, else 3.5 * mean weight / mean out-degree over all input
-// ids: light edges are then ~5% of a row; swept on Kronecker s26 with weights
-// 1..255 together with the tail switch, profiles/r01/tail_sweep.txt) and, once
-// per delta, the light
-// prefix length of every row and the number of heavy edges.
+// delta (explicit option, else auto_delta: c(n) x mean weight / mean out-degree over all
+// input ids, internal.h; light edges are then ~4-5% of a row) and, once per delta, the
+// light prefix length of every row and the number of heavy edges.
 int32_t tail_delta_of(const Graph& g, int32_t delta) {
     return (int32_t)std::min(65536.0, g.tail_delta < 0 ? 64.0 * delta : g.tail_delta);
 }
@@ -1596,11 +1594,7 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
     const Off* row = static_cast<const Off*>(R.row_ptr(g.off64));
     const unsigned maxgrid = (unsigned)ctx.cu_count * 8u;
     int32_t delta = (int32_t)g.delta;
-    if (delta <= 0) {
-        const double mean_deg = g.n ? (double)g.nnz / (double)g.n : 1.0;
-        const double d = 3.5 * g.mean_weight / std::max(1.0, mean_deg);
-        delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(d)));
-    }
+    if (delta <= 0) delta = (int32_t)auto_delta((double)g.n, (double)g.nnz, g.mean_weight);
     w.maxw = std::max(0ll, g.max_weight);  // (the relabel copy's reduction; the relabeled weights are the same)
     // whole-CSR records: u32 ids + u8 weights (split) when every weight fits 8 bits (the
     // relabel copy then wrote them as u8), else the interleaved u64 copy

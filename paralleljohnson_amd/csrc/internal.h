@@ -8,6 +8,7 @@
 #include <functional>
 #include <memory>
 #include <stdexcept>
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -92,6 +93,18 @@ struct PinnedBuf {
         if (count) PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), count * sizeof(T), hipHostMallocDefault));
     }
 };
+
+// The automatic light threshold of the weighted solvers (v2 and the weighted partition):
+// delta = c(n) x mean weight / mean out-degree, c(n) = 0.1875 log2(n) - 1.875 within
+// [2, 3.5]. Round 5 re-swept delta on Kronecker weights 1..255, edgefactor 16
+// (profiles/r05/delta_sweep_r5ag.txt): the best delta was 8-10 at s22, 10-11 at s24 and 12
+// at s26 (c = 2.25, 2.6, 3.0), against the constant 3.5 (delta 14) of round 1; +38%, +19%
+// and +4% GTEPS.
+inline double auto_delta(double n, double nnz, double mean_w) {
+    const double mean_deg = n > 0 ? nnz / n : 1.0;
+    const double c = std::min(3.5, std::max(2.0, 0.1875 * std::log2(std::max(n, 2.0)) - 1.875));
+    return std::max(1.0, std::min(65536.0, std::round(c * mean_w / std::max(1.0, mean_deg))));
+}
 
 inline unsigned grid_for(i64 work, int per_block, unsigned cap = 256u * 16u) {
     i64 g = (work + per_block - 1) / per_block;
@@ -205,7 +218,8 @@ struct Graph {
     double band_width = 0.0;   // v2: width of a band [lo, lo + band_width) (0 = delta, at most delta)
     double tail_delta = -1.0;  // v2: light threshold and band width of the tail (0 = off, < 0 = 64 x delta):
     int tail_after = 1;        // from the first band >= tail_after at which the edges of unsettled
-    double tail_frac = 0.1;    // vertices are < tail_frac x nnz (profiles/r01/tail_sweep.txt)
+    double tail_frac = 0.2;    // vertices are < tail_frac x nnz (profiles/r01/tail_sweep.txt; 0.1 until
+                               // round 5: 0.2 +1% at s22w-s26w with the round-5 delta, delta_sweep_r5ag.txt)
     double light_pull = 3.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
                                // the light edges of unsettled vertices / light_pull (0 = never; 2 -> 3 at
                                // the end of round 2 with merged rounds: +1%, interleaved A/B)

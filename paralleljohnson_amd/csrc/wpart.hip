@@ -1991,8 +1991,7 @@ void wpart_set_delta(WPart& p, int32_t delta) { wpart_use_delta(p, delta); }
 int32_t wpart_begin(WPart& p, i64 source, int32_t delta) {
     hipStream_t s = p.ctx->stream;
     if (delta <= 0) {
-        const double mean_deg = p.n ? (double)p.nnz / (double)p.n : 1.0;
-        delta = (int32_t)std::max(1.0, std::min(65536.0, std::round(3.5 * p.mean_w / std::max(1.0, mean_deg))));
+        delta = (int32_t)auto_delta((double)p.n, (double)p.nnz, p.mean_w);  // (the single-GPU rule)
     }
     wpart_use_delta(p, delta);
     p.sb_on = false;
