@@ -670,6 +670,12 @@ def test_partitioned_weighted_s22_world2(ctx, pj):
         assert 0 < b["exchange"] <= 8 * (2 * (3 * sent + q0) + 1.25 * sent * world), (b, sent)
         assert b["exchange"] < 24 * (1 << 22) / 4, b
     row, col, w = gs[0].get_csr()
+    # the automatic delta (both solvers' rule, internal.h auto_delta): c(n) x mean weight /
+    # mean out-degree, c = 0.1875 log2(n) - 1.875 within [2, 3.5] -- 2.25 at s22
+    n = len(row) - 1
+    mean_w = int(w.astype(np.int64).sum()) / len(col)  # (the generator's exact sum / 2M, as wpart's)
+    exp_delta = int(np.floor(2.25 * mean_w / (len(col) / n) + 0.5))
+    assert st[0]["delta"] == exp_delta, (st[0]["delta"], exp_delta)
     for p in parts:
         p.close()
     for g in gs:
