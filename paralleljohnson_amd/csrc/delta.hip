@@ -283,6 +283,9 @@ struct V2Ctl {
     V2Line minv[V2_NSH];    // min dist >= lo of the last select / pull (next band search), per shard
     V2Line dbg[8];          // PJ_V2_STATS builds: vertices, edges, atomics, marks, hub edges
 };
+#ifndef PJ_V2_FMIN
+#define PJ_V2_FMIN 1  // light pulls stop rows at the frontier's least distance (v2_flush_fmin)
+#endif
 #ifndef PJ_V2_PSTATS
 #define PJ_V2_PSTATS 0  // debug build: heavy-pull scan-length counters (printed per solve)
 #endif
@@ -364,6 +367,38 @@ __device__ __forceinline__ void v2_flush_min(int32_t mn, V2Ctl* ctl, u64* red) {
     }
     __syncthreads();
 }
+// The least distance the frontier of a count slot holds (.pad[1], PJ_V2_FMIN): every
+// write that lowers a vertex into the band is folded in (a relaxation that marks, a pull's
+// store, the selection of a band's first frontier), so it bounds the frontier from below
+// and a pull round can stop a row at fmin + w >= its best instead of lo + w.
+__device__ __forceinline__ void v2_flush_fmin(int32_t m, V2Line* sl, u64* red) {
+    if (!PJ_V2_FMIN) return;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int32_t y = __shfl_xor(m, off, 64);
+        m = y < m ? y : m;
+    }
+    if (lane_id() == 0) red[wave_id()] = (u64)(u32)m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t b = INT_INF;
+        for (int w = 0; w < DB / WAVE; ++w) b = min(b, (int32_t)(u32)red[w]);
+        if (b < INT_INF) atomicMin(&sl[blockIdx.x % V2_NSH].pad[1], (u64)b);
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ int32_t v2_slot_fmin(const V2Line* sl) {
+    u64 m = ~0ull;
+#pragma unroll
+    for (int i = 0; i < V2_NSH; ++i) m = sl[i].pad[1] < m ? sl[i].pad[1] : m;
+    return m < (u64)INT_INF ? (int32_t)m : INT_INF;
+}
+// the frontier bound of a pull round over slot c: max(lo, fmin), or lo without one
+__device__ __forceinline__ int32_t v2_pull_lo(const V2Args& a, int c) {
+    if (!PJ_V2_FMIN) return a.lo;
+    const int32_t f = v2_slot_fmin(a.ctl->cnt[c]);
+    return (f > a.lo && f < a.hi) ? f : a.lo;
+}
 __device__ __forceinline__ u64 v2_slot_edges(const V2Line* sl) {
     u64 t = 0;
 #pragma unroll
@@ -383,7 +418,7 @@ __device__ __forceinline__ u64 v2_slot_edges(const V2Line* sl) {
 template <bool LIGHT, int N>
 __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const u64 (&idx)[N],
                                           const int32_t (&du)[N], const bool (&val)[N], u64* __restrict__ fout,
-                                          u64& fe) {
+                                          u64& fe, int32_t& fm) {
     u32 t[N];
     long long nd[N];
     bool ok[N];
@@ -418,6 +453,7 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
             if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
         }
         mk[j] = LIGHT && imp && (int32_t)nd[j] < a.hi;
+        if (PJ_V2_FMIN && mk[j] && (int32_t)nd[j] < fm) fm = (int32_t)nd[j];
     }
     if (!LIGHT) return 0u;
     u32 newc = 0;
@@ -437,7 +473,7 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
 // PU consecutive edges [k, min(k + PU, lim)) of one source in one step
 template <bool LIGHT>
 __device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const ESrc ed, u64 k, u64 lim, int32_t du,
-                                          u64* __restrict__ fout, u64& fe) {
+                                          u64* __restrict__ fout, u64& fe, int32_t& fm) {
     u64 idx[PU];
     int32_t d[PU];
     bool val[PU];
@@ -447,17 +483,17 @@ __device__ __forceinline__ u32 v2_relax_n(const V2Args& a, const ESrc ed, u64 k,
         d[j] = du;
         val[j] = k + j < lim;
     }
-    return v2_relax_g<LIGHT, PU>(a, ed, idx, d, val, fout, fe);
+    return v2_relax_g<LIGHT, PU>(a, ed, idx, d, val, fout, fe, fm);
 }
 
 // one relaxation
 template <bool LIGHT>
 __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, int32_t du, u64* __restrict__ fout,
-                                        u64& fe) {
+                                        u64& fe, int32_t& fm) {
     const u64 idx[1] = {k};
     const int32_t d[1] = {du};
     const bool val[1] = {true};
-    return v2_relax_g<LIGHT, 1>(a, ed, idx, d, val, fout, fe);
+    return v2_relax_g<LIGHT, 1>(a, ed, idx, d, val, fout, fe, fm);
 }
 
 // Hub queue appends (whole wave; lanes with hub = true hand their segment [b, e) to the
@@ -542,7 +578,7 @@ __device__ __forceinline__ u32 v2_dense_find(const u32* off, u32 ns, u32 e) {
 template <typename Off>
 __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __restrict__ row, u64* __restrict__ fin,
                                               u64* __restrict__ fout, int hs, u32& newc, u64& fe, u64& mh, u64& ml,
-                                              V2Dense<Off>& sh) {
+                                              int32_t& fm, V2Dense<Off>& sh) {
     const int tid = threadIdx.x;
     const u64 mask = (1ull << V2_EB) - 1ull;
     const ESrc ed = v2_light_src(a);
@@ -634,7 +670,7 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
                 idx[j] = val[j] ? (u64)sh.b[sl] + (x - sh.off[sl]) : 0ull;
                 dj[j] = val[j] ? sh.du[sl] : 0;
             }
-            newc += v2_relax_g<true, V2_DNJ>(a, ed, idx, dj, val, fout, fe);
+            newc += v2_relax_g<true, V2_DNJ>(a, ed, idx, dj, val, fout, fe, fm);
         }
         __syncthreads();
     }
@@ -653,6 +689,7 @@ __device__ __forceinline__ void v2_zero_slot(const V2Args& a, int c) {
     if (blockIdx.x == 0 && threadIdx.x < V2_NSH) {
         a.ctl->cnt[c][threadIdx.x].v = 0;
         a.ctl->cnt[c][threadIdx.x].pad[0] = 0;
+        a.ctl->cnt[c][threadIdx.x].pad[1] = (u64)INT_INF;
     }
 }
 
@@ -675,6 +712,7 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
     const int lane = lane_id();
     u32 newc = 0;
     u64 mh = 0, ml = 0, fe = 0;
+    int32_t fm = INT_INF;
     const i64 nsc = (a.nwords + V2_SC - 1) / V2_SC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
         const i64 wbase = sc * V2_SC;
@@ -761,7 +799,7 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
             bool go = k < lim;
             while (__ballot(go)) {
                 if (go) {
-                    newc += v2_relax_n<LIGHT>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), k, lim, du, fout, fe);
+                    newc += v2_relax_n<LIGHT>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), k, lim, du, fout, fe, fm);
                     k = k + PU < lim ? k + PU : lim;
                     go = k < lim;
                 }
@@ -783,13 +821,15 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
                     const u64 kl = __shfl(k, l, 64), xl = __shfl(exc, l, 64);
                     const int32_t dl = __shfl(du, l, 64);
                     if (gi < tot)
-                        newc += v2_relax<LIGHT>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), kl + (gi - xl), dl, fout, fe);
+                        newc += v2_relax<LIGHT>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), kl + (gi - xl), dl, fout, fe,
+                                                fm);
                 }
             }
         }
     }
     if (LIGHT) {
         v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+        v2_flush_fmin(fm, a.ctl->cnt[(cin + 1) & 3], red);
         v2_flush2(mh, ml, a.ctl->mh, red);
     }
 }
@@ -803,7 +843,7 @@ struct V2HubLds {
 };
 template <bool LIGHT>
 __device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ fout, int hs, u64 packed, u32& newc,
-                                            u64& fe, V2HubLds& L) {
+                                            u64& fe, int32_t& fm, V2HubLds& L) {
     const u64 nq = packed >> V2_EB, total = packed & ((1ull << V2_EB) - 1ull);
     const u32* hv = a.hv + (u64)hs * a.hcap;
     const u64* hb = a.hbeg + (u64)hs * a.hcap;
@@ -829,7 +869,7 @@ __device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ f
             idx[j] = val[j] ? L.s_b[sl] + (e - L.sh.off[sl]) : 0ull;
             du[j] = val[j] ? L.s_du[sl] : 0;
         }
-        newc += v2_relax_g<LIGHT, NJ>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), idx, du, val, fout, fe);
+        newc += v2_relax_g<LIGHT, NJ>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), idx, du, val, fout, fe, fm);
         __syncthreads();
     }
 }
@@ -845,8 +885,12 @@ __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout,
     if ((packed >> V2_EB) == 0) return;
     u32 newc = 0;
     u64 fe = 0;
-    v2_hub_body<LIGHT>(a, fout, hs, packed, newc, fe, L);
-    if (LIGHT) v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+    int32_t fm = INT_INF;
+    v2_hub_body<LIGHT>(a, fout, hs, packed, newc, fe, fm, L);
+    if (LIGHT) {
+        v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+        v2_flush_fmin(fm, a.ctl->cnt[(cin + 1) & 3], red);
+    }
 }
 
 // Next band [lo, hi): fout words = members, count into slot cout, min dist >= lo.
@@ -890,6 +934,7 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fo
         }
     }
     v2_flush2(c, fe, a.ctl->cnt[cout], red);
+    v2_flush_fmin(mn, a.ctl->cnt[cout], red);  // (min over dist >= lo: below every member)
     v2_flush_min(mn, a.ctl, red);
 }
 
@@ -1059,6 +1104,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
         }
     }
     v2_flush2(ccount, fe, a.ctl->cnt[cout], red);
+    v2_flush_fmin(mn, a.ctl->cnt[cout], red);  // (min over every dist >= hi: below the next band's members)
     v2_flush_min(mn, a.ctl, red);
 }
 
@@ -1073,10 +1119,10 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
 template <typename Off>
 __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* __restrict__ row,
                                                    const u64* __restrict__ fin, u64* __restrict__ fout, u32* newb,
-                                                   u32& newc, u64& fe, u64& mh, u64& ml) {
+                                                   int32_t flo, u32& newc, u64& fe, u64& mh, u64& ml, int32_t& fm) {
     constexpr int NWV = DB / WAVE;
     const int lane = lane_id();
-    const int32_t lo = a.lo, hi = a.hi;
+    const int32_t lo = a.lo, hi = a.hi;  // flo: the frontier's least distance (v2_pull_lo), >= lo
     const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
     const i64 nsc = (a.nwords + PSC - 1) / PSC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
@@ -1108,7 +1154,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             const int32_t d = v < a.n ? a.dist[v] : 0;
             // (w1 filter: a frontier in-neighbour offers at least lo + the row's lightest weight)
             const int w1 = (a.w1 && v < a.n && d > lo) ? (int)a.w1[v] : 0;
-            const u64 m = __ballot(v < a.n && d > lo && (long long)lo + w1 < (long long)d);
+            const u64 m = __ballot(v < a.n && d > lo && (long long)flo + w1 < (long long)d);
             if (lane == k) mytodo = m;
         }
         // a vertex without light edges has no light in-edge (symmetric graph): not a candidate
@@ -1162,7 +1208,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             const Off kst = k;  // (PJ_V2_STATS: edges scanned)
             while (__ballot(go)) {
                 if (go) {
-                    if (pull_step_fin_cw<Off>(v2_light_src(a), a.dist, lfin, k, lim, lo, hi, cur)) {
+                    if (pull_step_fin_cw<Off>(v2_light_src(a), a.dist, lfin, k, lim, flo, hi, cur)) {
                         done = true;
                         go = false;
                     } else {
@@ -1187,7 +1233,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                     const bool valid = k0 < ke;
                     const u64 x = valid ? eat(v2_light_src(a), (u64)k0) : 0ull;
                     const u32 w = (u32)(x >> 32);
-                    const bool stop = !valid || (long long)lo + w >= (long long)cl;
+                    const bool stop = !valid || (long long)flo + w >= (long long)cl;
                     int32_t cand = INT_INF;
                     if (!stop) {
                         const int32_t du = pull_src(lfin, a.dist, (u32)x, hi);
@@ -1209,6 +1255,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             if (act && cur < d0) {
                 a.dist[v] = cur;
                 if (cur < hi) {
+                    if (cur < fm) fm = cur;
                     const i64 wl = (v >> 6) - gbase;
                     atomicOr(&newb[2 * wl + ((v >> 5) & 1)], 1u << (v & 31));
                     ++newc;
@@ -1235,7 +1282,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
 // atomicMin (the vertex's chunks run in different waves).
 __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __restrict__ fin, u64* __restrict__ fout,
                                                   const u32* __restrict__ lcv, const u32* __restrict__ lcc, u64 nlc,
-                                                  u32& newc, u64& fe) {
+                                                  int32_t flo, u32& newc, u64& fe, int32_t& fm) {
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
     const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
@@ -1247,7 +1294,7 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
         const u32 ls = (u32)(a.lrow[v + 1] - rb);
         const u64 kb = rb + (u64)lcc[it] * V2_PCH;
         const u64 ke = min(rb + ls, kb + V2_PCH);
-        if ((long long)lo + (eat(v2_light_src(a), kb) >> 32) >= (long long)d0) continue;
+        if ((long long)flo + (eat(v2_light_src(a), kb) >> 32) >= (long long)d0) continue;
         int32_t cur = d0;
         for (u64 kk = kb; kk < ke; kk += WAVE) {
             if (PJ_V2_STATS && lane == 0) atomicAdd(&a.ctl->dbg[7].v, min((u64)WAVE, ke - kk));
@@ -1255,7 +1302,7 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
             const bool valid = k0 < ke;
             const u64 x = valid ? eat(v2_light_src(a), k0) : 0ull;
             const u32 w = (u32)(x >> 32);
-            const bool stop = !valid || (long long)lo + w >= (long long)cur;
+            const bool stop = !valid || (long long)flo + w >= (long long)cur;
             int32_t cand = INT_INF;
             if (!stop) {
                 const int32_t du = pull_src(lfin, a.dist, (u32)x, hi);
@@ -1275,6 +1322,7 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
         if (lane == 0 && cur < d0) {
             const int32_t old = atomicMin(a.dist + v, cur);
             if (cur < old && cur < hi) {
+                if (cur < fm) fm = cur;
                 const u64 bit = 1ull << (v & 63);
                 if (!(atomicOr(fout + (v >> 6), bit) & bit)) {
                     ++newc;
@@ -1323,16 +1371,21 @@ __global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __res
         }
         u32 newc = 0;
         u64 mh = 0, ml = 0, fe = 0;
-        v2_dense_body<Off>(a, row, fin, fout, hs, newc, fe, mh, ml, lds.push);
+        int32_t fm = INT_INF;
+        v2_dense_body<Off>(a, row, fin, fout, hs, newc, fe, mh, ml, fm, lds.push);
         v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+        v2_flush_fmin(fm, a.ctl->cnt[(cin + 1) & 3], red);
         v2_flush2(mh, ml, a.ctl->mh, red);
         return;
     }
     u32 newc = 0;
     u64 fe = 0, mh = 0, ml = 0;
-    if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, newc, fe);
-    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], newc, fe, mh, ml);
+    int32_t fm = INT_INF;
+    const int32_t flo = v2_pull_lo(a, cin);
+    if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, flo, newc, fe, fm);
+    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], flo, newc, fe, mh, ml, fm);
     v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
+    v2_flush_fmin(fm, a.ctl->cnt[(cin + 1) & 3], red);
     v2_flush2(mh, ml, a.ctl->mh, red);
 }
 
@@ -1717,6 +1770,8 @@ __global__ void v2_init_k(int32_t* __restrict__ dist, i64 n, i64 nwords, i64 src
         for (int i = threadIdx.x; i < (int)(sizeof(V2Ctl) / sizeof(u64)); i += blockDim.x) c[i] = 0;
         __syncthreads();
         if (threadIdx.x < V2_NSH) ctl->minv[threadIdx.x].v = ~0ull;
+        // frontier minimum of the ring's slots: the source's 0 in slot 0, none elsewhere
+        if (threadIdx.x < 3 * V2_NSH) ctl->cnt[1 + threadIdx.x / V2_NSH][threadIdx.x % V2_NSH].pad[1] = (u64)INT_INF;
         if (threadIdx.x == 0 && src >= 0) ctl->cnt[0][0].v = 1;
     }
 }
@@ -1949,6 +2004,9 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 a.fesplit = w.lsplit2.p;
             }
             const bool pull_now = can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh;
+            if (PJ_V2_STATS)
+                fprintf(stderr, "heavy step lo %lld: members' heavy edges %llu, unsettled heavy edges %llu, %s\n", lo,
+                        (unsigned long long)mh, (unsigned long long)heavy_left, pull_now ? "pull" : mh ? "push" : "none");
             if (pull_now) {
                 v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi_t, cs);
                 PJ_LAUNCH_CHECK();
