@@ -875,6 +875,7 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "beta" && value > 0) g.beta = value;
     else if (k == "delta" && value >= 0) g.delta = value;
     else if (k == "pull_factor" && value >= 0) g.pull_factor = value;
+    else if (k == "defer_heavy" && value >= 0) g.defer_heavy = value;
     else if (k == "light_pull" && value >= 0) g.light_pull = value;
     else if (k == "tail_light_pull" && value > 0) g.tail_light_pull = value;
     else if (k == "round_log" && (value == 0 || value == 1)) g.round_log = (int)value;

@@ -322,6 +322,8 @@ struct V2Args {
     u64* hoff;   // [3][hcap]
     u64 hcap;
     u64* rlog;   // round_log option: [0] = rounds logged, then (kind, frontier, its light edges) per round
+    int32_t hz;  // heavy push: relax only the edges with du + w < hz (INT_INF = all; defer_heavy)
+    u64* dsave;  // heavy push: the member words are OR-ed in here (their far edges are deferred), or null
 };
 // the light edges of a band round (light CSR, or the light prefixes of cw in the tail)
 __device__ __forceinline__ ESrc v2_cw_src(const V2Args& a) {
@@ -697,7 +699,20 @@ template <typename Off, bool LIGHT>
 __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __restrict__ row, u64* __restrict__ fin,
                                                u64* __restrict__ fout, int cin, int hs, u64* red);
 
+// first position in [b, e) of a weight-sorted row whose weight is >= lim (binary search)
+__device__ __forceinline__ u64 v2_first_w_ge(const V2Args& a, u64 b, u64 e, long long lim) {
+    while (b < e) {
+        const u64 m = (b + e) >> 1;
+        const u32 w = a.w8 ? (u32)a.w8[m] : (u32)(a.cw[m] >> 32);
+        if ((long long)w >= lim) e = m;
+        else b = m + 1;
+    }
+    return b;
+}
+
 // Heavy push step: the heavy segments of the band's members (fin = mb; hub queue hs).
+// With a.hz < INT_INF only the edges landing below hz (the next band) are relaxed and
+// the member words are saved in a.dsave: the rest is left to the next heavy step.
 template <typename Off>
 __global__ __launch_bounds__(DB) void v2_heavy_push_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
                                                       int hs) {
@@ -721,6 +736,7 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
             mytodo = fin[wbase + lane];
             if (mytodo) {
                 fin[wbase + lane] = 0;
+                if (!LIGHT && a.dsave) a.dsave[wbase + lane] |= mytodo;  // (the wave owns the word)
                 if (LIGHT) {  // the wave owns these words of mb: plain read-modify-write
                     const u64 old = a.mb[wbase + lane];
                     mynew = mytodo & ~old;
@@ -786,9 +802,10 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
                         mh += (u64)row[v + 1] - (u64)row[v] - (e - b);
                         ml += e - b;
                     }
-                } else {      // heavy suffix of the row
+                } else {      // heavy suffix of the row (up to the horizon: defer_heavy)
                     b = (u64)row[v] + a.lsplit[v];
                     e = (u64)row[v + 1];
+                    if (a.hz < INT_INF) e = v2_first_w_ge(a, b, e, (long long)a.hz - du);
                 }
             }
             // long segment -> hub queue (wave-aggregated append; all lanes here)
@@ -1538,6 +1555,8 @@ struct DeltaSolve {
     DevBuf<int32_t> out_own;
     DevBuf<u64> f[3], mb;      // light-round frontier ring (v2_clear_words), band members
     DevBuf<u64> sb;            // settled-before-the-tail bitmap
+    DevBuf<u64> db;            // members whose far heavy edges are deferred (defer_heavy); all zero
+    bool db_dirty = true;      // unless a solve stopped with a deferral pending (an error)
     DevBuf<V2Ctl> ctl;
     V2Ctl* hctl = nullptr;     // mapped pinned host copy, written by v2_publish_k
     V2Ctl* hctl_dev = nullptr;
@@ -1787,6 +1806,7 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     v.f[2].alloc(nw);
     v.mb.alloc(nw);
     v.sb.alloc(nw);
+    v.db.alloc(nw);
     v.ctl.alloc(1);
     v.hcap = (u64)std::max<i64>(1, std::min<i64>(n, g.nnz / (i64)V2_HT + 1));
     v.hv.alloc(3 * v.hcap);  // the hub queue's ring of three slots
@@ -1859,6 +1879,8 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
         PJ_HIP(hipMemsetAsync(rlog.p, 0, sizeof(u64), s));
         a.rlog = rlog.p;
     }
+    a.hz = INT_INF;
+    a.dsave = nullptr;
     // the host's view of the counters: one block copies them into mapped host memory
     // (a D2H hipMemcpyAsync of the same 3.3 KB ran as a ~30 us blit per sync)
     // The host spins on the sequence number (wakes within ~1 us of the copy instead of
@@ -1902,6 +1924,10 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
         PJ_LAUNCH_CHECK();
     }
     if (valid && ls < n) {
+        if (v.db_dirty) {
+            PJ_HIP(hipMemsetAsync(v.db.p, 0, sizeof(u64) * (size_t)nwords, s));
+            v.db_dirty = false;
+        }
         int cs = 0, hr = 0, fi = 0;
         long long lo = 0;
         u64 heavy_left = w.heavy_total, light_left = w.light_total;
@@ -1919,6 +1945,37 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
         const bool defer_ok = g.defer_check && !PJ_V2_STATS && g.round_batch <= 2;
         bool deferred = false;
         bool finished = false;
+        // Deferred far heavy edges (defer_heavy): a heavy push of a band whose members hold
+        // many heavy edges relaxes only those landing in the next band; the members stay in db
+        // and their other heavy edges go with the next heavy step -- a pull that takes its stop
+        // rule from their band (lo_def), or a push of db's whole heavy rows first. Before an
+        // empty band's jump or the end, db is pushed whole (flush_def).
+        bool dpend = false;
+        long long lo_def = 0;
+        u64 mh_def = 0;
+        auto push_heavy = [&](u64* members, int32_t hz, u64* dsave) {
+            a.hz = hz;
+            a.dsave = dsave;
+            v2_heavy_push_k<Off><<<maxgrid, DB, 0, s>>>(a, row, members, hr);
+            PJ_LAUNCH_CHECK();
+            v2_hub_k<false><<<maxgrid, DB, 0, s>>>(a, nullptr, cs, hr, (hr + 1) % 3);
+            PJ_LAUNCH_CHECK();
+            a.hz = INT_INF;
+            a.dsave = nullptr;
+            hr = (hr + 1) % 3;
+            st.td_levels++;
+        };
+        // push db whole, then select the band from nlo (the bands below it are settled)
+        auto flush_def = [&](long long nlo) {
+            push_heavy(v.db.p, INT_INF, nullptr);
+            dpend = false;
+            v.db_dirty = false;
+            mh_def = 0;
+            a.lo = (int32_t)nlo;
+            a.hi = (int32_t)std::min<long long>(nlo + bw, INT_INF);
+            v2_select_k<<<maxgrid, DB, 0, s>>>(a, v.f[fi].p, cs);
+            PJ_LAUNCH_CHECK();
+        };
         while (lo < INT_INF && !finished) {
             const int32_t hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
             a.lo = (int32_t)lo;
@@ -1951,6 +2008,14 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 sync_ctl();
                 if (deferred) {
                     deferred = false;
+                    if (slot(cs_start) == 0 && dpend) {  // empty, but deferred edges may land past it
+                        st.levels--;
+                        lo = hi;
+                        flush_def(lo);
+                        deferred = true;
+                        jumped = true;
+                        break;
+                    }
                     if (slot(cs_start) == 0) {  // the band was empty: its rounds were idle
                         st.levels--;
                         const u64 mv = hminv();
@@ -2003,23 +2068,40 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 a.swrite = v.sb.p;
                 a.fesplit = w.lsplit2.p;
             }
-            const bool pull_now = can_pull && mh > 0 && (double)heavy_left < g.pull_factor * (double)mh;
+            const u64 mh_all = mh + mh_def;  // (a push would relax the deferred edges too)
+            const bool pull_now = can_pull && mh_all > 0 && (double)heavy_left < g.pull_factor * (double)mh_all;
             if (PJ_V2_STATS)
                 fprintf(stderr, "heavy step lo %lld: members' heavy edges %llu, unsettled heavy edges %llu, %s\n", lo,
                         (unsigned long long)mh, (unsigned long long)heavy_left, pull_now ? "pull" : mh ? "push" : "none");
             if (pull_now) {
+                // deferred members (dist >= lo_def) are probed like this band's (dist < hi)
+                if (dpend) a.lo = (int32_t)lo_def;
                 v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi_t, cs);
                 PJ_LAUNCH_CHECK();
+                a.lo = (int32_t)lo;
                 PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
+                if (dpend) PJ_HIP(hipMemsetAsync(v.db.p, 0, sizeof(u64) * (size_t)nwords, s));
+                if (dpend) v.db_dirty = false;
+                dpend = false;
+                mh_def = 0;
                 st.bu_levels++;
             } else {
+                if (dpend) {  // the deferred edges first, whole (db is cleared as read)
+                    push_heavy(v.db.p, INT_INF, nullptr);
+                    dpend = false;
+                    v.db_dirty = false;
+                    mh_def = 0;
+                }
                 if (mh > 0) {
-                    v2_heavy_push_k<Off><<<maxgrid, DB, 0, s>>>(a, row, v.mb.p, hr);
-                    PJ_LAUNCH_CHECK();
-                    v2_hub_k<false><<<maxgrid, DB, 0, s>>>(a, nullptr, cs, hr, (hr + 1) % 3);
-                    PJ_LAUNCH_CHECK();
-                    hr = (hr + 1) % 3;
-                    st.td_levels++;
+                    const bool dfr = can_pull && g.defer_heavy > 0.0 && !enter_tail && nhi_t < INT_INF &&
+                                     (double)mh >= g.defer_heavy * (double)g.nnz;
+                    if (dfr) v.db_dirty = true;
+                    push_heavy(v.mb.p, dfr ? nhi_t : INT_INF, dfr ? v.db.p : nullptr);
+                    if (dfr) {
+                        dpend = true;
+                        lo_def = lo;
+                        mh_def = mh;
+                    }
                 } else {
                     PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 }
@@ -2063,6 +2145,12 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 heavy_left = v.hctl->dbg[0].v;
                 light_left = tail_unsettled > heavy_left ? tail_unsettled - heavy_left : 0;
             }
+            if (slot(cs) == 0 && dpend) {  // the next band is empty; deferred edges land past it
+                lo = nhi_t;
+                flush_def(lo);
+                deferred = true;
+                continue;
+            }
             if (slot(cs) == 0) {
                 const u64 mv = hminv();
                 if (mv >= (u64)INT_INF) break;  // nothing reached beyond the settled bands
@@ -2075,6 +2163,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             }
             lo = hi;
         }
+        if (dpend) throw Error(PJ_ERR_HIP, "delta-stepping: deferred heavy edges left (internal error)");
     }
     if (g.n > 0) {
         unlabel_k<<<grid_for(g.n, 256, maxgrid), 256, 0, s>>>(R.inv.p, v.dist, g.n, n, v.out);

@@ -215,6 +215,9 @@ struct Graph {
     double alpha = 14.0, beta = 24.0, delta = 0.0;
     double pull_factor = 4.0;  // symmetric: pull a band's heavy edges when the heavy edges of unsettled
                                // vertices < pull_factor x the members' heavy edges (0 = never)
+    double defer_heavy = 0.002; // v2, symmetric: a heavy push of members holding >= defer_heavy x nnz heavy
+                                // edges relaxes only the edges that land in the next band and leaves the
+                                // rest to the next heavy step (§4.2; 0 = off)
     double band_width = 0.0;   // v2: width of a band [lo, lo + band_width) (0 = delta, at most delta)
     double tail_delta = -1.0;  // v2: light threshold and band width of the tail (0 = off, < 0 = 64 x delta):
     int tail_after = 1;        // from the first band >= tail_after at which the edges of unsettled

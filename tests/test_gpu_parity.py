@@ -334,6 +334,37 @@ def test_weighted_band_width(ctx, oracle, scale, ef):
     g.close()
 
 
+@pytest.mark.parametrize("scale,ef", [(12, 16), (14, 4), (15, 16)])
+def test_weighted_defer_heavy(ctx, oracle, scale, ef):
+    """Deferred far heavy edges (defer_heavy, delta.hip): a heavy push relaxes only the edges
+    that land in the next band and leaves the rest to the next heavy step (a pull whose stop
+    rule starts at the deferring band, or a whole push of the deferred members), and pushes
+    them whole before an empty band's jump or the end. Every heavy push deferred (1e-12),
+    the default threshold, never (0); pull rules that make the next step a pull or a push;
+    small deltas and narrow bands (empty bands, jumps); with and without the tail and the
+    deferred band check. Bit-exact against the oracle Dijkstra."""
+    g = ctx.generate_kronecker(scale, ef, 21 + scale, weighted=True)
+    row, col, wc = g.get_csr()
+    col = col.astype(np.uint32)
+    roots = [int(r) for r in g.sample_roots(11 + ef, 3)]
+    exp = {r: oracle.dijkstra(row, col, wc, r) for r in roots}
+    pushed_any = False  # (with defer_heavy 1e-12 every heavy push outside the tail switch defers)
+    for dh in (1e-12, 0.002, 0.0):
+        g.set_option("defer_heavy", dh)
+        for pf in (4.0, 0.3, 40.0):
+            g.set_option("pull_factor", pf)
+            for delta, bw, tf, dc in ((0, 0, 0.2, 1), (3, 0, 0.0, 1), (7, 2, 0.0, 0), (24, 0, 0.1, 1), (2, 1, 0.3, 0)):
+                g.set_option("delta", delta)
+                g.set_option("band_width", bw)
+                g.set_option("tail_frac", tf)
+                g.set_option("defer_check", dc)
+                for r in roots:
+                    assert (g.sssp(r) == exp[r]).all(), (dh, pf, delta, bw, tf, dc, r)
+                    pushed_any |= dh > 0 and g.stats()["td_levels"] > 0
+    assert pushed_any
+    g.close()
+
+
 @pytest.mark.parametrize("scale,ef", [(12, 16), (14, 4), (16, 1), (15, 16)])
 def test_weighted_pull_heavy(ctx, oracle, scale, ef):
     """Heavy edges by pull (symmetric graphs): never (push only), by the default
