@@ -1966,15 +1966,28 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             st.td_levels++;
         };
         // push db whole, then select the band from nlo (the bands below it are settled)
+        // (or, by the heavy-pull rule, a pull from lo_def that selects that band itself)
         auto flush_def = [&](long long nlo) {
-            push_heavy(v.db.p, INT_INF, nullptr);
+            const int32_t nhi = (int32_t)std::min<long long>(nlo + bw, INT_INF);
+            if (can_pull && (double)heavy_left < g.pull_factor * (double)mh_def) {
+                a.lo = (int32_t)lo_def;
+                a.hi = (int32_t)nlo;
+                v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi, cs);
+                PJ_LAUNCH_CHECK();
+                PJ_HIP(hipMemsetAsync(v.db.p, 0, sizeof(u64) * (size_t)nwords, s));
+                st.bu_levels++;
+            } else {
+                push_heavy(v.db.p, INT_INF, nullptr);
+                a.lo = (int32_t)nlo;
+                a.hi = nhi;
+                v2_select_k<<<maxgrid, DB, 0, s>>>(a, v.f[fi].p, cs);
+                PJ_LAUNCH_CHECK();
+            }
+            a.lo = (int32_t)nlo;
+            a.hi = nhi;
             dpend = false;
             v.db_dirty = false;
             mh_def = 0;
-            a.lo = (int32_t)nlo;
-            a.hi = (int32_t)std::min<long long>(nlo + bw, INT_INF);
-            v2_select_k<<<maxgrid, DB, 0, s>>>(a, v.f[fi].p, cs);
-            PJ_LAUNCH_CHECK();
         };
         while (lo < INT_INF && !finished) {
             const int32_t hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
@@ -2069,6 +2082,10 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 a.fesplit = w.lsplit2.p;
             }
             const u64 mh_all = mh + mh_def;  // (a push would relax the deferred edges too)
+            const bool dfr_ok = can_pull && g.defer_heavy > 0.0 && !enter_tail && nhi_t < INT_INF &&
+                                (double)mh >= g.defer_heavy * (double)g.nnz;
+            // (round 5: deferring heavy pulls the same way, the next heavy step pulling both
+            // bands, measured 1.5% slower: profiles/r05/defer_heavy_r5h7.txt)
             const bool pull_now = can_pull && mh_all > 0 && (double)heavy_left < g.pull_factor * (double)mh_all;
             if (PJ_V2_STATS)
                 fprintf(stderr, "heavy step lo %lld: members' heavy edges %llu, unsettled heavy edges %llu, %s\n", lo,
@@ -2093,8 +2110,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                     mh_def = 0;
                 }
                 if (mh > 0) {
-                    const bool dfr = can_pull && g.defer_heavy > 0.0 && !enter_tail && nhi_t < INT_INF &&
-                                     (double)mh >= g.defer_heavy * (double)g.nnz;
+                    const bool dfr = dfr_ok;
                     if (dfr) v.db_dirty = true;
                     push_heavy(v.mb.p, dfr ? nhi_t : INT_INF, dfr ? v.db.p : nullptr);
                     if (dfr) {
