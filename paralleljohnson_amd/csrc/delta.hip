@@ -286,6 +286,12 @@ struct V2Ctl {
 #ifndef PJ_V2_FMIN
 #define PJ_V2_FMIN 1  // light pulls stop rows at the frontier's least distance (v2_flush_fmin)
 #endif
+#ifndef PJ_V2_SELMB
+// the selections (v2_select_k, v2_pull_k's fused one) write the next band's member words of mb
+// and add the members' heavy / light degrees, so its first round finds no new members to count
+// one by one
+#define PJ_V2_SELMB 1
+#endif
 #ifndef PJ_V2_PSTATS
 #define PJ_V2_PSTATS 0  // debug build: heavy-pull scan-length counters (printed per solve)
 #endif
@@ -918,11 +924,13 @@ __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout,
 #define PJ_V2_SELW 4
 #endif
 constexpr int V2_SELW = PJ_V2_SELW;
-__global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fout, int cout) {
+template <typename Off>
+__global__ __launch_bounds__(DB) void v2_select_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fout,
+                                                  int cout) {
     __shared__ u64 red[DB / WAVE];
     const int lane = lane_id();
     u32 c = 0;
-    u64 fe = 0;
+    u64 fe = 0, mh = 0, ml = 0;
     int32_t mn = INT_INF;
     for (i64 w0 = ((i64)blockIdx.x * (DB / WAVE) + wave_id()) * V2_SELW; w0 < a.nwords;
          w0 += (i64)gridDim.x * (DB / WAVE) * V2_SELW) {
@@ -945,12 +953,23 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fo
                 if (lane == 0) a.swrite[wi] = sm;
             }
             if (d >= a.lo && d < mn) mn = d;
-            if (mem) fe += (a.fesplit ? a.fesplit : a.lsplit)[v];
-            if (lane == 0) fout[wi] = m;
+            if (mem) {
+                const u32 ls = (a.fesplit ? a.fesplit : a.lsplit)[v];
+                fe += ls;
+                if (PJ_V2_SELMB) {
+                    mh += (u64)row[v + 1] - (u64)row[v] - ls;
+                    ml += ls;
+                }
+            }
+            if (lane == 0) {
+                fout[wi] = m;
+                if (PJ_V2_SELMB) a.mb[wi] = m;  // (mb is clear here: the heavy step consumed it)
+            }
             c += lane == 0 ? (u32)__popcll(m) : 0u;
         }
     }
     v2_flush2(c, fe, a.ctl->cnt[cout], red);
+    if (PJ_V2_SELMB) v2_flush2(mh, ml, a.ctl->mh, red);
     v2_flush_fmin(mn, a.ctl->cnt[cout], red);  // (min over dist >= lo: below every member)
     v2_flush_min(mn, a.ctl, red);
 }
@@ -968,6 +987,7 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, u64* __restrict__ fo
 // tests of other lanes do not change. The wave owns its
 // PSC words: it writes the next band's member words of fout whole (and so clears
 // them), counts them into slot cout and folds min{new dist >= hi} into minv.
+constexpr bool V2_SELMB_PULL = PJ_V2_SELMB && PJ_V2_NOFIN >= 2;  // (the pull probes mb when NOFIN < 2)
 template <typename Off>
 __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fout,
                                                 int32_t nhi, int cout) {
@@ -979,7 +999,7 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
     const u64* hmb = PJ_V2_NOFIN >= 2 ? nullptr : a.mb;
     u32* newb = s_new[wave_id()];
     u32 ccount = 0;
-    u64 fe = 0;
+    u64 fe = 0, mh = 0, ml = 0;  // (the next band's members' degrees: PJ_V2_SELMB)
     int32_t mn = INT_INF;
     const i64 ngroups = a.nwords;
     const i64 nsc = (ngroups + PSC - 1) / PSC;
@@ -1004,7 +1024,14 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                 const bool sk = up && !cand;
                 if (sk && d < mn) mn = d;
                 nm = __ballot(sk && d < nhi);
-                if (sk && d < nhi) fe += (a.fesplit ? a.fesplit : a.lsplit)[v];
+                if (sk && d < nhi) {
+                    const u32 ls = (a.fesplit ? a.fesplit : a.lsplit)[v];
+                    fe += ls;
+                    if (PJ_V2_SELMB) {
+                        mh += (u64)row[v + 1] - (u64)row[v] - ls;
+                        ml += ls;
+                    }
+                }
             }
             if (lane == k) {
                 mytodo = m;
@@ -1110,17 +1137,24 @@ __global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict_
                 if (cur < nhi) {  // cur >= hi always here
                     const i64 wl = (v >> 6) - gbase;
                     atomicOr(&newb[2 * wl + ((v >> 5) & 1)], 1u << (v & 31));
-                    fe += (a.fesplit ? a.fesplit : a.lsplit)[v];
+                    const u32 ls = (a.fesplit ? a.fesplit : a.lsplit)[v];
+                    fe += ls;
+                    if (PJ_V2_SELMB) {
+                        mh += (u64)row[v + 1] - (u64)row[v] - ls;
+                        ml += ls;
+                    }
                 }
             }
         }
         if (lane < PSC && gbase + lane < a.nwords) {
             const u64 word = (u64)newb[2 * lane] | ((u64)newb[2 * lane + 1] << 32);
             fout[gbase + lane] = word;
+            if (V2_SELMB_PULL) a.mb[gbase + lane] = word;  // (no wave reads mb here: NOFIN 2)
             ccount += (u32)__popcll(word);
         }
     }
     v2_flush2(ccount, fe, a.ctl->cnt[cout], red);
+    if (V2_SELMB_PULL) v2_flush2(mh, ml, a.ctl->mh, red);
     v2_flush_fmin(mn, a.ctl->cnt[cout], red);  // (min over every dist >= hi: below the next band's members)
     v2_flush_min(mn, a.ctl, red);
 }
@@ -1950,6 +1984,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
         // and their other heavy edges go with the next heavy step -- a pull that takes its stop
         // rule from their band (lo_def), or a push of db's whole heavy rows first. Before an
         // empty band's jump or the end, db is pushed whole (flush_def).
+        u64 mh_carry = 0, ml_carry = 0;  // (PJ_V2_SELMB: the next band's members' degrees, published early)
         bool dpend = false;
         long long lo_def = 0;
         u64 mh_def = 0;
@@ -1980,7 +2015,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 push_heavy(v.db.p, INT_INF, nullptr);
                 a.lo = (int32_t)nlo;
                 a.hi = nhi;
-                v2_select_k<<<maxgrid, DB, 0, s>>>(a, v.f[fi].p, cs);
+                v2_select_k<Off><<<maxgrid, DB, 0, s>>>(a, row, v.f[fi].p, cs);
                 PJ_LAUNCH_CHECK();
             }
             a.lo = (int32_t)nlo;
@@ -1994,7 +2029,10 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             a.lo = (int32_t)lo;
             a.hi = hi;
             st.levels++;
-            u64 mh = 0, ml = 0;  // members' heavy / light degree sums (reset by every publish)
+            // members' heavy / light degree sums (reset by every publish; the band's first
+            // members were counted by its selection, read by a publish after the heavy step)
+            u64 mh = mh_carry, ml = ml_carry;
+            mh_carry = ml_carry = 0;
             const int cs_start = cs;
             bool jumped = false;
             // light rounds until the band's frontier is empty, launched round_batch per
@@ -2039,7 +2077,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                         lo = (long long)mv / bw * bw;  // jump to the next occupied band
                         a.lo = (int32_t)lo;
                         a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
-                        v2_select_k<<<maxgrid, DB, 0, s>>>(a, v.f[fi].p, cs);
+                        v2_select_k<Off><<<maxgrid, DB, 0, s>>>(a, row, v.f[fi].p, cs);
                         PJ_LAUNCH_CHECK();
                         jumped = true;
                         break;
@@ -2096,7 +2134,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi_t, cs);
                 PJ_LAUNCH_CHECK();
                 a.lo = (int32_t)lo;
-                PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
+                if (!V2_SELMB_PULL) PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 if (dpend) PJ_HIP(hipMemsetAsync(v.db.p, 0, sizeof(u64) * (size_t)nwords, s));
                 if (dpend) v.db_dirty = false;
                 dpend = false;
@@ -2118,12 +2156,12 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                         lo_def = lo;
                         mh_def = mh;
                     }
-                } else {
+                } else if (!PJ_V2_SELMB) {  // (else the select overwrites every mb word)
                     PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 }
                 a.lo = hi;
                 a.hi = nhi_t;
-                v2_select_k<<<maxgrid, DB, 0, s>>>(a, v.f[fi].p, cs);
+                v2_select_k<Off><<<maxgrid, DB, 0, s>>>(a, row, v.f[fi].p, cs);
                 PJ_LAUNCH_CHECK();
             }
             if (enter_tail) {
@@ -2173,9 +2211,13 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 lo = (long long)mv / bw * bw;  // jump to the next occupied band
                 a.lo = (int32_t)lo;
                 a.hi = (int32_t)std::min<long long>(lo + bw, INT_INF);
-                v2_select_k<<<maxgrid, DB, 0, s>>>(a, v.f[fi].p, cs);
+                v2_select_k<Off><<<maxgrid, DB, 0, s>>>(a, row, v.f[fi].p, cs);
                 PJ_LAUNCH_CHECK();
                 continue;
+            }
+            for (int i = 0; i < V2_NSH; ++i) {  // (the next band's members, counted by its selection)
+                mh_carry += v.hctl->mh[i].v;
+                ml_carry += v.hctl->mh[i].pad[0];
             }
             lo = hi;
         }
