@@ -292,6 +292,9 @@ struct V2Ctl {
 // one by one
 #define PJ_V2_SELMB 1
 #endif
+#ifndef PJ_V2_MBC
+#define PJ_V2_MBC 1  // light pulls count the frontier's new members compacted, a lane each
+#endif
 #ifndef PJ_V2_PSTATS
 #define PJ_V2_PSTATS 0  // debug build: heavy-pull scan-length counters (printed per solve)
 #endif
@@ -1190,6 +1193,33 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                 if (nmw) a.mb[gbase + lane] = old | f;
             }
         }
+#if PJ_V2_MBC
+        // (compacted: 64 new members per wave step, a lane each; one lane walking the bits of
+        // its word serialized a frontier of millions of new members in 16 lanes of the wave)
+        {
+            const u32 mc = (u32)__popcll(nmw);
+            const u32 mincl = wave_incl_scan(mc);
+            const u32 mex = mincl - mc;
+            const u32 MT = __shfl(mincl, 63, 64);
+            for (u32 r0 = 0; r0 < MT; r0 += WAVE) {
+                const u32 c = r0 + lane;
+                u32 jw = 0;
+#pragma unroll
+                for (u32 step = PSC / 2; step > 0; step >>= 1) {
+                    const u32 x = __shfl(mex, jw + step, 64);
+                    if (x <= c) jw += step;
+                }
+                const u32 ex = __shfl(mex, jw, 64);
+                const u64 tw = __shfl(nmw, jw, 64);
+                if (c < MT) {
+                    const i64 v = (gbase + jw) * 64 + select_bit(tw, c - ex);
+                    const u64 rb = (u64)row[v], ls = a.lsplit[v];
+                    mh += (u64)row[v + 1] - rb - ls;
+                    ml += ls;
+                }
+            }
+        }
+#else
         while (nmw) {
             const int b = __ffsll((long long)nmw) - 1;
             nmw &= nmw - 1;
@@ -1198,6 +1228,7 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             mh += (u64)row[v + 1] - rb - ls;
             ml += ls;
         }
+#endif
         u64 mytodo = 0;
 #pragma unroll
         for (int k = 0; k < PSC; ++k) {
