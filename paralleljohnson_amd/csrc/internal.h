@@ -223,9 +223,10 @@ struct Graph {
     int tail_after = 1;        // from the first band >= tail_after at which the edges of unsettled
     double tail_frac = 0.2;    // vertices are < tail_frac x nnz (profiles/r01/tail_sweep.txt; 0.1 until
                                // round 5: 0.2 +1% at s22w-s26w with the round-5 delta, delta_sweep_r5ag.txt)
-    double light_pull = 3.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
+    double light_pull = 6.0;   // v2, symmetric: pull a light round when its frontier's light edges exceed
                                // the light edges of unsettled vertices / light_pull (0 = never; 2 -> 3 at
-                               // the end of round 2 with merged rounds: +1%, interleaved A/B)
+                               // the end of round 2 with merged rounds: +1%, interleaved A/B; 3 -> 6 late
+                               // in round 5 with the cheaper pulls: +0.6%, profiles/r05/sweeps_r5h14.txt)
     double tail_light_pull = 3.0;  // the same rule in the tail's rounds
     int round_log = 0;         // debug: per light round (kind, frontier, light edges) on stderr
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
