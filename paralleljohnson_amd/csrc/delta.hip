@@ -292,6 +292,27 @@ struct V2Ctl {
 // one by one
 #define PJ_V2_SELMB 1
 #endif
+// Waves per SIMD the compiler must fit the register budget to (0 = its own choice): the light
+// round kernel took 81-91 VGPRs (5 waves per SIMD); at 7 (72 VGPRs, 16 bytes of scratch per lane)
+// its latency-bound pulls keep more loads in flight: k26w 596 -> 643 GTEPS interleaved (6: 634,
+// 8: 627 with 92 bytes of scratch; profiles/r05/occupancy_r5h17.txt). The heavy pull (65-73
+// VGPRs) at 8 measured equal.
+#ifndef PJ_V2_WPE_R
+#define PJ_V2_WPE_R 7
+#endif
+#ifndef PJ_V2_WPE_H
+#define PJ_V2_WPE_H 0
+#endif
+#if PJ_V2_WPE_R
+#define V2_WPE_R __attribute__((amdgpu_waves_per_eu(PJ_V2_WPE_R)))
+#else
+#define V2_WPE_R
+#endif
+#if PJ_V2_WPE_H
+#define V2_WPE_H __attribute__((amdgpu_waves_per_eu(PJ_V2_WPE_H)))
+#else
+#define V2_WPE_H
+#endif
 #ifndef PJ_V2_MBC
 #define PJ_V2_MBC 1  // light pulls count the frontier's new members compacted, a lane each
 #endif
@@ -992,7 +1013,7 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, const Off* __restric
 // them), counts them into slot cout and folds min{new dist >= hi} into minv.
 constexpr bool V2_SELMB_PULL = PJ_V2_SELMB && PJ_V2_NOFIN >= 2;  // (the pull probes mb when NOFIN < 2)
 template <typename Off>
-__global__ __launch_bounds__(DB) void v2_pull_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fout,
+__global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fout,
                                                 int32_t nhi, int cout) {
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
@@ -1425,7 +1446,7 @@ union V2RoundLds {  // the round kernel's LDS: a tile-dense push
 // short rows, v2_pull_light_body, over the whole grid; the two touch disjoint
 // vertices, frontier words are OR-ed in), a tile-dense push, or a sparse push.
 template <typename Off>
-__global__ __launch_bounds__(DB) void v2_pull_round_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
+__global__ __launch_bounds__(DB) V2_WPE_R void v2_pull_round_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
                                                       u64* __restrict__ fout, int cin, u64 pull_thresh,
                                                       const u32* __restrict__ lcv, const u32* __restrict__ lcc, u64 nlc,
                                                       int hs, u64 dense_min, u64* __restrict__ fclr) {
