@@ -687,9 +687,13 @@ def line(main_res, wl, value, mean_ms, achieved, traffic, tts_s, tts_phases, cpu
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            # the measured DRAM-side rate: PMC bytes per solve over this run's device time per solve
+            # (frac above 1 means the solve moves fewer bytes than the algorithmic model counts)
+            "traffic_frac": (round(traffic / (1e9 * t_kernel / (args.steps * world)) / HBM_PEAK_GBS, 4)
+                             if traffic and t_kernel > 0 else None),
             "scope": "one launch = one SSSP solve (every kernel of the solve); bytes = SURVEY.md §8d "
                      "algorithmic bytes; time = HIP events on libpj's stream; traffic = PMC "
-                     "2*FETCH_SIZE + WRITE_SIZE per solve (profiles/)",
+                     "2*FETCH_SIZE + WRITE_SIZE per solve (profiles/); traffic_frac = traffic / time / peak",
         },
         "cpu_baseline": cpu,
         "secondary": secondary or None,
