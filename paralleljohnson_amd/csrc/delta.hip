@@ -162,6 +162,41 @@ __device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __re
     return stop;
 }
 
+// the same step probing a byte map (dist - lo of the probed set, 0xFF = not in it): the heavy
+// pull's map is 1/4 of dist and stays in the Infinity Cache (PJ_V2_HMAP)
+template <typename Off, typename E>
+__device__ __forceinline__ bool pull_step_map(const E ed, const uint8_t* __restrict__ map, Off& k, Off lim,
+                                              int32_t lo, int32_t& cur) {
+    u32 w[PU], u[PU];
+    bool ok[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        ok[j] = k + (Off)j < lim;
+        const u64 x = ok[j] ? eat(ed, (u64)(k + j)) : 0ull;
+        w[j] = (u32)(x >> 32);
+        u[j] = (u32)x;
+    }
+    bool stop = false;
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+        if (ok[j] && (long long)lo + w[j] >= (long long)cur) stop = true;
+        ok[j] = ok[j] && !stop;
+        nv += ok[j];
+    }
+    uint32_t m[PU];
+#pragma unroll
+    for (int j = 0; j < PU; ++j) m[j] = ok[j] ? map[u[j]] : 0xFFu;
+#pragma unroll
+    for (int j = 0; j < PU; ++j)
+        if (m[j] != 0xFFu) {
+            const long long nd = (long long)lo + m[j] + w[j];
+            if (nd < cur) cur = (int32_t)nd;
+        }
+    k += (Off)nv;
+    return stop;
+}
+
 // Pull screening (v2_pull_k, v2_pull_light_body): a wave reads the dists of PSC
 // groups of 64 vertices, compacts the candidates into lanes, probes PSERIAL edges
 // per lane (wave-uniform loop), then scans the long rows with the whole wave.
@@ -313,6 +348,9 @@ struct V2Ctl {
 #else
 #define V2_WPE_H
 #endif
+#ifndef PJ_V2_HMAP
+#define PJ_V2_HMAP 1  // the heavy pull probes a byte map of the band (built per heavy pull) instead of dist
+#endif
 #ifndef PJ_V2_MBC
 #define PJ_V2_MBC 1  // light pulls count the frontier's new members compacted, a lane each
 #endif
@@ -353,6 +391,8 @@ struct V2Args {
     u64 hcap;
     u64* rlog;   // round_log option: [0] = rounds logged, then (kind, frontier, its light edges) per round
     int32_t hz;  // heavy push: relax only the edges with du + w < hz (INT_INF = all; defer_heavy)
+    const uint8_t* hmap;  // heavy pull: dist - lo of every vertex with dist in [lo, hi), 0xFF otherwise
+                          // (PJ_V2_HMAP; null = probe dist)
     u64* dsave;  // heavy push: the member words are OR-ed in here (their far edges are deferred), or null
 };
 // the light edges of a band round (light CSR, or the light prefixes of cw in the tail)
@@ -998,6 +1038,24 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, const Off* __restric
     v2_flush_min(mn, a.ctl, red);
 }
 
+// The heavy pull's probe map: dist - lo for dist in [lo, hi), 0xFF otherwise (hi - lo <= 255)
+__global__ __launch_bounds__(256) void v2_hmap_k(const int32_t* __restrict__ dist, i64 n, int32_t lo, int32_t hi,
+                                                 uint8_t* __restrict__ map) {
+    const i64 n4 = n / 4;
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (i64)gridDim.x * blockDim.x) {
+        const int4 d = reinterpret_cast<const int4*>(dist)[i];
+        const int32_t dd[4] = {d.x, d.y, d.z, d.w};
+        u32 m = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m |= (u32)((dd[j] >= lo && dd[j] < hi) ? dd[j] - lo : 0xFF) << (8 * j);
+        reinterpret_cast<u32*>(map)[i] = m;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        const i64 v = n4 * 4 + threadIdx.x;
+        map[v] = (uint8_t)((dist[v] >= lo && dist[v] < hi) ? dist[v] - lo : 0xFF);
+    }
+}
+
 // Pull step of the heavy edges of band [lo, hi) fused with the selection of the
 // next band [hi, nhi) -- symmetric graphs only, where a row is also the vertex's
 // in-edges with the same weights. Every vertex with dist >= hi looks through the
@@ -1100,7 +1158,8 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
                 if (go) {
                     // band members are exactly mb's bits: probe the (cache-resident)
                     // bitmap first, read dist only for members
-                    if (pull_step_fin_cw<Off>(v2_cw_src(a), a.dist, hmb, k, lim, lo, hi, cur)) {
+                    if (a.hmap ? pull_step_map<Off>(v2_cw_src(a), a.hmap, k, lim, lo, cur)
+                               : pull_step_fin_cw<Off>(v2_cw_src(a), a.dist, hmb, k, lim, lo, hi, cur)) {
                         done = true;
                         go = false;
                     } else {
@@ -1139,7 +1198,13 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
                     int32_t cand = INT_INF;
                     if (!stop) {
-                        const int32_t du = pull_src(hmb, a.dist, (u32)x, hi);
+                        int32_t du;
+                        if (a.hmap) {
+                            const u32 m = a.hmap[(u32)x];
+                            du = m != 0xFFu ? lo + (int32_t)m : INT_INF;
+                        } else {
+                            du = pull_src(hmb, a.dist, (u32)x, hi);
+                        }
                         if (du < INT_INF) {
                             const long long nd = (long long)du + w;
                             cand = nd < INT_INF ? (int32_t)nd : INT_INF;
@@ -1641,6 +1706,7 @@ struct DeltaSolve {
     DevBuf<int32_t> out_own;
     DevBuf<u64> f[3], mb;      // light-round frontier ring (v2_clear_words), band members
     DevBuf<u64> sb;            // settled-before-the-tail bitmap
+    DevBuf<uint8_t> hmap;      // the heavy pull's probe map (PJ_V2_HMAP)
     DevBuf<u64> db;            // members whose far heavy edges are deferred (defer_heavy); all zero
     bool db_dirty = true;      // unless a solve stopped with a deferral pending (an error)
     DevBuf<V2Ctl> ctl;
@@ -1893,6 +1959,7 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     v.mb.alloc(nw);
     v.sb.alloc(nw);
     v.db.alloc(nw);
+    if (PJ_V2_HMAP) v.hmap.alloc((size_t)(n ? n : 1) + 16);
     v.ctl.alloc(1);
     v.hcap = (u64)std::max<i64>(1, std::min<i64>(n, g.nnz / (i64)V2_HT + 1));
     v.hv.alloc(3 * v.hcap);  // the hub queue's ring of three slots
@@ -1967,6 +2034,15 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     }
     a.hz = INT_INF;
     a.dsave = nullptr;
+    a.hmap = nullptr;
+    // the heavy pull's probe map over [mlo, mhi) when its values fit a byte (else dist is probed)
+    auto set_hmap = [&](int32_t mlo, int32_t mhi) {
+        a.hmap = nullptr;
+        if (!PJ_V2_HMAP || n == 0 || (long long)mhi - (long long)mlo > 255) return;
+        v2_hmap_k<<<grid_for((n + 3) / 4, 256, maxgrid), 256, 0, s>>>(v.dist, n, mlo, mhi, v.hmap.p);
+        PJ_LAUNCH_CHECK();
+        a.hmap = v.hmap.p;
+    };
     // the host's view of the counters: one block copies them into mapped host memory
     // (a D2H hipMemcpyAsync of the same 3.3 KB ran as a ~30 us blit per sync)
     // The host spins on the sequence number (wakes within ~1 us of the copy instead of
@@ -2059,7 +2135,9 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             if (can_pull && (double)heavy_left < g.pull_factor * (double)mh_def) {
                 a.lo = (int32_t)lo_def;
                 a.hi = (int32_t)nlo;
+                set_hmap(a.lo, a.hi);
                 v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi, cs);
+                a.hmap = nullptr;
                 PJ_LAUNCH_CHECK();
                 PJ_HIP(hipMemsetAsync(v.db.p, 0, sizeof(u64) * (size_t)nwords, s));
                 st.bu_levels++;
@@ -2183,7 +2261,9 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             if (pull_now) {
                 // deferred members (dist >= lo_def) are probed like this band's (dist < hi)
                 if (dpend) a.lo = (int32_t)lo_def;
+                set_hmap(a.lo, a.hi);
                 v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi_t, cs);
+                a.hmap = nullptr;
                 PJ_LAUNCH_CHECK();
                 a.lo = (int32_t)lo;
                 if (!V2_SELMB_PULL) PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
