@@ -299,10 +299,13 @@ constexpr int V2_NSH = 8;     // shards of a count slot
 #endif
 constexpr int V2_HTILE = DB * PJ_V2_HTM;  // hub-queue tile: edges per workgroup step (PJ_V2_HTM per thread)
 #ifndef PJ_V2_PLMAX
-#define PJ_V2_PLMAX 64  // swept 32 / 128 (round 4): 1% / 14% slower
+// swept 32 / 128 in round 4 (1% / 14% slower than 64); late round 5, with the frontier-minimum
+// bound and the 7-wave light-round kernel, 96-160 with 512- or 1024-edge chunks are 4% faster
+// than 64 / 256 (profiles/r05/pull_rows_r5h27.txt)
+#define PJ_V2_PLMAX 128
 #endif
 #ifndef PJ_V2_PCH
-#define PJ_V2_PCH 256
+#define PJ_V2_PCH 1024
 #endif
 constexpr u32 V2_PLMAX = PJ_V2_PLMAX;  // pull rounds: longer light rows go to v2_pull_long_body
 constexpr u32 V2_PCH = PJ_V2_PCH;      // light edges per v2_pull_long_body work item
