@@ -200,7 +200,8 @@ const int32_t* pj_dist_device(pj_graph* g);
  * unit weights ~n x (256 W + 8 W (1 + L)) bytes (a 64 W x n int32 distance block,
  * the reached masks and an archive of L <= 32 levels' W-word masks per vertex, L
  * reduced to keep a slot within 8 GB; ms_streams slots, default 2, all slots within
- * 16 GB); weights ~8 n bytes of rows plus ~60 x nnz / 64 bytes of hub queues per
+ * 16 GB); weights ~9.4 n bytes of rows and bitmaps (the heavy pull's n-byte map
+ * included) plus ~60 x nnz / 64 bytes of hub queues per
  * extra slot. A slot beyond the first is added only while it takes at most half
  * the free device memory, and a failed allocation leaves the batch on the
  * slots it has (no error). Either way pj_last_stats
