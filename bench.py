@@ -17,9 +17,13 @@ synthetic, source 0). Inputs are generated on the device (no dataset access).
   value        = GTEPS = sum over ranks of m_r / max-over-ranks wall time of the
                  timed steps; m_r = CSR entries of the reached vertices
                  (Graph500 TEPS over directed entries; gteps_graph500 = value / 2)
-  roofline     = SURVEY.md §8d algorithmic bytes per SSSP
-                 B = 4N + n_r(12 + 2*O) + m_r(8 + 4*weighted) divided by the
-                 solve's device time (HIP events on libpj's stream)
+  roofline     = scanned-work bytes per SSSP, B = 4N + n_r(12 + 2*O) + the edge
+                 records the solve read (as stored) + the probes of their other
+                 ends, both counted on the device in every timed solve, divided by
+                 the solve's device time (HIP events on libpj's stream); traffic =
+                 the calibrated DRAM-side bytes of the per-kernel table measured on
+                 this build (profiles/traffic_k26w.json, else null); frac_model_8d
+                 keeps SURVEY.md §8d's every-reached-edge model
   cpu_baseline = the reference's BSP heap algorithm (oracle port of :466-594,
                  weights honoured) on host threads, rank 0 at N=1 only, on a
                  bounded sample of one solve of the same graph
@@ -104,12 +108,14 @@ def run_workload(ctx, key, args, rank, world, barrier, steps, warmup):
     gen_s = time.perf_counter() - t_gen
     for k in range(warmup):
         g.sssp(my_roots[k % len(my_roots)], copy=False)
-    kernel_ms = []
+    kernel_ms, work = [], []
     barrier()
     t0 = time.perf_counter()
     for k in range(steps):
         g.sssp(my_roots[k], copy=False)
-        kernel_ms.append(g.stats()["kernel_ms"])
+        st = g.stats()
+        kernel_ms.append(st["kernel_ms"])
+        work.append((st["scanned_edges"], st["probes"], st["work_bytes"]))
     barrier()
     elapsed = time.perf_counter() - t0
     reach, levels = {}, {}
@@ -121,7 +127,12 @@ def run_workload(ctx, key, args, rank, world, barrier, steps, warmup):
     m_sum = float(sum(reach[r][1] for r in my_roots[:steps]))
     b_sum = float(sum(algorithmic_bytes(g.n, reach[r][0], reach[r][1], g.nnz, wl["weighted"])
                       for r in my_roots[:steps]))
-    return dict(g=g, wl=wl, elapsed=elapsed, m_sum=m_sum, b_sum=b_sum, t_kernel=sum(kernel_ms) / 1000.0,
+    # the scanned-work model (weighted solves count their work on the device, every solve):
+    # 4N + n_r(12 + 2*O) + the records read as stored + the probes of their other ends
+    o = 4 if g.nnz < 2**31 else 8
+    w_sum = float(sum(4 * g.n + reach[r][0] * (12 + 2 * o) for r in my_roots[:steps]) + sum(x[2] for x in work))
+    return dict(g=g, wl=wl, elapsed=elapsed, m_sum=m_sum, b_sum=b_sum, w_sum=w_sum, t_kernel=sum(kernel_ms) / 1000.0,
+                scanned=float(sum(x[0] for x in work)), probes=float(sum(x[1] for x in work)),
                 roots=my_roots[:steps], reach=reach, levels=levels, gen_s=gen_s, build_s=build_s, prep_s=prep_s)
 
 
@@ -174,20 +185,48 @@ def time_to_solution(ctx_s, res, tts, td):
                          "in_process_breakdown": phases}
 
 
-def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
+def partition_transport(ctx, rank, world, backend):
+    """The partitioned leg's pj_comm: one rank without a transport at world 1; at world > 1
+    libpj's RCCL group (one process per GPU, the group id handed out by rank 0 over
+    torch.distributed), or under a gloo rehearsal (PJ_BENCH_BACKEND=gloo) the host-buffer
+    callbacks over torch.distributed, which transport_guard rejects before any GPU work."""
+    from paralleljohnson_amd.partition import Comm, TorchDistTransport
+    if world == 1:
+        return Comm.for_rank(ctx, 1, 0)
+    if backend != "nccl":
+        return Comm.from_callbacks(TorchDistTransport(), rank, world)
+    import torch.distributed as dist
+    box = [Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)  # bootstrap only: the solve's collectives are libpj's RCCL calls
+    return Comm.for_rank(ctx, world, rank, box[0])
+
+
+def transport_guard(comm, world):
+    """The group the partitioned leg runs on, as the transport itself reports it (RCCL:
+    ncclCommCount / ncclCommUserRank, the reference's MPI_Comm_size / rank at :291-292). At
+    world > 1 anything but an RCCL communicator of exactly `world` ranks fails the leg, so an
+    N-GPU line cannot report a partitioned solve that did not run over N GPUs."""
+    count, index = comm.transport_ranks()
+    info = {"transport": comm.kind, "transport_ranks": count, "transport_rank": index}
+    if world > 1 and (comm.kind != "rccl" or count != world):
+        raise RuntimeError(f"partitioned leg at world {world} needs an RCCL communicator of {world} ranks; the "
+                           f"transport is {comm.kind!r} reporting {count} rank(s)")
+    return info
+
+
+def run_partitioned(ctx, args, rank, world, barrier, backend="nccl", nroots=4):
     """configs[3]: Kronecker s{part_scale} unit-weight BFS, 1D vertex partition over the
-    `world` ranks (libpj's level loop, pj_part_bfs, over RCCL: one process per GPU, the
-    group id handed out by rank 0 over torch.distributed); strong scaling."""
-    from paralleljohnson_amd.partition import Comm, load_kronecker
+    `world` ranks (libpj's level loop, pj_part_bfs, over RCCL: one process per GPU); strong
+    scaling. The transport is formed and checked (transport_guard) before the graph is built."""
+    from paralleljohnson_amd.partition import load_kronecker
     t0 = time.perf_counter()
+    comm = partition_transport(ctx, rank, world, backend)
+    try:
+        tinfo = transport_guard(comm, world)
+    except Exception:
+        comm.close()
+        raise
     ops = load_kronecker(ctx, args.part_scale, args.edgefactor, args.seed, rank, world)
-    if world > 1:
-        import torch.distributed as dist
-        box = [Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)  # bootstrap only: the solve's collectives are libpj's RCCL calls
-        comm = Comm.for_rank(ctx, world, rank, box[0])
-    else:
-        comm = Comm.for_rank(ctx, 1, 0)
     build_s = time.perf_counter() - t0
     rng = np.random.default_rng(args.seed + 7)
     roots = []
@@ -208,7 +247,7 @@ def run_partitioned(ctx, args, rank, world, barrier, nroots=4):
                   for _, st in roots))
     st0 = roots[0][1]
     res = dict(elapsed=elapsed, m=m, b=b, n=ops.n, nnz_local=ops.nnz_local, build_s=build_s, roots=len(roots),
-               st0=st0, transport=comm.kind, build_phases=ops.build_phases())
+               st0=st0, transport=tinfo, build_phases=ops.build_phases())
     ops.close()
     comm.close()
     return res
@@ -420,8 +459,20 @@ def launch_check(rank, world, backend):
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         el, m = float(tm[0]), float(t[1])
+    line = {"launch_check": True, "n_gpus": world, "elapsed_max": el, "units_sum": m}
+    if os.environ.get("PJ_BENCH_FORCE_PART") == "1" and world > 1:
+        # the partitioned leg's transport and its guard (no GPU: the gloo rehearsal's
+        # host-buffer transport is rejected before any device work)
+        try:
+            comm = partition_transport(None, rank, world, backend)
+            try:
+                line["k28_partitioned"] = transport_guard(comm, world)
+            finally:
+                comm.close()
+        except Exception as e:  # noqa: BLE001 (reported as the bench line reports it)
+            line["k28_partitioned"] = {"error": f"rank {rank}: {type(e).__name__}: {e}"[:300]}
     if rank == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": world, "elapsed_max": el, "units_sum": m}), flush=True)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -502,23 +553,22 @@ def main():
         time.sleep(5.0)
     main_res = run_workload(ctx, args.workload, args, rank, world, barrier, args.steps, args.warmup)
     elapsed, m_sum, b_sum, t_kernel = main_res["elapsed"], main_res["m_sum"], main_res["b_sum"], main_res["t_kernel"]
+    w_sum, scanned, probes = main_res["w_sum"], main_res["scanned"], main_res["probes"]
     if dist is not None:
-        t = torch.tensor([elapsed, m_sum, b_sum, t_kernel], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, m_sum, b_sum, t_kernel, w_sum, scanned, probes], dtype=torch.float64, device="cuda")
         tmax = t[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
-        m_sum, b_sum, t_kernel = float(t[1]), float(t[2]), float(t[3])
+        m_sum, b_sum, t_kernel, w_sum, scanned, probes = (float(x) for x in t[1:])
     wl = main_res["wl"]
     g = main_res["g"]
     value = m_sum / elapsed / 1e9
-    achieved = b_sum / t_kernel / 1e9  # GB/s: algorithmic bytes per solve / device time per solve
-
-    traffic = None
-    tj_path = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
-    if os.path.exists(tj_path) and not args.scale:
-        with open(tj_path) as f:
-            traffic = json.load(f).get("hbm_bytes_per_sssp")
+    work = {"achieved": w_sum / t_kernel / 1e9,  # GB/s: scanned-work bytes per solve / device time per solve
+            "model_8d": b_sum / t_kernel / 1e9, "scanned": scanned, "probes": probes, "w_sum": w_sum}
+    if not wl["weighted"]:  # (the unit-weight BFS has no device work counters: SURVEY.md §8d's model)
+        work["achieved"] = work["model_8d"]
+    traffic = measured_traffic(args) if wl["weighted"] else None
 
     tts_s, tts_phases = time_to_solution(ctx_s, main_res, tts, tts_dir.name) if tts else (None, None)
     tts_dir.cleanup()
@@ -586,7 +636,7 @@ def main():
 
     def emit():
         if rank == 0:
-            print(json.dumps(line(main_res, wl, value, mean_ms, achieved, traffic, tts_s, tts_phases, cpu, secondary,
+            print(json.dumps(line(main_res, wl, value, mean_ms, work, traffic, tts_s, tts_phases, cpu, secondary,
                                   n_vertices, nnz, t_kernel, world, args)), flush=True)
 
     force_part = os.environ.get("PJ_BENCH_FORCE_PART") == "1"  # (tests the guard under a gloo rehearsal)
@@ -606,7 +656,7 @@ def main():
         wd.daemon = True
         wd.start()
         try:
-            pr = run_partitioned(ctx, args, rank, world, barrier)
+            pr = run_partitioned(ctx, args, rank, world, barrier, backend)
         except Exception as e:  # noqa: BLE001 (reported in the line, not fatal to it)
             pr = None
             secondary["k28_partitioned"] = {"error": f"rank {rank}: {type(e).__name__}: {e}"[:300]}
@@ -631,7 +681,8 @@ def main():
         per = el / pr["roots"]
         secondary["k28_partitioned"] = {
             "workload": f"graph500-kronecker-s{args.part_scale}-ef{args.edgefactor}-unit-bfs, 1D vertex "
-                        f"partition over {world} GPU(s), libpj level loop, transport {pr['transport']}",
+                        f"partition over {world} GPU(s), libpj level loop, transport {pr['transport']['transport']}",
+            **pr["transport"],
             "n_vertices": pr["n"], "nnz": 2 * (args.edgefactor << args.part_scale),
             "nnz_local_rank0": pr["nnz_local"], "roots": pr["roots"],
             "time_to_solution_ms": round(1000.0 * per, 3),
@@ -647,11 +698,69 @@ def main():
         dist.destroy_process_group()
 
 
-def line(main_res, wl, value, mean_ms, achieved, traffic, tts_s, tts_phases, cpu, secondary, n_vertices, nnz,
+def measured_traffic(args):
+    """The DRAM-side bytes per k26w solve of the last per-kernel table (tools/cycle.sh wtable ->
+    profiles/traffic_k26w.json) and its per-kernel rows -- only when the table was measured on
+    the loaded build (pj_build_id(): a digest of libpj's sources and flags); otherwise the
+    line carries traffic null and says why."""
+    import paralleljohnson_amd as pj
+    path = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
+    if args.scale or args.opt:
+        return {"bytes": None, "note": "not measured for this configuration"}
+    if not os.path.exists(path):
+        return {"bytes": None, "note": f"{os.path.relpath(path, ROOT)} missing"}
+    with open(path) as f:
+        tj = json.load(f)
+    if tj.get("build_id") != pj.build_id():
+        return {"bytes": None, "note": f"{os.path.relpath(path, ROOT)} was measured on build {tj.get('build_id')}, "
+                                       f"the loaded libpj is {pj.build_id()}: stale, not reported"}
+    return {"bytes": tj["hbm_bytes_per_sssp"], "table": tj, "path": os.path.relpath(path, ROOT)}
+
+
+def line(main_res, wl, value, mean_ms, work, traffic, tts_s, tts_phases, cpu, secondary, n_vertices, nnz,
          t_kernel, world, args):
     """The one JSON line of the run (rank 0)."""
     r0 = main_res["roots"][0]
     lv = main_res["levels"][r0]
+    solves = args.steps * world
+    t_solve = t_kernel / solves  # device seconds per solve
+    roofline = {
+        "bound": "hbm",
+        "achieved": round(work["achieved"], 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(work["achieved"] / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "traffic_frac": None,
+        "model": ("scanned work, counted on the device in every timed solve: 4N + n_r(12 + 2*O) + the edge records "
+                  "read as stored (4-byte packed light CSR, 5-byte u32 id + u8 weight) + the probes of their other "
+                  "ends (4-byte dist, 1-byte heavy-pull map); time = HIP events on libpj's stream, all kernels of a "
+                  "solve" if wl["weighted"] else "SURVEY.md §8d (unit-weight BFS: no work counters)"),
+        "bytes_per_sssp": round(work["w_sum"] / solves),
+        "scanned_edges_per_sssp": round(work["scanned"] / solves),
+        "probes_per_sssp": round(work["probes"] / solves),
+        "frac_model_8d": round(work["model_8d"] / HBM_PEAK_GBS, 4),
+        "model_8d": "SURVEY.md §8d: 4N + n_r(12 + 2*O) + m_r(8 + 4*weighted), every reached edge read; the solve "
+                    "scans a fraction of them (a pull stops a row at its first useless weight), so this figure can "
+                    "exceed 1 and bounds nothing",
+    }
+    if traffic is not None:
+        roofline["traffic_note"] = traffic.get("note")
+        if traffic.get("bytes"):
+            tb, tab = traffic["bytes"], traffic["table"]
+            roofline["traffic"] = round(tb)
+            roofline["traffic_frac"] = round(tb / t_solve / 1e9 / HBM_PEAK_GBS, 4)
+            roofline["traffic_note"] = (f"DRAM-side bytes per solve of {traffic['path']} (build {tab['build_id']}, "
+                                        f"the loaded one): (RDREQ - RDREQ_32B) x {tab['bytes_per_request']:.0f} + "
+                                        f"RDREQ_32B x 32 + WRITE_SIZE, calibrated by {tab['calibration']}; "
+                                        f"Infinity-Cache hits included (an upper bound)")
+            dom = max(tab["kernels"], key=lambda r: r["ms"])
+            roofline["dominant_kernel"] = {
+                "kernel": dom["kernel"], "ms_per_sssp": round(dom["ms"], 4),
+                "work_bytes": round(dom["work_bytes"]), "dram_bytes": round(dom["dram_bytes"]),
+                "work_frac": round(dom["work_bytes"] / (dom["ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "dram_frac": round(dom["dram_bytes"] / (dom["ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "source": traffic["path"] + " (rocprofv3 kernel trace + --pmc passes of tools/traffic_probe.py)"}
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -674,27 +783,18 @@ def line(main_res, wl, value, mean_ms, achieved, traffic, tts_s, tts_phases, cpu
         },
         "gteps_graph500": round(value / 2, 3),
         "ms_per_sssp": round(mean_ms, 4),
+        "scanned_edges_per_sssp": round(work["scanned"] / solves),
+        "m_r_per_sssp": round(main_res["m_sum"] / args.steps),
         "time_to_solution_s": tts_s,
         "time_to_solution_phases": tts_phases,
         "scaling_note": ("N>1: the graph is replicated and the roots are sharded (no exchange between GPUs), "
                          "i.e. ideal weak scaling; the partitioned multi-GPU solve is secondary.k28_partitioned"),
-        "kernel_ms_mean": round(1000.0 * t_kernel / (args.steps * world), 4),
+        "kernel_ms_mean": round(1000.0 * t_solve, 4),
+        "step": ("one SSSP: distances initialised -> final in the solver's degree-ordered ids on the device; the "
+                 "gather to input ids (0.2 ms at s26) runs with the first read of the result (D2H, sol_file, "
+                 "pj_dist_device) and is inside time_to_solution_s"),
         "bands_or_levels": lv[0], "relax_launches": lv[3],
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            # the measured DRAM-side rate: PMC bytes per solve over this run's device time per solve
-            # (frac above 1 means the solve moves fewer bytes than the algorithmic model counts)
-            "traffic_frac": (round(traffic / (1e9 * t_kernel / (args.steps * world)) / HBM_PEAK_GBS, 4)
-                             if traffic and t_kernel > 0 else None),
-            "scope": "one launch = one SSSP solve (every kernel of the solve); bytes = SURVEY.md §8d "
-                     "algorithmic bytes; time = HIP events on libpj's stream; traffic = PMC "
-                     "2*FETCH_SIZE + WRITE_SIZE per solve (profiles/); traffic_frac = traffic / time / peak",
-        },
+        "roofline": roofline,
         "cpu_baseline": cpu,
         "secondary": secondary or None,
     }

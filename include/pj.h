@@ -49,7 +49,10 @@ typedef struct pj_graph pj_graph;
 /* Per-solve statistics of the last pj_sssp* call on a graph. */
 typedef struct pj_stats {
     double kernel_ms;        /* device time, dist init -> distances final (HIP events on the ctx stream);
-                                the analogue of the reference's timed region :459-462 ... :597-605 */
+                                the analogue of the reference's timed region :459-462 ... :597-605.
+                                Weighted single-source solves end with the distances in the solver's
+                                degree-ordered ids; the gather to input ids runs when the result is
+                                first read (pj_copy_dist, pj_dist_device, ...) and is not in kernel_ms */
     double wall_ms;          /* host wall time of the call, incl. D2H of dist when requested */
     int64_t levels;          /* BFS levels / delta-stepping buckets processed */
     int64_t td_levels;       /* top-down (push) levels */
@@ -57,6 +60,15 @@ typedef struct pj_stats {
     int64_t reached;         /* n_r: vertices with dist < PJ_INT_INF (filled by pj_reach_stats) */
     int64_t reached_edges;   /* m_r: sum of out-degree over reached vertices (pj_reach_stats) */
     int64_t relax_rounds;    /* weighted: light/heavy relaxation rounds */
+    /* weighted (delta-stepping): the work of the relaxation kernels, counted on the device in
+     * every solve -- the analogue of the reference's edge scans (the loop of
+     * extract_local_pq :242-275 reads every out-edge of every popped vertex) */
+    int64_t scanned_edges;   /* edge records read (packed light CSR, or u32 id + u8 weight) */
+    int64_t probes;          /* reads of an edge's other end: its distance, the heavy pull's byte map,
+                                or the tail's settled bitmap */
+    int64_t work_bytes;      /* the bytes of both as stored (records of 4, 5 or 8 bytes, probes of 4 or 1) */
+    int64_t work_by_kernel[4][3]; /* (records, probes, bytes) of the light-round kernel, the light hub
+                                     kernel, the heavy pull and the heavy push */
 } pj_stats;
 
 /* ---- context ------------------------------------------------------------ */
@@ -71,6 +83,9 @@ int pj_destroy(pj_ctx* ctx);
 void* pj_stream(pj_ctx* ctx);
 const char* pj_last_error(void);
 const char* pj_version(void);
+/* A digest of the library's sources and compile flags (16 hex digits): measurements kept in
+ * files (profiles/) carry it, so a reader can tell whether they were taken on this build. */
+const char* pj_build_id(void);
 /* Device blocks of 1 GiB or more that libpj freed stay cached in the process (up to half
  * of the device's memory) and serve later big allocations whole or in slices: a fresh
  * allocation of memory just returned to the driver waits for it to be cleared (seconds
@@ -486,6 +501,11 @@ typedef struct pj_comm_callbacks {
 int pj_comm_create_callbacks(const pj_comm_callbacks* cb, pj_comm** out);
 /* kind: "self", "rccl", "host" or "callbacks" */
 int pj_comm_info(const pj_comm* c, int* rank, int* world, const char** kind);
+/* The group's size and this rank's index as the transport itself reports them -- for RCCL
+ * ncclCommCount / ncclCommUserRank of the communicator (the reference's MPI_Comm_size /
+ * MPI_Comm_rank, :291-292), the thread group's size for the host transport, 1 for self,
+ * the declared world for callbacks -- so that a launcher can prove the group it formed. */
+int pj_comm_transport_ranks(const pj_comm* c, int* count, int* index);
 int pj_comm_destroy(pj_comm* c);
 
 /* Statistics of one rank's partitioned solve. reached / reached_edges are for

@@ -57,10 +57,17 @@ class PJError(RuntimeError):
 class Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double), ("levels", ctypes.c_int64),
                 ("td_levels", ctypes.c_int64), ("bu_levels", ctypes.c_int64), ("reached", ctypes.c_int64),
-                ("reached_edges", ctypes.c_int64), ("relax_rounds", ctypes.c_int64)]
+                ("reached_edges", ctypes.c_int64), ("relax_rounds", ctypes.c_int64),
+                ("scanned_edges", ctypes.c_int64), ("probes", ctypes.c_int64), ("work_bytes", ctypes.c_int64),
+                ("work_by_kernel", (ctypes.c_int64 * 3) * 4)]
+    # rows of work_by_kernel (pj.h): (records, probes, bytes) per kernel class
+    WORK_KERNELS = ("light_round", "light_hub", "heavy_pull", "heavy_push")
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "work_by_kernel"}
+        d["work_by_kernel"] = {name: [int(x) for x in self.work_by_kernel[i]]
+                               for i, name in enumerate(self.WORK_KERNELS)}
+        return d
 
 
 class TreeReport(ctypes.Structure):
@@ -84,6 +91,7 @@ _SIGS = {
     "pj_stream": ([_P], _P),
     "pj_last_error": ([], ctypes.c_char_p),
     "pj_version": ([], ctypes.c_char_p),
+    "pj_build_id": ([], ctypes.c_char_p),
     "pj_trim_device_cache": ([_P], _INT),
     "pj_load_snap": ([_P, ctypes.c_char_p, _INT, _PP], _INT),
     "pj_load_snap_buffer": ([_P, ctypes.c_char_p, _I64, _INT, _PP], _INT),
@@ -153,6 +161,7 @@ _SIGS = {
     "pj_comm_create_group": ([_P, _INT, _INT, _P], _INT),
     "pj_comm_create_callbacks": ([_P, _PP], _INT),
     "pj_comm_info": ([_P, _P, _P, _P], _INT),
+    "pj_comm_transport_ranks": ([_P, _P, _P], _INT),
     "pj_comm_destroy": ([_P], _INT),
     "pj_part_bfs": ([_P, _P, _I64, _P], _INT),
     "pj_part_set_option": ([_P, ctypes.c_char_p, ctypes.c_double], _INT),
@@ -196,6 +205,12 @@ def _ptr(a: Optional[np.ndarray]):
 
 def version() -> str:
     return _lib.pj_version().decode()
+
+
+def build_id() -> str:
+    """Digest of libpj's sources and compile flags (pj_build_id): measurements kept under
+    profiles/ carry it, so a reader can tell whether they were taken on the loaded build."""
+    return _lib.pj_build_id().decode()
 
 
 def trim_device_cache() -> int:

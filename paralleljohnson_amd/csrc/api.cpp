@@ -695,7 +695,10 @@ int pj_sssp(pj_graph* pg, int64_t source, int32_t* dist_out) {
         if (g.weighted) delta_solve(g, source);
         else bfs_solve(g, source);
         g.last_source = source;
-        if (dist_out && g.n) copy_d2h_staged(*g.ctx, dist_out, g.dist.p, 4 * (size_t)g.n);
+        if (dist_out && g.n) {
+            delta_materialize(g);
+            copy_d2h_staged(*g.ctx, dist_out, g.dist.p, 4 * (size_t)g.n);
+        }
         g.stats.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         return (int)PJ_OK;
     });
@@ -709,6 +712,7 @@ int pj_copy_dist(pj_graph* pg, int32_t* dist_out) {
     }
     return guarded([&] {
         bind(*pg->g.ctx);
+        delta_materialize(pg->g);
         if (pg->g.n) copy_d2h_staged(*pg->g.ctx, dist_out, pg->g.dist.p, 4 * (size_t)pg->g.n);
         return (int)PJ_OK;
     });
@@ -730,7 +734,15 @@ int pj_host_unpin(void* p) {
     });
 }
 
-const int32_t* pj_dist_device(pj_graph* pg) { return (pg && pg->g.have_result) ? pg->g.dist.p : nullptr; }
+const int32_t* pj_dist_device(pj_graph* pg) {
+    if (!pg || !pg->g.have_result) return nullptr;
+    const int rc = guarded([&] {
+        bind(*pg->g.ctx);
+        delta_materialize(pg->g);  // (complete when it returns)
+        return (int)PJ_OK;
+    });
+    return rc == PJ_OK ? pg->g.dist.p : nullptr;
+}
 
 // ---- shortest-path tree (tree.hip) ---------------------------------------------
 
@@ -742,6 +754,7 @@ int pj_parent_tree(pj_graph* pg, int64_t* parent_out) {
     }
     return guarded([&] {
         bind(*pg->g.ctx);
+        delta_materialize(pg->g);
         parent_tree(pg->g, pg->g.last_source, parent_out);
         return (int)PJ_OK;
     });
@@ -755,6 +768,7 @@ int pj_validate_tree(pj_graph* pg, int64_t source, const int64_t* parent, pj_tre
     }
     return guarded([&] {
         bind(*pg->g.ctx);
+        delta_materialize(pg->g);
         validate_tree(pg->g, source, parent, out);
         return (int)PJ_OK;
     });
@@ -859,6 +873,7 @@ int pj_reach_stats(pj_graph* pg, pj_stats* out) {
     return guarded([&] {
         bind(*pg->g.ctx);
         i64 nr = 0, mr = 0;
+        delta_materialize(pg->g);
         reach_stats(pg->g, &nr, &mr);
         pg->g.stats.reached = nr;
         pg->g.stats.reached_edges = mr;
@@ -1730,6 +1745,14 @@ int pj_comm_info(const pj_comm* c, int* rank, int* world, const char** kind) {
     if (world) *world = c->c->world;
     if (kind) *kind = c->c->kind();
     return PJ_OK;
+}
+
+int pj_comm_transport_ranks(const pj_comm* c, int* count, int* index) {
+    if (!c || !count || !index) return arg_error("pj_comm_transport_ranks: bad argument");
+    return guarded([&] {
+        c->c->transport_ranks(count, index);
+        return (int)PJ_OK;
+    });
 }
 
 int pj_comm_destroy(pj_comm* c) {

@@ -122,6 +122,10 @@ struct ThreadComm final : Comm {
     int device = -1;
     u64 seq = 0;  // slot collectives so far (the same on every rank): the bank of the next one
     const char* kind() const override { return "host"; }
+    void transport_ranks(int* count, int* index) const override {
+        *count = g->world;
+        *index = rank;
+    }
 
     void allreduce(i64* v, int k, bool is_min, hipStream_t) override {
         if (k <= g->kslot) {  // one barrier: publish into this collective's bank, then reduce
@@ -241,6 +245,8 @@ struct RcclApi {
     decltype(&ncclGetErrorString) errorString = nullptr;
     decltype(&ncclCommAbort) commAbort = nullptr;
     decltype(&ncclCommGetAsyncError) getAsyncError = nullptr;
+    decltype(&ncclCommCount) commCount = nullptr;
+    decltype(&ncclCommUserRank) commUserRank = nullptr;
 };
 
 const RcclApi& rccl() {
@@ -266,11 +272,13 @@ const RcclApi& rccl() {
         PJ_SYM(errorString, ncclGetErrorString);
         PJ_SYM(commAbort, ncclCommAbort);
         PJ_SYM(getAsyncError, ncclCommGetAsyncError);
+        PJ_SYM(commCount, ncclCommCount);
+        PJ_SYM(commUserRank, ncclCommUserRank);
 #undef PJ_SYM
     });
     if (!api.h || !api.getUniqueId || !api.commInitRank || !api.commInitAll || !api.allReduce || !api.allGather ||
         !api.send || !api.recv || !api.groupStart || !api.groupEnd || !api.commDestroy || !api.errorString ||
-        !api.commAbort || !api.getAsyncError)
+        !api.commAbort || !api.getAsyncError || !api.commCount || !api.commUserRank)
         throw Error(PJ_ERR_COMM, "RCCL (librccl.so.1) is not available");
     return api;
 }
@@ -294,6 +302,11 @@ struct RcclComm final : Comm {
     DevBuf<i64> scratch;  // allreduce values / all-gathered count rows
     PinnedBuf<i64> host;
     const char* kind() const override { return "rccl"; }
+    void transport_ranks(int* count, int* index) const override {
+        usable();
+        nccl_check(rccl().commCount(c, count), "ncclCommCount");
+        nccl_check(rccl().commUserRank(c, index), "ncclCommUserRank");
+    }
 
     void init_buffers() {
         PJ_HIP(hipSetDevice(device));

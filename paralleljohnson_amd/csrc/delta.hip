@@ -91,37 +91,23 @@ __device__ __forceinline__ u64 eat(const ESrc& s, u64 k) {
     return s.e64[k];
 }
 
-// PJ_V2_NOFIN (1: light pulls, 2: light and heavy pulls): a pull takes its candidate from
-// every in-neighbour u with dist[u] < hi, one dist probe, instead of first testing u's bit
-// in the round's frontier (light) or the band's members (heavy) and reading dist[u] only for
-// a set bit. Exact: every u with dist[u] < hi outside that set has already relaxed its
-// edges of this kind at its current distance (a lowered vertex re-enters the frontier), so
-// dist[u] + w >= dist[v] and it never lowers v's running best.
-// k26w 450.6 / 450.6 -> 472.8 / 471.3 (1) -> 487.0 / 486.9 GTEPS (2) interleaved (r5a)
-#ifndef PJ_V2_NOFIN
-#define PJ_V2_NOFIN 2
-#endif
-
-// (Round 5: the bits probed first again on sparse rounds only -- light pull rounds whose
-// frontier is below n / 16 or n / 64, heavy pulls whose members hold below nnz / 16 edges --
-// measured 1-2% slower or equal, profiles/r05/ab_fbits_r5i.txt: dist alone everywhere.)
-// the candidate distance u offers through a pulled edge (INT_INF = none): bits == null
-// probes dist[u] alone (PJ_V2_NOFIN), else u's bit first. (Round 5: a per-round byte map of
-// the frontier's distances, dist - lo, probed instead of dist -- the map 4x denser in the
-// caches, built and undone by a kernel per round -- measured 7% slower: the pull rounds
-// gained 5% and the build launches cost more; removed, profiles/r05/ab_fmap_r5h.txt.)
-__device__ __forceinline__ int32_t pull_src(const u64* __restrict__ bits, const int32_t* __restrict__ dist, u32 u,
-                                            int32_t hi) {
-    if (!bits) {
-        const int32_t d = dist[u];
-        return d < hi ? d : INT_INF;
-    }
-    return ((bits[u >> 6] >> (u & 63)) & 1ull) ? dist[u] : INT_INF;
+// A pull takes its candidate from every in-neighbour u with dist[u] < hi, one dist probe
+// (round 5), instead of first testing u's bit in the round's frontier (light) or the band's
+// members (heavy) and reading dist[u] only for a set bit. Exact: every u with dist[u] < hi
+// outside that set has already relaxed its edges of this kind at its current distance (a
+// lowered vertex re-enters the frontier), so dist[u] + w >= dist[v] and it never lowers v's
+// running best. k26w 450.6 -> 487.0 GTEPS interleaved (profiles/r05/nofin_ab_r5a.txt); the
+// bits probed first on sparse rounds only measured 1-2% slower (ab_fbits_r5i.txt), and a
+// per-round byte map of the frontier's distances 7% slower (its build launches cost more
+// than the pulls gained, ab_fmap_r5h.txt).
+// the candidate distance u offers through a pulled edge (INT_INF = none)
+__device__ __forceinline__ int32_t pull_src(const int32_t* __restrict__ dist, u32 u, int32_t hi) {
+    const int32_t d = dist[u];
+    return d < hi ? d : INT_INF;
 }
 template <typename Off, typename E>
-__device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __restrict__ dist,
-                                                 const u64* __restrict__ fin, Off& k, Off lim, int32_t lo,
-                                                 int32_t hi, int32_t& cur) {
+__device__ __forceinline__ bool pull_step_dist(const E ed, const int32_t* __restrict__ dist, Off& k, Off lim,
+                                               int32_t lo, int32_t hi, int32_t& cur) {
     u32 w[PU], u[PU];
     bool ok[PU];
 #pragma unroll
@@ -140,18 +126,10 @@ __device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __re
         nv += ok[j];
     }
     int32_t du[PU];
-    if (!fin) {
 #pragma unroll
-        for (int j = 0; j < PU; ++j) du[j] = ok[j] ? dist[u[j]] : INT_INF;
+    for (int j = 0; j < PU; ++j) du[j] = ok[j] ? dist[u[j]] : INT_INF;
 #pragma unroll
-        for (int j = 0; j < PU; ++j) du[j] = du[j] < hi ? du[j] : INT_INF;
-    } else {
-        u64 fw[PU];
-#pragma unroll
-        for (int j = 0; j < PU; ++j) fw[j] = ok[j] ? fin[u[j] >> 6] : 0ull;
-#pragma unroll
-        for (int j = 0; j < PU; ++j) du[j] = (ok[j] && ((fw[j] >> (u[j] & 63)) & 1ull)) ? dist[u[j]] : INT_INF;
-    }
+    for (int j = 0; j < PU; ++j) du[j] = du[j] < hi ? du[j] : INT_INF;
 #pragma unroll
     for (int j = 0; j < PU; ++j)
         if (du[j] < INT_INF) {
@@ -163,7 +141,7 @@ __device__ __forceinline__ bool pull_step_fin_cw(const E ed, const int32_t* __re
 }
 
 // the same step probing a byte map (dist - lo of the probed set, 0xFF = not in it): the heavy
-// pull's map is 1/4 of dist and stays in the Infinity Cache (PJ_V2_HMAP)
+// pull's map is 1/4 of dist and stays in the Infinity Cache (v2_hmap_k)
 template <typename Off, typename E>
 __device__ __forceinline__ bool pull_step_map(const E ed, const uint8_t* __restrict__ map, Off& k, Off lim,
                                               int32_t lo, int32_t& cur) {
@@ -314,22 +292,22 @@ struct alignas(64) V2Line {
     u64 v;
     u64 pad[7];
 };
+// The work of a solve, always counted (SURVEY.md §8d's byte model counts every reached edge; a
+// pull stops a row at its first useless weight and most of a push's targets are probed once):
+// per kernel class, the edge records its relaxations read (.v), the probes of the edges' other
+// ends they issued (.pad[0]: dist, the heavy pull's byte map, or the tail's settled bitmap) and
+// the bytes of both as stored (.pad[1]: records of 4, 5 or 8 bytes, probes of 4 or 1). Each
+// wave sums its counts in wave-uniform registers; one atomic per workgroup and counter at the
+// end of a launch (v2_flush_work).
+enum { V2W_ROUND = 0, V2W_HUB = 1, V2W_HPULL = 2, V2W_HPUSH = 3, V2W_N = 4 };
 struct V2Ctl {
     V2Line cnt[4][V2_NSH];  // frontier vertices marked per light round (ring)
     V2Line hub[3];          // hub queue packed counters (ring)
     V2Line mh[V2_NSH];      // heavy edges of this band's members
     V2Line minv[V2_NSH];    // min dist >= lo of the last select / pull (next band search), per shard
-    V2Line dbg[8];          // PJ_V2_STATS builds: vertices, edges, atomics, marks, hub edges
+    V2Line aux;             // v2_heavy_left_k's sum (the tail switch's heavy_left)
+    V2Line work[V2W_N][V2_NSH];
 };
-#ifndef PJ_V2_FMIN
-#define PJ_V2_FMIN 1  // light pulls stop rows at the frontier's least distance (v2_flush_fmin)
-#endif
-#ifndef PJ_V2_SELMB
-// the selections (v2_select_k, v2_pull_k's fused one) write the next band's member words of mb
-// and add the members' heavy / light degrees, so its first round finds no new members to count
-// one by one
-#define PJ_V2_SELMB 1
-#endif
 // Waves per SIMD the compiler must fit the register budget to (0 = its own choice): the light
 // round kernel took 81-91 VGPRs (5 waves per SIMD); at 7 (72 VGPRs, 16 bytes of scratch per lane)
 // its latency-bound pulls keep more loads in flight: k26w 596 -> 643 GTEPS interleaved (6: 634,
@@ -351,18 +329,6 @@ struct V2Ctl {
 #else
 #define V2_WPE_H
 #endif
-#ifndef PJ_V2_HMAP
-#define PJ_V2_HMAP 1  // the heavy pull probes a byte map of the band (built per heavy pull) instead of dist
-#endif
-#ifndef PJ_V2_MBC
-#define PJ_V2_MBC 1  // light pulls count the frontier's new members compacted, a lane each
-#endif
-#ifndef PJ_V2_PSTATS
-#define PJ_V2_PSTATS 0  // debug build: heavy-pull scan-length counters (printed per solve)
-#endif
-#ifndef PJ_V2_STATS
-#define PJ_V2_STATS 0
-#endif
 
 struct V2Args {
     i64 n, nwords;
@@ -377,10 +343,9 @@ struct V2Args {
     const u32* col;   // relabeled ids beside w8 (split records of the whole CSR), when w8 is set
     const uint8_t* w8;
     const u64* hl;    // bit v: v has a light edge (lsplit[v] > 0) for this delta; null in the tail
-    const uint8_t* w1;  // (PJ_V2_LWF) the lightest weight of v's row (capped at 255), or null: the light
-                        // pull's candidate filter
-    const uint8_t* hw;  // (PJ_V2_HWF) weight of v's first heavy edge for the current threshold (capped
-                        // at 255; 0 = no heavy edge), or null: the heavy pull's candidate filter
+    const uint8_t* w1;  // the lightest weight of v's row (capped at 255): the light pull's candidate filter
+    const uint8_t* hw;  // weight of v's first heavy edge for the current threshold (capped at 255; 0 = no
+                        // heavy edge): the heavy pull's candidate filter
     int ltail;        // tail mode: light prefixes are row[v] + [0, lsplit[v]) of cw (no light CSR)
     const u64* sbits; // tail mode: settled-before-the-tail bitmap; relaxations skip its targets
     u64* swrite;      // the heavy step entering the tail writes that bitmap (pull / select)
@@ -395,7 +360,7 @@ struct V2Args {
     u64* rlog;   // round_log option: [0] = rounds logged, then (kind, frontier, its light edges) per round
     int32_t hz;  // heavy push: relax only the edges with du + w < hz (INT_INF = all; defer_heavy)
     const uint8_t* hmap;  // heavy pull: dist - lo of every vertex with dist in [lo, hi), 0xFF otherwise
-                          // (PJ_V2_HMAP; null = probe dist)
+                          // (null = probe dist: bands wider than 255)
     u64* dsave;  // heavy push: the member words are OR-ed in here (their far edges are deferred), or null
 };
 // the light edges of a band round (light CSR, or the light prefixes of cw in the tail)
@@ -406,6 +371,46 @@ __device__ __forceinline__ ESrc v2_cw_src(const V2Args& a) {
 __device__ __forceinline__ ESrc v2_light_src(const V2Args& a) {
     if (a.ltail) return v2_cw_src(a);
     return ESrc{a.lcw, a.lcw32, a.lcb, nullptr};
+}
+// bytes of one edge record as stored: u32 id + u8 weight, a packed 32-bit record, or u64
+__device__ __forceinline__ u32 esrc_bytes(const ESrc& s) { return s.w8 ? 5u : s.e32 ? 4u : 8u; }
+
+// A wave's work counts, flushed once per launch into ctl->work[kind] (one atomic per
+// workgroup and counter). The increments are taken from lane 0 (readfirstlane), so the
+// counters live in scalar registers and cost the latency-bound kernels no VGPR; every
+// increment is made in wave-uniform control flow.
+__device__ __forceinline__ u32 v2_uni(u32 x) { return (u32)__builtin_amdgcn_readfirstlane((int)x); }
+struct V2Work {
+    u32 rec = 0, prb = 0;
+    __device__ __forceinline__ void add(u32 r, u32 p) {
+        rec += v2_uni(r);
+        prb += v2_uni(p);
+    }
+};
+// div: every wave of the block added the same block-uniform counts (tile-wide work), so the
+// block's sum is divided by the waves
+__device__ __forceinline__ void v2_flush_work(const V2Args& a, int kind, const V2Work& wk, u32 rec_bytes,
+                                              u32 prb_bytes, u64* red, u32 div = 1) {
+    __syncthreads();
+    if (lane_id() == 0) {
+        red[wave_id()] = wk.rec;
+        red[DB / WAVE + wave_id()] = wk.prb;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 r = 0, p = 0;
+        for (int w = 0; w < DB / WAVE; ++w) {
+            r += red[w];
+            p += red[DB / WAVE + w];
+        }
+        r /= div;
+        p /= div;
+        V2Line& l = a.ctl->work[kind][blockIdx.x % V2_NSH];
+        if (r) atomicAdd(&l.v, r);
+        if (p) atomicAdd(&l.pad[0], p);
+        if (r | p) atomicAdd(&l.pad[1], r * rec_bytes + p * prb_bytes);
+    }
+    __syncthreads();
 }
 
 
@@ -442,12 +447,12 @@ __device__ __forceinline__ void v2_flush_min(int32_t mn, V2Ctl* ctl, u64* red) {
     }
     __syncthreads();
 }
-// The least distance the frontier of a count slot holds (.pad[1], PJ_V2_FMIN): every
-// write that lowers a vertex into the band is folded in (a relaxation that marks, a pull's
-// store, the selection of a band's first frontier), so it bounds the frontier from below
-// and a pull round can stop a row at fmin + w >= its best instead of lo + w.
+// The least distance the frontier of a count slot holds (.pad[1]): every write that lowers
+// a vertex into the band is folded in (a relaxation that marks, a pull's store, the selection
+// of a band's first frontier), so it bounds the frontier from below and a pull round can stop
+// a row at fmin + w >= its best instead of lo + w (round 5: the first band's big pull scanned
+// ~19M light edges instead of ~100M, +8%, profiles/r05/ab_fmin_r5h2.txt).
 __device__ __forceinline__ void v2_flush_fmin(int32_t m, V2Line* sl, u64* red) {
-    if (!PJ_V2_FMIN) return;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const int32_t y = __shfl_xor(m, off, 64);
@@ -470,7 +475,6 @@ __device__ __forceinline__ int32_t v2_slot_fmin(const V2Line* sl) {
 }
 // the frontier bound of a pull round over slot c: max(lo, fmin), or lo without one
 __device__ __forceinline__ int32_t v2_pull_lo(const V2Args& a, int c) {
-    if (!PJ_V2_FMIN) return a.lo;
     const int32_t f = v2_slot_fmin(a.ctl->cnt[c]);
     return (f > a.lo && f < a.hi) ? f : a.lo;
 }
@@ -516,28 +520,20 @@ __device__ __forceinline__ u32 v2_relax_g(const V2Args& a, const ESrc ed, const 
     for (int j = 0; j < N; ++j) {
         cd[j] = ok[j] ? dist_now(a.dist + t[j]) : 0;
     }
-    if (PJ_V2_STATS)
-        for (int j = 0; j < N; ++j)
-            if (ok[j]) atomicAdd(&a.ctl->dbg[1].v, 1ull);
     bool mk[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         const bool imp = ok[j] && (int32_t)nd[j] < cd[j];
-        if (imp) {
-            v2_dmin(a.dist + t[j], (int32_t)nd[j]);
-            if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[2].v, 1ull);
-        }
+        if (imp) v2_dmin(a.dist + t[j], (int32_t)nd[j]);
         mk[j] = LIGHT && imp && (int32_t)nd[j] < a.hi;
-        if (PJ_V2_FMIN && mk[j] && (int32_t)nd[j] < fm) fm = (int32_t)nd[j];
+        if (mk[j] && (int32_t)nd[j] < fm) fm = (int32_t)nd[j];
     }
     if (!LIGHT) return 0u;
     u32 newc = 0;
 #pragma unroll
     for (int j = 0; j < N; ++j)
         if (mk[j]) {
-            if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[4].v, 1ull);
             if (v2_mark(fout, t[j])) {
-                if (PJ_V2_STATS) atomicAdd(&a.ctl->dbg[3].v, 1ull);
                 ++newc;
                 fe += a.lsplit[t[j]];
             }
@@ -578,16 +574,6 @@ __device__ __forceinline__ u32 v2_relax(const V2Args& a, const ESrc ed, u64 k, i
 // tile's slot offsets and source distances staged in LDS). (Round 4: 256- or 128-edge chunk
 // descriptors, one wave each, measured 2-3% slower; a slot carrying the source's distance
 // instead of its id 1% slower; removed.)
-// heavy pull candidates filtered by the row's first heavy weight (V2Args::hw): k26w 447.1 /
-// 451.3 -> 452.3 / 455.3 GTEPS interleaved (r4c, profiles/r04/ab_r4c.txt)
-#ifndef PJ_V2_HWF
-#define PJ_V2_HWF 1
-#endif
-// light pull candidates filtered by the row's lightest weight (V2Args::w1): k26w 438.8 ->
-// 451.0 / 448.6 GTEPS interleaved (r4a, profiles/r04/ab_r4a.txt)
-#ifndef PJ_V2_LWF
-#define PJ_V2_LWF 1
-#endif
 __device__ __forceinline__ void v2_hub_append(const V2Args& a, int hs, bool hub, u32 v, int32_t du, u64 b, u64& e) {
     const int lane = lane_id();
     const u64 hm = __ballot(hub);
@@ -653,7 +639,7 @@ __device__ __forceinline__ u32 v2_dense_find(const u32* off, u32 ns, u32 e) {
 template <typename Off>
 __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __restrict__ row, u64* __restrict__ fin,
                                               u64* __restrict__ fout, int hs, u32& newc, u64& fe, u64& mh, u64& ml,
-                                              int32_t& fm, V2Dense<Off>& sh) {
+                                              int32_t& fm, V2Work& wk, V2Dense<Off>& sh) {
     const int tid = threadIdx.x;
     const u64 mask = (1ull << V2_EB) - 1ull;
     const ESrc ed = v2_light_src(a);
@@ -732,6 +718,7 @@ __device__ __forceinline__ void v2_dense_body(const V2Args& a, const Off* __rest
                 eo += (u32)(e[j] - b[j]);
             }
         const u32 ns = (u32)(tot >> V2_EB), te = (u32)(tot & mask);
+        wk.add(te, te);  // (block-uniform: flushed with div = waves)
         __syncthreads();
         for (u32 e0 = 0; e0 < te; e0 += DB * V2_DNJ) {
             u64 idx[V2_DNJ];
@@ -789,7 +776,7 @@ __device__ __forceinline__ u64 v2_first_w_ge(const V2Args& a, u64 b, u64 e, long
 template <typename Off>
 __global__ __launch_bounds__(DB) void v2_heavy_push_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fin,
                                                       int hs) {
-    __shared__ u64 red[DB / WAVE];
+    __shared__ u64 red[2 * DB / WAVE];
     v2_expand_body<Off, false>(a, row, fin, nullptr, 0, hs, red);
 }
 
@@ -801,6 +788,8 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
     u32 newc = 0;
     u64 mh = 0, ml = 0, fe = 0;
     int32_t fm = INT_INF;
+    V2Work wk;
+    const ESrc esrc = LIGHT ? v2_light_src(a) : v2_cw_src(a);
     const i64 nsc = (a.nwords + V2_SC - 1) / V2_SC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
         const i64 wbase = sc * V2_SC;
@@ -867,7 +856,6 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
                 const u32 bit = select_bit(tw, c - ex);
                 v = (u32)((wbase + jw) * 64 + bit);
                 du = a.dist[v];
-                if (PJ_V2_STATS && LIGHT) atomicAdd(&a.ctl->dbg[0].v, 1ull);
                 if (LIGHT) {  // light CSR (tail mode: the light prefix in cw)
                     b = a.ltail ? (u64)row[v] : a.lrow[v];
                     e = a.ltail ? b + a.lsplit[v] : a.lrow[v + 1];
@@ -883,13 +871,17 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
             }
             // long segment -> hub queue (wave-aggregated append; all lanes here)
             v2_hub_append(a, hs, e - b > V2_HT, v, du, b, e);
+            {  // the wave relaxes the rest of every segment: one record and one probe per edge
+                const u32 se = wave_sum((u32)(e - b));
+                wk.add(se, se);
+            }
             // lane-serial part
             u64 k = b;
             const u64 lim = (e - b > (u64)V2_LS) ? b + V2_LS : e;
             bool go = k < lim;
             while (__ballot(go)) {
                 if (go) {
-                    newc += v2_relax_n<LIGHT>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), k, lim, du, fout, fe, fm);
+                    newc += v2_relax_n<LIGHT>(a, esrc, k, lim, du, fout, fe, fm);
                     k = k + PU < lim ? k + PU : lim;
                     go = k < lim;
                 }
@@ -910,9 +902,7 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
                         if (__shfl(inc, l + step - 1, 64) <= gi) l += step;
                     const u64 kl = __shfl(k, l, 64), xl = __shfl(exc, l, 64);
                     const int32_t dl = __shfl(du, l, 64);
-                    if (gi < tot)
-                        newc += v2_relax<LIGHT>(a, LIGHT ? v2_light_src(a) : v2_cw_src(a), kl + (gi - xl), dl, fout, fe,
-                                                fm);
+                    if (gi < tot) newc += v2_relax<LIGHT>(a, esrc, kl + (gi - xl), dl, fout, fe, fm);
                 }
             }
         }
@@ -922,6 +912,7 @@ __device__ __forceinline__ void v2_expand_body(const V2Args& a, const Off* __res
         v2_flush_fmin(fm, a.ctl->cnt[(cin + 1) & 3], red);
         v2_flush2(mh, ml, a.ctl->mh, red);
     }
+    v2_flush_work(a, LIGHT ? V2W_ROUND : V2W_HPUSH, wk, esrc_bytes(esrc), 4u, red);
 }
 
 // Edge-balanced relaxation of hub queue hs (slots' edge offsets are monotonic:
@@ -933,12 +924,14 @@ struct V2HubLds {
 };
 template <bool LIGHT>
 __device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ fout, int hs, u64 packed, u32& newc,
-                                            u64& fe, int32_t& fm, V2HubLds& L) {
+                                            u64& fe, int32_t& fm, V2Work& wk, V2HubLds& L) {
     const u64 nq = packed >> V2_EB, total = packed & ((1ull << V2_EB) - 1ull);
     const u32* hv = a.hv + (u64)hs * a.hcap;
     const u64* hb = a.hbeg + (u64)hs * a.hcap;
     const u64* ho = a.hoff + (u64)hs * a.hcap;
     for (u64 e0 = (u64)blockIdx.x * V2_HTILE; e0 < total; e0 += (u64)gridDim.x * V2_HTILE) {
+        const u32 te = (u32)min((u64)V2_HTILE, total - e0);
+        wk.add(te, te);  // (block-uniform: flushed with div = waves)
         u64 s0;
         u32 ns;
         lb_tile_load<V2_HTILE>(ho, nq, e0, L.sh, s0, ns);
@@ -969,18 +962,21 @@ __device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ f
 template <bool LIGHT>
 __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout, int cin, int hs, int hz) {
     __shared__ V2HubLds L;
-    __shared__ u64 red[DB / WAVE];
+    __shared__ u64 red[2 * DB / WAVE];
     const u64 packed = a.ctl->hub[hs].v;
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->hub[hz].v = 0;
     if ((packed >> V2_EB) == 0) return;
     u32 newc = 0;
     u64 fe = 0;
     int32_t fm = INT_INF;
-    v2_hub_body<LIGHT>(a, fout, hs, packed, newc, fe, fm, L);
+    V2Work wk;
+    v2_hub_body<LIGHT>(a, fout, hs, packed, newc, fe, fm, wk, L);
     if (LIGHT) {
         v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
         v2_flush_fmin(fm, a.ctl->cnt[(cin + 1) & 3], red);
     }
+    v2_flush_work(a, LIGHT ? V2W_HUB : V2W_HPUSH, wk, esrc_bytes(LIGHT ? v2_light_src(a) : v2_cw_src(a)), 4u, red,
+                  DB / WAVE);
 }
 
 // Next band [lo, hi): fout words = members, count into slot cout, min dist >= lo.
@@ -1023,20 +1019,18 @@ __global__ __launch_bounds__(DB) void v2_select_k(V2Args a, const Off* __restric
             if (mem) {
                 const u32 ls = (a.fesplit ? a.fesplit : a.lsplit)[v];
                 fe += ls;
-                if (PJ_V2_SELMB) {
-                    mh += (u64)row[v + 1] - (u64)row[v] - ls;
-                    ml += ls;
-                }
+                mh += (u64)row[v + 1] - (u64)row[v] - ls;
+                ml += ls;
             }
             if (lane == 0) {
                 fout[wi] = m;
-                if (PJ_V2_SELMB) a.mb[wi] = m;  // (mb is clear here: the heavy step consumed it)
+                a.mb[wi] = m;  // (mb is clear here: the heavy step consumed it)
             }
             c += lane == 0 ? (u32)__popcll(m) : 0u;
         }
     }
     v2_flush2(c, fe, a.ctl->cnt[cout], red);
-    if (PJ_V2_SELMB) v2_flush2(mh, ml, a.ctl->mh, red);
+    v2_flush2(mh, ml, a.ctl->mh, red);
     v2_flush_fmin(mn, a.ctl->cnt[cout], red);  // (min over dist >= lo: below every member)
     v2_flush_min(mn, a.ctl, red);
 }
@@ -1072,20 +1066,19 @@ __global__ __launch_bounds__(256) void v2_hmap_k(const int32_t* __restrict__ dis
 // tests of other lanes do not change. The wave owns its
 // PSC words: it writes the next band's member words of fout whole (and so clears
 // them), counts them into slot cout and folds min{new dist >= hi} into minv.
-constexpr bool V2_SELMB_PULL = PJ_V2_SELMB && PJ_V2_NOFIN >= 2;  // (the pull probes mb when NOFIN < 2)
 template <typename Off>
 __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __restrict__ row, u64* __restrict__ fout,
                                                 int32_t nhi, int cout) {
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
-    __shared__ u64 red[NWV];
+    __shared__ u64 red[2 * NWV];
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    const u64* hmb = PJ_V2_NOFIN >= 2 ? nullptr : a.mb;
     u32* newb = s_new[wave_id()];
     u32 ccount = 0;
-    u64 fe = 0, mh = 0, ml = 0;  // (the next band's members' degrees: PJ_V2_SELMB)
+    u64 fe = 0, mh = 0, ml = 0;  // (the next band's members' degrees)
     int32_t mn = INT_INF;
+    V2Work wk;
     const i64 ngroups = a.nwords;
     const i64 nsc = (ngroups + PSC - 1) / PSC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
@@ -1098,9 +1091,9 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
             const bool up = v < a.n && d >= hi;
             // heavy-head filter: no band member can lower d below lo + (the row's lightest
             // heavy weight); such vertices (and those without heavy edges) are not scanned,
-            // but still join the next band / its minimum
-            // (without the filter every vertex >= hi is a candidate: the skipped ones are
-            // accounted below only when a.hw is set)
+            // but still join the next band / its minimum (round 4: +0.5%, profiles/r04/ab_r4c.txt)
+            // (the form with a.hw tested, although it is never null, compiles to 68 VGPRs where
+            // the unconditional one takes 84)
             const int h = (a.hw && up) ? (int)a.hw[v] : 1;
             const bool cand = up && (!a.hw || (h != 0 && (long long)lo + h < (long long)d));
             const u64 m = __ballot(cand);
@@ -1112,10 +1105,8 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
                 if (sk && d < nhi) {
                     const u32 ls = (a.fesplit ? a.fesplit : a.lsplit)[v];
                     fe += ls;
-                    if (PJ_V2_SELMB) {
-                        mh += (u64)row[v + 1] - (u64)row[v] - ls;
-                        ml += ls;
-                    }
+                    mh += (u64)row[v + 1] - (u64)row[v] - ls;
+                    ml += ls;
                 }
             }
             if (lane == k) {
@@ -1154,15 +1145,12 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
             }  // (edges in a.cw)
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
             bool go = act && k < lim, done = !act || k >= e;
-#if PJ_V2_PSTATS
-            const Off k0 = k;
-#endif
+            const Off kst = k;
             while (__ballot(go)) {
                 if (go) {
-                    // band members are exactly mb's bits: probe the (cache-resident)
-                    // bitmap first, read dist only for members
+                    // the band's byte map (cache-resident), else dist itself
                     if (a.hmap ? pull_step_map<Off>(v2_cw_src(a), a.hmap, k, lim, lo, cur)
-                               : pull_step_fin_cw<Off>(v2_cw_src(a), a.dist, hmb, k, lim, lo, hi, cur)) {
+                               : pull_step_dist<Off>(v2_cw_src(a), a.dist, k, lim, lo, hi, cur)) {
                         done = true;
                         go = false;
                     } else {
@@ -1171,22 +1159,10 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
                     }
                 }
             }
-#if PJ_V2_PSTATS  // (heavy-pull scan lengths: candidates, stopped within 2 / 4 / 8 / the serial part)
-            {
-                const u64 sc = (u64)(k - k0);
-                const u64 c0 = wave_sum((u64)act), c1 = wave_sum((u64)(act && done && sc <= 2)),
-                          c2 = wave_sum((u64)(act && done && sc <= 4)), c3 = wave_sum((u64)(act && done && sc <= 8)),
-                          c4 = wave_sum((u64)(act && done)), c5 = wave_sum(act ? (u64)(e - k0) : 0ull);
-                if (lane == 0) {
-                    atomicAdd(&a.ctl->dbg[2].v, c0);
-                    atomicAdd(&a.ctl->dbg[3].v, c1);
-                    atomicAdd(&a.ctl->dbg[4].v, c2);
-                    atomicAdd(&a.ctl->dbg[5].v, c3);
-                    atomicAdd(&a.ctl->dbg[6].v, c4);
-                    atomicAdd(&a.ctl->dbg[7].v, c5);
-                }
+            {  // a lane probed k - kst records; one more was read when its weight stopped the row
+                const u32 p = (u32)(k - kst);
+                wk.add(wave_sum(p + (u32)(act && done && k < e)), wave_sum(p));
             }
-#endif
             u64 open = __ballot(!done);
             while (open) {
                 const int l = __ffsll((long long)open) - 1;
@@ -1199,6 +1175,7 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
                     const u64 x = valid ? eat(v2_cw_src(a), (u64)k0) : 0ull;
                     const u32 w = (u32)(x >> 32);
                     const bool stop = !valid || (long long)lo + w >= (long long)cl;
+                    wk.add((u32)__popcll(__ballot(valid)), (u32)__popcll(__ballot(!stop)));
                     int32_t cand = INT_INF;
                     if (!stop) {
                         int32_t du;
@@ -1206,7 +1183,7 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
                             const u32 m = a.hmap[(u32)x];
                             du = m != 0xFFu ? lo + (int32_t)m : INT_INF;
                         } else {
-                            du = pull_src(hmb, a.dist, (u32)x, hi);
+                            du = pull_src(a.dist, (u32)x, hi);
                         }
                         if (du < INT_INF) {
                             const long long nd = (long long)du + w;
@@ -1231,24 +1208,23 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
                     atomicOr(&newb[2 * wl + ((v >> 5) & 1)], 1u << (v & 31));
                     const u32 ls = (a.fesplit ? a.fesplit : a.lsplit)[v];
                     fe += ls;
-                    if (PJ_V2_SELMB) {
-                        mh += (u64)row[v + 1] - (u64)row[v] - ls;
-                        ml += ls;
-                    }
+                    mh += (u64)row[v + 1] - (u64)row[v] - ls;
+                    ml += ls;
                 }
             }
         }
         if (lane < PSC && gbase + lane < a.nwords) {
             const u64 word = (u64)newb[2 * lane] | ((u64)newb[2 * lane + 1] << 32);
             fout[gbase + lane] = word;
-            if (V2_SELMB_PULL) a.mb[gbase + lane] = word;  // (no wave reads mb here: NOFIN 2)
+            a.mb[gbase + lane] = word;  // (no wave reads mb here: the probes read the map or dist)
             ccount += (u32)__popcll(word);
         }
     }
     v2_flush2(ccount, fe, a.ctl->cnt[cout], red);
-    if (V2_SELMB_PULL) v2_flush2(mh, ml, a.ctl->mh, red);
+    v2_flush2(mh, ml, a.ctl->mh, red);
     v2_flush_fmin(mn, a.ctl->cnt[cout], red);  // (min over every dist >= hi: below the next band's members)
     v2_flush_min(mn, a.ctl, red);
+    v2_flush_work(a, V2W_HPULL, wk, esrc_bytes(v2_cw_src(a)), a.hmap ? 1u : 4u, red);
 }
 
 // Pull form of a light round (symmetric graphs): every vertex that can still
@@ -1262,11 +1238,11 @@ __global__ __launch_bounds__(DB) V2_WPE_H void v2_pull_k(V2Args a, const Off* __
 template <typename Off>
 __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* __restrict__ row,
                                                    const u64* __restrict__ fin, u64* __restrict__ fout, u32* newb,
-                                                   int32_t flo, u32& newc, u64& fe, u64& mh, u64& ml, int32_t& fm) {
+                                                   int32_t flo, u32& newc, u64& fe, u64& mh, u64& ml, int32_t& fm,
+                                                   V2Work& wk) {
     constexpr int NWV = DB / WAVE;
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;  // flo: the frontier's least distance (v2_pull_lo), >= lo
-    const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
     const i64 nsc = (a.nwords + PSC - 1) / PSC;
     for (i64 sc = (i64)blockIdx.x * NWV + wave_id(); sc < nsc; sc += (i64)gridDim.x * NWV) {
         const i64 gbase = sc * PSC;
@@ -1282,9 +1258,9 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                 if (nmw) a.mb[gbase + lane] = old | f;
             }
         }
-#if PJ_V2_MBC
         // (compacted: 64 new members per wave step, a lane each; one lane walking the bits of
-        // its word serialized a frontier of millions of new members in 16 lanes of the wave)
+        // its word serialized a frontier of millions of new members in 16 lanes of the wave:
+        // +0.6%, profiles/r05/mbc_r5h10.txt)
         {
             const u32 mc = (u32)__popcll(nmw);
             const u32 mincl = wave_incl_scan(mc);
@@ -1308,23 +1284,14 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                 }
             }
         }
-#else
-        while (nmw) {
-            const int b = __ffsll((long long)nmw) - 1;
-            nmw &= nmw - 1;
-            const i64 v = (gbase + lane) * 64 + b;
-            const u64 rb = (u64)row[v], ls = a.lsplit[v];
-            mh += (u64)row[v + 1] - rb - ls;
-            ml += ls;
-        }
-#endif
         u64 mytodo = 0;
 #pragma unroll
         for (int k = 0; k < PSC; ++k) {
             const i64 v = (gbase + k) * 64 + lane;
             const int32_t d = v < a.n ? a.dist[v] : 0;
-            // (w1 filter: a frontier in-neighbour offers at least lo + the row's lightest weight)
-            const int w1 = (a.w1 && v < a.n && d > lo) ? (int)a.w1[v] : 0;
+            // (w1 filter: a frontier in-neighbour offers at least lo + the row's lightest weight;
+            // round 4: +2.5%, profiles/r04/ab_r4a.txt)
+            const int w1 = (v < a.n && d > lo) ? (int)a.w1[v] : 0;
             const u64 m = __ballot(v < a.n && d > lo && (long long)flo + w1 < (long long)d);
             if (lane == k) mytodo = m;
         }
@@ -1335,7 +1302,6 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
         const u32 incl = wave_incl_scan(cnt);
         const u32 myex = incl - cnt;
         const u32 T = __shfl(incl, 63, 64);
-        if (PJ_V2_STATS && lane == 0 && T) atomicAdd(&a.ctl->dbg[5].v, (u64)T);  // (pull candidates)
         // candidate c of the wave's list: its vertex, dist and light-row bounds
         auto fetch = [&](u32 c, bool& act, i64& v, int32_t& d0, Off& k, u32& ls) {
             act = c < T;
@@ -1376,21 +1342,26 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             if (act) e = (a.ltail || ls <= V2_PLMAX) ? k + (Off)ls : k;  // long rows: v2_pull_long_body
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
             bool go = act && k < lim, done = !act || k >= e;
-            const Off kst = k;  // (PJ_V2_STATS: edges scanned)
             while (__ballot(go)) {
+                // (counted with ballots in the wave-uniform loop: a start-of-row register held
+                // over the loop spilled in this 72-VGPR kernel) records the step reads; each
+                // row the step stops probes one fewer (PU - 1 fewer at most, when its first
+                // record stops it)
+                u32 r = 0;
+#pragma unroll
+                for (int j = 0; j < PU; ++j) r += (u32)__popcll(__ballot(go && k + (Off)j < lim));
+                bool stp = false;
                 if (go) {
-                    if (pull_step_fin_cw<Off>(v2_light_src(a), a.dist, lfin, k, lim, flo, hi, cur)) {
+                    if (pull_step_dist<Off>(v2_light_src(a), a.dist, k, lim, flo, hi, cur)) {
                         done = true;
                         go = false;
+                        stp = true;
                     } else {
                         go = k < lim;
                         done = k >= e;
                     }
                 }
-            }
-            if (PJ_V2_STATS) {
-                const u64 sc = wave_sum(act ? (u64)(k - kst) : 0ull);
-                if (lane == 0 && sc) atomicAdd(&a.ctl->dbg[6].v, sc);
+                wk.add(r, r - (u32)__popcll(__ballot(stp)));
             }
             u64 open = __ballot(!done);
             while (open) {
@@ -1399,15 +1370,15 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
                 const Off kb = __shfl(k, l, 64), ke = __shfl(e, l, 64);
                 int32_t cl = __shfl(cur, l, 64);
                 for (Off kk = kb; kk < ke; kk += WAVE) {
-                    if (PJ_V2_STATS && lane == 0) atomicAdd(&a.ctl->dbg[6].v, (u64)min((Off)WAVE, ke - kk));
                     const Off k0 = kk + lane;
                     const bool valid = k0 < ke;
                     const u64 x = valid ? eat(v2_light_src(a), (u64)k0) : 0ull;
                     const u32 w = (u32)(x >> 32);
                     const bool stop = !valid || (long long)flo + w >= (long long)cl;
+                    wk.add((u32)__popcll(__ballot(valid)), (u32)__popcll(__ballot(!stop)));
                     int32_t cand = INT_INF;
                     if (!stop) {
-                        const int32_t du = pull_src(lfin, a.dist, (u32)x, hi);
+                        const int32_t du = pull_src(a.dist, (u32)x, hi);
                         if (du < INT_INF) {
                             const long long nd = (long long)du + w;
                             cand = nd < INT_INF ? (int32_t)nd : INT_INF;
@@ -1453,10 +1424,9 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
 // atomicMin (the vertex's chunks run in different waves).
 __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __restrict__ fin, u64* __restrict__ fout,
                                                   const u32* __restrict__ lcv, const u32* __restrict__ lcc, u64 nlc,
-                                                  int32_t flo, u32& newc, u64& fe, int32_t& fm) {
+                                                  int32_t flo, u32& newc, u64& fe, int32_t& fm, V2Work& wk) {
     const int lane = lane_id();
     const int32_t lo = a.lo, hi = a.hi;
-    const u64* lfin = PJ_V2_NOFIN ? nullptr : fin;
     for (u64 it = (u64)blockIdx.x * (DB / WAVE) + wave_id(); it < nlc; it += (u64)gridDim.x * (DB / WAVE)) {
         const u32 v = lcv[it];
         const int32_t d0 = dist_now(a.dist + v);
@@ -1465,18 +1435,19 @@ __device__ __forceinline__ void v2_pull_long_body(const V2Args& a, const u64* __
         const u32 ls = (u32)(a.lrow[v + 1] - rb);
         const u64 kb = rb + (u64)lcc[it] * V2_PCH;
         const u64 ke = min(rb + ls, kb + V2_PCH);
+        wk.add(1u, 0u);  // (the chunk's first record, read by every lane for the skip test)
         if ((long long)flo + (eat(v2_light_src(a), kb) >> 32) >= (long long)d0) continue;
         int32_t cur = d0;
         for (u64 kk = kb; kk < ke; kk += WAVE) {
-            if (PJ_V2_STATS && lane == 0) atomicAdd(&a.ctl->dbg[7].v, min((u64)WAVE, ke - kk));
             const u64 k0 = kk + lane;
             const bool valid = k0 < ke;
             const u64 x = valid ? eat(v2_light_src(a), k0) : 0ull;
             const u32 w = (u32)(x >> 32);
             const bool stop = !valid || (long long)flo + w >= (long long)cur;
+            wk.add((u32)__popcll(__ballot(valid)), (u32)__popcll(__ballot(!stop)));
             int32_t cand = INT_INF;
             if (!stop) {
-                const int32_t du = pull_src(lfin, a.dist, (u32)x, hi);
+                const int32_t du = pull_src(a.dist, (u32)x, hi);
                 if (du < INT_INF) {
                     const long long nd = (long long)du + w;
                     cand = nd < INT_INF ? (int32_t)nd : INT_INF;
@@ -1520,7 +1491,7 @@ __global__ __launch_bounds__(DB) V2_WPE_R void v2_pull_round_k(V2Args a, const O
                                                       int hs, u64 dense_min, u64* __restrict__ fclr) {
     constexpr int NWV = DB / WAVE;
     __shared__ u32 s_new[NWV][2 * PSC];
-    __shared__ u64 red[NWV];
+    __shared__ u64 red[2 * NWV];
     __shared__ V2RoundLds<Off> lds;
     v2_zero_slot(a, (cin + 2) & 3);
     v2_clear_words(fclr, a.nwords);
@@ -1543,21 +1514,25 @@ __global__ __launch_bounds__(DB) V2_WPE_R void v2_pull_round_k(V2Args a, const O
         u32 newc = 0;
         u64 mh = 0, ml = 0, fe = 0;
         int32_t fm = INT_INF;
-        v2_dense_body<Off>(a, row, fin, fout, hs, newc, fe, mh, ml, fm, lds.push);
+        V2Work wk;
+        v2_dense_body<Off>(a, row, fin, fout, hs, newc, fe, mh, ml, fm, wk, lds.push);
         v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
         v2_flush_fmin(fm, a.ctl->cnt[(cin + 1) & 3], red);
         v2_flush2(mh, ml, a.ctl->mh, red);
+        v2_flush_work(a, V2W_ROUND, wk, esrc_bytes(v2_light_src(a)), 4u, red, NWV);
         return;
     }
     u32 newc = 0;
     u64 fe = 0, mh = 0, ml = 0;
     int32_t fm = INT_INF;
+    V2Work wk;
     const int32_t flo = v2_pull_lo(a, cin);
-    if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, flo, newc, fe, fm);
-    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], flo, newc, fe, mh, ml, fm);
+    if (nlc && !a.ltail) v2_pull_long_body(a, fin, fout, lcv, lcc, nlc, flo, newc, fe, fm, wk);
+    v2_pull_light_body<Off>(a, row, fin, fout, s_new[wave_id()], flo, newc, fe, mh, ml, fm, wk);
     v2_flush2(newc, fe, a.ctl->cnt[(cin + 1) & 3], red);
     v2_flush_fmin(fm, a.ctl->cnt[(cin + 1) & 3], red);
     v2_flush2(mh, ml, a.ctl->mh, red);
+    v2_flush_work(a, V2W_ROUND, wk, esrc_bytes(v2_light_src(a)), 4u, red);
 }
 
 // static chunk list of the long light rows: count, then append (order is irrelevant)
@@ -1709,7 +1684,7 @@ struct DeltaSolve {
     DevBuf<int32_t> out_own;
     DevBuf<u64> f[3], mb;      // light-round frontier ring (v2_clear_words), band members
     DevBuf<u64> sb;            // settled-before-the-tail bitmap
-    DevBuf<uint8_t> hmap;      // the heavy pull's probe map (PJ_V2_HMAP)
+    DevBuf<uint8_t> hmap;      // the heavy pull's probe map (v2_hmap_k)
     DevBuf<u64> db;            // members whose far heavy edges are deferred (defer_heavy); all zero
     bool db_dirty = true;      // unless a solve stopped with a deferral pending (an error)
     DevBuf<V2Ctl> ctl;
@@ -1752,8 +1727,8 @@ struct DeltaWork {
     u32 lcb = 0;
     int packed_for = -1;   // g.light_pack the light CSR was built for
     DevBuf<u64> hl;        // has-light-edges bitmap (per delta)
-    DevBuf<uint8_t> hw, hw2;  // (PJ_V2_HWF) first heavy weight per vertex for delta / the tail threshold
-    DevBuf<uint8_t> w1;       // (PJ_V2_LWF) lightest weight per vertex (any threshold)
+    DevBuf<uint8_t> hw, hw2;  // first heavy weight per vertex for delta / the tail threshold (v2_hw_k)
+    DevBuf<uint8_t> w1;       // lightest weight per vertex (any threshold, v2_w1_k)
     DeltaSolve main;
     std::vector<std::unique_ptr<DeltaSolve>> extra;  // concurrent batch solves
 };
@@ -1850,8 +1825,8 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
         PJ_LAUNCH_CHECK();
         PJ_HIP(hipMemcpyAsync(&w.nlc, acc.p, sizeof(u64), hipMemcpyDeviceToHost, s));
         PJ_HIP(hipStreamSynchronize(s));
-        if (PJ_V2_HWF) launch_hw<Off>(R, row, w.lsplit.p, n, w.hw, maxgrid, s);
-        if (PJ_V2_LWF && !w.w1.p) {
+        launch_hw<Off>(R, row, w.lsplit.p, n, w.hw, maxgrid, s);
+        if (!w.w1.p) {
             w.w1.alloc((size_t)std::max<i64>(n, 1));
             if (R.w8.p) v2_w1_k<Off, uint8_t><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w8.p, n, w.w1.p);
             else v2_w1_k<Off, u32><<<grid_for(n, 256, maxgrid), 256, 0, s>>>(row, R.w.p, n, w.w1.p);
@@ -1900,7 +1875,7 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
     if (tdelta > delta && w.lsplit2_delta != (u32)tdelta && n > 0) {
         w.lsplit2.ensure((size_t)n);
         launch_light_split<Off>(R, row, n, (u32)tdelta, w.lsplit2.p, maxgrid, s);
-        if (PJ_V2_HWF) launch_hw<Off>(R, row, w.lsplit2.p, n, w.hw2, maxgrid, s);
+        launch_hw<Off>(R, row, w.lsplit2.p, n, w.hw2, maxgrid, s);
         w.lsplit2_delta = (u32)tdelta;
         PJ_HIP(hipStreamSynchronize(s));
     }
@@ -1962,7 +1937,7 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     v.mb.alloc(nw);
     v.sb.alloc(nw);
     v.db.alloc(nw);
-    if (PJ_V2_HMAP) v.hmap.alloc((size_t)(n ? n : 1) + 16);
+    v.hmap.alloc((size_t)(n ? n : 1) + 16);
     v.ctl.alloc(1);
     v.hcap = (u64)std::max<i64>(1, std::min<i64>(n, g.nnz / (i64)V2_HT + 1));
     v.hv.alloc(3 * v.hcap);  // the hub queue's ring of three slots
@@ -1978,11 +1953,13 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     if (!v.ev1) PJ_HIP(hipEventCreate(&v.ev1));
 }
 
-// One single-source solve on v's stream into v.out (input ids); the preparation of
-// delta (prepare_delta) has run. Reads only the shared graph and DeltaWork arrays, so
-// solves of different DeltaSolve slots may run concurrently from different host threads.
+// One single-source solve on v's stream into v.dist (relabeled ids), and with unlabel set
+// into v.out (input ids) as well; the preparation of delta (prepare_delta) has run. Reads
+// only the shared graph and DeltaWork arrays, so solves of different DeltaSolve slots may
+// run concurrently from different host threads. Returns the source's relabeled id (>= n_scan:
+// a source without edges, -1: out of range).
 template <typename Off>
-void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source) {
+i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source, bool unlabel) {
     Ctx& ctx = *g.ctx;
     hipStream_t s = v.s;
     Relabeled& R = *g.rl;
@@ -1993,7 +1970,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     // error here, not a device fault)
     if (n > 0 && (!row || !v.dist || !v.out || !v.f[0].p || !v.f[1].p || !v.f[2].p || !v.mb.p || !v.sb.p ||
                   !v.ctl.p || !v.hv.p || !v.hbeg.p || !v.hoff.p || v.hv.n < 3 * v.hcap || !w.lsplit.p ||
-                  !w.lrow.p || (!w.lcw.p && !w.lcw32.p) || (PJ_V2_LWF && !w.w1.p) || (PJ_V2_HWF && !w.hw.p)))
+                  !w.lrow.p || (!w.lcw.p && !w.lcw32.p) || !w.w1.p || !w.hw.p || !v.hmap.p))
         throw Error(PJ_ERR_HIP, "delta-stepping: a solver buffer is missing (internal error)");
     const unsigned maxgrid = (unsigned)ctx.cu_count * (unsigned)PJ_V2_GPC;  // workgroups per CU of the v2 kernels (grid-stride)
     const unsigned pullgrid = (unsigned)ctx.cu_count * (unsigned)PJ_V2_GPC_PULL;
@@ -2019,8 +1996,8 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     a.col = R.col.p;
     a.w8 = g.split_w ? R.w8.p : nullptr;
     a.hl = g.light_filter ? w.hl.p : nullptr;
-    a.hw = PJ_V2_HWF ? w.hw.p : nullptr;
-    a.w1 = PJ_V2_LWF ? w.w1.p : nullptr;
+    a.hw = w.hw.p;
+    a.w1 = w.w1.p;
     // light rounds whose frontier holds more than dense_frac x n vertices run tile-dense
     const u64 dense_min = g.dense_frac > 0.0 ? (u64)(g.dense_frac * (double)n) : ~0ull;
     a.mb = v.mb.p;
@@ -2038,10 +2015,12 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     a.hz = INT_INF;
     a.dsave = nullptr;
     a.hmap = nullptr;
-    // the heavy pull's probe map over [mlo, mhi) when its values fit a byte (else dist is probed)
+    // the heavy pull's probe map over [mlo, mhi) when its values fit a byte (else dist is
+    // probed): v2_pull_k 853 -> 789 us per k26w solve for 34 us of map building (round 5,
+    // profiles/r05/hmap_r5h23.txt)
     auto set_hmap = [&](int32_t mlo, int32_t mhi) {
         a.hmap = nullptr;
-        if (!PJ_V2_HMAP || n == 0 || (long long)mhi - (long long)mlo > 255) return;
+        if (n == 0 || (long long)mhi - (long long)mlo > 255) return;
         v2_hmap_k<<<grid_for((n + 3) / 4, 256, maxgrid), 256, 0, s>>>(v.dist, n, mlo, mhi, v.hmap.p);
         PJ_LAUNCH_CHECK();
         a.hmap = v.hmap.p;
@@ -2107,7 +2086,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
         // check whether that band had any vertex (its start slot survives the first two
         // rounds of the counter ring) and, if not, the next occupied band (minv of the
         // heavy step, copied by the same publish before it resets minv).
-        const bool defer_ok = g.defer_check && !PJ_V2_STATS && g.round_batch <= 2;
+        const bool defer_ok = g.defer_check && g.round_batch <= 2;
         bool deferred = false;
         bool finished = false;
         // Deferred far heavy edges (defer_heavy): a heavy push of a band whose members hold
@@ -2115,7 +2094,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
         // and their other heavy edges go with the next heavy step -- a pull that takes its stop
         // rule from their band (lo_def), or a push of db's whole heavy rows first. Before an
         // empty band's jump or the end, db is pushed whole (flush_def).
-        u64 mh_carry = 0, ml_carry = 0;  // (PJ_V2_SELMB: the next band's members' degrees, published early)
+        u64 mh_carry = 0, ml_carry = 0;  // (the next band's members' degrees, counted by its selection and published early)
         bool dpend = false;
         long long lo_def = 0;
         u64 mh_def = 0;
@@ -2171,7 +2150,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             // light rounds until the band's frontier is empty, launched round_batch per
             // host check, doubling (starting each band at the previous band's round count,
             // or at 4 or 8, measured slower: idle rounds cost more than the checks they save)
-            int K = PJ_V2_STATS ? 1 : g.round_batch;
+            int K = g.round_batch;
             for (;;) {
                 const u64 pull_thresh = can_pull_light ? (u64)((double)light_left / light_pull) : ~0ull;
                 for (int q = 0; q < K; ++q) {
@@ -2220,16 +2199,8 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                     mh += v.hctl->mh[i].v;
                     ml += v.hctl->mh[i].pad[0];
                 }
-                if (PJ_V2_STATS) {
-                    fprintf(stderr, "band %d lo %lld rounds %d: frontier %llu edges %llu atomicmin %llu atomicor %llu marks %llu next %llu"
-                            " | pull candidates %llu short-row edges %llu long-chunk edges %llu\n",
-                            (int)st.levels, lo, K, v.hctl->dbg[0].v, v.hctl->dbg[1].v, v.hctl->dbg[2].v,
-                            v.hctl->dbg[4].v, v.hctl->dbg[3].v, slot(cs), v.hctl->dbg[5].v, v.hctl->dbg[6].v,
-                            v.hctl->dbg[7].v);
-                    PJ_HIP(hipMemsetAsync(v.ctl.p->dbg, 0, sizeof(v.ctl.p->dbg), s));
-                }
                 if (slot(cs) == 0) break;
-                K = PJ_V2_STATS ? 1 : std::min(2 * K, 16);
+                K = std::min(2 * K, 16);
             }
             if (finished) break;
             if (jumped) continue;  // (the select of the jumped-to band is enqueued)
@@ -2258,18 +2229,15 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             // (round 5: deferring heavy pulls the same way, the next heavy step pulling both
             // bands, measured 1.5% slower: profiles/r05/defer_heavy_r5h7.txt)
             const bool pull_now = can_pull && mh_all > 0 && (double)heavy_left < g.pull_factor * (double)mh_all;
-            if (PJ_V2_STATS)
-                fprintf(stderr, "heavy step lo %lld: members' heavy edges %llu, unsettled heavy edges %llu, %s\n", lo,
-                        (unsigned long long)mh, (unsigned long long)heavy_left, pull_now ? "pull" : mh ? "push" : "none");
             if (pull_now) {
-                // deferred members (dist >= lo_def) are probed like this band's (dist < hi)
+                // deferred members (dist >= lo_def) are probed like this band's (dist < hi): the
+                // map, when built, covers [lo_def, hi), and a dist probe takes every dist < hi
                 if (dpend) a.lo = (int32_t)lo_def;
                 set_hmap(a.lo, a.hi);
                 v2_pull_k<Off><<<heavygrid, DB, 0, s>>>(a, row, v.f[fi].p, nhi_t, cs);
                 a.hmap = nullptr;
                 PJ_LAUNCH_CHECK();
                 a.lo = (int32_t)lo;
-                if (!V2_SELMB_PULL) PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
                 if (dpend) PJ_HIP(hipMemsetAsync(v.db.p, 0, sizeof(u64) * (size_t)nwords, s));
                 if (dpend) v.db_dirty = false;
                 dpend = false;
@@ -2291,9 +2259,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                         lo_def = lo;
                         mh_def = mh;
                     }
-                } else if (!PJ_V2_SELMB) {  // (else the select overwrites every mb word)
-                    PJ_HIP(hipMemsetAsync(v.mb.p, 0, sizeof(u64) * (size_t)nwords, s));
-                }
+                }  // (the select below writes every mb word)
                 a.lo = hi;
                 a.hi = nhi_t;
                 v2_select_k<Off><<<maxgrid, DB, 0, s>>>(a, row, v.f[fi].p, cs);
@@ -2306,7 +2272,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                 a.fesplit = nullptr;
                 a.sbits = v.sb.p;
                 a.lsplit = w.lsplit2.p;
-                a.hw = PJ_V2_HWF ? w.hw2.p : nullptr;
+                a.hw = w.hw2.p;
                 a.ltail = 1;
                 bw = tdelta;
                 // light pulls in the tail (tail_pull): rows are scanned in weight order and
@@ -2319,8 +2285,8 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                     heavy_left = 0;  // every edge is light in the tail
                     light_left = tail_unsettled;
                 } else {
-                    PJ_HIP(hipMemsetAsync(&v.ctl.p->dbg[0], 0, sizeof(V2Line), s));
-                    v2_heavy_left_k<Off><<<maxgrid, DB, 0, s>>>(row, a.lsplit, v.dist, n, hi, &v.ctl.p->dbg[0].v);
+                    PJ_HIP(hipMemsetAsync(&v.ctl.p->aux, 0, sizeof(V2Line), s));
+                    v2_heavy_left_k<Off><<<maxgrid, DB, 0, s>>>(row, a.lsplit, v.dist, n, hi, &v.ctl.p->aux.v);
                     PJ_LAUNCH_CHECK();
                 }
             }
@@ -2331,7 +2297,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             }
             sync_ctl();
             if (enter_tail && (long long)tdelta <= w.maxw) {
-                heavy_left = v.hctl->dbg[0].v;
+                heavy_left = v.hctl->aux.v;
                 light_left = tail_unsettled > heavy_left ? tail_unsettled - heavy_left : 0;
             }
             if (slot(cs) == 0 && dpend) {  // the next band is empty; deferred edges land past it
@@ -2357,8 +2323,22 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
             lo = hi;
         }
         if (dpend) throw Error(PJ_ERR_HIP, "delta-stepping: deferred heavy edges left (internal error)");
+        // every exit of the band loop but the last band's end (lo reaching INT_INF) follows a
+        // publish of the counters after the solve's last relaxation kernel
+        if (lo >= INT_INF) sync_ctl();
+        for (int k = 0; k < V2W_N; ++k) {
+            for (int i = 0; i < V2_NSH; ++i) {
+                const V2Line& l = v.hctl->work[k][i];
+                st.work_by_kernel[k][0] += (int64_t)l.v;
+                st.work_by_kernel[k][1] += (int64_t)l.pad[0];
+                st.work_by_kernel[k][2] += (int64_t)l.pad[1];
+            }
+            st.scanned_edges += st.work_by_kernel[k][0];
+            st.probes += st.work_by_kernel[k][1];
+            st.work_bytes += st.work_by_kernel[k][2];
+        }
     }
-    if (g.n > 0) {
+    if (unlabel && g.n > 0) {
         unlabel_k<<<grid_for(g.n, 256, maxgrid), 256, 0, s>>>(R.inv.p, v.dist, g.n, n, v.out);
         PJ_LAUNCH_CHECK();
         if (valid && ls >= n) d_source_k<<<1, 1, 0, s>>>(source, v.out);  // a source without edges
@@ -2370,14 +2350,6 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
     st.kernel_ms = ms;
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
     v.st = st;
-    if (PJ_V2_PSTATS) {
-        V2Ctl h;
-        PJ_HIP(hipMemcpy(&h, v.ctl.p, sizeof(V2Ctl), hipMemcpyDeviceToHost));
-        fprintf(stderr, "heavy pulls: candidates %llu stopped within 2 %llu, 4 %llu, 8 %llu, serial %llu; "
-                "heavy edges of the candidates %llu\n", (unsigned long long)h.dbg[2].v, (unsigned long long)h.dbg[3].v,
-                (unsigned long long)h.dbg[4].v, (unsigned long long)h.dbg[5].v, (unsigned long long)h.dbg[6].v,
-                (unsigned long long)h.dbg[7].v);
-    }
     if (g.round_log) {  // debug: one stderr line per non-empty light round
         std::vector<u64> h(1 + 3 * 255);
         PJ_HIP(hipMemcpy(h.data(), rlog.p, sizeof(u64) * h.size(), hipMemcpyDeviceToHost));
@@ -2387,6 +2359,7 @@ void delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source
                     (unsigned long long)(h[3 + 3 * i] >> 40), kind[h[1 + 3 * i] % 4], (unsigned long long)h[2 + 3 * i],
                     (unsigned long long)(h[3 + 3 * i] & ((1ull << 40) - 1)));
     }
+    return valid ? ls : -1;
 }
 
 }  // namespace
@@ -2431,19 +2404,39 @@ int32_t delta_setup(Graph& g) {
     return delta;
 }
 
-void run_solve(Graph& g, DeltaSolve& v, int32_t delta, i64 source) {
-    if (g.off64) delta2_run<u64>(g, *g.delta_work, v, delta, source);
-    else delta2_run<u32>(g, *g.delta_work, v, delta, source);
+i64 run_solve(Graph& g, DeltaSolve& v, int32_t delta, i64 source, bool unlabel) {
+    if (g.off64) return delta2_run<u64>(g, *g.delta_work, v, delta, source, unlabel);
+    return delta2_run<u32>(g, *g.delta_work, v, delta, source, unlabel);
 }
 
 }  // namespace
 
+// The solve ends with the distances in the solver's degree-ordered ids (R.dist); the input-id
+// vector g.dist is materialized by its first consumer (delta_materialize: the D2H copy, the
+// sol_file writer, pj_dist_device, the tree and reach passes), one gather over inv[] of
+// 8 bytes per vertex (0.19 ms at s26) that the solve itself no longer carries.
 void delta_solve(Graph& g, i64 source) {
     const int32_t delta = delta_setup(g);
     DeltaSolve& v = g.delta_work->main;
-    run_solve(g, v, delta, source);
+    g.dist_pending = false;
+    const i64 ls = run_solve(g, v, delta, source, false);
     g.stats = v.st;
+    g.dist_pending = true;
+    g.pending_source = (ls >= g.rl->n_scan) ? source : -1;  // (a source without edges: 0 after the gather)
     g.have_result = true;
+}
+
+void delta_materialize(Graph& g) {
+    if (!g.dist_pending) return;
+    g.dist_pending = false;
+    if (g.n == 0) return;
+    hipStream_t s = g.ctx->stream;
+    unlabel_k<<<grid_for(g.n, 256, (unsigned)g.ctx->cu_count * (unsigned)PJ_V2_GPC), 256, 0, s>>>(
+        g.rl->inv.p, g.rl->dist.p, g.n, g.rl->n_scan, g.dist.p);
+    PJ_LAUNCH_CHECK();
+    if (g.pending_source >= 0) d_source_k<<<1, 1, 0, s>>>(g.pending_source, g.dist.p);
+    PJ_LAUNCH_CHECK();
+    PJ_HIP(hipStreamSynchronize(s));  // (readers may copy on other streams, e.g. small hipMemcpy)
 }
 
 // Johnson-style weighted batch: `slots` solves in flight at once, each on its own
@@ -2456,6 +2449,7 @@ void delta_solve(Graph& g, i64 source) {
 void delta_batch(Graph& g, const i64* sources, int n_src, int slots,
                  const std::function<void(int, const int32_t*, hipStream_t)>& on_row) {
     const int32_t delta = delta_setup(g);
+    g.dist_pending = false;  // (the main slot's rows overwrite R.dist and g.dist)
     DeltaWork& w = *g.delta_work;
     slots = std::max(1, std::min(slots, n_src));
     const i64 n_scan = g.rl->n_scan;
@@ -2497,13 +2491,18 @@ void delta_batch(Graph& g, const i64* sources, int n_src, int slots,
             PJ_HIP(hipSetDevice(g.ctx->device));
             DeltaSolve& v = *slot[(size_t)k];
             for (int i; (i = next.fetch_add(1)) < n_src;) {
-                run_solve(g, v, delta, sources[i]);
+                run_solve(g, v, delta, sources[i], true);  // (rows in input ids for on_row)
                 std::lock_guard<std::mutex> lk(mu);
                 sum.kernel_ms += v.st.kernel_ms;
                 sum.levels += v.st.levels;
                 sum.relax_rounds += v.st.relax_rounds;
                 sum.td_levels += v.st.td_levels;
                 sum.bu_levels += v.st.bu_levels;
+                sum.scanned_edges += v.st.scanned_edges;
+                sum.probes += v.st.probes;
+                sum.work_bytes += v.st.work_bytes;
+                for (int k = 0; k < V2W_N; ++k)
+                    for (int j = 0; j < 3; ++j) sum.work_by_kernel[k][j] += v.st.work_by_kernel[k][j];
                 on_row(i, v.out, v.s);
             }
         } catch (...) {

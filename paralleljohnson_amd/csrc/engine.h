@@ -28,6 +28,13 @@ struct Comm {
     int rank = 0, world = 1;
     virtual ~Comm() = default;
     virtual const char* kind() const = 0;
+    // the group's size and this rank's index as the transport itself reports them (RCCL:
+    // ncclCommCount / ncclCommUserRank of the communicator; the thread group's size; the
+    // callbacks' declared world), for a caller to check against the world it launched
+    virtual void transport_ranks(int* count, int* index) const {
+        *count = world;
+        *index = rank;
+    }
     // element-wise sum (or min) of k host values over the ranks (:589-590)
     virtual void allreduce(i64* v, int k, bool is_min, hipStream_t s) = 0;
     // recv[q] = what rank q sends to this rank (the counts MPI_Alltoall, :522-523)

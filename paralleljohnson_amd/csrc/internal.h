@@ -257,6 +257,10 @@ struct Graph {
     double ms_alpha = 16.0;  // batch BFS: push levels while the frontier's out-edges < nnz / ms_alpha
 
     bool have_result = false;
+    // weighted: the last solve's distances are still in the solver's ids (R.dist); the first
+    // consumer of g.dist gathers them into input ids (delta_materialize)
+    bool dist_pending = false;
+    i64 pending_source = -1;   // (a source without edges: its 0 is written after the gather)
     i64 last_source = -1;      // source of the single-source result in dist (parent tree)
     bool batch_stats = false;  // stats describe the last pj_sssp_batch
     pj_load_stats load{};      // how the graph was built (pj_graph_load_stats)
@@ -310,6 +314,9 @@ void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t see
 void bfs_solve(Graph& g, i64 source);
 i64 relabeled_id(const Relabeled& R, i64 v, hipStream_t s);  // relabel.hip: inv[v]
 void delta_solve(Graph& g, i64 source);
+// g.dist in input ids after a delta_solve (a no-op when it already is): every reader of g.dist
+// calls it first (enqueued on the ctx stream)
+void delta_materialize(Graph& g);
 // Weighted batch with `slots` concurrent solves (delta.hip); on_row(i, device row, stream)
 // is called once per source, serialised.
 void delta_batch(Graph& g, const i64* sources, int n_src, int slots,

@@ -128,6 +128,13 @@ class Comm:
         _check(_lib.pj_comm_info(self._h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(k)))
         self.rank, self.world, self.kind = r.value, w.value, k.value.decode()
 
+    def transport_ranks(self):
+        """(group size, this rank's index) as the transport itself reports them
+        (pj_comm_transport_ranks: ncclCommCount / ncclCommUserRank for RCCL)."""
+        c, i = _INT(), _INT()
+        _check(_lib.pj_comm_transport_ranks(self._h, ctypes.byref(c), ctypes.byref(i)))
+        return c.value, i.value
+
     @staticmethod
     def unique_id() -> bytes:
         """RCCL group id made by rank 0 and handed to every rank by the launcher."""
@@ -586,3 +593,45 @@ class Multi:
         _check(_lib.pj_multi_sssp_batch_write(self._h, _ptr(src), len(src), ctypes.cast(arr, ctypes.c_void_p),
                                               int(strict), ctypes.byref(ms)))
         return ms.value
+
+
+class TorchDistTransport:
+    """The callbacks of pj_comm_create_callbacks over torch.distributed on HOST buffers (e.g.
+    the gloo backend): libpj's protocol loops at world > 1 without a GPU (the CPU tests over
+    numpy steps). Its buffers must be host memory, so it cannot carry libpj's own partitions
+    (device buffers): bench.py's partitioned leg rejects it at world > 1."""
+
+    def __init__(self):
+        import torch.distributed as dist
+        self._dist = dist
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+
+    def allreduce(self, vals, is_min):
+        import torch
+        t = torch.from_numpy(vals.copy())
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.MIN if is_min else self._dist.ReduceOp.SUM)
+        vals[:] = t.numpy()
+
+    def alltoall_counts(self, send, recv):
+        import torch
+        s = torch.from_numpy(send.copy())
+        r = torch.empty_like(s)
+        self._dist.all_to_all_single(r, s)
+        recv[:] = r.numpy()
+
+    def alltoallv(self, send_ptr, scounts, recv_ptr, rcounts, elem):
+        import torch
+        sb, rb = (scounts * elem).tolist(), (rcounts * elem).tolist()
+        src = torch.from_numpy(_host(send_ptr, sum(sb)).copy()) if sum(sb) else torch.zeros(0, dtype=torch.uint8)
+        dst = torch.empty(sum(rb), dtype=torch.uint8)
+        self._dist.all_to_all_single(dst, src, output_split_sizes=rb, input_split_sizes=sb)
+        if sum(rb):
+            _host(recv_ptr, sum(rb))[:] = dst.numpy()
+
+    def allgather(self, own_ptr, all_ptr, nbytes):
+        import torch
+        own = torch.from_numpy(_host(own_ptr, nbytes).copy())
+        out = torch.empty(nbytes * self.world, dtype=torch.uint8)
+        self._dist.all_gather_into_tensor(out, own)
+        _host(all_ptr, nbytes * self.world)[:] = out.numpy()

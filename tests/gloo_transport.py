@@ -1,45 +1,12 @@
-"""A pj_comm transport over torch.distributed (gloo) for the CPU tests: the callbacks
-of pj_comm_create_callbacks (include/pj.h) on host buffers, so libpj's C++
-protocol loops (engine.cpp) run with world_size > 1 without a GPU.
-
-Test infrastructure only; the product transports are RCCL and the in-process
-device copies (comm.cpp)."""
+"""Helpers of the gloo CPU tests: the pj_comm callbacks over torch.distributed are
+paralleljohnson_amd.partition.TorchDistTransport (host buffers); gather_blocks collects
+every rank's distance slice. Test infrastructure only; the product transports are RCCL and
+the in-process device copies (comm.cpp)."""
 import numpy as np
 import torch
 import torch.distributed as dist
 
-from paralleljohnson_amd.partition import _host
-
-
-class GlooTransport:
-    def __init__(self):
-        self.world = dist.get_world_size()
-        self.rank = dist.get_rank()
-
-    def allreduce(self, vals, is_min):
-        t = torch.from_numpy(vals.copy())
-        dist.all_reduce(t, op=dist.ReduceOp.MIN if is_min else dist.ReduceOp.SUM)
-        vals[:] = t.numpy()
-
-    def alltoall_counts(self, send, recv):
-        s = torch.from_numpy(send.copy())
-        r = torch.empty_like(s)
-        dist.all_to_all_single(r, s)
-        recv[:] = r.numpy()
-
-    def alltoallv(self, send_ptr, scounts, recv_ptr, rcounts, elem):
-        sb, rb = (scounts * elem).tolist(), (rcounts * elem).tolist()
-        src = torch.from_numpy(_host(send_ptr, sum(sb)).copy()) if sum(sb) else torch.zeros(0, dtype=torch.uint8)
-        dst = torch.empty(sum(rb), dtype=torch.uint8)
-        dist.all_to_all_single(dst, src, output_split_sizes=rb, input_split_sizes=sb)
-        if sum(rb):
-            _host(recv_ptr, sum(rb))[:] = dst.numpy()
-
-    def allgather(self, own_ptr, all_ptr, nbytes):
-        own = torch.from_numpy(_host(own_ptr, nbytes).copy())
-        out = torch.empty(nbytes * self.world, dtype=torch.uint8)
-        dist.all_gather_into_tensor(out, own)
-        _host(all_ptr, nbytes * self.world)[:] = out.numpy()
+from paralleljohnson_amd.partition import TorchDistTransport as GlooTransport  # noqa: F401
 
 
 def gather_blocks(local, block, world, n):

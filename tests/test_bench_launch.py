@@ -50,3 +50,38 @@ def test_gpus_mismatching_the_launcher_fails():
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
     assert r.returncode != 0
     assert "--gpus 3 but the launcher started 2" in r.stderr
+
+
+def test_partitioned_leg_guard_rejects_a_non_rccl_group():
+    """at world > 1 the partitioned leg must run over an RCCL communicator
+    whose own rank count (ncclCommCount) equals the world; the gloo rehearsal's host-buffer
+    transport ("callbacks") is refused, and the refusal becomes the leg's error entry."""
+    env = dict(_env(), PJ_BENCH_FORCE_PART="1")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"], capture_output=True, text=True,
+                       timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    err = d["k28_partitioned"]["error"]
+    assert "needs an RCCL communicator of 2 ranks" in err and "'callbacks' reporting 2" in err, err
+
+
+def test_transport_guard_accepts_only_a_full_rccl_group():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class C:
+        def __init__(self, kind, count):
+            self.kind, self._n = kind, count
+
+        def transport_ranks(self):
+            return self._n, 0
+
+    assert bench.transport_guard(C("self", 1), 1) == {"transport": "self", "transport_ranks": 1, "transport_rank": 0}
+    assert bench.transport_guard(C("rccl", 4), 4)["transport_ranks"] == 4
+    for kind, n in (("rccl", 3), ("host", 4), ("callbacks", 4), ("self", 1)):
+        try:
+            bench.transport_guard(C(kind, n), 4)
+        except RuntimeError as e:
+            assert "needs an RCCL communicator of 4 ranks" in str(e)
+        else:
+            raise AssertionError((kind, n))

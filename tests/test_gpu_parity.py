@@ -353,7 +353,10 @@ def test_weighted_defer_heavy(ctx, oracle, scale, ef):
         g.set_option("defer_heavy", dh)
         for pf in (4.0, 0.3, 40.0):
             g.set_option("pull_factor", pf)
-            for delta, bw, tf, dc in ((0, 0, 0.2, 1), (3, 0, 0.0, 1), (7, 2, 0.0, 0), (24, 0, 0.1, 1), (2, 1, 0.3, 0)):
+            # (deltas above 127: bands too wide for the heavy pull's byte map, whose probes then read
+            # dist, the deferred members included: ADVICE r05)
+            for delta, bw, tf, dc in ((0, 0, 0.2, 1), (3, 0, 0.0, 1), (7, 2, 0.0, 0), (24, 0, 0.1, 1), (2, 1, 0.3, 0),
+                                      (160, 0, 0.0, 1), (200, 130, 0.0, 0)):
                 g.set_option("delta", delta)
                 g.set_option("band_width", bw)
                 g.set_option("tail_frac", tf)
@@ -718,3 +721,45 @@ def test_partitioned_weighted_s22_world2(ctx, pj):
     torch.cuda.empty_cache()
     # the certificate of the last solve's distances (got) against the single-GPU CSR
     assert sssp_certificate(row, col, w, got, roots[-1], device="cuda", chunk=1 << 27) == []
+
+
+@pytest.mark.gpu
+def test_weighted_work_counters_and_deferred_gather(ctx, oracle):
+    """The always-on work counters of a weighted solve (pj_stats.scanned_edges / probes /
+    work_bytes, per kernel class) are consistent, and the input-id distances gathered lazily
+    from the solver's ids (delta_materialize) are exact through every reader: the host copy,
+    pj_dist_device, the reach pass and the parent tree; a source without edges gets its 0."""
+    g = ctx.generate_kronecker(14, 16, 5, weighted=True)
+    row, col, wc = g.get_csr()
+    col = col.astype(np.uint32)
+    deg = np.diff(row)
+    roots = [int(r) for r in g.sample_roots(3, 3)]
+    for r in roots:
+        exp = oracle.dijkstra(row, col, wc, r)
+        g.sssp(r, copy=False)
+        st = g.stats()
+        byk = st["work_by_kernel"]
+        assert st["scanned_edges"] == sum(v[0] for v in byk.values()) > 0
+        assert st["probes"] == sum(v[1] for v in byk.values()) > 0
+        assert st["work_bytes"] == sum(v[2] for v in byk.values())
+        for rec, prb, nb in byk.values():
+            assert 0 <= prb <= rec + rec  # (a probe per record at most, a pull's stop record unprobed)
+            assert rec + prb <= nb <= 8 * rec + 4 * prb
+        assert byk["light_round"][0] > 0
+        # a solve scans fewer records than the reached vertices' rows hold, and never 4x more
+        m_r = int(deg[exp < oracle.INT_INF].sum())
+        assert st["scanned_edges"] <= 4 * m_r
+        assert g.dist_device_ptr() != 0  # (materializes the input-id row)
+        assert (g.copy_dist() == exp).all()
+        g.sssp(r, copy=False)
+        rs = g.reach_stats()
+        assert rs["reached"] == int((exp < oracle.INT_INF).sum()) and rs["reached_edges"] == m_r
+        par = g.parent_tree()
+        assert all(v == 0 for k, v in g.validate_tree(r, par).items() if k.startswith("bad"))
+        assert (g.sssp(r) == exp).all()
+    iso = int(np.nonzero(deg == 0)[0][0])
+    g.sssp(iso, copy=False)
+    assert g.stats()["scanned_edges"] == 0
+    d = g.copy_dist()
+    assert d[iso] == 0 and (np.delete(d, iso) == oracle.INT_INF).all()
+    g.close()

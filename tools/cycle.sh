@@ -6,8 +6,12 @@
 #   smoke         __graft_entry__.smoke()
 #   bench         the default bench line (bench args appended) -> bench.json
 #   kt            rocprofv3 kernel trace + stats of a short k26w bench run
-#   pmc           FETCH_SIZE / WRITE_SIZE passes over tools/traffic_probe.py (one counter per run)
-#   table         the per-kernel PMC table and traffic json from kt + pmc
+#   calib         FETCH_SIZE calibration: tools/calib/pj_gather_calib timed, then under --pmc (one counter
+#                 group per run) -> calib.log, calpmc_*/, gather_calib.json (tools/calib_table.py)
+#   wtable        the per-kernel table of k26w solves: kernel trace + --pmc passes (RDREQ / RDREQ_32B,
+#                 FETCH_SIZE, WRITE_SIZE) of tools/traffic_probe.py, its work counters -> pmc_table.txt,
+#                 traffic_k26w.json (tools/pmc_solve_table.py, calibrated by gather_calib.json: this
+#                 cycle's calib step if it ran, else profiles/r06/gather_calib.json)
 #   probe:<cmd>   any python command line under a 240 s limit (e.g. probe:tools/stats_probe.py 26 3)
 #   vtests:<v>:<pytest args>  -m gpu tests under the libpj build variant <v>
 #   ktp:<cmd>     rocprofv3 kernel trace + stats of any python command line -> kt_<name>/
@@ -46,14 +50,27 @@ for st in "${LIST[@]}"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
         python3 bench.py --no-cpu-baseline --no-secondary --no-partitioned --no-tts --steps 8 --warmup 1 "$@" \
         > "$OUT/kt.log" 2>&1 || { echo "kt failed"; tail "$OUT/kt.log"; exit 1; } ;;
-    pmc)
-      for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o run -- \
-          python3 tools/traffic_probe.py 26 4 1 > "$OUT/pmc_$c.log" 2>&1 || { echo "pmc $c failed"; exit 1; }
-      done ;;
-    table)
-      python3 tools/pmc_solve_table.py "$OUT" > "$OUT/pmc_table.txt" 2>&1 || { echo "table failed"; exit 1; }
-      python3 tools/traffic_json.py "$OUT" > "$OUT/traffic_k26w.json" 2>&1 || { echo "traffic failed"; exit 1; }
+    calib)
+      B=tools/calib/pj_gather_calib
+      timeout -k 10 120 $B 4096 3 > "$OUT/calib.log" 2>&1 || { echo "calib failed"; tail "$OUT/calib.log"; exit 1; }
+      for grp in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_BUBBLE_sum TCC_EA0_RDREQ_DRAM_sum" FETCH_SIZE WRITE_SIZE; do
+        gn=$(echo "$grp" | tr ' ' '+')
+        timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d "$OUT/calpmc_$gn" -o run -- $B 4096 3 \
+          > "$OUT/calpmc_$gn.log" 2>&1 || { echo "calib pmc $grp failed"; tail "$OUT/calpmc_$gn.log"; exit 1; }
+      done
+      python3 tools/calib_table.py "$OUT" > "$OUT/gather_calib.json" || { echo "calib table failed"; exit 1; }
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('bytes/request', d.get('bytes_per_request'), 'dword gathers/s', d.get('random_dword_gathers_per_s'))" "$OUT/gather_calib.json" ;;
+    wtable)
+      P="tools/traffic_probe.py 26 ${WT_SOLVES:-6} 1"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/wkt" -o run -- python3 -u $P \
+        --json "$OUT/probe_work.json" > "$OUT/wkt.log" 2>&1 || { echo "wtable trace failed"; tail "$OUT/wkt.log"; exit 1; }
+      for grp in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" FETCH_SIZE WRITE_SIZE; do
+        gn=$(echo "$grp" | tr ' ' '+')
+        timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d "$OUT/wpmc_$gn" -o run -- python3 -u $P \
+          > "$OUT/wpmc_$gn.log" 2>&1 || { echo "wtable pmc $grp failed"; tail "$OUT/wpmc_$gn.log"; exit 1; }
+      done
+      CAL=profiles/r06/gather_calib.json; [ -f "$OUT/gather_calib.json" ] && CAL="$OUT/gather_calib.json"
+      python3 tools/pmc_solve_table.py "$OUT" "$CAL" > "$OUT/pmc_table.txt" 2>&1 || { echo "table failed"; cat "$OUT/pmc_table.txt"; exit 1; }
       cat "$OUT/pmc_table.txt" ;;
     probe)
       timeout -k 10 240 python3 -u $arg > "$OUT/probe_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-40).log" 2>&1 \
