@@ -383,6 +383,9 @@ __device__ __forceinline__ u32 v2_uni(u32 x) { return (u32)__builtin_amdgcn_read
 struct V2Work {
     u32 rec = 0, prb = 0;
     __device__ __forceinline__ void add(u32 r, u32 p) {
+#ifdef PJ_V2_NOCOUNT  // (measurement build only: the counters' own cost, A/B)
+        return;
+#endif
         rec += v2_uni(r);
         prb += v2_uni(p);
     }
