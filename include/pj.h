@@ -441,9 +441,10 @@ int pj_wpart_begin(pj_wpart* p, int64_t source, int32_t delta, int32_t* delta_ou
 int pj_wpart_select(pj_wpart* p, int32_t lo, int32_t hi, int64_t* out);
 /* light != 0: the frontier relaxes its light edges (w < delta) and joins the
  * band's members; light == 0: the members relax their heavy edges. counts[o] =
- * the pairs queued for owner o. With send != NULL (room for their sum) the
- * pairs are also packed into it owner-major; with send == NULL the caller
- * sizes its buffer and calls pj_wpart_pack before any other step of p
+ * the pairs queued for owner o. send must be NULL at world > 1 (PJ_ERR_ARG
+ * otherwise: no bound on the pairs is known before the relax, since the queue
+ * keeps one pair per improving remote relaxation); the caller sizes its buffer
+ * from the counts and calls pj_wpart_pack before any other step of p
  * (PJ_ERR_STATE otherwise: the cache already counts the pairs as sent). The ids
  * are the partition's internal ids (with the per-block degree order,
  * PJ_WP_RELABEL, a block's relabeled ids): only their owner, id / block, is

@@ -451,8 +451,9 @@ def write_parents(parent, path: str):
 
 class Pinned:
     """A host array page-locked by host_pin. Holds the array, so its pages cannot be freed
-    (and the address reused by another array) while the registration stands; unpins on
-    close(), at the end of a `with` block, or when the handle is garbage-collected."""
+    (and the address reused by another array) while the registration stands. The module's
+    registry keeps the handle too (so that host_unpin(array) finds it), so dropping the
+    handle does NOT unpin: close(), the end of a `with` block or host_unpin(array) does."""
 
     def __init__(self, a: np.ndarray):
         self.array = a
@@ -480,7 +481,7 @@ class Pinned:
             pass
 
 
-_PINNED = {}  # address -> Pinned (keeps the array alive while registered)
+_PINNED = {}  # address -> Pinned (keeps the handle and its array alive until close / host_unpin)
 
 
 def host_pin(a: np.ndarray) -> Pinned:

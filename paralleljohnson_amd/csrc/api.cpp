@@ -1308,8 +1308,15 @@ int pj_wpart_select(pj_wpart* p, int32_t lo, int32_t hi, int64_t* out) {
 int pj_wpart_relax(pj_wpart* p, int light, int32_t lo, int32_t hi, uint64_t* send, int64_t* counts) {
     if (!p || !counts || lo < 0 || hi < lo) return arg_error("pj_wpart_relax: bad argument");
     return guarded([&] {
-        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
-        wpart_relax(*reinterpret_cast<WPart*>(p), light, lo, hi, (u64*)send, counts);
+        WPart& P = *reinterpret_cast<WPart*>(p);
+        // (the claim queue keeps one pair per improving remote relaxation, and an overflow rerun
+        // re-sends from every band member: no bound known before the relax sizes a caller's
+        // buffer, so the pairs are packed only into a buffer sized from the counts)
+        if (send && wpart_world(P) > 1)
+            throw Error(PJ_ERR_ARG, "pj_wpart_relax: pass send = NULL at world > 1, size the buffer from the counts "
+                                    "and call pj_wpart_pack");
+        bind(wpart_ctx(P));
+        wpart_relax(P, light, lo, hi, counts);
         return (int)PJ_OK;
     });
 }

@@ -2463,8 +2463,8 @@ void delta_batch(Graph& g, const i64* sources, int n_src, int slots,
     const double slot_bytes = 4.0 * (double)(n_scan + g.n) + 5.0 * 8.0 * (double)((n_scan + 63) / 64) +
                               60.0 * (double)std::max<i64>(1, std::min<i64>(n_scan, g.nnz / (i64)V2_HT + 1));
     while ((int)w.extra.size() < slots - 1) {
-        size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) != hipSuccess || slot_bytes > 0.5 * (double)fr) break;
+        const size_t fr = dev_free_bytes();  // (libpj's idle cached blocks count as free)
+        if (slot_bytes > 0.5 * (double)fr) break;
         std::unique_ptr<DeltaSolve> v(new DeltaSolve());
         try {
             PJ_HIP(hipStreamCreateWithFlags(&v->s, hipStreamNonBlocking));

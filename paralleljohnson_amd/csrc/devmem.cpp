@@ -11,13 +11,17 @@
 // free blocks go back first) and is handed out again, whole or in slices,
 // to later requests on the same device. A request takes the smallest free range that holds
 // it and leaves the rest of the range free (a world-2 build's two ranks take the two halves
-// of a block a world-1 build freed); a freed slice merges with its free neighbours. A
-// request that fails while the cache holds blocks returns every wholly free block to the
-// driver and tries again, so the cache never costs an allocation that would otherwise
-// succeed. A big free synchronizes the block's device first, as hipFree does: work still
+// of a block a world-1 build freed); a freed slice merges with its free neighbours. A libpj
+// allocation (big or small) that fails while the cache holds blocks returns every wholly free
+// block to the driver and tries again, so the cache never costs libpj an allocation that
+// would otherwise succeed; the free-memory estimates that size libpj's optional buffers
+// (batch slots) count the cache's idle bytes as free (dev_free_bytes). Other allocators in the
+// same process (e.g. torch) do not see the cached blocks: such callers trim the cache first
+// (pj_trim_device_cache). A big free synchronizes the block's device first, as hipFree does: work still
 // in flight on any stream may use the memory, and the next owner of a slice may be another
 // stream (another rank's, or another batch slot's).
 #include <algorithm>
+#include <cstdlib>
 #include <iterator>
 #include <map>
 #include <mutex>
@@ -94,7 +98,17 @@ BigCache& cache() {
 void* dev_alloc(size_t bytes) {
     void* p = nullptr;
     if (bytes < BIG) {
-        PJ_HIP(hipMalloc(&p, bytes));
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {  // the cache's idle blocks back to the driver, then once more
+            (void)hipGetLastError();
+            BigCache& c = cache();
+            std::lock_guard<std::mutex> lk(c.mu);
+            if (c.held > 0) {
+                c.flush();
+                e = hipMalloc(&p, bytes);
+            }
+        }
+        PJ_HIP(e);
         return p;
     }
     int dev = 0;
@@ -111,7 +125,13 @@ void* dev_alloc(size_t bytes) {
                 bi = it;
             }
     }
-    if (bb) return c.take(bb, bi, bytes);
+    if (bb) {
+        void* q = c.take(bb, bi, bytes);
+        // test hook: a cached slice handed out full of 0xFF, so that a buffer relying on the zeroed
+        // pages of fresh driver memory shows up (tests/test_partition.py)
+        if (std::getenv("PJ_DEVMEM_POISON")) PJ_HIP(hipMemset(q, 0xFF, bytes));
+        return q;
+    }
     const size_t bb_bytes = (bytes + SLACK - 1) / SLACK * SLACK + SLACK;
     hipError_t e = hipMalloc(&p, bb_bytes);
     if (e != hipSuccess && c.held > 0) {
@@ -183,6 +203,22 @@ void dev_free(void* p, size_t bytes) {
             c.release(x);
         }
     }
+}
+
+size_t dev_free_bytes() {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fr;
+    BigCache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (const Blk* b : c.blocks)
+        if (b->dev == dev)
+            for (const auto& r : b->free_ranges) fr += r.second;
+    return fr;
 }
 
 size_t dev_trim() {

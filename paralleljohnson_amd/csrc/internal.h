@@ -48,6 +48,7 @@ void set_error(const std::string& msg);
 void* dev_alloc(size_t bytes);
 void dev_free(void* p, size_t bytes);
 size_t dev_trim();  // cached big blocks without a live slice back to the driver; bytes released
+size_t dev_free_bytes();  // free device memory of the current device, the cache's idle ranges included
 
 template <typename T>
 struct DevBuf {
@@ -344,7 +345,7 @@ std::vector<WPart*> wparts_from_coo_group(const std::vector<Ctx*>& ctxs, DevBuf<
 void wpart_info(const WPart& p, i64* out8);
 int32_t wpart_begin(WPart& p, i64 source, int32_t delta);
 void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2);
-void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts);
+void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, i64* counts);
 void wpart_pack(WPart& p, u64* send);
 void wpart_device_bytes(const WPart& p, i64* out4);
 void wpart_apply(WPart& p, const u64* recv, i64 nr, int light, int32_t lo, int32_t hi);

@@ -778,8 +778,8 @@ void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_
         mw.slots.push_back(std::move(sl));
     }
     while ((int)mw.slots.size() < nslots) {
-        size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) != hipSuccess || sb > 0.5 * (double)fr) break;
+        const size_t fr = dev_free_bytes();  // (libpj's idle cached blocks count as free)
+        if (sb > 0.5 * (double)fr) break;
         std::unique_ptr<MsSlot> sl(new MsSlot());
         try {
             ms_slot_alloc(g, *sl, mw.W, lcap, true);

@@ -2048,15 +2048,14 @@ void wpart_select(WPart& p, int32_t lo, int32_t hi, i64* out2) {
 // heavy edges, with the sent-pair cache cleared so that no pair is skipped for having
 // been "sent" by the run whose queue was dropped. Redundant work, but only until the
 // queue has grown: it keeps its size.
-static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts,
+static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, i64* counts,
                              DevBuf<u64>* pre);
-void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts) {
-    wpart_relax_impl(p, light, lo, hi, send, counts, nullptr);
+void wpart_relax(WPart& p, int light, int32_t lo, int32_t hi, i64* counts) {
+    wpart_relax_impl(p, light, lo, hi, counts, nullptr);
 }
 // pre != NULL (the engine's send buffer): grown to the queue's capacity and packed right
 // behind the count kernel, before the one host wait of the step (no second wait to pack)
-static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* send, i64* counts,
-                             DevBuf<u64>* pre) {
+static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, i64* counts, DevBuf<u64>* pre) {
     hipStream_t s = p.ctx->stream;
     if (p.pending_pack) throw Error(PJ_ERR_STATE, "wpart relax: the last relax's pairs were not packed");
     p.clear_stat();
@@ -2102,7 +2101,6 @@ static void wpart_relax_impl(WPart& p, int light, int32_t lo, int32_t hi, u64* s
     }
     for (int o = 0; o < p.world; ++o) counts[o] = p.world > 1 ? (i64)p.hstat[o] : 0;
     p.pending_pack = p.world > 1 && !pre;
-    if (send) wpart_pack(p, send);
 }
 
 // The queued pairs (id | cand << 32), owner-major, into send (room for the sum of the
@@ -2195,7 +2193,7 @@ struct WPartGpuSteps final : DeltaSteps {
     int32_t begin(i64 source, int32_t delta) override { return wpart_begin(p, source, delta); }
     void select(int32_t lo, int32_t hi, i64* out2) override { wpart_select(p, lo, hi, out2); }
     void relax(int light, int32_t lo, int32_t hi, i64* counts) override {
-        wpart_relax_impl(p, light, lo, hi, nullptr, counts, p.world > 1 ? &send_b : nullptr);
+        wpart_relax_impl(p, light, lo, hi, counts, p.world > 1 ? &send_b : nullptr);
         send = send_b.p;
     }
     void apply(i64 nr, int light, int32_t lo, int32_t hi) override { wpart_apply(p, recv_b.p, nr, light, lo, hi); }

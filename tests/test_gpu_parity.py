@@ -212,6 +212,43 @@ def test_device_cache_slices_and_trim(ctx, pj):
     assert pj.trim_device_cache() >= 2**30
 
 
+def test_partitions_built_in_poisoned_cached_blocks(ctx, pj, monkeypatch):
+    """the partitioned builds are why the device cache exists, and a cached slice
+    is handed out as the last owner left it, not zeroed like fresh driver memory. With
+    PJ_DEVMEM_POISON every cached slice comes out full of 0xFF; the weighted and unit-weight
+    partitions (world 2, host transport) built twice through such slices -- the second build in
+    the first one's freed blocks -- must still answer as the single-GPU solvers do."""
+    from paralleljohnson_amd.partition import (Comm, bfs_group, delta_group, gather_group, load_kronecker,
+                                               load_weighted_kronecker)
+    pj.trim_device_cache()
+    exp = {}
+    for weighted in (True, False):
+        g = ctx.generate_kronecker(24, 16, 3, weighted=weighted)
+        roots = [int(r) for r in g.sample_roots(5, 2)]
+        exp[weighted] = {r: g.sssp(r) for r in roots}
+        g.close()  # (its >= 1 GiB arrays stay cached for the partitions below)
+    monkeypatch.setenv("PJ_DEVMEM_POISON", "1")
+    ctxs = [pj.Context(0) for _ in range(2)]
+    comms = Comm.group(ctxs, "host")
+    try:
+        for build in range(2):
+            for weighted in (True, False):
+                load = load_weighted_kronecker if weighted else load_kronecker
+                parts = [load(ctxs[k], 24, 16, 3, k, 2) for k in range(2)]
+                for r, d in exp[weighted].items():
+                    (delta_group if weighted else bfs_group)(parts, comms, r)
+                    assert (gather_group(parts, comms) == d).all(), (build, weighted, r)
+                for p in parts:
+                    p.close()
+    finally:
+        for c in comms:
+            c.close()
+        for c in ctxs:
+            c.close()
+        monkeypatch.delenv("PJ_DEVMEM_POISON")
+        pj.trim_device_cache()
+
+
 def test_weighted_delta_stepping(ctx, oracle):
     rng = np.random.default_rng(21)
     for trial in range(6):

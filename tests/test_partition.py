@@ -448,6 +448,25 @@ def test_wpart_claim_queue_overflow(pj, oracle, world):
 
 
 @pytest.mark.gpu
+def test_wpart_relax_refuses_a_send_buffer_at_world2(pj):
+    """no bound on a relax's queued pairs is known before it runs, so at world > 1
+    pj_wpart_relax takes no send buffer (PJ_ERR_ARG): the caller sizes one from the counts and
+    calls pj_wpart_pack."""
+    import ctypes
+    from paralleljohnson_amd.partition import load_weighted
+    ctx = pj.Context(0)
+    g = ctx.load_coo([0, 1, 2, 3], [1, 2, 3, 0], [1, 2, 3, 4], n=200)
+    parts = [load_weighted(ctx, g, r, 2) for r in range(2)]
+    counts = np.zeros(2, np.int64)
+    rc = pj._lib.pj_wpart_relax(parts[0]._h, 1, 0, 10, ctypes.c_void_p(4096), counts.ctypes.data_as(ctypes.c_void_p))
+    assert rc == -1 and b"pass send = NULL" in pj._lib.pj_last_error()
+    for p in parts:
+        p.close()
+    g.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_multi_weighted_partition_state_shrinks(pj, oracle):
     """pj_multi with a weighted partitioned Kronecker s24 (every rank enumerates the tuples
     and keeps its block's rows: pj_wpart_generate_kronecker) at world 2, 4 and 8 (ranks
