@@ -82,6 +82,7 @@ struct LevelCnt {
     u64 found[NSH];    // newly visited vertices
     u64 in_next[NSH];  // in-degree sum of newly visited vertices
     u64 fnz[NSH];      // newly visited vertices with out-degree > 0 (the next frontier)
+    u64 scan[NSH];     // pull levels: in-edges probed (a push level's edges are its frontier's, d.mq)
 };
 
 struct LevelState {
@@ -111,7 +112,11 @@ struct BfsArgs {
     LevelCnt* C;    // [3]
     LevelState* S;  // [2]
     u64* nmode;     // [2] push / pull levels run (device)
-    int64_t* host;  // mapped host words: [0] levels run (-1 while running), [1] push, [2] pull, [3] launches
+    int64_t* host;  // mapped host words: [0] levels run (-1 while running), [1] push, [2] pull, [3] launches,
+                    // [4] edges scanned (push: every frontier out-edge; pull: every in-edge probed)
+    u64* wtot;      // device: edges scanned by the levels so far (block 0 of each launch adds the last one's)
+    u64* llog;      // level_log option: per launch (L, mode | kind << 8, frontier, its out-edges, found, scanned
+                    // by the previous launch), or null
     u64* stamps;    // PJ_BFS_STAMPS builds: [launch * 64 + slot] 100 MHz timestamps of block 0
 };
 
@@ -209,6 +214,7 @@ struct BlockQ {
 
 struct Acc {
     u64 m = 0, f = 0, in = 0, fz = 0;
+    u64 scan = 0;  // (pull levels, lane 0 of each wave: the wave's in-edge probes)
 };
 
 __device__ __forceinline__ void hub_direct(const BfsArgs& a, LevelCnt* cacc, int32_t L, bool ish, u32 v, u32 deg,
@@ -317,12 +323,14 @@ __device__ __forceinline__ void flush_acc(LevelCnt* c, const Acc& acc, u64* red)
     const u64 f = block_sum<NW>(acc.f, red);
     const u64 in = block_sum<NW>(acc.in, red);
     const u64 fz = block_sum<NW>(acc.fz, red);
+    const u64 sc = block_sum<NW>(acc.scan, red);
     if (threadIdx.x == 0) {
         const int sh = blockIdx.x % NSH;
         if (m) atomicAdd(&c->m_next[sh], m);
         if (f) atomicAdd(&c->found[sh], f);
         if (in) atomicAdd(&c->in_next[sh], in);
         if (fz) atomicAdd(&c->fnz[sh], fz);
+        if (sc) atomicAdd(&c->scan[sh], sc);
     }
 }
 
@@ -410,6 +418,7 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
         u32 E;
         const u32 ex = block_excl_scan<NW>(t < F ? ss.cdeg[t] : 0u, ss.scan, E);
         ss.cex[t] = ex;
+        if (t == 0) *a.wtot += E;  // (the level walks every frontier out-edge)
         if (t == 0) ss.nn = 0;
         __syncthreads();
         u32 vv[SEPT];
@@ -520,6 +529,7 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
                 a.host[1] = (int64_t)a.nmode[0];
                 a.host[2] = (int64_t)a.nmode[1];
                 a.host[3] = (int64_t)li + 1;
+                a.host[4] = (int64_t)*a.wtot;
                 __atomic_store_n(&a.host[0], (int64_t)L2, __ATOMIC_RELEASE);
             }
             return;
@@ -608,6 +618,28 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
     if (blockIdx.x == 0) {
         u64* zp = reinterpret_cast<u64*>(a.C + (li + 1) % 3);
         for (u32 i = t; i < sizeof(LevelCnt) / 8; i += TB) zp[i] = 0;
+        if (t == 0 && dec > 0) {
+            // edges scanned: the previous launch's pull probes, and this launch's push edges
+            // (small levels add their own)
+            const LevelCnt& pc = a.C[(li + 2) % 3];
+            u64 ps = 0;
+#pragma unroll
+            for (int k = 0; k < NSH; ++k) ps += pc.scan[k];
+            *a.wtot += ps + ((go && d.mode == 0 && !small) ? d.mq : 0ull);
+        }
+        if (t == 0 && a.llog && li < 64) {  // (every launch, the idle ones behind the end too)
+            const LevelCnt& pc = a.C[(li + 2) % 3];
+            u64 ps = 0;
+#pragma unroll
+            for (int k = 0; k < NSH; ++k) ps += pc.scan[k];
+            u64* e = a.llog + 6 * (u64)li;
+            e[0] = (u64)(int64_t)L;
+            e[1] = (u64)d.mode | ((u64)(small ? 2 : dec == 2 ? (queued ? 0 : 1) : dec == 1 ? 3 : 4) << 8);
+            e[2] = queued ? nfr : d.found;
+            e[3] = d.mq;
+            e[4] = d.found;
+            e[5] = dec > 0 ? ps : 0;
+        }
         if (t == 0 && !small) {
             LevelState& s = a.S[li & 1];
             s.mode = d.mode;
@@ -621,6 +653,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                 a.host[1] = (int64_t)a.nmode[0];
                 a.host[2] = (int64_t)a.nmode[1];
                 a.host[3] = (int64_t)li + 1;
+                a.host[4] = (int64_t)*a.wtot;
                 __atomic_store_n(&a.host[0], (int64_t)L, __ATOMIC_RELEASE);
             }
         }
@@ -785,6 +818,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
         u32 scw = SC;
         while (scw > 1 && (a.nwords + scw - 1) / scw < (i64)gridDim.x * NW) scw >>= 1;
         const i64 nsc = (a.nwords + scw - 1) / scw;
+        u32 lsc = 0;  // in-edge probes of this lane's candidates (the wave's ones, for the wave-wide scans)
         for (i64 sc = (i64)blockIdx.x * NW + wave_id(); sc < nsc; sc += (i64)gridDim.x * NW) {
             const i64 wbase = sc * scw;
             const bool mine = lane < (int)scw && wbase + lane < a.nwords;
@@ -886,6 +920,10 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                         }
                     }
                 }
+                // (probes so far: stage A took min(PB1, row), stage B min(PB2, rest) of the open
+                // candidates, the serial loop one per step, so k - b up to the row's end)
+#pragma unroll
+                for (int j = 0; j < RPI; ++j) lsc += act[j] ? (u32)(min(k[j], e[j]) - b[j]) : 0u;
                 // wave-cooperative scan of the long rows that are still open
 #pragma unroll
                 for (int j = 0; j < RPI; ++j) {
@@ -895,7 +933,8 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                         open &= open - 1;
                         const Off kb = __shfl(k[j], l, 64), ke = __shfl(e[j], l, 64);
                         bool hit = false;
-                        for (Off kk = kb; kk < ke; kk += 2 * WAVE) {
+                        Off kk = kb;
+                        for (; kk < ke; kk += 2 * WAVE) {
                             const Off k0 = kk + lane, k1 = kk + WAVE + lane;
                             const u32 u0 = k0 < ke ? g.ccol[k0] : 0u;
                             const u32 u1 = k1 < ke ? g.ccol[k1] : 0u;
@@ -907,7 +946,10 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                                 break;
                             }
                         }
-                        if (lane == l) fnd[j] = hit;
+                        if (lane == l) {
+                            fnd[j] = hit;
+                            lsc += (u32)(min(kk + (Off)(2 * WAVE), ke) - kb);  // (the steps up to the hit)
+                        }
                     }
                 }
 #pragma unroll
@@ -934,6 +976,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                 a.fnew[wbase + lane] = mynew;
             }
         }
+        acc.scan += lsc;
     }
     flush(q, a, cacc, L);
     flush_acc(cacc, acc, red);
@@ -988,8 +1031,10 @@ __global__ __launch_bounds__(TB) void bfs_init_k(BfsArgs a, Graph_d<Off> g, cons
         st.level = -1;
         st.m_u = nnz;
         a.nmode[0] = a.nmode[1] = 0;
+        *a.wtot = 0;
         a.host[0] = -1;
         a.host[3] = 0;
+        a.host[4] = 0;
     }
 }
 
@@ -1105,6 +1150,13 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     a.C = reinterpret_cast<LevelCnt*>(w.ctl.p);
     a.S = reinterpret_cast<LevelState*>(w.ctl.p + 3 * sizeof(LevelCnt));
     a.nmode = reinterpret_cast<u64*>(w.ctl.p + 3 * sizeof(LevelCnt) + 2 * sizeof(LevelState));
+    a.wtot = a.nmode + 2;
+    DevBuf<u64> llog;
+    if (g.level_log) {
+        llog.alloc(6 * 64);
+        PJ_HIP(hipMemsetAsync(llog.p, 0xFF, 6 * 64 * sizeof(u64), s));
+        a.llog = llog.p;
+    }
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.host), w.host, 0));
     Graph_d<Off> gd{static_cast<const Off*>(g.row_ptr()), g.col.p, static_cast<const Off*>(g.crow_ptr()),
                     g.ccol_ptr()};
@@ -1169,9 +1221,25 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     if (valid) {
         st.td_levels = ((volatile int64_t*)w.host)[1];
         st.bu_levels = ((volatile int64_t*)w.host)[2];
+        // edges scanned: every record read is a u32 column id and every one probes a visited bit
+        // (an 8-byte bitmap word; the N-bit bitmap stays in the L2s)
+        st.scanned_edges = st.probes = ((volatile int64_t*)w.host)[4];
+        st.work_bytes = 4 * st.scanned_edges + 8 * st.probes;
     }
     g.stats = st;
     g.have_result = true;
+    if (g.level_log && valid) {  // debug: one stderr line per level launch
+        std::vector<u64> h(6 * 64);
+        PJ_HIP(hipMemcpy(h.data(), llog.p, h.size() * sizeof(u64), hipMemcpyDeviceToHost));
+        static const char* kind[5] = {"queued", "bitmap", "small", "end", "idle"};
+        for (int l = 0; l < 64 && h[6 * (size_t)l] != ~0ull; ++l) {
+            const u64* e = &h[6 * (size_t)l];
+            std::fprintf(stderr, "level_launch %d level %lld mode %s frontier_from %s frontier %llu frontier_edges %llu "
+                         "prev_found %llu prev_scanned %llu\n", l, (long long)(int64_t)e[0], (e[1] & 255) ? "pull" : "push",
+                         kind[std::min<u64>((e[1] >> 8) & 7, 4)], (unsigned long long)e[2], (unsigned long long)e[3],
+                         (unsigned long long)e[4], (unsigned long long)e[5]);
+        }
+    }
 #if PJ_BFS_STAMPS
     {  // per launch: decide, then per small level (start, edges done, counters done), block 0's end
         std::vector<u64> h(64 * 64);
@@ -1205,7 +1273,7 @@ void bfs_workspace(Graph& g) {
     w.vis2.alloc(nwords ? nwords : 1);
     w.zmask.alloc(nwords ? nwords : 1);
     w.fnew.alloc(nwords ? nwords : 1);
-    w.ctl.alloc(3 * sizeof(LevelCnt) + 2 * sizeof(LevelState) + 2 * sizeof(u64));
+    w.ctl.alloc(3 * sizeof(LevelCnt) + 2 * sizeof(LevelState) + 3 * sizeof(u64));  // (+ nmode[2], wtot)
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.host), 8 * sizeof(int64_t), hipHostMallocMapped));
     if (nwords) {
         hipStream_t s = g.ctx->stream;

@@ -230,6 +230,7 @@ struct Graph {
                                // in round 5 with the cheaper pulls: +0.6%, profiles/r05/sweeps_r5h14.txt)
     double tail_light_pull = 3.0;  // the same rule in the tail's rounds
     int round_log = 0;         // debug: per light round (kind, frontier, light edges) on stderr
+    int level_log = 0;         // debug: per BFS level launch (level, direction, frontier, edges, scanned) on stderr
     int force_mode = 0;  // 0 auto, 1 push (top-down) only, 2 pull (bottom-up) from level 0
     int level_batch = 0; // BFS levels enqueued per host check (0 = the previous solve's count, then 2, 4, 8, ...)
     double dense_frac = 0.1; // delta v2: a light round with a frontier above dense_frac x n runs tile-dense (0 = never;

@@ -12,6 +12,8 @@
 #                 FETCH_SIZE, WRITE_SIZE) of tools/traffic_probe.py, its work counters -> pmc_table.txt,
 #                 traffic_k26w.json (tools/pmc_solve_table.py, calibrated by gather_calib.json: this
 #                 cycle's calib step if it ran, else profiles/r06/gather_calib.json)
+#   klevels[:opts] per-level table of configs[1] (K22 BFS): tools/k22_levels.py under a kernel trace and --pmc
+#                 passes -> k22_levels.txt (tools/k22_level_table.py); opts = libpj options k=v~k=v
 #   probe:<cmd>   any python command line under a 240 s limit (e.g. probe:tools/stats_probe.py 26 3)
 #   vtests:<v>:<pytest args>  -m gpu tests under the libpj build variant <v>
 #   ktp:<cmd>     rocprofv3 kernel trace + stats of any python command line -> kt_<name>/
@@ -72,6 +74,18 @@ for st in "${LIST[@]}"; do
       CAL=profiles/r06/gather_calib.json; [ -f "$OUT/gather_calib.json" ] && CAL="$OUT/gather_calib.json"
       python3 tools/pmc_solve_table.py "$OUT" "$CAL" > "$OUT/pmc_table.txt" 2>&1 || { echo "table failed"; cat "$OUT/pmc_table.txt"; exit 1; }
       cat "$OUT/pmc_table.txt" ;;
+    klevels)
+      P="tools/k22_levels.py ${KL_ROOTS:-4} $arg"
+      timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/klkt" -o run -- python3 -u $P \
+        > "$OUT/klkt.log" 2> "$OUT/klevels.log" || { echo "klevels trace failed"; tail "$OUT/klevels.log"; exit 1; }
+      for grp in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" FETCH_SIZE WRITE_SIZE; do
+        gn=$(echo "$grp" | tr ' ' '+')
+        timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/klpmc_$gn" -o run -- python3 -u $P \
+          > "$OUT/klpmc_$gn.log" 2>&1 || { echo "klevels pmc $grp failed"; tail "$OUT/klpmc_$gn.log"; exit 1; }
+      done
+      CAL=profiles/r06/gather_calib.json; [ -f "$OUT/gather_calib.json" ] && CAL="$OUT/gather_calib.json"
+      python3 tools/k22_level_table.py "$OUT" "$CAL" > "$OUT/k22_levels.txt" 2>&1 || { echo "level table failed"; cat "$OUT/k22_levels.txt"; exit 1; }
+      tail -8 "$OUT/k22_levels.txt" ;;
     probe)
       timeout -k 10 240 python3 -u $arg > "$OUT/probe_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-40).log" 2>&1 \
         || { echo "probe failed: $arg"; exit 1; } ;;
