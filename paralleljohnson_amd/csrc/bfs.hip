@@ -1074,6 +1074,30 @@ __global__ void reach_k(const int32_t* __restrict__ dist, i64 n, const Off* __re
     }
 }
 
+// Hub-first in-rows for the pull levels (option hub_first): key of in-edge k of row r =
+// (r << kb) | (2^kb - 1 - bucket(in-degree of its source u)), bucket = floor(8 log2(deg + 1))
+// capped at 2^kb - 1, so one stable radix sort of (key, u) lays every in-row out with its
+// highest-degree in-neighbours first (ties in file order). A pull probes a row in order and
+// stops at its first visited in-neighbour; the hubs are visited in the first levels.
+template <typename Off>
+__global__ void hub_first_keys_k(const Off* __restrict__ crow, const u32* __restrict__ ccol, i64 n, i64 nnz, int kb,
+                                 u32* __restrict__ key, u32* __restrict__ val) {
+    const u32 top = (1u << kb) - 1u;
+    for (i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += (i64)gridDim.x * blockDim.x) {
+        i64 lo = 0, hi = n;  // the row holding entry k: largest r with crow[r] <= k
+        while (hi - lo > 1) {
+            const i64 mid = (lo + hi) >> 1;
+            if ((i64)crow[mid] <= k) lo = mid;
+            else hi = mid;
+        }
+        const u32 u = ccol[k];
+        const u64 deg = (u64)(crow[u + 1] - crow[u]);
+        const u32 b = min(top, (u32)(8.0f * log2f((float)deg + 1.0f)));
+        key[k] = ((u32)lo << kb) | (top - b);
+        val[k] = u;
+    }
+}
+
 int edge_bits(i64 nnz) {
     int b = 1;
     while (b < 63 && ((u64)1 << b) <= (u64)nnz) ++b;
@@ -1091,6 +1115,8 @@ struct BfsWorkHolder {
     DevBuf<u64> fnew;   // frontier bitmap written by pull levels
     DevBuf<uint8_t> ctl;  // C[3] + S[2] + nmode[2]
     int64_t* host = nullptr;  // mapped pinned host words (see BfsArgs::host)
+    DevBuf<u32> ccol_hf;      // hub_first: the in-rows with their highest-degree in-neighbours first
+    bool hf_built = false;
     int32_t last_launches = 0;  // level launches the previous solve used: sizes the first batch
     ~BfsWorkHolder() {
         if (host) (void)hipHostFree(host);
@@ -1159,7 +1185,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     }
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.host), w.host, 0));
     Graph_d<Off> gd{static_cast<const Off*>(g.row_ptr()), g.col.p, static_cast<const Off*>(g.crow_ptr()),
-                    g.ccol_ptr()};
+                    (w.hf_built && g.hub_first) ? w.ccol_hf.p : g.ccol_ptr()};
 #if PJ_BFS_STAMPS
     static DevBuf<u64> stamps;
     stamps.ensure(64 * 64);
@@ -1256,6 +1282,28 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
 #endif
 }
 
+// the hub-first in-rows (once per graph, at the first solve that asks for them); graphs whose
+// row ids leave fewer than 3 key bits keep their file-order rows
+template <typename Off>
+void build_hub_first(Graph& g, BfsWorkHolder& w) {
+    int rb = 1;
+    while (rb < 40 && ((i64)1 << rb) < g.n + 1) ++rb;
+    const int kb = std::min(8, 32 - rb);
+    if (w.hf_built || g.nnz == 0 || kb < 3 || g.nnz >= ((i64)1 << 32)) return;
+    hipStream_t s = g.ctx->stream;
+    DevBuf<u32> key((size_t)g.nnz), kalt((size_t)g.nnz), vals((size_t)g.nnz), valt((size_t)g.nnz);
+    hub_first_keys_k<Off><<<grid_for(g.nnz, 256, (unsigned)g.ctx->cu_count * 16u), 256, 0, s>>>(
+        static_cast<const Off*>(g.crow_ptr()), g.ccol_ptr(), g.n, g.nnz, kb, key.p, vals.p);
+    PJ_LAUNCH_CHECK();
+    SortWs ws;
+    u32 *kr = nullptr, *vr = nullptr;
+    radix_sort_pairs<u32>(key.p, kalt.p, vals.p, valt.p, g.nnz, rb + kb, ws, s, &kr, &vr);
+    if (vr == vals.p) w.ccol_hf = std::move(vals);
+    else w.ccol_hf = std::move(valt);
+    PJ_HIP(hipStreamSynchronize(s));
+    w.hf_built = true;
+}
+
 void bfs_workspace(Graph& g) {
     const size_t n = (size_t)g.n;
     const size_t nwords = (n + 63) / 64;
@@ -1296,6 +1344,10 @@ void bfs_workspace(Graph& g) {
 
 void bfs_solve(Graph& g, i64 source) {
     bfs_workspace(g);
+    if (g.hub_first) {
+        if (g.off64) build_hub_first<u64>(g, *g.bfs_work);
+        else build_hub_first<u32>(g, *g.bfs_work);
+    }
     if (g.off64) bfs_run<u64>(g, *g.bfs_work, source);
     else bfs_run<u32>(g, *g.bfs_work, source);
 }

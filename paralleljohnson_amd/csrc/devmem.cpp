@@ -129,7 +129,12 @@ void* dev_alloc(size_t bytes) {
         void* q = c.take(bb, bi, bytes);
         // test hook: a cached slice handed out full of 0xFF, so that a buffer relying on the zeroed
         // pages of fresh driver memory shows up (tests/test_partition.py)
-        if (std::getenv("PJ_DEVMEM_POISON")) PJ_HIP(hipMemset(q, 0xFF, bytes));
+        // (a device-wide wait after it: the memset runs on the null stream, which does not order
+        // against libpj's non-blocking streams)
+        if (std::getenv("PJ_DEVMEM_POISON")) {
+            PJ_HIP(hipMemset(q, 0xFF, bytes));
+            PJ_HIP(hipDeviceSynchronize());
+        }
         return q;
     }
     const size_t bb_bytes = (bytes + SLACK - 1) / SLACK * SLACK + SLACK;

@@ -249,6 +249,7 @@ struct Graph {
     int batch_streams = 2; // weighted batches (pj_sssp_batch*): solves in flight at once, one stream each
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
     int bfs_small = 1;   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)
+    int hub_first = 0;   // BFS: pull levels probe a copy of the in-rows ordered highest-degree in-neighbour first
     int bfs_spare = 0;   // BFS: launches beyond the previous solve's count in the first batch (1 measured
                          // 2-3% slower on K22: the spare launch costs more than the occasional round trip)
     int max_levels = 0;  // debug: truncate the BFS after this many levels (0 = off)

@@ -92,8 +92,11 @@ def test_bfs_random_graphs(ctx, oracle, kind, direction, small):
         row, col, _ = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n)
         roots = [int(src[0]) if len(src) else 0, int(rng.integers(0, n)), n, -5]
         for r in roots:
-            d = g.sssp(r)
-            assert (d == oracle.bfs(row, col, r)).all(), (kind, direction, trial, r)
+            exp = oracle.bfs(row, col, r)
+            for hf in (0, 1):  # (file-order in-rows, then the hub-first copy the pull levels probe)
+                g.set_option("hub_first", hf)
+                d = g.sssp(r)
+                assert (d == exp).all(), (kind, direction, trial, r, hf)
         g.close()
 
 
@@ -157,7 +160,9 @@ def test_bfs_kronecker(ctx, oracle, scale):
         assert (d == exp).all()
         for direction in (1, 2, 0):  # push only, pull whenever possible, automatic
             g.set_option("direction", direction)
-            assert (g.sssp(int(r)) == exp).all(), direction
+            for hf in (1, 0):
+                g.set_option("hub_first", hf)
+                assert (g.sssp(int(r)) == exp).all(), (direction, hf)
         st = g.reach_stats()
         reached = exp < INF
         assert st["reached"] == reached.sum()
@@ -176,6 +181,12 @@ def test_bfs_kronecker_s22_full_size(ctx, oracle):
     assert (d == exp).all()
     st = g.stats()
     assert st["bu_levels"] > 0 and st["td_levels"] > 0  # direction switching exercised
+    # edges scanned (pj_stats): at least the frontier edges of the push levels, at most every
+    # reached edge once per level
+    assert 0 < st["scanned_edges"] <= (st["levels"] + 1) * int(np.diff(row)[exp < INF].sum())
+    for hf in (1, 0):  # pull levels over the hub-first in-rows, and back
+        g.set_option("hub_first", hf)
+        assert (g.sssp(r) == exp).all(), hf
     # push-only levels of millions of vertices overflow the per-block hub staging (the
     # overflow path once lost hubs in about 1 of 50 such solves), with and without the
     # one-workgroup small levels
