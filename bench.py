@@ -717,6 +717,23 @@ def measured_traffic(args):
     return {"bytes": tj["hbm_bytes_per_sssp"], "table": tj, "path": os.path.relpath(path, ROOT)}
 
 
+def gather_ceiling(probes_per_solve, t_solve):
+    """The probes' rate against the chip's random-gather ceiling, measured by the FETCH_SIZE
+    calibration (profiles/r06/gather_calib.json: random 4-byte words from a 4 GiB table, each
+    a 128-byte memory-side request): the bound of a latency- and line-bound kernel whose bytes
+    fraction says little (a 4-byte probe moves a 128-byte line)."""
+    path = os.path.join(ROOT, "profiles", "r06", "gather_calib.json")
+    if not probes_per_solve or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        cal = json.load(f)
+    ceil = cal["random_dword_gathers_per_s"]
+    rate = probes_per_solve / t_solve
+    return {"probe_rate_per_s": round(rate), "probe_ceiling_per_s": round(ceil),
+            "probe_frac": round(rate / ceil, 4),
+            "probe_ceiling_source": "profiles/r06/gather_calib.json (tools/calib/gather_calib.hip, cal_dwords_k)"}
+
+
 def line(main_res, wl, value, mean_ms, work, traffic, tts_s, tts_phases, cpu, secondary, n_vertices, nnz,
          t_kernel, world, args):
     """The one JSON line of the run (rank 0)."""
@@ -740,6 +757,7 @@ def line(main_res, wl, value, mean_ms, work, traffic, tts_s, tts_phases, cpu, se
         "scanned_edges_per_sssp": round(work["scanned"] / solves),
         "probes_per_sssp": round(work["probes"] / solves),
         "frac_model_8d": round(work["model_8d"] / HBM_PEAK_GBS, 4),
+        **gather_ceiling(work["probes"] / solves, t_solve),
         "model_8d": "SURVEY.md §8d: 4N + n_r(12 + 2*O) + m_r(8 + 4*weighted), every reached edge read; the solve "
                     "scans a fraction of them (a pull stops a row at its first useless weight), so this figure can "
                     "exceed 1 and bounds nothing",

@@ -1115,8 +1115,6 @@ struct BfsWorkHolder {
     DevBuf<u64> fnew;   // frontier bitmap written by pull levels
     DevBuf<uint8_t> ctl;  // C[3] + S[2] + nmode[2]
     int64_t* host = nullptr;  // mapped pinned host words (see BfsArgs::host)
-    DevBuf<u32> ccol_hf;      // hub_first: the in-rows with their highest-degree in-neighbours first
-    bool hf_built = false;
     int32_t last_launches = 0;  // level launches the previous solve used: sizes the first batch
     ~BfsWorkHolder() {
         if (host) (void)hipHostFree(host);
@@ -1185,7 +1183,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     }
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.host), w.host, 0));
     Graph_d<Off> gd{static_cast<const Off*>(g.row_ptr()), g.col.p, static_cast<const Off*>(g.crow_ptr()),
-                    (w.hf_built && g.hub_first) ? w.ccol_hf.p : g.ccol_ptr()};
+                    pull_ccol(g)};
 #if PJ_BFS_STAMPS
     static DevBuf<u64> stamps;
     stamps.ensure(64 * 64);
@@ -1285,11 +1283,11 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
 // the hub-first in-rows (once per graph, at the first solve that asks for them); graphs whose
 // row ids leave fewer than 3 key bits keep their file-order rows
 template <typename Off>
-void build_hub_first(Graph& g, BfsWorkHolder& w) {
+void build_hub_first(Graph& g) {
     int rb = 1;
     while (rb < 40 && ((i64)1 << rb) < g.n + 1) ++rb;
     const int kb = std::min(8, 32 - rb);
-    if (w.hf_built || g.nnz == 0 || kb < 3 || g.nnz >= ((i64)1 << 32)) return;
+    if (g.ccol_hf.p || g.nnz == 0 || kb < 3 || g.nnz >= ((i64)1 << 32)) return;
     hipStream_t s = g.ctx->stream;
     DevBuf<u32> key((size_t)g.nnz), kalt((size_t)g.nnz), vals((size_t)g.nnz), valt((size_t)g.nnz);
     hub_first_keys_k<Off><<<grid_for(g.nnz, 256, (unsigned)g.ctx->cu_count * 16u), 256, 0, s>>>(
@@ -1298,10 +1296,9 @@ void build_hub_first(Graph& g, BfsWorkHolder& w) {
     SortWs ws;
     u32 *kr = nullptr, *vr = nullptr;
     radix_sort_pairs<u32>(key.p, kalt.p, vals.p, valt.p, g.nnz, rb + kb, ws, s, &kr, &vr);
-    if (vr == vals.p) w.ccol_hf = std::move(vals);
-    else w.ccol_hf = std::move(valt);
+    if (vr == vals.p) g.ccol_hf = std::move(vals);
+    else g.ccol_hf = std::move(valt);
     PJ_HIP(hipStreamSynchronize(s));
-    w.hf_built = true;
 }
 
 void bfs_workspace(Graph& g) {
@@ -1342,12 +1339,15 @@ void bfs_workspace(Graph& g) {
 
 }  // namespace
 
+const u32* pull_ccol(Graph& g) {
+    if (!g.hub_first) return g.ccol_ptr();
+    if (g.off64) build_hub_first<u64>(g);
+    else build_hub_first<u32>(g);
+    return g.ccol_hf.p ? g.ccol_hf.p : g.ccol_ptr();
+}
+
 void bfs_solve(Graph& g, i64 source) {
     bfs_workspace(g);
-    if (g.hub_first) {
-        if (g.off64) build_hub_first<u64>(g, *g.bfs_work);
-        else build_hub_first<u32>(g, *g.bfs_work);
-    }
     if (g.off64) bfs_run<u64>(g, *g.bfs_work, source);
     else bfs_run<u32>(g, *g.bfs_work, source);
 }

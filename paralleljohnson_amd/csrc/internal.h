@@ -194,6 +194,7 @@ struct Graph {
     DevBuf<u64> row64, crow64;
     DevBuf<u32> col, ccol;  // ccol/crow*: CSC (in-edges) for pull steps; alias CSR when symmetric
     DevBuf<u32> w;          // CSR-aligned weights (weighted graphs)
+    DevBuf<u32> ccol_hf;    // hub_first: the in-rows ordered highest-degree in-neighbour first (pull_ccol)
 
     // per-solve workspace (lazily sized)
     DevBuf<int32_t> dist;
@@ -315,6 +316,9 @@ void generate_kronecker_device(Ctx& ctx, int scale, int edgefactor, uint64_t see
 
 // solvers
 void bfs_solve(Graph& g, i64 source);
+// the in-rows the pull levels probe (BFS and MS-BFS): with the hub_first option a copy ordered
+// highest in-degree in-neighbour first, built on first use; else the CSC (the CSR if symmetric)
+const u32* pull_ccol(Graph& g);
 i64 relabeled_id(const Relabeled& R, i64 v, hipStream_t s);  // relabel.hip: inv[v]
 void delta_solve(Graph& g, i64 source);
 // g.dist in input ids after a delta_solve (a no-op when it already is): every reader of g.dist

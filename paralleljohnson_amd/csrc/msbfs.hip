@@ -613,7 +613,7 @@ static void ms_pass(Graph& g, MsSlot& w, const int64_t* sources, int ns, double*
     hipStream_t s = w.s;
     const i64 n = g.n;
     const Off* crow = static_cast<const Off*>(g.crow_ptr());
-    const u32* ccol = g.ccol_ptr();
+    const u32* ccol = pull_ccol(g);
     PJ_HIP(hipMemcpyAsync(w.src.p, sources, sizeof(int64_t) * (size_t)ns, hipMemcpyHostToDevice, s));
     int64_t* host_dev = nullptr;
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&host_dev), w.host, 0));
@@ -756,6 +756,7 @@ static void ms_slot_alloc(Graph& g, MsSlot& sl, int W, int lcap, bool own_stream
 }
 
 void msbfs_each(Graph& g, const int64_t* sources, int n_src, const MsPassFn& on_pass) {
+    (void)pull_ccol(g);  // (built here, once, before the slots' host threads read it)
     const int W = ms_words(g, n_src);
     const int per = 64 * W;
     const int npass = (n_src + per - 1) / per;

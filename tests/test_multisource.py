@@ -22,11 +22,14 @@ def ms1024_sources(row, k=1024):
     return np.nonzero(np.diff(row) >= 1)[0][:k]
 
 
-def test_ms1024_full_size(ctx, oracle):
+@pytest.mark.parametrize("hub_first", [0, 1])
+def test_ms1024_full_size(ctx, oracle, hub_first):
     """configs[4] exactly as bench.py times it: the web-Google-shaped graph (916,428 ids,
     5,105,039 edges, seed 1), the 1024 smallest ids with out-degree >= 1, the default
-    pass width (512 sources per pass); every one of the 1024 rows equals the oracle BFS."""
+    pass width (512 sources per pass); every one of the 1024 rows equals the oracle BFS.
+    hub_first = 1: the pull levels probe the in-rows ordered highest in-degree first."""
     g = ctx.generate_webgraph(916428, 5105039, 1)
+    g.set_option("hub_first", hub_first)
     row, col, _ = g.get_csr()
     col = col.view(np.uint32)
     sources = ms1024_sources(row)

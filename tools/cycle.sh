@@ -14,7 +14,7 @@
 #                 cycle's calib step if it ran, else profiles/r06/gather_calib.json)
 #   klevels[:opts] per-level table of configs[1] (K22 BFS): tools/k22_levels.py under a kernel trace and --pmc
 #                 passes -> k22_levels.txt (tools/k22_level_table.py); opts = libpj options k=v~k=v
-#   probe:<cmd>   any python command line under a 240 s limit (e.g. probe:tools/stats_probe.py 26 3)
+#   probe:<cmd>   any python command line under a 240 s limit (e.g. probe:tools/probe_ms.py)
 #   vtests:<v>:<pytest args>  -m gpu tests under the libpj build variant <v>
 #   ktp:<cmd>     rocprofv3 kernel trace + stats of any python command line -> kt_<name>/
 #   vktp:<v>:<cmd>  the same under the libpj build variant <v> -> kt_<v>_<name>/

@@ -29,7 +29,8 @@ for r in [roots[0]] + roots:  # (the first solve also prepares the solver: its k
     g.sssp(r, copy=False)
     st = g.stats()
     rs = g.reach_stats()  # (the gather to input ids and the reach pass: not solve kernels, excluded by name)
-    per.append(dict(root=r, **st, reached=rs["reached"], reached_edges=rs["reached_edges"]))
+    st.update(root=r, reached=rs["reached"], reached_edges=rs["reached_edges"])
+    per.append(st)
 res = {"build_id": pj.build_id(), "scale": scale, "weighted": weighted, "n": g.n, "nnz": g.nnz, "roots": roots,
        "solves": per,
        "note": "solves[0] repeats roots[0] and carries the solver preparation; every solve's v2_init_k starts it"}
