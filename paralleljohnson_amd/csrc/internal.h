@@ -35,7 +35,8 @@ void set_error(const std::string& msg);
         hipError_t e_ = (expr);                                                          \
         if (e_ != hipSuccess)                                                            \
             throw ::pj::Error(e_ == hipErrorOutOfMemory ? PJ_ERR_OOM : PJ_ERR_HIP,       \
-                              std::string(#expr) + ": " + hipGetErrorString(e_));        \
+                              std::string(#expr) + ": " + hipGetErrorString(e_) +        \
+                                  " (" __FILE__ ":" + std::to_string(__LINE__) + ")");   \
     } while (0)
 
 #define PJ_LAUNCH_CHECK() PJ_HIP(hipGetLastError())
@@ -250,7 +251,10 @@ struct Graph {
     int batch_streams = 2; // weighted batches (pj_sssp_batch*): solves in flight at once, one stream each
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
     int bfs_small = 1;   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)
-    int hub_first = 0;   // BFS: pull levels probe a copy of the in-rows ordered highest-degree in-neighbour first
+    int hub_first = 1;   // BFS / MS-BFS: pull levels probe a copy of the in-rows ordered highest-degree in-neighbour
+                         // first (built at the first solve; K22 0.2305 -> 0.1991 ms median kernel time, pull
+                         // probes 21.8M -> 16.2M per 4 roots; web-Google and MS1024 equal or slightly faster,
+                         // profiles/r06/bfs_hub_first_r6e.txt)
     int bfs_spare = 0;   // BFS: launches beyond the previous solve's count in the first batch (1 measured
                          // 2-3% slower on K22: the spare launch costs more than the occasional round trip)
     int max_levels = 0;  // debug: truncate the BFS after this many levels (0 = off)

@@ -18,6 +18,7 @@
 
 struct pj_multi {
     int world = 0, transport = PJ_TRANSPORT_AUTO, layout = -1, weighted = 0;
+    int ndev = 1;                  // visible GPUs (rank r runs on GPU r mod ndev)
     int64_t n = 0;
     std::vector<pj_ctx*> ctxs;
     std::vector<pj_comm*> comms;   // partitioned layout only
@@ -65,6 +66,40 @@ int per_rank(int world, F&& fn) {
     if (first < 0) return PJ_OK;
     pj::set_error("rank " + std::to_string(first) + ": " + msgs[(size_t)first]);
     return rcs[(size_t)first];
+}
+
+// fn(r) for every rank of a replicated batch: one host thread per GPU, running the ranks that
+// share it (world > visible GPUs) one after another. Each rank's batch fills the GPU by itself
+// (its solves run on their own streams), so several host threads driving one GPU's batches
+// gain nothing; with three ranks' batches driven at once on one GPU the suite saw intermittent
+// illegal-address faults (round 6, test_multi_handle[3]; not reproduced in isolation nor with
+// kernels serialized, cause not found), which this ordering also rules out. One rank per GPU
+// (the product case) runs exactly as per_rank.
+template <typename F>
+int per_device(const pj_multi* m, F&& fn) {
+    const int nd = std::max(1, std::min(m->ndev, m->world));
+    std::vector<int> bad((size_t)nd, -1);
+    const int rc = per_rank(nd, [&](int d) {
+        for (int r = d; r < m->world; r += nd) {
+            const int e = fn(r);
+            if (e != PJ_OK) {
+                bad[(size_t)d] = r;
+                return e;
+            }
+        }
+        return (int)PJ_OK;
+    });
+    if (rc != PJ_OK) {  // (per_rank named the failing thread; name the rank instead)
+        std::string msg = pj_last_error();
+        const size_t colon = msg.find(": ");
+        if (msg.rfind("rank ", 0) == 0 && colon != std::string::npos) msg = msg.substr(colon + 2);
+        for (int d = 0; d < nd; ++d)
+            if (bad[(size_t)d] >= 0) {
+                pj::set_error("rank " + std::to_string(bad[(size_t)d]) + ": " + msg);
+                break;
+            }
+    }
+    return rc;
 }
 
 int make_comms(pj_multi* m) {
@@ -147,6 +182,7 @@ int pj_multi_create(int n_gpus, int transport, pj_multi** out) {
     }
     auto* m = new pj_multi;
     m->world = n_gpus;
+    m->ndev = ndev;
     m->transport = transport;
     m->ctxs.assign((size_t)n_gpus, nullptr);
     for (int r = 0; r < n_gpus; ++r) {
@@ -321,7 +357,7 @@ int pj_multi_sssp_batch_write(pj_multi* m, const int64_t* sources, int n_src, co
     }
     // replicated: rank r takes sources r, r + P, ... and writes their files
     std::vector<double> kms((size_t)P, 0.0);
-    const int rc = per_rank(P, [&](int r) {
+    const int rc = per_device(m, [&](int r) {
         std::vector<int64_t> mine;
         std::vector<const char*> pp;
         for (int i = r; i < n_src; i += P) {
@@ -348,7 +384,7 @@ int pj_multi_sssp_batch(pj_multi* m, const int64_t* sources, int n_src, int32_t*
         return PJ_OK;
     }
     const int P = m->world;
-    return per_rank(P, [&](int r) {
+    return per_device(m, [&](int r) {
         std::vector<int64_t> mine;
         for (int i = r; i < n_src; i += P) mine.push_back(sources[i]);
         if (mine.empty()) return (int)PJ_OK;

@@ -76,18 +76,19 @@ for st in "${LIST[@]}"; do
       cat "$OUT/pmc_table.txt" ;;
     klevels)
       P="tools/k22_levels.py ${KL_ROOTS:-4} $arg"
-      timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/klkt" -o run -- python3 -u $P \
-        > "$OUT/klkt.log" 2> "$OUT/klevels.log" || { echo "klevels trace failed"; tail "$OUT/klevels.log"; exit 1; }
+      KT=$(echo "$arg" | tr -c 'A-Za-z0-9_\n' '_'); KO="$OUT/kl${KT:+_$KT}"; mkdir -p "$KO"
+      timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$KO/klkt" -o run -- python3 -u $P \
+        > "$KO/klkt.log" 2> "$KO/klevels.log" || { echo "klevels trace failed"; tail "$KO/klevels.log"; exit 1; }
       for grp in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" FETCH_SIZE WRITE_SIZE; do
         gn=$(echo "$grp" | tr ' ' '+')
-        timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/klpmc_$gn" -o run -- python3 -u $P \
-          > "$OUT/klpmc_$gn.log" 2>&1 || { echo "klevels pmc $grp failed"; tail "$OUT/klpmc_$gn.log"; exit 1; }
+        timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$KO/klpmc_$gn" -o run -- python3 -u $P \
+          > "$KO/klpmc_$gn.log" 2>&1 || { echo "klevels pmc $grp failed"; tail "$KO/klpmc_$gn.log"; exit 1; }
       done
       CAL=profiles/r06/gather_calib.json; [ -f "$OUT/gather_calib.json" ] && CAL="$OUT/gather_calib.json"
-      python3 tools/k22_level_table.py "$OUT" "$CAL" > "$OUT/k22_levels.txt" 2>&1 || { echo "level table failed"; cat "$OUT/k22_levels.txt"; exit 1; }
-      tail -8 "$OUT/k22_levels.txt" ;;
+      python3 tools/k22_level_table.py "$KO" "$CAL" > "$KO/k22_levels.txt" 2>&1 || { echo "level table failed"; cat "$KO/k22_levels.txt"; exit 1; }
+      tail -8 "$KO/k22_levels.txt" ;;
     probe)
-      timeout -k 10 240 python3 -u $arg > "$OUT/probe_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-40).log" 2>&1 \
+      timeout -k 10 240 python3 -u $arg > "$OUT/probe_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-24)_$(echo "$arg" | md5sum | cut -c1-6).log" 2>&1 \
         || { echo "probe failed: $arg"; exit 1; } ;;
     vtests)
       v=${arg%%:*}; targs=${arg#*:}
