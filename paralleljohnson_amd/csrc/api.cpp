@@ -887,6 +887,7 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     Graph& g = pg->g;
     std::string k(key);
     if (k == "alpha" && value > 0) g.alpha = value;
+    else if (k == "pull_vertex" && value >= 0) g.pull_vertex = value;
     else if (k == "beta" && value > 0) g.beta = value;
     else if (k == "delta" && value >= 0) g.delta = value;
     else if (k == "pull_factor" && value >= 0) g.pull_factor = value;

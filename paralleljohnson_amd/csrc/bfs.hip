@@ -92,13 +92,16 @@ struct LevelState {
     int32_t level; // last level computed
     double m_u;    // Beamer: in-edges of unvisited vertices
     u64 prev_found;
-    u64 pad[5];
+    double n_u;    // unvisited vertices with an edge (the pull level's candidates: pull_vertex rule)
+    u64 pad[4];
 };
 
 struct BfsArgs {
     i64 n, nwords;
     int eb;  // edge bits of the packed hub counter
     double alpha, beta;
+    double pv;  // pull_vertex: push -> pull also when the frontier's out-edges exceed pv x the unvisited
+                // vertices (0 = Beamer's rule alone)
     int force;  // 0 auto, 1 push only, 2 pull whenever possible
     int small;  // one-workgroup levels for small push frontiers
     int32_t max_levels;  // debug: stop after this many levels
@@ -143,7 +146,7 @@ struct Graph_d {
 struct Decision {
     int32_t L;  // the level this launch computes
     int32_t mode, vsel, prev_mode;
-    double m_u;
+    double m_u, n_u;
     u64 found;
     u64 nseg[NQS];
     u64 nh, he, mq;
@@ -163,6 +166,7 @@ __device__ __forceinline__ int decide(const BfsArgs& a, int32_t li, Decision& d)
     d.prev_mode = ps.mode;
     d.vsel = ps.vsel;
     d.m_u = ps.m_u;
+    d.n_u = ps.n_u;
     d.found = ps.prev_found;
     d.nh = d.he = d.mq = 0;
     if (ps.done) return 0;
@@ -186,11 +190,14 @@ __device__ __forceinline__ int decide(const BfsArgs& a, int32_t li, Decision& d)
     d.mq = mq;
     d.found = fd;
     d.m_u = ps.m_u - (double)in;
+    d.n_u = ps.n_u - (double)fd;
     if (fz == 0 || L + 1 >= INT_INF || L >= a.max_levels) return 1;
     if (a.force == 1) d.mode = 0;
     else if (a.force == 2) d.mode = 1;
     else if (d.mode == 0) {
-        if ((double)mq > d.m_u / a.alpha) d.mode = 1;
+        // Beamer's rule (the pull's cost as every unvisited in-edge), or with hub-first in-rows,
+        // where most unvisited vertices stop at their first probe, the unvisited vertices
+        if ((double)mq > d.m_u / a.alpha || (a.pv > 0.0 && (double)mq > a.pv * d.n_u)) d.mode = 1;
     } else if ((double)fd < (double)a.n / a.beta && fd < ps.prev_found) {
         d.mode = 0;
     }
@@ -410,7 +417,7 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
     }
     u64* vis = a.vis[d.vsel];
     int32_t L = d.L;
-    double m_u = d.m_u;
+    double m_u = d.m_u, n_u = d.n_u;
     u64 fprev = d.found, nlev = 0;
     for (;;) {
         __syncthreads();
@@ -513,6 +520,7 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
             F = NF;
             fprev = f;
             m_u = m_u2;
+            n_u -= (double)f;
             L = L2;
             continue;
         }
@@ -525,6 +533,7 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
                 s.vsel = d.vsel;
                 s.level = L2;
                 s.m_u = m_u2;
+                s.n_u = n_u - (double)f;
                 s.prev_found = f;
                 a.host[1] = (int64_t)a.nmode[0];
                 a.host[2] = (int64_t)a.nmode[1];
@@ -588,6 +597,7 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
             s.vsel = d.vsel;
             s.level = L;
             s.m_u = m_u;
+            s.n_u = n_u;
             s.prev_found = fprev;
         }
         return;
@@ -647,6 +657,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
             s.vsel = (go && d.mode == 1) ? 1 - d.vsel : d.vsel;
             s.level = L;
             s.m_u = d.m_u;
+            s.n_u = d.n_u;
             s.prev_found = d.found;
             if (go) a.nmode[d.mode] += 1;
             if (dec == 1) {
@@ -987,7 +998,7 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
 // C[2] / state S[1] describe the one-vertex frontier.
 template <typename Off>
 __global__ __launch_bounds__(TB) void bfs_init_k(BfsArgs a, Graph_d<Off> g, const u64* __restrict__ zmask, i64 s,
-                                                 double nnz) {
+                                                 double nnz, double n_live) {
     const i64 n4 = a.n / 4;
     const i64 tid = (i64)blockIdx.x * TB + threadIdx.x, nth = (i64)gridDim.x * TB;
     int4* d4 = reinterpret_cast<int4*>(a.dist);
@@ -1030,6 +1041,7 @@ __global__ __launch_bounds__(TB) void bfs_init_k(BfsArgs a, Graph_d<Off> g, cons
         st = LevelState{};
         st.level = -1;
         st.m_u = nnz;
+        st.n_u = n_live;
         a.nmode[0] = a.nmode[1] = 0;
         *a.wtot = 0;
         a.host[0] = -1;
@@ -1044,7 +1056,8 @@ __global__ __launch_bounds__(TB) void bfs_init_k(BfsArgs a, Graph_d<Off> g, cons
 // out-edges may not: it would pose as a parent without ever being reached.)
 template <typename Off>
 __global__ void zmask_k(const Off* __restrict__ row, const Off* __restrict__ crow, i64 n, i64 nwords,
-                        u64* __restrict__ z) {
+                        u64* __restrict__ z, u64* __restrict__ nz) {
+    u64 c = 0;
     for (i64 w = (i64)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (i64)gridDim.x * blockDim.x) {
         u64 m = 0;
         for (int j = 0; j < 64; ++j) {
@@ -1052,7 +1065,10 @@ __global__ void zmask_k(const Off* __restrict__ row, const Off* __restrict__ cro
             if (v < n && crow[v + 1] == crow[v] && row[v + 1] == row[v]) m |= 1ull << j;
         }
         z[w] = m;
+        c += (u64)__popcll(m);
     }
+    c = wave_sum(c);
+    if (lane_id() == 0 && c) atomicAdd(nz, c);  // (isolated vertices)
 }
 
 template <typename Off>
@@ -1116,6 +1132,7 @@ struct BfsWorkHolder {
     DevBuf<uint8_t> ctl;  // C[3] + S[2] + nmode[2]
     int64_t* host = nullptr;  // mapped pinned host words (see BfsArgs::host)
     int32_t last_launches = 0;  // level launches the previous solve used: sizes the first batch
+    i64 n_live = 0;             // vertices with an edge (not in zmask)
     ~BfsWorkHolder() {
         if (host) (void)hipHostFree(host);
     }
@@ -1157,6 +1174,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     a.nwords = nwords;
     a.eb = edge_bits(g.nnz);
     a.alpha = g.alpha;
+    a.pv = g.pull_vertex;
     a.beta = g.beta;
     a.force = g.force_mode;
     a.small = g.bfs_small;
@@ -1207,7 +1225,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
         // clear it here, or the first spin_wait sees it and ends the solve after one batch
         *(volatile int64_t*)w.host = -1;
         bfs_init_k<Off><<<grid_for(std::max(n / 4, nwords), TB, (unsigned)ctx.cu_count * 4u), TB, 0, s>>>(
-            a, gd, w.zmask.p, source, (double)g.nnz);
+            a, gd, w.zmask.p, source, (double)g.nnz, (double)w.n_live);
         PJ_LAUNCH_CHECK();
         int32_t li = 0;  // launch index (a launch runs one level, or several small ones)
         // first batch: the previous solve's launches, so a repeated solve on the same graph
@@ -1322,16 +1340,21 @@ void bfs_workspace(Graph& g) {
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.host), 8 * sizeof(int64_t), hipHostMallocMapped));
     if (nwords) {
         hipStream_t s = g.ctx->stream;
+        DevBuf<u64> nz(1);
+        PJ_HIP(hipMemsetAsync(nz.p, 0, sizeof(u64), s));
         if (g.off64)
             zmask_k<u64><<<grid_for((i64)nwords, 256), 256, 0, s>>>(static_cast<const u64*>(g.row_ptr()),
                                                                     static_cast<const u64*>(g.crow_ptr()), g.n,
-                                                                    (i64)nwords, w.zmask.p);
+                                                                    (i64)nwords, w.zmask.p, nz.p);
         else
             zmask_k<u32><<<grid_for((i64)nwords, 256), 256, 0, s>>>(static_cast<const u32*>(g.row_ptr()),
                                                                     static_cast<const u32*>(g.crow_ptr()), g.n,
-                                                                    (i64)nwords, w.zmask.p);
+                                                                    (i64)nwords, w.zmask.p, nz.p);
         PJ_LAUNCH_CHECK();
+        u64 iso = 0;
+        PJ_HIP(hipMemcpyAsync(&iso, nz.p, sizeof(u64), hipMemcpyDeviceToHost, s));
         PJ_HIP(hipStreamSynchronize(s));
+        w.n_live = g.n - (i64)iso;
     }
     if (!g.ev0) PJ_HIP(hipEventCreate(&g.ev0));
     if (!g.ev1) PJ_HIP(hipEventCreate(&g.ev1));

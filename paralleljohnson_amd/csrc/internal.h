@@ -216,6 +216,8 @@ struct Graph {
 
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;
+    double pull_vertex = 0.0;  // BFS: push -> pull also when the frontier's out-edges > pull_vertex x the
+                               // unvisited vertices (0 = Beamer's rule alone)
     double pull_factor = 4.0;  // symmetric: pull a band's heavy edges when the heavy edges of unsettled
                                // vertices < pull_factor x the members' heavy edges (0 = never)
     double defer_heavy = 0.002; // v2, symmetric: a heavy push of members holding >= defer_heavy x nnz heavy
