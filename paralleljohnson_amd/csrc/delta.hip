@@ -1343,11 +1343,9 @@ __device__ __forceinline__ void v2_pull_light_body(const V2Args& a, const Off* _
             int32_t cur = d0;
             Off e = k;
             if (act) e = (a.ltail || ls <= V2_PLMAX) ? k + (Off)ls : k;  // long rows: v2_pull_long_body
-#ifdef PJ_V2_PWIDE  // (measurement: rows longer than PJ_V2_PWIDE light edges go wave-wide at once)
-            const Off lim = (e - k > (Off)PJ_V2_PWIDE) ? k : (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
-#else
+            // (round 6: rows above 32 or 64 light edges sent wave-wide at once instead of walked
+            // PSERIAL edges by their lane first measured 23% slower, profiles/r06/pwide_ab_r6g.txt)
             const Off lim = (e - k > (Off)PSERIAL) ? k + (Off)PSERIAL : e;
-#endif
             bool go = act && k < lim, done = !act || k >= e;
             while (__ballot(go)) {
                 // (counted with ballots in the wave-uniform loop: a start-of-row register held
