@@ -238,7 +238,9 @@ int pj_reach_stats(pj_graph* g, pj_stats* out);
  * delta-stepping (0 = automatic: c(n) x mean weight / mean out-degree, c(n) =
  * 0.1875 log2(n) - 1.875 within [2, 3.5], swept on Kronecker s22-s26), direction (0 auto, 1 push, 2 pull),
  * bfs_small (one-workgroup levels for small frontiers, 0/1), hub_first (BFS pull levels
- * probe in-rows ordered highest-degree in-neighbour first, 0/1, default 1), batch_streams
+ * probe in-rows ordered highest-degree in-neighbour first, 0/1, default 1), pull_vertex
+ * (BFS: push -> pull also when the frontier's out-edges exceed pull_vertex x the unvisited
+ * vertices, default 2, 0 = Beamer's rule alone), batch_streams
  * (weighted batches: solves in flight, 1-8), defer_heavy (a heavy push of members
  * holding >= defer_heavy x nnz heavy edges relaxes the next band's part only and
  * leaves the rest to the next heavy step; 0 = off, default 0.002) and the batch /

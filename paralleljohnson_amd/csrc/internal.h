@@ -216,8 +216,12 @@ struct Graph {
 
     // options
     double alpha = 14.0, beta = 24.0, delta = 0.0;
-    double pull_vertex = 0.0;  // BFS: push -> pull also when the frontier's out-edges > pull_vertex x the
-                               // unvisited vertices (0 = Beamer's rule alone)
+    double pull_vertex = 2.0;  // BFS: push -> pull also when the frontier's out-edges > pull_vertex x the
+                               // unvisited vertices (0 = Beamer's rule alone). With hub-first in-rows a
+                               // pull probes ~2 in-edges per unvisited vertex, a push pays an atomic per
+                               // frontier edge: K22 bench roots 0.2224 -> 0.2007 ms mean kernel time
+                               // (1: 0.2006, 0.5: 0.2095, 4: 0.2227; web-Google equal at 1),
+                               // profiles/r06/bfs_pull_vertex_r6h.txt
     double pull_factor = 4.0;  // symmetric: pull a band's heavy edges when the heavy edges of unsettled
                                // vertices < pull_factor x the members' heavy edges (0 = never)
     double defer_heavy = 0.002; // v2, symmetric: a heavy push of members holding >= defer_heavy x nnz heavy
