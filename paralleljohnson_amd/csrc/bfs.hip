@@ -1131,6 +1131,7 @@ struct BfsWorkHolder {
     DevBuf<u64> fnew;   // frontier bitmap written by pull levels
     DevBuf<uint8_t> ctl;  // C[3] + S[2] + nmode[2]
     int64_t* host = nullptr;  // mapped pinned host words (see BfsArgs::host)
+    int64_t* host_dev = nullptr;  // their device address
     int32_t last_launches = 0;  // level launches the previous solve used: sizes the first batch
     i64 n_live = 0;             // vertices with an edge (not in zmask)
     ~BfsWorkHolder() {
@@ -1199,7 +1200,7 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
         PJ_HIP(hipMemsetAsync(llog.p, 0xFF, 6 * 64 * sizeof(u64), s));
         a.llog = llog.p;
     }
-    PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.host), w.host, 0));
+    a.host = w.host_dev;
     Graph_d<Off> gd{static_cast<const Off*>(g.row_ptr()), g.col.p, static_cast<const Off*>(g.crow_ptr()),
                     pull_ccol(g)};
 #if PJ_BFS_STAMPS
@@ -1338,6 +1339,7 @@ void bfs_workspace(Graph& g) {
     w.fnew.alloc(nwords ? nwords : 1);
     w.ctl.alloc(3 * sizeof(LevelCnt) + 2 * sizeof(LevelState) + 3 * sizeof(u64));  // (+ nmode[2], wtot)
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.host), 8 * sizeof(int64_t), hipHostMallocMapped));
+    PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&w.host_dev), w.host, 0));
     if (nwords) {
         hipStream_t s = g.ctx->stream;
         DevBuf<u64> nz(1);
