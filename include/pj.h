@@ -544,7 +544,10 @@ int pj_part_bfs_group(int world, pj_part* const* parts, pj_comm* const* comms, i
 int pj_part_gather_dist(pj_part* p, pj_comm* comm, int32_t* dist_out);
 
 /* Weighted partitioned solve (delta-stepping, wpart.hip + engine.cpp);
- * delta <= 0 picks the single-GPU default. */
+ * delta <= 0 picks the single-GPU default. At world 1 (the rank holds the whole
+ * graph) the solve is the single-GPU solver's (delta.hip v2 on the rank's rows) unless
+ * option "single_gpu" is 0; the pj_part_stats light-round and band counts are then
+ * v2's. */
 int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st);
 /* pj_wpart_set_option keys: "tail_frac" (switch to the tail threshold once the edges of
  * the vertices not settled yet, over all ranks, drop below tail_frac x all edges; 0 = off;
@@ -559,6 +562,7 @@ int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj
  * count their frontier per workgroup the pull no longer pays, profiles/r03/wpart_light_pull_r3ad.txt)
  * and "tail_light_pull" (the same rule in the tail's bands, independent of light_pull, the
  * frontier map then 16-bit; 0 = push; default 3). Every rank must use the same values.
+ * "single_gpu" (0/1, default 1: the world-1 solve runs delta.hip's v2, see pj_wpart_delta).
  * "queue_shard" (this rank only, any time between steps): the claim queue's shard
  * capacity in pairs from now on, >= 1 (64 shards; it still grows when a round
  * overflows it: tests use small values to run that path). */

@@ -1823,6 +1823,7 @@ int pj_wpart_set_option(pj_wpart* p, const char* key, double value) {
     else if (k == "pull_factor" && value >= 0) wpart_pull_factor(P) = value;
     else if (k == "light_pull" && value >= 0) wpart_light_pull(P) = value;
     else if (k == "tail_light_pull" && value >= 0) wpart_tail_light_pull(P) = value;
+    else if (k == "single_gpu" && (value == 0 || value == 1)) wpart_single_gpu(P) = (int)value;
     else if (k == "queue_shard" && value >= 1 && value <= 1e9)
         return guarded([&] {
             bind(wpart_ctx(P));
@@ -1836,8 +1837,10 @@ int pj_wpart_set_option(pj_wpart* p, const char* key, double value) {
 int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj_part_stats* st) {
     if (!p || !comm) return arg_error("pj_wpart_delta: bad argument");
     return guarded([&] {
-        bind(wpart_ctx(*reinterpret_cast<WPart*>(p)));
-        delta_engine(wpart_steps(*reinterpret_cast<WPart*>(p)), *comm->c, source, delta, st);
+        WPart& P = *reinterpret_cast<WPart*>(p);
+        bind(wpart_ctx(P));
+        if (wpart_single(P) && comm->c->world == 1) wpart_solve_single(P, source, delta, st);
+        else delta_engine(wpart_steps(P), *comm->c, source, delta, st);
         return (int)PJ_OK;
     });
 }

@@ -206,6 +206,10 @@ BfsParams& part_params(Part& p);
 const Ctx& part_ctx(const Part& p);
 const Ctx& wpart_ctx(const WPart& p);
 int wpart_world(const WPart& p);
+// world 1 (option "single_gpu", default on): the solve runs delta.hip's single-GPU solver
+bool wpart_single(const WPart& p);
+int& wpart_single_gpu(WPart& p);
+void wpart_solve_single(WPart& p, i64 source, int32_t delta, pj_part_stats* st);
 bool wpart_pending(const WPart& p);
 void wpart_set_queue_shard(WPart& p, i64 pairs);
 double* wpart_tail_params(WPart& p);  // [0] tail_frac, [1] tail_mult (pj_wpart_set_option)

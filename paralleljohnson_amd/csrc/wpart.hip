@@ -37,6 +37,7 @@
 // Row segments longer than WP_LONG edges go to a queue relaxed edge-balanced
 // over the whole grid (1024-edge tiles, lb.h).
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <thread>
 
@@ -1209,6 +1210,8 @@ struct WPart {
     DevBuf<u64> lq_b, lq_e;
     PinnedStat hstat;
     std::unique_ptr<DeltaSteps> steps;  // engine view with its own exchange buffers (lazy)
+    int single_gpu = 1;                 // world 1: solve with delta.hip's v2 (wpart_solve_single)
+    std::unique_ptr<Graph> g1;          // (its Graph over copies of the rows, built at the first solve)
     unsigned grid() const { return (unsigned)ctx->cu_count * 8u; }
     unsigned qgrid() const {  // (region-major: the shards and the spill)
         return (unsigned)(WQ_S + 1) * std::max(1u, grid() / (unsigned)(WQ_S + 1));
@@ -2162,6 +2165,76 @@ void wpart_copy_dist(WPart& p, int32_t* host) {
     }
     PJ_HIP(hipMemcpy(host, p.dist.p, sizeof(int32_t) * (size_t)p.nl, hipMemcpyDeviceToHost));
 }
+
+// ---- world 1: the single-GPU solver --------------------------------------------------
+// A one-rank partition holds the whole graph, and its rows (in the block's degree order,
+// columns mapped through the same order) are a complete weight-sorted CSR. Its solve is
+// therefore delta.hip's v2 -- the single-GPU path's band and round kernels -- on a Graph over
+// copies of those rows (built at the first solve: 2 x 4 bytes per entry), and the distances
+// come back into p.dist, so the step API, the gather and the reach pass see them as the band
+// loop's. Option "single_gpu" 0 keeps the band loop of engine.cpp over this file's kernels
+// (what every rank runs at world > 1).
+__global__ void wp_narrow_k(const u64* __restrict__ in, i64 m, u32* __restrict__ out) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x) out[i] = (u32)in[i];
+}
+
+void wpart_solve_single(WPart& p, i64 source, int32_t delta, pj_part_stats* st) {
+    const auto t0 = std::chrono::steady_clock::now();
+    hipStream_t s = p.ctx->stream;
+    if (!p.g1) {
+        auto g = std::make_unique<Graph>();
+        g->ctx = p.ctx;
+        g->n = p.n;
+        g->nnz = p.nnz_local;
+        g->weighted = true;
+        g->symmetric = p.symmetric;
+        g->off64 = (u64)g->nnz > 0xFFFFFFFFull;
+        const size_t nr = (size_t)p.n + 1, m = (size_t)std::max<i64>(g->nnz, 1);
+        if (g->off64) {
+            g->row64.alloc(nr);
+            PJ_HIP(hipMemcpyAsync(g->row64.p, p.row.p, 8 * nr, hipMemcpyDeviceToDevice, s));
+        } else {
+            g->row32.alloc(nr);
+            wp_narrow_k<<<grid_for((i64)nr, 256, p.grid()), 256, 0, s>>>(p.row.p, (i64)nr, g->row32.p);
+            PJ_LAUNCH_CHECK();
+        }
+        g->col.alloc(m);
+        g->w.alloc(m);
+        if (g->nnz) {
+            PJ_HIP(hipMemcpyAsync(g->col.p, p.col.p, 4 * (size_t)g->nnz, hipMemcpyDeviceToDevice, s));
+            PJ_HIP(hipMemcpyAsync(g->w.p, p.w.p, 4 * (size_t)g->nnz, hipMemcpyDeviceToDevice, s));
+        }
+        PJ_HIP(hipStreamSynchronize(s));
+        p.g1 = std::move(g);
+    }
+    Graph& g = *p.g1;
+    g.delta = delta > 0 ? (double)delta : 0.0;
+    i64 src = source;
+    if (source >= 0 && source < p.n && p.rl_inv.p) {  // the block's degree order: the source's new id
+        u32 x = 0;
+        PJ_HIP(hipMemcpyAsync(&x, p.rl_inv.p + source, sizeof(u32), hipMemcpyDeviceToHost, s));
+        PJ_HIP(hipStreamSynchronize(s));
+        src = (i64)x;
+    }
+    delta_solve(g, src);
+    delta_materialize(g);  // (g.dist in the block's ids, complete on return)
+    if (p.nl) PJ_HIP(hipMemcpyAsync(p.dist.p, g.dist.p, 4 * (size_t)p.nl, hipMemcpyDeviceToDevice, s));
+    i64 rc[2] = {0, 0};
+    wpart_reach(p, rc);  // (synchronizes the stream)
+    if (st) {
+        *st = pj_part_stats{};
+        st->solve_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        st->levels = st->bands = g.stats.levels;
+        st->rounds = g.stats.relax_rounds;
+        st->td_levels = g.stats.td_levels;
+        st->bu_levels = g.stats.bu_levels;
+        st->reached = rc[0];
+        st->reached_edges = rc[1];
+        st->delta = delta > 0 ? delta : (int32_t)auto_delta((double)g.n, (double)g.nnz, g.mean_weight);
+    }
+}
+bool wpart_single(const WPart& p) { return p.world == 1 && p.single_gpu; }
+int& wpart_single_gpu(WPart& p) { return p.single_gpu; }
 
 // ------------------------------------------------------------ engine view ---
 namespace {

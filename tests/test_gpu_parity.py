@@ -93,10 +93,13 @@ def test_bfs_random_graphs(ctx, oracle, kind, direction, small):
         roots = [int(src[0]) if len(src) else 0, int(rng.integers(0, n)), n, -5]
         for r in roots:
             exp = oracle.bfs(row, col, r)
-            for hf in (0, 1):  # (file-order in-rows, then the hub-first copy the pull levels probe)
+            for hf, pv in ((0, 0), (1, 0), (1, 2), (1, 0.1)):
+                # (file-order in-rows, then the hub-first copy the pull levels probe; the
+                # vertex-count direction rule off, at its default and eager)
                 g.set_option("hub_first", hf)
+                g.set_option("pull_vertex", pv)
                 d = g.sssp(r)
-                assert (d == exp).all(), (kind, direction, trial, r, hf)
+                assert (d == exp).all(), (kind, direction, trial, r, hf, pv)
         g.close()
 
 
@@ -187,6 +190,18 @@ def test_bfs_kronecker_s22_full_size(ctx, oracle):
     for hf in (1, 0):  # pull levels over the hub-first in-rows, and back
         g.set_option("hub_first", hf)
         assert (g.sssp(r) == exp).all(), hf
+    g.set_option("hub_first", 1)
+    # the bench's root whose second level the vertex-count rule turns from a 6.18M-edge push
+    # into a pull (profiles/r06/k22_levels_pmc_*.txt), with the rule off, at its default, eager
+    r2 = 3377866
+    exp2 = oracle.bfs(row, col, r2)
+    bu = {}
+    for pv in (0, 2, 0.1):
+        g.set_option("pull_vertex", pv)
+        assert (g.sssp(r2) == exp2).all(), pv
+        bu[pv] = g.stats()["bu_levels"]
+    assert bu[2] > bu[0]  # (the rule fired)
+    g.set_option("pull_vertex", 2)
     # push-only levels of millions of vertices overflow the per-block hub staging (the
     # overflow path once lost hubs in about 1 of 50 such solves), with and without the
     # one-workgroup small levels

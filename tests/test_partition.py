@@ -364,20 +364,25 @@ def test_wpart_group(pj, oracle, world, transport):
                 gr.close()
         g0.close()
         # (delta 60, light pull always: light rows of hundreds of edges, the long-row chunk list)
-        for delta, tf, tm, pf, lp in ((0, 0.1, 64, 4, 3), (7, 2.0, 3, 1e9, 1e9), (60, 0.0, 64, 0, 0),
-                                      (7, 0.1, 64, 1e9, 3), (0, 0.0, 64, 4, 1e9), (60, 0.1, 64, 4, 1e9)):
-            for p in parts:
-                p.set_option("tail_frac", tf)
-                p.set_option("tail_mult", tm)
-                p.set_option("pull_factor", pf)
-                p.set_option("light_pull", lp)
-            for source in (0, n // 3, n - 1, n + 2):
-                st = delta_group(parts, comms, source, delta)
-                exp = oracle.dijkstra(row, col, wc, source) if source < n else np.full(n, INF, np.int32)
-                assert np.array_equal(gather_group(parts, comms), exp), (name, delta, tf, tm, pf, lp, source, world)
-                reached = exp < INF
-                assert [st[0]["reached"], st[0]["reached_edges"]] == [int(reached.sum()),
-                                                                      int(np.diff(row)[reached].sum())]
+        # (world 1: the single-GPU solver, option single_gpu 1, then the band loop over
+        # wpart.hip's kernels that every rank runs at world > 1)
+        for single in ((1, 0) if world == 1 else (1,)):
+            for delta, tf, tm, pf, lp in ((0, 0.1, 64, 4, 3), (7, 2.0, 3, 1e9, 1e9), (60, 0.0, 64, 0, 0),
+                                          (7, 0.1, 64, 1e9, 3), (0, 0.0, 64, 4, 1e9), (60, 0.1, 64, 4, 1e9)):
+                for p in parts:
+                    p.set_option("single_gpu", single)
+                    p.set_option("tail_frac", tf)
+                    p.set_option("tail_mult", tm)
+                    p.set_option("pull_factor", pf)
+                    p.set_option("light_pull", lp)
+                for source in (0, n // 3, n - 1, n + 2):
+                    st = delta_group(parts, comms, source, delta)
+                    exp = oracle.dijkstra(row, col, wc, source) if source < n else np.full(n, INF, np.int32)
+                    assert np.array_equal(gather_group(parts, comms), exp), (name, delta, tf, tm, pf, lp, source,
+                                                                             world, single)
+                    reached = exp < INF
+                    assert [st[0]["reached"], st[0]["reached_edges"]] == [int(reached.sum()),
+                                                                          int(np.diff(row)[reached].sum())]
         for p in parts:
             p.close()
 
