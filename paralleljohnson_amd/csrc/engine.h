@@ -209,6 +209,7 @@ int wpart_world(const WPart& p);
 // world 1 (option "single_gpu", default on): the solve runs delta.hip's single-GPU solver
 bool wpart_single(const WPart& p);
 int& wpart_single_gpu(WPart& p);
+int& wpart_pull_fmin(WPart& p);  // light pulls' frontier-minimum bound (option "pull_fmin", default 1)
 void wpart_solve_single(WPart& p, i64 source, int32_t delta, pj_part_stats* st);
 bool wpart_pending(const WPart& p);
 void wpart_set_queue_shard(WPart& p, i64 pairs);

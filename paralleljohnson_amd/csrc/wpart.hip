@@ -930,16 +930,54 @@ __global__ void wp_plong_fill_k(const u32* __restrict__ lsplit, i64 nl, u64* __r
             }
         }
 }
+// The least dist - lo in the all-gathered frontier map (every rank's frontier), into *out
+// (~0: none). A light pull stops a row at flo + w >= its best, flo = lo + that minimum, instead
+// of lo + w: no frontier in-neighbour offers less than flo + w (v2's frontier-minimum bound,
+// delta.hip v2_pull_lo; one pass over the map, which every rank holds after the all-gather).
+template <typename MT>
+__global__ __launch_bounds__(256) void wp_map_min_k(const MT* __restrict__ map, i64 m, u32* __restrict__ out) {
+    constexpr MT NONE = (MT)~(MT)0;
+    u32 mn = ~0u;
+    const i64 m4 = m / 4;
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m4; i += (i64)gridDim.x * blockDim.x) {
+        MT x[4];
+        if constexpr (sizeof(MT) == 1) {
+            const u32 q = reinterpret_cast<const u32*>(map)[i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = (MT)(q >> (8 * j));
+        } else {
+            const u64 q = reinterpret_cast<const u64*>(map)[i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = (MT)(q >> (16 * j));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (x[j] != NONE && (u32)x[j] < mn) mn = x[j];
+    }
+    for (i64 i = m4 * 4 + (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x)
+        if (map[i] != NONE && (u32)map[i] < mn) mn = map[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const u32 y = __shfl_xor(mn, off, 64);
+        mn = y < mn ? y : mn;
+    }
+    if (lane_id() == 0 && mn != ~0u) atomicMin(out, mn);
+}
+__device__ __forceinline__ int32_t wp_flo(const u32* fminp, int32_t lo) {
+    const u32 f = fminp ? *fminp : ~0u;
+    return f != ~0u ? lo + (int32_t)f : lo;
+}
+
 // a wave per chunk: skipped when even its lightest edge cannot help, else scanned with the
 // early stop; the result goes in with atomicMin (a vertex's chunks run in different waves)
 // and the vertex's next-frontier bit with a returning atomicOr (counted once)
 template <typename MT>
 __global__ __launch_bounds__(WB) void wp_pull_long_k(WArgs a, const MT* __restrict__ fmap, const u32* __restrict__ lv,
-                                                     const u32* __restrict__ lc, u64 nlc) {
+                                                     const u32* __restrict__ lc, u64 nlc, const u32* __restrict__ fminp) {
     constexpr MT NONE = (MT)~(MT)0;
     __shared__ u64 red[WB / WAVE];
     const int lane = lane_id();
-    const int32_t lo = a.dlo, hi = a.dhi;
+    const int32_t lo = a.dlo, hi = a.dhi, flo = wp_flo(fminp, lo);
     u64 marks = 0;
     for (u64 it = (u64)blockIdx.x * (WB / WAVE) + wave_id(); it < nlc; it += (u64)gridDim.x * (WB / WAVE)) {
         const u32 v = lv[it];
@@ -948,13 +986,13 @@ __global__ __launch_bounds__(WB) void wp_pull_long_k(WArgs a, const MT* __restri
         const u64 rb = a.row[v];
         const u64 kb = rb + (u64)lc[it] * WP_PCH;
         const u64 ke = min(rb + (u64)a.lsplit[v], kb + WP_PCH);
-        if ((long long)lo + a.w[kb] >= (long long)d0) continue;
+        if ((long long)flo + a.w[kb] >= (long long)d0) continue;
         int32_t cur = d0;
         for (u64 kk = kb; kk < ke; kk += WAVE) {
             const u64 k0 = kk + lane;
             const bool valid = k0 < ke;
             const u32 w = valid ? a.w[k0] : 0u;
-            const bool stop = !valid || (long long)lo + w >= (long long)cur;
+            const bool stop = !valid || (long long)flo + w >= (long long)cur;
             int32_t cand = INT_INF;
             if (!stop) {
                 const MT m = fmap[a.col[k0]];
@@ -987,11 +1025,12 @@ __global__ __launch_bounds__(WB) void wp_pull_long_k(WArgs a, const MT* __restri
 // it) and the next-frontier word is OR-ed in (wp_pull_long_k, launched before, may have
 // set bits of it). Rows longer than plmax are wp_pull_long_k's.
 template <typename MT>
-__global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const MT* __restrict__ fmap, u32 plmax) {
+__global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const MT* __restrict__ fmap, u32 plmax,
+                                                      const u32* __restrict__ fminp) {
     constexpr MT NONE = (MT)~(MT)0;
     __shared__ u64 red[WB / WAVE];
     const int lane = lane_id();
-    const int32_t lo = a.dlo, hi = a.dhi;
+    const int32_t lo = a.dlo, hi = a.dhi, flo = wp_flo(fminp, lo);
     const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
     u64 marks = 0;
     for (i64 b0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; b0 < a.nl; b0 += nwaves * 64) {
@@ -1020,7 +1059,7 @@ __global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const MT* __restr
         bool done = !act || k >= e;
         while (act && k < lim) {
             const u32 w = a.w[k];
-            if ((long long)lo + w >= (long long)cur) {
+            if ((long long)flo + w >= (long long)cur) {
                 done = true;
                 break;
             }
@@ -1039,7 +1078,7 @@ __global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const MT* __restr
                 const u64 k0 = kk + lane;
                 const bool valid = k0 < ke;
                 const u32 w = valid ? a.w[k0] : 0u;
-                const bool stop = !valid || (long long)lo + w >= (long long)cl;
+                const bool stop = !valid || (long long)flo + w >= (long long)cl;
                 int32_t cand = INT_INF;
                 if (!stop) {
                     const MT m = fmap[a.col[k0]];
@@ -1211,6 +1250,8 @@ struct WPart {
     PinnedStat hstat;
     std::unique_ptr<DeltaSteps> steps;  // engine view with its own exchange buffers (lazy)
     int single_gpu = 1;                 // world 1: solve with delta.hip's v2 (wpart_solve_single)
+    int pull_fmin = 1;                  // light pulls stop rows at the frontier's least distance (wp_map_min_k)
+    DevBuf<u32> fmin;                   // (its device word)
     std::unique_ptr<Graph> g1;          // (its Graph over copies of the rows, built at the first solve)
     unsigned grid() const { return (unsigned)ctx->cu_count * 8u; }
     unsigned qgrid() const {  // (region-major: the shards and the spill)
@@ -1880,8 +1921,18 @@ void wpart_frontier_slice(WPart& p, int32_t lo, int32_t hi) {
 void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
     p.clear_stat();
+    const u32* fminp = nullptr;
+    if (p.nl > 0 && p.pull_fmin) {  // the frontier-minimum bound of this round (wp_map_min_k)
+        if (!p.fmin.p) p.fmin.alloc(1);
+        PJ_HIP(hipMemsetAsync(p.fmin.p, 0xFF, sizeof(u32), s));
+        const i64 m = (i64)p.world * p.block;
+        if (p.map16) wp_map_min_k<uint16_t><<<grid_for(m / 4 + 1, 256, p.grid()), 256, 0, s>>>(p.fmap16.p, m, p.fmin.p);
+        else wp_map_min_k<uint8_t><<<grid_for(m / 4 + 1, 256, p.grid()), 256, 0, s>>>(p.mmap.p, m, p.fmin.p);
+        PJ_LAUNCH_CHECK();
+        fminp = p.fmin.p;
+    }
     if (p.nl > 0 && p.map16) {  // the tail's bands (hubs settled; a list would mostly hold settled rows)
-        wp_pull_light_k<uint16_t><<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.fmap16.p, ~0u);
+        wp_pull_light_k<uint16_t><<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.fmap16.p, ~0u, fminp);
         PJ_LAUNCH_CHECK();
     } else if (p.nl > 0) {
         WPart::PullLong& L = p.pl;
@@ -1905,10 +1956,10 @@ void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
         }
         const WArgs a = p.args(lo, hi);
         if (L.n) {
-            wp_pull_long_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, L.v.p, L.c.p, L.n);
+            wp_pull_long_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, L.v.p, L.c.p, L.n, fminp);
             PJ_LAUNCH_CHECK();
         }
-        wp_pull_light_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, WP_PLMAX);
+        wp_pull_light_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, WP_PLMAX, fminp);
         PJ_LAUNCH_CHECK();
     }
 }
@@ -2235,6 +2286,7 @@ void wpart_solve_single(WPart& p, i64 source, int32_t delta, pj_part_stats* st) 
 }
 bool wpart_single(const WPart& p) { return p.world == 1 && p.single_gpu; }
 int& wpart_single_gpu(WPart& p) { return p.single_gpu; }
+int& wpart_pull_fmin(WPart& p) { return p.pull_fmin; }
 
 // ------------------------------------------------------------ engine view ---
 namespace {
