@@ -89,7 +89,7 @@ def make_graph(ctx, wl, args):
 
 def run_workload(ctx, key, args, rank, world, barrier, steps, warmup):
     """Timed SSSPs of one workload on this rank; returns per-rank sums."""
-    import paralleljohnson_amd as pj  # noqa: F401
+    import paralleljohnson_amd as pj
     wl = WORKLOADS[key]
     t_gen = time.perf_counter()
     g = make_graph(ctx, wl, args)
@@ -108,16 +108,16 @@ def run_workload(ctx, key, args, rank, world, barrier, steps, warmup):
     gen_s = time.perf_counter() - t_gen
     for k in range(warmup):
         g.sssp(my_roots[k % len(my_roots)], copy=False)
-    kernel_ms, work = [], []
+    sts = [pj.Stats() for _ in range(steps)]  # (filled in the loop, read after it: no dicts in the timed region)
     barrier()
     t0 = time.perf_counter()
     for k in range(steps):
         g.sssp(my_roots[k], copy=False)
-        st = g.stats()
-        kernel_ms.append(st["kernel_ms"])
-        work.append((st["scanned_edges"], st["probes"], st["work_bytes"]))
+        g.stats_into(sts[k])
     barrier()
     elapsed = time.perf_counter() - t0
+    kernel_ms = [st.kernel_ms for st in sts]
+    work = [(st.scanned_edges, st.probes, st.work_bytes) for st in sts]
     reach, levels = {}, {}
     for r in set(my_roots):  # untimed: reached-component statistics per root
         g.sssp(r, copy=False)

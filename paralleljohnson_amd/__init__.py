@@ -298,6 +298,11 @@ class Graph:
         _check(_lib.pj_last_stats(self._h, ctypes.byref(st)))
         return st.as_dict()
 
+    def stats_into(self, st: "Stats") -> "Stats":
+        """The last solve's statistics into a caller's Stats (no dict built: timed loops)."""
+        _check(_lib.pj_last_stats(self._h, ctypes.byref(st)))
+        return st
+
     def reach_stats(self) -> dict:
         st = Stats()
         _check(_lib.pj_reach_stats(self._h, ctypes.byref(st)))
