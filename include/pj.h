@@ -558,8 +558,9 @@ int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj
  * vertices' heavy edges are fewer than pull_factor x the members'; symmetric graphs only;
  * 0 = always push; default 4) and "light_pull" (a light round whose frontier has more light
  * edges than the vertices above the band start / light_pull runs as a pull through an
- * all-gathered frontier map; symmetric graphs; 0 = push; default 0: since the push rounds
- * count their frontier per workgroup the pull no longer pays, profiles/r03/wpart_light_pull_r3ad.txt)
+ * all-gathered frontier map, stopping a row at the frontier's least distance + its weight
+ * ("pull_fmin" 1, default); symmetric graphs; 0 = push; default 3 since round 6,
+ * profiles/r06/wpart_light_pull_r6l.txt)
  * and "tail_light_pull" (the same rule in the tail's bands, independent of light_pull, the
  * frontier map then 16-bit; 0 = push; default 3). Every rank must use the same values.
  * "single_gpu" (0/1, default 1: the world-1 solve runs delta.hip's v2, see pj_wpart_delta).

@@ -1212,10 +1212,11 @@ struct WPart {
     double pull_factor = 4.0;      // heavy pull when unsettled heavy edges < pull_factor x members' (0 = push)
     double tail_light_pull = 3.0;  // the same rule after the tail switch (independent of light_pull; 0 =
                                    // push), with a 16-bit frontier map for the tail's wide bands
-    double light_pull = 0.0;       // light pull round when the frontier's light edges > the light edges
-                                   // of the vertices above lo / light_pull (0 = push; 3 was the default
-                                   // until the push rounds counted their frontier per workgroup: then
-                                   // 0 measured best at s24w / s26w, world 1 and 2, r3ad)
+    double light_pull = 3.0;       // light pull round when the frontier's light edges > the light edges
+                                   // of the vertices above lo / light_pull (0 = push). 0 from round 3
+                                   // (r3ad) until round 6: with the pulls' frontier-minimum bound, 3
+                                   // measured 9.57-9.81 against 10.02-10.03 ms at world 2 (s26w,
+                                   // interleaved, profiles/r06/wpart_light_pull_r6l.txt)
     bool symmetric = false;        // rows are also the in-edges (Kronecker graphs): the heavy pull applies
     DevBuf<uint8_t> mmap;          // replicated member map of the heavy pull (world x block bytes)
     DevBuf<uint16_t> fmap16;       // replicated frontier map of a light pull in a band wider than 255
