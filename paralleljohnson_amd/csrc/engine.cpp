@@ -275,6 +275,11 @@ void delta_engine(DeltaSteps& S, Comm& comm, i64 source, int32_t delta_in, pj_pa
                     S.light_counts((int32_t)lo, (int32_t)hi, lc);
                     comm.allreduce(lc, 2, false, s);
                     if (lc[0] > 0 && (double)lc[0] * lpf > (double)lc[1]) {
+                        i64 fm = S.frontier_min();  // (-1 on every rank alike: no bound)
+                        if (fm >= 0) {
+                            comm.allreduce(&fm, 1, true, s);
+                            S.set_frontier_min(fm);
+                        }
                         S.frontier_slice((int32_t)lo, (int32_t)hi);
                         if (S.world > 1) {
                             const size_t sl = S.member_bytes();

@@ -181,6 +181,11 @@ struct DeltaSteps {
     virtual double tail_light_pull_factor() { return light_pull_factor(); }
     virtual int32_t pull_map_width() { return 255; }
     virtual void light_counts(int32_t lo, int32_t hi, i64* out2) { (void)lo, (void)hi, out2[0] = out2[1] = 0; }
+    // the least distance of this rank's frontier (after light_counts; INT_INF: none or not
+    // counted), and every rank's, min-all-reduced by the loop before a light pull: the pull's
+    // rows stop at that minimum + w instead of lo + w (optional: -1 keeps lo)
+    virtual i64 frontier_min() { return -1; }
+    virtual void set_frontier_min(i64 m) { (void)m; }
     virtual void frontier_slice(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
     virtual void light_pull(int32_t lo, int32_t hi) { (void)lo, (void)hi; }
 };

@@ -864,6 +864,7 @@ __global__ __launch_bounds__(WB) void wp_pull_heavy_k(WArgs a, const uint8_t* __
 __global__ __launch_bounds__(WB) void wp_light_counts_k(WArgs a, u64* __restrict__ out) {
     __shared__ u64 red[WB / WAVE];
     u64 f = 0, u = 0;
+    int32_t fm = INT_INF;  // (out[2]: the least distance of this rank's frontier, the pulls' bound)
     constexpr int LU = 4;  // vertices per thread step, loads issued together
     const i64 stride = (i64)gridDim.x * WB;
     for (i64 v0 = (i64)blockIdx.x * WB + threadIdx.x; v0 < a.nl; v0 += LU * stride) {
@@ -880,7 +881,10 @@ __global__ __launch_bounds__(WB) void wp_light_counts_k(WArgs a, u64* __restrict
 #pragma unroll
         for (int j = 0; j < LU; ++j) {
             const i64 v = v0 + (i64)j * stride;
-            if ((fw[j] >> (v & 63)) & 1ull) f += ls[j];
+            if ((fw[j] >> (v & 63)) & 1ull) {
+                f += ls[j];
+                fm = d[j] < fm ? d[j] : fm;
+            }
             if (v < a.nl && d[j] > a.dlo) u += ls[j];
         }
     }
@@ -890,6 +894,12 @@ __global__ __launch_bounds__(WB) void wp_light_counts_k(WArgs a, u64* __restrict
         if (f) atomicAdd(&out[0], f);
         if (u) atomicAdd(&out[1], u);
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int32_t y = __shfl_xor(fm, off, 64);
+        fm = y < fm ? y : fm;
+    }
+    if (lane_id() == 0 && fm < INT_INF) atomicMin(&out[2], (u64)fm);
 }
 // this rank's slice of the frontier map: dist - lo of a frontier vertex, all ones otherwise
 // (MT = u8 for bands up to 255 wide, u16 for the tail's wide bands)
@@ -930,54 +940,21 @@ __global__ void wp_plong_fill_k(const u32* __restrict__ lsplit, i64 nl, u64* __r
             }
         }
 }
-// The least dist - lo in the all-gathered frontier map (every rank's frontier), into *out
-// (~0: none). A light pull stops a row at flo + w >= its best, flo = lo + that minimum, instead
-// of lo + w: no frontier in-neighbour offers less than flo + w (v2's frontier-minimum bound,
-// delta.hip v2_pull_lo; one pass over the map, which every rank holds after the all-gather).
-template <typename MT>
-__global__ __launch_bounds__(256) void wp_map_min_k(const MT* __restrict__ map, i64 m, u32* __restrict__ out) {
-    constexpr MT NONE = (MT)~(MT)0;
-    u32 mn = ~0u;
-    const i64 m4 = m / 4;
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m4; i += (i64)gridDim.x * blockDim.x) {
-        MT x[4];
-        if constexpr (sizeof(MT) == 1) {
-            const u32 q = reinterpret_cast<const u32*>(map)[i];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) x[j] = (MT)(q >> (8 * j));
-        } else {
-            const u64 q = reinterpret_cast<const u64*>(map)[i];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) x[j] = (MT)(q >> (16 * j));
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (x[j] != NONE && (u32)x[j] < mn) mn = x[j];
-    }
-    for (i64 i = m4 * 4 + (i64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (i64)gridDim.x * blockDim.x)
-        if (map[i] != NONE && (u32)map[i] < mn) mn = map[i];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const u32 y = __shfl_xor(mn, off, 64);
-        mn = y < mn ? y : mn;
-    }
-    if (lane_id() == 0 && mn != ~0u) atomicMin(out, mn);
-}
-__device__ __forceinline__ int32_t wp_flo(const u32* fminp, int32_t lo) {
-    const u32 f = fminp ? *fminp : ~0u;
-    return f != ~0u ? lo + (int32_t)f : lo;
-}
+// A light pull stops a row at flo + w >= its best, flo = the least distance of every rank's
+// frontier (the ranks' wp_light_counts_k minima, min-all-reduced by the engine), instead of
+// lo + w: no frontier in-neighbour offers less than flo + w (v2's frontier-minimum bound,
+// delta.hip v2_pull_lo).
 
 // a wave per chunk: skipped when even its lightest edge cannot help, else scanned with the
 // early stop; the result goes in with atomicMin (a vertex's chunks run in different waves)
 // and the vertex's next-frontier bit with a returning atomicOr (counted once)
 template <typename MT>
 __global__ __launch_bounds__(WB) void wp_pull_long_k(WArgs a, const MT* __restrict__ fmap, const u32* __restrict__ lv,
-                                                     const u32* __restrict__ lc, u64 nlc, const u32* __restrict__ fminp) {
+                                                     const u32* __restrict__ lc, u64 nlc, int32_t flo) {
     constexpr MT NONE = (MT)~(MT)0;
     __shared__ u64 red[WB / WAVE];
     const int lane = lane_id();
-    const int32_t lo = a.dlo, hi = a.dhi, flo = wp_flo(fminp, lo);
+    const int32_t lo = a.dlo, hi = a.dhi;
     u64 marks = 0;
     for (u64 it = (u64)blockIdx.x * (WB / WAVE) + wave_id(); it < nlc; it += (u64)gridDim.x * (WB / WAVE)) {
         const u32 v = lv[it];
@@ -1026,11 +1003,11 @@ __global__ __launch_bounds__(WB) void wp_pull_long_k(WArgs a, const MT* __restri
 // set bits of it). Rows longer than plmax are wp_pull_long_k's.
 template <typename MT>
 __global__ __launch_bounds__(WB) void wp_pull_light_k(WArgs a, const MT* __restrict__ fmap, u32 plmax,
-                                                      const u32* __restrict__ fminp) {
+                                                      int32_t flo) {
     constexpr MT NONE = (MT)~(MT)0;
     __shared__ u64 red[WB / WAVE];
     const int lane = lane_id();
-    const int32_t lo = a.dlo, hi = a.dhi, flo = wp_flo(fminp, lo);
+    const int32_t lo = a.dlo, hi = a.dhi;
     const i64 nwaves = (i64)gridDim.x * (WB / WAVE);
     u64 marks = 0;
     for (i64 b0 = ((i64)blockIdx.x * (WB / WAVE) + wave_id()) * 64; b0 < a.nl; b0 += nwaves * 64) {
@@ -1251,8 +1228,9 @@ struct WPart {
     PinnedStat hstat;
     std::unique_ptr<DeltaSteps> steps;  // engine view with its own exchange buffers (lazy)
     int single_gpu = 1;                 // world 1: solve with delta.hip's v2 (wpart_solve_single)
-    int pull_fmin = 1;                  // light pulls stop rows at the frontier's least distance (wp_map_min_k)
-    DevBuf<u32> fmin;                   // (its device word)
+    int pull_fmin = 1;                  // light pulls stop rows at the frontier's least distance
+    i64 fmin_own = INT_INF;             // this rank's frontier minimum (wpart_light_counts)
+    i64 fmin_all = INT_INF;             // every rank's (DeltaSteps::set_frontier_min), or -1: none
     std::unique_ptr<Graph> g1;          // (its Graph over copies of the rows, built at the first solve)
     unsigned grid() const { return (unsigned)ctx->cu_count * 8u; }
     unsigned qgrid() const {  // (region-major: the shards and the spill)
@@ -1892,16 +1870,19 @@ void wpart_heavy_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
 
 void wpart_light_counts(WPart& p, int32_t lo, int32_t hi, i64* out2) {
     hipStream_t s = p.ctx->stream;
-    u64 h[2] = {0, 0};
+    u64 h[3] = {0, 0, ~0ull};
     if (p.nl > 0) {
         u64* acc = p.stat.p + ST_ACC;
         PJ_HIP(hipMemsetAsync(acc, 0, 2 * sizeof(u64), s));
+        PJ_HIP(hipMemsetAsync(acc + 2, 0xFF, sizeof(u64), s));
         wp_light_counts_k<<<grid_for(p.nl, WB, p.grid()), WB, 0, s>>>(p.args(lo, hi), acc);
         PJ_LAUNCH_CHECK();
-        p.read_acc(h, 2);
+        p.read_acc(h, 3);
     }
     out2[0] = (i64)h[0];
     out2[1] = (i64)h[1];
+    p.fmin_own = h[2] < (u64)INT_INF ? (i64)h[2] : (i64)INT_INF;
+    p.fmin_all = -1;  // (until the engine hands over every rank's minimum)
 }
 
 void wpart_frontier_slice(WPart& p, int32_t lo, int32_t hi) {
@@ -1922,18 +1903,11 @@ void wpart_frontier_slice(WPart& p, int32_t lo, int32_t hi) {
 void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
     hipStream_t s = p.ctx->stream;
     p.clear_stat();
-    const u32* fminp = nullptr;
-    if (p.nl > 0 && p.pull_fmin) {  // the frontier-minimum bound of this round (wp_map_min_k)
-        if (!p.fmin.p) p.fmin.alloc(1);
-        PJ_HIP(hipMemsetAsync(p.fmin.p, 0xFF, sizeof(u32), s));
-        const i64 m = (i64)p.world * p.block;
-        if (p.map16) wp_map_min_k<uint16_t><<<grid_for(m / 4 + 1, 256, p.grid()), 256, 0, s>>>(p.fmap16.p, m, p.fmin.p);
-        else wp_map_min_k<uint8_t><<<grid_for(m / 4 + 1, 256, p.grid()), 256, 0, s>>>(p.mmap.p, m, p.fmin.p);
-        PJ_LAUNCH_CHECK();
-        fminp = p.fmin.p;
-    }
+    // the frontier-minimum bound (every rank's frontier; the engine's min-all-reduce of the
+    // ranks' light-count minima): flo in [lo, hi), else lo
+    const int32_t flo = (p.pull_fmin && p.fmin_all > lo && p.fmin_all < hi) ? (int32_t)p.fmin_all : lo;
     if (p.nl > 0 && p.map16) {  // the tail's bands (hubs settled; a list would mostly hold settled rows)
-        wp_pull_light_k<uint16_t><<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.fmap16.p, ~0u, fminp);
+        wp_pull_light_k<uint16_t><<<p.grid(), WB, 0, s>>>(p.args(lo, hi), p.fmap16.p, ~0u, flo);
         PJ_LAUNCH_CHECK();
     } else if (p.nl > 0) {
         WPart::PullLong& L = p.pl;
@@ -1957,10 +1931,10 @@ void wpart_light_pull(WPart& p, int32_t lo, int32_t hi) {
         }
         const WArgs a = p.args(lo, hi);
         if (L.n) {
-            wp_pull_long_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, L.v.p, L.c.p, L.n, fminp);
+            wp_pull_long_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, L.v.p, L.c.p, L.n, flo);
             PJ_LAUNCH_CHECK();
         }
-        wp_pull_light_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, WP_PLMAX, fminp);
+        wp_pull_light_k<uint8_t><<<p.grid(), WB, 0, s>>>(a, p.mmap.p, WP_PLMAX, flo);
         PJ_LAUNCH_CHECK();
     }
 }
@@ -2350,6 +2324,8 @@ struct WPartGpuSteps final : DeltaSteps {
     double tail_light_pull_factor() override { return p.symmetric ? p.tail_light_pull : 0.0; }
     int32_t pull_map_width() override { return 65534; }
     void light_counts(int32_t lo, int32_t hi, i64* out2) override { wpart_light_counts(p, lo, hi, out2); }
+    i64 frontier_min() override { return p.fmin_own; }
+    void set_frontier_min(i64 m) override { p.fmin_all = m; }
     void frontier_slice(int32_t lo, int32_t hi) override { wpart_frontier_slice(p, lo, hi); }
     void light_pull(int32_t lo, int32_t hi) override { wpart_light_pull(p, lo, hi); }
 };
