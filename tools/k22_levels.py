@@ -4,7 +4,8 @@ then ROOTS solves run with the level_log option: libpj prints one stderr line pe
 (level, push / pull, where the frontier came from, its vertices and out-edges, and the in-edge
 probes the previous launch scanned). tools/cycle.sh `klevels` runs this under the kernel trace
 and --pmc passes; tools/k22_level_table.py joins them launch by launch.
-Usage: python tools/k22_levels.py [roots=4] [opt=value ...]"""
+Usage: python tools/k22_levels.py [roots=4] [graph=wg] [opt=value ...]  (graph=wg: configs[0]'s
+web-Google-shaped graph, source 0 and sampled roots)"""
 import os
 import sys
 
@@ -13,12 +14,13 @@ sys.path.insert(0, R)
 import paralleljohnson_amd as pj  # noqa: E402
 
 nroots = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+opts = dict(kv.split("=") for kv in sys.argv[2:])
 ctx = pj.Context(0)
-g = ctx.generate_kronecker(22, 16, 1)
-for kv in sys.argv[2:]:
-    k, v = kv.split("=")
+wg = opts.pop("graph", "k22") == "wg"
+g = ctx.generate_webgraph() if wg else ctx.generate_kronecker(22, 16, 1)
+for k, v in opts.items():
     g.set_option(k, float(v))
-roots = [int(r) for r in g.sample_roots(2, nroots)]
+roots = ([0] + [int(r) for r in g.sample_roots(2, nroots - 1)]) if wg else [int(r) for r in g.sample_roots(2, nroots)]
 g.sssp(roots[0], copy=False)  # (workspace; unlogged)
 g.set_option("level_log", 1)
 for r in roots:
