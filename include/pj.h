@@ -433,7 +433,9 @@ int pj_wpart_info(const pj_wpart* p, int64_t* out);
  * pj_wpart_load_snap) also holds 8 bytes per vertex of the WHOLE graph for a moment
  * (every vertex's degree and the relabel table of all blocks, which the rank's column
  * ids go through; 20 bytes until round 5), plus 16 bytes per vertex of one block for
- * the block-by-block sort; none of it stays. */
+ * the block-by-block sort; none of it stays. At world 1 after a single-GPU solve
+ * (option "single_gpu") the rows figure includes that solver's copy of the rows, its
+ * relabeled copy and its workspace (~14 bytes per entry more). */
 int pj_wpart_device_bytes(const pj_wpart* p, int64_t* out);
 /* Start a solve from `source` (dist := INF, then the source); delta <= 0 picks
  * the single-GPU default (c(n) x mean weight / mean degree, c(n) = 0.1875 log2(n) -

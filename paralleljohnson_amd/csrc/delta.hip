@@ -1740,6 +1740,30 @@ struct DeltaWork {
 
 void delete_delta_work(DeltaWork* p) { delete p; }
 
+// device bytes of a weighted graph's solver state: the relabeled copy and the delta
+// workspace with its solve slots (what delta_solve / delta_batch added to the graph's CSR)
+i64 delta_device_bytes(const Graph& g) {
+    size_t b = 0;
+    if (g.rl) {
+        const Relabeled& R = *g.rl;
+        b += R.perm.bytes() + R.inv.bytes() + R.row32.bytes() + R.row64.bytes() + R.col.bytes() + R.w8.bytes() +
+             R.w.bytes() + R.dist.bytes();
+    }
+    if (g.delta_work) {
+        const DeltaWork& w = *g.delta_work;
+        b += w.lsplit.bytes() + w.lsplit2.bytes() + w.lcv.bytes() + w.lcc.bytes() + w.cw.bytes() + w.lrow.bytes() +
+             w.lcw.bytes() + w.lcw32.bytes() + w.hl.bytes() + w.hw.bytes() + w.hw2.bytes() + w.w1.bytes();
+        auto slot = [&](const DeltaSolve& v) {
+            b += v.dist_own.bytes() + v.out_own.bytes() + v.f[0].bytes() + v.f[1].bytes() + v.f[2].bytes() +
+                 v.mb.bytes() + v.sb.bytes() + v.hmap.bytes() + v.db.bytes() + v.ctl.bytes() + v.hv.bytes() +
+                 v.hbeg.bytes() + v.hoff.bytes();
+        };
+        slot(w.main);
+        for (const auto& x : w.extra) slot(*x);
+    }
+    return (i64)b;
+}
+
 void preload_delta_module() {
     hipFuncAttributes fa;
     (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&light_split_k<u32, uint8_t>));

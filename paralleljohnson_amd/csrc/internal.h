@@ -334,6 +334,7 @@ void delta_solve(Graph& g, i64 source);
 // g.dist in input ids after a delta_solve (a no-op when it already is): every reader of g.dist
 // calls it first (enqueued on the ctx stream)
 void delta_materialize(Graph& g);
+i64 delta_device_bytes(const Graph& g);  // the relabeled copy + delta workspace and solve slots
 // Weighted batch with `slots` concurrent solves (delta.hip); on_row(i, device row, stream)
 // is called once per source, serialised.
 void delta_batch(Graph& g, const i64* sources, int n_src, int slots,

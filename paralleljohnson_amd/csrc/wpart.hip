@@ -1840,6 +1840,9 @@ void wpart_info(const WPart& p, i64* out) {
 // and the exchange buffers (sized to the largest round's pairs)
 void wpart_device_bytes(const WPart& p, i64* out4) {
     out4[0] = (i64)(p.row.bytes() + p.col.bytes() + p.w.bytes());
+    if (p.g1)  // (world 1: the single-GPU solver's copy of the rows, its relabeled copy and workspace)
+        out4[0] += (i64)(p.g1->row32.bytes() + p.g1->row64.bytes() + p.g1->col.bytes() + p.g1->w.bytes() +
+                         p.g1->dist.bytes()) + delta_device_bytes(*p.g1);
     out4[1] = (i64)(p.lsplit.bytes() + p.lsplit_alt.bytes() + p.dist.bytes() + p.fr.bytes() + p.frn.bytes() +
                     p.mb.bytes() + p.lq_v.bytes() + p.lq_b.bytes() + p.lq_e.bytes() + p.stat.bytes() +
                     p.rc.bytes() + p.qctr.bytes() + p.rl_inv.bytes() + p.pl.v.bytes() + p.pl.c.bytes() +
