@@ -2059,10 +2059,13 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
     // The host spins on the sequence number (wakes within ~1 us of the copy instead of
     // the stream synchronization's latency); after 0.2 s of spinning it synchronizes the
     // stream, which surfaces a failed kernel instead of spinning forever.
-    auto sync_ctl = [&]() {
+    auto publish_ctl = [&]() {
         const u64 seq = ++v.seq;
         v2_publish_k<<<1, 256, 0, s>>>(v.ctl.p, reinterpret_cast<u64*>(v.hctl_dev), v.hseq_dev, seq);
         PJ_LAUNCH_CHECK();
+        return seq;
+    };
+    auto wait_ctl = [&](u64 seq) {
         if (g.spin_sync) {
             const auto t0 = std::chrono::steady_clock::now();
             while (__atomic_load_n(v.hseq, __ATOMIC_ACQUIRE) != seq) {
@@ -2075,6 +2078,7 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
             PJ_HIP(hipStreamSynchronize(s));
         }
     };
+    auto sync_ctl = [&]() { wait_ctl(publish_ctl()); };
     auto slot = [&](int c) {
         u64 t = 0;
         for (int i = 0; i < V2_NSH; ++i) t += v.hctl->cnt[c][i].v;
@@ -2182,7 +2186,7 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
             int K = g.round_batch;
             for (;;) {
                 const u64 pull_thresh = can_pull_light ? (u64)((double)light_left / light_pull) : ~0ull;
-                for (int q = 0; q < K; ++q) {
+                auto round = [&]() {
                     u64* fin = v.f[fi].p;
                     u64* fout = v.f[(fi + 1) % 3].p;
                     u64* fclr = v.f[(fi + 2) % 3].p;
@@ -2196,8 +2200,17 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
                     cs = (cs + 1) & 3;
                     hr = (hr + 1) % 3;
                     st.relax_rounds++;
-                }
-                sync_ctl();
+                };
+                for (int q = 0; q < K; ++q) round();
+                // spec_round: one more round enqueued behind the publish runs while the host waits
+                // for it -- the next round of the band, or an empty one (a launch that reads a zero
+                // count) when the band has ended; the ring state stays consistent either way, since
+                // every later step writes its frontier words whole and counts into a slot the rounds
+                // before zeroed
+                const int cpub = cs;
+                const u64 pseq = publish_ctl();
+                if (g.spec_round) round();
+                wait_ctl(pseq);
                 if (deferred) {
                     deferred = false;
                     if (slot(cs_start) == 0 && dpend) {  // empty, but deferred edges may land past it
@@ -2228,8 +2241,8 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
                     mh += v.hctl->mh[i].v;
                     ml += v.hctl->mh[i].pad[0];
                 }
-                if (slot(cs) == 0) break;
-                K = std::min(2 * K, 16);
+                if (slot(cpub) == 0) break;
+                K = std::max(1, std::min(2 * K, 16) - (g.spec_round ? 1 : 0));
             }
             if (finished) break;
             if (jumped) continue;  // (the select of the jumped-to band is enqueued)
