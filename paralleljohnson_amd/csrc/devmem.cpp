@@ -93,6 +93,18 @@ BigCache& cache() {
     return *c;
 }
 
+// test hook: with PJ_DEVMEM_POISON set, every allocation (a cached slice, or a small block the
+// driver may hand back from a recent free) starts full of 0xFF, so that a buffer relying on the
+// zeroed pages of fresh driver memory, or a kernel reading words its pass never wrote, shows up
+// (tests/test_partition.py, tests/test_gpu_parity.py); a device-wide wait after it: the memset
+// runs on the null stream, which does not order against libpj's non-blocking streams
+void poison(void* p, size_t bytes) {
+    if (p && bytes && std::getenv("PJ_DEVMEM_POISON")) {
+        PJ_HIP(hipMemset(p, 0xFF, bytes));
+        PJ_HIP(hipDeviceSynchronize());
+    }
+}
+
 }  // namespace
 
 void* dev_alloc(size_t bytes) {
@@ -109,6 +121,7 @@ void* dev_alloc(size_t bytes) {
             }
         }
         PJ_HIP(e);
+        poison(p, bytes);
         return p;
     }
     int dev = 0;
@@ -127,14 +140,7 @@ void* dev_alloc(size_t bytes) {
     }
     if (bb) {
         void* q = c.take(bb, bi, bytes);
-        // test hook: a cached slice handed out full of 0xFF, so that a buffer relying on the zeroed
-        // pages of fresh driver memory shows up (tests/test_partition.py)
-        // (a device-wide wait after it: the memset runs on the null stream, which does not order
-        // against libpj's non-blocking streams)
-        if (std::getenv("PJ_DEVMEM_POISON")) {
-            PJ_HIP(hipMemset(q, 0xFF, bytes));
-            PJ_HIP(hipDeviceSynchronize());
-        }
+        poison(q, bytes);
         return q;
     }
     const size_t bb_bytes = (bytes + SLACK - 1) / SLACK * SLACK + SLACK;

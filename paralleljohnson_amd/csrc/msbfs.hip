@@ -119,8 +119,13 @@ __device__ __forceinline__ void ms_add_fedges(MsCtl* c, int slot, u64 x) {
 __device__ __forceinline__ bool ms_is_push(const MsCtl* c, int32_t L, u64 push_max) {
     return ms_fedges(c, (L + 2) % 3) < push_max;
 }
+// (done first: once level D's prep finds level D-1 empty it returns before zeroing ring slot
+// (D+1) % 3, which still holds level D-2's 1, so without it level D+2 of a batch launched past
+// the end would run again on archive entries this pass never wrote -- recycled memory whose
+// row bitmap may hold bits past n, which the push takes as vertices: the intermittent illegal
+// address of round 6, test_multi_handle, the first batch of a freshly loaded graph)
 __device__ __forceinline__ bool ms_live(const MsCtl* c, int32_t L) {
-    return c->active[(L + 2) % 3] != 0 && L + 1 < INT_INF;
+    return c->done == 0 && c->active[(L + 2) % 3] != 0 && L + 1 < INT_INF;
 }
 
 template <int W>
@@ -298,7 +303,7 @@ __global__ __launch_bounds__(MB) void ms_push_k(i64 n, const Off* __restrict__ r
         if (PJ_MS_FZ) {
             const u64 zw = Z[base >> 6];
             if (!zw) continue;
-            if ((zw >> lane) & 1ull) f = mload<W>(F, u);
+            if (u < n && ((zw >> lane) & 1ull)) f = mload<W>(F, u);
         } else if (u < n) {
             f = mload<W>(F, u);
         }

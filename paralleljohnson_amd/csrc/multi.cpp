@@ -71,9 +71,9 @@ int per_rank(int world, F&& fn) {
 // fn(r) for every rank of a replicated batch: one host thread per GPU, running the ranks that
 // share it (world > visible GPUs) one after another. Each rank's batch fills the GPU by itself
 // (its solves run on their own streams), so several host threads driving one GPU's batches
-// gain nothing; with three ranks' batches driven at once on one GPU the suite saw intermittent
-// illegal-address faults (round 6, test_multi_handle[3]; not reproduced in isolation nor with
-// kernels serialized, cause not found), which this ordering also rules out. One rank per GPU
+// gain nothing. (The intermittent illegal address test_multi_handle showed in round 6 was not
+// this concurrency: it came back with the ranks in order, and was msbfs.hip's level ring
+// running again past a pass's end on unwritten archive entries; see ms_live.) One rank per GPU
 // (the product case) runs exactly as per_rank.
 template <typename F>
 int per_device(const pj_multi* m, F&& fn) {

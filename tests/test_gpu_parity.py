@@ -548,6 +548,32 @@ def test_msbfs_batch_rows(ctx, oracle, kind):
         assert (out[i] == oracle.bfs(row, col, r)).all(), (kind, i, r)
 
 
+def test_msbfs_levels_past_the_end_in_poisoned_memory(ctx, oracle, monkeypatch):
+    """Regression (round 6, the intermittent illegal address of test_multi_handle): the first
+    batch of a fresh graph launches 16 levels, far past a shallow pass's end, and its level
+    archive is whatever memory the allocator handed back. The level ring must stay ended once a
+    level finds nothing (no later level may run on entries the pass never wrote, whose row
+    bitmaps can hold bits past n). With PJ_DEVMEM_POISON every allocation starts full of 0xFF;
+    fresh graphs with n not a multiple of 64, 2-3 source batches (one out of range), rows equal
+    the oracle BFS."""
+    monkeypatch.setenv("PJ_DEVMEM_POISON", "1")
+    try:
+        for t, (kind, n) in enumerate([("hub", 2500), ("uniform", 3001), ("hub", 777), ("chain", 130)]):
+            rng = np.random.default_rng(4100 + t)
+            src, dst = random_graph(rng, kind, n)
+            row, col, _ = oracle.coo2csr(src.astype(np.uint32), dst.astype(np.uint32), n)
+            a, b = (int(src[0]), int(src[len(src) // 2])) if len(src) else (1, 2)
+            for sources in ([a, n + 5], [0, n - 1, b]):
+                g = ctx.load_coo(src, dst, n=n)
+                for _ in range(2):  # (the second batch starts from the first one's level count)
+                    out = g.sssp_batch(sources)
+                    for i, r in enumerate(sources):
+                        assert (out[i] == oracle.bfs(row, col, r)).all(), (kind, n, sources, i)
+                g.close()
+    finally:
+        monkeypatch.delenv("PJ_DEVMEM_POISON")
+
+
 @pytest.mark.parametrize("streams", [1, 2, 3])
 def test_msbfs_stream_slots(ctx, oracle, tmp_path, streams):
     """Batched BFS passes on 1-3 concurrent slots (msbfs.hip: one stream, mask set and distance
