@@ -141,6 +141,8 @@ struct Graph_d {
     const u32* col;
     const Off* crow;
     const u32* ccol;
+    const u64* hf2;  // (option pull_first) per vertex its in-row's first two entries, ccol[crow[v]] in the
+                     // low half and ccol[crow[v] + 1] in the high half (~0u past the row's end); else null
 };
 
 struct Decision {
@@ -872,12 +874,24 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
                         e[j] = g.crow[v[j] + 1];
                     }
                 // probes, stage A: the first PB1 in-edges of every candidate (independent
-                // loads); most vertices of a dense pull level find a parent here
+                // loads); most vertices of a dense pull level find a parent here. With the
+                // dense copy hf2 the candidates' ids come 8 bytes per vertex from consecutive
+                // addresses, instead of one in-row start (a line of its own) per candidate.
                 u32 u[RPI][PB1];
+                static_assert(PB1 == 2, "hf2 holds two in-neighbours");
+                if (g.hf2) {
 #pragma unroll
-                for (int j = 0; j < RPI; ++j)
+                    for (int j = 0; j < RPI; ++j) {
+                        const u64 h = act[j] ? g.hf2[v[j]] : ~0ull;
+                        u[j][0] = (u32)h;
+                        u[j][1] = (u32)(h >> 32);
+                    }
+                } else {
 #pragma unroll
-                    for (int p = 0; p < PB1; ++p) u[j][p] = (b[j] + p < e[j]) ? g.ccol[b[j] + p] : 0u;
+                    for (int j = 0; j < RPI; ++j)
+#pragma unroll
+                        for (int p = 0; p < PB1; ++p) u[j][p] = (b[j] + p < e[j]) ? g.ccol[b[j] + p] : 0u;
+                }
                 bool open_any = false;
 #pragma unroll
                 for (int j = 0; j < RPI; ++j) {
@@ -1114,6 +1128,16 @@ __global__ void hub_first_keys_k(const Off* __restrict__ crow, const u32* __rest
     }
 }
 
+// hf2[v] = the first two entries of in-row v (~0u for the missing ones)
+template <typename Off>
+__global__ void first_in_k(const Off* __restrict__ crow, const u32* __restrict__ ccol, i64 n, u64* __restrict__ hf2) {
+    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (i64)gridDim.x * blockDim.x) {
+        const Off b = crow[v], e = crow[v + 1];
+        const u32 x0 = b < e ? ccol[b] : ~0u, x1 = b + 1 < e ? ccol[b + 1] : ~0u;
+        hf2[v] = (u64)x0 | ((u64)x1 << 32);
+    }
+}
+
 int edge_bits(i64 nnz) {
     int b = 1;
     while (b < 63 && ((u64)1 << b) <= (u64)nnz) ++b;
@@ -1134,6 +1158,8 @@ struct BfsWorkHolder {
     int64_t* host_dev = nullptr;  // their device address
     int32_t last_launches = 0;  // level launches the previous solve used: sizes the first batch
     i64 n_live = 0;             // vertices with an edge (not in zmask)
+    DevBuf<u64> hf2;            // (pull_first) the first two entries of every in-row of hf2_src
+    const u32* hf2_src = nullptr;
     ~BfsWorkHolder() {
         if (host) (void)hipHostFree(host);
     }
@@ -1202,7 +1228,16 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     }
     a.host = w.host_dev;
     Graph_d<Off> gd{static_cast<const Off*>(g.row_ptr()), g.col.p, static_cast<const Off*>(g.crow_ptr()),
-                    pull_ccol(g)};
+                    pull_ccol(g), nullptr};
+    if (g.pull_first && n > 0) {  // (built once per in-row order: hub_first may switch it)
+        if (w.hf2_src != gd.ccol) {
+            w.hf2.ensure((size_t)n);
+            first_in_k<Off><<<grid_for(n, 256, (unsigned)ctx.cu_count * 8u), 256, 0, s>>>(gd.crow, gd.ccol, n, w.hf2.p);
+            PJ_LAUNCH_CHECK();
+            w.hf2_src = gd.ccol;
+        }
+        gd.hf2 = w.hf2.p;
+    }
 #if PJ_BFS_STAMPS
     static DevBuf<u64> stamps;
     stamps.ensure(64 * 64);

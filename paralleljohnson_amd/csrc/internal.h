@@ -262,6 +262,8 @@ struct Graph {
                          // first (built at the first solve; K22 0.2305 -> 0.1991 ms median kernel time, pull
                          // probes 21.8M -> 16.2M per 4 roots; web-Google and MS1024 equal or slightly faster,
                          // profiles/r06/bfs_hub_first_r6e.txt)
+    int pull_first = 1;  // BFS pull levels: the first two in-neighbours of every row from a dense copy (8 bytes
+                         // per vertex, read coalesced) instead of one row-start line per candidate
     int bfs_spare = 0;   // BFS: launches beyond the previous solve's count in the first batch (1 measured
                          // 2-3% slower on K22: the spare launch costs more than the occasional round trip)
     int max_levels = 0;  // debug: truncate the BFS after this many levels (0 = off)

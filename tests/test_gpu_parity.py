@@ -93,13 +93,15 @@ def test_bfs_random_graphs(ctx, oracle, kind, direction, small):
         roots = [int(src[0]) if len(src) else 0, int(rng.integers(0, n)), n, -5]
         for r in roots:
             exp = oracle.bfs(row, col, r)
-            for hf, pv in ((0, 0), (1, 0), (1, 2), (1, 0.1)):
+            for hf, pv, pf in ((0, 0, 1), (1, 0, 1), (1, 2, 1), (1, 0.1, 1), (1, 2, 0), (0, 0.1, 0)):
                 # (file-order in-rows, then the hub-first copy the pull levels probe; the
-                # vertex-count direction rule off, at its default and eager)
+                # vertex-count direction rule off, at its default and eager; the pulls' first
+                # two probes from the dense copy of the rows' first entries, or from the rows)
                 g.set_option("hub_first", hf)
                 g.set_option("pull_vertex", pv)
+                g.set_option("pull_first", pf)
                 d = g.sssp(r)
-                assert (d == exp).all(), (kind, direction, trial, r, hf, pv)
+                assert (d == exp).all(), (kind, direction, trial, r, hf, pv, pf)
         g.close()
 
 
@@ -163,9 +165,11 @@ def test_bfs_kronecker(ctx, oracle, scale):
         assert (d == exp).all()
         for direction in (1, 2, 0):  # push only, pull whenever possible, automatic
             g.set_option("direction", direction)
-            for hf in (1, 0):
+            for hf, pf in ((1, 1), (0, 1), (1, 0)):
                 g.set_option("hub_first", hf)
-                assert (g.sssp(int(r)) == exp).all(), (direction, hf)
+                g.set_option("pull_first", pf)
+                assert (g.sssp(int(r)) == exp).all(), (direction, hf, pf)
+            g.set_option("pull_first", 1)
         st = g.reach_stats()
         reached = exp < INF
         assert st["reached"] == reached.sum()
