@@ -88,7 +88,8 @@ for st in "${LIST[@]}"; do
       python3 tools/k22_level_table.py "$KO" "$CAL" > "$KO/k22_levels.txt" 2>&1 || { echo "level table failed"; cat "$KO/k22_levels.txt"; exit 1; }
       tail -8 "$KO/k22_levels.txt" ;;
     probe)
-      timeout -k 10 240 python3 -u $arg > "$OUT/probe_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-24)_$(echo "$arg" | md5sum | cut -c1-6).log" 2>&1 \
+      PN=$((PN + 1))  # (a step number: repeated probes of one command keep their logs)
+      timeout -k 10 240 python3 -u $arg > "$OUT/probe_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-24)_$(echo "$arg" | md5sum | cut -c1-6)_$PN.log" 2>&1 \
         || { echo "probe failed: $arg"; exit 1; } ;;
     vtests)
       v=${arg%%:*}; targs=${arg#*:}
