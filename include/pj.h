@@ -57,8 +57,9 @@ typedef struct pj_stats {
     int64_t levels;          /* BFS levels / delta-stepping buckets processed */
     int64_t td_levels;       /* top-down (push) levels */
     int64_t bu_levels;       /* bottom-up (pull) levels */
-    int64_t reached;         /* n_r: vertices with dist < PJ_INT_INF (filled by pj_reach_stats) */
-    int64_t reached_edges;   /* m_r: sum of out-degree over reached vertices (pj_reach_stats) */
+    int64_t reached;         /* n_r: vertices with dist < PJ_INT_INF (filled by pj_reach_stats; a unit-weight
+                                single-source solve fills it from its levels' counters) */
+    int64_t reached_edges;   /* m_r: sum of out-degree over reached vertices (likewise) */
     int64_t relax_rounds;    /* weighted: light/heavy relaxation rounds */
     /* weighted (delta-stepping): the work of the relaxation kernels, counted on the device in
      * every solve -- the analogue of the reference's edge scans (the loop of

@@ -1783,6 +1783,8 @@ int pj_part_set_option(pj_part* p, const char* key, double value) {
     else if (k == "beta" && value > 0) prm.beta = value;
     else if (k == "direction" && (value == 0 || value == 1 || value == 2)) prm.force = (int)value;
     else if (k == "exchange_cap" && (value == -1 || value == 0 || value >= 64)) prm.xcap = (i64)value;
+    else if (k == "single_gpu" && (value == 0 || value == 1))
+        part_single_gpu(*reinterpret_cast<Part*>(p)) = (int)value;
     else return arg_error("pj_part_set_option: unknown key or bad value");
     return PJ_OK;
 }
@@ -1792,6 +1794,10 @@ int pj_part_bfs(pj_part* p, pj_comm* comm, int64_t source, pj_part_stats* st) {
     return guarded([&] {
         bind(part_ctx(*reinterpret_cast<Part*>(p)));
         Part& P = *reinterpret_cast<Part*>(p);
+        if (part_single(P) && comm->c->world == 1) {
+            part_solve_single(P, source, st);
+            return (int)PJ_OK;
+        }
         BfsSteps& S = part_steps(P);
         bool& iso = part_iso_ready(P, comm->c.get());
         bfs_engine(S, *comm->c, source, part_params(P), iso, st);

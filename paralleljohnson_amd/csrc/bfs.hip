@@ -93,7 +93,8 @@ struct LevelState {
     double m_u;    // Beamer: in-edges of unvisited vertices
     u64 prev_found;
     double n_u;    // unvisited vertices with an edge (the pull level's candidates: pull_vertex rule)
-    u64 pad[4];
+    u64 nr, mr;    // reached vertices and their out-edges, summed over the levels whose counters were read
+    u64 pad[2];
 };
 
 struct BfsArgs {
@@ -116,7 +117,8 @@ struct BfsArgs {
     LevelState* S;  // [2]
     u64* nmode;     // [2] push / pull levels run (device)
     int64_t* host;  // mapped host words: [0] levels run (-1 while running), [1] push, [2] pull, [3] launches,
-                    // [4] edges scanned (push: every frontier out-edge; pull: every in-edge probed)
+                    // [4] edges scanned (push: every frontier out-edge; pull: every in-edge probed),
+                    // [5] reached vertices, [6] their out-edges (n_r, m_r: the levels' counters summed)
     u64* wtot;      // device: edges scanned by the levels so far (block 0 of each launch adds the last one's)
     u64* llog;      // level_log option: per launch (L, mode | kind << 8, frontier, its out-edges, found, scanned
                     // by the previous launch), or null
@@ -149,6 +151,7 @@ struct Decision {
     int32_t L;  // the level this launch computes
     int32_t mode, vsel, prev_mode;
     double m_u, n_u;
+    u64 nr, mr;  // LevelState::nr / mr with the previous launch's counters added
     u64 found;
     u64 nseg[NQS];
     u64 nh, he, mq;
@@ -171,6 +174,8 @@ __device__ __forceinline__ int decide(const BfsArgs& a, int32_t li, Decision& d)
     d.n_u = ps.n_u;
     d.found = ps.prev_found;
     d.nh = d.he = d.mq = 0;
+    d.nr = ps.nr;
+    d.mr = ps.mr;
     if (ps.done) return 0;
     u64 nn = 0;
 #pragma unroll
@@ -191,6 +196,8 @@ __device__ __forceinline__ int decide(const BfsArgs& a, int32_t li, Decision& d)
     }
     d.mq = mq;
     d.found = fd;
+    d.nr += fd;
+    d.mr += mq;
     d.m_u = ps.m_u - (double)in;
     d.n_u = ps.n_u - (double)fd;
     if (fz == 0 || L + 1 >= INT_INF || L >= a.max_levels) return 1;
@@ -421,6 +428,7 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
     int32_t L = d.L;
     double m_u = d.m_u, n_u = d.n_u;
     u64 fprev = d.found, nlev = 0;
+    u64 nr = d.nr, mr = d.mr;  // (plus the levels this launch consumes itself)
     for (;;) {
         __syncthreads();
         bfs_stamp(a, li, 2 + 3 * (int)nlev);
@@ -521,6 +529,8 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
             }
             F = NF;
             fprev = f;
+            nr += f;
+            mr += mq;
             m_u = m_u2;
             n_u -= (double)f;
             L = L2;
@@ -537,10 +547,14 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
                 s.m_u = m_u2;
                 s.n_u = n_u - (double)f;
                 s.prev_found = f;
+                s.nr = nr + f;
+                s.mr = mr + mq;
                 a.host[1] = (int64_t)a.nmode[0];
                 a.host[2] = (int64_t)a.nmode[1];
                 a.host[3] = (int64_t)li + 1;
                 a.host[4] = (int64_t)*a.wtot;
+                a.host[5] = (int64_t)(nr + f);
+                a.host[6] = (int64_t)(mr + mq);
                 __atomic_store_n(&a.host[0], (int64_t)L2, __ATOMIC_RELEASE);
             }
             return;
@@ -601,6 +615,8 @@ __device__ void small_levels(const BfsArgs& a, const Graph_d<Off>& g, const Deci
             s.m_u = m_u;
             s.n_u = n_u;
             s.prev_found = fprev;
+            s.nr = nr;  // (level L's own counts go to C: the next launch's decide adds them)
+            s.mr = mr;
         }
         return;
     }
@@ -661,12 +677,16 @@ __global__ __launch_bounds__(TB) void bfs_level_k(BfsArgs a, Graph_d<Off> g, int
             s.m_u = d.m_u;
             s.n_u = d.n_u;
             s.prev_found = d.found;
+            s.nr = d.nr;
+            s.mr = d.mr;
             if (go) a.nmode[d.mode] += 1;
             if (dec == 1) {
                 a.host[1] = (int64_t)a.nmode[0];
                 a.host[2] = (int64_t)a.nmode[1];
                 a.host[3] = (int64_t)li + 1;
                 a.host[4] = (int64_t)*a.wtot;
+                a.host[5] = (int64_t)d.nr;
+                a.host[6] = (int64_t)d.mr;
                 __atomic_store_n(&a.host[0], (int64_t)L, __ATOMIC_RELEASE);
             }
         }
@@ -1303,6 +1323,9 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
         // (an 8-byte bitmap word; the N-bit bitmap stays in the L2s)
         st.scanned_edges = st.probes = ((volatile int64_t*)w.host)[4];
         st.work_bytes = 4 * st.scanned_edges + 8 * st.probes;
+        // n_r and m_r from the levels' counters (what pj_reach_stats computes with a pass of its own)
+        st.reached = ((volatile int64_t*)w.host)[5];
+        st.reached_edges = ((volatile int64_t*)w.host)[6];
     }
     g.stats = st;
     g.have_result = true;

@@ -212,6 +212,9 @@ const Ctx& part_ctx(const Part& p);
 const Ctx& wpart_ctx(const WPart& p);
 int wpart_world(const WPart& p);
 // world 1 (option "single_gpu", default on): the solve runs delta.hip's single-GPU solver
+bool part_single(const Part& p);  // world 1 with option single_gpu: bfs.hip's solver (part_solve_single)
+int& part_single_gpu(Part& p);
+void part_solve_single(Part& p, i64 source, pj_part_stats* st);
 bool wpart_single(const WPart& p);
 int& wpart_single_gpu(WPart& p);
 int& wpart_pull_fmin(WPart& p);  // light pulls' frontier-minimum bound (option "pull_fmin", default 1)

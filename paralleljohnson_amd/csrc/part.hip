@@ -42,6 +42,7 @@
 //          MPI_Allreduce termination test at :589-590) and all-gathers the vis
 //          slices before pull levels.
 #include <chrono>
+#include <memory>
 #include <cmath>
 #include <thread>
 
@@ -557,6 +558,8 @@ struct Part {
     i64 pw_lo = 0, pw_span = 0;  // the piece the next part_pack packs (span 0: the whole level)
     int32_t level = 0;
     std::unique_ptr<BfsSteps> steps;  // engine view with its own exchange buffers (lazy)
+    int single_gpu = 1;               // world 1: solve with bfs.hip's single-GPU BFS (part_solve_single)
+    std::unique_ptr<Graph> g1;        // (its Graph: borrows this partition's rows for each solve)
     const Comm* iso_comm = nullptr;   // transport the replicated isolated mask was gathered over
     bool iso_ok = false;
     BfsParams prm;
@@ -1135,6 +1138,57 @@ struct PartGpuSteps final : BfsSteps {
 };
 
 }  // namespace
+
+// World 1: the one rank owns every vertex and its rows are the whole CSR (and CSC), so the
+// solve is bfs.hip's -- the single-GPU path's level kernels (hub-first in-rows, the dense first
+// in-neighbours, one-workgroup small levels, launch batches), not this file's level loop -- on
+// a Graph that borrows the partition's row arrays and distance array for the solve (swapped in
+// and out, no copy). Its workspace and derived rows stay with it for the next solve. The
+// distances land in p.dist, so the gather, the reach pass and the step API see them as the
+// level loop's. Option "single_gpu" 0 keeps the level loop (what every rank runs at world > 1).
+void part_solve_single(Part& p, i64 source, pj_part_stats* st) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!p.g1) {
+        auto g = std::make_unique<Graph>();
+        g->ctx = p.ctx;
+        g->n = p.n;
+        g->nnz = p.nnz_local;
+        g->symmetric = p.symmetric;
+        g->off64 = p.off64;
+        p.g1 = std::move(g);
+    }
+    Graph& g = *p.g1;
+    g.alpha = p.prm.alpha;
+    g.beta = p.prm.beta;
+    g.force_mode = p.prm.force;
+    struct Lend {  // the partition's arrays in the Graph for the solve, back on every exit
+        Part& p;
+        Graph& g;
+        void swap_all() {
+            std::swap(p.row32, g.row32);
+            std::swap(p.row64, g.row64);
+            std::swap(p.col, g.col);
+            std::swap(p.crow32, g.crow32);
+            std::swap(p.crow64, g.crow64);
+            std::swap(p.ccol, g.ccol);
+            std::swap(p.dist, g.dist);
+        }
+        Lend(Part& pp, Graph& gg) : p(pp), g(gg) { swap_all(); }
+        ~Lend() { swap_all(); }
+    } lend(p, g);
+    bfs_solve(g, source);
+    if (st) {
+        *st = pj_part_stats{};
+        st->solve_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        st->levels = g.stats.levels;
+        st->td_levels = g.stats.td_levels;
+        st->bu_levels = g.stats.bu_levels;
+        st->reached = g.stats.reached;
+        st->reached_edges = g.stats.reached_edges;
+    }
+}
+bool part_single(const Part& p) { return p.world == 1 && p.single_gpu; }
+int& part_single_gpu(Part& p) { return p.single_gpu; }
 
 BfsSteps& part_steps(Part& p) {
     if (!p.steps) p.steps.reset(new PartGpuSteps(p));

@@ -102,6 +102,9 @@ def test_bfs_random_graphs(ctx, oracle, kind, direction, small):
                 g.set_option("pull_first", pf)
                 d = g.sssp(r)
                 assert (d == exp).all(), (kind, direction, trial, r, hf, pv, pf)
+                st = g.stats()  # (n_r, m_r from the levels' counters, small levels included)
+                reached = exp < INF
+                assert (st["reached"], st["reached_edges"]) == (int(reached.sum()), int(np.diff(row)[reached].sum()))
         g.close()
 
 

@@ -254,19 +254,29 @@ def _group(pj, world, transport="host"):
 @pytest.mark.parametrize("transport", ["self", "rccl"])
 def test_part_world1_gpu(ctx, oracle, force, transport):
     """pj_part_bfs at world 1: no transport, and a one-rank RCCL group (the RCCL calls
-    of the loop -- allreduce, allgather, grouped send/recv -- with nothing to send)."""
+    of the loop -- allreduce, allgather, grouped send/recv -- with nothing to send). Option
+    single_gpu 1 (default) solves with bfs.hip's single-GPU BFS on the partition's borrowed
+    rows, 0 with the level loop; both alternate on one partition (the arrays go back after
+    each borrowed solve)."""
     from paralleljohnson_amd.partition import Comm, load_coo
     comm = Comm.for_rank(ctx, 1, 0, Comm.unique_id() if transport == "rccl" else None)
     assert comm.kind == transport
     for kind, n, s, d in _cases():
         ops = load_coo(ctx, s, d, n, 0, 1, symmetric=(kind == "sym"))
         ops.set_option("direction", force)
+        row, _, _ = _csr(oracle, s, d, n)
         for source in (0, n // 3, n - 1, n + 5, -1):
-            st = ops.bfs(comm, source)
-            got = ops.gather_dist(comm)
             exp = _oracle_dist(oracle, s, d, n, source)
-            assert np.array_equal(got, exp), (kind, source, force)
-            assert st["reached"] == int(np.sum(exp < INF)) and ops.reach()[0] == st["reached"]
+            reached = exp < INF
+            for single in (1, 0):
+                ops.set_option("single_gpu", single)
+                st = ops.bfs(comm, source)
+                got = ops.gather_dist(comm)
+                assert np.array_equal(got, exp), (kind, source, force, single)
+                assert st["reached"] == int(reached.sum()) and ops.reach()[0] == st["reached"]
+                assert st["reached_edges"] == int(np.diff(row)[reached].sum()), (kind, source, force, single)
+                if force == 1:
+                    assert st["bu_levels"] == 0
         ops.close()
     comm.close()
 
@@ -281,13 +291,16 @@ def test_part_kronecker_matches_single_gpu(ctx, pj, oracle):
     comm = Comm.for_rank(ctx, 1, 0)
     assert ops.nnz_local == g.nnz
     for r in g.sample_roots(5, 4):
-        st = ops.bfs(comm, int(r))
-        got = ops.gather_dist(comm)
-        assert np.array_equal(got, g.sssp(int(r))), r
-        assert np.array_equal(got, oracle.bfs(row, col.view(np.uint32), int(r))), r
-        rs = g.reach_stats()
-        assert (st["reached"], st["reached_edges"]) == (rs["reached"], rs["reached_edges"])
-        assert st["td_levels"] >= 1 and st["bu_levels"] >= 1  # both directions exercised
+        exp = oracle.bfs(row, col.view(np.uint32), int(r))
+        for single in (1, 0):  # (bfs.hip on the borrowed rows, then the level loop)
+            ops.set_option("single_gpu", single)
+            st = ops.bfs(comm, int(r))
+            got = ops.gather_dist(comm)
+            assert np.array_equal(got, g.sssp(int(r))), (r, single)
+            assert np.array_equal(got, exp), (r, single)
+            rs = g.reach_stats()
+            assert (st["reached"], st["reached_edges"]) == (rs["reached"], rs["reached_edges"])
+            assert st["td_levels"] >= 1 and st["bu_levels"] >= 1  # both directions exercised
     ops.close()
     g.close()
 
