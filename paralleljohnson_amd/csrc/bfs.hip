@@ -1221,7 +1221,6 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     a.nwords = nwords;
     a.eb = edge_bits(g.nnz);
     a.alpha = g.alpha;
-    a.pv = g.pull_vertex;
     a.beta = g.beta;
     a.force = g.force_mode;
     a.small = g.bfs_small;
@@ -1249,6 +1248,11 @@ void bfs_run(Graph& g, BfsWorkHolder& w, i64 source) {
     a.host = w.host_dev;
     Graph_d<Off> gd{static_cast<const Off*>(g.row_ptr()), g.col.p, static_cast<const Off*>(g.crow_ptr()),
                     pull_ccol(g), nullptr};
+    // the vertex-count rule's cost model (a pull probes ~2 in-edges per unvisited vertex) holds for
+    // hub-first in-rows only: without them (option off, or nnz >= 2^32) Beamer's rule alone. On
+    // Kronecker s28 (no hub-first copy) one bench root's second level pulled 1.19G in-edges in
+    // 20.6 ms under it, against a 9 ms push (profiles/r06/k28_single_r6y.txt)
+    a.pv = (g.hub_first && g.ccol_hf.p && gd.ccol == g.ccol_hf.p) ? g.pull_vertex : 0.0;
     if (g.pull_first && n > 0) {  // (built once per in-row order: hub_first may switch it)
         if (w.hf2_src != gd.ccol) {
             w.hf2.ensure((size_t)n);

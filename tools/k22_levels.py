@@ -4,8 +4,9 @@ then ROOTS solves run with the level_log option: libpj prints one stderr line pe
 (level, push / pull, where the frontier came from, its vertices and out-edges, and the in-edge
 probes the previous launch scanned). tools/cycle.sh `klevels` runs this under the kernel trace
 and --pmc passes; tools/k22_level_table.py joins them launch by launch.
-Usage: python tools/k22_levels.py [roots=4] [graph=wg] [opt=value ...]  (graph=wg: configs[0]'s
-web-Google-shaped graph, source 0 and sampled roots)"""
+Usage: python tools/k22_levels.py [roots=4] [graph=wg|kNN] [rootlist=a/b/...] [opt=value ...]  (graph=wg:
+configs[0]'s web-Google-shaped graph, source 0 and sampled roots; kNN: Kronecker scale NN; rootlist: these
+roots instead of the sampled ones)"""
 import os
 import sys
 
@@ -16,11 +17,15 @@ import paralleljohnson_amd as pj  # noqa: E402
 nroots = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 opts = dict(kv.split("=") for kv in sys.argv[2:])
 ctx = pj.Context(0)
-wg = opts.pop("graph", "k22") == "wg"
-g = ctx.generate_webgraph() if wg else ctx.generate_kronecker(22, 16, 1)
+gname = opts.pop("graph", "k22")
+rootlist = opts.pop("rootlist", "")
+wg = gname == "wg"
+g = ctx.generate_webgraph() if wg else ctx.generate_kronecker(int(gname[1:]), 16, 1)
 for k, v in opts.items():
     g.set_option(k, float(v))
 roots = ([0] + [int(r) for r in g.sample_roots(2, nroots - 1)]) if wg else [int(r) for r in g.sample_roots(2, nroots)]
+if rootlist:
+    roots = [int(x) for x in rootlist.split("/")]
 g.sssp(roots[0], copy=False)  # (workspace; unlogged)
 g.set_option("level_log", 1)
 for r in roots:

@@ -1,7 +1,8 @@
 """The single-GPU BFS (bfs.hip) on configs[3]'s graph (Kronecker s28 ef16, unit weights, 2^33 entries),
 for comparison with the world-1 partitioned leg (part.hip, secondary.k28_partitioned): the bench's roots
 (sample_roots seed 4, 4 roots), mean / median kernel ms and GTEPS by the reached edges.
-Usage: python tools/k28_bfs_time.py [scale=28] [key=value ...]  (libpj graph options)"""
+Usage: python tools/k28_bfs_time.py [scale=28] [rootlist=a/b/..] [key=value ...]  (libpj graph options;
+rootlist: these roots instead)"""
 import os
 import sys
 import time
@@ -14,13 +15,14 @@ import paralleljohnson_amd as pj  # noqa: E402
 
 opts = dict(kv.split("=") for kv in sys.argv[1:])
 scale = int(opts.pop("scale", "28"))
+rootlist = opts.pop("rootlist", "")
 ctx = pj.Context(0)
 t0 = time.time()
 g = ctx.generate_kronecker(scale, 16, 1)
 print(f"s{scale}: n {g.n} nnz {g.nnz} built in {time.time() - t0:.2f} s", flush=True)
 for k, v in opts.items():
     g.set_option(k, float(v))
-roots = [int(r) for r in g.sample_roots(4, 4)]
+roots = [int(x) for x in rootlist.split("/")] if rootlist else [int(r) for r in g.sample_roots(4, 4)]
 g.sssp(roots[0], copy=False)  # (workspace)
 ts, te = [], []
 for rep in range(3):
