@@ -2209,7 +2209,7 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
                 // before zeroed
                 const int cpub = cs;
                 const u64 pseq = publish_ctl();
-                if (g.spec_round) round();
+                for (int q = 0; q < g.spec_round; ++q) round();
                 wait_ctl(pseq);
                 if (deferred) {
                     deferred = false;
@@ -2242,7 +2242,7 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
                     ml += v.hctl->mh[i].pad[0];
                 }
                 if (slot(cpub) == 0) break;
-                K = std::max(1, std::min(2 * K, 16) - (g.spec_round ? 1 : 0));
+                K = std::max(1, std::min(2 * K, 16) - g.spec_round);
             }
             if (finished) break;
             if (jumped) continue;  // (the select of the jumped-to band is enqueued)

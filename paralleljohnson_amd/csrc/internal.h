@@ -254,7 +254,7 @@ struct Graph {
     int hub_gpc = 4;       // kernels' 24); swept (24,24) (6,7) (12,14) (12,7) (12,4) (16,7): (12,4) best
     int heavy_gpc = 0;     // delta v2: workgroups per CU of the heavy pull (0 = 24; 7-32 swept, 12-32 equal)
     int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)
-    int spec_round = 1;  // delta v2: one more light round enqueued behind each check's publish (0/1)
+    int spec_round = 1;  // delta v2: light rounds enqueued behind each check's publish (0-2)
     int batch_streams = 2; // weighted batches (pj_sssp_batch*): solves in flight at once, one stream each
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
     int bfs_small = 1;   // BFS: one workgroup runs the levels of small push frontiers (bfs.hip small_levels)

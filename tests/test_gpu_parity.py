@@ -400,7 +400,7 @@ def test_weighted_band_width(ctx, oracle, scale, ef):
             g.set_option("tail_after", ta)
             g.set_option("tail_frac", 2.0 if td else 0.0)  # (switch as soon as tail_after allows)
             for r in roots:
-                for sr in (0, 1):
+                for sr in (0, 1, 2):
                     g.set_option("spec_round", sr)
                     assert (g.sssp(r) == exp[r]).all(), (pf, lp, delta, bw, td, ta, r, sr)
     g.close()
@@ -434,7 +434,7 @@ def test_weighted_defer_heavy(ctx, oracle, scale, ef):
                 g.set_option("tail_frac", tf)
                 g.set_option("defer_check", dc)
                 for r in roots:
-                    for sr in (0, 1):  # (spec_round: a light round enqueued behind every check's publish)
+                    for sr in (0, 1, 2):  # (spec_round: light rounds enqueued behind every check's publish)
                         g.set_option("spec_round", sr)
                         assert (g.sssp(r) == exp[r]).all(), (dh, pf, delta, bw, tf, dc, r, sr)
                         pushed_any |= dh > 0 and g.stats()["td_levels"] > 0
