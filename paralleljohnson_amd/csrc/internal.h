@@ -251,9 +251,11 @@ struct Graph {
     int spin_sync = 1;     // delta v2: the host spins on a published sequence word instead of a stream sync (0/1)
     int defer_check = 1;   // delta v2: no host check right after a heavy step (0/1)
     int round_gpc = 12;    // delta v2: workgroups per CU of the light-round / hub launches (0 = the heavy
-    int hub_gpc = 4;       // kernels' 24); swept (24,24) (6,7) (12,14) (12,7) (12,4) (16,7): (12,4) best
+    int hub_gpc = 3;       // kernels' 24); swept (24,24) (6,7) (12,14) (12,7) (12,4) (16,7): (12,4) best; with
+                           // spec_round and round_batch 1, hub 3 +0.5% (profiles/r06/round_batch_ab_r6ab.txt)
     int heavy_gpc = 0;     // delta v2: workgroups per CU of the heavy pull (0 = 24; 7-32 swept, 12-32 equal)
-    int round_batch = 2; // delta v2: light rounds enqueued per host check at a band's start (at least)
+    int round_batch = 1; // delta v2: light rounds enqueued per host check at a band's start (at least; 2 until
+                         // spec_round: 1 then +1.2%, 3 -2.5%, profiles/r06/round_batch_ab_r6aa.txt / _r6ab.txt)
     int spec_round = 1;  // delta v2: light rounds enqueued behind each check's publish (0-2)
     int batch_streams = 2; // weighted batches (pj_sssp_batch*): solves in flight at once, one stream each
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)
