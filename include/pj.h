@@ -245,8 +245,8 @@ int pj_reach_stats(pj_graph* g, pj_stats* out);
  * (weighted batches: solves in flight, 1-8), defer_heavy (a heavy push of members
  * holding >= defer_heavy x nnz heavy edges relaxes the next band's part only and
  * leaves the rest to the next heavy step; 0 = off, default 0.002), spec_round (delta:
- * one more light round enqueued behind each band-end check, run while the host reads
- * it, 0/1, default 1) and the batch /
+ * light rounds enqueued behind each band-end check, run while the host reads it, 0-2,
+ * default 1) and the batch /
  * grid knobs documented in DESIGN.md §4.2b. Returns PJ_ERR_ARG on bad values. */
 int pj_set_option(pj_graph* g, const char* key, double value);
 
