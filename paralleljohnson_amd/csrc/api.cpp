@@ -1785,7 +1785,6 @@ int pj_part_set_option(pj_part* p, const char* key, double value) {
     else if (k == "exchange_cap" && (value == -1 || value == 0 || value >= 64)) prm.xcap = (i64)value;
     else if (k == "single_gpu" && (value == 0 || value == 1))
         part_single_gpu(*reinterpret_cast<Part*>(p)) = (int)value;
-    else if (k == "pull_first" && (value == 0 || value == 1)) prm.pull_first = (int)value;
     else return arg_error("pj_part_set_option: unknown key or bad value");
     return PJ_OK;
 }

@@ -194,7 +194,6 @@ struct BfsParams {
     double alpha = 14.0, beta = 24.0;
     int force = 0;  // 0 auto, 1 push only, 2 pull from level 1 on
     i64 xcap = -1;  // exchange buffer cap in ids per rank and direction (-1: block / 16; 0: none)
-    int pull_first = 1;  // part.hip pulls: the first probes from a dense copy of the in-rows' first entries
 };
 
 // The rank-local loops. `iso_ready` says the replicated isolated mask in

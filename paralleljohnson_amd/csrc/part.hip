@@ -71,8 +71,6 @@ struct PartD {
     const u32* col;
     const Off* crow;
     const u32* ccol;
-    const uint4* hf4;  // (option pull_first) per owned vertex its in-row's first PB1 entries (~0u past the
-                       // row's end), read 16 bytes per candidate from consecutive addresses; else null
 };
 
 __device__ __forceinline__ bool claim(u64* vis, u32 v) {
@@ -481,17 +479,8 @@ __global__ __launch_bounds__(TB) void part_pull_k(PartArgs a, PartD<Off> g, int3
             }
             bool fnd = false;
             u32 u[PB1];
-            static_assert(PB1 == 4, "hf4 holds four in-neighbours");
-            if (g.hf4) {  // (stage A from the dense copy: no line of the in-row's start per candidate)
-                const uint4 h = act ? g.hf4[v] : make_uint4(0u, 0u, 0u, 0u);
-                u[0] = h.x;
-                u[1] = h.y;
-                u[2] = h.z;
-                u[3] = h.w;
-            } else {
 #pragma unroll
-                for (int p = 0; p < PB1; ++p) u[p] = (b + p < e) ? g.ccol[b + p] : 0u;
-            }
+            for (int p = 0; p < PB1; ++p) u[p] = (b + p < e) ? g.ccol[b + p] : 0u;
 #pragma unroll
             for (int p = 0; p < PB1; ++p) fnd |= (b + p < e) && vbit(vis, u[p]);
             Off k = b + PB1;
@@ -528,21 +517,6 @@ __global__ __launch_bounds__(TB) void part_pull_k(PartArgs a, PartD<Off> g, int3
             }
         }
         if (mine) a.frn[wbase + lane] = (u64)newb[2 * lane] | ((u64)newb[2 * lane + 1] << 32);
-    }
-}
-
-// hf4[v] = the first PB1 entries of owned in-row v (~0u for the missing ones)
-template <typename Off>
-__global__ void part_first_in_k(const Off* __restrict__ crow, const u32* __restrict__ ccol, i64 nl,
-                                uint4* __restrict__ hf4) {
-    for (i64 v = (i64)blockIdx.x * blockDim.x + threadIdx.x; v < nl; v += (i64)gridDim.x * blockDim.x) {
-        const Off b = crow[v], e = crow[v + 1];
-        uint4 h;
-        h.x = b < e ? ccol[b] : ~0u;
-        h.y = b + 1 < e ? ccol[b + 1] : ~0u;
-        h.z = b + 2 < e ? ccol[b + 2] : ~0u;
-        h.w = b + 3 < e ? ccol[b + 3] : ~0u;
-        hf4[v] = h;
     }
 }
 
@@ -585,7 +559,6 @@ struct Part {
     int32_t level = 0;
     std::unique_ptr<BfsSteps> steps;  // engine view with its own exchange buffers (lazy)
     int single_gpu = 1;               // world 1: solve with bfs.hip's single-GPU BFS (part_solve_single)
-    DevBuf<uint4> hf4;                // (pull_first) the first PB1 entries of every owned in-row (lazy)
     std::unique_ptr<Graph> g1;        // (its Graph: borrows this partition's rows for each solve)
     const Comm* iso_comm = nullptr;   // transport the replicated isolated mask was gathered over
     bool iso_ok = false;
@@ -644,7 +617,6 @@ PartD<Off> part_d(const Part& p) {
     }
     d.col = p.col.p;
     d.ccol = p.symmetric ? p.col.p : p.ccol.p;
-    d.hf4 = p.prm.pull_first ? p.hf4.p : nullptr;
     return d;
 }
 
@@ -1073,13 +1045,6 @@ void part_apply(Part& p, int level, u64* vis, const u32* recv, i64 nr) {
 
 void part_pull(Part& p, int level, u64* vis) {
     hipStream_t s = p.ctx->stream;
-    if (p.prm.pull_first && !p.hf4.p && p.nl > 0) {  // (once per partition, at its first pull level)
-        p.hf4.alloc((size_t)p.nl);
-        const unsigned g4 = grid_for(p.nl, 256, (unsigned)p.ctx->cu_count * 8u);
-        if (p.off64) part_first_in_k<u64><<<g4, 256, 0, s>>>(part_d<u64>(p).crow, part_d<u64>(p).ccol, p.nl, p.hf4.p);
-        else part_first_in_k<u32><<<g4, 256, 0, s>>>(part_d<u32>(p).crow, part_d<u32>(p).ccol, p.nl, p.hf4.p);
-        PJ_LAUNCH_CHECK();
-    }
     PartArgs a = part_args(p, vis);
     const i64 nsc = (p.bw + SC - 1) / SC;
     const unsigned grid = grid_for(nsc, NW, (unsigned)p.ctx->cu_count * PJ_PART_GPC);

@@ -321,7 +321,6 @@ def test_part_group_one_gpu(pj, oracle, world, force, cap):
         for p in parts:
             p.set_option("direction", force)
             p.set_option("exchange_cap", cap)
-            p.set_option("pull_first", 1 if kind == "sym" else cap != 64)  # (dense first in-neighbours or not)
         row, _, _ = _csr(oracle, s, d, n)
         for source in (0, n // 3, n - 1, n + 5):
             st = bfs_group(parts, comms, source)
