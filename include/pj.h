@@ -239,9 +239,11 @@ int pj_reach_stats(pj_graph* g, pj_stats* out);
  * delta-stepping (0 = automatic: c(n) x mean weight / mean out-degree, c(n) =
  * 0.1875 log2(n) - 1.875 within [2, 3.5], swept on Kronecker s22-s26), direction (0 auto, 1 push, 2 pull),
  * bfs_small (one-workgroup levels for small frontiers, 0/1), hub_first (BFS pull levels
- * probe in-rows ordered highest-degree in-neighbour first, 0/1, default 1), pull_vertex
- * (BFS: push -> pull also when the frontier's out-edges exceed pull_vertex x the unvisited
- * vertices, default 2, 0 = Beamer's rule alone), batch_streams
+ * probe in-rows ordered highest-degree in-neighbour first, 0/1, default 1), pull_first (BFS
+ * pull levels take their first two probes from a dense copy of the in-rows' first entries,
+ * 0/1, default 1), pull_vertex (BFS: push -> pull also when the frontier's out-edges exceed
+ * pull_vertex x the unvisited vertices, default 2, 0 = Beamer's rule alone; applied only with
+ * hub-first in-rows), batch_streams
  * (weighted batches: solves in flight, 1-8), defer_heavy (a heavy push of members
  * holding >= defer_heavy x nnz heavy edges relaxes the next band's part only and
  * leaves the rest to the next heavy step; 0 = off, default 0.002), spec_round (delta:
@@ -538,7 +540,9 @@ typedef struct pj_part_stats {
  * hold; a push level with more goes out in pieces by word range of the owners' slices,
  * each piece its own count exchange, alltoallv and host wait; -1 = max(block / 16,
  * 4096) ids (default), 0 = no cap, else at least 64 ids: smaller caps are
- * PJ_ERR_ARG). Every rank must use the same values. */
+ * PJ_ERR_ARG), "single_gpu" (0/1, default 1: at world 1 the solve is the single-GPU BFS's,
+ * bfs.hip on the rank's rows, borrowed for the solve; the stats are its level counters').
+ * Every rank must use the same values. */
 int pj_part_bfs(pj_part* p, pj_comm* comm, int64_t source, pj_part_stats* st);
 int pj_part_set_option(pj_part* p, const char* key, double value);
 /* All ranks of a one-process group at once (one host thread per rank);
@@ -569,6 +573,7 @@ int pj_wpart_delta(pj_wpart* p, pj_comm* comm, int64_t source, int32_t delta, pj
  * and "tail_light_pull" (the same rule in the tail's bands, independent of light_pull, the
  * frontier map then 16-bit; 0 = push; default 3). Every rank must use the same values.
  * "single_gpu" (0/1, default 1: the world-1 solve runs delta.hip's v2, see pj_wpart_delta).
+ * "grid_per_cu" (this rank only): workgroups per CU of the grid-stride kernels, 1-32, default 8.
  * "queue_shard" (this rank only, any time between steps): the claim queue's shard
  * capacity in pairs from now on, >= 1 (64 shards; it still grows when a round
  * overflows it: tests use small values to run that path). */

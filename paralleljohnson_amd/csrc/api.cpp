@@ -1833,6 +1833,7 @@ int pj_wpart_set_option(pj_wpart* p, const char* key, double value) {
     else if (k == "tail_light_pull" && value >= 0) wpart_tail_light_pull(P) = value;
     else if (k == "single_gpu" && (value == 0 || value == 1)) wpart_single_gpu(P) = (int)value;
     else if (k == "pull_fmin" && (value == 0 || value == 1)) wpart_pull_fmin(P) = (int)value;
+    else if (k == "grid_per_cu" && value >= 1 && value <= 32) wpart_grid_per_cu(P) = (int)value;
     else if (k == "queue_shard" && value >= 1 && value <= 1e9)
         return guarded([&] {
             bind(wpart_ctx(P));

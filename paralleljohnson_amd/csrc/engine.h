@@ -217,6 +217,7 @@ int& part_single_gpu(Part& p);
 void part_solve_single(Part& p, i64 source, pj_part_stats* st);
 bool wpart_single(const WPart& p);
 int& wpart_single_gpu(WPart& p);
+int& wpart_grid_per_cu(WPart& p);  // workgroups per CU of its grid-stride kernels (option "grid_per_cu", default 8)
 int& wpart_pull_fmin(WPart& p);  // light pulls' frontier-minimum bound (option "pull_fmin", default 1)
 void wpart_solve_single(WPart& p, i64 source, int32_t delta, pj_part_stats* st);
 bool wpart_pending(const WPart& p);

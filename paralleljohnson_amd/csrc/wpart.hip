@@ -1232,7 +1232,8 @@ struct WPart {
     i64 fmin_own = INT_INF;             // this rank's frontier minimum (wpart_light_counts)
     i64 fmin_all = INT_INF;             // every rank's (DeltaSteps::set_frontier_min), or -1: none
     std::unique_ptr<Graph> g1;          // (its Graph over copies of the rows, built at the first solve)
-    unsigned grid() const { return (unsigned)ctx->cu_count * 8u; }
+    int gpc = 8;                        // workgroups per CU of the grid-stride kernels (option grid_per_cu)
+    unsigned grid() const { return (unsigned)ctx->cu_count * (unsigned)gpc; }
     unsigned qgrid() const {  // (region-major: the shards and the spill)
         return (unsigned)(WQ_S + 1) * std::max(1u, grid() / (unsigned)(WQ_S + 1));
     }
@@ -2265,6 +2266,7 @@ void wpart_solve_single(WPart& p, i64 source, int32_t delta, pj_part_stats* st) 
 bool wpart_single(const WPart& p) { return p.world == 1 && p.single_gpu; }
 int& wpart_single_gpu(WPart& p) { return p.single_gpu; }
 int& wpart_pull_fmin(WPart& p) { return p.pull_fmin; }
+int& wpart_grid_per_cu(WPart& p) { return p.gpc; }
 
 // ------------------------------------------------------------ engine view ---
 namespace {

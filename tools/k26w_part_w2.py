@@ -22,7 +22,7 @@ g = ctxs[0].generate_kronecker(scale, 16, 1, weighted=True)
 roots = [int(x) for x in g.sample_roots(2, 3)]
 g.close()
 parts = [load_weighted_kronecker(ctxs[r], scale, 16, 1, r, 2) for r in range(2)]
-base = {}
+base = {"grid_per_cu": 8}
 for ps in range(passes):
     for o in sets:
         for p in parts:
