@@ -2242,7 +2242,7 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
                     ml += v.hctl->mh[i].pad[0];
                 }
                 if (slot(cpub) == 0) break;
-                K = std::max(1, std::min((int)std::ceil(g.round_growth * K), 16) - g.spec_round);
+                K = std::max(1, std::min(2 * K, 16) - g.spec_round);
             }
             if (finished) break;
             if (jumped) continue;  // (the select of the jumped-to band is enqueued)
