@@ -318,6 +318,9 @@ struct V2Host {
     u64 work[V2W_N][3];      // work[k][*] (v, pad[0], pad[1]) summed: records, probes, bytes
 };
 constexpr int V2H_N = (int)(sizeof(V2Host) / sizeof(u64));
+#ifndef PJ_V2_FULLPUB
+#define PJ_V2_FULLPUB 0  // (A/B build switch: the publish also copies the whole block, as before)
+#endif
 // Waves per SIMD the compiler must fit the register budget to (0 = its own choice): the light
 // round kernel took 81-91 VGPRs (5 waves per SIMD); at 7 (72 VGPRs, 16 bytes of scratch per lane)
 // its latency-bound pulls keep more loads in flight: k26w 596 -> 643 GTEPS interleaved (6: 634,
@@ -1948,6 +1951,10 @@ __global__ __launch_bounds__(256) void v2_publish_k(V2Ctl* __restrict__ ctl, u64
         }
         host[t] = x;
     }
+    if (PJ_V2_FULLPUB) {
+        const u64* c = reinterpret_cast<const u64*>(ctl);
+        for (int i = t; i < (int)(sizeof(V2Ctl) / sizeof(u64)); i += 256) host[V2H_N + i] = c[i];
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence_system();
@@ -2000,7 +2007,8 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     v.hv.alloc(3 * v.hcap);  // the hub queue's ring of three slots
     v.hbeg.alloc(3 * v.hcap);
     v.hoff.alloc(3 * v.hcap);
-    PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hctl), sizeof(V2Host), hipHostMallocMapped));
+    PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hctl), sizeof(V2Host) + (PJ_V2_FULLPUB ? sizeof(V2Ctl) : 0),
+                         hipHostMallocMapped));
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&v.hctl_dev), v.hctl, 0));
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hseq), 64, hipHostMallocMapped | hipHostMallocCoherent));
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&v.hseq_dev), v.hseq, 0));
