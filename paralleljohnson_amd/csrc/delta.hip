@@ -308,19 +308,6 @@ struct V2Ctl {
     V2Line aux;             // v2_heavy_left_k's sum (the tail switch's heavy_left)
     V2Line work[V2W_N][V2_NSH];
 };
-// What the host reads of V2Ctl, reduced over the shards by v2_publish_k (200 bytes instead of the
-// block's ~10 KB of 64-byte lines: the publish's system-scope fence waits for fewer host writes)
-struct V2Host {
-    u64 cnt[4];              // cnt[c][*].v summed: the light rounds' marked frontier vertices (ring)
-    u64 mh, ml;              // mh[*].v / mh[*].pad[0] summed: the members' heavy / light degree sums
-    u64 minv;                // minv[*].v minimum
-    u64 aux;                 // aux.v
-    u64 work[V2W_N][3];      // work[k][*] (v, pad[0], pad[1]) summed: records, probes, bytes
-};
-constexpr int V2H_N = (int)(sizeof(V2Host) / sizeof(u64));
-#ifndef PJ_V2_FULLPUB
-#define PJ_V2_FULLPUB 0  // (A/B build switch: the publish also copies the whole block, as before)
-#endif
 // Waves per SIMD the compiler must fit the register budget to (0 = its own choice): the light
 // round kernel took 81-91 VGPRs (5 waves per SIMD); at 7 (72 VGPRs, 16 bytes of scratch per lane)
 // its latency-bound pulls keep more loads in flight: k26w 596 -> 643 GTEPS interleaved (6: 634,
@@ -1706,8 +1693,8 @@ struct DeltaSolve {
     DevBuf<u64> db;            // members whose far heavy edges are deferred (defer_heavy); all zero
     bool db_dirty = true;      // unless a solve stopped with a deferral pending (an error)
     DevBuf<V2Ctl> ctl;
-    V2Host* hctl = nullptr;    // mapped pinned host words, written by v2_publish_k
-    V2Host* hctl_dev = nullptr;
+    V2Ctl* hctl = nullptr;     // mapped pinned host copy, written by v2_publish_k
+    V2Ctl* hctl_dev = nullptr;
     u64* hseq = nullptr;       // mapped pinned sequence word of v2_publish_k
     u64* hseq_dev = nullptr;
     u64 seq = 0;
@@ -1924,37 +1911,15 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
     return delta;
 }
 
-// reduces the counter block into V2Host words in mapped host memory (thread t computes word
-// t over the shards), then (system-scope release) the sequence number the host spins on; then
-// resets the counters the host consumes per check (the members' degree sums mh, which the host
-// accumulates over a band's checks, and minv), so no memset launch precedes the next band or
-// heavy step
+// copies the counter block to mapped host memory, then (system-scope release) the
+// sequence number the host spins on; then resets the counters the host consumes
+// per check (the members' degree sums mh, which the host accumulates over a band's
+// checks, and minv), so no memset launch precedes the next band or heavy step
 __global__ __launch_bounds__(256) void v2_publish_k(V2Ctl* __restrict__ ctl, u64* __restrict__ host, u64* seqp,
                                                     u64 seq) {
-    const int t = threadIdx.x;
-    if (t < V2H_N) {
-        u64 x = 0;
-        if (t < 4) {
-            for (int i = 0; i < V2_NSH; ++i) x += ctl->cnt[t][i].v;
-        } else if (t == 4) {
-            for (int i = 0; i < V2_NSH; ++i) x += ctl->mh[i].v;
-        } else if (t == 5) {
-            for (int i = 0; i < V2_NSH; ++i) x += ctl->mh[i].pad[0];
-        } else if (t == 6) {
-            x = ~0ull;
-            for (int i = 0; i < V2_NSH; ++i) x = min(x, ctl->minv[i].v);
-        } else if (t == 7) {
-            x = ctl->aux.v;
-        } else {
-            const int k = (t - 8) / 3, f = (t - 8) % 3;
-            for (int i = 0; i < V2_NSH; ++i) x += f == 0 ? ctl->work[k][i].v : ctl->work[k][i].pad[f - 1];
-        }
-        host[t] = x;
-    }
-    if (PJ_V2_FULLPUB) {
-        const u64* c = reinterpret_cast<const u64*>(ctl);
-        for (int i = t; i < (int)(sizeof(V2Ctl) / sizeof(u64)); i += 256) host[V2H_N + i] = c[i];
-    }
+    const u64* c = reinterpret_cast<const u64*>(ctl);
+    constexpr int nw = sizeof(V2Ctl) / sizeof(u64);
+    for (int i = threadIdx.x; i < nw; i += 256) host[i] = c[i];
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence_system();
@@ -2007,8 +1972,7 @@ void ensure_solve(Graph& g, DeltaSolve& v) {
     v.hv.alloc(3 * v.hcap);  // the hub queue's ring of three slots
     v.hbeg.alloc(3 * v.hcap);
     v.hoff.alloc(3 * v.hcap);
-    PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hctl), sizeof(V2Host) + (PJ_V2_FULLPUB ? sizeof(V2Ctl) : 0),
-                         hipHostMallocMapped));
+    PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hctl), sizeof(V2Ctl), hipHostMallocMapped));
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&v.hctl_dev), v.hctl, 0));
     PJ_HIP(hipHostMalloc(reinterpret_cast<void**>(&v.hseq), 64, hipHostMallocMapped | hipHostMallocCoherent));
     PJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&v.hseq_dev), v.hseq, 0));
@@ -2115,8 +2079,16 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
         }
     };
     auto sync_ctl = [&]() { wait_ctl(publish_ctl()); };
-    auto slot = [&](int c) { return v.hctl->cnt[c]; };
-    auto hminv = [&]() { return v.hctl->minv; };
+    auto slot = [&](int c) {
+        u64 t = 0;
+        for (int i = 0; i < V2_NSH; ++i) t += v.hctl->cnt[c][i].v;
+        return t;
+    };
+    auto hminv = [&]() {
+        u64 m = ~0ull;
+        for (int i = 0; i < V2_NSH; ++i) m = std::min<u64>(m, v.hctl->minv[i].v);
+        return m;
+    };
 
     pj_stats st{};
     const bool valid = source >= 0 && source < g.n;
@@ -2265,8 +2237,10 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
                         break;
                     }
                 }
-                mh += v.hctl->mh;
-                ml += v.hctl->ml;
+                for (int i = 0; i < V2_NSH; ++i) {
+                    mh += v.hctl->mh[i].v;
+                    ml += v.hctl->mh[i].pad[0];
+                }
                 if (slot(cpub) == 0) break;
                 K = std::max(1, std::min(2 * K, 16) - g.spec_round);
             }
@@ -2365,7 +2339,7 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
             }
             sync_ctl();
             if (enter_tail && (long long)tdelta <= w.maxw) {
-                heavy_left = v.hctl->aux;
+                heavy_left = v.hctl->aux.v;
                 light_left = tail_unsettled > heavy_left ? tail_unsettled - heavy_left : 0;
             }
             if (slot(cs) == 0 && dpend) {  // the next band is empty; deferred edges land past it
@@ -2384,8 +2358,10 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
                 PJ_LAUNCH_CHECK();
                 continue;
             }
-            mh_carry += v.hctl->mh;  // (the next band's members, counted by its selection)
-            ml_carry += v.hctl->ml;
+            for (int i = 0; i < V2_NSH; ++i) {  // (the next band's members, counted by its selection)
+                mh_carry += v.hctl->mh[i].v;
+                ml_carry += v.hctl->mh[i].pad[0];
+            }
             lo = hi;
         }
         if (dpend) throw Error(PJ_ERR_HIP, "delta-stepping: deferred heavy edges left (internal error)");
@@ -2393,7 +2369,12 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
         // publish of the counters after the solve's last relaxation kernel
         if (lo >= INT_INF) sync_ctl();
         for (int k = 0; k < V2W_N; ++k) {
-            for (int f = 0; f < 3; ++f) st.work_by_kernel[k][f] += (int64_t)v.hctl->work[k][f];
+            for (int i = 0; i < V2_NSH; ++i) {
+                const V2Line& l = v.hctl->work[k][i];
+                st.work_by_kernel[k][0] += (int64_t)l.v;
+                st.work_by_kernel[k][1] += (int64_t)l.pad[0];
+                st.work_by_kernel[k][2] += (int64_t)l.pad[1];
+            }
             st.scanned_edges += st.work_by_kernel[k][0];
             st.probes += st.work_by_kernel[k][1];
             st.work_bytes += st.work_by_kernel[k][2];
