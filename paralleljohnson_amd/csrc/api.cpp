@@ -897,7 +897,6 @@ int pj_set_option(pj_graph* pg, const char* key, double value) {
     else if (k == "round_log" && (value == 0 || value == 1)) g.round_log = (int)value;
     else if (k == "level_log" && (value == 0 || value == 1)) g.level_log = (int)value;
     else if (k == "spec_round" && (value == 0 || value == 1 || value == 2)) g.spec_round = (int)value;
-    else if (k == "fuse_pub" && (value == 0 || value == 1)) g.fuse_pub = (int)value;
     else if (k == "hub_first" && (value == 0 || value == 1)) g.hub_first = (int)value;
     else if (k == "pull_first" && (value == 0 || value == 1)) g.pull_first = (int)value;
     else if (k == "band_width" && value >= 0) g.band_width = value;

@@ -307,7 +307,6 @@ struct V2Ctl {
     V2Line minv[V2_NSH];    // min dist >= lo of the last select / pull (next band search), per shard
     V2Line aux;             // v2_heavy_left_k's sum (the tail switch's heavy_left)
     V2Line work[V2W_N][V2_NSH];
-    V2Line pubd;            // blocks of a publishing hub launch done (its last block publishes)
 };
 // Waves per SIMD the compiler must fit the register budget to (0 = its own choice): the light
 // round kernel took 81-91 VGPRs (5 waves per SIMD); at 7 (72 VGPRs, 16 bytes of scratch per lane)
@@ -961,47 +960,15 @@ __device__ __forceinline__ void v2_hub_body(const V2Args& a, u64* __restrict__ f
     }
 }
 
-// The publish by one block: the counter block into mapped host memory, then (system-scope
-// release) the sequence number the host spins on, then the resets of the counters the host
-// consumes per check (the members' degree sums mh, which the host accumulates over a band's
-// checks, and minv), so no memset launch precedes the next band or heavy step. Agent-scope
-// loads: the caller may be the last block of a launch whose other blocks' atomics it reads.
-__device__ __forceinline__ void v2_publish_body(V2Ctl* ctl, u64* host, u64* seqp, u64 seq) {
-    u64* c = reinterpret_cast<u64*>(ctl);
-    constexpr int nw = sizeof(V2Ctl) / sizeof(u64);
-    for (int i = threadIdx.x; i < nw; i += blockDim.x)
-        host[i] = __hip_atomic_load(c + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence_system();
-        __hip_atomic_store(seqp, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (threadIdx.x < V2_NSH) {
-        ctl->mh[threadIdx.x].v = 0;
-        ctl->mh[threadIdx.x].pad[0] = 0;
-        ctl->minv[threadIdx.x].v = ~0ull;
-    }
-}
-
 // The hub queue hs of one round in its own launch. Zeroes the next ring slot hz for
-// later appends. seq != 0 (option fuse_pub): the launch also publishes the counters, as a
-// v2_publish_k behind it would -- by block 0 at once when the queue is empty (the round
-// kernel before it left the counters final), else by the block that finishes last.
+// later appends.
 template <bool LIGHT>
-__global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout, int cin, int hs, int hz,
-                                               u64* __restrict__ host, u64* seqp, u64 seq) {
+__global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout, int cin, int hs, int hz) {
     __shared__ V2HubLds L;
     __shared__ u64 red[2 * DB / WAVE];
-    __shared__ int s_last;
     const u64 packed = a.ctl->hub[hs].v;
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->hub[hz].v = 0;
-    if ((packed >> V2_EB) == 0) {
-        if (seq && blockIdx.x == 0) {
-            __syncthreads();
-            v2_publish_body(a.ctl, host, seqp, seq);
-        }
-        return;
-    }
+    if ((packed >> V2_EB) == 0) return;
     u32 newc = 0;
     u64 fe = 0;
     int32_t fm = INT_INF;
@@ -1013,19 +980,6 @@ __global__ __launch_bounds__(DB) void v2_hub_k(V2Args a, u64* __restrict__ fout,
     }
     v2_flush_work(a, LIGHT ? V2W_HUB : V2W_HPUSH, wk, esrc_bytes(LIGHT ? v2_light_src(a) : v2_cw_src(a)), 4u, red,
                   DB / WAVE);
-    if (seq) {  // (every block reaches this: only the empty-queue case returned early)
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            s_last = atomicAdd(&a.ctl->pubd.v, 1ull) == (u64)gridDim.x - 1ull;
-        }
-        __syncthreads();
-        if (s_last) {
-            __threadfence();
-            if (threadIdx.x == 0) a.ctl->pubd.v = 0;
-            v2_publish_body(a.ctl, host, seqp, seq);
-        }
-    }
 }
 
 // Next band [lo, hi): fout words = members, count into slot cout, min dist >= lo.
@@ -1963,7 +1917,19 @@ int32_t prepare_delta(Graph& g, DeltaWork& w) {
 // checks, and minv), so no memset launch precedes the next band or heavy step
 __global__ __launch_bounds__(256) void v2_publish_k(V2Ctl* __restrict__ ctl, u64* __restrict__ host, u64* seqp,
                                                     u64 seq) {
-    v2_publish_body(ctl, host, seqp, seq);
+    const u64* c = reinterpret_cast<const u64*>(ctl);
+    constexpr int nw = sizeof(V2Ctl) / sizeof(u64);
+    for (int i = threadIdx.x; i < nw; i += 256) host[i] = c[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(seqp, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (threadIdx.x < V2_NSH) {
+        ctl->mh[threadIdx.x].v = 0;
+        ctl->mh[threadIdx.x].pad[0] = 0;
+    }
+    if (threadIdx.x < V2_NSH) ctl->minv[threadIdx.x].v = ~0ull;
 }
 
 // solve start in one launch: dist := INF (the source 0), frontier 0 := {source},
@@ -2170,7 +2136,7 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
             a.dsave = dsave;
             v2_heavy_push_k<Off><<<maxgrid, DB, 0, s>>>(a, row, members, hr);
             PJ_LAUNCH_CHECK();
-            v2_hub_k<false><<<maxgrid, DB, 0, s>>>(a, nullptr, cs, hr, (hr + 1) % 3, nullptr, nullptr, 0);
+            v2_hub_k<false><<<maxgrid, DB, 0, s>>>(a, nullptr, cs, hr, (hr + 1) % 3);
             PJ_LAUNCH_CHECK();
             a.hz = INT_INF;
             a.dsave = nullptr;
@@ -2220,7 +2186,7 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
             int K = g.round_batch;
             for (;;) {
                 const u64 pull_thresh = can_pull_light ? (u64)((double)light_left / light_pull) : ~0ull;
-                auto round = [&](u64 pub) {  // (pub: the publish's sequence number, fused into the hub launch)
+                auto round = [&]() {
                     u64* fin = v.f[fi].p;
                     u64* fout = v.f[(fi + 1) % 3].p;
                     u64* fclr = v.f[(fi + 2) % 3].p;
@@ -2228,30 +2194,22 @@ i64 delta2_run(Graph& g, DeltaWork& w, DeltaSolve& v, int32_t delta, i64 source,
                     v2_pull_round_k<Off><<<roundgrid, DB, 0, s>>>(a, row, fin, fout, cs, pull_thresh, w.lcv.p,
                                                                  w.lcc.p, w.nlc, hr, dense_min, fclr);
                     PJ_LAUNCH_CHECK();
-                    v2_hub_k<true><<<hubgrid, DB, 0, s>>>(a, fout, cs, hr, (hr + 1) % 3,
-                                                          pub ? reinterpret_cast<u64*>(v.hctl_dev) : nullptr,
-                                                          v.hseq_dev, pub);
+                    v2_hub_k<true><<<hubgrid, DB, 0, s>>>(a, fout, cs, hr, (hr + 1) % 3);
                     PJ_LAUNCH_CHECK();
                     fi = (fi + 1) % 3;
                     cs = (cs + 1) & 3;
                     hr = (hr + 1) % 3;
                     st.relax_rounds++;
                 };
-                u64 pseq = 0;
-                if (g.fuse_pub) {
-                    pseq = ++v.seq;
-                    for (int q = 0; q < K; ++q) round(q == K - 1 ? pseq : 0);
-                } else {
-                    for (int q = 0; q < K; ++q) round(0);
-                }
+                for (int q = 0; q < K; ++q) round();
                 // spec_round: one more round enqueued behind the publish runs while the host waits
                 // for it -- the next round of the band, or an empty one (a launch that reads a zero
                 // count) when the band has ended; the ring state stays consistent either way, since
                 // every later step writes its frontier words whole and counts into a slot the rounds
                 // before zeroed
                 const int cpub = cs;
-                if (!g.fuse_pub) pseq = publish_ctl();
-                for (int q = 0; q < g.spec_round; ++q) round(0);
+                const u64 pseq = publish_ctl();
+                for (int q = 0; q < g.spec_round; ++q) round();
                 wait_ctl(pseq);
                 if (deferred) {
                     deferred = false;

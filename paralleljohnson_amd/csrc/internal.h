@@ -256,7 +256,6 @@ struct Graph {
     int heavy_gpc = 0;     // delta v2: workgroups per CU of the heavy pull (0 = 24; 7-32 swept, 12-32 equal)
     int round_batch = 1; // delta v2: light rounds enqueued per host check at a band's start (at least; 2 until
                          // spec_round: 1 then +1.2%, 3 -2.5%, profiles/r06/round_batch_ab_r6aa.txt / _r6ab.txt)
-    int fuse_pub = 1;    // delta v2: a band check's publish runs in the last round's hub launch (0/1)
     int spec_round = 1;  // delta v2: light rounds enqueued behind each check's publish (0-2)
     int batch_streams = 2; // weighted batches (pj_sssp_batch*): solves in flight at once, one stream each
     int grid_per_cu = 0; // BFS level kernel workgroups per CU (0 = auto: 2 below 2^25 entries, else 4)

@@ -400,10 +400,9 @@ def test_weighted_band_width(ctx, oracle, scale, ef):
             g.set_option("tail_after", ta)
             g.set_option("tail_frac", 2.0 if td else 0.0)  # (switch as soon as tail_after allows)
             for r in roots:
-                for sr, fp in ((0, 1), (1, 1), (2, 1), (1, 0)):
+                for sr in (0, 1, 2):
                     g.set_option("spec_round", sr)
-                    g.set_option("fuse_pub", fp)
-                    assert (g.sssp(r) == exp[r]).all(), (pf, lp, delta, bw, td, ta, r, sr, fp)
+                    assert (g.sssp(r) == exp[r]).all(), (pf, lp, delta, bw, td, ta, r, sr)
     g.close()
 
 
@@ -435,12 +434,9 @@ def test_weighted_defer_heavy(ctx, oracle, scale, ef):
                 g.set_option("tail_frac", tf)
                 g.set_option("defer_check", dc)
                 for r in roots:
-                    # (spec_round: light rounds enqueued behind every check's publish; fuse_pub: the
-                    # publish in the last round's hub launch, or a launch of its own)
-                    for sr, fp in ((0, 1), (1, 1), (2, 1), (1, 0)):
+                    for sr in (0, 1, 2):  # (spec_round: light rounds enqueued behind every check's publish)
                         g.set_option("spec_round", sr)
-                        g.set_option("fuse_pub", fp)
-                        assert (g.sssp(r) == exp[r]).all(), (dh, pf, delta, bw, tf, dc, r, sr, fp)
+                        assert (g.sssp(r) == exp[r]).all(), (dh, pf, delta, bw, tf, dc, r, sr)
                         pushed_any |= dh > 0 and g.stats()["td_levels"] > 0
     assert pushed_any
     g.close()
