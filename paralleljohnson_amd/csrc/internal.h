@@ -215,7 +215,10 @@ struct Graph {
     std::unique_ptr<Relabeled> rl;  // weighted: built on the first delta solve
 
     // options
-    double alpha = 14.0, beta = 24.0, delta = 0.0;
+    double alpha = 14.0, delta = 0.0;
+    double beta = 32.0;  // BFS: pull -> push once the frontier is below n / beta and shrinking (24 until round 6:
+                         // 32 with the hub-first pulls, K22 median kernel time 0.190 -> 0.182 ms, web-Google
+                         // equal, profiles/r06/bfs_beta_r6aq.txt)
     double pull_vertex = 2.0;  // BFS: push -> pull also when the frontier's out-edges > pull_vertex x the
                                // unvisited vertices (0 = Beamer's rule alone). With hub-first in-rows a
                                // pull probes ~2 in-edges per unvisited vertex, a push pays an atomic per
