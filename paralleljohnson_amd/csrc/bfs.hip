@@ -42,7 +42,9 @@ namespace pj {
 namespace {
 
 #ifndef PJ_RPI
-#define PJ_RPI 4
+#define PJ_RPI 1  // 4 until round 6: with hub-first rows and the dense first in-neighbours one round of 64
+                  // candidates at a time is faster (K22 mean kernel time 0.1906 -> 0.1827 ms, web-Google
+                  // 0.2277 -> 0.2216; 2: 0.1847 / 0.2222, 8: 0.245 / 0.255; profiles/r06/bfs_rpi_r6av.txt)
 #endif
 #ifndef PJ_PB2
 #define PJ_PB2 8
