@@ -312,9 +312,11 @@ struct V2Ctl {
 // round kernel took 81-91 VGPRs (5 waves per SIMD); at 7 (72 VGPRs, 16 bytes of scratch per lane)
 // its latency-bound pulls keep more loads in flight: k26w 596 -> 643 GTEPS interleaved (6: 634,
 // 8: 627 with 92 bytes of scratch; profiles/r05/occupancy_r5h17.txt). The heavy pull (65-73
-// VGPRs) at 8 measured equal.
+// VGPRs) at 8 measured equal. Round 6 (the speculative round, one round per check at a band's
+// start, 3 hub workgroups per CU): 6 beats 7 by 0.7% over 6 interleaved passes
+// (profiles/r06/delta_variants_r6ba.txt).
 #ifndef PJ_V2_WPE_R
-#define PJ_V2_WPE_R 7
+#define PJ_V2_WPE_R 6
 #endif
 #ifndef PJ_V2_WPE_H
 #define PJ_V2_WPE_H 0
