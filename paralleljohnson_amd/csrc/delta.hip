@@ -319,7 +319,8 @@ struct V2Ctl {
 #define PJ_V2_WPE_R 6
 #endif
 #ifndef PJ_V2_WPE_H
-#define PJ_V2_WPE_H 0
+#define PJ_V2_WPE_H 8  // the heavy pull: 0 (the compiler's choice) until round 6; 8 +1.0% over 7 interleaved
+                       // passes once the round kernel ran at 6 (profiles/r06/delta_variants_r6be.txt)
 #endif
 #if PJ_V2_WPE_R
 #define V2_WPE_R __attribute__((amdgpu_waves_per_eu(PJ_V2_WPE_R)))
